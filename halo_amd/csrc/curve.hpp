@@ -1,0 +1,240 @@
+// Device group arithmetic for Pallas / Vesta (y^2 = x^3 + 5) on gfx950.
+//
+// Replaces ark-ec 0.5.0 short-Weierstrass `Projective`/`Affine` arithmetic used on the hot path
+// (reference: crates/group/src/group.rs:28-29,48-56; crates/accumulation/src/pedersen.rs:21-26;
+// crates/accumulation/src/pcdl.rs:413-429).
+//
+// Accumulators use XYZZ coordinates (x = X/ZZ, y = Y/ZZZ, ZZ^3 = ZZZ^2): mixed addition costs
+// 8M + 2S with no inversion, which is the cheapest complete-enough formula for bucket
+// accumulation.  Affine points are (x, y) in internal Montgomery form; the identity is encoded as
+// (0, 0) (not on the curve, matching `PastaAffine::identity`, crates/group/src/wrappers.rs:91-93).
+#pragma once
+#include "fields.hpp"
+
+namespace halo {
+
+struct PallasCurve {
+    using Base = FqCfg;
+    using Scalar = FpCfg;
+    using K = PallasCurveCfg;
+};
+struct VestaCurve {
+    using Base = FpCfg;
+    using Scalar = FqCfg;
+    using K = VestaCurveCfg;
+};
+
+template <class F>
+struct Affine {
+    Fe<F> x, y;
+};
+
+template <class F>
+struct XYZZ {
+    Fe<F> X, Y, ZZ, ZZZ;
+};
+
+template <class F>
+HALO_DEV bool aff_is_id(const Affine<F>& a) {
+    return fe_is_zero(a.x) && fe_is_zero(a.y);
+}
+
+template <class F>
+HALO_DEV XYZZ<F> xyzz_id() {
+    XYZZ<F> r;
+    r.X = fe_one<F>();
+    r.Y = fe_one<F>();
+    r.ZZ = fe_zero<F>();
+    r.ZZZ = fe_zero<F>();
+    return r;
+}
+
+template <class F>
+HALO_DEV bool xyzz_is_id(const XYZZ<F>& p) {
+    return fe_is_zero(p.ZZ);
+}
+
+template <class F>
+HALO_DEV XYZZ<F> xyzz_from_aff(const Affine<F>& a) {
+    if (aff_is_id(a)) return xyzz_id<F>();
+    XYZZ<F> r;
+    r.X = a.x;
+    r.Y = a.y;
+    r.ZZ = fe_one<F>();
+    r.ZZZ = fe_one<F>();
+    return r;
+}
+
+template <class F>
+HALO_DEV Affine<F> aff_neg(const Affine<F>& a) {
+    Affine<F> r;
+    r.x = a.x;
+    r.y = fe_neg(a.y);
+    return r;
+}
+
+// dbl-2008-s-1 (a = 0): 2M + 4S ... (U=2Y, V=U^2, W=U*V, S=X*V, M=3X^2)
+template <class F>
+HALO_DEV XYZZ<F> xyzz_dbl(const XYZZ<F>& p) {
+    if (xyzz_is_id(p)) return p;
+    const Fe<F> U = fe_dbl(p.Y);
+    const Fe<F> V = fe_sqr(U);
+    const Fe<F> W = fe_mul(U, V);
+    const Fe<F> S = fe_mul(p.X, V);
+    const Fe<F> X2 = fe_sqr(p.X);
+    const Fe<F> M = fe_add(fe_dbl(X2), X2);
+    XYZZ<F> r;
+    r.X = fe_sub(fe_sqr(M), fe_dbl(S));
+    r.Y = fe_sub(fe_mul(M, fe_sub(S, r.X)), fe_mul(W, p.Y));
+    r.ZZ = fe_mul(V, p.ZZ);
+    r.ZZZ = fe_mul(W, p.ZZZ);
+    return r;
+}
+
+// Doubling of an affine point into XYZZ (mdbl-2008-s-1)
+template <class F>
+HALO_DEV XYZZ<F> xyzz_mdbl(const Affine<F>& a) {
+    const Fe<F> U = fe_dbl(a.y);
+    const Fe<F> V = fe_sqr(U);
+    const Fe<F> W = fe_mul(U, V);
+    const Fe<F> S = fe_mul(a.x, V);
+    const Fe<F> X2 = fe_sqr(a.x);
+    const Fe<F> M = fe_add(fe_dbl(X2), X2);
+    XYZZ<F> r;
+    r.X = fe_sub(fe_sqr(M), fe_dbl(S));
+    r.Y = fe_sub(fe_mul(M, fe_sub(S, r.X)), fe_mul(W, a.y));
+    r.ZZ = V;
+    r.ZZZ = W;
+    return r;
+}
+
+// Mixed addition p + q (madd-2008-s), handles identity and the doubling / inverse cases.
+template <class F>
+HALO_DEV XYZZ<F> xyzz_madd(const XYZZ<F>& p, const Affine<F>& q) {
+    if (aff_is_id(q)) return p;
+    if (xyzz_is_id(p)) return xyzz_from_aff(q);
+    const Fe<F> U2 = fe_mul(q.x, p.ZZ);
+    const Fe<F> S2 = fe_mul(q.y, p.ZZZ);
+    const Fe<F> P = fe_sub(U2, p.X);
+    const Fe<F> R = fe_sub(S2, p.Y);
+    if (fe_is_zero(P)) {
+        if (fe_is_zero(R)) return xyzz_mdbl(q);
+        return xyzz_id<F>();
+    }
+    const Fe<F> PP = fe_sqr(P);
+    const Fe<F> PPP = fe_mul(P, PP);
+    const Fe<F> Q = fe_mul(p.X, PP);
+    XYZZ<F> r;
+    r.X = fe_sub(fe_sub(fe_sqr(R), PPP), fe_dbl(Q));
+    r.Y = fe_sub(fe_mul(R, fe_sub(Q, r.X)), fe_mul(p.Y, PPP));
+    r.ZZ = fe_mul(p.ZZ, PP);
+    r.ZZZ = fe_mul(p.ZZZ, PPP);
+    return r;
+}
+
+// General addition (add-2008-s), handles identity and the doubling / inverse cases.
+template <class F>
+HALO_DEV XYZZ<F> xyzz_add(const XYZZ<F>& p, const XYZZ<F>& q) {
+    if (xyzz_is_id(q)) return p;
+    if (xyzz_is_id(p)) return q;
+    const Fe<F> U1 = fe_mul(p.X, q.ZZ);
+    const Fe<F> U2 = fe_mul(q.X, p.ZZ);
+    const Fe<F> S1 = fe_mul(p.Y, q.ZZZ);
+    const Fe<F> S2 = fe_mul(q.Y, p.ZZZ);
+    const Fe<F> P = fe_sub(U2, U1);
+    const Fe<F> R = fe_sub(S2, S1);
+    if (fe_is_zero(P)) {
+        if (fe_is_zero(R)) return xyzz_dbl(p);
+        return xyzz_id<F>();
+    }
+    const Fe<F> PP = fe_sqr(P);
+    const Fe<F> PPP = fe_mul(P, PP);
+    const Fe<F> Q = fe_mul(U1, PP);
+    XYZZ<F> r;
+    r.X = fe_sub(fe_sub(fe_sqr(R), PPP), fe_dbl(Q));
+    r.Y = fe_sub(fe_mul(R, fe_sub(Q, r.X)), fe_mul(S1, PPP));
+    r.ZZ = fe_mul(fe_mul(p.ZZ, q.ZZ), PP);
+    r.ZZZ = fe_mul(fe_mul(p.ZZZ, q.ZZZ), PPP);
+    return r;
+}
+
+template <class F>
+HALO_DEV XYZZ<F> xyzz_neg(const XYZZ<F>& p) {
+    XYZZ<F> r = p;
+    r.Y = fe_neg(p.Y);
+    return r;
+}
+
+// XYZZ -> affine (one inversion); identity -> (0, 0)
+template <class F>
+HALO_DEV Affine<F> xyzz_to_aff(const XYZZ<F>& p) {
+    Affine<F> r;
+    if (xyzz_is_id(p)) {
+        r.x = fe_zero<F>();
+        r.y = fe_zero<F>();
+        return r;
+    }
+    const Fe<F> t = fe_inv(fe_mul(p.ZZ, p.ZZZ));  // 1 / (ZZ * ZZZ)
+    r.x = fe_mul(p.X, fe_mul(t, p.ZZZ));          // X / ZZ
+    r.y = fe_mul(p.Y, fe_mul(t, p.ZZ));           // Y / ZZZ
+    return r;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Storage: packed points.  Affine internal = 2 x 32 B (x, y); XYZZ internal = 4 x 32 B.
+// ---------------------------------------------------------------------------------------------
+template <class F>
+HALO_DEV Affine<F> aff_load(const uint4* p) {
+    Affine<F> a;
+    a.x = fe_load<F>(p);
+    a.y = fe_load<F>(p + 2);
+    return a;
+}
+template <class F>
+HALO_DEV void aff_store(uint4* p, const Affine<F>& a) {
+    fe_store(p, a.x);
+    fe_store(p + 2, a.y);
+}
+template <class F>
+HALO_DEV XYZZ<F> xyzz_load(const uint4* p) {
+    XYZZ<F> a;
+    a.X = fe_load<F>(p);
+    a.Y = fe_load<F>(p + 2);
+    a.ZZ = fe_load<F>(p + 4);
+    a.ZZZ = fe_load<F>(p + 6);
+    return a;
+}
+template <class F>
+HALO_DEV void xyzz_store(uint4* p, const XYZZ<F>& a) {
+    fe_store(p, a.X);
+    fe_store(p + 2, a.Y);
+    fe_store(p + 4, a.ZZ);
+    fe_store(p + 6, a.ZZZ);
+}
+
+// WrappedPoint (ark Montgomery x, y; (0,0) = identity) -> internal affine
+template <class F>
+HALO_DEV Affine<F> aff_from_wrapped(const uint4* p) {
+    Affine<F> a;
+    a.x = fe_from_ark<F>(p);
+    a.y = fe_from_ark<F>(p + 2);
+    return a;
+}
+template <class F>
+HALO_DEV void aff_to_wrapped(uint4* p, const Affine<F>& a) {
+    fe_to_ark(p, a.x);
+    fe_to_ark(p + 2, a.y);
+}
+
+// Variable-base scalar multiplication k * P (k canonical, 8 x u32 words), left-to-right binary.
+template <class F>
+HALO_DEV XYZZ<F> xyzz_scalar_mul(const Affine<F>& P, const uint32_t (&k)[8]) {
+    XYZZ<F> acc = xyzz_id<F>();
+    for (int i = 255; i >= 0; i--) {
+        acc = xyzz_dbl(acc);
+        if ((k[i >> 5] >> (i & 31)) & 1u) acc = xyzz_madd(acc, P);
+    }
+    return acc;
+}
+
+}  // namespace halo

@@ -1,0 +1,94 @@
+// Host-side runtime shared by every translation unit of libhalo_gpu.so: error reporting,
+// per-device state, device memory helpers.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstddef>
+#include <cstdint>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/halo_gpu.h"
+
+namespace halo {
+
+// ---- errors ---------------------------------------------------------------------------------
+int set_error(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+void clear_error();
+
+#define HALO_HIP(expr)                                                                      \
+    do {                                                                                    \
+        hipError_t _e = (expr);                                                             \
+        if (_e != hipSuccess)                                                               \
+            return ::halo::set_error(HALO_EDEVICE, "%s failed: %s (%s:%d)", #expr,          \
+                                     hipGetErrorString(_e), __FILE__, __LINE__);            \
+    } while (0)
+
+#define HALO_CHECK(expr)              \
+    do {                              \
+        int _rc = (expr);             \
+        if (_rc != HALO_OK) return _rc; \
+    } while (0)
+
+// ---- device buffers ---------------------------------------------------------------------------
+// Grow-only device buffer (no shrinking; reused across calls so that timed regions never allocate).
+struct DevBuf {
+    void* ptr = nullptr;
+    size_t bytes = 0;
+    int reserve(size_t n);  // ensures capacity >= n bytes
+    template <class T>
+    T* as() const { return static_cast<T*>(ptr); }
+    ~DevBuf();
+};
+
+// Per-device, per-curve state (the OnceLock<PublicParams> analogue, crates/group/src/pp.rs:63-94)
+struct SrsState {
+    DevBuf gs;          // n internal-format affine points (64 B each)
+    size_t n = 0;
+    bool has_sh = false;
+    uint32_t S[16];     // internal packed (x, y)
+    uint32_t H[16];
+    DevBuf shifted;     // optional window-shifted copies
+    int shifted_c = 0;  // window bits of `shifted`
+    int shifted_windows = 0;
+};
+
+struct DeviceState {
+    int device = -1;
+    std::mutex mu;                 // serialises API calls on this device
+    SrsState srs[2];               // per curve
+    // scratch
+    DevBuf scratch[8];
+    // NTT twiddle caches: key (field, log, inverse)
+    struct Twiddles {
+        int field, logn, inverse;
+        DevBuf hi, lo;
+        int lo_bits;
+    };
+    std::vector<std::unique_ptr<Twiddles>> tw;
+    struct RTable {
+        int field, logr, inverse;
+        DevBuf t;
+    };
+    std::vector<std::unique_ptr<RTable>> rt;
+};
+
+// Current device's state (calls halo_init(current device) lazily).  Returns nullptr on failure
+// (with the error set).
+DeviceState* current_state();
+
+// Pinned staging helpers
+int copy_h2d(void* dst, const void* src, size_t bytes, hipStream_t s);
+int copy_d2h(void* dst, const void* src, size_t bytes, hipStream_t s);
+
+inline bool is_pow2(size_t n) { return n && !(n & (n - 1)); }
+inline unsigned ilog2(size_t n) {
+    unsigned r = 0;
+    while ((size_t(1) << (r + 1)) <= n) r++;
+    return r;
+}
+
+}  // namespace halo

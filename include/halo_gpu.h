@@ -1,0 +1,183 @@
+/*
+ * halo_gpu.h -- C ABI of the MI355X (gfx950) backend for the rasmus-kirk/halo proving hot path.
+ *
+ * Every entry point replaces one reference function (or the arkworks call inside it) on the path
+ * named by BASELINE.json's north_star; the reference interface each one stands in for is cited
+ * next to it (paths relative to the reference root).  A Rust `extern "C"` shim that binds these
+ * symbols is given in INTEGRATION.md.
+ *
+ * Conventions
+ *  - Field elements (`halo_fe_t`): 4 x u64 little-endian limbs in arkworks Montgomery form
+ *    (R = 2^256), canonical in [0, p) -- the in-memory layout of `ark_ff::Fp256` / `BigInt<4>`,
+ *    so `&[Fr]` can be passed zero-copy.
+ *  - Points (`halo_wrapped_point_t`): `WrappedPoint { x: [u64; 4], y: [u64; 4] }`
+ *    (crates/group/src/wrappers.rs:592-597, #[repr(C)]), affine, Montgomery limbs; the identity is
+ *    (0, 0) (`PastaAffine::identity`, wrappers.rs:91-93).  Every point-valued result is returned in
+ *    this canonical affine form, so results compare bit-exactly.
+ *  - Curves: HALO_PALLAS (base field Fq, scalars Fp = ark_pallas::Fr), HALO_VESTA (base Fp,
+ *    scalars Fq).  Fields: HALO_FP (ark_pallas::Fr), HALO_FQ (ark_pallas::Fq)
+ *    (crates/group/src/lib.rs:8-9).
+ *  - Host-pointer entry points take caller-owned host buffers, borrowed for the call only.
+ *    `_dev` entry points take device pointers (hipMalloc'd on the current device) plus a
+ *    `hipStream_t` passed as `void*` (NULL = default stream) and are asynchronous with respect to
+ *    the host unless stated otherwise.
+ *  - Errors: the reference panics (`assert!`) on contract violations; this ABI never aborts and
+ *    returns a nonzero `halo_status_t` instead, with the reference's panic message available from
+ *    `halo_last_error()` (thread-local).
+ *  - Thread safety: every call is re-entrant.  Device-resident state (SRS, twiddles, scratch) is
+ *    per (device, curve/field), created once under a mutex (mirrors the `OnceLock<PublicParams>`
+ *    of crates/group/src/pp.rs:63-94 and wrappers.rs:28-29).
+ */
+#ifndef HALO_GPU_H
+#define HALO_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct { uint64_t l[4]; } halo_fe_t;
+typedef struct { uint64_t x[4]; uint64_t y[4]; } halo_wrapped_point_t;
+
+typedef enum { HALO_PALLAS = 0, HALO_VESTA = 1 } halo_curve_t;
+typedef enum { HALO_FP = 0, HALO_FQ = 1 } halo_field_t;
+
+typedef enum {
+    HALO_OK = 0,
+    HALO_EINVAL = 1,     /* bad argument (null pointer, unknown curve/field, length mismatch) */
+    HALO_ENOMEM = 2,     /* device allocation failed */
+    HALO_EDEVICE = 3,    /* HIP runtime / kernel error, or no GPU */
+    HALO_ENOTPOW2 = 4,   /* "n ({n}) is not a power of two"  (pcdl.rs:282, pp.rs:32) */
+    HALO_ESRSRANGE = 5,  /* "d ({d}) <= D ({D})" / SRS too short (pcdl.rs:284, pp.rs:33) */
+    HALO_EDEGREE = 6,    /* "p_deg ({p_deg}) <= d ({d})" (pcdl.rs:283) */
+    HALO_ELENGTH = 7     /* "ms must be larger than Gs" (pedersen.rs:14-19) */
+} halo_status_t;
+
+/* ------------------------------------------------------------------ runtime */
+/* Selects the HIP device used by subsequent calls from this thread and creates its context. */
+int halo_init(int device);
+/* Number of visible GPUs (0 when no GPU is present). */
+int halo_device_count(void);
+/* Message of the last failed call on this thread ("" if none). */
+const char* halo_last_error(void);
+/* ABI version (major * 100 + minor). */
+int halo_abi_version(void);
+/* Blocks until all work queued by this library on `stream` is complete. */
+int halo_stream_sync(void* stream);
+
+/* ------------------------------------------------------------------ a10: SRS provider
+ * Replaces PublicParams::{new, set_pp, get_pp} (crates/group/src/pp.rs:26-94): the SRS bases Gs,
+ * S and H become device-resident once per (device, curve).  `gs` is the decoded
+ * `Vec<WrappedPoint>` of crates/group/.precompute/<curve>/gs-XX.bin (or any prefix of it). */
+int halo_srs_upload(halo_curve_t curve, const halo_wrapped_point_t* gs, size_t n,
+                    const halo_wrapped_point_t* S, const halo_wrapped_point_t* H);
+/* Current resident SRS length (0 if none). */
+int halo_srs_len(halo_curve_t curve, size_t* n);
+/* Synthetic SRS for sizes beyond the reference's N = 2^20 (crates/group/src/consts.rs:1):
+ * G_j = k_j * (-1, 2) with k_j from halo_synth_scalar(seed, j), generated on the device.
+ * S, H as in the reference are left unchanged if already uploaded. */
+int halo_srs_synthesize(halo_curve_t curve, size_t n, uint64_t seed);
+/* The canonical (non-Montgomery) discrete log k_j used by halo_srs_synthesize (host function; lets
+ * a verifier check MSM results over synthetic bases in O(n) field operations). */
+void halo_synth_scalar(halo_curve_t curve, uint64_t seed, uint64_t j, uint64_t out_canonical[4]);
+/* Precomputes the window-shifted copies 2^(c*w) * G_i of the resident SRS used by the
+ * single-bucket-set MSM (trades HBM capacity for the per-window combination); optional. */
+int halo_srs_precompute_windows(halo_curve_t curve);
+
+/* ------------------------------------------------------------------ a3/a4: MSM
+ * sum_{i < min(n_bases, n_scalars)} scalars[i] * bases[i]
+ * Replaces `Projective::msm_unchecked` as called by group::point_dot_affine
+ * (crates/group/src/group.rs:48-50) and pedersen::commit (crates/accumulation/src/pedersen.rs:21).
+ * Empty input -> identity (0, 0). */
+int halo_msm(halo_curve_t curve, const halo_wrapped_point_t* bases, size_t n_bases,
+             const halo_fe_t* scalars, size_t n_scalars, halo_wrapped_point_t* out);
+/* Same over the resident SRS prefix Gs[0..n) (the pcdl::commit path, pcdl.rs:286). */
+int halo_msm_srs(halo_curve_t curve, const halo_fe_t* scalars, size_t n, halo_wrapped_point_t* out);
+/* pedersen::commit(w, Gs, ms) (crates/accumulation/src/pedersen.rs:7-27): asserts
+ * Gs.len() >= ms.len(), MSM, then + S*w when `w` is non-NULL. */
+int halo_pedersen_commit(halo_curve_t curve, const halo_fe_t* w, const halo_wrapped_point_t* gs,
+                         size_t n_gs, const halo_fe_t* ms, size_t n_ms, halo_wrapped_point_t* out);
+/* pcdl::commit(p, d, w) (crates/accumulation/src/pcdl.rs:275-287): n = d + 1 must be a power of
+ * two, deg(p) <= d <= D, then pedersen::commit(w, Gs[0..n], p.coeffs) over the resident SRS.
+ * `coeffs` has `len` entries (trailing zeros allowed). */
+int halo_pcdl_commit(halo_curve_t curve, const halo_fe_t* coeffs, size_t len, size_t d,
+                     const halo_fe_t* w, halo_wrapped_point_t* out);
+/* Device-pointer MSM: d_bases (n WrappedPoints, or NULL to use the resident SRS prefix) and
+ * d_scalars (n halo_fe_t) in HBM; result written to host `out`.  Synchronous on `stream`. */
+int halo_msm_dev(halo_curve_t curve, const void* d_bases, const void* d_scalars, size_t n,
+                 halo_wrapped_point_t* out, void* stream);
+/* Window size the device MSM uses for n points. */
+int halo_msm_window_bits(size_t n);
+
+/* ------------------------------------------------------------------ a5/a6/a7: NTT
+ * Radix-2 domain of size N = 2^log_n, omega = 5^((p-1)/N) (ark-poly Radix2EvaluationDomain,
+ * crates/group/src/poly.rs:11).  Natural order in and out. */
+/* In-place forward (evals[i] = p(omega^i)) or inverse (includes the N^-1 scaling). */
+int halo_ntt(halo_field_t field, halo_fe_t* inout, unsigned log_n, int inverse);
+/* Evals::from_poly(_ref) / DensePolynomial::evaluate_over_domain(_by_ref) (poly.rs:56-64):
+ * `len` coefficients (len may exceed N: reduced mod X^N - 1 first) -> N evaluations. */
+int halo_evaluate_over_domain(halo_field_t field, const halo_fe_t* coeffs, size_t len,
+                              unsigned log_n, halo_fe_t* evals);
+/* Evals::interpolate(_by_ref) (poly.rs:133-139): N evaluations -> coefficients with trailing
+ * zeros trimmed (`*out_len` = trimmed length, <= N). */
+int halo_interpolate(halo_field_t field, const halo_fe_t* evals, unsigned log_n, halo_fe_t* coeffs,
+                     size_t* out_len);
+/* &DensePolynomial * &DensePolynomial (FFT multiply; protocol.rs:132-139, pcdl.rs:215):
+ * out has room for la + lb - 1 entries; *out_len = trimmed length. */
+int halo_poly_mul(halo_field_t field, const halo_fe_t* a, size_t la, const halo_fe_t* b, size_t lb,
+                  halo_fe_t* out, size_t* out_len);
+/* Batched device NTT: `batch` contiguous transforms of size 2^log_n at d_data, in place. */
+int halo_ntt_dev(halo_field_t field, void* d_data, unsigned log_n, size_t batch, int inverse,
+                 void* stream);
+
+/* ------------------------------------------------------------------ a8: evaluation / dots */
+/* DensePolynomial::evaluate (Horner; pcdl.rs:49,471), k polynomials at one point z. */
+int halo_poly_eval_batch(halo_field_t field, const halo_fe_t* const* polys, const size_t* lens,
+                         size_t k, const halo_fe_t* z, halo_fe_t* out);
+/* group::scalar_dot (crates/group/src/group.rs:43-45). */
+int halo_scalar_dot(halo_field_t field, const halo_fe_t* xs, const halo_fe_t* ys, size_t n,
+                    halo_fe_t* out);
+/* group::construct_powers (crates/group/src/group.rs:58-66): out[i] = z^i, i < n. */
+int halo_construct_powers(halo_field_t field, const halo_fe_t* z, size_t n, halo_fe_t* out);
+
+/* ------------------------------------------------------------------ a9: IPA folding
+ * The round loop of pcdl::open_without_eval (crates/accumulation/src/pcdl.rs:404-438) with the
+ * vectors device-resident across rounds; the caller keeps the Fiat-Shamir transcript and
+ * supplies xi each round.  Session lifecycle:
+ *   begin(cs = p'.coeffs resized to n, z, H') -> per round: round_lr -> (transcript) -> fold
+ *   -> end(U = G[0], c = c[0]).  gs starts as the resident SRS prefix Gs[0..n) (pcdl.rs:393). */
+typedef struct halo_ipa_session halo_ipa_session;
+int halo_ipa_begin(halo_curve_t curve, const halo_fe_t* cs, size_t n, const halo_fe_t* z,
+                   const halo_wrapped_point_t* H_prime, halo_ipa_session** out);
+/* L = <c_r, G_l> + H' <c_r, z_l>,  R = <c_l, G_r> + H' <c_l, z_r>  (pcdl.rs:412-418) */
+int halo_ipa_round_lr(halo_ipa_session* s, halo_wrapped_point_t* L, halo_wrapped_point_t* R);
+/* G_l[j] = G_l[j] + xi G_r[j] (affine), c_l[j] += xi^-1 c_r[j], z_l[j] += xi z_r[j]; m /= 2
+ * (pcdl.rs:427-437). */
+int halo_ipa_fold(halo_ipa_session* s, const halo_fe_t* xi, const halo_fe_t* xi_inv);
+/* Current half-length m, and the folded vectors (length 2m) copied back to the host (any of the
+ * output pointers may be NULL). */
+int halo_ipa_state(halo_ipa_session* s, size_t* m, halo_wrapped_point_t* gs, halo_fe_t* cs,
+                   halo_fe_t* zs);
+int halo_ipa_end(halo_ipa_session* s, halo_wrapped_point_t* U, halo_fe_t* c);
+/* One stateless fold over host vectors of length 2m (the loop body of pcdl.rs:427-435), in place
+ * on the left halves. */
+int halo_ipa_fold_host(halo_curve_t curve, halo_wrapped_point_t* gs, halo_fe_t* cs, halo_fe_t* zs,
+                       size_t m, const halo_fe_t* xi, const halo_fe_t* xi_inv);
+
+/* ------------------------------------------------------------------ field self-test helpers
+ * Elementwise device field ops over host arrays (used by the parity tests of a1):
+ * op 0 = mul, 1 = add, 2 = sub, 3 = sqr(a), 4 = inverse(a) (0 -> 0), 5 = neg(a). */
+int halo_field_op(halo_field_t field, int op, const halo_fe_t* a, const halo_fe_t* b, size_t n,
+                  halo_fe_t* out);
+/* Elementwise device curve ops over host arrays (parity tests of a2):
+ * op 0 = a + b, 1 = 2a, 2 = k * a (k = scalars, Montgomery). */
+int halo_curve_op(halo_curve_t curve, int op, const halo_wrapped_point_t* a,
+                  const halo_wrapped_point_t* b, const halo_fe_t* k, size_t n,
+                  halo_wrapped_point_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HALO_GPU_H */
