@@ -90,6 +90,13 @@ def load(path: str = LIB_PATH):
         raise RuntimeError(
             f"{path} is missing: build it with `make -C halo_amd/csrc` (or __graft_entry__.build()); "
             "halo_amd has no CPU fallback")
+    # One HIP runtime per process: PyTorch-ROCm bundles its own libamdhip64.so.7.  Load it first so
+    # that this library's NEEDED libamdhip64.so.7 binds to the same runtime (otherwise two HIP
+    # runtimes end up in the process and the second one sees no devices).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(path)
     for name, args in SIGNATURES.items():
         try:
