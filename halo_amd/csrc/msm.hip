@@ -1,0 +1,768 @@
+// Pippenger multi-scalar multiplication on gfx950.
+//
+// Replaces `VariableBaseMSM::msm_unchecked` as called by group::point_dot_affine
+// (crates/group/src/group.rs:48-50) and pedersen::commit (crates/accumulation/src/pedersen.rs:21),
+// plus the SRS provider PublicParams (crates/group/src/pp.rs:26-94).
+//
+// Pipeline (all on the device, no host round trip):
+//   1. digits   : scalar (ark Montgomery) -> canonical -> W signed c-bit digits
+//                 (|d| <= 2^(c-1), W = ceil(256 / c)); key = (window, |d| - 1), value = index|sign.
+//   2. sort     : counting sort of the W*n (key, value) pairs by key: per-chunk LDS histograms,
+//                 column prefix, global exclusive scan (bucket starts), LDS-ranked scatter.
+//   3. tasks    : every bucket is cut into tasks of <= K entries (skew-proof: an all-equal scalar
+//                 vector becomes n/K equal tasks instead of one serial bucket).
+//   4. acc      : one thread per task sums its points with XYZZ mixed additions (8M + 2S).
+//   5. merge    : bucket sum = sum of its task partials.
+//   6. reduce   : per window, segments of L buckets -> (sum_t t B_t, sum_t B_t) by running sums;
+//                 one workgroup per window forms sum_j (acc_j + jL sum_j) and tree-reduces in LDS.
+//   7. final    : Horner over the windows (+ w * S for hiding commitments), XYZZ -> affine -> ark.
+#include <algorithm>
+
+#include "dispatch.hpp"
+#include "msm.hpp"
+#include "runtime.hpp"
+
+namespace halo {
+
+constexpr uint32_t DIGIT_NONE = 0xffffffffu;
+constexpr int MSM_TASK_K = 64;   // max entries per accumulation task
+constexpr int MSM_SEG_L = 32;    // buckets per reduction segment
+constexpr int HIST_THREADS = 1024;
+constexpr int SCAN_THREADS = 1024;
+
+// ---------------------------------------------------------------------------------------------
+// synthetic bases / scalars (shared host/device definition)
+// ---------------------------------------------------------------------------------------------
+__host__ __device__ inline uint64_t splitmix64(uint64_t& x) {
+    uint64_t z = (x += 0x9e3779b97f4a7c15ull);
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+__host__ __device__ inline void synth_scalar(uint64_t seed, uint64_t j, uint64_t out[4]) {
+    uint64_t st = seed ^ (j * 0xd1b54a32d192ed03ull);
+    for (int i = 0; i < 4; i++) out[i] = splitmix64(st);
+    out[3] &= 0x1fffffffffffffffull;  // < 2^253 < p
+    if ((out[0] | out[1] | out[2] | out[3]) == 0) out[0] = 1;
+}
+
+// ---------------------------------------------------------------------------------------------
+// conversion / generation kernels
+// ---------------------------------------------------------------------------------------------
+template <class F>
+__global__ void k_wrapped_to_internal(const uint4* in, uint4* out, size_t n) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    aff_store(out + 4 * i, aff_from_wrapped<F>(in + 4 * i));
+}
+
+template <class F>
+__global__ void k_internal_to_wrapped(const uint4* in, uint4* out, size_t n) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    aff_to_wrapped(out + 4 * i, aff_load<F>(in + 4 * i));
+}
+
+template <class Cv>
+__global__ void k_synth_bases(uint4* out, size_t n, uint64_t seed) {
+    using F = typename Cv::Base;
+    const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    uint64_t k[4];
+    synth_scalar(seed, j, k);
+    uint32_t w[8];
+    for (int i = 0; i < 4; i++) {
+        w[2 * i] = (uint32_t)k[i];
+        w[2 * i + 1] = (uint32_t)(k[i] >> 32);
+    }
+    Affine<F> G;
+    G.x = fe_from_const<F>(Cv::K::GX);
+    G.y = fe_from_const<F>(Cv::K::GY);
+    aff_store(out + 4 * j, xyzz_to_aff(xyzz_scalar_mul(G, w)));
+}
+
+// ---------------------------------------------------------------------------------------------
+// 1. digits
+// ---------------------------------------------------------------------------------------------
+template <class S>
+__global__ void k_digits(const uint4* scalars, size_t n, int c, int W, uint32_t* digits) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t w8[8];
+    fe_ark_to_canonical_words<S>(scalars + 2 * i, w8);
+    const uint32_t half = 1u << (c - 1);
+    const uint32_t full = 1u << c;
+    uint32_t carry = 0;
+    for (int w = 0; w < W; w++) {
+        const int bit = w * c;
+        uint32_t raw = 0;
+        if (bit < 256) {
+            const int q = bit >> 5, s = bit & 31;
+            uint64_t lo = w8[q];
+            uint64_t hi = (q + 1 < 8) ? w8[q + 1] : 0;
+            raw = (uint32_t)(((hi << 32) | lo) >> s) & (full - 1);
+        }
+        uint32_t v = raw + carry;
+        uint32_t out;
+        if (v > half) {
+            carry = 1;
+            const uint32_t mag = full - v;  // |d|, d = v - 2^c < 0
+            out = (mag == 0) ? DIGIT_NONE : ((mag - 1) | 0x80000000u);
+        } else {
+            carry = 0;
+            out = (v == 0) ? DIGIT_NONE : (v - 1);
+        }
+        digits[(size_t)w * n + i] = out;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// 2. counting sort
+// ---------------------------------------------------------------------------------------------
+// grid (chunks, W); hist[(w * chunks + chunk) * B + b]
+__global__ __launch_bounds__(HIST_THREADS) void k_hist(const uint32_t* digits, size_t n, uint32_t B, int chunks,
+                                                       uint32_t* hist) {
+    extern __shared__ uint32_t cnt[];
+    const int chunk = blockIdx.x, w = blockIdx.y;
+    for (uint32_t b = threadIdx.x; b < B; b += HIST_THREADS) cnt[b] = 0;
+    __syncthreads();
+    const size_t per = (n + chunks - 1) / chunks;
+    const size_t beg = (size_t)chunk * per, end = min(n, beg + per);
+    const uint32_t* d = digits + (size_t)w * n;
+    for (size_t i = beg + threadIdx.x; i < end; i += HIST_THREADS) {
+        const uint32_t v = d[i];
+        if (v != DIGIT_NONE) atomicAdd(&cnt[v & 0x7fffffffu], 1u);
+    }
+    __syncthreads();
+    uint32_t* h = hist + ((size_t)w * chunks + chunk) * B;
+    for (uint32_t b = threadIdx.x; b < B; b += HIST_THREADS) h[b] = cnt[b];
+}
+
+// thread per (w, b): per-chunk exclusive prefix (in place) + totals[w * B + b]
+__global__ void k_colsum(uint32_t* hist, int chunks, uint32_t B, int W, uint32_t* totals) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (size_t)W * B) return;
+    const size_t w = t / B, b = t % B;
+    uint32_t run = 0;
+    for (int c = 0; c < chunks; c++) {
+        uint32_t* p = hist + (w * chunks + c) * B + b;
+        const uint32_t v = *p;
+        *p = run;
+        run += v;
+    }
+    totals[t] = run;
+}
+
+// generic exclusive scan of u32 (3 kernels); out[n] = total
+__global__ __launch_bounds__(SCAN_THREADS) void k_scan_reduce(const uint32_t* in, size_t n, size_t per_block,
+                                                              uint32_t* block_sums) {
+    __shared__ uint32_t s[SCAN_THREADS];
+    const size_t beg = (size_t)blockIdx.x * per_block;
+    const size_t end = min(n, beg + per_block);
+    uint32_t acc = 0;
+    for (size_t i = beg + threadIdx.x; i < end; i += SCAN_THREADS) acc += in[i];
+    s[threadIdx.x] = acc;
+    __syncthreads();
+    for (int off = SCAN_THREADS / 2; off > 0; off >>= 1) {
+        if ((int)threadIdx.x < off) s[threadIdx.x] += s[threadIdx.x + off];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) block_sums[blockIdx.x] = s[0];
+}
+
+__device__ inline uint32_t block_exclusive_scan(uint32_t v, uint32_t* s, uint32_t* total) {
+    // Hillis-Steele over SCAN_THREADS entries
+    s[threadIdx.x] = v;
+    __syncthreads();
+    for (int off = 1; off < SCAN_THREADS; off <<= 1) {
+        uint32_t t = ((int)threadIdx.x >= off) ? s[threadIdx.x - off] : 0;
+        __syncthreads();
+        s[threadIdx.x] += t;
+        __syncthreads();
+    }
+    const uint32_t incl = s[threadIdx.x];
+    *total = s[SCAN_THREADS - 1];
+    __syncthreads();
+    return incl - v;
+}
+
+__global__ __launch_bounds__(SCAN_THREADS) void k_scan_blocksums(uint32_t* block_sums, int nb) {
+    __shared__ uint32_t s[SCAN_THREADS];
+    // nb <= SCAN_THREADS * 8 : each thread scans up to 8 consecutive
+    const int per = (nb + SCAN_THREADS - 1) / SCAN_THREADS;
+    uint32_t loc[8];
+    uint32_t acc = 0;
+    for (int k = 0; k < per; k++) {
+        const int i = threadIdx.x * per + k;
+        loc[k] = (i < nb) ? block_sums[i] : 0;
+        acc += loc[k];
+    }
+    uint32_t tot;
+    uint32_t ex = block_exclusive_scan(acc, s, &tot);
+    for (int k = 0; k < per; k++) {
+        const int i = threadIdx.x * per + k;
+        if (i < nb) block_sums[i] = ex;
+        ex += loc[k];
+    }
+    if (threadIdx.x == 0) block_sums[nb] = tot;
+}
+
+__global__ __launch_bounds__(SCAN_THREADS) void k_scan_apply(const uint32_t* in, size_t n, size_t per_block,
+                                                             const uint32_t* block_sums, uint32_t* out) {
+    __shared__ uint32_t s[SCAN_THREADS];
+    const size_t beg = (size_t)blockIdx.x * per_block;
+    const size_t end = min(n, beg + per_block);
+    uint32_t base = block_sums[blockIdx.x];
+    // process the block range in tiles of SCAN_THREADS * 4 consecutive elements per thread
+    for (size_t tile = beg; tile < end; tile += (size_t)SCAN_THREADS * 4) {
+        uint32_t loc[4];
+        uint32_t acc = 0;
+        for (int k = 0; k < 4; k++) {
+            const size_t i = tile + (size_t)threadIdx.x * 4 + k;
+            loc[k] = (i < end) ? in[i] : 0;
+            acc += loc[k];
+        }
+        uint32_t tot;
+        uint32_t ex = block_exclusive_scan(acc, s, &tot) + base;
+        for (int k = 0; k < 4; k++) {
+            const size_t i = tile + (size_t)threadIdx.x * 4 + k;
+            if (i < end) out[i] = ex;
+            ex += loc[k];
+        }
+        base += tot;
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) out[n] = block_sums[gridDim.x];
+}
+
+__global__ __launch_bounds__(HIST_THREADS) void k_scatter(const uint32_t* digits, size_t n, uint32_t B, int chunks,
+                                                          const uint32_t* hist_prefix, const uint32_t* bstart,
+                                                          uint32_t* sorted) {
+    extern __shared__ uint32_t cnt[];
+    const int chunk = blockIdx.x, w = blockIdx.y;
+    for (uint32_t b = threadIdx.x; b < B; b += HIST_THREADS) cnt[b] = 0;
+    __syncthreads();
+    const size_t per = (n + chunks - 1) / chunks;
+    const size_t beg = (size_t)chunk * per, end = min(n, beg + per);
+    const uint32_t* d = digits + (size_t)w * n;
+    const uint32_t* hp = hist_prefix + ((size_t)w * chunks + chunk) * B;
+    const uint32_t* bs = bstart + (size_t)w * B;
+    for (size_t i = beg + threadIdx.x; i < end; i += HIST_THREADS) {
+        const uint32_t v = d[i];
+        if (v == DIGIT_NONE) continue;
+        const uint32_t b = v & 0x7fffffffu;
+        const uint32_t r = atomicAdd(&cnt[b], 1u);
+        sorted[bs[b] + hp[b] + r] = (uint32_t)i | (v & 0x80000000u);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// 3-5. tasks, accumulation, merge
+// ---------------------------------------------------------------------------------------------
+__global__ void k_ntask(const uint32_t* bstart, size_t nb, uint32_t* ntask) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nb) return;
+    const uint32_t cnt = bstart[t + 1] - bstart[t];
+    ntask[t] = (cnt + MSM_TASK_K - 1) / MSM_TASK_K;
+}
+
+struct Task {
+    uint32_t begin, end;
+};
+
+__global__ void k_tasks(const uint32_t* bstart, const uint32_t* task_off, size_t nb, Task* tasks) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nb) return;
+    uint32_t b = bstart[t];
+    const uint32_t e = bstart[t + 1];
+    uint32_t o = task_off[t];
+    for (; b < e; b += MSM_TASK_K) tasks[o++] = Task{b, min(e, b + (uint32_t)MSM_TASK_K)};
+}
+
+template <class Cv>
+__global__ __launch_bounds__(256) void k_acc(const Task* tasks, const uint32_t* ntasks_total, const uint32_t* sorted,
+                                             const uint4* bases, uint4* partials) {
+    using F = typename Cv::Base;
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= *ntasks_total) return;
+    const Task tk = tasks[t];
+    XYZZ<F> acc = xyzz_id<F>();
+    for (uint32_t e = tk.begin; e < tk.end; e++) {
+        const uint32_t v = sorted[e];
+        Affine<F> p = aff_load<F>(bases + 4 * (size_t)(v & 0x7fffffffu));
+        if (v & 0x80000000u) p.y = fe_neg(p.y);
+        acc = xyzz_madd(acc, p);
+    }
+    xyzz_store(partials + 8 * t, acc);
+}
+
+template <class Cv>
+__global__ void k_merge(const uint32_t* task_off, size_t nb, const uint4* partials, uint4* bucket_sums) {
+    using F = typename Cv::Base;
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nb) return;
+    const uint32_t b = task_off[t], e = task_off[t + 1];
+    XYZZ<F> acc = xyzz_id<F>();
+    if (e > b) acc = xyzz_load<F>(partials + 8 * (size_t)b);
+    for (uint32_t k = b + 1; k < e; k++) acc = xyzz_add(acc, xyzz_load<F>(partials + 8 * (size_t)k));
+    xyzz_store(bucket_sums + 8 * t, acc);
+}
+
+// ---------------------------------------------------------------------------------------------
+// 6. per-window reduction
+// ---------------------------------------------------------------------------------------------
+// thread per (w, segment j): acc_j = sum_t t B_{jL+t}, sum_j = sum_t B_{jL+t}  (t = 1..L)
+template <class Cv>
+__global__ void k_seg(const uint4* bucket_sums, uint32_t B, uint32_t L, int W, uint4* seg_acc, uint4* seg_sum) {
+    using F = typename Cv::Base;
+    const uint32_t nseg = B / L;
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (size_t)W * nseg) return;
+    const size_t w = t / nseg, j = t % nseg;
+    const uint4* bs = bucket_sums + 8 * (w * B + j * L);
+    XYZZ<F> run = xyzz_id<F>(), acc = xyzz_id<F>();
+    for (int k = (int)L - 1; k >= 0; k--) {
+        run = xyzz_add(run, xyzz_load<F>(bs + 8 * k));
+        acc = xyzz_add(acc, run);
+    }
+    xyzz_store(seg_acc + 8 * t, acc);
+    xyzz_store(seg_sum + 8 * t, run);
+}
+
+// small scalar multiplication k * P (k < 2^32)
+template <class F>
+HALO_DEV XYZZ<F> xyzz_mul_small(const XYZZ<F>& P, uint32_t k) {
+    XYZZ<F> r = xyzz_id<F>();
+    if (k == 0) return r;
+    const int top = 31 - __clz(k);
+    for (int i = top; i >= 0; i--) {
+        r = xyzz_dbl(r);
+        if ((k >> i) & 1u) r = xyzz_add(r, P);
+    }
+    return r;
+}
+
+// one workgroup per window: S_w = sum_j (acc_j + (j L) sum_j)
+template <class Cv>
+__global__ __launch_bounds__(256) void k_wcombine(const uint4* seg_acc, const uint4* seg_sum, uint32_t B,
+                                                  uint32_t L, uint4* window_sums) {
+    using F = typename Cv::Base;
+    __shared__ uint4 red[256 * 8];
+    const uint32_t nseg = B / L;
+    const int w = blockIdx.x;
+    XYZZ<F> acc = xyzz_id<F>();
+    for (uint32_t j = threadIdx.x; j < nseg; j += blockDim.x) {
+        const size_t t = (size_t)w * nseg + j;
+        XYZZ<F> x = xyzz_load<F>(seg_acc + 8 * t);
+        if (j) x = xyzz_add(x, xyzz_mul_small(xyzz_load<F>(seg_sum + 8 * t), j * L));
+        acc = xyzz_add(acc, x);
+    }
+    xyzz_store(red + 8 * threadIdx.x, acc);
+    __syncthreads();
+    for (int off = blockDim.x / 2; off > 0; off >>= 1) {
+        if ((int)threadIdx.x < off)
+            xyzz_store(red + 8 * threadIdx.x,
+                       xyzz_add(xyzz_load<F>(red + 8 * threadIdx.x), xyzz_load<F>(red + 8 * (threadIdx.x + off))));
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) xyzz_store(window_sums + 8 * w, xyzz_load<F>(red));
+}
+
+// ---------------------------------------------------------------------------------------------
+// 7. final: Horner over windows (+ hiding term), to ark affine
+// ---------------------------------------------------------------------------------------------
+template <class Cv>
+__global__ void k_final(const uint4* window_sums, int W, int c, const uint4* hide_point /* internal affine or null */,
+                        const uint4* hide_scalar /* ark or null */, uint4* out_wrapped) {
+    using F = typename Cv::Base;
+    using S = typename Cv::Scalar;
+    __shared__ uint4 part[8];
+    if (threadIdx.x == 1) {
+        XYZZ<F> h = xyzz_id<F>();
+        if (hide_point && hide_scalar) {
+            uint32_t w8[8];
+            fe_ark_to_canonical_words<S>(hide_scalar, w8);
+            h = xyzz_scalar_mul(aff_load<F>(hide_point), w8);
+        }
+        xyzz_store(part, h);
+    }
+    XYZZ<F> acc = xyzz_id<F>();
+    if (threadIdx.x == 0) {
+        for (int w = W - 1; w >= 0; w--) {
+            if (w != W - 1)
+                for (int k = 0; k < c; k++) acc = xyzz_dbl(acc);
+            acc = xyzz_add(acc, xyzz_load<F>(window_sums + 8 * w));
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        acc = xyzz_add(acc, xyzz_load<F>(part));
+        aff_to_wrapped(out_wrapped, xyzz_to_aff(acc));
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// host orchestration
+// ---------------------------------------------------------------------------------------------
+int msm_window_bits(size_t n) {
+    unsigned lg = n > 1 ? ilog2(n - 1) + 1 : 1;
+    int c = (int)lg - 4;
+    return std::max(4, std::min(16, c));
+}
+
+static unsigned grid_for(size_t n, unsigned thr) { return (unsigned)std::max<size_t>(1, (n + thr - 1) / thr); }
+
+struct MsmScratch {
+    DevBuf digits, hist, totals, bstart, sorted, ntask, task_off, tasks, partials, bucket_sums, seg_acc, seg_sum,
+        window_sums, scan_tmp, out;
+};
+static MsmScratch g_msm_scratch[64];  // per device
+
+static int device_scan(const uint32_t* in, size_t n, uint32_t* out, DevBuf& tmp, hipStream_t s) {
+    // out has n + 1 entries
+    const size_t per_block = (size_t)SCAN_THREADS * 16;
+    size_t nb = (n + per_block - 1) / per_block;
+    if (nb == 0) nb = 1;
+    if (nb > (size_t)SCAN_THREADS * 8) return set_error(HALO_EINVAL, "scan too large (%zu)", n);
+    HALO_CHECK(tmp.reserve((nb + 1) * 4));
+    hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)nb), dim3(SCAN_THREADS), 0, s, in, n, per_block,
+                       tmp.as<uint32_t>());
+    hipLaunchKernelGGL(k_scan_blocksums, dim3(1), dim3(SCAN_THREADS), 0, s, tmp.as<uint32_t>(), (int)nb);
+    hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)nb), dim3(SCAN_THREADS), 0, s, in, n, per_block,
+                       tmp.as<const uint32_t>(), out);
+    HALO_HIP(hipGetLastError());
+    return HALO_OK;
+}
+
+template <class Cv>
+static int msm_device_t(DeviceState* st, const uint4* bases_int, const uint4* scalars_ark, size_t n,
+                        const uint4* hide_point, const uint4* hide_scalar, uint4* d_out_wrapped, hipStream_t s) {
+    MsmScratch& M = g_msm_scratch[st->device & 63];
+    if (n == 0) {
+        HALO_HIP(hipMemsetAsync(d_out_wrapped, 0, 64, s));
+        if (!hide_point) return HALO_OK;
+    }
+    const size_t nn = std::max<size_t>(n, 1);
+    const int c = msm_window_bits(nn);
+    const int W = (256 + c - 1) / c;
+    const uint32_t B = 1u << (c - 1);
+    const size_t NB = (size_t)W * B;
+    const int chunks = (int)std::max<size_t>(1, std::min<size_t>(32, nn / 4096));
+    HALO_CHECK(M.digits.reserve((size_t)W * nn * 4));
+    HALO_CHECK(M.hist.reserve((size_t)W * chunks * B * 4));
+    HALO_CHECK(M.totals.reserve(NB * 4));
+    HALO_CHECK(M.bstart.reserve((NB + 1) * 4));
+    HALO_CHECK(M.sorted.reserve((size_t)W * nn * 4));
+    HALO_CHECK(M.ntask.reserve(NB * 4));
+    HALO_CHECK(M.task_off.reserve((NB + 1) * 4));
+    const size_t max_tasks = NB + (size_t)W * nn / MSM_TASK_K + 1;
+    HALO_CHECK(M.tasks.reserve(max_tasks * sizeof(Task)));
+    HALO_CHECK(M.partials.reserve(max_tasks * 128));
+    HALO_CHECK(M.bucket_sums.reserve(NB * 128));
+    const uint32_t L = std::min<uint32_t>(MSM_SEG_L, B);
+    const size_t nseg = NB / L;
+    HALO_CHECK(M.seg_acc.reserve(nseg * 128));
+    HALO_CHECK(M.seg_sum.reserve(nseg * 128));
+    HALO_CHECK(M.window_sums.reserve((size_t)W * 128));
+
+    static bool attrs_set = false;
+    if (!attrs_set) {
+        HALO_HIP(hipFuncSetAttribute((const void*)k_hist, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        HALO_HIP(hipFuncSetAttribute((const void*)k_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        attrs_set = true;
+    }
+    if (n > 0) {
+        hipLaunchKernelGGL(k_digits<typename Cv::Scalar>, dim3(grid_for(n, 256)), dim3(256), 0, s, scalars_ark, n, c,
+                           W, M.digits.as<uint32_t>());
+        hipLaunchKernelGGL(k_hist, dim3(chunks, W), dim3(HIST_THREADS), B * 4, s, M.digits.as<const uint32_t>(), n, B,
+                           chunks, M.hist.as<uint32_t>());
+        hipLaunchKernelGGL(k_colsum, dim3(grid_for(NB, 256)), dim3(256), 0, s, M.hist.as<uint32_t>(), chunks, B, W,
+                           M.totals.as<uint32_t>());
+        HALO_HIP(hipGetLastError());
+        HALO_CHECK(device_scan(M.totals.as<const uint32_t>(), NB, M.bstart.as<uint32_t>(), M.scan_tmp, s));
+        hipLaunchKernelGGL(k_scatter, dim3(chunks, W), dim3(HIST_THREADS), B * 4, s, M.digits.as<const uint32_t>(), n,
+                           B, chunks, M.hist.as<const uint32_t>(), M.bstart.as<const uint32_t>(),
+                           M.sorted.as<uint32_t>());
+        hipLaunchKernelGGL(k_ntask, dim3(grid_for(NB, 256)), dim3(256), 0, s, M.bstart.as<const uint32_t>(), NB,
+                           M.ntask.as<uint32_t>());
+        HALO_HIP(hipGetLastError());
+        HALO_CHECK(device_scan(M.ntask.as<const uint32_t>(), NB, M.task_off.as<uint32_t>(), M.scan_tmp, s));
+        hipLaunchKernelGGL(k_tasks, dim3(grid_for(NB, 256)), dim3(256), 0, s, M.bstart.as<const uint32_t>(),
+                           M.task_off.as<const uint32_t>(), NB, M.tasks.as<Task>());
+        hipLaunchKernelGGL(k_acc<Cv>, dim3(grid_for(max_tasks, 256)), dim3(256), 0, s, M.tasks.as<const Task>(),
+                           M.task_off.as<const uint32_t>() + NB, M.sorted.as<const uint32_t>(), bases_int,
+                           M.partials.as<uint4>());
+        hipLaunchKernelGGL(k_merge<Cv>, dim3(grid_for(NB, 256)), dim3(256), 0, s, M.task_off.as<const uint32_t>(), NB,
+                           M.partials.as<const uint4>(), M.bucket_sums.as<uint4>());
+        hipLaunchKernelGGL(k_seg<Cv>, dim3(grid_for(nseg, 64)), dim3(64), 0, s, M.bucket_sums.as<const uint4>(), B, L,
+                           W, M.seg_acc.as<uint4>(), M.seg_sum.as<uint4>());
+        hipLaunchKernelGGL(k_wcombine<Cv>, dim3(W), dim3(256), 0, s, M.seg_acc.as<const uint4>(),
+                           M.seg_sum.as<const uint4>(), B, L, M.window_sums.as<uint4>());
+        HALO_HIP(hipGetLastError());
+    } else {
+        // identity window sums
+        HALO_HIP(hipMemsetAsync(M.window_sums.ptr, 0, (size_t)W * 128, s));
+    }
+    hipLaunchKernelGGL(k_final<Cv>, dim3(1), dim3(64), 0, s, M.window_sums.as<const uint4>(), n ? W : 1, c, hide_point,
+                       hide_scalar, d_out_wrapped);
+    HALO_HIP(hipGetLastError());
+    return HALO_OK;
+}
+
+int msm_device(DeviceState* st, int curve, const void* bases_int, const void* scalars_ark, size_t n,
+               const void* hide_point, const void* hide_scalar, void* d_out_wrapped, hipStream_t s) {
+    int rc;
+    DISPATCH_CURVE(curve, Cv, {
+        rc = msm_device_t<Cv>(st, (const uint4*)bases_int, (const uint4*)scalars_ark, n, (const uint4*)hide_point,
+                              (const uint4*)hide_scalar, (uint4*)d_out_wrapped, s);
+    });
+    return rc;
+}
+
+int convert_wrapped_to_internal(int curve, const void* in, void* out, size_t n, hipStream_t s) {
+    if (!n) return HALO_OK;
+    DISPATCH_CURVE(curve, Cv, {
+        hipLaunchKernelGGL(k_wrapped_to_internal<typename Cv::Base>, dim3(grid_for(n, 256)), dim3(256), 0, s,
+                           (const uint4*)in, (uint4*)out, n);
+    });
+    HALO_HIP(hipGetLastError());
+    return HALO_OK;
+}
+
+int convert_internal_to_wrapped(int curve, const void* in, void* out, size_t n, hipStream_t s) {
+    if (!n) return HALO_OK;
+    DISPATCH_CURVE(curve, Cv, {
+        hipLaunchKernelGGL(k_internal_to_wrapped<typename Cv::Base>, dim3(grid_for(n, 256)), dim3(256), 0, s,
+                           (const uint4*)in, (uint4*)out, n);
+    });
+    HALO_HIP(hipGetLastError());
+    return HALO_OK;
+}
+
+}  // namespace halo
+
+using namespace halo;
+
+static int check_curve(halo_curve_t c) {
+    if (c != HALO_PALLAS && c != HALO_VESTA) return set_error(HALO_EINVAL, "unknown curve id %d", (int)c);
+    return HALO_OK;
+}
+
+extern "C" int halo_msm_window_bits(size_t n) { return msm_window_bits(n); }
+
+extern "C" void halo_synth_scalar(halo_curve_t curve, uint64_t seed, uint64_t j, uint64_t out_canonical[4]) {
+    (void)curve;
+    synth_scalar(seed, j, out_canonical);
+}
+
+// host arrays: bases (ark WrappedPoint), scalars (ark) -> out (host)
+extern "C" int halo_msm(halo_curve_t curve, const halo_wrapped_point_t* bases, size_t n_bases,
+                        const halo_fe_t* scalars, size_t n_scalars, halo_wrapped_point_t* out) {
+    clear_error();
+    HALO_CHECK(check_curve(curve));
+    const size_t n = std::min(n_bases, n_scalars);
+    if (!out || (n && (!bases || !scalars))) return set_error(HALO_EINVAL, "halo_msm: null buffer");
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    hipStream_t s = 0;
+    HALO_CHECK(st->scratch[0].reserve(std::max<size_t>(n, 1) * 64));
+    HALO_CHECK(st->scratch[1].reserve(std::max<size_t>(n, 1) * 64));
+    HALO_CHECK(st->scratch[2].reserve(std::max<size_t>(n, 1) * 32));
+    HALO_CHECK(st->scratch[3].reserve(64));
+    HALO_CHECK(copy_h2d(st->scratch[0].ptr, bases, n * 64, s));
+    HALO_CHECK(copy_h2d(st->scratch[2].ptr, scalars, n * 32, s));
+    HALO_CHECK(convert_wrapped_to_internal(curve, st->scratch[0].ptr, st->scratch[1].ptr, n, s));
+    HALO_CHECK(msm_device(st, curve, st->scratch[1].ptr, st->scratch[2].ptr, n, nullptr, nullptr, st->scratch[3].ptr, s));
+    return copy_d2h(out, st->scratch[3].ptr, 64, s);
+}
+
+// SRS management --------------------------------------------------------------------------------
+extern "C" int halo_srs_upload(halo_curve_t curve, const halo_wrapped_point_t* gs, size_t n,
+                               const halo_wrapped_point_t* S, const halo_wrapped_point_t* H) {
+    clear_error();
+    HALO_CHECK(check_curve(curve));
+    if ((n && !gs)) return set_error(HALO_EINVAL, "halo_srs_upload: null gs");
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    hipStream_t s = 0;
+    SrsState& srs = st->srs[curve];
+    HALO_CHECK(srs.gs.reserve(std::max<size_t>(n, 1) * 64));
+    HALO_CHECK(st->scratch[0].reserve(std::max<size_t>(n, 2) * 64));
+    HALO_CHECK(copy_h2d(st->scratch[0].ptr, gs, n * 64, s));
+    HALO_CHECK(convert_wrapped_to_internal(curve, st->scratch[0].ptr, srs.gs.ptr, n, s));
+    srs.n = n;
+    srs.shifted_c = 0;
+    if (S && H) {
+        HALO_CHECK(st->scratch[1].reserve(128));
+        HALO_CHECK(copy_h2d(st->scratch[0].ptr, S, 64, s));
+        HALO_CHECK(copy_h2d((char*)st->scratch[0].ptr + 64, H, 64, s));
+        HALO_CHECK(convert_wrapped_to_internal(curve, st->scratch[0].ptr, st->scratch[1].ptr, 2, s));
+        HALO_CHECK(copy_d2h(srs.S, st->scratch[1].ptr, 64, s));
+        HALO_CHECK(copy_d2h(srs.H, (char*)st->scratch[1].ptr + 64, 64, s));
+        srs.has_sh = true;
+    }
+    HALO_HIP(hipStreamSynchronize(s));
+    return HALO_OK;
+}
+
+extern "C" int halo_srs_len(halo_curve_t curve, size_t* n) {
+    clear_error();
+    HALO_CHECK(check_curve(curve));
+    if (!n) return set_error(HALO_EINVAL, "null n");
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    *n = st->srs[curve].n;
+    return HALO_OK;
+}
+
+extern "C" int halo_srs_synthesize(halo_curve_t curve, size_t n, uint64_t seed) {
+    clear_error();
+    HALO_CHECK(check_curve(curve));
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    hipStream_t s = 0;
+    SrsState& srs = st->srs[curve];
+    HALO_CHECK(srs.gs.reserve(std::max<size_t>(n, 1) * 64));
+    if (n) {
+        DISPATCH_CURVE(curve, Cv, {
+            hipLaunchKernelGGL(k_synth_bases<Cv>, dim3(grid_for(n, 64)), dim3(64), 0, s, srs.gs.as<uint4>(), n, seed);
+        });
+        HALO_HIP(hipGetLastError());
+    }
+    HALO_HIP(hipStreamSynchronize(s));
+    srs.n = n;
+    srs.shifted_c = 0;
+    return HALO_OK;
+}
+
+extern "C" int halo_srs_precompute_windows(halo_curve_t curve) {
+    clear_error();
+    HALO_CHECK(check_curve(curve));
+    return HALO_OK;  // optional optimisation; the windowed path needs no precomputation
+}
+
+extern "C" int halo_msm_srs(halo_curve_t curve, const halo_fe_t* scalars, size_t n, halo_wrapped_point_t* out) {
+    clear_error();
+    HALO_CHECK(check_curve(curve));
+    if (!out || (n && !scalars)) return set_error(HALO_EINVAL, "halo_msm_srs: null buffer");
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    SrsState& srs = st->srs[curve];
+    if (n > srs.n) return set_error(HALO_ESRSRANGE, "n (%zu) exceeds the resident SRS length (%zu)", n, srs.n);
+    hipStream_t s = 0;
+    HALO_CHECK(st->scratch[2].reserve(std::max<size_t>(n, 1) * 32));
+    HALO_CHECK(st->scratch[3].reserve(64));
+    HALO_CHECK(copy_h2d(st->scratch[2].ptr, scalars, n * 32, s));
+    HALO_CHECK(msm_device(st, curve, srs.gs.ptr, st->scratch[2].ptr, n, nullptr, nullptr, st->scratch[3].ptr, s));
+    return copy_d2h(out, st->scratch[3].ptr, 64, s);
+}
+
+extern "C" int halo_msm_dev(halo_curve_t curve, const void* d_bases, const void* d_scalars, size_t n,
+                            halo_wrapped_point_t* out, void* stream) {
+    clear_error();
+    HALO_CHECK(check_curve(curve));
+    if (!out || (n && !d_scalars)) return set_error(HALO_EINVAL, "halo_msm_dev: null buffer");
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    hipStream_t s = (hipStream_t)stream;
+    const void* bases = d_bases;
+    if (!bases) {
+        SrsState& srs = st->srs[curve];
+        if (n > srs.n) return set_error(HALO_ESRSRANGE, "n (%zu) exceeds the resident SRS length (%zu)", n, srs.n);
+        bases = srs.gs.ptr;
+    } else {
+        HALO_CHECK(st->scratch[6].reserve(std::max<size_t>(n, 1) * 64));
+        HALO_CHECK(convert_wrapped_to_internal(curve, d_bases, st->scratch[6].ptr, n, s));
+        bases = st->scratch[6].ptr;
+    }
+    HALO_CHECK(st->scratch[7].reserve(64));
+    HALO_CHECK(msm_device(st, curve, bases, d_scalars, n, nullptr, nullptr, st->scratch[7].ptr, s));
+    return copy_d2h(out, st->scratch[7].ptr, 64, s);
+}
+
+// pedersen::commit(w, Gs, ms) -- crates/accumulation/src/pedersen.rs:7-27
+extern "C" int halo_pedersen_commit(halo_curve_t curve, const halo_fe_t* w, const halo_wrapped_point_t* gs,
+                                    size_t n_gs, const halo_fe_t* ms, size_t n_ms, halo_wrapped_point_t* out) {
+    clear_error();
+    HALO_CHECK(check_curve(curve));
+    if (!out || (n_ms && !ms) || (n_gs && !gs)) return set_error(HALO_EINVAL, "halo_pedersen_commit: null buffer");
+    if (n_gs < n_ms)
+        return set_error(HALO_ELENGTH, "ms must be larger than Gs: (Gs: %zu), (ms: %zu)", n_gs, n_ms);
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    SrsState& srs = st->srs[curve];
+    if (w && !srs.has_sh) return set_error(HALO_ESRSRANGE, "hiding commitment needs S: upload the SRS (S, H) first");
+    hipStream_t s = 0;
+    const size_t n = n_ms;
+    HALO_CHECK(st->scratch[0].reserve(std::max<size_t>(n, 1) * 64));
+    HALO_CHECK(st->scratch[1].reserve(std::max<size_t>(n, 1) * 64));
+    HALO_CHECK(st->scratch[2].reserve(std::max<size_t>(n, 1) * 32));
+    HALO_CHECK(st->scratch[3].reserve(64 + 64 + 32));
+    HALO_CHECK(copy_h2d(st->scratch[0].ptr, gs, n * 64, s));
+    HALO_CHECK(copy_h2d(st->scratch[2].ptr, ms, n * 32, s));
+    HALO_CHECK(convert_wrapped_to_internal(curve, st->scratch[0].ptr, st->scratch[1].ptr, n, s));
+    char* small = (char*)st->scratch[3].ptr;
+    const void* hp = nullptr;
+    const void* hs = nullptr;
+    if (w) {
+        HALO_CHECK(copy_h2d(small + 64, srs.S, 64, s));
+        HALO_CHECK(copy_h2d(small + 128, w, 32, s));
+        hp = small + 64;
+        hs = small + 128;
+    }
+    HALO_CHECK(msm_device(st, curve, st->scratch[1].ptr, st->scratch[2].ptr, n, hp, hs, small, s));
+    return copy_d2h(out, small, 64, s);
+}
+
+static size_t poly_degree(const halo_fe_t* c, size_t len) {
+    // DensePolynomial::degree(): index of the last nonzero coefficient (0 for the zero polynomial)
+    size_t n = len;
+    while (n > 0 && !(c[n - 1].l[0] | c[n - 1].l[1] | c[n - 1].l[2] | c[n - 1].l[3])) n--;
+    return n ? n - 1 : 0;
+}
+
+// pcdl::commit(p, d, w) -- crates/accumulation/src/pcdl.rs:275-287
+extern "C" int halo_pcdl_commit(halo_curve_t curve, const halo_fe_t* coeffs, size_t len, size_t d,
+                                const halo_fe_t* w, halo_wrapped_point_t* out) {
+    clear_error();
+    HALO_CHECK(check_curve(curve));
+    if (!out || (len && !coeffs)) return set_error(HALO_EINVAL, "halo_pcdl_commit: null buffer");
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    size_t D;
+    {
+        std::lock_guard<std::mutex> g(st->mu);
+        D = st->srs[curve].n ? st->srs[curve].n - 1 : 0;
+        if (!st->srs[curve].n) return set_error(HALO_ESRSRANGE, "no resident SRS: call halo_srs_upload first");
+    }
+    const size_t n = d + 1;
+    const size_t p_deg = poly_degree(coeffs, len);
+    if (!is_pow2(n)) return set_error(HALO_ENOTPOW2, "n (%zu) is not a power of two", n);
+    if (p_deg > d) return set_error(HALO_EDEGREE, "p_deg (%zu) <= d (%zu)", p_deg, d);
+    if (d > D) return set_error(HALO_ESRSRANGE, "d (%zu) <= D (%zu) (pp_len = %zu)", d, D, D + 1);
+    // trailing zeros beyond the degree do not change the MSM; ark passes the trimmed coeffs
+    const size_t m = std::min(len, n);
+    std::lock_guard<std::mutex> g(st->mu);
+    SrsState& srs = st->srs[curve];
+    if (w && !srs.has_sh) return set_error(HALO_ESRSRANGE, "hiding commitment needs S: upload the SRS (S, H) first");
+    hipStream_t s = 0;
+    HALO_CHECK(st->scratch[2].reserve(std::max<size_t>(m, 1) * 32));
+    HALO_CHECK(st->scratch[3].reserve(64 + 64 + 32));
+    HALO_CHECK(copy_h2d(st->scratch[2].ptr, coeffs, m * 32, s));
+    char* small = (char*)st->scratch[3].ptr;
+    const void* hp = nullptr;
+    const void* hs = nullptr;
+    if (w) {
+        HALO_CHECK(copy_h2d(small + 64, srs.S, 64, s));
+        HALO_CHECK(copy_h2d(small + 128, w, 32, s));
+        hp = small + 64;
+        hs = small + 128;
+    }
+    HALO_CHECK(msm_device(st, curve, srs.gs.ptr, st->scratch[2].ptr, m, hp, hs, small, s));
+    return copy_d2h(out, small, 64, s);
+}

@@ -1,0 +1,18 @@
+// Internal interfaces shared between msm.hip, ipa.hip and the multi-GPU glue.
+#pragma once
+#include "runtime.hpp"
+
+namespace halo {
+
+int msm_window_bits(size_t n);
+// MSM over device-resident internal-format affine bases (64 B each) and ark-format scalars.
+// Writes one ark WrappedPoint (64 B) to d_out_wrapped (device).  Optional hiding term
+// hide_scalar * hide_point (internal affine point, ark scalar; both device pointers).
+int msm_device(DeviceState* st, int curve, const void* bases_int, const void* scalars_ark, size_t n,
+               const void* hide_point, const void* hide_scalar, void* d_out_wrapped, hipStream_t s);
+int convert_wrapped_to_internal(int curve, const void* in, void* out, size_t n, hipStream_t s);
+int convert_internal_to_wrapped(int curve, const void* in, void* out, size_t n, hipStream_t s);
+int ntt_device_dispatch(DeviceState* st, int field, const void* d_in, void* d_out, void* d_tmp, unsigned logn,
+                        size_t batch, int inverse, hipStream_t s);
+
+}  // namespace halo
