@@ -1,0 +1,262 @@
+#!/usr/bin/env python3
+"""Benchmark of the halo proving hot path on MI355X (BASELINE.json metric: MSM points/s + NTT elems/s).
+
+Workload at N=1 (BASELINE.json configs[1]): a 2^20-point Pippenger MSM over Pallas against the
+device-resident SRS, bit-exact with the reference semantics (crates/accumulation/src/pedersen.rs:21,
+pcdl::commit pcdl.rs:275).  One "step" = one MSM over a fresh batch of 2^20 scalars resident in HBM.
+Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): the MSM's points are partitioned
+across ranks (rank r owns SRS block r, SURVEY §8e point-partition); each rank computes its partial
+sum, the partial points (64 B each) are all-gathered over RCCL and summed on the device
+(halo_point_sum) -- weak scaling, value = total points of all ranks / max-over-ranks time.
+
+Also measured (reported under "extra"): the 2^22 NTT + iNTT pair (BASELINE.json configs[2]).
+
+The roofline object prices the dominant kernel (MSM bucket accumulation, `k_acc`): achieved =
+96 B/point (64 B affine base + 32 B scalar) x points per launch / its mean launch time
+from hipEvents recorded on its stream inside libhalo_gpu (halo_profile_*).  cpu_baseline times the
+C restatement of arkworks' msm_bigint_wnaf (oracle/oracle.c, "port") on the host cores, rank 0, N=1.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+MSM_BYTES_PER_POINT = 96
+NTT_BYTES_PER_ELEM = 64  # read + write 32 B per transform
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--logn", type=int, default=20, help="log2 MSM points per rank")
+    ap.add_argument("--ntt-logn", type=int, default=22)
+    ap.add_argument("--curve", default="pallas")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    import torch
+    import torch.distributed as dist
+
+    from halo_amd import _lib as H
+
+    H.ensure_device(local)
+    torch.cuda.set_device(local)
+    L = H.load()
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    curve = H.CURVES[args.curve]
+    n = 1 << args.logn
+
+    # ---- setup (outside the timed region): resident SRS = this rank's block of the global SRS
+    seed = 0x48414C4F + rank  # distinct bases per rank
+    H.check(L.halo_srs_synthesize(curve, n, seed))
+    H.check(L.halo_srs_precompute_windows(curve))
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(1234 + rank)
+
+    def fresh_scalars(k):
+        s = torch.randint(-(2**63), 2**63 - 1, (k, n, 4), dtype=torch.int64, device="cuda", generator=gen)
+        s[..., 3] &= 0x0FFFFFFFFFFFFFFF  # < 2^252 < r: valid canonical Montgomery representatives
+        return s
+
+    nbatch = max(1, min(args.steps, 8))
+    scalars = fresh_scalars(nbatch)
+    stream = torch.cuda.current_stream().cuda_stream
+    out = np.zeros(8, dtype=np.uint64)
+    gathered = np.zeros((world, 8), dtype=np.uint64)
+
+    def step(i):
+        H.check(L.halo_msm_dev(curve, None, ctypes.c_void_p(scalars[i % nbatch].data_ptr()), n, H.ptr(out),
+                               ctypes.c_void_p(stream)))
+        if world > 1:
+            t = torch.from_numpy(out.view(np.int64).copy()).cuda()
+            parts = [torch.empty_like(t) for _ in range(world)]
+            dist.all_gather(parts, t)
+            for r, p in enumerate(parts):
+                gathered[r] = p.cpu().numpy().view(np.uint64)
+            H.check(L.halo_point_sum(curve, H.ptr(gathered), world, H.ptr(out)))
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    L.halo_profile_reset()
+    L.halo_profile_enable(1)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    L.halo_profile_enable(0)
+    elapsed = t1 - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    launches = ctypes.c_size_t(0)
+    acc_ms = ctypes.c_double(0)
+    H.check(L.halo_profile_read(b"msm_acc", ctypes.byref(launches), ctypes.byref(acc_ms)))
+    acc_avg_ms = acc_ms.value / max(1, launches.value)
+
+    # ---- NTT + iNTT pair at 2^ntt_logn (configs[2]); rank-local, reported under extra
+    N = 1 << args.ntt_logn
+    x = torch.randint(-(2**63), 2**63 - 1, (N, 4), dtype=torch.int64, device="cuda", generator=gen)
+    x[:, 3] &= 0x0FFFFFFFFFFFFFFF
+    x0 = x.clone()
+    xp = ctypes.c_void_p(x.data_ptr())
+    for _ in range(2):
+        H.check(L.halo_ntt_dev(H.FP, xp, args.ntt_logn, 1, 0, ctypes.c_void_p(stream)))
+        H.check(L.halo_ntt_dev(H.FP, xp, args.ntt_logn, 1, 1, ctypes.c_void_p(stream)))
+    torch.cuda.synchronize()
+    ntt_ok = bool(torch.equal(x, x0))
+    L.halo_profile_reset()
+    L.halo_profile_enable(1)
+    nrep = 10
+    torch.cuda.synchronize()
+    a0 = time.perf_counter()
+    for _ in range(nrep):
+        H.check(L.halo_ntt_dev(H.FP, xp, args.ntt_logn, 1, 0, ctypes.c_void_p(stream)))
+        H.check(L.halo_ntt_dev(H.FP, xp, args.ntt_logn, 1, 1, ctypes.c_void_p(stream)))
+    torch.cuda.synchronize()
+    a1 = time.perf_counter()
+    L.halo_profile_enable(0)
+    nl = ctypes.c_size_t(0)
+    nms = ctypes.c_double(0)
+    H.check(L.halo_profile_read(b"ntt_pass", ctypes.byref(nl), ctypes.byref(nms)))
+    ntt_ok = ntt_ok and bool(torch.equal(x, x0))
+    ntt_pair_ms = (a1 - a0) * 1e3 / nrep
+
+    if rank != 0:
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    total_points = n * world * args.steps
+    value = total_points / elapsed
+    ms_per_step = elapsed * 1e3 / args.steps
+    acc_bytes = MSM_BYTES_PER_POINT * n
+    achieved = acc_bytes / (acc_avg_ms * 1e-3) / 1e9 if acc_avg_ms > 0 else 0.0
+
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    if os.path.exists(pmc_path):
+        try:
+            pmc = json.load(open(pmc_path))
+            traffic = pmc.get("msm_acc", {}).get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+
+    cpu = None
+    if not args.no_cpu and world == 1:
+        cpu = cpu_baseline(L, H, curve, n, scalars[0], out_check=True, budget_s=args.cpu_seconds)
+
+    line = {
+        "metric": "MSM points/sec (Pippenger, Pallas, 2^20 points, resident SRS)",
+        "value": value,
+        "unit": "points/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32 limbs (255-bit Montgomery field, integer)",
+        "data": "synthetic: uniform random scalars; SRS bases G_j = k_j*(-1,2) with seeded k_j (known discrete logs)",
+        "config": {
+            "workload": f"msm_2^{args.logn}_pallas_resident_srs (BASELINE.json configs[1]; point-partitioned across ranks)",
+            "points_per_rank": n,
+            "window_bits": L.halo_msm_window_bits(n),
+            "parallelism": f"point-partition x{world}, RCCL all-gather of partial sums",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "k_acc (MSM bucket accumulation)",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "algorithmic_bytes_per_launch": acc_bytes,
+            "avg_launch_ms": acc_avg_ms,
+            "note": "the MSM is bound by 255-bit modular multiplication on the VALU, not HBM (SURVEY §7 hard part 1)",
+        },
+        "cpu_baseline": cpu,
+        "extra": {
+            "ntt": {
+                "workload": f"ntt+intt_2^{args.ntt_logn}_fp (BASELINE.json configs[2])",
+                "pair_ms": ntt_pair_ms,
+                "elems_per_s_pair": N / (ntt_pair_ms * 1e-3),
+                "roundtrip_bit_exact": ntt_ok,
+                "pass_kernel_avg_ms": nms.value / max(1, nl.value),
+                "roofline_frac_pair": (2 * NTT_BYTES_PER_ELEM * N) / (ntt_pair_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            }
+        },
+    }
+    print(json.dumps(line))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline(L, H, curve, n, scalars_dev, out_check, budget_s):
+    """Rank 0, N=1 only: the C port of arkworks msm_bigint_wnaf (oracle/oracle.c) on host cores."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import corc  # noqa: E402  (oracle: only the cpu_baseline leg may load it)
+
+    bases = np.zeros((n, 8), dtype=np.uint64)
+    H.check(L.halo_srs_read(curve, 0, n, H.ptr(bases)))
+    sc = np.ascontiguousarray(scalars_dev.cpu().numpy().view(np.uint64))
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    threads = min(threads, 16)
+    gpu_out = np.zeros(8, dtype=np.uint64)
+    H.check(L.halo_msm(curve, H.ptr(bases), n, H.ptr(sc), n, H.ptr(gpu_out)))
+    reps = 0
+    t0 = time.perf_counter()
+    cpu_out = None
+    while True:
+        cpu_out = corc.msm("pallas" if curve == 0 else "vesta", bases, sc, threads=threads)
+        reps += 1
+        if time.perf_counter() - t0 >= budget_s or reps >= 5:
+            break
+    dt = (time.perf_counter() - t0) / reps
+    return {
+        "value": n / dt,
+        "unit": "points/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{reps} x full 2^{n.bit_length() - 1}-point MSM (same bases/scalars as the GPU), C restatement of "
+                  f"ark-ec 0.5 msm_bigint_wnaf, c={corc.msm_window_size(n)}, OpenMP over windows",
+        "gpu_matches_cpu": bool(np.array_equal(cpu_out, gpu_out)) if out_check else None,
+    }
+
+
+if __name__ == "__main__":
+    main()

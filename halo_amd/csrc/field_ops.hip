@@ -7,7 +7,7 @@
 namespace halo {
 
 template <class F>
-__global__ void k_field_op(int op, const uint4* a, const uint4* b, uint4* out, size_t n) {
+__global__ __launch_bounds__(256) void k_field_op(int op, const uint4* a, const uint4* b, uint4* out, size_t n) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     Fe<F> x = fe_from_ark<F>(a + 2 * i);
@@ -29,7 +29,7 @@ __global__ void k_field_op(int op, const uint4* a, const uint4* b, uint4* out, s
 }
 
 template <class Cv>
-__global__ void k_curve_op(int op, const uint4* a, const uint4* b, const uint4* k, uint4* out, size_t n) {
+__global__ __launch_bounds__(64) void k_curve_op(int op, const uint4* a, const uint4* b, const uint4* k, uint4* out, size_t n) {
     using F = typename Cv::Base;
     using S = typename Cv::Scalar;
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;

@@ -279,26 +279,18 @@ HALO_DEV Fe<C> fe_select(bool c, const Fe<C>& a, const Fe<C>& b) {
     return r;
 }
 
-// a^e for a 256-bit exponent given as 4 x u64 (little endian), left-to-right 4-bit fixed window.
+// a^e for a 256-bit exponent given as 4 x u64 (little endian), left-to-right 2-bit fixed window
+// (small table: keeps register pressure low in latency-bound single-thread kernels).
 template <class C>
 HALO_DEV Fe<C> fe_pow(const Fe<C>& a, const uint64_t (&e)[4]) {
-    Fe<C> tbl[16];
-    tbl[0] = fe_one<C>();
-    tbl[1] = a;
-#pragma unroll
-    for (int i = 2; i < 16; i++) tbl[i] = fe_mul(tbl[i - 1], a);
+    const Fe<C> a2 = fe_sqr(a);
+    const Fe<C> a3 = fe_mul(a2, a);
     Fe<C> r = fe_one<C>();
-    for (int nib = 63; nib >= 0; nib--) {
+    for (int i = 127; i >= 0; i--) {
         r = fe_sqr(r);
         r = fe_sqr(r);
-        r = fe_sqr(r);
-        r = fe_sqr(r);
-        const uint32_t d = (uint32_t)(e[nib >> 4] >> ((nib & 15) * 4)) & 15u;
-        // constant-index table access (avoid scratch): select
-        Fe<C> t = tbl[0];
-#pragma unroll
-        for (int k = 1; k < 16; k++) t = fe_select(d == (uint32_t)k, tbl[k], t);
-        r = fe_mul(r, t);
+        const uint32_t d = (uint32_t)(e[i >> 5] >> ((i & 31) * 2)) & 3u;
+        if (d) r = fe_mul(r, d == 1 ? a : (d == 2 ? a2 : a3));
     }
     return r;
 }

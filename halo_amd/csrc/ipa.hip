@@ -1,0 +1,571 @@
+// IPA inner-product folding, polynomial evaluation, dot products, powers, FFT multiplication
+// (SURVEY §8 rows a7, a8, a9).
+//
+//  * IPA session: the round loop of pcdl::open_without_eval (crates/accumulation/src/pcdl.rs:404-438)
+//    with G, c, z device-resident across rounds.  Per round the host (which owns the Poseidon
+//    transcript, pcdl.rs:421-425) asks for L, R and then supplies xi.
+//      L = <c_r, G_l> + H' <c_r, z_l>,  R = <c_l, G_r> + H' <c_l, z_r>     (pcdl.rs:412-418)
+//      G_l[j] = (G_l[j] + xi G_r[j]).into_affine(); c_l[j] += xi^-1 c_r[j]; z_l[j] += xi z_r[j]
+//                                                                       (pcdl.rs:427-435)
+//    The G fold multiplies every lane by the SAME scalar xi, so all lanes follow one control path
+//    (the NAF of xi, computed once per workgroup into LDS and read wave-uniformly); the dot products
+//    are device reductions whose results feed the MSM's hiding-term slot (k_final) directly, so a
+//    round never round-trips scalars through the host.
+//  * DensePolynomial::evaluate (Horner, pcdl.rs:49,471): chunked Horner + z^offset + tree sum.
+//  * group::scalar_dot / construct_powers (crates/group/src/group.rs:43-45,58-66).
+//  * &Poly * &Poly (protocol.rs:132-139, pcdl.rs:215): NTT, pointwise product, iNTT, trim.
+#include <algorithm>
+#include <vector>
+
+#include "dispatch.hpp"
+#include "msm.hpp"
+#include "runtime.hpp"
+
+namespace halo {
+
+// ---------------------------------------------------------------------------------------------
+// reductions / elementwise
+// ---------------------------------------------------------------------------------------------
+constexpr int RED_THREADS = 256;
+
+// partial[blockIdx] = sum_{i in block range} x[i] * y[i].  x is read raw (ark value X = x 2^256) and
+// y converted to internal (y R'), so fe_mul(X, Y) = x y 2^256: every partial is the product already
+// in ark form and the final sum only needs canonicalising.
+template <class F>
+__global__ __launch_bounds__(RED_THREADS) void k_dot_partial(const uint4* x, const uint4* y, size_t n, size_t per_block,
+                                                             uint4* partial) {
+    __shared__ uint4 red[RED_THREADS * 2];
+    const size_t beg = (size_t)blockIdx.x * per_block, end = min(n, beg + per_block);
+    Fe<F> acc = fe_zero<F>();
+    for (size_t i = beg + threadIdx.x; i < end; i += RED_THREADS)
+        acc = fe_add(acc, fe_mul(fe_load<F>(x + 2 * i), fe_from_ark<F>(y + 2 * i)));
+    fe_store(red + 2 * threadIdx.x, acc);
+    __syncthreads();
+    for (int off = RED_THREADS / 2; off > 0; off >>= 1) {
+        if ((int)threadIdx.x < off)
+            fe_store(red + 2 * threadIdx.x, fe_add(fe_load<F>(red + 2 * threadIdx.x), fe_load<F>(red + 2 * (threadIdx.x + off))));
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) fe_store(partial + 2 * blockIdx.x, fe_load<F>(red));
+}
+
+// out_ark = ARK(sum_b partial[b]) where partial values are "ark-valued products" (see above)
+template <class F>
+__global__ __launch_bounds__(RED_THREADS) void k_sum_partials_to_ark(const uint4* partial, size_t nb, uint4* out_ark) {
+    __shared__ uint4 red[RED_THREADS * 2];
+    Fe<F> acc = fe_zero<F>();
+    for (size_t i = threadIdx.x; i < nb; i += RED_THREADS) acc = fe_add(acc, fe_load<F>(partial + 2 * i));
+    fe_store(red + 2 * threadIdx.x, acc);
+    __syncthreads();
+    for (int off = RED_THREADS / 2; off > 0; off >>= 1) {
+        if ((int)threadIdx.x < off)
+            fe_store(red + 2 * threadIdx.x, fe_add(fe_load<F>(red + 2 * threadIdx.x), fe_load<F>(red + 2 * (threadIdx.x + off))));
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        // acc holds sum of ark-form values (x y 2^256 mod p, weakly reduced): canonicalize
+        fe_store(out_ark, fe_canon(fe_reduce_2p(fe_load<F>(red))));
+    }
+}
+
+// out[i] = z^i, i < n (ark in / out); each thread produces a run of `run` consecutive powers
+template <class F>
+__global__ void k_powers(const uint4* z_ark, size_t n, size_t run, uint4* out) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t beg = t * run;
+    if (beg >= n) return;
+    const Fe<F> z = fe_from_ark<F>(z_ark);
+    Fe<F> p = fe_one<F>(), b = z;
+    for (size_t e = beg; e; e >>= 1) {
+        if (e & 1) p = fe_mul(p, b);
+        b = fe_sqr(b);
+    }
+    const size_t end = min(n, beg + run);
+    for (size_t i = beg; i < end; i++) {
+        fe_to_ark(out + 2 * i, p);
+        p = fe_mul(p, z);
+    }
+}
+
+// Chunked Horner: partial[(poly, chunk)] = z^start * sum_{i in chunk} c_i z^(i - start)  (internal)
+template <class F>
+__global__ __launch_bounds__(RED_THREADS) void k_eval_chunks(const uint4* const* polys, const size_t* lens,
+                                                             const uint4* z_ark, size_t chunk, int nchunks,
+                                                             uint4* partial) {
+    __shared__ uint4 red[RED_THREADS * 2];
+    const int pi = blockIdx.y;
+    const size_t len = lens[pi];
+    const uint4* c = polys[pi];
+    const Fe<F> z = fe_from_ark<F>(z_ark);
+    const size_t per_block = chunk * RED_THREADS;
+    const size_t tbeg = (size_t)blockIdx.x * per_block + (size_t)threadIdx.x * chunk;
+    Fe<F> acc = fe_zero<F>();
+    if (tbeg < len) {
+        const size_t tend = min(len, tbeg + chunk);
+        for (size_t i = tend; i-- > tbeg;) acc = fe_add(fe_mul(acc, z), fe_from_ark<F>(c + 2 * i));
+        Fe<F> p = fe_one<F>(), b = z;
+        for (size_t e = tbeg; e; e >>= 1) {
+            if (e & 1) p = fe_mul(p, b);
+            b = fe_sqr(b);
+        }
+        acc = fe_mul(acc, p);
+    }
+    fe_store(red + 2 * threadIdx.x, acc);
+    __syncthreads();
+    for (int off = RED_THREADS / 2; off > 0; off >>= 1) {
+        if ((int)threadIdx.x < off)
+            fe_store(red + 2 * threadIdx.x, fe_add(fe_load<F>(red + 2 * threadIdx.x), fe_load<F>(red + 2 * (threadIdx.x + off))));
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) fe_store(partial + 2 * ((size_t)pi * nchunks + blockIdx.x), fe_load<F>(red));
+}
+
+template <class F>
+__global__ __launch_bounds__(RED_THREADS) void k_sum_internal_to_ark(const uint4* partial, int per, uint4* out_ark) {
+    __shared__ uint4 red[RED_THREADS * 2];
+    const int pi = blockIdx.x;
+    Fe<F> acc = fe_zero<F>();
+    for (int i = threadIdx.x; i < per; i += RED_THREADS) acc = fe_add(acc, fe_load<F>(partial + 2 * ((size_t)pi * per + i)));
+    fe_store(red + 2 * threadIdx.x, acc);
+    __syncthreads();
+    for (int off = RED_THREADS / 2; off > 0; off >>= 1) {
+        if ((int)threadIdx.x < off)
+            fe_store(red + 2 * threadIdx.x, fe_add(fe_load<F>(red + 2 * threadIdx.x), fe_load<F>(red + 2 * (threadIdx.x + off))));
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) fe_to_ark(out_ark + 2 * pi, fe_load<F>(red));
+}
+
+// pointwise a[i] *= b[i] (ark in / out)
+template <class F>
+__global__ void k_pointwise_mul(uint4* a, const uint4* b, size_t n) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    fe_to_ark(a + 2 * i, fe_mul(fe_from_ark<F>(a + 2 * i), fe_from_ark<F>(b + 2 * i)));
+}
+
+// ---------------------------------------------------------------------------------------------
+// IPA fold
+// ---------------------------------------------------------------------------------------------
+// gs: internal affine (2m points), cs/zs: ark scalars (2m).  xi / xi_inv: ark.
+template <class Cv>
+__global__ __launch_bounds__(128) void k_ipa_fold(uint4* gs, uint4* cs, uint4* zs, size_t m, const uint4* xi_ark,
+                                                  const uint4* xi_inv_ark) {
+    using F = typename Cv::Base;
+    using S = typename Cv::Scalar;
+    __shared__ int8_t naf[260];
+    __shared__ int naf_top_s;
+    if (threadIdx.x == 0) {
+        // non-adjacent form of the canonical xi
+        uint32_t k[9];
+        uint32_t w8[8];
+        fe_ark_to_canonical_words<S>(xi_ark, w8);
+        for (int i = 0; i < 8; i++) k[i] = w8[i];
+        k[8] = 0;
+        int top = -1;
+        for (int i = 0; i < 258; i++) {
+            int d = 0;
+            if (k[0] & 1u) {
+                d = 2 - (int)(k[0] & 3u);  // +1 or -1
+                // k -= d
+                if (d == 1) {
+                    k[0] -= 1;
+                } else {
+                    uint32_t c = 1;
+                    for (int q = 0; q < 9 && c; q++) {
+                        k[q] += 1;
+                        c = (k[q] == 0);
+                    }
+                }
+            }
+            naf[i] = (int8_t)d;
+            if (d) top = i;
+            for (int q = 0; q < 8; q++) k[q] = (k[q] >> 1) | (k[q + 1] << 31);
+            k[8] >>= 1;
+        }
+        naf_top_s = top;
+    }
+    __syncthreads();
+    const int naf_top = naf_top_s;
+    const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= m) return;
+    // scalars
+    const Fe<S> xi = fe_from_ark<S>(xi_ark);
+    const Fe<S> xinv = fe_from_ark<S>(xi_inv_ark);
+    fe_to_ark(cs + 2 * j, fe_add(fe_from_ark<S>(cs + 2 * j), fe_mul(fe_from_ark<S>(cs + 2 * (j + m)), xinv)));
+    fe_to_ark(zs + 2 * j, fe_add(fe_from_ark<S>(zs + 2 * j), fe_mul(fe_from_ark<S>(zs + 2 * (j + m)), xi)));
+    // G_l[j] + xi * G_r[j]: every lane shares xi, so the NAF digit schedule (in LDS, computed once
+    // per workgroup) is wave-uniform: 255 doublings + ~85 mixed additions, no divergence.
+    const Affine<F> gr = aff_load<F>(gs + 4 * (j + m));
+    const Affine<F> grn = aff_neg(gr);
+    XYZZ<F> acc = xyzz_id<F>();
+    for (int i = naf_top; i >= 0; i--) {
+        acc = xyzz_dbl(acc);
+        const int d = __builtin_amdgcn_readfirstlane((int)naf[i]);
+        if (d > 0) acc = xyzz_madd(acc, gr);
+        else if (d < 0) acc = xyzz_madd(acc, grn);
+    }
+    acc = xyzz_madd(acc, aff_load<F>(gs + 4 * j));
+    aff_store(gs + 4 * j, xyzz_to_aff(acc));
+}
+
+template <class Cv>
+__global__ __launch_bounds__(64) void k_pow2_table_from_wrapped(const uint4* P_wrapped, uint4* out_aff, int count) {
+    using F = typename Cv::Base;
+    if (threadIdx.x != 0) return;
+    XYZZ<F> p = xyzz_from_aff(aff_from_wrapped<F>(P_wrapped));
+    for (int i = 0; i < count; i++) {
+        aff_store(out_aff + 4 * i, xyzz_to_aff(p));
+        p = xyzz_dbl(p);
+    }
+}
+
+template <class Cv>
+__global__ void k_copy_first_wrapped(const uint4* gs_int, const uint4* cs, uint4* out_U, uint4* out_c) {
+    using F = typename Cv::Base;
+    if (threadIdx.x != 0) return;
+    aff_to_wrapped(out_U, aff_load<F>(gs_int));
+    out_c[0] = cs[0];
+    out_c[1] = cs[1];
+}
+
+// ---------------------------------------------------------------------------------------------
+// host helpers
+// ---------------------------------------------------------------------------------------------
+static unsigned gridn(size_t n, unsigned t) { return (unsigned)std::max<size_t>(1, (n + t - 1) / t); }
+
+// dot product of two device ark vectors -> device ark scalar (out_ark), using tmp (>= 2048*32 B)
+static int dot_device(int field, const void* x, const void* y, size_t n, void* out_ark, void* tmp, hipStream_t s) {
+    const size_t per_block = std::max<size_t>(RED_THREADS * 8, (n + 1023) / 1024);
+    const size_t nb = std::max<size_t>(1, (n + per_block - 1) / per_block);
+    DISPATCH_FIELD(field, F, {
+        hipLaunchKernelGGL(k_dot_partial<F>, dim3((unsigned)nb), dim3(RED_THREADS), 0, s, (const uint4*)x,
+                           (const uint4*)y, n, per_block, (uint4*)tmp);
+        hipLaunchKernelGGL(k_sum_partials_to_ark<F>, dim3(1), dim3(RED_THREADS), 0, s, (const uint4*)tmp, nb,
+                           (uint4*)out_ark);
+    });
+    HALO_HIP(hipGetLastError());
+    return HALO_OK;
+}
+
+}  // namespace halo
+
+using namespace halo;
+
+struct halo_ipa_session {
+    int curve;
+    size_t n, m;
+    DevBuf gs, cs, zs, htab, small, tmp;
+    hipStream_t s;
+};
+
+static int check_field_i(halo_field_t f) {
+    if (f != HALO_FP && f != HALO_FQ) return set_error(HALO_EINVAL, "unknown field id %d", (int)f);
+    return HALO_OK;
+}
+
+extern "C" int halo_scalar_dot(halo_field_t field, const halo_fe_t* xs, const halo_fe_t* ys, size_t n, halo_fe_t* out) {
+    clear_error();
+    HALO_CHECK(check_field_i(field));
+    if (!out || (n && (!xs || !ys))) return set_error(HALO_EINVAL, "halo_scalar_dot: null buffer");
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    hipStream_t s = 0;
+    HALO_CHECK(st->scratch[0].reserve(std::max<size_t>(n, 1) * 32));
+    HALO_CHECK(st->scratch[1].reserve(std::max<size_t>(n, 1) * 32));
+    HALO_CHECK(st->scratch[2].reserve(2048 * 32 + 64));
+    HALO_CHECK(copy_h2d(st->scratch[0].ptr, xs, n * 32, s));
+    HALO_CHECK(copy_h2d(st->scratch[1].ptr, ys, n * 32, s));
+    char* t = (char*)st->scratch[2].ptr;
+    HALO_CHECK(dot_device(field, st->scratch[0].ptr, st->scratch[1].ptr, n, t + 2048 * 32, t, s));
+    return copy_d2h(out, t + 2048 * 32, 32, s);
+}
+
+extern "C" int halo_construct_powers(halo_field_t field, const halo_fe_t* z, size_t n, halo_fe_t* out) {
+    clear_error();
+    HALO_CHECK(check_field_i(field));
+    if (!z || (n && !out)) return set_error(HALO_EINVAL, "halo_construct_powers: null buffer");
+    if (!n) return HALO_OK;
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    hipStream_t s = 0;
+    HALO_CHECK(st->scratch[0].reserve(n * 32 + 32));
+    char* b = (char*)st->scratch[0].ptr;
+    HALO_CHECK(copy_h2d(b, z, 32, s));
+    const size_t run = 16;
+    DISPATCH_FIELD(field, F, {
+        hipLaunchKernelGGL(k_powers<F>, dim3(gridn((n + run - 1) / run, 128)), dim3(128), 0, s, (const uint4*)b, n, run,
+                           (uint4*)(b + 32));
+    });
+    HALO_HIP(hipGetLastError());
+    return copy_d2h(out, b + 32, n * 32, s);
+}
+
+extern "C" int halo_poly_eval_batch(halo_field_t field, const halo_fe_t* const* polys, const size_t* lens, size_t k,
+                                    const halo_fe_t* z, halo_fe_t* out) {
+    clear_error();
+    HALO_CHECK(check_field_i(field));
+    if (!z || (k && (!polys || !lens || !out))) return set_error(HALO_EINVAL, "halo_poly_eval_batch: null buffer");
+    if (!k) return HALO_OK;
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    hipStream_t s = 0;
+    size_t total = 0, maxlen = 0;
+    for (size_t i = 0; i < k; i++) {
+        if (lens[i] && !polys[i]) return set_error(HALO_EINVAL, "halo_poly_eval_batch: null polynomial %zu", i);
+        total += lens[i];
+        maxlen = std::max(maxlen, lens[i]);
+    }
+    const size_t chunk = 32;
+    const int nchunks = (int)std::max<size_t>(1, (maxlen + chunk * RED_THREADS - 1) / (chunk * RED_THREADS));
+    HALO_CHECK(st->scratch[0].reserve(std::max<size_t>(total, 1) * 32));
+    HALO_CHECK(st->scratch[1].reserve(k * (sizeof(void*) + sizeof(size_t)) + 64));
+    HALO_CHECK(st->scratch[2].reserve((size_t)k * nchunks * 32 + k * 32));
+    std::vector<const void*> dptr(k);
+    size_t off = 0;
+    char* base = (char*)st->scratch[0].ptr;
+    for (size_t i = 0; i < k; i++) {
+        dptr[i] = base + off * 32;
+        HALO_CHECK(copy_h2d(base + off * 32, polys[i], lens[i] * 32, s));
+        off += lens[i];
+    }
+    char* meta = (char*)st->scratch[1].ptr;
+    HALO_CHECK(copy_h2d(meta, dptr.data(), k * sizeof(void*), s));
+    HALO_CHECK(copy_h2d(meta + k * sizeof(void*), lens, k * sizeof(size_t), s));
+    HALO_CHECK(copy_h2d(meta + k * (sizeof(void*) + sizeof(size_t)), z, 32, s));
+    char* part = (char*)st->scratch[2].ptr;
+    DISPATCH_FIELD(field, F, {
+        hipLaunchKernelGGL(k_eval_chunks<F>, dim3(nchunks, (unsigned)k), dim3(RED_THREADS), 0, s,
+                           (const uint4* const*)meta, (const size_t*)(meta + k * sizeof(void*)),
+                           (const uint4*)(meta + k * (sizeof(void*) + sizeof(size_t))), chunk, nchunks, (uint4*)part);
+        hipLaunchKernelGGL(k_sum_internal_to_ark<F>, dim3((unsigned)k), dim3(RED_THREADS), 0, s, (const uint4*)part,
+                           nchunks, (uint4*)(part + (size_t)k * nchunks * 32));
+    });
+    HALO_HIP(hipGetLastError());
+    return copy_d2h(out, part + (size_t)k * nchunks * 32, k * 32, s);
+}
+
+extern "C" int halo_poly_mul(halo_field_t field, const halo_fe_t* a, size_t la, const halo_fe_t* b, size_t lb,
+                             halo_fe_t* out, size_t* out_len) {
+    clear_error();
+    HALO_CHECK(check_field_i(field));
+    if ((la && !a) || (lb && !b) || !out_len) return set_error(HALO_EINVAL, "halo_poly_mul: null buffer");
+    if (la == 0 || lb == 0) {
+        *out_len = 0;  // the zero polynomial
+        return HALO_OK;
+    }
+    if (!out) return set_error(HALO_EINVAL, "halo_poly_mul: null out");
+    const size_t rl = la + lb - 1;
+    unsigned logn = 0;
+    while (((size_t)1 << logn) < rl) logn++;
+    if (logn > 28) return set_error(HALO_EINVAL, "halo_poly_mul: product too large");
+    const size_t N = (size_t)1 << logn;
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    hipStream_t s = 0;
+    for (int i = 0; i < 5; i++) HALO_CHECK(st->scratch[i].reserve(N * 32));
+    char* A = (char*)st->scratch[0].ptr;
+    char* Bv = (char*)st->scratch[1].ptr;
+    char* FA = (char*)st->scratch[2].ptr;
+    char* FB = (char*)st->scratch[3].ptr;
+    char* T = (char*)st->scratch[4].ptr;
+    HALO_HIP(hipMemsetAsync(A, 0, N * 32, s));
+    HALO_HIP(hipMemsetAsync(Bv, 0, N * 32, s));
+    HALO_CHECK(copy_h2d(A, a, la * 32, s));
+    HALO_CHECK(copy_h2d(Bv, b, lb * 32, s));
+    HALO_CHECK(ntt_device_dispatch(st, field, A, FA, T, logn, 1, 0, s));
+    HALO_CHECK(ntt_device_dispatch(st, field, Bv, FB, T, logn, 1, 0, s));
+    DISPATCH_FIELD(field, F, {
+        hipLaunchKernelGGL(k_pointwise_mul<F>, dim3(gridn(N, 256)), dim3(256), 0, s, (uint4*)FA, (const uint4*)FB, N);
+    });
+    HALO_HIP(hipGetLastError());
+    HALO_CHECK(ntt_device_dispatch(st, field, FA, A, T, logn, 1, 1, s));
+    std::vector<halo_fe_t> tmp(rl);
+    HALO_CHECK(copy_d2h(tmp.data(), A, rl * 32, s));
+    size_t n = rl;
+    while (n > 0 && !(tmp[n - 1].l[0] | tmp[n - 1].l[1] | tmp[n - 1].l[2] | tmp[n - 1].l[3])) n--;
+    std::copy(tmp.begin(), tmp.begin() + n, out);
+    *out_len = n;
+    return HALO_OK;
+}
+
+// ------------------------------------------------------------------------------------------ IPA
+extern "C" int halo_ipa_begin(halo_curve_t curve, const halo_fe_t* cs, size_t n, const halo_fe_t* z,
+                              const halo_wrapped_point_t* H_prime, halo_ipa_session** out) {
+    clear_error();
+    if (curve != HALO_PALLAS && curve != HALO_VESTA) return set_error(HALO_EINVAL, "unknown curve");
+    if (!cs || !z || !H_prime || !out) return set_error(HALO_EINVAL, "halo_ipa_begin: null argument");
+    if (n <= 1) return set_error(HALO_EINVAL, "assertion failed: n > 1");
+    if (!is_pow2(n)) return set_error(HALO_ENOTPOW2, "n (%zu) is not a power of two", n);
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    SrsState& srs = st->srs[curve];
+    if (n > srs.n) return set_error(HALO_ESRSRANGE, "d (%zu) <= D (%zu)", n - 1, srs.n ? srs.n - 1 : 0);
+    auto* ses = new halo_ipa_session();
+    ses->curve = curve;
+    ses->n = n;
+    ses->m = n / 2;
+    ses->s = 0;
+    hipStream_t s = ses->s;
+    int rc = HALO_OK;
+    do {
+        if ((rc = ses->gs.reserve(n * 64))) break;
+        if ((rc = ses->cs.reserve(n * 32))) break;
+        if ((rc = ses->zs.reserve(n * 32))) break;
+        if ((rc = ses->htab.reserve(256 * 64))) break;
+        if ((rc = ses->small.reserve(512))) break;
+        if ((rc = ses->tmp.reserve(4096 * 32))) break;
+        if (hipMemcpyAsync(ses->gs.ptr, srs.gs.ptr, n * 64, hipMemcpyDeviceToDevice, s) != hipSuccess) {
+            rc = set_error(HALO_EDEVICE, "copy of the SRS prefix failed");
+            break;
+        }
+        if ((rc = copy_h2d(ses->cs.ptr, cs, n * 32, s))) break;
+        char* sm = (char*)ses->small.ptr;
+        if ((rc = copy_h2d(sm, z, 32, s))) break;
+        if ((rc = copy_h2d(sm + 64, H_prime, 64, s))) break;
+        const size_t run = 16;
+        DISPATCH_CURVE(curve, Cv, {
+            hipLaunchKernelGGL(k_powers<typename Cv::Scalar>, dim3(gridn((n + run - 1) / run, 128)), dim3(128), 0, s,
+                               (const uint4*)sm, n, run, ses->zs.as<uint4>());
+            hipLaunchKernelGGL(k_pow2_table_from_wrapped<Cv>, dim3(1), dim3(64), 0, s, (const uint4*)(sm + 64),
+                               ses->htab.as<uint4>(), 256);
+        });
+        if (hipGetLastError() != hipSuccess) rc = set_error(HALO_EDEVICE, "ipa begin launch failed");
+    } while (0);
+    if (rc) {
+        delete ses;
+        return rc;
+    }
+    *out = ses;
+    return HALO_OK;
+}
+
+extern "C" int halo_ipa_round_lr(halo_ipa_session* ses, halo_wrapped_point_t* L, halo_wrapped_point_t* R) {
+    clear_error();
+    if (!ses || !L || !R) return set_error(HALO_EINVAL, "halo_ipa_round_lr: null argument");
+    if (ses->m == 0) return set_error(HALO_EINVAL, "halo_ipa_round_lr: no rounds left");
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    hipStream_t s = ses->s;
+    const size_t m = ses->m;
+    const int sf = ses->curve == HALO_PALLAS ? HALO_FP : HALO_FQ;
+    char* sm = (char*)ses->small.ptr;  // [0,32) z, [64,128) H', [128,160) dot_l, [160,192) dot_r, [256,320) L, [320,384) R
+    const char* cs = ses->cs.as<const char>();
+    const char* zs = ses->zs.as<const char>();
+    const char* gs = ses->gs.as<const char>();
+    HALO_CHECK(dot_device(sf, cs + m * 32, zs, m, sm + 128, ses->tmp.ptr, s));        // <c_r, z_l>
+    HALO_CHECK(dot_device(sf, cs, zs + m * 32, m, sm + 160, ses->tmp.ptr, s));        // <c_l, z_r>
+    HALO_CHECK(msm_device(st, ses->curve, gs, cs + m * 32, m, ses->htab.ptr, sm + 128, sm + 256, s));   // L
+    HALO_CHECK(msm_device(st, ses->curve, gs + m * 64, cs, m, ses->htab.ptr, sm + 160, sm + 320, s));   // R
+    HALO_CHECK(copy_d2h(L, sm + 256, 64, s));
+    HALO_CHECK(copy_d2h(R, sm + 320, 64, s));
+    return HALO_OK;
+}
+
+extern "C" int halo_ipa_fold(halo_ipa_session* ses, const halo_fe_t* xi, const halo_fe_t* xi_inv) {
+    clear_error();
+    if (!ses || !xi || !xi_inv) return set_error(HALO_EINVAL, "halo_ipa_fold: null argument");
+    if (ses->m == 0) return set_error(HALO_EINVAL, "halo_ipa_fold: no rounds left");
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    hipStream_t s = ses->s;
+    char* sm = (char*)ses->small.ptr;
+    HALO_CHECK(copy_h2d(sm + 384, xi, 32, s));
+    HALO_CHECK(copy_h2d(sm + 416, xi_inv, 32, s));
+    const size_t m = ses->m;
+    DISPATCH_CURVE(ses->curve, Cv, {
+        ProfScope prof("ipa_fold", s);
+        HALO_LAUNCH(prof, k_ipa_fold<Cv>, dim3(gridn(m, 128)), dim3(128), 0, s, ses->gs.as<uint4>(), ses->cs.as<uint4>(),
+                    ses->zs.as<uint4>(), m, (const uint4*)(sm + 384), (const uint4*)(sm + 416));
+    });
+    HALO_HIP(hipGetLastError());
+    HALO_HIP(hipStreamSynchronize(s));
+    ses->m /= 2;
+    return HALO_OK;
+}
+
+extern "C" int halo_ipa_state(halo_ipa_session* ses, size_t* m, halo_wrapped_point_t* gs, halo_fe_t* cs, halo_fe_t* zs) {
+    clear_error();
+    if (!ses) return set_error(HALO_EINVAL, "halo_ipa_state: null session");
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    hipStream_t s = ses->s;
+    const size_t len = std::max<size_t>(2 * ses->m, 1);
+    if (m) *m = ses->m;
+    if (gs) {
+        HALO_CHECK(ses->tmp.reserve(std::max<size_t>(len * 64, 4096 * 32)));
+        HALO_CHECK(convert_internal_to_wrapped(ses->curve, ses->gs.ptr, ses->tmp.ptr, len, s));
+        HALO_CHECK(copy_d2h(gs, ses->tmp.ptr, len * 64, s));
+    }
+    if (cs) HALO_CHECK(copy_d2h(cs, ses->cs.ptr, len * 32, s));
+    if (zs) HALO_CHECK(copy_d2h(zs, ses->zs.ptr, len * 32, s));
+    return HALO_OK;
+}
+
+extern "C" int halo_ipa_end(halo_ipa_session* ses, halo_wrapped_point_t* U, halo_fe_t* c) {
+    clear_error();
+    if (!ses) return set_error(HALO_EINVAL, "halo_ipa_end: null session");
+    int rc = HALO_OK;
+    if (U || c) {
+        DeviceState* st = current_state();
+        if (!st) {
+            delete ses;
+            return HALO_EDEVICE;
+        }
+        std::lock_guard<std::mutex> g(st->mu);
+        hipStream_t s = ses->s;
+        char* sm = (char*)ses->small.ptr;
+        DISPATCH_CURVE(ses->curve, Cv, {
+            hipLaunchKernelGGL(k_copy_first_wrapped<Cv>, dim3(1), dim3(64), 0, s, ses->gs.as<const uint4>(),
+                               ses->cs.as<const uint4>(), (uint4*)(sm + 256), (uint4*)(sm + 320));
+        });
+        if (hipGetLastError() != hipSuccess) rc = set_error(HALO_EDEVICE, "ipa end launch failed");
+        if (!rc && U) rc = copy_d2h(U, sm + 256, 64, s);
+        if (!rc && c) rc = copy_d2h(c, sm + 320, 32, s);
+    }
+    delete ses;
+    return rc;
+}
+
+extern "C" int halo_ipa_fold_host(halo_curve_t curve, halo_wrapped_point_t* gs, halo_fe_t* cs, halo_fe_t* zs, size_t m,
+                                  const halo_fe_t* xi, const halo_fe_t* xi_inv) {
+    clear_error();
+    if (curve != HALO_PALLAS && curve != HALO_VESTA) return set_error(HALO_EINVAL, "unknown curve");
+    if (!xi || !xi_inv || (m && (!gs || !cs || !zs))) return set_error(HALO_EINVAL, "halo_ipa_fold_host: null argument");
+    if (!m) return HALO_OK;
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    hipStream_t s = 0;
+    HALO_CHECK(st->scratch[0].reserve(2 * m * 64));
+    HALO_CHECK(st->scratch[1].reserve(2 * m * 64));
+    HALO_CHECK(st->scratch[2].reserve(2 * m * 32));
+    HALO_CHECK(st->scratch[3].reserve(2 * m * 32));
+    HALO_CHECK(st->scratch[4].reserve(64));
+    char* sm = (char*)st->scratch[4].ptr;
+    HALO_CHECK(copy_h2d(st->scratch[0].ptr, gs, 2 * m * 64, s));
+    HALO_CHECK(copy_h2d(st->scratch[2].ptr, cs, 2 * m * 32, s));
+    HALO_CHECK(copy_h2d(st->scratch[3].ptr, zs, 2 * m * 32, s));
+    HALO_CHECK(copy_h2d(sm, xi, 32, s));
+    HALO_CHECK(copy_h2d(sm + 32, xi_inv, 32, s));
+    HALO_CHECK(convert_wrapped_to_internal(curve, st->scratch[0].ptr, st->scratch[1].ptr, 2 * m, s));
+    DISPATCH_CURVE(curve, Cv, {
+        hipLaunchKernelGGL(k_ipa_fold<Cv>, dim3(gridn(m, 128)), dim3(128), 0, s, st->scratch[1].as<uint4>(),
+                           st->scratch[2].as<uint4>(), st->scratch[3].as<uint4>(), m, (const uint4*)sm,
+                           (const uint4*)(sm + 32));
+    });
+    HALO_HIP(hipGetLastError());
+    HALO_CHECK(convert_internal_to_wrapped(curve, st->scratch[1].ptr, st->scratch[0].ptr, m, s));
+    HALO_CHECK(copy_d2h(gs, st->scratch[0].ptr, m * 64, s));
+    HALO_CHECK(copy_d2h(cs, st->scratch[2].ptr, m * 32, s));
+    HALO_CHECK(copy_d2h(zs, st->scratch[3].ptr, m * 32, s));
+    return HALO_OK;
+}

@@ -64,7 +64,7 @@ __global__ void k_internal_to_wrapped(const uint4* in, uint4* out, size_t n) {
 }
 
 template <class Cv>
-__global__ void k_synth_bases(uint4* out, size_t n, uint64_t seed) {
+__global__ __launch_bounds__(64) void k_synth_bases(uint4* out, size_t n, uint64_t seed) {
     using F = typename Cv::Base;
     const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n) return;
@@ -280,7 +280,8 @@ __global__ void k_tasks(const uint32_t* bstart, const uint32_t* task_off, size_t
 
 template <class Cv>
 __global__ __launch_bounds__(256) void k_acc(const Task* tasks, const uint32_t* ntasks_total, const uint32_t* sorted,
-                                             const uint4* bases, uint4* partials) {
+                                             const uint4* bases, uint32_t n_per_window, size_t stride,
+                                             uint4* partials) {
     using F = typename Cv::Base;
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= *ntasks_total) return;
@@ -288,7 +289,9 @@ __global__ __launch_bounds__(256) void k_acc(const Task* tasks, const uint32_t* 
     XYZZ<F> acc = xyzz_id<F>();
     for (uint32_t e = tk.begin; e < tk.end; e++) {
         const uint32_t v = sorted[e];
-        Affine<F> p = aff_load<F>(bases + 4 * (size_t)(v & 0x7fffffffu));
+        size_t idx = v & 0x7fffffffu;
+        if (stride) idx = (idx / n_per_window) * stride + idx % n_per_window;  // window-shifted SRS
+        Affine<F> p = aff_load<F>(bases + 4 * idx);
         if (v & 0x80000000u) p.y = fe_neg(p.y);
         acc = xyzz_madd(acc, p);
     }
@@ -296,7 +299,7 @@ __global__ __launch_bounds__(256) void k_acc(const Task* tasks, const uint32_t* 
 }
 
 template <class Cv>
-__global__ void k_merge(const uint32_t* task_off, size_t nb, const uint4* partials, uint4* bucket_sums) {
+__global__ __launch_bounds__(256) void k_merge(const uint32_t* task_off, size_t nb, const uint4* partials, uint4* bucket_sums) {
     using F = typename Cv::Base;
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= nb) return;
@@ -308,11 +311,16 @@ __global__ void k_merge(const uint32_t* task_off, size_t nb, const uint4* partia
 }
 
 // ---------------------------------------------------------------------------------------------
-// 6. per-window reduction
+// 6. per-window reduction  S_w = sum_{b=1..B} b * BS[w][b], organised for low dependency depth
+//    (every stage is latency-bound: a lone XYZZ add is ~14 dependent modmuls):
+//    A. segments of L buckets: acc_j = sum_t t BS[jL+t], sum_j = sum_t BS[jL+t] (2L serial adds)
+//    B. S_w = sum_j acc_j + L * sum_j j sum_j, and sum_j j sum_j = sum_k 2^k T_k with
+//       T_k = sum_{j : bit k of j} sum_j  -> (nbits + 1) independent tree sums per window
+//    C. S_w = A + sum_k 2^(k + log L) T_k: lane k doubles T_k (k + log L times), LDS tree sum.
 // ---------------------------------------------------------------------------------------------
-// thread per (w, segment j): acc_j = sum_t t B_{jL+t}, sum_j = sum_t B_{jL+t}  (t = 1..L)
 template <class Cv>
-__global__ void k_seg(const uint4* bucket_sums, uint32_t B, uint32_t L, int W, uint4* seg_acc, uint4* seg_sum) {
+__global__ __launch_bounds__(64) void k_seg(const uint4* bucket_sums, uint32_t B, uint32_t L, int W, uint4* seg_acc,
+                                            uint4* seg_sum) {
     using F = typename Cv::Base;
     const uint32_t nseg = B / L;
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -328,76 +336,128 @@ __global__ void k_seg(const uint4* bucket_sums, uint32_t B, uint32_t L, int W, u
     xyzz_store(seg_sum + 8 * t, run);
 }
 
-// small scalar multiplication k * P (k < 2^32)
-template <class F>
-HALO_DEV XYZZ<F> xyzz_mul_small(const XYZZ<F>& P, uint32_t k) {
-    XYZZ<F> r = xyzz_id<F>();
-    if (k == 0) return r;
-    const int top = 31 - __clz(k);
-    for (int i = top; i >= 0; i--) {
-        r = xyzz_dbl(r);
-        if ((k >> i) & 1u) r = xyzz_add(r, P);
-    }
-    return r;
-}
-
-// one workgroup per window: S_w = sum_j (acc_j + (j L) sum_j)
+// grid (nbits + 1, W), 256 threads.  out[w * (nbits + 1) + k]:
+//   k <  nbits : T_k = sum_{j : bit k of j} seg_sum[w][j]
+//   k == nbits : A   = sum_j seg_acc[w][j]
 template <class Cv>
-__global__ __launch_bounds__(256) void k_wcombine(const uint4* seg_acc, const uint4* seg_sum, uint32_t B,
-                                                  uint32_t L, uint4* window_sums) {
+__global__ __launch_bounds__(256) void k_bitsums(const uint4* seg_acc, const uint4* seg_sum, uint32_t nseg,
+                                                 uint32_t nbits, uint4* out) {
     using F = typename Cv::Base;
     __shared__ uint4 red[256 * 8];
-    const uint32_t nseg = B / L;
-    const int w = blockIdx.x;
+    const uint32_t k = blockIdx.x, w = blockIdx.y;
+    const uint4* src = (k == nbits) ? seg_acc : seg_sum;
     XYZZ<F> acc = xyzz_id<F>();
-    for (uint32_t j = threadIdx.x; j < nseg; j += blockDim.x) {
-        const size_t t = (size_t)w * nseg + j;
-        XYZZ<F> x = xyzz_load<F>(seg_acc + 8 * t);
-        if (j) x = xyzz_add(x, xyzz_mul_small(xyzz_load<F>(seg_sum + 8 * t), j * L));
-        acc = xyzz_add(acc, x);
+    for (uint32_t j = threadIdx.x; j < nseg; j += 256) {
+        if (k < nbits && !((j >> k) & 1u)) continue;
+        acc = xyzz_add(acc, xyzz_load<F>(src + 8 * ((size_t)w * nseg + j)));
     }
     xyzz_store(red + 8 * threadIdx.x, acc);
     __syncthreads();
-    for (int off = blockDim.x / 2; off > 0; off >>= 1) {
+    for (int off = 128; off > 0; off >>= 1) {
         if ((int)threadIdx.x < off)
             xyzz_store(red + 8 * threadIdx.x,
                        xyzz_add(xyzz_load<F>(red + 8 * threadIdx.x), xyzz_load<F>(red + 8 * (threadIdx.x + off))));
         __syncthreads();
     }
-    if (threadIdx.x == 0) xyzz_store(window_sums + 8 * w, xyzz_load<F>(red));
+    if (threadIdx.x == 0) xyzz_store(out + 8 * ((size_t)w * (nbits + 1) + k), xyzz_load<F>(red));
+}
+
+// grid W, 64 threads: S_w = A + sum_k 2^(k + logL) T_k
+template <class Cv>
+__global__ __launch_bounds__(64) void k_bitcombine(const uint4* bits, uint32_t nbits, uint32_t logL,
+                                                   uint4* window_sums) {
+    using F = typename Cv::Base;
+    __shared__ uint4 red[64 * 8];
+    const uint32_t w = blockIdx.x, k = threadIdx.x;
+    XYZZ<F> v = xyzz_id<F>();
+    if (k <= nbits) {
+        v = xyzz_load<F>(bits + 8 * ((size_t)w * (nbits + 1) + k));
+        if (k < nbits)
+            for (uint32_t d = 0; d < k + logL; d++) v = xyzz_dbl(v);
+    }
+    xyzz_store(red + 8 * k, v);
+    __syncthreads();
+    for (int off = 32; off > 0; off >>= 1) {
+        if ((int)k < off) xyzz_store(red + 8 * k, xyzz_add(xyzz_load<F>(red + 8 * k), xyzz_load<F>(red + 8 * (k + off))));
+        __syncthreads();
+    }
+    if (k == 0) xyzz_store(window_sums + 8 * w, xyzz_load<F>(red));
 }
 
 // ---------------------------------------------------------------------------------------------
-// 7. final: Horner over windows (+ hiding term), to ark affine
+// 7. final: Horner over the windows (wave 0), hiding term w * S from the table 2^i S (waves 1-4),
+//    XYZZ -> affine -> ark WrappedPoint.
 // ---------------------------------------------------------------------------------------------
 template <class Cv>
-__global__ void k_final(const uint4* window_sums, int W, int c, const uint4* hide_point /* internal affine or null */,
-                        const uint4* hide_scalar /* ark or null */, uint4* out_wrapped) {
+__global__ __launch_bounds__(320) void k_final(const uint4* window_sums, int W, int c,
+                                               const uint4* hide_table /* 256 internal affine 2^i S, or null */,
+                                               const uint4* hide_scalar /* ark or null */, uint4* out_wrapped) {
     using F = typename Cv::Base;
     using S = typename Cv::Scalar;
-    __shared__ uint4 part[8];
-    if (threadIdx.x == 1) {
-        XYZZ<F> h = xyzz_id<F>();
-        if (hide_point && hide_scalar) {
-            uint32_t w8[8];
-            fe_ark_to_canonical_words<S>(hide_scalar, w8);
-            h = xyzz_scalar_mul(aff_load<F>(hide_point), w8);
-        }
-        xyzz_store(part, h);
-    }
-    XYZZ<F> acc = xyzz_id<F>();
-    if (threadIdx.x == 0) {
+    __shared__ uint4 red[256 * 8];
+    __shared__ uint32_t kw[8];
+    const int tid = threadIdx.x;
+    XYZZ<F> horner = xyzz_id<F>();
+    if (tid == 0) {
         for (int w = W - 1; w >= 0; w--) {
             if (w != W - 1)
-                for (int k = 0; k < c; k++) acc = xyzz_dbl(acc);
-            acc = xyzz_add(acc, xyzz_load<F>(window_sums + 8 * w));
+                for (int k = 0; k < c; k++) horner = xyzz_dbl(horner);
+            horner = xyzz_add(horner, xyzz_load<F>(window_sums + 8 * w));
         }
     }
+    if (tid == 64 && hide_table && hide_scalar) fe_ark_to_canonical_words<S>(hide_scalar, kw);
     __syncthreads();
-    if (threadIdx.x == 0) {
-        acc = xyzz_add(acc, xyzz_load<F>(part));
-        aff_to_wrapped(out_wrapped, xyzz_to_aff(acc));
+    if (tid >= 64) {
+        const int i = tid - 64;
+        XYZZ<F> v = xyzz_id<F>();
+        if (hide_table && hide_scalar && ((kw[i >> 5] >> (i & 31)) & 1u))
+            v = xyzz_from_aff(aff_load<F>(hide_table + 4 * i));
+        xyzz_store(red + 8 * i, v);
     }
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+        const int i = tid - 64;
+        if (tid >= 64 && i < off)
+            xyzz_store(red + 8 * i, xyzz_add(xyzz_load<F>(red + 8 * i), xyzz_load<F>(red + 8 * (i + off))));
+        __syncthreads();
+    }
+    if (tid == 0) aff_to_wrapped(out_wrapped, xyzz_to_aff(xyzz_add(horner, xyzz_load<F>(red))));
+}
+
+// ---------------------------------------------------------------------------------------------
+// SRS precomputation: window-shifted bases 2^(c w) G_i (w < W) and the hiding table 2^i S
+// ---------------------------------------------------------------------------------------------
+template <class Cv>
+__global__ __launch_bounds__(64) void k_shift_windows(const uint4* gs, size_t n, int c, int W, uint4* out) {
+    using F = typename Cv::Base;
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const Affine<F> g = aff_load<F>(gs + 4 * i);
+    aff_store(out + 4 * i, g);
+    XYZZ<F> p = xyzz_from_aff(g);
+    for (int w = 1; w < W; w++) {
+        for (int k = 0; k < c; k++) p = xyzz_dbl(p);
+        aff_store(out + 4 * ((size_t)w * n + i), xyzz_to_aff(p));
+    }
+}
+
+template <class Cv>
+__global__ __launch_bounds__(64) void k_pow2_points(const uint4* P_int, uint4* out_xyzz, int count) {
+    using F = typename Cv::Base;
+    if (threadIdx.x != 0) return;
+    XYZZ<F> p = xyzz_from_aff(aff_load<F>(P_int));
+    for (int i = 0; i < count; i++) {
+        xyzz_store(out_xyzz + 8 * i, p);
+        p = xyzz_dbl(p);
+    }
+}
+
+template <class Cv>
+__global__ __launch_bounds__(64) void k_xyzz_to_aff(const uint4* in, uint4* out, int count) {
+    using F = typename Cv::Base;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    aff_store(out + 4 * i, xyzz_to_aff(xyzz_load<F>(in + 8 * i)));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -406,14 +466,14 @@ __global__ void k_final(const uint4* window_sums, int W, int c, const uint4* hid
 int msm_window_bits(size_t n) {
     unsigned lg = n > 1 ? ilog2(n - 1) + 1 : 1;
     int c = (int)lg - 4;
-    return std::max(4, std::min(16, c));
+    return std::max(6, std::min(16, c));
 }
 
 static unsigned grid_for(size_t n, unsigned thr) { return (unsigned)std::max<size_t>(1, (n + thr - 1) / thr); }
 
 struct MsmScratch {
     DevBuf digits, hist, totals, bstart, sorted, ntask, task_off, tasks, partials, bucket_sums, seg_acc, seg_sum,
-        window_sums, scan_tmp, out;
+        bits, window_sums, scan_tmp, out;
 };
 static MsmScratch g_msm_scratch[64];  // per device
 
@@ -433,22 +493,27 @@ static int device_scan(const uint32_t* in, size_t n, uint32_t* out, DevBuf& tmp,
     return HALO_OK;
 }
 
+// bases_int: n internal affine points, or (shifted) W * n window-shifted points (single bucket set).
 template <class Cv>
-static int msm_device_t(DeviceState* st, const uint4* bases_int, const uint4* scalars_ark, size_t n,
-                        const uint4* hide_point, const uint4* hide_scalar, uint4* d_out_wrapped, hipStream_t s) {
+static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, size_t shift_stride,
+                        const uint4* scalars_ark, size_t n, int c_req, const uint4* hide_table, const uint4* hide_scalar, uint4* d_out_wrapped,
+                        hipStream_t s) {
     MsmScratch& M = g_msm_scratch[st->device & 63];
-    if (n == 0) {
-        HALO_HIP(hipMemsetAsync(d_out_wrapped, 0, 64, s));
-        if (!hide_point) return HALO_OK;
-    }
     const size_t nn = std::max<size_t>(n, 1);
-    const int c = msm_window_bits(nn);
+    const int c = c_req ? c_req : msm_window_bits(nn);
     const int W = (256 + c - 1) / c;
     const uint32_t B = 1u << (c - 1);
-    const size_t NB = (size_t)W * B;
-    const int chunks = (int)std::max<size_t>(1, std::min<size_t>(32, nn / 4096));
+    // sort geometry: SW windows of SN entries each (shifted: one window over all W * n digits)
+    const int SW = shifted ? 1 : W;
+    const size_t SN = shifted ? (size_t)W * nn : nn;
+    const size_t NB = (size_t)SW * B;
+    const int chunks = (int)std::max<size_t>(1, std::min<size_t>(shifted ? 256 : 32, SN / 4096));
+    const uint32_t L = std::min<uint32_t>(MSM_SEG_L, B);
+    const uint32_t logL = ilog2(L);
+    const uint32_t nseg = B / L;
+    const uint32_t nbits = nseg > 1 ? ilog2(nseg - 1) + 1 : 0;
     HALO_CHECK(M.digits.reserve((size_t)W * nn * 4));
-    HALO_CHECK(M.hist.reserve((size_t)W * chunks * B * 4));
+    HALO_CHECK(M.hist.reserve((size_t)SW * chunks * B * 4));
     HALO_CHECK(M.totals.reserve(NB * 4));
     HALO_CHECK(M.bstart.reserve((NB + 1) * 4));
     HALO_CHECK(M.sorted.reserve((size_t)W * nn * 4));
@@ -458,10 +523,9 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, const uint4* sc
     HALO_CHECK(M.tasks.reserve(max_tasks * sizeof(Task)));
     HALO_CHECK(M.partials.reserve(max_tasks * 128));
     HALO_CHECK(M.bucket_sums.reserve(NB * 128));
-    const uint32_t L = std::min<uint32_t>(MSM_SEG_L, B);
-    const size_t nseg = NB / L;
-    HALO_CHECK(M.seg_acc.reserve(nseg * 128));
-    HALO_CHECK(M.seg_sum.reserve(nseg * 128));
+    HALO_CHECK(M.seg_acc.reserve((size_t)SW * nseg * 128));
+    HALO_CHECK(M.seg_sum.reserve((size_t)SW * nseg * 128));
+    HALO_CHECK(M.bits.reserve((size_t)SW * (nbits + 1) * 128));
     HALO_CHECK(M.window_sums.reserve((size_t)W * 128));
 
     static bool attrs_set = false;
@@ -473,14 +537,14 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, const uint4* sc
     if (n > 0) {
         hipLaunchKernelGGL(k_digits<typename Cv::Scalar>, dim3(grid_for(n, 256)), dim3(256), 0, s, scalars_ark, n, c,
                            W, M.digits.as<uint32_t>());
-        hipLaunchKernelGGL(k_hist, dim3(chunks, W), dim3(HIST_THREADS), B * 4, s, M.digits.as<const uint32_t>(), n, B,
-                           chunks, M.hist.as<uint32_t>());
-        hipLaunchKernelGGL(k_colsum, dim3(grid_for(NB, 256)), dim3(256), 0, s, M.hist.as<uint32_t>(), chunks, B, W,
+        hipLaunchKernelGGL(k_hist, dim3(chunks, SW), dim3(HIST_THREADS), B * 4, s, M.digits.as<const uint32_t>(), SN,
+                           B, chunks, M.hist.as<uint32_t>());
+        hipLaunchKernelGGL(k_colsum, dim3(grid_for(NB, 256)), dim3(256), 0, s, M.hist.as<uint32_t>(), chunks, B, SW,
                            M.totals.as<uint32_t>());
         HALO_HIP(hipGetLastError());
         HALO_CHECK(device_scan(M.totals.as<const uint32_t>(), NB, M.bstart.as<uint32_t>(), M.scan_tmp, s));
-        hipLaunchKernelGGL(k_scatter, dim3(chunks, W), dim3(HIST_THREADS), B * 4, s, M.digits.as<const uint32_t>(), n,
-                           B, chunks, M.hist.as<const uint32_t>(), M.bstart.as<const uint32_t>(),
+        hipLaunchKernelGGL(k_scatter, dim3(chunks, SW), dim3(HIST_THREADS), B * 4, s, M.digits.as<const uint32_t>(),
+                           SN, B, chunks, M.hist.as<const uint32_t>(), M.bstart.as<const uint32_t>(),
                            M.sorted.as<uint32_t>());
         hipLaunchKernelGGL(k_ntask, dim3(grid_for(NB, 256)), dim3(256), 0, s, M.bstart.as<const uint32_t>(), NB,
                            M.ntask.as<uint32_t>());
@@ -488,31 +552,53 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, const uint4* sc
         HALO_CHECK(device_scan(M.ntask.as<const uint32_t>(), NB, M.task_off.as<uint32_t>(), M.scan_tmp, s));
         hipLaunchKernelGGL(k_tasks, dim3(grid_for(NB, 256)), dim3(256), 0, s, M.bstart.as<const uint32_t>(),
                            M.task_off.as<const uint32_t>(), NB, M.tasks.as<Task>());
-        hipLaunchKernelGGL(k_acc<Cv>, dim3(grid_for(max_tasks, 256)), dim3(256), 0, s, M.tasks.as<const Task>(),
+        ProfScope prof("msm_acc", s);
+        HALO_LAUNCH(prof, k_acc<Cv>, dim3(grid_for(max_tasks, 256)), dim3(256), 0, s, M.tasks.as<const Task>(),
                            M.task_off.as<const uint32_t>() + NB, M.sorted.as<const uint32_t>(), bases_int,
+                           (uint32_t)nn, (shifted && shift_stride != nn) ? shift_stride : (size_t)0,
                            M.partials.as<uint4>());
         hipLaunchKernelGGL(k_merge<Cv>, dim3(grid_for(NB, 256)), dim3(256), 0, s, M.task_off.as<const uint32_t>(), NB,
                            M.partials.as<const uint4>(), M.bucket_sums.as<uint4>());
-        hipLaunchKernelGGL(k_seg<Cv>, dim3(grid_for(nseg, 64)), dim3(64), 0, s, M.bucket_sums.as<const uint4>(), B, L,
-                           W, M.seg_acc.as<uint4>(), M.seg_sum.as<uint4>());
-        hipLaunchKernelGGL(k_wcombine<Cv>, dim3(W), dim3(256), 0, s, M.seg_acc.as<const uint4>(),
-                           M.seg_sum.as<const uint4>(), B, L, M.window_sums.as<uint4>());
+        hipLaunchKernelGGL(k_seg<Cv>, dim3(grid_for((size_t)SW * nseg, 64)), dim3(64), 0, s,
+                           M.bucket_sums.as<const uint4>(), B, L, SW, M.seg_acc.as<uint4>(), M.seg_sum.as<uint4>());
+        hipLaunchKernelGGL(k_bitsums<Cv>, dim3(nbits + 1, SW), dim3(256), 0, s, M.seg_acc.as<const uint4>(),
+                           M.seg_sum.as<const uint4>(), nseg, nbits, M.bits.as<uint4>());
+        hipLaunchKernelGGL(k_bitcombine<Cv>, dim3(SW), dim3(64), 0, s, M.bits.as<const uint4>(), nbits, logL,
+                           M.window_sums.as<uint4>());
         HALO_HIP(hipGetLastError());
     } else {
-        // identity window sums
-        HALO_HIP(hipMemsetAsync(M.window_sums.ptr, 0, (size_t)W * 128, s));
+        HALO_HIP(hipMemsetAsync(M.window_sums.ptr, 0, (size_t)SW * 128, s));
     }
-    hipLaunchKernelGGL(k_final<Cv>, dim3(1), dim3(64), 0, s, M.window_sums.as<const uint4>(), n ? W : 1, c, hide_point,
+    hipLaunchKernelGGL(k_final<Cv>, dim3(1), dim3(320), 0, s, M.window_sums.as<const uint4>(), SW, c, hide_table,
                        hide_scalar, d_out_wrapped);
     HALO_HIP(hipGetLastError());
     return HALO_OK;
 }
 
 int msm_device(DeviceState* st, int curve, const void* bases_int, const void* scalars_ark, size_t n,
-               const void* hide_point, const void* hide_scalar, void* d_out_wrapped, hipStream_t s) {
+               const void* hide_table, const void* hide_scalar, void* d_out_wrapped, hipStream_t s) {
     int rc;
     DISPATCH_CURVE(curve, Cv, {
-        rc = msm_device_t<Cv>(st, (const uint4*)bases_int, (const uint4*)scalars_ark, n, (const uint4*)hide_point,
+        rc = msm_device_t<Cv>(st, (const uint4*)bases_int, false, 0, (const uint4*)scalars_ark, n, 0,
+                              (const uint4*)hide_table, (const uint4*)hide_scalar, (uint4*)d_out_wrapped, s);
+    });
+    return rc;
+}
+
+// MSM over the resident SRS prefix Gs[0..n): uses the window-shifted copies when present.
+int msm_srs_device(DeviceState* st, int curve, const void* scalars_ark, size_t n, const void* hide_scalar,
+                   void* d_out_wrapped, hipStream_t s) {
+    SrsState& srs = st->srs[curve];
+    if (n > srs.n) return set_error(HALO_ESRSRANGE, "n (%zu) exceeds the resident SRS length (%zu)", n, srs.n);
+    const void* table = hide_scalar ? srs.s_table.ptr : nullptr;
+    if (hide_scalar && !srs.has_sh) return set_error(HALO_ESRSRANGE, "hiding commitment needs S: upload (S, H)");
+    int rc;
+    // the shifted copies hold W windows of srs.n points each; an MSM of n <= srs.n points uses the
+    // prefix of every window (point index w * srs.n + i)
+    const bool use_shifted = srs.shifted_c != 0;
+    DISPATCH_CURVE(curve, Cv, {
+        rc = msm_device_t<Cv>(st, use_shifted ? srs.shifted.as<const uint4>() : srs.gs.as<const uint4>(), use_shifted,
+                              srs.n, (const uint4*)scalars_ark, n, use_shifted ? srs.shifted_c : 0, (const uint4*)table,
                               (const uint4*)hide_scalar, (uint4*)d_out_wrapped, s);
     });
     return rc;
@@ -538,9 +624,61 @@ int convert_internal_to_wrapped(int curve, const void* in, void* out, size_t n, 
     return HALO_OK;
 }
 
+// hiding table 2^i S (i < 256), internal affine
+static int build_s_table(DeviceState* st, int curve, hipStream_t s) {
+    SrsState& srs = st->srs[curve];
+    HALO_CHECK(srs.s_table.reserve(256 * 64));
+    HALO_CHECK(st->scratch[7].reserve(256 * 128 + 64));
+    char* tmp = (char*)st->scratch[7].ptr;
+    HALO_CHECK(copy_h2d(tmp + 256 * 128, srs.S, 64, s));
+    DISPATCH_CURVE(curve, Cv, {
+        hipLaunchKernelGGL(k_pow2_points<Cv>, dim3(1), dim3(64), 0, s, (const uint4*)(tmp + 256 * 128), (uint4*)tmp,
+                           256);
+        hipLaunchKernelGGL(k_xyzz_to_aff<Cv>, dim3(4), dim3(64), 0, s, (const uint4*)tmp, srs.s_table.as<uint4>(), 256);
+    });
+    HALO_HIP(hipGetLastError());
+    return HALO_OK;
+}
+
+int srs_precompute_windows(DeviceState* st, int curve, hipStream_t s) {
+    SrsState& srs = st->srs[curve];
+    if (!srs.n) return set_error(HALO_ESRSRANGE, "no resident SRS to precompute");
+    const int c = msm_window_bits(srs.n);
+    const int W = (256 + c - 1) / c;
+    HALO_CHECK(srs.shifted.reserve((size_t)W * srs.n * 64));
+    DISPATCH_CURVE(curve, Cv, {
+        hipLaunchKernelGGL(k_shift_windows<Cv>, dim3(grid_for(srs.n, 64)), dim3(64), 0, s, srs.gs.as<const uint4>(),
+                           srs.n, c, W, srs.shifted.as<uint4>());
+    });
+    HALO_HIP(hipGetLastError());
+    HALO_HIP(hipStreamSynchronize(s));
+    srs.shifted_c = c;
+    return HALO_OK;
+}
+
 }  // namespace halo
 
 using namespace halo;
+
+namespace halo {
+template <class Cv>
+__global__ __launch_bounds__(256) void k_point_sum(const uint4* pts_wrapped, size_t k, uint4* out_wrapped) {
+    using F = typename Cv::Base;
+    __shared__ uint4 red[256 * 8];
+    XYZZ<F> acc = xyzz_id<F>();
+    for (size_t i = threadIdx.x; i < k; i += 256) acc = xyzz_madd(acc, aff_from_wrapped<F>(pts_wrapped + 4 * i));
+    xyzz_store(red + 8 * threadIdx.x, acc);
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+        if ((int)threadIdx.x < off)
+            xyzz_store(red + 8 * threadIdx.x,
+                       xyzz_add(xyzz_load<F>(red + 8 * threadIdx.x), xyzz_load<F>(red + 8 * (threadIdx.x + off))));
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) aff_to_wrapped(out_wrapped, xyzz_to_aff(xyzz_load<F>(red)));
+}
+
+}  // namespace halo
 
 static int check_curve(halo_curve_t c) {
     if (c != HALO_PALLAS && c != HALO_VESTA) return set_error(HALO_EINVAL, "unknown curve id %d", (int)c);
@@ -548,6 +686,40 @@ static int check_curve(halo_curve_t c) {
 }
 
 extern "C" int halo_msm_window_bits(size_t n) { return msm_window_bits(n); }
+
+extern "C" int halo_point_sum(halo_curve_t curve, const halo_wrapped_point_t* pts, size_t k, halo_wrapped_point_t* out) {
+    clear_error();
+    HALO_CHECK(check_curve(curve));
+    if (!out || (k && !pts)) return set_error(HALO_EINVAL, "halo_point_sum: null buffer");
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    hipStream_t s = 0;
+    HALO_CHECK(st->scratch[0].reserve(std::max<size_t>(k, 1) * 64 + 64));
+    char* buf = (char*)st->scratch[0].ptr;
+    HALO_CHECK(copy_h2d(buf + 64, pts, k * 64, s));
+    DISPATCH_CURVE(curve, Cv, {
+        hipLaunchKernelGGL(k_point_sum<Cv>, dim3(1), dim3(256), 0, s, (const uint4*)(buf + 64), k, (uint4*)buf);
+    });
+    HALO_HIP(hipGetLastError());
+    return copy_d2h(out, buf, 64, s);
+}
+
+extern "C" int halo_srs_read(halo_curve_t curve, size_t offset, size_t n, halo_wrapped_point_t* out) {
+    clear_error();
+    HALO_CHECK(check_curve(curve));
+    if (!out && n) return set_error(HALO_EINVAL, "halo_srs_read: null buffer");
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    SrsState& srs = st->srs[curve];
+    if (offset + n > srs.n) return set_error(HALO_ESRSRANGE, "range [%zu, %zu) exceeds the SRS length %zu", offset, offset + n, srs.n);
+    if (!n) return HALO_OK;
+    hipStream_t s = 0;
+    HALO_CHECK(st->scratch[0].reserve(n * 64));
+    HALO_CHECK(convert_internal_to_wrapped(curve, srs.gs.as<const char>() + offset * 64, st->scratch[0].ptr, n, s));
+    return copy_d2h(out, st->scratch[0].ptr, n * 64, s);
+}
 
 extern "C" void halo_synth_scalar(halo_curve_t curve, uint64_t seed, uint64_t j, uint64_t out_canonical[4]) {
     (void)curve;
@@ -601,6 +773,7 @@ extern "C" int halo_srs_upload(halo_curve_t curve, const halo_wrapped_point_t* g
         HALO_CHECK(copy_d2h(srs.S, st->scratch[1].ptr, 64, s));
         HALO_CHECK(copy_d2h(srs.H, (char*)st->scratch[1].ptr + 64, 64, s));
         srs.has_sh = true;
+        HALO_CHECK(build_s_table(st, curve, s));
     }
     HALO_HIP(hipStreamSynchronize(s));
     return HALO_OK;
@@ -640,7 +813,10 @@ extern "C" int halo_srs_synthesize(halo_curve_t curve, size_t n, uint64_t seed) 
 extern "C" int halo_srs_precompute_windows(halo_curve_t curve) {
     clear_error();
     HALO_CHECK(check_curve(curve));
-    return HALO_OK;  // optional optimisation; the windowed path needs no precomputation
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    return srs_precompute_windows(st, curve, 0);
 }
 
 extern "C" int halo_msm_srs(halo_curve_t curve, const halo_fe_t* scalars, size_t n, halo_wrapped_point_t* out) {
@@ -650,13 +826,11 @@ extern "C" int halo_msm_srs(halo_curve_t curve, const halo_fe_t* scalars, size_t
     DeviceState* st = current_state();
     if (!st) return HALO_EDEVICE;
     std::lock_guard<std::mutex> g(st->mu);
-    SrsState& srs = st->srs[curve];
-    if (n > srs.n) return set_error(HALO_ESRSRANGE, "n (%zu) exceeds the resident SRS length (%zu)", n, srs.n);
     hipStream_t s = 0;
     HALO_CHECK(st->scratch[2].reserve(std::max<size_t>(n, 1) * 32));
     HALO_CHECK(st->scratch[3].reserve(64));
     HALO_CHECK(copy_h2d(st->scratch[2].ptr, scalars, n * 32, s));
-    HALO_CHECK(msm_device(st, curve, srs.gs.ptr, st->scratch[2].ptr, n, nullptr, nullptr, st->scratch[3].ptr, s));
+    HALO_CHECK(msm_srs_device(st, curve, st->scratch[2].ptr, n, nullptr, st->scratch[3].ptr, s));
     return copy_d2h(out, st->scratch[3].ptr, 64, s);
 }
 
@@ -669,18 +843,14 @@ extern "C" int halo_msm_dev(halo_curve_t curve, const void* d_bases, const void*
     if (!st) return HALO_EDEVICE;
     std::lock_guard<std::mutex> g(st->mu);
     hipStream_t s = (hipStream_t)stream;
-    const void* bases = d_bases;
-    if (!bases) {
-        SrsState& srs = st->srs[curve];
-        if (n > srs.n) return set_error(HALO_ESRSRANGE, "n (%zu) exceeds the resident SRS length (%zu)", n, srs.n);
-        bases = srs.gs.ptr;
+    HALO_CHECK(st->scratch[7].reserve(64));
+    if (!d_bases) {
+        HALO_CHECK(msm_srs_device(st, curve, d_scalars, n, nullptr, st->scratch[7].ptr, s));
     } else {
         HALO_CHECK(st->scratch[6].reserve(std::max<size_t>(n, 1) * 64));
         HALO_CHECK(convert_wrapped_to_internal(curve, d_bases, st->scratch[6].ptr, n, s));
-        bases = st->scratch[6].ptr;
+        HALO_CHECK(msm_device(st, curve, st->scratch[6].ptr, d_scalars, n, nullptr, nullptr, st->scratch[7].ptr, s));
     }
-    HALO_CHECK(st->scratch[7].reserve(64));
-    HALO_CHECK(msm_device(st, curve, bases, d_scalars, n, nullptr, nullptr, st->scratch[7].ptr, s));
     return copy_d2h(out, st->scratch[7].ptr, 64, s);
 }
 
@@ -702,20 +872,14 @@ extern "C" int halo_pedersen_commit(halo_curve_t curve, const halo_fe_t* w, cons
     HALO_CHECK(st->scratch[0].reserve(std::max<size_t>(n, 1) * 64));
     HALO_CHECK(st->scratch[1].reserve(std::max<size_t>(n, 1) * 64));
     HALO_CHECK(st->scratch[2].reserve(std::max<size_t>(n, 1) * 32));
-    HALO_CHECK(st->scratch[3].reserve(64 + 64 + 32));
+    HALO_CHECK(st->scratch[3].reserve(64 + 32));
     HALO_CHECK(copy_h2d(st->scratch[0].ptr, gs, n * 64, s));
     HALO_CHECK(copy_h2d(st->scratch[2].ptr, ms, n * 32, s));
     HALO_CHECK(convert_wrapped_to_internal(curve, st->scratch[0].ptr, st->scratch[1].ptr, n, s));
     char* small = (char*)st->scratch[3].ptr;
-    const void* hp = nullptr;
-    const void* hs = nullptr;
-    if (w) {
-        HALO_CHECK(copy_h2d(small + 64, srs.S, 64, s));
-        HALO_CHECK(copy_h2d(small + 128, w, 32, s));
-        hp = small + 64;
-        hs = small + 128;
-    }
-    HALO_CHECK(msm_device(st, curve, st->scratch[1].ptr, st->scratch[2].ptr, n, hp, hs, small, s));
+    if (w) HALO_CHECK(copy_h2d(small + 64, w, 32, s));
+    HALO_CHECK(msm_device(st, curve, st->scratch[1].ptr, st->scratch[2].ptr, n, w ? srs.s_table.ptr : nullptr,
+                          w ? small + 64 : nullptr, small, s));
     return copy_d2h(out, small, 64, s);
 }
 
@@ -734,35 +898,24 @@ extern "C" int halo_pcdl_commit(halo_curve_t curve, const halo_fe_t* coeffs, siz
     if (!out || (len && !coeffs)) return set_error(HALO_EINVAL, "halo_pcdl_commit: null buffer");
     DeviceState* st = current_state();
     if (!st) return HALO_EDEVICE;
-    size_t D;
-    {
-        std::lock_guard<std::mutex> g(st->mu);
-        D = st->srs[curve].n ? st->srs[curve].n - 1 : 0;
-        if (!st->srs[curve].n) return set_error(HALO_ESRSRANGE, "no resident SRS: call halo_srs_upload first");
-    }
+    std::lock_guard<std::mutex> g(st->mu);
+    SrsState& srs = st->srs[curve];
+    if (!srs.n) return set_error(HALO_ESRSRANGE, "no resident SRS: call halo_srs_upload first");
+    const size_t D = srs.n - 1;
     const size_t n = d + 1;
     const size_t p_deg = poly_degree(coeffs, len);
     if (!is_pow2(n)) return set_error(HALO_ENOTPOW2, "n (%zu) is not a power of two", n);
     if (p_deg > d) return set_error(HALO_EDEGREE, "p_deg (%zu) <= d (%zu)", p_deg, d);
     if (d > D) return set_error(HALO_ESRSRANGE, "d (%zu) <= D (%zu) (pp_len = %zu)", d, D, D + 1);
-    // trailing zeros beyond the degree do not change the MSM; ark passes the trimmed coeffs
-    const size_t m = std::min(len, n);
-    std::lock_guard<std::mutex> g(st->mu);
-    SrsState& srs = st->srs[curve];
     if (w && !srs.has_sh) return set_error(HALO_ESRSRANGE, "hiding commitment needs S: upload the SRS (S, H) first");
+    // coefficients past the degree are zero and contribute nothing to the MSM
+    const size_t m = std::min(len, n);
     hipStream_t s = 0;
     HALO_CHECK(st->scratch[2].reserve(std::max<size_t>(m, 1) * 32));
-    HALO_CHECK(st->scratch[3].reserve(64 + 64 + 32));
+    HALO_CHECK(st->scratch[3].reserve(64 + 32));
     HALO_CHECK(copy_h2d(st->scratch[2].ptr, coeffs, m * 32, s));
     char* small = (char*)st->scratch[3].ptr;
-    const void* hp = nullptr;
-    const void* hs = nullptr;
-    if (w) {
-        HALO_CHECK(copy_h2d(small + 64, srs.S, 64, s));
-        HALO_CHECK(copy_h2d(small + 128, w, 32, s));
-        hp = small + 64;
-        hs = small + 128;
-    }
-    HALO_CHECK(msm_device(st, curve, srs.gs.ptr, st->scratch[2].ptr, m, hp, hs, small, s));
+    if (w) HALO_CHECK(copy_h2d(small + 64, w, 32, s));
+    HALO_CHECK(msm_srs_device(st, curve, st->scratch[2].ptr, m, w ? small + 64 : nullptr, small, s));
     return copy_d2h(out, small, 64, s);
 }

@@ -7,9 +7,14 @@ namespace halo {
 int msm_window_bits(size_t n);
 // MSM over device-resident internal-format affine bases (64 B each) and ark-format scalars.
 // Writes one ark WrappedPoint (64 B) to d_out_wrapped (device).  Optional hiding term
-// hide_scalar * hide_point (internal affine point, ark scalar; both device pointers).
+// hide_scalar * P where hide_table = {2^i P : i < 256} (internal affine; both device pointers).
 int msm_device(DeviceState* st, int curve, const void* bases_int, const void* scalars_ark, size_t n,
-               const void* hide_point, const void* hide_scalar, void* d_out_wrapped, hipStream_t s);
+               const void* hide_table, const void* hide_scalar, void* d_out_wrapped, hipStream_t s);
+// MSM over the resident SRS prefix (window-shifted copies when precomputed); optional hiding
+// scalar (ark, device pointer) times S.
+int msm_srs_device(DeviceState* st, int curve, const void* scalars_ark, size_t n, const void* hide_scalar,
+                   void* d_out_wrapped, hipStream_t s);
+int srs_precompute_windows(DeviceState* st, int curve, hipStream_t s);
 int convert_wrapped_to_internal(int curve, const void* in, void* out, size_t n, hipStream_t s);
 int convert_internal_to_wrapped(int curve, const void* in, void* out, size_t n, hipStream_t s);
 int ntt_device_dispatch(DeviceState* st, int field, const void* d_in, void* d_out, void* d_tmp, unsigned logn,

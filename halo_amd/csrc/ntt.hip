@@ -300,7 +300,8 @@ static int ntt_device(DeviceState* st, int field, const void* d_in, void* d_out,
         const size_t rt_entries = lr ? ((size_t)1 << (lr - 1)) : 1;
         const size_t lds = (NTT_E + rt_entries) * NLIMB * 4;
         dim3 grid((unsigned)(NJ / T), (unsigned)batch);
-        hipLaunchKernelGGL(k_ntt_pass<F>, grid, dim3(NTT_THREADS), lds, s, a);
+        ProfScope prof("ntt_pass", s);
+        HALO_LAUNCH(prof, k_ntt_pass<F>, grid, dim3(NTT_THREADS), lds, s, a);
         HALO_HIP(hipGetLastError());
         log_ns += lr;
     }

@@ -73,9 +73,89 @@ int copy_d2h(void* dst, const void* src, size_t bytes, hipStream_t s) {
     return HALO_OK;
 }
 
+// ---- profiling ------------------------------------------------------------------------------
+struct ProfEntry {
+    std::string name;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+    size_t launches = 0;
+    double total_ms = 0;
+};
+static std::mutex g_prof_mu;
+static std::vector<ProfEntry> g_prof;
+static bool g_prof_on = false;
+
+bool prof_enabled() { return g_prof_on; }
+
+ProfScope::ProfScope(const char* name, hipStream_t stream) {
+    if (!g_prof_on) return;
+    s = stream;
+    std::lock_guard<std::mutex> g(g_prof_mu);
+    for (size_t i = 0; i < g_prof.size(); i++)
+        if (g_prof[i].name == name) slot = (int)i;
+    if (slot < 0) {
+        g_prof.push_back(ProfEntry{name, {}, 0, 0.0});
+        slot = (int)g_prof.size() - 1;
+    }
+    if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) {
+        slot = -1;
+        return;
+    }
+}
+
+ProfScope::~ProfScope() {
+    if (slot < 0) return;
+    std::lock_guard<std::mutex> g(g_prof_mu);
+    g_prof[slot].pending.emplace_back(a, b);
+}
+
+static void prof_drain() {
+    for (auto& e : g_prof) {
+        for (auto& p : e.pending) {
+            (void)hipEventSynchronize(p.second);
+            float ms = 0;
+            if (hipEventElapsedTime(&ms, p.first, p.second) == hipSuccess) {
+                e.total_ms += ms;
+                e.launches++;
+            }
+            (void)hipEventDestroy(p.first);
+            (void)hipEventDestroy(p.second);
+        }
+        e.pending.clear();
+    }
+}
+
 }  // namespace halo
 
 using namespace halo;
+
+extern "C" int halo_profile_enable(int on) {
+    std::lock_guard<std::mutex> g(g_prof_mu);
+    g_prof_on = on != 0;
+    return HALO_OK;
+}
+
+extern "C" int halo_profile_reset(void) {
+    std::lock_guard<std::mutex> g(g_prof_mu);
+    prof_drain();
+    g_prof.clear();
+    return HALO_OK;
+}
+
+extern "C" int halo_profile_read(const char* name, size_t* launches, double* total_ms) {
+    clear_error();
+    if (!name) return set_error(HALO_EINVAL, "null name");
+    std::lock_guard<std::mutex> g(g_prof_mu);
+    prof_drain();
+    for (auto& e : g_prof)
+        if (e.name == name) {
+            if (launches) *launches = e.launches;
+            if (total_ms) *total_ms = e.total_ms;
+            return HALO_OK;
+        }
+    if (launches) *launches = 0;
+    if (total_ms) *total_ms = 0;
+    return HALO_OK;
+}
 
 extern "C" {
 

@@ -1,6 +1,7 @@
 // Host-side runtime shared by every translation unit of libhalo_gpu.so: error reporting,
 // per-device state, device memory helpers.
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdarg>
@@ -51,6 +52,7 @@ struct SrsState {
     bool has_sh = false;
     uint32_t S[16];     // internal packed (x, y)
     uint32_t H[16];
+    DevBuf s_table;     // 2^i S (i < 256), internal affine: hiding term of pedersen::commit
     DevBuf shifted;     // optional window-shifted copies
     int shifted_c = 0;  // window bits of `shifted`
     int shifted_windows = 0;
@@ -83,6 +85,27 @@ DeviceState* current_state();
 // Pinned staging helpers
 int copy_h2d(void* dst, const void* src, size_t bytes, hipStream_t s);
 int copy_d2h(void* dst, const void* src, size_t bytes, hipStream_t s);
+
+// ---- measurement hooks (halo_profile_*) ----------------------------------------------------
+// ProfScope owns a start/stop hipEvent pair for one launch when profiling is enabled; the launch
+// goes through hipExtLaunchKernelGGL, which records the kernel's own start/stop on its stream
+// (HALO_LAUNCH), so the measured time is the kernel's execution only.
+bool prof_enabled();
+struct ProfScope {
+    int slot = -1;
+    hipEvent_t a = nullptr, b = nullptr;
+    hipStream_t s = nullptr;
+    ProfScope(const char* name, hipStream_t stream);
+    ~ProfScope();
+};
+
+#define HALO_LAUNCH(prof, kern, grid, block, shmem, stream, ...)                                       \
+    do {                                                                                              \
+        if ((prof).slot >= 0)                                                                         \
+            hipExtLaunchKernelGGL(kern, grid, block, shmem, stream, (prof).a, (prof).b, 0, __VA_ARGS__); \
+        else                                                                                          \
+            hipLaunchKernelGGL(kern, grid, block, shmem, stream, __VA_ARGS__);                        \
+    } while (0)
 
 inline bool is_pow2(size_t n) { return n && !(n & (n - 1)); }
 inline unsigned ilog2(size_t n) {

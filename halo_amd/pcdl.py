@@ -1,0 +1,86 @@
+"""Mirror of crates/accumulation/src/pcdl.rs (commit + the IPA round loop) on the MI355X backend.
+
+The Fiat-Shamir transcript (Poseidon sponge, crates/poseidon) stays with the caller: the round loop
+of ``open_without_eval`` (pcdl.rs:404-438) asks a ``challenge(xi_prev, L, R) -> xi`` callable for
+each round's challenge, exactly where the reference calls ``transcript.challenge()``.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Callable
+
+import numpy as np
+
+from . import _lib as H
+from .group import _curve
+
+
+def commit(p, d: int, w=None, curve="pallas") -> np.ndarray:
+    """pcdl.rs:275-287: n = d + 1 must be a power of two, deg(p) <= d <= D, then
+    pedersen::commit(w, Gs[0..n], p.coeffs) over the resident SRS."""
+    H.ensure_device()
+    c = H.fe_array(p) if len(p) else np.zeros((0, 4), dtype=np.uint64)
+    wa = H.fe_array(w, 1) if w is not None else None
+    out = np.zeros(8, dtype=np.uint64)
+    H.check(H.load().halo_pcdl_commit(_curve(curve), H.ptr(c) if len(c) else None, len(c), d, H.ptr(wa), H.ptr(out)))
+    return out
+
+
+class IpaSession:
+    """Device-resident (G, c, z) of one opening; mirrors the loop state of pcdl.rs:392-438."""
+
+    def __init__(self, cs, z, H_prime, curve="pallas"):
+        H.ensure_device()
+        self.curve = _curve(curve)
+        cs = H.fe_array(cs)
+        self.n = len(cs)
+        zz = H.fe_array(z, 1)
+        hp = H.point_array(H_prime)
+        s = ctypes.c_void_p()
+        H.check(H.load().halo_ipa_begin(self.curve, H.ptr(cs), self.n, H.ptr(zz), H.ptr(hp), ctypes.byref(s)))
+        self._s = s
+
+    def round_lr(self):
+        L = np.zeros(8, dtype=np.uint64)
+        R = np.zeros(8, dtype=np.uint64)
+        H.check(H.load().halo_ipa_round_lr(self._s, H.ptr(L), H.ptr(R)))
+        return L, R
+
+    def fold(self, xi, xi_inv):
+        H.check(H.load().halo_ipa_fold(self._s, H.ptr(H.fe_array(xi, 1)), H.ptr(H.fe_array(xi_inv, 1))))
+
+    def state(self):
+        m = ctypes.c_size_t(0)
+        H.check(H.load().halo_ipa_state(self._s, ctypes.byref(m), None, None, None))
+        k = max(2 * m.value, 1)
+        gs = np.zeros((k, 8), dtype=np.uint64)
+        cs = np.zeros((k, 4), dtype=np.uint64)
+        zs = np.zeros((k, 4), dtype=np.uint64)
+        H.check(H.load().halo_ipa_state(self._s, ctypes.byref(m), H.ptr(gs), H.ptr(cs), H.ptr(zs)))
+        return m.value, gs, cs, zs
+
+    def end(self):
+        U = np.zeros(8, dtype=np.uint64)
+        c = np.zeros(4, dtype=np.uint64)
+        H.check(H.load().halo_ipa_end(self._s, H.ptr(U), H.ptr(c)))
+        self._s = None
+        return U, c
+
+
+def ipa_rounds(cs, z, H_prime, challenge: Callable, inverse: Callable, curve="pallas"):
+    """The round loop of open_without_eval (pcdl.rs:392-450) given p'.coeffs resized to n, z, H' and
+    the caller's transcript.  ``challenge(xi_prev, L, R)`` returns the next xi (ark limbs, shape (4,));
+    ``inverse(xi)`` returns xi^-1.  Returns (Ls, Rs, U, c)."""
+    ses = IpaSession(cs, z, H_prime, curve)
+    n = ses.n
+    lg_n = n.bit_length() - 1
+    Ls, Rs = [], []
+    xi = None
+    for _ in range(lg_n):
+        L, R = ses.round_lr()
+        Ls.append(L)
+        Rs.append(R)
+        xi = challenge(xi, L, R)
+        ses.fold(xi, inverse(xi))
+    U, c = ses.end()
+    return Ls, Rs, U, c

@@ -86,6 +86,9 @@ void halo_synth_scalar(halo_curve_t curve, uint64_t seed, uint64_t j, uint64_t o
  * single-bucket-set MSM (trades HBM capacity for the per-window combination); optional. */
 int halo_srs_precompute_windows(halo_curve_t curve);
 
+/* Copies resident SRS points Gs[offset .. offset + n) back to the host as WrappedPoints. */
+int halo_srs_read(halo_curve_t curve, size_t offset, size_t n, halo_wrapped_point_t* out);
+
 /* ------------------------------------------------------------------ a3/a4: MSM
  * sum_{i < min(n_bases, n_scalars)} scalars[i] * bases[i]
  * Replaces `Projective::msm_unchecked` as called by group::point_dot_affine
@@ -108,6 +111,9 @@ int halo_pcdl_commit(halo_curve_t curve, const halo_fe_t* coeffs, size_t len, si
  * d_scalars (n halo_fe_t) in HBM; result written to host `out`.  Synchronous on `stream`. */
 int halo_msm_dev(halo_curve_t curve, const void* d_bases, const void* d_scalars, size_t n,
                  halo_wrapped_point_t* out, void* stream);
+/* Sum of k points (host arrays) on the device: the combine step after an RCCL all-gather of
+ * per-rank partial MSMs (RCCL has no elliptic-curve reduction operator). */
+int halo_point_sum(halo_curve_t curve, const halo_wrapped_point_t* pts, size_t k, halo_wrapped_point_t* out);
 /* Window size the device MSM uses for n points. */
 int halo_msm_window_bits(size_t n);
 
@@ -165,6 +171,14 @@ int halo_ipa_end(halo_ipa_session* s, halo_wrapped_point_t* U, halo_fe_t* c);
  * on the left halves. */
 int halo_ipa_fold_host(halo_curve_t curve, halo_wrapped_point_t* gs, halo_fe_t* cs, halo_fe_t* zs,
                        size_t m, const halo_fe_t* xi, const halo_fe_t* xi_inv);
+
+/* ------------------------------------------------------------------ measurement hooks
+ * When enabled, the library brackets its dominant kernels (MSM bucket accumulation, NTT passes)
+ * with hipEvents on the stream they run on; halo_profile_read returns the number of launches and
+ * the summed kernel time in ms for a kernel name ("msm_acc", "ntt_pass") since the last reset. */
+int halo_profile_enable(int on);
+int halo_profile_read(const char* name, size_t* launches, double* total_ms);
+int halo_profile_reset(void);
 
 /* ------------------------------------------------------------------ field self-test helpers
  * Elementwise device field ops over host arrays (used by the parity tests of a1):

@@ -1,0 +1,149 @@
+"""GPU parity: IPA folding, polynomial evaluation / dots / powers (a8).
+
+The IPA round loop is driven exactly like pcdl::open_without_eval (pcdl.rs:392-450): device-resident
+(G, c, z), L/R per round, a host transcript supplying xi, fold.  The transcript here is a
+deterministic stand-in (SHA3 of the round's L, R); the same stand-in drives the pure-Python oracle
+loop, so every L, R, the final U and c compare bit-exactly.  test_u_check (pcdl.rs:627-687) pins
+the fold against the h(X)-coefficient MSM.
+"""
+import hashlib
+import random
+
+import numpy as np
+import pytest
+
+import pasta as P
+from halo_amd import group, pcdl, poly
+
+pytestmark = pytest.mark.gpu
+CURVES = [("pallas", 0), ("vesta", 1)]
+
+
+def fe(vals, m):
+    return np.array([P.int_to_limbs(P.to_mont(v % m, m)) for v in vals], dtype=np.uint64).reshape(-1, 4)
+
+
+def unfe(a, m):
+    return [P.from_mont(P.limbs_to_int(r), m) for r in np.asarray(a).reshape(-1, 4)]
+
+
+@pytest.mark.parametrize("cname,cid", CURVES)
+def test_fold_host_golden(hal, golden, cname, cid):
+    L = hal.load()
+    gs = np.ascontiguousarray(golden[f"ref_srs_{cname}_b00_first64"][:16].copy())
+    cs = np.ascontiguousarray(golden[f"ipa_{cname}_cs"].copy())
+    zs = np.ascontiguousarray(golden[f"ipa_{cname}_zs"].copy())
+    xi, xinv = golden[f"ipa_{cname}_xi"]
+    hal.check(L.halo_ipa_fold_host(cid, hal.ptr(gs), hal.ptr(cs), hal.ptr(zs), 8, hal.ptr(np.ascontiguousarray(xi)),
+                                   hal.ptr(np.ascontiguousarray(xinv))))
+    assert np.array_equal(gs[:8], golden[f"ipa_{cname}_gs1"])
+    assert np.array_equal(cs[:8], golden[f"ipa_{cname}_cs1"])
+    assert np.array_equal(zs[:8], golden[f"ipa_{cname}_zs1"])
+
+
+@pytest.mark.parametrize("cname,cid", CURVES)
+def test_u_check(hal, golden, corc, cname, cid):
+    """pcdl.rs:627-687: folding G[0..8] with xis = [0,1,2,3] gives <h, G>."""
+    c = P.CURVES[cname]
+    r = c.scalar
+    g = corc.srs_generate(cname, 8)
+    group.PublicParams.upload(cname, g, precompute_windows=False)
+    ses = pcdl.IpaSession(np.zeros((8, 4), dtype=np.uint64), fe([5], r), g[0], cname)
+    for xi in (1, 2, 3):
+        ses.fold(fe([xi], r), fe([P.inv(xi, r)], r))
+    U, _ = ses.end()
+    assert np.array_equal(U, golden[f"ucheck_{cname}_U"][0])
+    assert np.array_equal(U, group.point_dot_affine(golden[f"ucheck_{cname}_hcoeffs"], g, cname))
+
+
+def transcript(cname):
+    c = P.CURVES[cname]
+
+    def challenge(xi_prev, L, R):
+        h = hashlib.sha3_256((b"" if xi_prev is None else np.asarray(xi_prev).tobytes()) + L.tobytes() + R.tobytes())
+        v = int.from_bytes(h.digest(), "little") % c.scalar or 1
+        return fe([v], c.scalar)[0]
+
+    def inverse(x):
+        return fe([P.inv(P.from_mont(P.limbs_to_int(x), c.scalar), c.scalar)], c.scalar)[0]
+
+    return challenge, inverse
+
+
+@pytest.mark.parametrize("cname,cid", CURVES)
+@pytest.mark.parametrize("n", [2, 16, 64])
+def test_ipa_rounds_vs_oracle(hal, corc, cname, cid, n):
+    """The whole round loop of pcdl.rs:404-438 against a pure-Python restatement."""
+    c = P.CURVES[cname]
+    r = c.scalar
+    g = corc.srs_generate(cname, 64)
+    group.PublicParams.upload(cname, g, precompute_windows=False)
+    rng = random.Random(n)
+    cs = [rng.randrange(r) for _ in range(n)]
+    z = rng.randrange(r)
+    Hp = P.mul_fast(c, rng.randrange(r), c.generator)
+    challenge, inverse = transcript(cname)
+    Ls, Rs, U, cfin = pcdl.ipa_rounds(fe(cs, r), fe([z], r), np.array(P.point_to_wrapped(c, Hp), dtype=np.uint64),
+                                      challenge, inverse, cname)
+    # oracle loop
+    G = [P.wrapped_to_point(c, list(x)) for x in g[:n]]
+    C, Z = cs[:], P.construct_powers(z, n, r)
+    xi = None
+    for k in range(n.bit_length() - 1):
+        m = len(G) // 2
+        L = P.add(c, P.msm(c, G[:m], C[m:]), P.mul_fast(c, P.scalar_dot(C[m:], Z[:m], r), Hp))
+        R = P.add(c, P.msm(c, G[m:], C[:m]), P.mul_fast(c, P.scalar_dot(C[:m], Z[m:], r), Hp))
+        assert list(Ls[k]) == P.point_to_wrapped(c, L), k
+        assert list(Rs[k]) == P.point_to_wrapped(c, R), k
+        xi = challenge(xi, np.array(P.point_to_wrapped(c, L), dtype=np.uint64),
+                       np.array(P.point_to_wrapped(c, R), dtype=np.uint64))
+        x = P.from_mont(P.limbs_to_int(xi), r)
+        _, _, _, _, G, C, Z = P.ipa_round(c, G, C, Z, x)
+    assert list(U) == P.point_to_wrapped(c, G[0])
+    assert unfe(cfin, r) == [C[0]]
+
+
+def test_ipa_fold_large_vs_c_oracle(hal, corc):
+    """One fold at m = 2^14 (per-element scalar multiplication + affine normalisation)."""
+    c = P.PALLAS
+    r = c.scalar
+    m = 1 << 14
+    g = corc.srs_generate("pallas", 2 * m)
+    rng = np.random.default_rng(3)
+    cs = rng.integers(0, 2**62, size=(2 * m, 4), dtype=np.uint64)
+    zs = rng.integers(0, 2**62, size=(2 * m, 4), dtype=np.uint64)
+    xi = fe([12345678901234567890123456789], r)[0]
+    xinv = fe([P.inv(12345678901234567890123456789, r)], r)[0]
+    eg, ec, ez = corc.ipa_fold("pallas", g, cs, zs, xi, xinv)
+    G, C, Z = g.copy(), cs.copy(), zs.copy()
+    hal.check(hal.load().halo_ipa_fold_host(0, hal.ptr(G), hal.ptr(C), hal.ptr(Z), m, hal.ptr(np.ascontiguousarray(xi)),
+                                            hal.ptr(np.ascontiguousarray(xinv))))
+    assert np.array_equal(G[:m], eg) and np.array_equal(C[:m], ec) and np.array_equal(Z[:m], ez)
+
+
+@pytest.mark.parametrize("tag", ["fp", "fq"])
+def test_poly_eval_golden_and_batch(hal, golden, corc, tag):
+    m = P.FIELDS[tag]
+    p40 = golden[f"eval_{tag}_poly"]
+    for z, v in zip(golden[f"eval_{tag}_z"], golden[f"eval_{tag}_out"]):
+        assert np.array_equal(poly.evaluate_batch([p40], z, tag)[0], v)
+    rng = np.random.default_rng(1)
+    polys = [np.ascontiguousarray(rng.integers(0, 2**62, size=(k, 4), dtype=np.uint64)) for k in (0, 1, 7, 8191, 100000)]
+    z = fe([987654321987654321], m)[0]
+    got = poly.evaluate_batch(polys, z, tag)
+    for p, v in zip(polys, got):
+        exp = corc.poly_eval(tag, p, z) if len(p) else np.zeros(4, dtype=np.uint64)
+        assert np.array_equal(v, exp)
+
+
+@pytest.mark.parametrize("tag", ["fp", "fq"])
+def test_scalar_dot_and_powers(hal, corc, tag):
+    m = P.FIELDS[tag]
+    rng = np.random.default_rng(2)
+    for n in (0, 1, 1000, 100003):
+        x = np.ascontiguousarray(rng.integers(0, 2**62, size=(n, 4), dtype=np.uint64))
+        y = np.ascontiguousarray(rng.integers(0, 2**62, size=(n, 4), dtype=np.uint64))
+        assert np.array_equal(group.scalar_dot(x, y, tag), corc.scalar_dot(tag, x, y) if n else np.zeros(4, np.uint64))
+    z = 31337
+    pw = group.construct_powers(fe([z], m), 1000, tag)
+    assert unfe(pw, m) == P.construct_powers(z, 1000, m)

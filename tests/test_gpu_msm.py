@@ -1,0 +1,215 @@
+"""GPU parity: MSM, pedersen::commit, pcdl::commit, SRS provider.
+
+Bit-exact against the committed golden vectors over the reference SRS, against the C oracle
+(ark-ec msm_bigint_wnaf restatement) up to 2^16, and at BASELINE sizes (2^20 reference-recipe SRS,
+2^22 synthetic SRS) against the size-independent identity MSM(G, s) = (sum_j s_j k_j) * G where
+k_j are the known discrete logs of the bases.
+"""
+import random
+
+import numpy as np
+import pytest
+
+import pasta as P
+from halo_amd import group, pcdl, pedersen
+
+pytestmark = pytest.mark.gpu
+CURVES = [("pallas", 0), ("vesta", 1)]
+
+
+def fe(vals, m):
+    return np.array([P.int_to_limbs(P.to_mont(v % m, m)) for v in vals], dtype=np.uint64).reshape(-1, 4)
+
+
+def rand_sc(n, seed):
+    rng = np.random.default_rng(seed)
+    a = rng.integers(0, 2**63, size=(n, 4), dtype=np.uint64) * 2 + rng.integers(0, 2, size=(n, 4), dtype=np.uint64)
+    a[:, 3] &= np.uint64(0x3FFFFFFFFFFFFFFF)
+    return np.ascontiguousarray(a)
+
+
+def limbs_canon(x) -> int:
+    return int(x[0]) | int(x[1]) << 64 | int(x[2]) << 128 | int(x[3]) << 192
+
+
+@pytest.mark.parametrize("cname,cid", CURVES)
+def test_msm_golden_reference_srs(hal, golden, cname, cid):
+    bases = golden[f"ref_srs_{cname}_b00_first64"]
+    for n in (1, 2, 5, 16, 64):
+        got = group.point_dot_affine(golden[f"msm_{cname}_n{n}_scalars"], bases[:n], cname)
+        assert np.array_equal(got, golden[f"msm_{cname}_n{n}_result"][0]), n
+
+
+@pytest.mark.parametrize("cname,cid", CURVES)
+def test_msm_vs_c_oracle(hal, corc, cname, cid):
+    c = P.CURVES[cname]
+    g = corc.srs_generate(cname, 1 << 16)
+    for n in (0, 1, 3, 31, 32, 33, 100, 1000, 4096, 5000, 1 << 16):
+        sc = rand_sc(n, n)
+        if n >= 8:
+            sc[0] = 0                                           # zero scalar
+            sc[1] = fe([c.scalar - 1], c.scalar)[0]             # r - 1
+            sc[2] = sc[3]                                       # repeated scalar
+            sc[4] = fe([1 << 15], c.scalar)[0]                  # digit on a window boundary
+        exp = corc.msm(cname, g[:n], sc) if n else np.zeros(8, dtype=np.uint64)
+        assert np.array_equal(group.point_dot_affine(sc, g[:n], cname), exp), n
+
+
+@pytest.mark.parametrize("cname,cid", CURVES)
+def test_msm_length_is_min_of_inputs(hal, corc, cname, cid):
+    """msm_unchecked uses min(#bases, #scalars) (trimmed coefficient vectors, trace.rs:196)."""
+    g = corc.srs_generate(cname, 300)
+    sc = rand_sc(200, 1)
+    assert np.array_equal(group.point_dot_affine(sc, g, cname), corc.msm(cname, g[:200], sc))
+    assert np.array_equal(group.point_dot_affine(rand_sc(300, 2), g[:50], cname), corc.msm(cname, g[:50], rand_sc(300, 2)))
+
+
+@pytest.mark.parametrize("cname,cid", CURVES)
+def test_msm_skewed_scalars(hal, corc, cname, cid):
+    """All-equal scalars put every point in one bucket per window (task splitting path)."""
+    g = corc.srs_generate(cname, 1 << 14)
+    sc = np.ascontiguousarray(np.repeat(rand_sc(1, 5), 1 << 14, axis=0))
+    assert np.array_equal(group.point_dot_affine(sc, g, cname), corc.msm(cname, g, sc))
+    small = np.zeros((1 << 12, 4), dtype=np.uint64)
+    small[:, 0] = np.arange(1 << 12) % 3  # tiny scalars: most windows empty
+    assert np.array_equal(group.point_dot_affine(small, g[: 1 << 12], cname), corc.msm(cname, g[: 1 << 12], small))
+
+
+@pytest.mark.parametrize("cname,cid", CURVES)
+def test_pedersen_homomorphism_and_hiding(hal, golden, corc, cname, cid):
+    """pedersen.rs:38-79 (homomorphism) with hiding S * w; S, H from the reference's sh.bin."""
+    c = P.CURVES[cname]
+    r = c.scalar
+    g = corc.srs_generate(cname, 4096)
+    S, Hh = golden[f"ref_sh_{cname}"]
+    group.PublicParams.upload(cname, g, S, Hh, precompute_windows=False)
+    rng = random.Random(17)
+    for n in (2, 100, 4096):
+        m1 = [rng.randrange(r) for _ in range(n)]
+        m2 = [rng.randrange(r) for _ in range(n)]
+        w1, w2 = rng.randrange(r), rng.randrange(r)
+        inner = pedersen.commit(fe([w1 + w2], r), g[:n], fe([a + b for a, b in zip(m1, m2)], r), cname)
+        outer = P.add(c, P.wrapped_to_point(c, list(pedersen.commit(fe([w1], r), g[:n], fe(m1, r), cname))),
+                      P.wrapped_to_point(c, list(pedersen.commit(fe([w2], r), g[:n], fe(m2, r), cname))))
+        assert list(inner) == P.point_to_wrapped(c, outer)
+        exp = P.add(c, P.wrapped_to_point(c, list(corc.msm(cname, g[:n], fe(m1, r)))),
+                    P.mul_fast(c, w1, P.wrapped_to_point(c, list(S))))
+        assert list(pedersen.commit(fe([w1], r), g[:n], fe(m1, r), cname)) == P.point_to_wrapped(c, exp)
+
+
+def test_pedersen_length_assert(hal, corc):
+    g = corc.srs_generate("pallas", 8)
+    with pytest.raises(AssertionError, match="ms must be larger than Gs"):
+        pedersen.commit(None, g[:4], rand_sc(8, 1), "pallas")
+
+
+@pytest.mark.parametrize("cname,cid", CURVES)
+def test_pcdl_commit_reference_srs(hal, golden, corc, cname, cid):
+    """pcdl.rs:275-287 over the resident reference-recipe SRS (2^16 here), both MSM paths (windowed,
+    and window-shifted precomputed bases), with and without hiding; and its assertion messages."""
+    c = P.CURVES[cname]
+    r = c.scalar
+    n = 1 << 16
+    g = corc.srs_generate(cname, n)
+    S, Hh = golden[f"ref_sh_{cname}"]
+    for pre in (False, True):
+        group.PublicParams.upload(cname, g, S, Hh, precompute_windows=pre)
+        for d in (0, 1, 255, 4095, n - 1):
+            coeffs = rand_sc(d + 1, d)
+            exp = corc.msm(cname, g[: d + 1], coeffs)
+            assert np.array_equal(pcdl.commit(coeffs, d, None, cname), exp), (pre, d)
+        w = rand_sc(1, 9)
+        coeffs = rand_sc(1000, 3)
+        exp = P.add(c, P.wrapped_to_point(c, list(corc.msm(cname, g[:1000], coeffs))),
+                    P.mul_fast(c, P.from_mont(limbs_canon(w[0]), r), P.wrapped_to_point(c, list(S))))
+        assert list(pcdl.commit(coeffs, 1023, w, cname)) == P.point_to_wrapped(c, exp)
+    with pytest.raises(AssertionError, match=r"n \(11\) is not a power of two"):
+        pcdl.commit(rand_sc(4, 1), 10, None, cname)
+    with pytest.raises(AssertionError, match=r"p_deg \(7\) <= d \(3\)"):
+        pcdl.commit(rand_sc(8, 1), 3, None, cname)
+    with pytest.raises(AssertionError, match=r"d \(131071\) <= D \(65535\)"):
+        pcdl.commit(rand_sc(4, 1), (1 << 17) - 1, None, cname)
+
+
+@pytest.mark.parametrize("cname,cid", CURVES)
+def test_msm_2p20_reference_srs_known_logs(hal, corc, cname, cid):
+    """BASELINE configs[1]: 2^20-point MSM over the reference SRS recipe, bit-exact via the known
+    discrete logs h(j) of the reference's own SRS (crates/group/src/main.rs:55-67)."""
+    c = P.CURVES[cname]
+    r = c.scalar
+    n = 1 << 20
+    g = corc.srs_generate(cname, n)
+    group.PublicParams.upload(cname, g, precompute_windows=True)
+    sc = rand_sc(n, 2024)
+    got = pcdl.commit(sc, n - 1, None, cname)
+    # sum_j s_j h(srs_index(j)): only 16447 distinct hash indices
+    logs = {}
+    acc = 0
+    sb = sc.tobytes()
+    for j in range(n):
+        t = P.srs_index(j)
+        if t not in logs:
+            logs[t] = P.srs_hash_scalar(c, t)
+        acc += int.from_bytes(sb[32 * j:32 * j + 32], "little") * logs[t]
+    acc = acc * pow(1 << 256, -1, r) % r
+    exp = P.mul_fast(c, acc, c.generator)
+    assert list(got) == P.point_to_wrapped(c, exp)
+
+
+def test_msm_2p22_synthetic_srs_known_logs(hal):
+    """2^22 points (beyond the reference N = 2^20): synthetic SRS G_j = k_j G, checked as
+    (sum_j s_j k_j) G with k_j from halo_synth_scalar."""
+    c = P.PALLAS
+    r = c.scalar
+    n = 1 << 22
+    seed = 99
+    group.PublicParams.synthesize("pallas", n, seed, precompute_windows=True)
+    sc = rand_sc(n, 7)
+    got = pcdl.commit(sc, n - 1, None, "pallas")
+    k = synth_scalars_np(seed, n)
+    from halo_amd.group import synth_scalar
+    assert [limbs_canon(k[j]) for j in (0, 1, n - 1)] == [synth_scalar(seed, j) for j in (0, 1, n - 1)]
+    sb = sc.tobytes()
+    kb = k.tobytes()
+    acc = 0
+    for j in range(n):
+        acc += int.from_bytes(sb[32 * j:32 * j + 32], "little") * int.from_bytes(kb[32 * j:32 * j + 32], "little")
+    acc = acc * pow(1 << 256, -1, r) % r  # scalars are Montgomery: s = S / 2^256
+    assert list(got) == P.point_to_wrapped(c, P.mul_fast(c, acc, c.generator))
+
+
+def synth_scalars_np(seed: int, n: int) -> np.ndarray:
+    """numpy restatement of halo_synth_scalar (splitmix64 stream per index; top word masked)."""
+    M = np.uint64(0xFFFFFFFFFFFFFFFF)
+    j = np.arange(n, dtype=np.uint64)
+    st = np.uint64(seed) ^ (j * np.uint64(0xD1B54A32D192ED03))
+    out = np.zeros((n, 4), dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        for i in range(4):
+            st = st + np.uint64(0x9E3779B97F4A7C15)
+            z = st.copy()
+            z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+            z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+            out[:, i] = z ^ (z >> np.uint64(31))
+    out[:, 3] &= np.uint64(0x1FFFFFFFFFFFFFFF)
+    zero = (out == 0).all(axis=1)
+    out[zero, 0] = 1
+    del M
+    return out
+
+
+def test_point_sum(hal, corc):
+    c = P.PALLAS
+    g = corc.srs_generate("pallas", 40)
+    exp = None
+    for x in g[:37]:
+        exp = P.add(c, exp, P.wrapped_to_point(c, list(x)))
+    assert list(group.point_sum(g[:37], "pallas")) == P.point_to_wrapped(c, exp)
+    assert list(group.point_sum(g[:0], "pallas")) == [0] * 8
+
+
+def test_srs_read_roundtrip(hal, corc):
+    g = corc.srs_generate("vesta", 1000)
+    group.PublicParams.upload("vesta", g, precompute_windows=False)
+    assert group.PublicParams.len("vesta") == 1000
+    assert np.array_equal(group.PublicParams.read("vesta", 100, 50), g[100:150])

@@ -1,0 +1,159 @@
+"""GPU parity: NTT / iNTT / evaluate_over_domain / interpolate / poly_mul.
+
+Small sizes are checked against the committed golden vectors and the C oracle bit-for-bit; the
+BASELINE sizes (2^20, 2^22) through size-independent properties: iNTT(NTT(x)) == x, linearity, and
+spot evaluations p(omega^i) by Horner on the CPU oracle.
+"""
+import ctypes
+import random
+
+import numpy as np
+import pytest
+
+import pasta as P
+from halo_amd import poly
+
+pytestmark = pytest.mark.gpu
+
+
+def rand_fe(n, seed):
+    rng = np.random.default_rng(seed)
+    a = rng.integers(0, 2**63, size=(n, 4), dtype=np.uint64) * 2 + rng.integers(0, 2, size=(n, 4), dtype=np.uint64)
+    a[:, 3] &= np.uint64(0x3FFFFFFFFFFFFFFF)  # < 2^254 < p
+    return np.ascontiguousarray(a)
+
+
+def fe(vals, m):
+    return np.array([P.int_to_limbs(P.to_mont(v % m, m)) for v in vals], dtype=np.uint64).reshape(-1, 4)
+
+
+def unfe(a, m):
+    return [P.from_mont(P.limbs_to_int(r), m) for r in np.asarray(a).reshape(-1, 4)]
+
+
+@pytest.mark.parametrize("tag,fid", [("fp", 0), ("fq", 1)])
+def test_ntt_golden(hal, golden, tag, fid):
+    L = hal.load()
+    for logn in range(0, 9):
+        x = np.ascontiguousarray(golden[f"ntt_{tag}_log{logn}_in"].copy())
+        hal.check(L.halo_ntt(fid, hal.ptr(x), logn, 0))
+        assert np.array_equal(x, golden[f"ntt_{tag}_log{logn}_out"]), logn
+        hal.check(L.halo_ntt(fid, hal.ptr(x), logn, 1))
+        assert np.array_equal(x, golden[f"ntt_{tag}_log{logn}_in"]), logn
+
+
+@pytest.mark.parametrize("tag,fid", [("fp", 0), ("fq", 1)])
+def test_ntt_vs_c_oracle(hal, corc, tag, fid):
+    L = hal.load()
+    for logn in (9, 10, 11, 12, 13, 15, 16, 17, 18):
+        x = rand_fe(1 << logn, logn)
+        exp = corc.ntt(tag, x)
+        got = x.copy()
+        hal.check(L.halo_ntt(fid, hal.ptr(got), logn, 0))
+        assert np.array_equal(got, exp), logn
+        hal.check(L.halo_ntt(fid, hal.ptr(got), logn, 1))
+        assert np.array_equal(got, x), logn
+
+
+@pytest.mark.parametrize("logn", [20, 22])
+def test_ntt_full_size_properties(hal, corc, logn):
+    """BASELINE config 3 sizes: round trip, linearity, and Horner spot checks."""
+    L = hal.load()
+    m = P.FP_MODULUS
+    n = 1 << logn
+    x = rand_fe(n, 100 + logn)
+    ev = x.copy()
+    hal.check(L.halo_ntt(0, hal.ptr(ev), logn, 0))
+    back = ev.copy()
+    hal.check(L.halo_ntt(0, hal.ptr(back), logn, 1))
+    assert np.array_equal(back, x)
+    w = P.root_of_unity(m, n)
+    for i in (0, 1, 12345 % n, n - 1):
+        z = fe([pow(w, i, m)], m)[0]
+        assert np.array_equal(corc.poly_eval("fp", x, z), ev[i]), i
+    # linearity: NTT(x + y) == NTT(x) + NTT(y), checked on a window of outputs
+    y = rand_fe(n, 7)
+    ey = y.copy()
+    hal.check(L.halo_ntt(0, hal.ptr(ey), logn, 0))
+    s = np.ascontiguousarray(fe([(a + b) % m for a, b in zip(unfe(x[:n], m), unfe(y[:n], m))], m)) if logn <= 16 else None
+    if s is None:
+        # sum on the device via field_op (add), then transform
+        s = np.zeros_like(x)
+        hal.check(L.halo_field_op(0, 1, hal.ptr(x), hal.ptr(y), n, hal.ptr(s)))
+    es = s.copy()
+    hal.check(L.halo_ntt(0, hal.ptr(es), logn, 0))
+    idx = slice(n // 2, n // 2 + 256)
+    chk = np.zeros((256, 4), dtype=np.uint64)
+    hal.check(L.halo_field_op(0, 1, hal.ptr(np.ascontiguousarray(ev[idx])), hal.ptr(np.ascontiguousarray(ey[idx])), 256,
+                              hal.ptr(chk)))
+    assert np.array_equal(chk, es[idx])
+
+
+def test_ntt_batched_device(hal, corc):
+    import torch
+    L = hal.load()
+    for logn, batch in ((12, 5), (17, 3), (8, 7)):
+        n = 1 << logn
+        x = rand_fe(batch * n, logn)
+        d = torch.from_numpy(x.view(np.int64)).cuda()
+        hal.check(L.halo_ntt_dev(1, ctypes.c_void_p(d.data_ptr()), logn, batch, 0, None))
+        torch.cuda.synchronize()
+        got = d.cpu().numpy().view(np.uint64)
+        for b in range(batch):
+            assert np.array_equal(got[b * n:(b + 1) * n], corc.ntt("fq", x[b * n:(b + 1) * n])), (logn, b)
+
+
+@pytest.mark.parametrize("tag", ["fp", "fq"])
+def test_evaluate_over_domain_and_interpolate(hal, golden, tag):
+    """poly.rs:56-64,133-139: longer-than-domain input is reduced mod X^N - 1; short input is
+    zero-padded; interpolate trims trailing zeros (DensePolynomial::from_coefficients_vec)."""
+    m = P.FIELDS[tag]
+    d16 = poly.Domain(16, tag)
+    ev = poly.Evals.from_poly_ref(golden[f"fold_{tag}_in40"], d16)
+    assert np.array_equal(ev.evals, golden[f"fold_{tag}_out16"])
+    rng = random.Random(9)
+    coeffs = [rng.randrange(m) for _ in range(10)]
+    d64 = poly.Domain(64, tag)
+    ev = poly.Evals.from_poly(fe(coeffs, m), d64)
+    assert unfe(ev.evals, m) == P.ntt(coeffs, 64, m)
+    back = ev.interpolate()
+    assert back.shape == (10, 4) and unfe(back, m) == coeffs
+    zero = poly.Evals(np.zeros((8, 4), dtype=np.uint64), poly.Domain(8, tag))
+    assert zero.interpolate().shape == (0, 4)
+    # from_vec_and_domain rotates right by one (poly.rs:21-31)
+    e = poly.Evals.from_vec_and_domain(fe([1, 2, 3, 4], m), poly.Domain(4, tag))
+    assert unfe(e.evals, m) == [4, 1, 2, 3]
+
+
+@pytest.mark.parametrize("tag", ["fp", "fq"])
+def test_evals_add_sub_mul_scale(hal, tag):
+    """protocol.rs:1037-1118 evals_add / evals_sub / evals_mul / evals_scale on the GPU NTT."""
+    m = P.FIELDS[tag]
+    rng = random.Random(21)
+    for n in (32, 1024):
+        a = [rng.randrange(m) for _ in range(n)]
+        b = [rng.randrange(m) for _ in range(n)]
+        dom = poly.Domain(n, tag)
+        ea = unfe(poly.Evals.from_poly_ref(fe(a, m), dom).evals, m)
+        eb = unfe(poly.Evals.from_poly_ref(fe(b, m), dom).evals, m)
+        s = poly.Evals(fe([x + y for x, y in zip(ea, eb)], m), dom).interpolate()
+        assert unfe(s, m) == P.trim([(x + y) % m for x, y in zip(a, b)])
+        d = poly.Evals(fe([x - y for x, y in zip(ea, eb)], m), dom).interpolate()
+        assert unfe(d, m) == P.trim([(x - y) % m for x, y in zip(a, b)])
+        k = rng.randrange(m)
+        sc = poly.Evals(fe([x * k for x in ea], m), dom).interpolate()
+        assert unfe(sc, m) == P.trim([x * k % m for x in a])
+        big = poly.Domain(2 * n, tag)
+        ea2 = unfe(poly.Evals.from_poly_ref(fe(a, m), big).evals, m)
+        eb2 = unfe(poly.Evals.from_poly_ref(fe(b, m), big).evals, m)
+        prod = unfe(poly.Evals(fe([x * y for x, y in zip(ea2, eb2)], m), big).interpolate(), m)
+        if n == 32:
+            assert prod == P.poly_mul(a, b, m)
+        assert unfe(poly.poly_mul(fe(a, m), fe(b, m), tag), m) == prod
+
+
+def test_poly_mul_edge(hal):
+    m = P.FP_MODULUS
+    assert poly.poly_mul(np.zeros((0, 4), dtype=np.uint64), fe([1, 2], m)).shape == (0, 4)
+    assert unfe(poly.poly_mul(fe([3], m), fe([5], m)), m) == [15]
+    assert unfe(poly.poly_mul(fe([m - 1, 1], m), fe([1, 1], m)), m) == [m - 1, 0, 1]  # (X-1)(X+1) = X^2 - 1

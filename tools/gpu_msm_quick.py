@@ -31,3 +31,18 @@ for cname,cid in [('pallas',0),('vesta',1)]:
     print(cname,'srs',np.array_equal(out,C.msm(cname,g[:n],sc)))
     # pcdl commit error
     rc=L.halo_pcdl_commit(cid,H.ptr(sc),10,10,None,H.ptr(out)); print('pcdl err',rc,H.last_error())
+    # pedersen with hiding: MSM + w*S  (S = g[0] here)
+    n=1000; sc=rand_sc(n); w=rand_sc(1)
+    exp_pt=P.add(c, P.wrapped_to_point(c,list(C.msm(cname,g[:n],sc))), P.mul_fast(c, P.from_mont(P.limbs_to_int(w[0]),c.scalar), P.wrapped_to_point(c,list(g[0]))))
+    H.check(L.halo_pedersen_commit(cid,H.ptr(w),H.ptr(np.ascontiguousarray(g[:n])),n,H.ptr(sc),n,H.ptr(out)))
+    print(cname,'pedersen hiding',list(out)==P.point_to_wrapped(c,exp_pt))
+    # precomputed windows
+    H.check(L.halo_srs_precompute_windows(cid))
+    for n in [1<<16, 1<<15, 1000, 1]:
+        sc=rand_sc(n)
+        H.check(L.halo_msm_srs(cid,H.ptr(sc),n,H.ptr(out)))
+        print(cname,'shifted srs',n,np.array_equal(out,C.msm(cname,g[:n],sc)))
+    sc=rand_sc(4096)
+    H.check(L.halo_pcdl_commit(cid,H.ptr(sc),4096,4095,H.ptr(w),H.ptr(out)))
+    exp_pt=P.add(c, P.wrapped_to_point(c,list(C.msm(cname,g[:4096],sc))), P.mul_fast(c, P.from_mont(P.limbs_to_int(w[0]),c.scalar), P.wrapped_to_point(c,list(g[0]))))
+    print(cname,'pcdl commit hiding shifted',list(out)==P.point_to_wrapped(c,exp_pt))
