@@ -58,6 +58,7 @@ def main():
     import torch.distributed as dist
 
     from halo_amd import _lib as H
+    from halo_amd.dist import allgather_points
 
     H.ensure_device(local)
     torch.cuda.set_device(local)
@@ -83,18 +84,13 @@ def main():
     scalars = fresh_scalars(nbatch)
     stream = torch.cuda.current_stream().cuda_stream
     out = np.zeros(8, dtype=np.uint64)
-    gathered = np.zeros((world, 8), dtype=np.uint64)
 
     def step(i):
         H.check(L.halo_msm_dev(curve, None, ctypes.c_void_p(scalars[i % nbatch].data_ptr()), n, H.ptr(out),
                                ctypes.c_void_p(stream)))
         if world > 1:
-            t = torch.from_numpy(out.view(np.int64).copy()).cuda()
-            parts = [torch.empty_like(t) for _ in range(world)]
-            dist.all_gather(parts, t)
-            for r, p in enumerate(parts):
-                gathered[r] = p.cpu().numpy().view(np.uint64)
-            H.check(L.halo_point_sum(curve, H.ptr(gathered), world, H.ptr(out)))
+            parts = allgather_points(out, dist, device=torch.device("cuda", local))
+            H.check(L.halo_point_sum(curve, H.ptr(np.ascontiguousarray(parts)), world, H.ptr(out)))
 
     for i in range(args.warmup):
         step(i)

@@ -1,0 +1,77 @@
+"""N > 1 path on CPU: world_size-2 gloo run of halo_amd.dist.sharded_msm (the protocol bench.py
+uses with RCCL on GPUs).  The per-rank partial MSM and the final point sum are computed by the C
+oracle here (no GPU in this container); the test checks the partition, the all-gather and the
+combine give the unsharded result on every rank."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, n, q):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import torch.distributed as dist
+
+    import corc
+    import pasta as P
+    from halo_amd.dist import shard_range, sharded_msm
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = corc.srs_generate("pallas", n)
+    rng = np.random.default_rng(42)
+    sc = rng.integers(0, 2**62, size=(n, 4), dtype=np.uint64)
+    c = P.PALLAS
+
+    def partial(lo, hi):
+        return corc.msm("pallas", g[lo:hi], sc[lo:hi]) if hi > lo else np.zeros(8, dtype=np.uint64)
+
+    def psum(parts):
+        acc = None
+        for p in parts:
+            acc = P.add(c, acc, P.wrapped_to_point(c, list(p)))
+        return np.array(P.point_to_wrapped(c, acc), dtype=np.uint64)
+
+    res = sharded_msm(partial, psum, n, dist)
+    lo, hi = shard_range(n, rank, world)
+    q.put((rank, res.tolist(), (lo, hi)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_sharded_msm_gloo(corc, world):
+    n = 3000
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    g = corc.srs_generate("pallas", n)
+    rng = np.random.default_rng(42)
+    sc = rng.integers(0, 2**62, size=(n, 4), dtype=np.uint64)
+    exp = corc.msm("pallas", g, sc).tolist()
+    ranges = sorted(r[2] for r in out)
+    assert ranges[0][0] == 0 and ranges[-1][1] == n and ranges[0][1] == ranges[1][0]
+    for _, res, _ in out:
+        assert res == exp
