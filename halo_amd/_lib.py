@@ -61,8 +61,11 @@ SIGNATURES = {
     "halo_pcdl_commit": [ctypes.c_int, _vp, _sz, _sz, _vp, _vp],
     "halo_msm_dev": [ctypes.c_int, _vp, _vp, _sz, _vp, _vp],
     "halo_msm_window_bits": [_sz],
+    "halo_msm_dev_async": [ctypes.c_int, _vp, _vp, _sz, _vp, _vp],
+    "halo_msm_join": [_vp],
     "halo_srs_read": [ctypes.c_int, _sz, _sz, _vp],
     "halo_point_sum": [ctypes.c_int, _vp, _sz, _vp],
+    "halo_point_sum_dev": [ctypes.c_int, _vp, _sz, _sz, _vp, _vp],
     "halo_profile_enable": [ctypes.c_int],
     "halo_profile_read": [ctypes.c_char_p, ctypes.POINTER(_sz), ctypes.POINTER(ctypes.c_double)],
     "halo_profile_reset": [],

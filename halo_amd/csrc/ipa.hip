@@ -461,8 +461,10 @@ extern "C" int halo_ipa_round_lr(halo_ipa_session* ses, halo_wrapped_point_t* L,
     const char* gs = ses->gs.as<const char>();
     HALO_CHECK(dot_device(sf, cs + m * 32, zs, m, sm + 128, ses->tmp.ptr, s));        // <c_r, z_l>
     HALO_CHECK(dot_device(sf, cs, zs + m * 32, m, sm + 160, ses->tmp.ptr, s));        // <c_l, z_r>
-    HALO_CHECK(msm_device(st, ses->curve, gs, cs + m * 32, m, ses->htab.ptr, sm + 128, sm + 256, s));   // L
-    HALO_CHECK(msm_device(st, ses->curve, gs + m * 64, cs, m, ses->htab.ptr, sm + 160, sm + 320, s));   // R
+    // L and R are independent: the second MSM's accumulation overlaps the first one's tail
+    HALO_CHECK(msm_device(st, ses->curve, gs, cs + m * 32, m, ses->htab.ptr, sm + 128, sm + 256, s, true));   // L
+    HALO_CHECK(msm_device(st, ses->curve, gs + m * 64, cs, m, ses->htab.ptr, sm + 160, sm + 320, s, true));   // R
+    HALO_CHECK(msm_join(st, s));
     HALO_CHECK(copy_d2h(L, sm + 256, 64, s));
     HALO_CHECK(copy_d2h(R, sm + 320, 64, s));
     return HALO_OK;

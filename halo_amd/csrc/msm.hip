@@ -473,9 +473,29 @@ static unsigned grid_for(size_t n, unsigned thr) { return (unsigned)std::max<siz
 
 struct MsmScratch {
     DevBuf digits, hist, totals, bstart, sorted, ntask, task_off, tasks, partials, bucket_sums, seg_acc, seg_sum,
-        bits, window_sums, scan_tmp, out;
+        bits, window_sums, scan_tmp, conv;
+    hipEvent_t acc_done = nullptr, tail_done = nullptr;
+    bool tail_pending = false;
 };
-static MsmScratch g_msm_scratch[64];  // per device
+// Two scratch sets per device: MSM k+1's digit/sort/accumulation phase (throughput-bound, whole
+// GPU) runs on the caller's stream while MSM k's reduction tail (latency-bound, a few waves) runs
+// on the per-device tail stream.
+struct MsmPipe {
+    MsmScratch set[2];
+    int next = 0;
+    hipStream_t tail = nullptr;
+};
+static MsmPipe g_msm_pipe[64];  // per device
+
+static int pipe_init(MsmPipe& P) {
+    if (P.tail) return HALO_OK;
+    HALO_HIP(hipStreamCreateWithFlags(&P.tail, hipStreamNonBlocking));
+    for (auto& m : P.set) {
+        HALO_HIP(hipEventCreateWithFlags(&m.acc_done, hipEventDisableTiming));
+        HALO_HIP(hipEventCreateWithFlags(&m.tail_done, hipEventDisableTiming));
+    }
+    return HALO_OK;
+}
 
 static int device_scan(const uint32_t* in, size_t n, uint32_t* out, DevBuf& tmp, hipStream_t s) {
     // out has n + 1 entries
@@ -496,9 +516,15 @@ static int device_scan(const uint32_t* in, size_t n, uint32_t* out, DevBuf& tmp,
 // bases_int: n internal affine points, or (shifted) W * n window-shifted points (single bucket set).
 template <class Cv>
 static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, size_t shift_stride,
-                        const uint4* scalars_ark, size_t n, int c_req, const uint4* hide_table, const uint4* hide_scalar, uint4* d_out_wrapped,
-                        hipStream_t s) {
-    MsmScratch& M = g_msm_scratch[st->device & 63];
+                        const uint4* scalars_ark, size_t n, int c_req, const uint4* hide_table, const uint4* hide_scalar,
+                        uint4* d_out_wrapped, hipStream_t s, bool async) {
+    MsmPipe& PP = g_msm_pipe[st->device & 63];
+    HALO_CHECK(pipe_init(PP));
+    MsmScratch& M = PP.set[PP.next];
+    PP.next ^= 1;
+    // the previous user of this scratch set must have finished its tail
+    if (M.tail_pending) HALO_HIP(hipStreamWaitEvent(s, M.tail_done, 0));
+    const hipStream_t ts = PP.tail;
     const size_t nn = std::max<size_t>(n, 1);
     const int c = c_req ? c_req : msm_window_bits(nn);
     const int W = (256 + c - 1) / c;
@@ -559,35 +585,57 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
                            M.partials.as<uint4>());
         hipLaunchKernelGGL(k_merge<Cv>, dim3(grid_for(NB, 256)), dim3(256), 0, s, M.task_off.as<const uint32_t>(), NB,
                            M.partials.as<const uint4>(), M.bucket_sums.as<uint4>());
-        hipLaunchKernelGGL(k_seg<Cv>, dim3(grid_for((size_t)SW * nseg, 64)), dim3(64), 0, s,
-                           M.bucket_sums.as<const uint4>(), B, L, SW, M.seg_acc.as<uint4>(), M.seg_sum.as<uint4>());
-        hipLaunchKernelGGL(k_bitsums<Cv>, dim3(nbits + 1, SW), dim3(256), 0, s, M.seg_acc.as<const uint4>(),
-                           M.seg_sum.as<const uint4>(), nseg, nbits, M.bits.as<uint4>());
-        hipLaunchKernelGGL(k_bitcombine<Cv>, dim3(SW), dim3(64), 0, s, M.bits.as<const uint4>(), nbits, logL,
-                           M.window_sums.as<uint4>());
         HALO_HIP(hipGetLastError());
     } else {
         HALO_HIP(hipMemsetAsync(M.window_sums.ptr, 0, (size_t)SW * 128, s));
     }
-    hipLaunchKernelGGL(k_final<Cv>, dim3(1), dim3(320), 0, s, M.window_sums.as<const uint4>(), SW, c, hide_table,
+    // ---- tail (latency-bound) on the tail stream, overlapping the caller's next MSM
+    HALO_HIP(hipEventRecord(M.acc_done, s));
+    HALO_HIP(hipStreamWaitEvent(ts, M.acc_done, 0));
+    if (n > 0) {
+        hipLaunchKernelGGL(k_seg<Cv>, dim3(grid_for((size_t)SW * nseg, 64)), dim3(64), 0, ts,
+                           M.bucket_sums.as<const uint4>(), B, L, SW, M.seg_acc.as<uint4>(), M.seg_sum.as<uint4>());
+        hipLaunchKernelGGL(k_bitsums<Cv>, dim3(nbits + 1, SW), dim3(256), 0, ts, M.seg_acc.as<const uint4>(),
+                           M.seg_sum.as<const uint4>(), nseg, nbits, M.bits.as<uint4>());
+        hipLaunchKernelGGL(k_bitcombine<Cv>, dim3(SW), dim3(64), 0, ts, M.bits.as<const uint4>(), nbits, logL,
+                           M.window_sums.as<uint4>());
+    }
+    hipLaunchKernelGGL(k_final<Cv>, dim3(1), dim3(320), 0, ts, M.window_sums.as<const uint4>(), SW, c, hide_table,
                        hide_scalar, d_out_wrapped);
     HALO_HIP(hipGetLastError());
+    HALO_HIP(hipEventRecord(M.tail_done, ts));
+    M.tail_pending = true;
+    if (!async) HALO_HIP(hipStreamWaitEvent(s, M.tail_done, 0));
+    return HALO_OK;
+}
+
+// Conversion buffer of the scratch set the next MSM will use (for caller-supplied ark bases).
+DevBuf& msm_next_conv_buffer(DeviceState* st) {
+    MsmPipe& PP = g_msm_pipe[st->device & 63];
+    return PP.set[PP.next].conv;
+}
+
+// Makes `s` wait (device-side) for every MSM tail still in flight on this device.
+int msm_join(DeviceState* st, hipStream_t s) {
+    MsmPipe& PP = g_msm_pipe[st->device & 63];
+    for (auto& m : PP.set)
+        if (m.tail_pending) HALO_HIP(hipStreamWaitEvent(s, m.tail_done, 0));
     return HALO_OK;
 }
 
 int msm_device(DeviceState* st, int curve, const void* bases_int, const void* scalars_ark, size_t n,
-               const void* hide_table, const void* hide_scalar, void* d_out_wrapped, hipStream_t s) {
+               const void* hide_table, const void* hide_scalar, void* d_out_wrapped, hipStream_t s, bool async) {
     int rc;
     DISPATCH_CURVE(curve, Cv, {
         rc = msm_device_t<Cv>(st, (const uint4*)bases_int, false, 0, (const uint4*)scalars_ark, n, 0,
-                              (const uint4*)hide_table, (const uint4*)hide_scalar, (uint4*)d_out_wrapped, s);
+                              (const uint4*)hide_table, (const uint4*)hide_scalar, (uint4*)d_out_wrapped, s, async);
     });
     return rc;
 }
 
 // MSM over the resident SRS prefix Gs[0..n): uses the window-shifted copies when present.
 int msm_srs_device(DeviceState* st, int curve, const void* scalars_ark, size_t n, const void* hide_scalar,
-                   void* d_out_wrapped, hipStream_t s) {
+                   void* d_out_wrapped, hipStream_t s, bool async) {
     SrsState& srs = st->srs[curve];
     if (n > srs.n) return set_error(HALO_ESRSRANGE, "n (%zu) exceeds the resident SRS length (%zu)", n, srs.n);
     const void* table = hide_scalar ? srs.s_table.ptr : nullptr;
@@ -599,7 +647,7 @@ int msm_srs_device(DeviceState* st, int curve, const void* scalars_ark, size_t n
     DISPATCH_CURVE(curve, Cv, {
         rc = msm_device_t<Cv>(st, use_shifted ? srs.shifted.as<const uint4>() : srs.gs.as<const uint4>(), use_shifted,
                               srs.n, (const uint4*)scalars_ark, n, use_shifted ? srs.shifted_c : 0, (const uint4*)table,
-                              (const uint4*)hide_scalar, (uint4*)d_out_wrapped, s);
+                              (const uint4*)hide_scalar, (uint4*)d_out_wrapped, s, async);
     });
     return rc;
 }
@@ -703,6 +751,20 @@ extern "C" int halo_point_sum(halo_curve_t curve, const halo_wrapped_point_t* pt
     });
     HALO_HIP(hipGetLastError());
     return copy_d2h(out, buf, 64, s);
+}
+
+extern "C" int halo_point_sum_dev(halo_curve_t curve, const void* d_pts, size_t k, size_t stride_bytes, void* d_out,
+                                  void* stream) {
+    clear_error();
+    HALO_CHECK(check_curve(curve));
+    if (!d_out || (k && !d_pts)) return set_error(HALO_EINVAL, "halo_point_sum_dev: null buffer");
+    if (stride_bytes != 64) return set_error(HALO_EINVAL, "halo_point_sum_dev: only contiguous (64-B stride) points");
+    hipStream_t s = (hipStream_t)stream;
+    DISPATCH_CURVE(curve, Cv, {
+        hipLaunchKernelGGL(k_point_sum<Cv>, dim3(1), dim3(256), 0, s, (const uint4*)d_pts, k, (uint4*)d_out);
+    });
+    HALO_HIP(hipGetLastError());
+    return HALO_OK;
 }
 
 extern "C" int halo_srs_read(halo_curve_t curve, size_t offset, size_t n, halo_wrapped_point_t* out) {
@@ -852,6 +914,30 @@ extern "C" int halo_msm_dev(halo_curve_t curve, const void* d_bases, const void*
         HALO_CHECK(msm_device(st, curve, st->scratch[6].ptr, d_scalars, n, nullptr, nullptr, st->scratch[7].ptr, s));
     }
     return copy_d2h(out, st->scratch[7].ptr, 64, s);
+}
+
+extern "C" int halo_msm_dev_async(halo_curve_t curve, const void* d_bases, const void* d_scalars, size_t n,
+                                  void* d_out, void* stream) {
+    clear_error();
+    HALO_CHECK(check_curve(curve));
+    if (!d_out || (n && !d_scalars)) return set_error(HALO_EINVAL, "halo_msm_dev_async: null buffer");
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    hipStream_t s = (hipStream_t)stream;
+    if (!d_bases) return msm_srs_device(st, curve, d_scalars, n, nullptr, d_out, s, true);
+    DevBuf& conv = msm_next_conv_buffer(st);
+    HALO_CHECK(conv.reserve(std::max<size_t>(n, 1) * 64));
+    HALO_CHECK(convert_wrapped_to_internal(curve, d_bases, conv.ptr, n, s));
+    return msm_device(st, curve, conv.ptr, d_scalars, n, nullptr, nullptr, d_out, s, true);
+}
+
+extern "C" int halo_msm_join(void* stream) {
+    clear_error();
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    return msm_join(st, (hipStream_t)stream);
 }
 
 // pedersen::commit(w, Gs, ms) -- crates/accumulation/src/pedersen.rs:7-27

@@ -9,11 +9,14 @@ int msm_window_bits(size_t n);
 // Writes one ark WrappedPoint (64 B) to d_out_wrapped (device).  Optional hiding term
 // hide_scalar * P where hide_table = {2^i P : i < 256} (internal affine; both device pointers).
 int msm_device(DeviceState* st, int curve, const void* bases_int, const void* scalars_ark, size_t n,
-               const void* hide_table, const void* hide_scalar, void* d_out_wrapped, hipStream_t s);
+               const void* hide_table, const void* hide_scalar, void* d_out_wrapped, hipStream_t s,
+               bool async = false);
+// Makes stream s wait for every MSM reduction tail still in flight (async MSMs).
+int msm_join(DeviceState* st, hipStream_t s);
 // MSM over the resident SRS prefix (window-shifted copies when precomputed); optional hiding
 // scalar (ark, device pointer) times S.
 int msm_srs_device(DeviceState* st, int curve, const void* scalars_ark, size_t n, const void* hide_scalar,
-                   void* d_out_wrapped, hipStream_t s);
+                   void* d_out_wrapped, hipStream_t s, bool async = false);
 int srs_precompute_windows(DeviceState* st, int curve, hipStream_t s);
 int convert_wrapped_to_internal(int curve, const void* in, void* out, size_t n, hipStream_t s);
 int convert_internal_to_wrapped(int curve, const void* in, void* out, size_t n, hipStream_t s);

@@ -111,9 +111,20 @@ int halo_pcdl_commit(halo_curve_t curve, const halo_fe_t* coeffs, size_t len, si
  * d_scalars (n halo_fe_t) in HBM; result written to host `out`.  Synchronous on `stream`. */
 int halo_msm_dev(halo_curve_t curve, const void* d_bases, const void* d_scalars, size_t n,
                  halo_wrapped_point_t* out, void* stream);
+/* Asynchronous device MSM for batches of commitments: enqueues the MSM on `stream` and returns;
+ * the 64-B result lands in device memory d_out.  Consecutive calls pipeline: the reduction tail
+ * of MSM k overlaps the accumulation of MSM k+1 (two scratch sets, a per-device tail stream).
+ * Buffers must stay valid until halo_msm_join(stream) has been ordered before their reuse. */
+int halo_msm_dev_async(halo_curve_t curve, const void* d_bases, const void* d_scalars, size_t n,
+                       void* d_out, void* stream);
+/* Makes `stream` wait (device-side, no host sync) for every asynchronous MSM still in flight. */
+int halo_msm_join(void* stream);
 /* Sum of k points (host arrays) on the device: the combine step after an RCCL all-gather of
  * per-rank partial MSMs (RCCL has no elliptic-curve reduction operator). */
 int halo_point_sum(halo_curve_t curve, const halo_wrapped_point_t* pts, size_t k, halo_wrapped_point_t* out);
+/* Device variant: k WrappedPoints at d_pts (stride_bytes = 64) summed into d_out, on `stream`. */
+int halo_point_sum_dev(halo_curve_t curve, const void* d_pts, size_t k, size_t stride_bytes, void* d_out,
+                       void* stream);
 /* Window size the device MSM uses for n points. */
 int halo_msm_window_bits(size_t n);
 
