@@ -73,19 +73,21 @@ HALO_DEV Affine<F> aff_neg(const Affine<F>& a) {
     return r;
 }
 
-// dbl-2008-s-1 (a = 0): 2M + 4S ... (U=2Y, V=U^2, W=U*V, S=X*V, M=3X^2)
+// dbl-2008-s-1 (a = 0): U = 2Y, V = U^2, W = U V, S = X V, M = 3 X^2,
+// X3 = M^2 - 2S, Y3 = M (S - X3) - W Y, ZZ3 = V ZZ, ZZZ3 = W ZZZ.
+// Intermediates that only feed multiplications are left lazily reduced (fields.hpp).
 template <class F>
 HALO_DEV XYZZ<F> xyzz_dbl(const XYZZ<F>& p) {
     if (xyzz_is_id(p)) return p;
-    const Fe<F> U = fe_dbl(p.Y);
+    const Fe<F> U = fe_add_nc(p.Y, p.Y);
     const Fe<F> V = fe_sqr(U);
     const Fe<F> W = fe_mul(U, V);
     const Fe<F> S = fe_mul(p.X, V);
     const Fe<F> X2 = fe_sqr(p.X);
-    const Fe<F> M = fe_add(fe_dbl(X2), X2);
+    const Fe<F> M = fe_norm(fe_add_nc(X2, fe_add_nc(X2, X2)));  // < 6p
     XYZZ<F> r;
-    r.X = fe_sub(fe_sqr(M), fe_dbl(S));
-    r.Y = fe_sub(fe_mul(M, fe_sub(S, r.X)), fe_mul(W, p.Y));
+    r.X = fe_reduce_8p(fe_sub_k<4>(fe_sqr(M), fe_add_nc(S, S)));
+    r.Y = fe_sub(fe_mul(M, fe_sub_k<2>(S, r.X)), fe_mul(W, p.Y));
     r.ZZ = fe_mul(V, p.ZZ);
     r.ZZZ = fe_mul(W, p.ZZZ);
     return r;
@@ -94,40 +96,42 @@ HALO_DEV XYZZ<F> xyzz_dbl(const XYZZ<F>& p) {
 // Doubling of an affine point into XYZZ (mdbl-2008-s-1)
 template <class F>
 HALO_DEV XYZZ<F> xyzz_mdbl(const Affine<F>& a) {
-    const Fe<F> U = fe_dbl(a.y);
+    const Fe<F> U = fe_add_nc(a.y, a.y);
     const Fe<F> V = fe_sqr(U);
     const Fe<F> W = fe_mul(U, V);
     const Fe<F> S = fe_mul(a.x, V);
     const Fe<F> X2 = fe_sqr(a.x);
-    const Fe<F> M = fe_add(fe_dbl(X2), X2);
+    const Fe<F> M = fe_norm(fe_add_nc(X2, fe_add_nc(X2, X2)));
     XYZZ<F> r;
-    r.X = fe_sub(fe_sqr(M), fe_dbl(S));
-    r.Y = fe_sub(fe_mul(M, fe_sub(S, r.X)), fe_mul(W, a.y));
+    r.X = fe_reduce_8p(fe_sub_k<4>(fe_sqr(M), fe_add_nc(S, S)));
+    r.Y = fe_sub(fe_mul(M, fe_sub_k<2>(S, r.X)), fe_mul(W, a.y));
     r.ZZ = V;
     r.ZZZ = W;
     return r;
 }
 
 // Mixed addition p + q (madd-2008-s), handles identity and the doubling / inverse cases.
+// P = U2 - X1 == 0 is detected through ZZ3 = ZZ1 P^2 == 0 (ZZ1 != 0 here), off the common path.
 template <class F>
 HALO_DEV XYZZ<F> xyzz_madd(const XYZZ<F>& p, const Affine<F>& q) {
     if (aff_is_id(q)) return p;
     if (xyzz_is_id(p)) return xyzz_from_aff(q);
     const Fe<F> U2 = fe_mul(q.x, p.ZZ);
     const Fe<F> S2 = fe_mul(q.y, p.ZZZ);
-    const Fe<F> P = fe_sub(U2, p.X);
-    const Fe<F> R = fe_sub(S2, p.Y);
-    if (fe_is_zero(P)) {
-        if (fe_is_zero(R)) return xyzz_mdbl(q);
+    const Fe<F> P = fe_sub_k<2>(U2, p.X);  // < 4p
+    const Fe<F> R = fe_sub_k<2>(S2, p.Y);  // < 4p
+    const Fe<F> PP = fe_sqr(P);
+    const Fe<F> ZZ3 = fe_mul(p.ZZ, PP);
+    if (fe_is_zero(ZZ3)) {
+        if (fe_is_zero_4p(R)) return xyzz_mdbl(q);
         return xyzz_id<F>();
     }
-    const Fe<F> PP = fe_sqr(P);
     const Fe<F> PPP = fe_mul(P, PP);
     const Fe<F> Q = fe_mul(p.X, PP);
     XYZZ<F> r;
-    r.X = fe_sub(fe_sub(fe_sqr(R), PPP), fe_dbl(Q));
-    r.Y = fe_sub(fe_mul(R, fe_sub(Q, r.X)), fe_mul(p.Y, PPP));
-    r.ZZ = fe_mul(p.ZZ, PP);
+    r.X = fe_reduce_8p(fe_sub_k<6>(fe_sqr(R), fe_add_nc(PPP, fe_add_nc(Q, Q))));
+    r.Y = fe_sub(fe_mul(R, fe_sub_k<2>(Q, r.X)), fe_mul(p.Y, PPP));
+    r.ZZ = ZZ3;
     r.ZZZ = fe_mul(p.ZZZ, PPP);
     return r;
 }
@@ -141,19 +145,20 @@ HALO_DEV XYZZ<F> xyzz_add(const XYZZ<F>& p, const XYZZ<F>& q) {
     const Fe<F> U2 = fe_mul(q.X, p.ZZ);
     const Fe<F> S1 = fe_mul(p.Y, q.ZZZ);
     const Fe<F> S2 = fe_mul(q.Y, p.ZZZ);
-    const Fe<F> P = fe_sub(U2, U1);
-    const Fe<F> R = fe_sub(S2, S1);
-    if (fe_is_zero(P)) {
-        if (fe_is_zero(R)) return xyzz_dbl(p);
+    const Fe<F> P = fe_sub_k<2>(U2, U1);
+    const Fe<F> R = fe_sub_k<2>(S2, S1);
+    const Fe<F> PP = fe_sqr(P);
+    const Fe<F> ZZ3 = fe_mul(fe_mul(p.ZZ, q.ZZ), PP);
+    if (fe_is_zero(ZZ3)) {
+        if (fe_is_zero_4p(R)) return xyzz_dbl(p);
         return xyzz_id<F>();
     }
-    const Fe<F> PP = fe_sqr(P);
     const Fe<F> PPP = fe_mul(P, PP);
     const Fe<F> Q = fe_mul(U1, PP);
     XYZZ<F> r;
-    r.X = fe_sub(fe_sub(fe_sqr(R), PPP), fe_dbl(Q));
-    r.Y = fe_sub(fe_mul(R, fe_sub(Q, r.X)), fe_mul(S1, PPP));
-    r.ZZ = fe_mul(fe_mul(p.ZZ, q.ZZ), PP);
+    r.X = fe_reduce_8p(fe_sub_k<6>(fe_sqr(R), fe_add_nc(PPP, fe_add_nc(Q, Q))));
+    r.Y = fe_sub(fe_mul(R, fe_sub_k<2>(Q, r.X)), fe_mul(S1, PPP));
+    r.ZZ = ZZ3;
     r.ZZZ = fe_mul(fe_mul(p.ZZZ, q.ZZZ), PPP);
     return r;
 }

@@ -236,6 +236,72 @@ HALO_DEV Fe<C> fe_dbl(const Fe<C>& a) {
     return fe_add(a, a);
 }
 
+// ---- lazy ("loose") operations: results are valid Montgomery-multiplication inputs (value < 8p,
+// limbs < 2^30) but not reduced below 2p.  See DESIGN.md §3 for the bounds.
+
+// a + b without carry propagation (a, b normalized, < 2p): limbs < 2^30, value < 4p.
+template <class C>
+HALO_DEV Fe<C> fe_add_nc(const Fe<C>& a, const Fe<C>& b) {
+    Fe<C> r;
+#pragma unroll
+    for (int i = 0; i < NLIMB; i++) r.v[i] = a.v[i] + b.v[i];
+    return r;
+}
+
+// a - b + K p with signed carry propagation: a normalized (< 2p), b with limbs < 2^31 and b < K p;
+// result normalized, in (0, 2p + K p).  K in {2, 4, 6, 8}.
+template <int K, class C>
+HALO_DEV Fe<C> fe_sub_k(const Fe<C>& a, const Fe<C>& b) {
+    const uint32_t* kp = (K == 2) ? C::P2 : (K == 4) ? C::P4 : (K == 6) ? C::P6 : C::P8;
+    Fe<C> s;
+    int32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < NLIMB; i++) {
+        int32_t x = (int32_t)a.v[i] - (int32_t)b.v[i] + (int32_t)kp[i] + c;
+        s.v[i] = (i == NLIMB - 1) ? (uint32_t)x : ((uint32_t)x & LIMB_MASK);
+        c = x >> LIMB_BITS;
+    }
+    return s;
+}
+
+// carry-normalize limbs (value unchanged); input limbs < 2^31
+template <class C>
+HALO_DEV Fe<C> fe_norm(const Fe<C>& a) {
+    Fe<C> r;
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < NLIMB; i++) {
+        const uint32_t x = a.v[i] + c;
+        r.v[i] = (i == NLIMB - 1) ? x : (x & LIMB_MASK);
+        c = x >> LIMB_BITS;
+    }
+    return r;
+}
+
+// x < 8p (normalized) -> x < 2p
+template <class C>
+HALO_DEV Fe<C> fe_reduce_8p(const Fe<C>& x) {
+    Fe<C> t;
+    int32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < NLIMB; i++) {
+        int32_t d = (int32_t)x.v[i] - (int32_t)C::P4[i] + c;
+        t.v[i] = (uint32_t)d & LIMB_MASK;
+        c = d >> LIMB_BITS;
+    }
+    const bool ge = (c >= 0);
+    Fe<C> r;
+#pragma unroll
+    for (int i = 0; i < NLIMB; i++) r.v[i] = ge ? t.v[i] : x.v[i];
+    return fe_reduce_2p(r);
+}
+
+// x == 0 (mod p) for a normalized x < 4p
+template <class C>
+HALO_DEV bool fe_is_zero_4p(const Fe<C>& x) {
+    return fe_is_zero(fe_reduce_2p(x));
+}
+
 // Canonical representative in [0, p)
 template <class C>
 HALO_DEV Fe<C> fe_canon(const Fe<C>& x) {

@@ -279,7 +279,7 @@ __global__ void k_tasks(const uint32_t* bstart, const uint32_t* task_off, size_t
 }
 
 template <class Cv>
-__global__ __launch_bounds__(256) void k_acc(const Task* tasks, const uint32_t* ntasks_total, const uint32_t* sorted,
+__global__ __launch_bounds__(256, 4) void k_acc(const Task* tasks, const uint32_t* ntasks_total, const uint32_t* sorted,
                                              const uint4* bases, uint32_t n_per_window, size_t stride,
                                              uint4* partials) {
     using F = typename Cv::Base;
