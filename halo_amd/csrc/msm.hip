@@ -7,8 +7,8 @@
 // Pipeline (all on the device, no host round trip):
 //   1. digits   : scalar (ark Montgomery) -> canonical -> W signed c-bit digits
 //                 (|d| <= 2^(c-1), W = ceil(256 / c)); key = (window, |d| - 1), value = index|sign.
-//   2. sort     : counting sort of the W*n (key, value) pairs by key: per-chunk LDS histograms,
-//                 column prefix, global exclusive scan (bucket starts), LDS-ranked scatter.
+//   2. sort     : stable LSD radix sort (8-bit digits, LDS-staged coalesced runs; sort.hip) of the
+//                 W*n (bucket key, point ref) pairs; bucket starts from the sorted keys.
 //   3. tasks    : every bucket is cut into tasks of <= K entries (skew-proof: an all-equal scalar
 //                 vector becomes n/K equal tasks instead of one serial bucket).
 //   4. acc      : one thread per task sums its points with XYZZ mixed additions (8M + 2S).
@@ -21,14 +21,13 @@
 #include "dispatch.hpp"
 #include "msm.hpp"
 #include "runtime.hpp"
+#include "sort.hpp"
 
 namespace halo {
 
 constexpr uint32_t DIGIT_NONE = 0xffffffffu;
 constexpr int MSM_TASK_K = 64;   // max entries per accumulation task
 constexpr int MSM_SEG_L = 32;    // buckets per reduction segment
-constexpr int HIST_THREADS = 1024;
-constexpr int SCAN_THREADS = 1024;
 
 // ---------------------------------------------------------------------------------------------
 // synthetic bases / scalars (shared host/device definition)
@@ -113,145 +112,6 @@ __global__ void k_digits(const uint4* scalars, size_t n, int c, int W, uint32_t*
             out = (v == 0) ? DIGIT_NONE : (v - 1);
         }
         digits[(size_t)w * n + i] = out;
-    }
-}
-
-// ---------------------------------------------------------------------------------------------
-// 2. counting sort
-// ---------------------------------------------------------------------------------------------
-// grid (chunks, W); hist[(w * chunks + chunk) * B + b]
-__global__ __launch_bounds__(HIST_THREADS) void k_hist(const uint32_t* digits, size_t n, uint32_t B, int chunks,
-                                                       uint32_t* hist) {
-    extern __shared__ uint32_t cnt[];
-    const int chunk = blockIdx.x, w = blockIdx.y;
-    for (uint32_t b = threadIdx.x; b < B; b += HIST_THREADS) cnt[b] = 0;
-    __syncthreads();
-    const size_t per = (n + chunks - 1) / chunks;
-    const size_t beg = (size_t)chunk * per, end = min(n, beg + per);
-    const uint32_t* d = digits + (size_t)w * n;
-    for (size_t i = beg + threadIdx.x; i < end; i += HIST_THREADS) {
-        const uint32_t v = d[i];
-        if (v != DIGIT_NONE) atomicAdd(&cnt[v & 0x7fffffffu], 1u);
-    }
-    __syncthreads();
-    uint32_t* h = hist + ((size_t)w * chunks + chunk) * B;
-    for (uint32_t b = threadIdx.x; b < B; b += HIST_THREADS) h[b] = cnt[b];
-}
-
-// thread per (w, b): per-chunk exclusive prefix (in place) + totals[w * B + b]
-__global__ void k_colsum(uint32_t* hist, int chunks, uint32_t B, int W, uint32_t* totals) {
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= (size_t)W * B) return;
-    const size_t w = t / B, b = t % B;
-    uint32_t run = 0;
-    for (int c = 0; c < chunks; c++) {
-        uint32_t* p = hist + (w * chunks + c) * B + b;
-        const uint32_t v = *p;
-        *p = run;
-        run += v;
-    }
-    totals[t] = run;
-}
-
-// generic exclusive scan of u32 (3 kernels); out[n] = total
-__global__ __launch_bounds__(SCAN_THREADS) void k_scan_reduce(const uint32_t* in, size_t n, size_t per_block,
-                                                              uint32_t* block_sums) {
-    __shared__ uint32_t s[SCAN_THREADS];
-    const size_t beg = (size_t)blockIdx.x * per_block;
-    const size_t end = min(n, beg + per_block);
-    uint32_t acc = 0;
-    for (size_t i = beg + threadIdx.x; i < end; i += SCAN_THREADS) acc += in[i];
-    s[threadIdx.x] = acc;
-    __syncthreads();
-    for (int off = SCAN_THREADS / 2; off > 0; off >>= 1) {
-        if ((int)threadIdx.x < off) s[threadIdx.x] += s[threadIdx.x + off];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) block_sums[blockIdx.x] = s[0];
-}
-
-__device__ inline uint32_t block_exclusive_scan(uint32_t v, uint32_t* s, uint32_t* total) {
-    // Hillis-Steele over SCAN_THREADS entries
-    s[threadIdx.x] = v;
-    __syncthreads();
-    for (int off = 1; off < SCAN_THREADS; off <<= 1) {
-        uint32_t t = ((int)threadIdx.x >= off) ? s[threadIdx.x - off] : 0;
-        __syncthreads();
-        s[threadIdx.x] += t;
-        __syncthreads();
-    }
-    const uint32_t incl = s[threadIdx.x];
-    *total = s[SCAN_THREADS - 1];
-    __syncthreads();
-    return incl - v;
-}
-
-__global__ __launch_bounds__(SCAN_THREADS) void k_scan_blocksums(uint32_t* block_sums, int nb) {
-    __shared__ uint32_t s[SCAN_THREADS];
-    // nb <= SCAN_THREADS * 8 : each thread scans up to 8 consecutive
-    const int per = (nb + SCAN_THREADS - 1) / SCAN_THREADS;
-    uint32_t loc[8];
-    uint32_t acc = 0;
-    for (int k = 0; k < per; k++) {
-        const int i = threadIdx.x * per + k;
-        loc[k] = (i < nb) ? block_sums[i] : 0;
-        acc += loc[k];
-    }
-    uint32_t tot;
-    uint32_t ex = block_exclusive_scan(acc, s, &tot);
-    for (int k = 0; k < per; k++) {
-        const int i = threadIdx.x * per + k;
-        if (i < nb) block_sums[i] = ex;
-        ex += loc[k];
-    }
-    if (threadIdx.x == 0) block_sums[nb] = tot;
-}
-
-__global__ __launch_bounds__(SCAN_THREADS) void k_scan_apply(const uint32_t* in, size_t n, size_t per_block,
-                                                             const uint32_t* block_sums, uint32_t* out) {
-    __shared__ uint32_t s[SCAN_THREADS];
-    const size_t beg = (size_t)blockIdx.x * per_block;
-    const size_t end = min(n, beg + per_block);
-    uint32_t base = block_sums[blockIdx.x];
-    // process the block range in tiles of SCAN_THREADS * 4 consecutive elements per thread
-    for (size_t tile = beg; tile < end; tile += (size_t)SCAN_THREADS * 4) {
-        uint32_t loc[4];
-        uint32_t acc = 0;
-        for (int k = 0; k < 4; k++) {
-            const size_t i = tile + (size_t)threadIdx.x * 4 + k;
-            loc[k] = (i < end) ? in[i] : 0;
-            acc += loc[k];
-        }
-        uint32_t tot;
-        uint32_t ex = block_exclusive_scan(acc, s, &tot) + base;
-        for (int k = 0; k < 4; k++) {
-            const size_t i = tile + (size_t)threadIdx.x * 4 + k;
-            if (i < end) out[i] = ex;
-            ex += loc[k];
-        }
-        base += tot;
-    }
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) out[n] = block_sums[gridDim.x];
-}
-
-__global__ __launch_bounds__(HIST_THREADS) void k_scatter(const uint32_t* digits, size_t n, uint32_t B, int chunks,
-                                                          const uint32_t* hist_prefix, const uint32_t* bstart,
-                                                          uint32_t* sorted) {
-    extern __shared__ uint32_t cnt[];
-    const int chunk = blockIdx.x, w = blockIdx.y;
-    for (uint32_t b = threadIdx.x; b < B; b += HIST_THREADS) cnt[b] = 0;
-    __syncthreads();
-    const size_t per = (n + chunks - 1) / chunks;
-    const size_t beg = (size_t)chunk * per, end = min(n, beg + per);
-    const uint32_t* d = digits + (size_t)w * n;
-    const uint32_t* hp = hist_prefix + ((size_t)w * chunks + chunk) * B;
-    const uint32_t* bs = bstart + (size_t)w * B;
-    for (size_t i = beg + threadIdx.x; i < end; i += HIST_THREADS) {
-        const uint32_t v = d[i];
-        if (v == DIGIT_NONE) continue;
-        const uint32_t b = v & 0x7fffffffu;
-        const uint32_t r = atomicAdd(&cnt[b], 1u);
-        sorted[bs[b] + hp[b] + r] = (uint32_t)i | (v & 0x80000000u);
     }
 }
 
@@ -472,8 +332,9 @@ int msm_window_bits(size_t n) {
 static unsigned grid_for(size_t n, unsigned thr) { return (unsigned)std::max<size_t>(1, (n + thr - 1) / thr); }
 
 struct MsmScratch {
-    DevBuf digits, hist, totals, bstart, sorted, ntask, task_off, tasks, partials, bucket_sums, seg_acc, seg_sum,
-        bits, window_sums, scan_tmp, conv;
+    DevBuf digits, bstart, ntask, task_off, tasks, partials, bucket_sums, seg_acc, seg_sum, bits, window_sums,
+        scan_tmp, conv;
+    SortScratch sort;
     hipEvent_t acc_done = nullptr, tail_done = nullptr;
     bool tail_pending = false;
 };
@@ -497,22 +358,6 @@ static int pipe_init(MsmPipe& P) {
     return HALO_OK;
 }
 
-static int device_scan(const uint32_t* in, size_t n, uint32_t* out, DevBuf& tmp, hipStream_t s) {
-    // out has n + 1 entries
-    const size_t per_block = (size_t)SCAN_THREADS * 16;
-    size_t nb = (n + per_block - 1) / per_block;
-    if (nb == 0) nb = 1;
-    if (nb > (size_t)SCAN_THREADS * 8) return set_error(HALO_EINVAL, "scan too large (%zu)", n);
-    HALO_CHECK(tmp.reserve((nb + 1) * 4));
-    hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)nb), dim3(SCAN_THREADS), 0, s, in, n, per_block,
-                       tmp.as<uint32_t>());
-    hipLaunchKernelGGL(k_scan_blocksums, dim3(1), dim3(SCAN_THREADS), 0, s, tmp.as<uint32_t>(), (int)nb);
-    hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)nb), dim3(SCAN_THREADS), 0, s, in, n, per_block,
-                       tmp.as<const uint32_t>(), out);
-    HALO_HIP(hipGetLastError());
-    return HALO_OK;
-}
-
 // bases_int: n internal affine points, or (shifted) W * n window-shifted points (single bucket set).
 template <class Cv>
 static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, size_t shift_stride,
@@ -533,16 +378,13 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
     const int SW = shifted ? 1 : W;
     const size_t SN = shifted ? (size_t)W * nn : nn;
     const size_t NB = (size_t)SW * B;
-    const int chunks = (int)std::max<size_t>(1, std::min<size_t>(shifted ? 256 : 32, SN / 4096));
     const uint32_t L = std::min<uint32_t>(MSM_SEG_L, B);
     const uint32_t logL = ilog2(L);
     const uint32_t nseg = B / L;
     const uint32_t nbits = nseg > 1 ? ilog2(nseg - 1) + 1 : 0;
+    const uint32_t key_bits = NB > 1 ? ilog2(NB - 1) + 1 : 1;
     HALO_CHECK(M.digits.reserve((size_t)W * nn * 4));
-    HALO_CHECK(M.hist.reserve((size_t)SW * chunks * B * 4));
-    HALO_CHECK(M.totals.reserve(NB * 4));
     HALO_CHECK(M.bstart.reserve((NB + 1) * 4));
-    HALO_CHECK(M.sorted.reserve((size_t)W * nn * 4));
     HALO_CHECK(M.ntask.reserve(NB * 4));
     HALO_CHECK(M.task_off.reserve((NB + 1) * 4));
     const size_t max_tasks = NB + (size_t)W * nn / MSM_TASK_K + 1;
@@ -554,35 +396,24 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
     HALO_CHECK(M.bits.reserve((size_t)SW * (nbits + 1) * 128));
     HALO_CHECK(M.window_sums.reserve((size_t)W * 128));
 
-    static bool attrs_set = false;
-    if (!attrs_set) {
-        HALO_HIP(hipFuncSetAttribute((const void*)k_hist, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        HALO_HIP(hipFuncSetAttribute((const void*)k_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        attrs_set = true;
-    }
     if (n > 0) {
         hipLaunchKernelGGL(k_digits<typename Cv::Scalar>, dim3(grid_for(n, 256)), dim3(256), 0, s, scalars_ark, n, c,
                            W, M.digits.as<uint32_t>());
-        hipLaunchKernelGGL(k_hist, dim3(chunks, SW), dim3(HIST_THREADS), B * 4, s, M.digits.as<const uint32_t>(), SN,
-                           B, chunks, M.hist.as<uint32_t>());
-        hipLaunchKernelGGL(k_colsum, dim3(grid_for(NB, 256)), dim3(256), 0, s, M.hist.as<uint32_t>(), chunks, B, SW,
-                           M.totals.as<uint32_t>());
         HALO_HIP(hipGetLastError());
-        HALO_CHECK(device_scan(M.totals.as<const uint32_t>(), NB, M.bstart.as<uint32_t>(), M.scan_tmp, s));
-        hipLaunchKernelGGL(k_scatter, dim3(chunks, SW), dim3(HIST_THREADS), B * 4, s, M.digits.as<const uint32_t>(),
-                           SN, B, chunks, M.hist.as<const uint32_t>(), M.bstart.as<const uint32_t>(),
-                           M.sorted.as<uint32_t>());
+        uint32_t *skeys = nullptr, *svals = nullptr;
+        const uint32_t* scount = nullptr;
+        HALO_CHECK(msm_radix_sort(M.digits.as<const uint32_t>(), (size_t)W * nn, SN, B, key_bits, M.sort, &skeys,
+                                  &svals, &scount, M.bstart.as<uint32_t>(), NB, s));
         hipLaunchKernelGGL(k_ntask, dim3(grid_for(NB, 256)), dim3(256), 0, s, M.bstart.as<const uint32_t>(), NB,
                            M.ntask.as<uint32_t>());
         HALO_HIP(hipGetLastError());
-        HALO_CHECK(device_scan(M.ntask.as<const uint32_t>(), NB, M.task_off.as<uint32_t>(), M.scan_tmp, s));
+        HALO_CHECK(device_exclusive_scan(M.ntask.as<const uint32_t>(), NB, M.task_off.as<uint32_t>(), M.scan_tmp, s));
         hipLaunchKernelGGL(k_tasks, dim3(grid_for(NB, 256)), dim3(256), 0, s, M.bstart.as<const uint32_t>(),
                            M.task_off.as<const uint32_t>(), NB, M.tasks.as<Task>());
         ProfScope prof("msm_acc", s);
         HALO_LAUNCH(prof, k_acc<Cv>, dim3(grid_for(max_tasks, 256)), dim3(256), 0, s, M.tasks.as<const Task>(),
-                           M.task_off.as<const uint32_t>() + NB, M.sorted.as<const uint32_t>(), bases_int,
-                           (uint32_t)nn, (shifted && shift_stride != nn) ? shift_stride : (size_t)0,
-                           M.partials.as<uint4>());
+                    M.task_off.as<const uint32_t>() + NB, (const uint32_t*)svals, bases_int, (uint32_t)nn,
+                    (shifted && shift_stride != nn) ? shift_stride : (size_t)0, M.partials.as<uint4>());
         hipLaunchKernelGGL(k_merge<Cv>, dim3(grid_for(NB, 256)), dim3(256), 0, s, M.task_off.as<const uint32_t>(), NB,
                            M.partials.as<const uint4>(), M.bucket_sums.as<uint4>());
         HALO_HIP(hipGetLastError());

@@ -1,0 +1,327 @@
+// Stable LSD radix sort of the MSM's (bucket key, point reference) pairs (part of SURVEY §8 row a3).
+//
+// ark-ec's CPU Pippenger scatters every point straight into its bucket (a random read-modify-write
+// per point per window).  On MI355X the buckets are instead formed by sorting the W*n digit entries
+// by bucket key, so the accumulation kernel reads each bucket's points as one contiguous run.
+//
+// Design (per 8-bit digit pass, tiles of 4096 entries, 256 threads):
+//   k_rs_hist    : per-tile LDS histogram of the digit -> hist[digit * ntiles + tile]
+//   scan         : exclusive scan of hist (digit-major) -> every tile's global run start per digit
+//   k_rs_scatter : stable in-tile ranking (each wave ranks its own contiguous quarter of the tile with
+//                  ballots that find equal digits among lanes; per-wave histograms order the waves),
+//                  the tile is staged in LDS in digit order and written back as contiguous runs per
+//                  digit (coalesced).
+// Pass 0 reads the raw digit array (skipping zero digits) and forms key = window * B + |d| - 1 and
+// value = point index | sign; later passes read the previous pass's pairs.  The number of valid
+// entries is known only on the device (scan total) -- kernels bound themselves by it, so no host
+// round trip is needed.
+#include <algorithm>
+
+#include "fields.hpp"
+#include "runtime.hpp"
+#include "sort.hpp"
+
+namespace halo {
+
+constexpr int RS_THREADS = 256;
+constexpr int RS_ROUNDS = 16;
+constexpr int RS_TILE = RS_THREADS * RS_ROUNDS;  // 4096
+constexpr int RS_BINS = 256;
+constexpr uint32_t RS_NONE = 0xffffffffu;
+
+struct RsIn {
+    const uint32_t* digits;  // pass 0 only
+    const uint32_t* keys;    // later passes
+    const uint32_t* vals;
+    const uint32_t* count;   // device count of valid entries (later passes)
+    size_t E;                // pass 0: number of digit entries
+    size_t npw;              // pass 0: entries per window (key = (e / npw) * B + |d| - 1)
+    uint32_t B;
+    uint32_t pass;
+    uint32_t shift;  // digit = (key >> shift) & 255
+};
+
+// entry e of the pass input -> (key, val) or invalid
+HALO_DEV bool rs_fetch(const RsIn& in, size_t e, size_t limit, uint32_t& key, uint32_t& val) {
+    if (e >= limit) return false;
+    if (in.pass == 0) {
+        const uint32_t d = in.digits[e];
+        if (d == RS_NONE) return false;
+        // entries < 2^32; one window (npw >= E) needs no division
+        const uint32_t w = (in.npw >= in.E) ? 0u : (uint32_t)e / (uint32_t)in.npw;
+        key = w * in.B + (d & 0x7fffffffu);
+        val = ((uint32_t)e - w * (uint32_t)in.npw) | (d & 0x80000000u);
+        return true;
+    }
+    key = in.keys[e];
+    val = in.vals[e];
+    return true;
+}
+
+HALO_DEV size_t rs_limit(const RsIn& in) { return in.pass == 0 ? in.E : (size_t)*in.count; }
+
+__global__ __launch_bounds__(RS_THREADS) void k_rs_hist(RsIn in, uint32_t ntiles, uint32_t* hist) {
+    __shared__ uint32_t h[RS_BINS];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const size_t limit = rs_limit(in);
+    const size_t base = (size_t)blockIdx.x * RS_TILE;
+    for (int r = 0; r < RS_ROUNDS; r++) {
+        uint32_t k, v;
+        if (rs_fetch(in, base + (size_t)r * RS_THREADS + threadIdx.x, limit, k, v))
+            atomicAdd(&h[(k >> in.shift) & 255u], 1u);
+    }
+    __syncthreads();
+    hist[(size_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
+}
+
+// Each wave owns a contiguous quarter of the tile (1024 entries, 16 rounds of 64), so ranking is
+// wave-local (ballots + a wave-private LDS run counter per digit) and the workgroup needs only
+// three barriers: after the per-wave histograms, after the prefix, after staging.
+__global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(RsIn in, uint32_t ntiles, const uint32_t* offsets,
+                                                           uint32_t* keys_out, uint32_t* vals_out) {
+    constexpr int WAVES = RS_THREADS / 64;
+    constexpr int PER_WAVE = RS_TILE / WAVES;  // 1024
+    __shared__ uint32_t goff[RS_BINS];           // global start of this tile's run per digit
+    __shared__ uint32_t lstart[RS_BINS];         // tile-local start per digit
+    __shared__ uint32_t wpos[WAVES][RS_BINS];    // per-wave histogram, then per-wave next position
+    __shared__ uint32_t skey[RS_TILE], sval[RS_TILE];
+    __shared__ uint32_t total;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const size_t limit = rs_limit(in);
+    const size_t wbase = (size_t)blockIdx.x * RS_TILE + (size_t)wave * PER_WAVE;
+    constexpr int R = PER_WAVE / 64;
+    uint32_t K[R], V[R];
+    uint32_t validmask = 0;
+    // all loads of the tile issued back to back (memory-level parallelism), kept in registers
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        K[r] = 0;
+        V[r] = 0;
+        if (rs_fetch(in, wbase + (size_t)r * 64 + lane, limit, K[r], V[r])) validmask |= 1u << r;
+    }
+    goff[tid] = offsets[(size_t)tid * ntiles + blockIdx.x];
+#pragma unroll
+    for (int w = 0; w < WAVES; w++) wpos[w][tid] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < R; r++)
+        if ((validmask >> r) & 1u) atomicAdd(&wpos[wave][(K[r] >> in.shift) & 255u], 1u);
+    __syncthreads();
+    // thread tid = digit: tile-local exclusive prefix over digits (wave-0 shuffle scan of 4 digits/lane)
+    {
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int w = 0; w < WAVES; w++) cnt += wpos[w][tid];
+        lstart[tid] = cnt;
+    }
+    __syncthreads();
+    if (wave == 0) {
+        uint32_t c[4];
+        uint32_t sum = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            c[q] = lstart[lane * 4 + q];
+            sum += c[q];
+        }
+        uint32_t incl = sum;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t t = __shfl_up(incl, off);
+            if (lane >= off) incl += t;
+        }
+        uint32_t ex = incl - sum;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            lstart[lane * 4 + q] = ex;
+            ex += c[q];
+        }
+        if (lane == 63) total = incl;
+    }
+    __syncthreads();
+    {
+        uint32_t p = lstart[tid];
+#pragma unroll
+        for (int w = 0; w < WAVES; w++) {
+            const uint32_t c = wpos[w][tid];
+            wpos[w][tid] = p;
+            p += c;
+        }
+    }
+    __syncthreads();
+    // stable, wave-local ranking: 16 rounds of 64 consecutive entries
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const uint32_t k = K[r], v = V[r];
+        const bool valid = (validmask >> r) & 1u;
+        const uint32_t dg = (k >> in.shift) & 255u;
+        uint64_t same = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; b++) {
+            const uint64_t m = __ballot((dg >> b) & 1u);
+            same &= ((dg >> b) & 1u) ? m : ~m;
+        }
+        const uint64_t below = same & ((1ull << lane) - 1ull);
+        if (valid) {
+            const uint32_t pos = wpos[wave][dg] + (uint32_t)__popcll(below);
+            skey[pos] = k;
+            sval[pos] = v;
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (valid && below == 0) wpos[wave][dg] += (uint32_t)__popcll(same);
+        __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    // write runs: staging index i belongs to digit dg, global position goff[dg] + (i - lstart[dg])
+    for (uint32_t i = tid; i < total; i += RS_THREADS) {
+        const uint32_t k = skey[i];
+        const uint32_t dg = (k >> in.shift) & 255u;
+        const uint32_t g = goff[dg] + (i - lstart[dg]);
+        keys_out[g] = k;
+        vals_out[g] = sval[i];
+    }
+}
+
+// bstart[b] = first position of key b in the sorted keys (b <= NB; bstart[NB] = count)
+__global__ void k_bucket_starts(const uint32_t* keys, const uint32_t* count, size_t NB, size_t cap, uint32_t* bstart) {
+    const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t n = *count;
+    if (e > n || e > cap) return;
+    const int64_t prev = (e == 0) ? -1 : (int64_t)keys[e - 1];
+    const int64_t cur = (e == n) ? (int64_t)NB : (int64_t)keys[e];
+    for (int64_t b = prev + 1; b <= cur; b++) bstart[b] = (uint32_t)e;
+}
+
+// exclusive scan (3 kernels) of n u32 -> out[0..n], out[n] = total
+constexpr int SC_THREADS = 1024;
+__device__ inline uint32_t sc_block_excl(uint32_t v, uint32_t* s, uint32_t* total) {
+    s[threadIdx.x] = v;
+    __syncthreads();
+    for (int off = 1; off < SC_THREADS; off <<= 1) {
+        const uint32_t t = ((int)threadIdx.x >= off) ? s[threadIdx.x - off] : 0;
+        __syncthreads();
+        s[threadIdx.x] += t;
+        __syncthreads();
+    }
+    const uint32_t incl = s[threadIdx.x];
+    *total = s[SC_THREADS - 1];
+    __syncthreads();
+    return incl - v;
+}
+
+__global__ __launch_bounds__(SC_THREADS) void k_sc_reduce(const uint32_t* in, size_t n, size_t per, uint32_t* sums) {
+    __shared__ uint32_t s[SC_THREADS];
+    const size_t beg = (size_t)blockIdx.x * per, end = min(n, beg + per);
+    uint32_t acc = 0;
+    for (size_t i = beg + threadIdx.x; i < end; i += SC_THREADS) acc += in[i];
+    s[threadIdx.x] = acc;
+    __syncthreads();
+    for (int off = SC_THREADS / 2; off > 0; off >>= 1) {
+        if ((int)threadIdx.x < off) s[threadIdx.x] += s[threadIdx.x + off];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) sums[blockIdx.x] = s[0];
+}
+
+__global__ __launch_bounds__(SC_THREADS) void k_sc_sums(uint32_t* sums, int nb) {
+    __shared__ uint32_t s[SC_THREADS];
+    const int per = (nb + SC_THREADS - 1) / SC_THREADS;
+    uint32_t loc[8];
+    uint32_t acc = 0;
+    for (int k = 0; k < per; k++) {
+        const int i = threadIdx.x * per + k;
+        loc[k] = (i < nb) ? sums[i] : 0;
+        acc += loc[k];
+    }
+    uint32_t tot;
+    uint32_t ex = sc_block_excl(acc, s, &tot);
+    for (int k = 0; k < per; k++) {
+        const int i = threadIdx.x * per + k;
+        if (i < nb) sums[i] = ex;
+        ex += loc[k];
+    }
+    if (threadIdx.x == 0) sums[nb] = tot;
+}
+
+__global__ __launch_bounds__(SC_THREADS) void k_sc_apply(const uint32_t* in, size_t n, size_t per, const uint32_t* sums,
+                                                         uint32_t* out) {
+    __shared__ uint32_t s[SC_THREADS];
+    const size_t beg = (size_t)blockIdx.x * per, end = min(n, beg + per);
+    uint32_t base = sums[blockIdx.x];
+    for (size_t tile = beg; tile < end; tile += (size_t)SC_THREADS * 4) {
+        uint32_t loc[4];
+        uint32_t acc = 0;
+        for (int k = 0; k < 4; k++) {
+            const size_t i = tile + (size_t)threadIdx.x * 4 + k;
+            loc[k] = (i < end) ? in[i] : 0;
+            acc += loc[k];
+        }
+        uint32_t tot;
+        uint32_t ex = sc_block_excl(acc, s, &tot) + base;
+        for (int k = 0; k < 4; k++) {
+            const size_t i = tile + (size_t)threadIdx.x * 4 + k;
+            if (i < end) out[i] = ex;
+            ex += loc[k];
+        }
+        base += tot;
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) out[n] = sums[gridDim.x];
+}
+
+int device_exclusive_scan(const uint32_t* in, size_t n, uint32_t* out, DevBuf& tmp, hipStream_t s) {
+    const size_t per = (size_t)SC_THREADS * 16;
+    size_t nb = std::max<size_t>(1, (n + per - 1) / per);
+    if (nb > (size_t)SC_THREADS * 8) return set_error(HALO_EINVAL, "scan too large (%zu)", n);
+    HALO_CHECK(tmp.reserve((nb + 1) * 4));
+    hipLaunchKernelGGL(k_sc_reduce, dim3((unsigned)nb), dim3(SC_THREADS), 0, s, in, n, per, tmp.as<uint32_t>());
+    hipLaunchKernelGGL(k_sc_sums, dim3(1), dim3(SC_THREADS), 0, s, tmp.as<uint32_t>(), (int)nb);
+    hipLaunchKernelGGL(k_sc_apply, dim3((unsigned)nb), dim3(SC_THREADS), 0, s, in, n, per, tmp.as<const uint32_t>(),
+                       out);
+    HALO_HIP(hipGetLastError());
+    return HALO_OK;
+}
+
+int msm_radix_sort(const uint32_t* digits, size_t E, size_t npw, uint32_t B, uint32_t key_bits, SortScratch& S,
+                   uint32_t** keys_out, uint32_t** vals_out, const uint32_t** count_out, uint32_t* bstart, size_t NB,
+                   hipStream_t s) {
+    const uint32_t ntiles = (uint32_t)std::max<size_t>(1, (E + RS_TILE - 1) / RS_TILE);
+    const size_t hn = (size_t)RS_BINS * ntiles;
+    HALO_CHECK(S.keys[0].reserve(std::max<size_t>(E, 1) * 4));
+    HALO_CHECK(S.keys[1].reserve(std::max<size_t>(E, 1) * 4));
+    HALO_CHECK(S.vals[0].reserve(std::max<size_t>(E, 1) * 4));
+    HALO_CHECK(S.vals[1].reserve(std::max<size_t>(E, 1) * 4));
+    HALO_CHECK(S.hist.reserve(hn * 4));
+    HALO_CHECK(S.offs.reserve((hn + 1) * 4));
+    HALO_CHECK(S.count.reserve(16));
+    const uint32_t passes = std::max<uint32_t>(1, (key_bits + 7) / 8);
+    int cur = 0;
+    for (uint32_t p = 0; p < passes; p++) {
+        RsIn in;
+        in.digits = digits;
+        in.keys = S.keys[cur ^ 1].as<const uint32_t>();
+        in.vals = S.vals[cur ^ 1].as<const uint32_t>();
+        in.count = S.count.as<const uint32_t>();
+        in.E = E;
+        in.npw = npw;
+        in.B = B;
+        in.pass = p;
+        in.shift = 8 * p;
+        hipLaunchKernelGGL(k_rs_hist, dim3(ntiles), dim3(RS_THREADS), 0, s, in, ntiles, S.hist.as<uint32_t>());
+        HALO_CHECK(device_exclusive_scan(S.hist.as<const uint32_t>(), hn, S.offs.as<uint32_t>(), S.scan_tmp, s));
+        if (p == 0)  // number of valid (nonzero-digit) entries = scan total
+            HALO_HIP(hipMemcpyAsync(S.count.ptr, S.offs.as<uint32_t>() + hn, 4, hipMemcpyDeviceToDevice, s));
+        hipLaunchKernelGGL(k_rs_scatter, dim3(ntiles), dim3(RS_THREADS), 0, s, in, ntiles, S.offs.as<const uint32_t>(),
+                           S.keys[cur].as<uint32_t>(), S.vals[cur].as<uint32_t>());
+        HALO_HIP(hipGetLastError());
+        cur ^= 1;
+    }
+    *keys_out = S.keys[cur ^ 1].as<uint32_t>();
+    *vals_out = S.vals[cur ^ 1].as<uint32_t>();
+    *count_out = S.count.as<const uint32_t>();
+    hipLaunchKernelGGL(k_bucket_starts, dim3((unsigned)((E + 1 + 255) / 256)), dim3(256), 0, s, *keys_out,
+                       S.count.as<const uint32_t>(), NB, E, bstart);
+    HALO_HIP(hipGetLastError());
+    return HALO_OK;
+}
+
+}  // namespace halo

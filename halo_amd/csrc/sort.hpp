@@ -1,0 +1,21 @@
+// Device radix sort / scan used by the MSM (sort.hip).
+#pragma once
+#include "runtime.hpp"
+
+namespace halo {
+
+struct SortScratch {
+    DevBuf keys[2], vals[2], hist, offs, count, scan_tmp;
+};
+
+// Exclusive scan of n u32 values: out[0..n) exclusive prefix, out[n] = total.
+int device_exclusive_scan(const uint32_t* in, size_t n, uint32_t* out, DevBuf& tmp, hipStream_t s);
+
+// Sorts the MSM digit entries (digits[e], DIGIT_NONE entries dropped) by key =
+// (e / npw) * B + (|d| - 1), stable; values = (e mod npw) | sign.  key_bits = bits of the largest
+// key.  Fills bstart[0..NB] (bucket b's entries are [bstart[b], bstart[b+1]) of the sorted arrays).
+int msm_radix_sort(const uint32_t* digits, size_t E, size_t npw, uint32_t B, uint32_t key_bits, SortScratch& S,
+                   uint32_t** keys_out, uint32_t** vals_out, const uint32_t** count_out, uint32_t* bstart, size_t NB,
+                   hipStream_t s);
+
+}  // namespace halo
