@@ -21,6 +21,6 @@ int srs_precompute_windows(DeviceState* st, int curve, hipStream_t s);
 int convert_wrapped_to_internal(int curve, const void* in, void* out, size_t n, hipStream_t s);
 int convert_internal_to_wrapped(int curve, const void* in, void* out, size_t n, hipStream_t s);
 int ntt_device_dispatch(DeviceState* st, int field, const void* d_in, void* d_out, void* d_tmp, unsigned logn,
-                        size_t batch, int inverse, hipStream_t s);
+                        size_t batch, int inverse, hipStream_t s, void* d_tmp2 = nullptr);
 
 }  // namespace halo

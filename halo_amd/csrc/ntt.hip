@@ -15,124 +15,263 @@
 // ark ABI format and the last pass converts back (with the N^-1 scaling for the inverse); the
 // intermediate buffers hold the internal packed format.
 #include <algorithm>
+#include <cstdlib>
 
 #include "dispatch.hpp"
 #include "runtime.hpp"
 
 namespace halo {
 
-constexpr int NTT_E = 1024;       // elements per workgroup
-constexpr int NTT_THREADS = 256;  // threads per workgroup
+constexpr int NTT_E = 1024;  // elements per workgroup (LDS-resident R-point DFTs)
 constexpr int NTT_MAX_LOG_R_MULTI = 8;
+constexpr int NTT_TW_MAX = 256;  // stage-twiddle table entries (stages 0..7)
+constexpr unsigned NTT_FULL_TABLE_MAX_LOG = 24;  // per-pass twiddle tables up to 2^24
 
 struct NttPassArgs {
     const uint4* in;
     uint4* out;
-    const uint4* tw_hi;
+    const uint4* tw;        // per-pass pre-twiddle table tw[rho * Ns + jj] (internal packed), or null
+    const uint4* tw_hi;     // 2-level fallback (logn > NTT_FULL_TABLE_MAX_LOG)
     const uint4* tw_lo;
-    const uint4* rtab;
+    const uint4* stage_tw;  // entry 2^s - 1 + k = omega_{2^(s+1)}^k (s < 8, k < 2^s)
     uint32_t logn, log_r, log_ns, lo_bits;
-    uint32_t in_ark, out_ark, scale;
-    uint32_t ninv[NLIMB];  // N^-1 (internal form) applied at the output when scale != 0
-    size_t stride;         // elements between consecutive transforms of a batch
+    uint32_t in_ark, out_ark;
+    // Output multiplier.  The first pass takes the ark words (x 2^256 mod p) directly as internal
+    // values, i.e. as x 2^-5 in Montgomery form with R' = 2^261; the transform is linear, so the last
+    // pass multiplies by 2^261 (forward) or 2^261 / N (inverse) and emits ark words again: the
+    // input conversion costs no multiplication.
+    uint32_t out_const[NLIMB];
+    size_t stride;              // elements between consecutive transforms of a batch
 };
 
+// LDS layout: limb-major (SoA), limb l of position p at smem[l * NTT_E + swz(p)].  swz XORs the
+// bank bits with a linear function of p >> 5, chosen (by exhaustive check over every access pattern
+// of the load, group and store phases for r = 1..8) so that every ds_read_b32 / ds_write_b32 is
+// conflict-free.
+template <int EPT>
+struct NttSwz;
+template <>
+struct NttSwz<8> {
+    static constexpr uint32_t C[5] = {25, 18, 15, 10, 30};
+};
+template <>
+struct NttSwz<4> {
+    static constexpr uint32_t C[5] = {31, 22, 5, 27, 10};
+};
+template <int EPT>
+HALO_DEV uint32_t ntt_swz_hi(uint32_t hi) {  // linear map of (p >> 5) onto the bank bits
+    uint32_t m = 0;
+#pragma unroll
+    for (int b = 0; b < 5; b++) m ^= ((hi >> b) & 1u) ? NttSwz<EPT>::C[b] : 0u;
+    return m;
+}
+template <int EPT>
+HALO_DEV uint32_t ntt_swz(uint32_t p) {
+    return p ^ ntt_swz_hi<EPT>(p >> 5);
+}
+
 template <class F>
-HALO_DEV Fe<F> lds_get(const uint32_t* s, int idx) {
+HALO_DEV Fe<F> lds_get_soa(const uint32_t* s, uint32_t idx, uint32_t stride) {
     Fe<F> r;
 #pragma unroll
-    for (int l = 0; l < NLIMB; l++) r.v[l] = s[idx * NLIMB + l];
+    for (int l = 0; l < NLIMB; l++) r.v[l] = s[l * stride + idx];
     return r;
 }
 template <class F>
-HALO_DEV void lds_put(uint32_t* s, int idx, const Fe<F>& a) {
+HALO_DEV void lds_put_soa(uint32_t* s, uint32_t idx, uint32_t stride, const Fe<F>& a) {
 #pragma unroll
-    for (int l = 0; l < NLIMB; l++) s[idx * NLIMB + l] = a.v[l];
+    for (int l = 0; l < NLIMB; l++) s[l * stride + idx] = a.v[l];
 }
 
-template <class F>
-__global__ __launch_bounds__(NTT_THREADS) void k_ntt_pass(NttPassArgs a) {
+// x < 2^259 with normalized limbs -> x mod p in [0, 2p): subtract (q - 1) p with q = floor(x / 2^254)
+// (p = 2^254 + delta, delta < 2^126, for both Pasta fields).
+template <class C>
+HALO_DEV Fe<C> fe_reduce_q(const Fe<C>& x) {
+    const int32_t qm = 1 - (int32_t)(x.v[NLIMB - 1] >> 22);
+    Fe<C> r;
+    int64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < NLIMB; i++) {
+        int64_t d = (int64_t)x.v[i] + c;
+        if (C::P[i] != 0) d += (int64_t)qm * (int64_t)C::P[i];
+        r.v[i] = (i == NLIMB - 1) ? (uint32_t)d : ((uint32_t)d & LIMB_MASK);
+        c = d >> LIMB_BITS;
+    }
+    return r;
+}
+
+// G radix-2 DIT stages s .. s+G-1 over the EPT register-resident elements at positions base + m 2^s
+// (m < EPT).  Stage s' pairs m and m + 2^(s'-s) and multiplies the upper element by
+// omega_{2^(s'+1)}^k, k = (base + m 2^s) mod 2^s'.  Lazy reduction: values entering a pass are < 4p
+// (< 2p except raw ark words), stage 0 doubles that bound, every later stage adds at most 2p
+// (u + t and u - t + 2p with t = v w < 2p), so after 8 stages they are < 22p: still valid
+// Montgomery inputs (< 64p), reduced once at the end of the pass (fe_reduce_q, < 32p).
+template <class F, bool TWG>
+HALO_DEV Fe<F> ntt_stage_tw(const uint32_t* twl, const uint4* twg, uint32_t idx) {
+    if (TWG) return fe_load<F>(twg + 2 * idx);
+    return lds_get_soa<F>(twl, idx, NTT_TW_MAX);
+}
+
+template <class F, int EPT, int LG, bool TWG>
+HALO_DEV void ntt_group(Fe<F> (&v)[EPT], uint32_t s, uint32_t G, uint32_t k0, const uint32_t* twl, const uint4* twg) {
+#pragma unroll
+    for (int g = 0; g < LG; g++) {
+        if ((uint32_t)g >= G) break;
+        const uint32_t sp = s + (uint32_t)g;
+#pragma unroll
+        for (int m = 0; m < EPT; m++) {
+            if (m & (1 << g)) continue;
+            const int m2 = m + (1 << g);
+            Fe<F> t = v[m2];
+            if (sp != 0) {
+                const uint32_t k = k0 + ((uint32_t)(m & ((1 << g) - 1)) << s);
+                t = fe_mul(t, ntt_stage_tw<F, TWG>(twl, twg, (1u << sp) - 1u + k));
+            }
+            // stage 0 (no multiplication): t is a pass input, < 4p even for non-canonical ark words
+            v[m2] = (sp == 0) ? fe_sub_k<4>(v[m], t) : fe_sub_k<2>(v[m], t);
+            v[m] = fe_norm(fe_add_nc(v[m], t));
+        }
+    }
+}
+
+// One Stockham pass: R = 2^log_r point DFTs over the columns j of the N/R x R view.  A workgroup
+// owns T = NTT_E / R consecutive columns.  Each thread holds EPT elements in registers; the first
+// LG stages are done straight from the global loads, the rest in groups of LG stages through LDS,
+// and a final coalesced store phase writes y[(j / Ns) Ns R + (j mod Ns) + k Ns].
+template <class F, int EPT, bool TWG>
+__global__ __launch_bounds__(NTT_E / EPT) void k_ntt_pass(NttPassArgs a) {
+    constexpr int LG = (EPT == 8) ? 3 : 2;
+    constexpr uint32_t TH = NTT_E / EPT;
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    const uint32_t R = 1u << a.log_r;
-    const size_t N = (size_t)1 << a.logn;
-    const size_t NJ = N >> a.log_r;  // columns per transform
-    const uint32_t T = (uint32_t)((NJ < (size_t)(NTT_E >> a.log_r)) ? NJ : (NTT_E >> a.log_r));
-    const uint32_t E = T * R;
-    const size_t Ns = (size_t)1 << a.log_ns;
     uint32_t* data = smem;
-    uint32_t* rt = smem + NTT_E * NLIMB;
+    uint32_t* twl = smem + NTT_E * NLIMB;
+    const uint32_t r = a.log_r;
+    const uint32_t R = 1u << r;
+    const size_t N = (size_t)1 << a.logn;
+    const size_t NJ = N >> r;
+    const uint32_t T = (uint32_t)((NJ < (size_t)(NTT_E >> r)) ? NJ : (NTT_E >> r));
+    const uint32_t EB = T * R;  // elements in this block
+    const size_t Ns = (size_t)1 << a.log_ns;
     const size_t j0 = (size_t)blockIdx.x * T;
     const uint4* in = a.in + (size_t)blockIdx.y * a.stride * 2;
     uint4* out = a.out + (size_t)blockIdx.y * a.stride * 2;
+    const uint32_t tau = threadIdx.x;
 
-    // omega_R table (x < R/2) into LDS
-    for (uint32_t x = threadIdx.x; x < R / 2; x += NTT_THREADS) lds_put(rt, x, fe_load<F>(a.rtab + 2 * x));
+    // stage twiddles (entries < R - 1) into LDS
+    if (!TWG)
+        for (uint32_t x = tau; x + 1 < R; x += TH) lds_put_soa(twl, x, NTT_TW_MAX, fe_load<F>(a.stage_tw + 2 * x));
 
-    // load + Stockham twiddle, bit-reversed placement for the DIT stages
-    const size_t tw_step = N >> (a.log_ns + a.log_r);  // N / (Ns R)
-    const uint32_t lo_mask = (1u << a.lo_bits) - 1;
-    for (uint32_t idx = threadIdx.x; idx < E; idx += NTT_THREADS) {
-        const uint32_t r = idx / T, t = idx % T;
-        const size_t j = j0 + t;
-        const uint4* src = in + 2 * (j + (size_t)r * NJ);
-        Fe<F> v = a.in_ark ? fe_from_ark<F>(src) : fe_load<F>(src);
-        if (a.log_ns != 0 && r != 0) {
-            const size_t x = (size_t)r * ((j & (Ns - 1)) * tw_step);
-            if (x != 0) {
-                Fe<F> w = fe_load<F>(a.tw_lo + 2 * (x & lo_mask));
-                const size_t xh = x >> a.lo_bits;
-                if (xh != 0) w = fe_mul(w, fe_load<F>(a.tw_hi + 2 * xh));
-                v = fe_mul(v, w);
+    // ---- load + pre-twiddle + first LG stages (positions base + m)
+    uint32_t base;
+    if (R >= (uint32_t)EPT) {
+        const uint32_t q = tau / T, t = tau % T;
+        base = t * R + EPT * q;
+    } else {
+        base = EPT * tau;
+    }
+    Fe<F> v[EPT];
+    const size_t tw_step = N >> (a.log_ns + r);  // N / (Ns R)
+#pragma unroll
+    for (int m = 0; m < EPT; m++) {
+        const uint32_t pos = base + m;
+        if (pos < EB) {
+            const uint32_t t = pos >> r;
+            const uint32_t rho = r ? (__brev(pos & (R - 1)) >> (32 - r)) : 0;
+            const size_t j = j0 + t;
+            const uint4* src = in + 2 * (j + (size_t)rho * NJ);
+            Fe<F> x = fe_load<F>(src);  // ark words are used as internal values (see out_const)
+            if (!a.in_ark && a.log_ns != 0 && rho != 0) {
+                const size_t jj = j & (Ns - 1);
+                Fe<F> w;
+                if (a.tw) {
+                    w = fe_load<F>(a.tw + 2 * ((size_t)rho * Ns + jj));
+                } else {
+                    const size_t e = (size_t)rho * jj * tw_step;
+                    const uint32_t lo_mask = (1u << a.lo_bits) - 1;
+                    w = fe_load<F>(a.tw_lo + 2 * (e & lo_mask));
+                    const size_t eh = e >> a.lo_bits;
+                    if (eh) w = fe_mul(w, fe_load<F>(a.tw_hi + 2 * eh));
+                }
+                x = fe_mul(x, w);
             }
+            v[m] = x;
+        } else {
+            v[m] = fe_zero<F>();
         }
-        const uint32_t rb = a.log_r ? (__brev(r) >> (32 - a.log_r)) : 0;
-        lds_put(data, t * R + rb, v);
+    }
+    __syncthreads();  // stage twiddles visible
+    const uint32_t G0 = r < (uint32_t)LG ? r : (uint32_t)LG;
+    ntt_group<F, EPT, LG, TWG>(v, 0, G0, 0, twl, a.stage_tw);
+    {
+        const uint32_t pb = ntt_swz<EPT>(base);
+#pragma unroll
+        for (int m = 0; m < EPT; m++)
+            if (base + m < EB) lds_put_soa(data, pb ^ (uint32_t)m, NTT_E, v[m]);
     }
     __syncthreads();
 
-    // radix-2 DIT stages inside each column's R-point DFT
-    for (uint32_t s = 0; s < a.log_r; s++) {
+    // ---- remaining stages in groups of LG through LDS
+    for (uint32_t s = G0; s < r; s += LG) {
+        const uint32_t G = (r - s) < (uint32_t)LG ? (r - s) : (uint32_t)LG;
         const uint32_t h = 1u << s;
-        for (uint32_t b = threadIdx.x; b < E / 2; b += NTT_THREADS) {
-            const uint32_t t = b >> (a.log_r - 1);
-            const uint32_t q = b & ((R >> 1) - 1);
-            const uint32_t k = q & (h - 1);
-            const uint32_t i0 = t * R + ((q >> s) << (s + 1)) + k;
-            const uint32_t i1 = i0 + h;
-            const Fe<F> u = lds_get<F>(data, i0);
-            Fe<F> v = lds_get<F>(data, i1);
-            if (k != 0) v = fe_mul(v, lds_get<F>(rt, k << (a.log_r - 1 - s)));
-            lds_put(data, i0, fe_add(u, v));
-            lds_put(data, i1, fe_sub(u, v));
+        const uint32_t gb = (tau & (h - 1)) | ((tau >> s) << (s + LG));
+        const uint32_t shb = ntt_swz_hi<EPT>(gb >> 5);
+#pragma unroll
+        for (int m = 0; m < EPT; m++) {
+            const uint32_t pos = gb + (uint32_t)m * h;
+            const uint32_t ph = (pos ^ shb) ^ ntt_swz_hi<EPT>(((uint32_t)m * h) >> 5);
+            if (pos < EB) v[m] = lds_get_soa<F>(data, ph, NTT_E);
+        }
+        ntt_group<F, EPT, LG, TWG>(v, s, G, tau & (h - 1), twl, a.stage_tw);
+#pragma unroll
+        for (int m = 0; m < EPT; m++) {
+            const uint32_t pos = gb + (uint32_t)m * h;
+            const uint32_t ph = (pos ^ shb) ^ ntt_swz_hi<EPT>(((uint32_t)m * h) >> 5);
+            if (pos < EB) lds_put_soa(data, ph, NTT_E, v[m]);
         }
         __syncthreads();
     }
 
-    // store y[(j / Ns) Ns R + (j mod Ns) + k Ns]
-    for (uint32_t idx = threadIdx.x; idx < E; idx += NTT_THREADS) {
+    // ---- store y[(j / Ns) Ns R + (j mod Ns) + k Ns]
+    Fe<F> oc;
+#pragma unroll
+    for (int l = 0; l < NLIMB; l++) oc.v[l] = a.out_const[l];
+#pragma unroll
+    for (int i = 0; i < EPT; i++) {
+        const uint32_t idx = tau + TH * (uint32_t)i;
+        if (idx >= EB) continue;
         uint32_t k, t;
         if (a.log_ns == 0) {
-            t = idx / R;
-            k = idx % R;
+            t = idx >> r;
+            k = idx & (R - 1);
         } else {
             k = idx / T;
             t = idx % T;
         }
         const size_t j = j0 + t;
-        const size_t dst = ((j >> a.log_ns) << (a.log_ns + a.log_r)) + (j & (Ns - 1)) + (size_t)k * Ns;
-        Fe<F> v = lds_get<F>(data, t * R + k);
+        const size_t dst = ((j >> a.log_ns) << (a.log_ns + r)) + (j & (Ns - 1)) + (size_t)k * Ns;
+        Fe<F> x = lds_get_soa<F>(data, ntt_swz<EPT>(t * R + k), NTT_E);
         if (a.out_ark) {
-            if (a.scale) {
-                Fe<F> ni;
-#pragma unroll
-                for (int l = 0; l < NLIMB; l++) ni.v[l] = a.ninv[l];
-                v = fe_mul(v, ni);
-            }
-            fe_to_ark(out + 2 * dst, v);
+            fe_store(out + 2 * dst, fe_canon(fe_mul(x, oc)));
         } else {
-            fe_store(out + 2 * dst, v);
+            fe_store(out + 2 * dst, fe_reduce_q(x));
         }
     }
+}
+
+// Per-pass pre-twiddle table: tab[rho * Ns + jj] = omega_N^(rho jj N / (Ns R)) (internal packed).
+template <class F>
+__global__ void k_pass_twiddles(uint4* tab, uint32_t log_r, uint32_t log_ns, uint32_t logn, const uint4* lo,
+                                const uint4* hi, uint32_t lo_bits) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t cnt = (size_t)1 << (log_r + log_ns);
+    if (i >= cnt) return;
+    const size_t rho = i >> log_ns, jj = i & (((size_t)1 << log_ns) - 1);
+    const size_t e = rho * jj * ((size_t)1 << (logn - log_ns - log_r));
+    Fe<F> w = fe_load<F>(lo + 2 * (e & (((size_t)1 << lo_bits) - 1)));
+    const size_t eh = e >> lo_bits;
+    if (eh) w = fe_mul(w, fe_load<F>(hi + 2 * eh));
+    fe_store(tab + 2 * i, w);
 }
 
 // out[i] = base^(i * step) for i < count (internal packed format).  base given in internal form.
@@ -181,6 +320,37 @@ static int launch_pow_table(uint4* out, size_t count, const Fe<F>& base, uint64_
     return HALO_OK;
 }
 
+// k_ntt_pass variant: bit 1 = 8 elements per thread (radix-8 register groups; else radix-4),
+// bit 0 = stage twiddles read from global (L1/L2) instead of staged in LDS.  HALO_NTT_CFG overrides
+// the default (kept for measurement).
+static int ntt_cfg() {
+    static const int v = [] {
+        const char* e = getenv("HALO_NTT_CFG");
+        return e ? (atoi(e) & 3) : 1;
+    }();
+    return v;
+}
+
+static std::vector<unsigned> ntt_radices(unsigned logn) {
+    std::vector<unsigned> r;
+    const unsigned loge = 10;  // log2(NTT_E)
+    if (logn <= NTT_MAX_LOG_R_MULTI || logn <= loge) {
+        // one pass (R = N <= NTT_E): r > 8 would overflow the stage-twiddle table
+        if (logn <= NTT_MAX_LOG_R_MULTI) {
+            r.push_back(logn);
+            return r;
+        }
+    }
+    const unsigned passes = (logn + NTT_MAX_LOG_R_MULTI - 1) / NTT_MAX_LOG_R_MULTI;
+    unsigned left = logn;
+    for (unsigned p = 0; p < passes; p++) {
+        unsigned take = (left + (passes - p) - 1) / (passes - p);
+        r.push_back(take);
+        left -= take;
+    }
+    return r;
+}
+
 template <class F>
 static int get_twiddles(DeviceState* st, int field, unsigned logn, int inverse, DeviceState::Twiddles** out,
                         hipStream_t s) {
@@ -200,53 +370,41 @@ static int get_twiddles(DeviceState* st, int field, unsigned logn, int inverse, 
     const Fe<F> w = host_fe<F>(inverse ? F::OMEGA_INV[logn] : F::OMEGA[logn]);
     HALO_CHECK(launch_pow_table<F>(t->lo.as<uint4>(), nlo, w, 1, s));
     HALO_CHECK(launch_pow_table<F>(t->hi.as<uint4>(), nhi, w, (uint64_t)nlo, s));
+    // stage twiddles omega_{2^(s+1)}^k (the same for every N; kept per table for simplicity)
+    HALO_CHECK(t->stage.reserve(NTT_TW_MAX * 32));
+    for (unsigned sg = 0; sg < 8; sg++) {
+        const Fe<F> ws = host_fe<F>(inverse ? F::OMEGA_INV[sg + 1] : F::OMEGA[sg + 1]);
+        HALO_CHECK(launch_pow_table<F>(t->stage.as<uint4>() + 2 * (((size_t)1 << sg) - 1), (size_t)1 << sg, ws, 1, s));
+    }
+    // per-pass pre-twiddle tables (one multiplication per element instead of two)
+    if (logn <= NTT_FULL_TABLE_MAX_LOG) {
+        const std::vector<unsigned> rad = ntt_radices(logn);
+        unsigned log_ns = 0;
+        for (size_t p = 0; p < rad.size(); p++) {
+            if (p > 0) {
+                const size_t cnt = (size_t)1 << (rad[p] + log_ns);
+                HALO_CHECK(t->pass[p].reserve(cnt * 32));
+                const unsigned thr = 256, blocks = (unsigned)((cnt + thr - 1) / thr);
+                hipLaunchKernelGGL(k_pass_twiddles<F>, dim3(blocks), dim3(thr), 0, s, t->pass[p].as<uint4>(), rad[p],
+                                   log_ns, logn, t->lo.as<const uint4>(), t->hi.as<const uint4>(),
+                                   (uint32_t)t->lo_bits);
+                HALO_HIP(hipGetLastError());
+            }
+            log_ns += rad[p];
+        }
+        t->has_pass = true;
+    }
     *out = t.get();
     st->tw.push_back(std::move(t));
     return HALO_OK;
 }
 
-template <class F>
-static int get_rtable(DeviceState* st, int field, unsigned logr, int inverse, const uint4** out, hipStream_t s) {
-    for (auto& t : st->rt)
-        if (t->field == field && t->logr == (int)logr && t->inverse == inverse) {
-            *out = t->t.as<const uint4>();
-            return HALO_OK;
-        }
-    auto t = std::make_unique<DeviceState::RTable>();
-    t->field = field;
-    t->logr = (int)logr;
-    t->inverse = inverse;
-    const size_t cnt = logr ? ((size_t)1 << (logr - 1)) : 1;
-    HALO_CHECK(t->t.reserve(cnt * 32));
-    const Fe<F> w = host_fe<F>(inverse ? F::OMEGA_INV[logr] : F::OMEGA[logr]);
-    HALO_CHECK(launch_pow_table<F>(t->t.as<uint4>(), cnt, w, 1, s));
-    *out = t->t.as<const uint4>();
-    st->rt.push_back(std::move(t));
-    return HALO_OK;
-}
-
-static std::vector<unsigned> ntt_radices(unsigned logn) {
-    std::vector<unsigned> r;
-    const unsigned loge = 10;  // log2(NTT_E)
-    if (logn <= loge) {
-        r.push_back(logn);
-        return r;
-    }
-    const unsigned passes = (logn + NTT_MAX_LOG_R_MULTI - 1) / NTT_MAX_LOG_R_MULTI;
-    unsigned left = logn;
-    for (unsigned p = 0; p < passes; p++) {
-        unsigned take = (left + (passes - p) - 1) / (passes - p);
-        r.push_back(take);
-        left -= take;
-    }
-    return r;
-}
-
 // Device NTT over `batch` transforms: reads d_in (ark format), writes d_out (ark format).
-// d_tmp must hold batch * N elements (32 B) when more than one pass is needed; d_in may equal d_out.
+// The passes ping-pong between d_out and d_tmp; when d_in == d_out and the first pass would write
+// d_in, d_tmp2 (same size) takes that pass's output instead.  Buffers hold batch * N elements.
 template <class F>
-static int ntt_device(DeviceState* st, int field, const void* d_in, void* d_out, void* d_tmp, unsigned logn,
-                      size_t batch, int inverse, hipStream_t s) {
+static int ntt_device(DeviceState* st, int field, const void* d_in, void* d_out, void* d_tmp, void* d_tmp2,
+                      unsigned logn, size_t batch, int inverse, hipStream_t s) {
     if (logn > 30) return set_error(HALO_EINVAL, "NTT domain 2^%u too large", logn);
     const size_t N = (size_t)1 << logn;
     if (logn == 0) {
@@ -256,52 +414,47 @@ static int ntt_device(DeviceState* st, int field, const void* d_in, void* d_out,
     DeviceState::Twiddles* tw = nullptr;
     HALO_CHECK(get_twiddles<F>(st, field, logn, inverse, &tw, s));
     const std::vector<unsigned> rad = ntt_radices(logn);
-    // ping-pong: pass p reads src, writes dst; final pass must write d_out.
-    // Choose buffers so that the last pass lands in d_out and no pass reads and writes one buffer.
     const int P = (int)rad.size();
     std::vector<const void*> srcs(P);
     std::vector<void*> dsts(P);
-    {
-        void* bufs[2] = {d_out, d_tmp};
-        // walk backwards: last dst = d_out
-        int cur = 0;  // index in bufs for dst of pass p
-        for (int p = P - 1; p >= 0; p--) {
-            dsts[p] = bufs[cur];
-            cur ^= 1;
-        }
-        for (int p = 0; p < P; p++) srcs[p] = (p == 0) ? d_in : dsts[p - 1];
-        if (P > 1 && d_in == dsts[0]) {
-            // first pass would read and write the same buffer: stage through the other buffer
-            return set_error(HALO_EINVAL, "internal: NTT buffer aliasing");
-        }
+    dsts[P - 1] = d_out;
+    for (int p = P - 2; p >= 0; p--) dsts[p] = (dsts[p + 1] == d_out) ? d_tmp : d_out;
+    if (P > 1 && dsts[0] == d_in) {
+        if (!d_tmp2) return set_error(HALO_EINVAL, "internal: NTT buffer aliasing");
+        dsts[0] = d_tmp2;
     }
+    for (int p = 0; p < P; p++) srcs[p] = (p == 0) ? d_in : dsts[p - 1];
     unsigned log_ns = 0;
     for (int p = 0; p < P; p++) {
         const unsigned lr = rad[p];
-        const uint4* rtab = nullptr;
-        HALO_CHECK(get_rtable<F>(st, field, lr, inverse, &rtab, s));
         NttPassArgs a;
         a.in = (const uint4*)srcs[p];
         a.out = (uint4*)dsts[p];
+        a.tw = (tw->has_pass && p > 0) ? tw->pass[p].as<const uint4>() : nullptr;
         a.tw_hi = tw->hi.as<const uint4>();
         a.tw_lo = tw->lo.as<const uint4>();
-        a.rtab = rtab;
+        a.stage_tw = tw->stage.as<const uint4>();
         a.logn = logn;
         a.log_r = lr;
         a.log_ns = log_ns;
         a.lo_bits = (uint32_t)tw->lo_bits;
         a.in_ark = (p == 0);
         a.out_ark = (p == P - 1);
-        a.scale = (p == P - 1) && inverse;
-        for (int l = 0; l < NLIMB; l++) a.ninv[l] = F::N_INV[logn][l];
+        for (int l = 0; l < NLIMB; l++) a.out_const[l] = inverse ? F::NINV_ARK[logn][l] : F::ONE[l];
         a.stride = N;
         const size_t NJ = N >> lr;
         const size_t T = std::min(NJ, (size_t)(NTT_E >> lr));
-        const size_t rt_entries = lr ? ((size_t)1 << (lr - 1)) : 1;
-        const size_t lds = (NTT_E + rt_entries) * NLIMB * 4;
+        const int cfg = ntt_cfg();
+        const bool twg = cfg & 1;
+        const size_t lds = (size_t)(NTT_E + (twg ? 0 : NTT_TW_MAX)) * NLIMB * 4;
         dim3 grid((unsigned)(NJ / T), (unsigned)batch);
         ProfScope prof("ntt_pass", s);
-        HALO_LAUNCH(prof, k_ntt_pass<F>, grid, dim3(NTT_THREADS), lds, s, a);
+        switch (cfg) {
+            case 0: HALO_LAUNCH(prof, (k_ntt_pass<F, 4, false>), grid, dim3(NTT_E / 4), lds, s, a); break;
+            case 1: HALO_LAUNCH(prof, (k_ntt_pass<F, 4, true>), grid, dim3(NTT_E / 4), lds, s, a); break;
+            case 2: HALO_LAUNCH(prof, (k_ntt_pass<F, 8, false>), grid, dim3(NTT_E / 8), lds, s, a); break;
+            default: HALO_LAUNCH(prof, (k_ntt_pass<F, 8, true>), grid, dim3(NTT_E / 8), lds, s, a); break;
+        }
         HALO_HIP(hipGetLastError());
         log_ns += lr;
     }
@@ -309,9 +462,9 @@ static int ntt_device(DeviceState* st, int field, const void* d_in, void* d_out,
 }
 
 int ntt_device_dispatch(DeviceState* st, int field, const void* d_in, void* d_out, void* d_tmp, unsigned logn,
-                        size_t batch, int inverse, hipStream_t s) {
+                        size_t batch, int inverse, hipStream_t s, void* d_tmp2) {
     int rc;
-    DISPATCH_FIELD(field, F, { rc = ntt_device<F>(st, field, d_in, d_out, d_tmp, logn, batch, inverse, s); });
+    DISPATCH_FIELD(field, F, { rc = ntt_device<F>(st, field, d_in, d_out, d_tmp, d_tmp2, logn, batch, inverse, s); });
     return rc;
 }
 
@@ -357,7 +510,7 @@ static int ntt_host(halo_field_t field, const halo_fe_t* in, size_t len, unsigne
         HALO_CHECK(copy_h2d(a, in, len * 32, s));
     }
     // passes ping-pong between b and c, reading a
-    HALO_CHECK(ntt_device_dispatch(st, field, a, b, c, logn, 1, inverse, s));
+    HALO_CHECK(ntt_device_dispatch(st, field, a, b, c, logn, 1, inverse, s, nullptr));
     return copy_d2h(out, b, N * 32, s);
 }
 
@@ -402,14 +555,10 @@ extern "C" int halo_ntt_dev(halo_field_t field, void* d_data, unsigned log_n, si
     std::lock_guard<std::mutex> g(st->mu);
     const size_t N = (size_t)1 << log_n;
     hipStream_t s = (hipStream_t)stream;
-    // in place: the passes ping-pong through a scratch buffer; with an odd pass count the first
-    // pass must not write d_data, so stage the input in scratch[5] first in that case.
-    const size_t P = ntt_radices(log_n).size();
+    // in place: the passes ping-pong through scratch (a second scratch buffer takes the first pass
+    // when the pass count is odd, so no pass reads and writes one buffer)
     HALO_CHECK(st->scratch[4].reserve(batch * N * 32));
-    if (P % 2 == 1 && P > 1) {
-        HALO_CHECK(st->scratch[5].reserve(batch * N * 32));
-        HALO_HIP(hipMemcpyAsync(st->scratch[5].ptr, d_data, batch * N * 32, hipMemcpyDeviceToDevice, s));
-        return ntt_device_dispatch(st, field, st->scratch[5].ptr, d_data, st->scratch[4].ptr, log_n, batch, inverse, s);
-    }
-    return ntt_device_dispatch(st, field, d_data, d_data, st->scratch[4].ptr, log_n, batch, inverse, s);
+    HALO_CHECK(st->scratch[5].reserve(batch * N * 32));
+    return ntt_device_dispatch(st, field, d_data, d_data, st->scratch[4].ptr, log_n, batch, inverse, s,
+                               st->scratch[5].ptr);
 }

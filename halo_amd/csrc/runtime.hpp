@@ -69,6 +69,9 @@ struct DeviceState {
         int field, logn, inverse;
         DevBuf hi, lo;
         int lo_bits;
+        DevBuf stage;    // stage twiddles: entry 2^s - 1 + k = omega_{2^(s+1)}^k, s < 8
+        DevBuf pass[4];  // per-pass pre-twiddle tables (logn <= 24), see ntt.hip
+        bool has_pass = false;
     };
     std::vector<std::unique_ptr<Twiddles>> tw;
     struct RTable {

@@ -1,0 +1,103 @@
+// Microbenchmark: throughput of halo::fe_mul (compiler-scheduled column sums) versus a variant whose
+// column accumulations are single v_mad_u64_u32 chains (inline asm), on gfx950.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <vector>
+#include "fields.hpp"
+using namespace halo;
+#define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while(0)
+
+__device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {
+    uint64_t d; uint64_t cc;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(cc) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+__device__ __forceinline__ uint64_t mad64s(uint32_t a, uint32_t b, uint64_t c) {
+    uint64_t d; uint64_t cc;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(cc) : "v"(a), "s"(b), "v"(c));
+    return d;
+}
+
+template <class C>
+__device__ __forceinline__ Fe<C> fe_mul_asm(const Fe<C>& a, const Fe<C>& b) {
+    uint32_t m[NLIMB];
+    Fe<C> r;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 2 * NLIMB - 1; k++) {
+#pragma unroll
+        for (int i = 0; i < NLIMB; i++) {
+            const int j = k - i;
+            if (j < 0 || j >= NLIMB) continue;
+            acc = mad64(a.v[i], b.v[j], acc);
+        }
+#pragma unroll
+        for (int i = 0; i < NLIMB; i++) {
+            const int j = k - i;
+            if (i >= k || j < 1 || j >= NLIMB || C::P[j] == 0) continue;
+            acc = mad64s(m[i], C::P[j], acc);
+        }
+        if (k < NLIMB) {
+            const uint32_t mk = (0u - (uint32_t)acc) & LIMB_MASK;
+            m[k] = mk;
+            acc += mk;
+            acc >>= LIMB_BITS;
+        } else {
+            r.v[k - NLIMB] = (uint32_t)acc & LIMB_MASK;
+            acc >>= LIMB_BITS;
+        }
+    }
+    r.v[NLIMB - 1] = (uint32_t)acc;
+    return r;
+}
+
+template <int V>
+__global__ void bench(uint4* d, int iters) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    Fe<FqCfg> a = fe_load<FqCfg>(d + 4 * i), b = fe_load<FqCfg>(d + 4 * i + 2);
+    for (int k = 0; k < iters; k++) {
+        Fe<FqCfg> c = V == 0 ? fe_mul(a, b) : fe_mul_asm(a, b);
+        b = a;
+        a = c;
+    }
+    fe_store(d + 4 * i, a);
+}
+
+template <typename K>
+double timeit(K kern, uint4* d, int blocks, int threads, int iters) {
+    hipEvent_t e0, e1; CHECK(hipEventCreate(&e0)); CHECK(hipEventCreate(&e1));
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(threads), 0, 0, d, iters);
+    CHECK(hipDeviceSynchronize());
+    CHECK(hipEventRecord(e0));
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(threads), 0, 0, d, iters);
+    CHECK(hipEventRecord(e1)); CHECK(hipEventSynchronize(e1));
+    float ms; CHECK(hipEventElapsedTime(&ms, e0, e1));
+    return ms;
+}
+
+int main() {
+    const int threads = 256;
+    for (int wps : {1, 2, 4, 8}) {
+        const int blocks = 256 * wps;  // wps waves per SIMD
+        size_t n = (size_t)threads * blocks;
+        uint4* d; CHECK(hipMalloc(&d, n * 4 * sizeof(uint4)));
+        std::vector<uint32_t> h(n * 16);
+        for (size_t i = 0; i < h.size(); i++) h[i] = (uint32_t)(i * 2654435761u + 12345) & 0x3fffffffu;
+        CHECK(hipMemcpy(d, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+        const int iters = 512;
+        double t0 = timeit(bench<0>, d, blocks, threads, iters);
+        CHECK(hipMemcpy(d, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+        double t1 = timeit(bench<1>, d, blocks, threads, iters);
+        std::vector<uint32_t> o0(n * 16), o1(n * 16);
+        CHECK(hipMemcpy(d, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+        hipLaunchKernelGGL(bench<0>, dim3(blocks), dim3(threads), 0, 0, d, 7);
+        CHECK(hipMemcpy(o0.data(), d, h.size() * 4, hipMemcpyDeviceToHost));
+        CHECK(hipMemcpy(d, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+        hipLaunchKernelGGL(bench<1>, dim3(blocks), dim3(threads), 0, 0, d, 7);
+        CHECK(hipMemcpy(o1.data(), d, h.size() * 4, hipMemcpyDeviceToHost));
+        printf("waves/SIMD %d: compiler %.3e modmul/s, asm-chain %.3e modmul/s, same=%d\n", wps,
+               n * (double)iters / (t0 * 1e-3), n * (double)iters / (t1 * 1e-3), (int)(o0 == o1));
+        CHECK(hipFree(d));
+    }
+    return 0;
+}
