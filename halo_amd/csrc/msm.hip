@@ -27,7 +27,7 @@ namespace halo {
 
 constexpr uint32_t DIGIT_NONE = 0xffffffffu;
 constexpr int MSM_TASK_K = 64;   // max entries per accumulation task
-constexpr int MSM_SEG_L = 32;    // buckets per reduction segment
+constexpr int MSM_SEG_L = 32;    // columns of the bucket reduction grid (k_rowcol)
 
 // ---------------------------------------------------------------------------------------------
 // synthetic bases / scalars (shared host/device definition)
@@ -89,6 +89,30 @@ __global__ void k_digits(const uint4* scalars, size_t n, int c, int W, uint32_t*
     if (i >= n) return;
     uint32_t w8[8];
     fe_ark_to_canonical_words<S>(scalars + 2 * i, w8);
+    // s > p / 2: use p - s < 2^254 and flip every digit's sign (s P = -(p - s) P), so that
+    // W = ceil(255 / c) windows suffice (msm_windows)
+    uint32_t t8[8];
+    {
+        int64_t br = 0;
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const int64_t d = (int64_t)(uint32_t)(S::MODULUS64[q >> 1] >> (32 * (q & 1))) - (int64_t)w8[q] + br;
+            t8[q] = (uint32_t)d;
+            br = d >> 32;
+        }
+    }
+    bool neg = false;  // p - s < s
+#pragma unroll
+    for (int q = 7; q >= 0; q--) {
+        if (t8[q] != w8[q]) {
+            neg = t8[q] < w8[q];
+            break;
+        }
+    }
+    if (neg)
+#pragma unroll
+        for (int q = 0; q < 8; q++) w8[q] = t8[q];
+    const uint32_t nflip = neg ? 0x80000000u : 0u;
     const uint32_t half = 1u << (c - 1);
     const uint32_t full = 1u << c;
     uint32_t carry = 0;
@@ -106,10 +130,10 @@ __global__ void k_digits(const uint4* scalars, size_t n, int c, int W, uint32_t*
         if (v > half) {
             carry = 1;
             const uint32_t mag = full - v;  // |d|, d = v - 2^c < 0
-            out = (mag == 0) ? DIGIT_NONE : ((mag - 1) | 0x80000000u);
+            out = (mag == 0) ? DIGIT_NONE : (((mag - 1) | 0x80000000u) ^ nflip);
         } else {
             carry = 0;
-            out = (v == 0) ? DIGIT_NONE : (v - 1);
+            out = (v == 0) ? DIGIT_NONE : ((v - 1) | nflip);
         }
         digits[(size_t)w * n + i] = out;
     }
@@ -118,24 +142,25 @@ __global__ void k_digits(const uint4* scalars, size_t n, int c, int W, uint32_t*
 // ---------------------------------------------------------------------------------------------
 // 3-5. tasks, accumulation, merge
 // ---------------------------------------------------------------------------------------------
-__global__ void k_ntask(const uint32_t* bstart, size_t nb, uint32_t* ntask) {
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= nb) return;
-    const uint32_t cnt = bstart[t + 1] - bstart[t];
-    ntask[t] = (cnt + MSM_TASK_K - 1) / MSM_TASK_K;
-}
-
 struct Task {
     uint32_t begin, end;
 };
 
-__global__ void k_tasks(const uint32_t* bstart, const uint32_t* task_off, size_t nb, Task* tasks) {
+// Task slots without a prefix scan: bucket b owns slots [b + bstart[b] / K, b + 1 + bstart[b + 1] / K)
+// (disjoint, since ceil(cnt / K) <= floor(cnt / K) + 1).  Its first ceil(cnt / K) slots get chunks
+// of <= K consecutive sorted entries, the rest are empty (identity partials).  task_off[b] = the
+// first slot, task_off[nb] = total slot count (read by k_acc on the device).
+__global__ void k_tasks(const uint32_t* bstart, size_t nb, uint32_t* task_off, Task* tasks) {
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= nb) return;
     uint32_t b = bstart[t];
     const uint32_t e = bstart[t + 1];
-    uint32_t o = task_off[t];
+    uint32_t o = (uint32_t)t + b / MSM_TASK_K;
+    const uint32_t o_end = (uint32_t)t + 1 + e / MSM_TASK_K;
+    task_off[t] = o;
+    if (t == nb - 1) task_off[nb] = o_end;
     for (; b < e; b += MSM_TASK_K) tasks[o++] = Task{b, min(e, b + (uint32_t)MSM_TASK_K)};
+    for (; o < o_end; o++) tasks[o] = Task{0, 0};
 }
 
 template <class Cv>
@@ -171,76 +196,103 @@ __global__ __launch_bounds__(256) void k_merge(const uint32_t* task_off, size_t 
 }
 
 // ---------------------------------------------------------------------------------------------
-// 6. per-window reduction  S_w = sum_{b=1..B} b * BS[w][b], organised for low dependency depth
-//    (every stage is latency-bound: a lone XYZZ add is ~14 dependent modmuls):
-//    A. segments of L buckets: acc_j = sum_t t BS[jL+t], sum_j = sum_t BS[jL+t] (2L serial adds)
-//    B. S_w = sum_j acc_j + L * sum_j j sum_j, and sum_j j sum_j = sum_k 2^k T_k with
-//       T_k = sum_{j : bit k of j} sum_j  -> (nbits + 1) independent tree sums per window
-//    C. S_w = A + sum_k 2^(k + log L) T_k: lane k doubles T_k (k + log L times), LDS tree sum.
+// 6. per-window reduction  S_w = sum_{i<B} (i + 1) BS[w][i], organised for low dependency depth
+//    (every stage is latency-bound: a lone XYZZ add is ~14 dependent modmuls).  View the buckets as
+//    H rows x L columns, i = h L + l:
+//      sum_i (i + 1) BS_i = sum_h R_h + L sum_h h R_h + sum_l l C_l,
+//      R_h = sum_l BS[h L + l] (row sums), C_l = sum_h BS[h L + l] (column sums),
+//      sum_h h R_h = sum_j 2^j U_j, U_j = sum_{h : bit j of h} R_h, and likewise V_j for the columns.
+//    k_rowcol: R and C (tree sums, depth ~12); k_bitterms: sum_h R_h, U_j, V_j (independent tree
+//    sums, depth ~12); k_bitcombine: lane k doubles its term (<= log B times), then a tree sum.
+//    ~2.1 B adds in total at depth ~40 (a running-sum reduction needs 2 B adds at depth 2 B / #threads).
 // ---------------------------------------------------------------------------------------------
-template <class Cv>
-__global__ __launch_bounds__(64) void k_seg(const uint4* bucket_sums, uint32_t B, uint32_t L, int W, uint4* seg_acc,
-                                            uint4* seg_sum) {
-    using F = typename Cv::Base;
-    const uint32_t nseg = B / L;
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= (size_t)W * nseg) return;
-    const size_t w = t / nseg, j = t % nseg;
-    const uint4* bs = bucket_sums + 8 * (w * B + j * L);
-    XYZZ<F> run = xyzz_id<F>(), acc = xyzz_id<F>();
-    for (int k = (int)L - 1; k >= 0; k--) {
-        run = xyzz_add(run, xyzz_load<F>(bs + 8 * k));
-        acc = xyzz_add(acc, run);
+template <class F>
+HALO_DEV void lds_tree_sum(uint4* red, uint32_t tid, uint32_t n) {  // red[0] = sum of red[0..n), n pow2
+    for (uint32_t off = n >> 1; off > 0; off >>= 1) {
+        __syncthreads();
+        if (tid < off) xyzz_store(red + 8 * tid, xyzz_add(xyzz_load<F>(red + 8 * tid), xyzz_load<F>(red + 8 * (tid + off))));
     }
-    xyzz_store(seg_acc + 8 * t, acc);
-    xyzz_store(seg_sum + 8 * t, run);
+    __syncthreads();
 }
 
-// grid (nbits + 1, W), 256 threads.  out[w * (nbits + 1) + k]:
-//   k <  nbits : T_k = sum_{j : bit k of j} seg_sum[w][j]
-//   k == nbits : A   = sum_j seg_acc[w][j]
+// grid (ceil(H / (256 / L)) + L, SW), 256 threads
 template <class Cv>
-__global__ __launch_bounds__(256) void k_bitsums(const uint4* seg_acc, const uint4* seg_sum, uint32_t nseg,
-                                                 uint32_t nbits, uint4* out) {
+__global__ __launch_bounds__(256) void k_rowcol(const uint4* bucket_sums, uint32_t L, uint32_t H, uint4* rows,
+                                                uint4* cols) {
     using F = typename Cv::Base;
     __shared__ uint4 red[256 * 8];
-    const uint32_t k = blockIdx.x, w = blockIdx.y;
-    const uint4* src = (k == nbits) ? seg_acc : seg_sum;
-    XYZZ<F> acc = xyzz_id<F>();
-    for (uint32_t j = threadIdx.x; j < nseg; j += 256) {
-        if (k < nbits && !((j >> k) & 1u)) continue;
-        acc = xyzz_add(acc, xyzz_load<F>(src + 8 * ((size_t)w * nseg + j)));
-    }
-    xyzz_store(red + 8 * threadIdx.x, acc);
-    __syncthreads();
-    for (int off = 128; off > 0; off >>= 1) {
-        if ((int)threadIdx.x < off)
-            xyzz_store(red + 8 * threadIdx.x,
-                       xyzz_add(xyzz_load<F>(red + 8 * threadIdx.x), xyzz_load<F>(red + 8 * (threadIdx.x + off))));
+    const uint32_t w = blockIdx.y, tid = threadIdx.x;
+    const uint32_t B = L * H;
+    const uint4* bs = bucket_sums + 8 * (size_t)w * B;
+    const uint32_t rpb = 256 / L;  // rows per block
+    const uint32_t nrb = (H + rpb - 1) / rpb;
+    if (blockIdx.x < nrb) {
+        const uint32_t h = blockIdx.x * rpb + tid / L, l = tid % L;
+        XYZZ<F> v = xyzz_id<F>();
+        if (h < H) v = xyzz_load<F>(bs + 8 * ((size_t)h * L + l));
+        xyzz_store(red + 8 * tid, v);
+        // tree over the L lanes of each row (rows are contiguous groups of L threads)
+        for (uint32_t off = L >> 1; off > 0; off >>= 1) {
+            __syncthreads();
+            if (l < off)
+                xyzz_store(red + 8 * tid, xyzz_add(xyzz_load<F>(red + 8 * tid), xyzz_load<F>(red + 8 * (tid + off))));
+        }
         __syncthreads();
+        if (l == 0 && h < H) xyzz_store(rows + 8 * ((size_t)w * H + h), xyzz_load<F>(red + 8 * tid));
+    } else {
+        const uint32_t l = blockIdx.x - nrb;
+        XYZZ<F> acc = xyzz_id<F>();
+        for (uint32_t h = tid; h < H; h += 256) acc = xyzz_add(acc, xyzz_load<F>(bs + 8 * ((size_t)h * L + l)));
+        xyzz_store(red + 8 * tid, acc);
+        lds_tree_sum<F>(red, tid, 256);
+        if (tid == 0) xyzz_store(cols + 8 * ((size_t)w * L + l), xyzz_load<F>(red));
     }
-    if (threadIdx.x == 0) xyzz_store(out + 8 * ((size_t)w * (nbits + 1) + k), xyzz_load<F>(red));
 }
 
-// grid W, 64 threads: S_w = A + sum_k 2^(k + logL) T_k
+// grid (1 + logH + logL, SW), 256 threads.  out[w * NT + k]:
+//   k == 0             : sum_h R_h
+//   1 <= k <= logH     : U_{k-1} = sum_{h : bit k-1} R_h
+//   k >  logH          : V_{k-1-logH} = sum_{l : bit k-1-logH} C_l
 template <class Cv>
-__global__ __launch_bounds__(64) void k_bitcombine(const uint4* bits, uint32_t nbits, uint32_t logL,
+__global__ __launch_bounds__(256) void k_bitterms(const uint4* rows, const uint4* cols, uint32_t H, uint32_t L,
+                                                  uint32_t logH, uint4* out) {
+    using F = typename Cv::Base;
+    __shared__ uint4 red[256 * 8];
+    const uint32_t k = blockIdx.x, w = blockIdx.y, tid = threadIdx.x;
+    const uint32_t NT = gridDim.x;
+    const bool is_col = k > logH;
+    const uint32_t cnt = is_col ? L : H;
+    const uint4* src = is_col ? cols + 8 * (size_t)w * L : rows + 8 * (size_t)w * H;
+    const uint32_t bit = is_col ? (k - 1 - logH) : (k - 1);
+    XYZZ<F> acc = xyzz_id<F>();
+    for (uint32_t j = tid; j < cnt; j += 256) {
+        if (k != 0 && !((j >> bit) & 1u)) continue;
+        acc = xyzz_add(acc, xyzz_load<F>(src + 8 * j));
+    }
+    xyzz_store(red + 8 * tid, acc);
+    lds_tree_sum<F>(red, tid, 256);
+    if (tid == 0) xyzz_store(out + 8 * ((size_t)w * NT + k), xyzz_load<F>(red));
+}
+
+// grid SW, 64 threads: S_w = T_0 + sum_j 2^(j + logL) U_j + sum_j 2^j V_j
+template <class Cv>
+__global__ __launch_bounds__(64) void k_bitcombine(const uint4* terms, uint32_t NT, uint32_t logH, uint32_t logL,
                                                    uint4* window_sums) {
     using F = typename Cv::Base;
     __shared__ uint4 red[64 * 8];
     const uint32_t w = blockIdx.x, k = threadIdx.x;
     XYZZ<F> v = xyzz_id<F>();
-    if (k <= nbits) {
-        v = xyzz_load<F>(bits + 8 * ((size_t)w * (nbits + 1) + k));
-        if (k < nbits)
-            for (uint32_t d = 0; d < k + logL; d++) v = xyzz_dbl(v);
+    if (k < NT) {
+        v = xyzz_load<F>(terms + 8 * ((size_t)w * NT + k));
+        const uint32_t d = (k == 0) ? 0 : (k <= logH ? (k - 1 + logL) : (k - 1 - logH));
+        for (uint32_t i = 0; i < d; i++) v = xyzz_dbl(v);
     }
     xyzz_store(red + 8 * k, v);
-    __syncthreads();
-    for (int off = 32; off > 0; off >>= 1) {
-        if ((int)k < off) xyzz_store(red + 8 * k, xyzz_add(xyzz_load<F>(red + 8 * k), xyzz_load<F>(red + 8 * (k + off))));
+    for (uint32_t off = 32; off > 0; off >>= 1) {
         __syncthreads();
+        if (k < off) xyzz_store(red + 8 * k, xyzz_add(xyzz_load<F>(red + 8 * k), xyzz_load<F>(red + 8 * (k + off))));
     }
+    __syncthreads();
     if (k == 0) xyzz_store(window_sums + 8 * w, xyzz_load<F>(red));
 }
 
@@ -323,6 +375,17 @@ __global__ __launch_bounds__(64) void k_xyzz_to_aff(const uint4* in, uint4* out,
 // ---------------------------------------------------------------------------------------------
 // host orchestration
 // ---------------------------------------------------------------------------------------------
+// windows of c bits for scalars reduced to [0, p/2] (k_digits): 254 bits + the signed-digit carry
+int msm_windows(int c) { return (255 + c - 1) / c; }
+
+// window bits of the window-shifted SRS copies: one more bit than the plain MSM choice when that
+// saves a window (c = 17 at 2^20: 15 windows instead of 16; the single bucket set of 2^16 buckets
+// keeps the reduction and the 2-pass sort cheap)
+int msm_shifted_window_bits(size_t n) {
+    const int c = msm_window_bits(n);
+    return (msm_windows(c + 1) < msm_windows(c) && c + 1 <= 17) ? c + 1 : c;
+}
+
 int msm_window_bits(size_t n) {
     unsigned lg = n > 1 ? ilog2(n - 1) + 1 : 1;
     int c = (int)lg - 4;
@@ -332,7 +395,7 @@ int msm_window_bits(size_t n) {
 static unsigned grid_for(size_t n, unsigned thr) { return (unsigned)std::max<size_t>(1, (n + thr - 1) / thr); }
 
 struct MsmScratch {
-    DevBuf digits, bstart, ntask, task_off, tasks, partials, bucket_sums, seg_acc, seg_sum, bits, window_sums,
+    DevBuf digits, bstart, task_off, tasks, partials, bucket_sums, seg_acc, seg_sum, bits, window_sums,
         scan_tmp, conv;
     SortScratch sort;
     hipEvent_t acc_done = nullptr, tail_done = nullptr;
@@ -372,7 +435,7 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
     const hipStream_t ts = PP.tail;
     const size_t nn = std::max<size_t>(n, 1);
     const int c = c_req ? c_req : msm_window_bits(nn);
-    const int W = (256 + c - 1) / c;
+    const int W = msm_windows(c);
     const uint32_t B = 1u << (c - 1);
     // sort geometry: SW windows of SN entries each (shifted: one window over all W * n digits)
     const int SW = shifted ? 1 : W;
@@ -380,20 +443,20 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
     const size_t NB = (size_t)SW * B;
     const uint32_t L = std::min<uint32_t>(MSM_SEG_L, B);
     const uint32_t logL = ilog2(L);
-    const uint32_t nseg = B / L;
-    const uint32_t nbits = nseg > 1 ? ilog2(nseg - 1) + 1 : 0;
+    const uint32_t H = B / L;
+    const uint32_t logH = ilog2(H);
+    const uint32_t NT = 1 + logH + logL;  // reduction bit terms per window (<= 64)
     const uint32_t key_bits = NB > 1 ? ilog2(NB - 1) + 1 : 1;
     HALO_CHECK(M.digits.reserve((size_t)W * nn * 4));
     HALO_CHECK(M.bstart.reserve((NB + 1) * 4));
-    HALO_CHECK(M.ntask.reserve(NB * 4));
     HALO_CHECK(M.task_off.reserve((NB + 1) * 4));
     const size_t max_tasks = NB + (size_t)W * nn / MSM_TASK_K + 1;
     HALO_CHECK(M.tasks.reserve(max_tasks * sizeof(Task)));
     HALO_CHECK(M.partials.reserve(max_tasks * 128));
     HALO_CHECK(M.bucket_sums.reserve(NB * 128));
-    HALO_CHECK(M.seg_acc.reserve((size_t)SW * nseg * 128));
-    HALO_CHECK(M.seg_sum.reserve((size_t)SW * nseg * 128));
-    HALO_CHECK(M.bits.reserve((size_t)SW * (nbits + 1) * 128));
+    HALO_CHECK(M.seg_acc.reserve((size_t)SW * H * 128));  // row sums
+    HALO_CHECK(M.seg_sum.reserve((size_t)SW * L * 128));  // column sums
+    HALO_CHECK(M.bits.reserve((size_t)SW * NT * 128));
     HALO_CHECK(M.window_sums.reserve((size_t)W * 128));
 
     if (n > 0) {
@@ -404,31 +467,29 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
         const uint32_t* scount = nullptr;
         HALO_CHECK(msm_radix_sort(M.digits.as<const uint32_t>(), (size_t)W * nn, SN, B, key_bits, M.sort, &skeys,
                                   &svals, &scount, M.bstart.as<uint32_t>(), NB, s));
-        hipLaunchKernelGGL(k_ntask, dim3(grid_for(NB, 256)), dim3(256), 0, s, M.bstart.as<const uint32_t>(), NB,
-                           M.ntask.as<uint32_t>());
-        HALO_HIP(hipGetLastError());
-        HALO_CHECK(device_exclusive_scan(M.ntask.as<const uint32_t>(), NB, M.task_off.as<uint32_t>(), M.scan_tmp, s));
-        hipLaunchKernelGGL(k_tasks, dim3(grid_for(NB, 256)), dim3(256), 0, s, M.bstart.as<const uint32_t>(),
-                           M.task_off.as<const uint32_t>(), NB, M.tasks.as<Task>());
+        hipLaunchKernelGGL(k_tasks, dim3(grid_for(NB, 256)), dim3(256), 0, s, M.bstart.as<const uint32_t>(), NB,
+                           M.task_off.as<uint32_t>(), M.tasks.as<Task>());
         ProfScope prof("msm_acc", s);
         HALO_LAUNCH(prof, k_acc<Cv>, dim3(grid_for(max_tasks, 256)), dim3(256), 0, s, M.tasks.as<const Task>(),
                     M.task_off.as<const uint32_t>() + NB, (const uint32_t*)svals, bases_int, (uint32_t)nn,
                     (shifted && shift_stride != nn) ? shift_stride : (size_t)0, M.partials.as<uint4>());
-        hipLaunchKernelGGL(k_merge<Cv>, dim3(grid_for(NB, 256)), dim3(256), 0, s, M.task_off.as<const uint32_t>(), NB,
-                           M.partials.as<const uint4>(), M.bucket_sums.as<uint4>());
         HALO_HIP(hipGetLastError());
     } else {
         HALO_HIP(hipMemsetAsync(M.window_sums.ptr, 0, (size_t)SW * 128, s));
     }
-    // ---- tail (latency-bound) on the tail stream, overlapping the caller's next MSM
+    // ---- tail (latency-bound: task merge and bucket reduction) on the tail stream, overlapping the
+    // caller's next MSM
     HALO_HIP(hipEventRecord(M.acc_done, s));
     HALO_HIP(hipStreamWaitEvent(ts, M.acc_done, 0));
     if (n > 0) {
-        hipLaunchKernelGGL(k_seg<Cv>, dim3(grid_for((size_t)SW * nseg, 64)), dim3(64), 0, ts,
-                           M.bucket_sums.as<const uint4>(), B, L, SW, M.seg_acc.as<uint4>(), M.seg_sum.as<uint4>());
-        hipLaunchKernelGGL(k_bitsums<Cv>, dim3(nbits + 1, SW), dim3(256), 0, ts, M.seg_acc.as<const uint4>(),
-                           M.seg_sum.as<const uint4>(), nseg, nbits, M.bits.as<uint4>());
-        hipLaunchKernelGGL(k_bitcombine<Cv>, dim3(SW), dim3(64), 0, ts, M.bits.as<const uint4>(), nbits, logL,
+        hipLaunchKernelGGL(k_merge<Cv>, dim3(grid_for(NB, 256)), dim3(256), 0, ts, M.task_off.as<const uint32_t>(), NB,
+                           M.partials.as<const uint4>(), M.bucket_sums.as<uint4>());
+        const uint32_t nrb = (H + (256 / L) - 1) / (256 / L);
+        hipLaunchKernelGGL(k_rowcol<Cv>, dim3(nrb + L, SW), dim3(256), 0, ts, M.bucket_sums.as<const uint4>(), L, H,
+                           M.seg_acc.as<uint4>(), M.seg_sum.as<uint4>());
+        hipLaunchKernelGGL(k_bitterms<Cv>, dim3(NT, SW), dim3(256), 0, ts, M.seg_acc.as<const uint4>(),
+                           M.seg_sum.as<const uint4>(), H, L, logH, M.bits.as<uint4>());
+        hipLaunchKernelGGL(k_bitcombine<Cv>, dim3(SW), dim3(64), 0, ts, M.bits.as<const uint4>(), NT, logH, logL,
                            M.window_sums.as<uint4>());
     }
     hipLaunchKernelGGL(k_final<Cv>, dim3(1), dim3(320), 0, ts, M.window_sums.as<const uint4>(), SW, c, hide_table,
@@ -522,8 +583,8 @@ static int build_s_table(DeviceState* st, int curve, hipStream_t s) {
 int srs_precompute_windows(DeviceState* st, int curve, hipStream_t s) {
     SrsState& srs = st->srs[curve];
     if (!srs.n) return set_error(HALO_ESRSRANGE, "no resident SRS to precompute");
-    const int c = msm_window_bits(srs.n);
-    const int W = (256 + c - 1) / c;
+    const int c = msm_shifted_window_bits(srs.n);
+    const int W = msm_windows(c);
     HALO_CHECK(srs.shifted.reserve((size_t)W * srs.n * 64));
     DISPATCH_CURVE(curve, Cv, {
         hipLaunchKernelGGL(k_shift_windows<Cv>, dim3(grid_for(srs.n, 64)), dim3(64), 0, s, srs.gs.as<const uint4>(),

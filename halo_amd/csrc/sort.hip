@@ -5,8 +5,9 @@
 // by bucket key, so the accumulation kernel reads each bucket's points as one contiguous run.
 //
 // Design (per 8-bit digit pass, tiles of 4096 entries, 256 threads):
-//   k_rs_hist    : per-tile LDS histogram of the digit -> hist[digit * ntiles + tile]
-//   scan         : exclusive scan of hist (digit-major) -> every tile's global run start per digit
+//   k_rs_hist    : per-tile LDS histogram of the digit -> hist[tile][digit] (coalesced)
+//   colscan/chunkscan : digit-major exclusive prefix of that table without transposing it
+//                  -> every tile's global run start per digit
 //   k_rs_scatter : stable in-tile ranking (each wave ranks its own contiguous quarter of the tile with
 //                  ballots that find equal digits among lanes; per-wave histograms order the waves),
 //                  the tile is staged in LDS in digit order and written back as contiguous runs per
@@ -72,13 +73,62 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_hist(RsIn in, uint32_t ntiles
             atomicAdd(&h[(k >> in.shift) & 255u], 1u);
     }
     __syncthreads();
-    hist[(size_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
+    hist[(size_t)blockIdx.x * RS_BINS + threadIdx.x] = h[threadIdx.x];  // tile-major: coalesced
+}
+
+// Offsets from the tile-major histogram without a transposed copy.  k_rs_colscan: per chunk of
+// RS_CH tiles and per digit, the exclusive prefix over the chunk's tiles (in place) and the chunk
+// total.  k_rs_chunkscan (one block, thread = digit): exclusive prefix of the chunk totals per digit
+// plus the digit's base (exclusive scan of digit totals), in place; on pass 0 it also stores the
+// number of valid entries.  Tile t's run for digit d then starts at hist[t][d] + chunk[t / RS_CH][d].
+constexpr int RS_CH = 64;
+__global__ __launch_bounds__(RS_BINS) void k_rs_colscan(uint32_t* hist, uint32_t ntiles, uint32_t* chunk) {
+    const uint32_t d = threadIdx.x, t0 = blockIdx.x * RS_CH;
+    uint32_t v[RS_CH];
+#pragma unroll
+    for (int i = 0; i < RS_CH; i++) v[i] = (t0 + i < ntiles) ? hist[(size_t)(t0 + i) * RS_BINS + d] : 0u;
+    uint32_t run = 0;
+#pragma unroll
+    for (int i = 0; i < RS_CH; i++) {
+        if (t0 + i < ntiles) hist[(size_t)(t0 + i) * RS_BINS + d] = run;
+        run += v[i];
+    }
+    chunk[(size_t)blockIdx.x * RS_BINS + d] = run;
+}
+
+__global__ __launch_bounds__(RS_BINS) void k_rs_chunkscan(uint32_t* chunk, uint32_t nchunks, uint32_t* count) {
+    __shared__ uint32_t s[RS_BINS];
+    const uint32_t d = threadIdx.x;
+    constexpr int U = 16;
+    uint32_t run = 0;
+    for (uint32_t c0 = 0; c0 < nchunks; c0 += U) {
+        uint32_t v[U];
+#pragma unroll
+        for (int i = 0; i < U; i++) v[i] = (c0 + i < nchunks) ? chunk[(size_t)(c0 + i) * RS_BINS + d] : 0u;
+#pragma unroll
+        for (int i = 0; i < U; i++) {
+            if (c0 + i < nchunks) chunk[(size_t)(c0 + i) * RS_BINS + d] = run;
+            run += v[i];
+        }
+    }
+    // exclusive scan of the digit totals
+    s[d] = run;
+    __syncthreads();
+    for (int off = 1; off < RS_BINS; off <<= 1) {
+        const uint32_t t = (d >= (uint32_t)off) ? s[d - off] : 0u;
+        __syncthreads();
+        s[d] += t;
+        __syncthreads();
+    }
+    const uint32_t base = s[d] - run;
+    if (count && d == RS_BINS - 1) *count = s[d];
+    for (uint32_t c = 0; c < nchunks; c++) chunk[(size_t)c * RS_BINS + d] += base;
 }
 
 // Each wave owns a contiguous quarter of the tile (1024 entries, 16 rounds of 64), so ranking is
 // wave-local (ballots + a wave-private LDS run counter per digit) and the workgroup needs only
 // three barriers: after the per-wave histograms, after the prefix, after staging.
-__global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(RsIn in, uint32_t ntiles, const uint32_t* offsets,
+__global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(RsIn in, const uint32_t* tile_off, const uint32_t* chunk_off,
                                                            uint32_t* keys_out, uint32_t* vals_out) {
     constexpr int WAVES = RS_THREADS / 64;
     constexpr int PER_WAVE = RS_TILE / WAVES;  // 1024
@@ -100,7 +150,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(RsIn in, uint32_t nti
         V[r] = 0;
         if (rs_fetch(in, wbase + (size_t)r * 64 + lane, limit, K[r], V[r])) validmask |= 1u << r;
     }
-    goff[tid] = offsets[(size_t)tid * ntiles + blockIdx.x];
+    goff[tid] = tile_off[(size_t)blockIdx.x * RS_BINS + tid] + chunk_off[(size_t)(blockIdx.x / RS_CH) * RS_BINS + tid];
 #pragma unroll
     for (int w = 0; w < WAVES; w++) wpos[w][tid] = 0;
     __syncthreads();
@@ -290,8 +340,9 @@ int msm_radix_sort(const uint32_t* digits, size_t E, size_t npw, uint32_t B, uin
     HALO_CHECK(S.keys[1].reserve(std::max<size_t>(E, 1) * 4));
     HALO_CHECK(S.vals[0].reserve(std::max<size_t>(E, 1) * 4));
     HALO_CHECK(S.vals[1].reserve(std::max<size_t>(E, 1) * 4));
+    const uint32_t nchunks = (ntiles + RS_CH - 1) / RS_CH;
     HALO_CHECK(S.hist.reserve(hn * 4));
-    HALO_CHECK(S.offs.reserve((hn + 1) * 4));
+    HALO_CHECK(S.offs.reserve((size_t)nchunks * RS_BINS * 4));
     HALO_CHECK(S.count.reserve(16));
     const uint32_t passes = std::max<uint32_t>(1, (key_bits + 7) / 8);
     int cur = 0;
@@ -307,11 +358,13 @@ int msm_radix_sort(const uint32_t* digits, size_t E, size_t npw, uint32_t B, uin
         in.pass = p;
         in.shift = 8 * p;
         hipLaunchKernelGGL(k_rs_hist, dim3(ntiles), dim3(RS_THREADS), 0, s, in, ntiles, S.hist.as<uint32_t>());
-        HALO_CHECK(device_exclusive_scan(S.hist.as<const uint32_t>(), hn, S.offs.as<uint32_t>(), S.scan_tmp, s));
-        if (p == 0)  // number of valid (nonzero-digit) entries = scan total
-            HALO_HIP(hipMemcpyAsync(S.count.ptr, S.offs.as<uint32_t>() + hn, 4, hipMemcpyDeviceToDevice, s));
-        hipLaunchKernelGGL(k_rs_scatter, dim3(ntiles), dim3(RS_THREADS), 0, s, in, ntiles, S.offs.as<const uint32_t>(),
-                           S.keys[cur].as<uint32_t>(), S.vals[cur].as<uint32_t>());
+        hipLaunchKernelGGL(k_rs_colscan, dim3(nchunks), dim3(RS_BINS), 0, s, S.hist.as<uint32_t>(), ntiles,
+                           S.offs.as<uint32_t>());
+        // pass 0 also stores the number of valid (nonzero-digit) entries
+        hipLaunchKernelGGL(k_rs_chunkscan, dim3(1), dim3(RS_BINS), 0, s, S.offs.as<uint32_t>(), nchunks,
+                           p == 0 ? S.count.as<uint32_t>() : nullptr);
+        hipLaunchKernelGGL(k_rs_scatter, dim3(ntiles), dim3(RS_THREADS), 0, s, in, S.hist.as<const uint32_t>(),
+                           S.offs.as<const uint32_t>(), S.keys[cur].as<uint32_t>(), S.vals[cur].as<uint32_t>());
         HALO_HIP(hipGetLastError());
         cur ^= 1;
     }
