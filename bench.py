@@ -9,7 +9,8 @@ across ranks (rank r owns SRS block r, SURVEY §8e point-partition); each rank c
 sum, the partial points (64 B each) are all-gathered over RCCL and summed on the device
 (halo_point_sum) -- weak scaling, value = total points of all ranks / max-over-ranks time.
 
-Also measured (reported under "extra"): the 2^22 NTT + iNTT pair (BASELINE.json configs[2]).
+Also measured (reported under "extra"): the 2^22 NTT + iNTT pair (BASELINE.json configs[2]) and, under
+"extra.sizes", the 2^24 MSM (BASELINE.json configs[4] per rank) and the 2^24 NTT + iNTT pair.
 
 The roofline object prices the dominant kernel (MSM bucket accumulation, `k_acc`): achieved =
 96 B/point (64 B affine base + 32 B scalar) x points per launch / its mean launch time
@@ -45,6 +46,7 @@ def parse():
     ap.add_argument("--curve", default="pallas")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--sizes", default="24", help="extra MSM / NTT sizes (log2, comma separated) under extra.sizes")
     return ap.parse_args()
 
 
@@ -67,107 +69,135 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     curve = H.CURVES[args.curve]
     n = 1 << args.logn
-
-    # ---- setup (outside the timed region): resident SRS = this rank's block of the global SRS
-    seed = 0x48414C4F + rank  # distinct bases per rank
-    H.check(L.halo_srs_synthesize(curve, n, seed))
-    H.check(L.halo_srs_precompute_windows(curve))
     gen = torch.Generator(device="cuda")
     gen.manual_seed(1234 + rank)
-
-    def fresh_scalars(k):
-        s = torch.randint(-(2**63), 2**63 - 1, (k, n, 4), dtype=torch.int64, device="cuda", generator=gen)
-        s[..., 3] &= 0x0FFFFFFFFFFFFFFF  # < 2^252 < r: valid canonical Montgomery representatives
-        return s
-
-    nbatch = max(1, min(args.steps, 8))
-    scalars = fresh_scalars(nbatch)
     stream = torch.cuda.current_stream().cuda_stream
     sp = ctypes.c_void_p(stream)
-    total_steps = args.warmup + args.steps
-    d_out = torch.zeros((total_steps, 8), dtype=torch.int64, device="cuda")
-    d_final = torch.zeros((total_steps, 8), dtype=torch.int64, device="cuda")
-    out = np.zeros(8, dtype=np.uint64)
 
-    def run_steps(first, k):
-        """k MSM steps enqueued back to back (pipelined: each step's reduction tail overlaps the
-        next step's accumulation), then the multi-rank combine; no host synchronisation inside."""
-        for i in range(first, first + k):
-            H.check(L.halo_msm_dev_async(curve, None, ctypes.c_void_p(scalars[i % nbatch].data_ptr()), n,
-                                         ctypes.c_void_p(d_out[i].data_ptr()), sp))
-        H.check(L.halo_msm_join(sp))
+    def measure_msm(logn, steps, warmup, check_sync=True):
+        """Pipelined MSM throughput at 2^logn points per rank against a resident synthetic SRS."""
+        n = 1 << logn
+        # ---- setup (outside the timed region): resident SRS = this rank's block of the global SRS
+        seed = 0x48414C4F + rank  # distinct bases per rank
+        H.check(L.halo_srs_synthesize(curve, n, seed))
+        H.check(L.halo_srs_precompute_windows(curve))
+        nbatch = max(1, min(steps, 8 if logn <= 22 else 2))
+        # < 2^252 < r: valid canonical Montgomery representatives
+        scalars = torch.randint(-(2**63), 2**63 - 1, (nbatch, n, 4), dtype=torch.int64, device="cuda", generator=gen)
+        scalars[..., 3] &= 0x0FFFFFFFFFFFFFFF
+        total_steps = warmup + steps
+        d_out = torch.zeros((total_steps, 8), dtype=torch.int64, device="cuda")
+        d_final = torch.zeros((total_steps, 8), dtype=torch.int64, device="cuda")
+        out = np.zeros(8, dtype=np.uint64)
+
+        def run_steps(first, k):
+            """k MSM steps enqueued back to back (pipelined: each step's reduction tail overlaps the
+            next step's accumulation), then the multi-rank combine; no host synchronisation inside."""
+            for i in range(first, first + k):
+                H.check(L.halo_msm_dev_async(curve, None, ctypes.c_void_p(scalars[i % nbatch].data_ptr()), n,
+                                             ctypes.c_void_p(d_out[i].data_ptr()), sp))
+            H.check(L.halo_msm_join(sp))
+            if world > 1:
+                parts = [torch.empty((k, 8), dtype=torch.int64, device="cuda") for _ in range(world)]
+                dist.all_gather(parts, d_out[first:first + k].contiguous())
+                stacked = torch.stack(parts, dim=1).contiguous()  # (k, world, 8)
+                for j in range(k):
+                    H.check(L.halo_point_sum_dev(curve, ctypes.c_void_p(stacked[j].data_ptr()), world, 64,
+                                                 ctypes.c_void_p(d_final[first + j].data_ptr()), sp))
+
+        run_steps(0, warmup)
+        torch.cuda.synchronize()
         if world > 1:
-            parts = [torch.empty((k, 8), dtype=torch.int64, device="cuda") for _ in range(world)]
-            dist.all_gather(parts, d_out[first:first + k].contiguous())
-            stacked = torch.stack(parts, dim=1).contiguous()  # (k, world, 8)
-            for j in range(k):
-                H.check(L.halo_point_sum_dev(curve, ctypes.c_void_p(stacked[j].data_ptr()), world, 64,
-                                             ctypes.c_void_p(d_final[first + j].data_ptr()), sp))
+            dist.barrier()
+        L.halo_profile_reset()
+        L.halo_profile_enable(1)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        run_steps(warmup, steps)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t1 = time.perf_counter()
+        L.halo_profile_enable(0)
+        elapsed = t1 - t0
+        if world > 1:
+            tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            elapsed = float(tt.item())
+        launches = ctypes.c_size_t(0)
+        acc_ms = ctypes.c_double(0)
+        H.check(L.halo_profile_read(b"msm_acc", ctypes.byref(launches), ctypes.byref(acc_ms)))
+        acc_avg_ms = acc_ms.value / max(1, launches.value)
+        # every step's result must equal the synchronous (non-pipelined) MSM of the same scalars
+        sync_ok = True
+        lat = []
+        for i in range(min(nbatch, 4) if check_sync else 1):
+            torch.cuda.synchronize()
+            a0 = time.perf_counter()
+            H.check(L.halo_msm_dev(curve, None, ctypes.c_void_p(scalars[i].data_ptr()), n, H.ptr(out), sp))
+            lat.append((time.perf_counter() - a0) * 1e3)
+            for j in range(warmup, total_steps):
+                if j % nbatch == i:
+                    sync_ok &= bool(np.array_equal(d_out[j].cpu().numpy().view(np.uint64), out))
+        return elapsed, acc_avg_ms, sync_ok, lat, scalars[0]
 
-    run_steps(0, args.warmup)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    L.halo_profile_reset()
-    L.halo_profile_enable(1)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    run_steps(args.warmup, args.steps)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    L.halo_profile_enable(0)
-    elapsed = t1 - t0
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-    # every step's result must equal the synchronous (non-pipelined) MSM of the same scalars
-    sync_ok = True
-    lat = []
-    for i in range(min(nbatch, 4)):
+    elapsed, acc_avg_ms, sync_ok, lat, scalars0 = measure_msm(args.logn, args.steps, args.warmup)
+    window_bits = L.halo_srs_window_bits(curve)
+
+    # ---- NTT + iNTT pairs (configs[2] at 2^22, and the other BASELINE sizes); rank-local, under extra
+    def measure_ntt(logn, nrep=10):
+        N = 1 << logn
+        x = torch.randint(-(2**63), 2**63 - 1, (N, 4), dtype=torch.int64, device="cuda", generator=gen)
+        x[:, 3] &= 0x0FFFFFFFFFFFFFFF
+        x0 = x.clone()
+        xp = ctypes.c_void_p(x.data_ptr())
+        for _ in range(2):
+            H.check(L.halo_ntt_dev(H.FP, xp, logn, 1, 0, sp))
+            H.check(L.halo_ntt_dev(H.FP, xp, logn, 1, 1, sp))
+        torch.cuda.synchronize()
+        ok = bool(torch.equal(x, x0))
+        L.halo_profile_reset()
+        L.halo_profile_enable(1)
         torch.cuda.synchronize()
         a0 = time.perf_counter()
-        H.check(L.halo_msm_dev(curve, None, ctypes.c_void_p(scalars[i].data_ptr()), n, H.ptr(out), sp))
-        lat.append((time.perf_counter() - a0) * 1e3)
-        for j in range(args.warmup, total_steps):
-            if j % nbatch == i:
-                sync_ok &= bool(np.array_equal(d_out[j].cpu().numpy().view(np.uint64), out))
-    launches = ctypes.c_size_t(0)
-    acc_ms = ctypes.c_double(0)
-    H.check(L.halo_profile_read(b"msm_acc", ctypes.byref(launches), ctypes.byref(acc_ms)))
-    acc_avg_ms = acc_ms.value / max(1, launches.value)
+        for _ in range(nrep):
+            H.check(L.halo_ntt_dev(H.FP, xp, logn, 1, 0, sp))
+            H.check(L.halo_ntt_dev(H.FP, xp, logn, 1, 1, sp))
+        torch.cuda.synchronize()
+        a1 = time.perf_counter()
+        L.halo_profile_enable(0)
+        nl = ctypes.c_size_t(0)
+        nms = ctypes.c_double(0)
+        H.check(L.halo_profile_read(b"ntt_pass", ctypes.byref(nl), ctypes.byref(nms)))
+        ok = ok and bool(torch.equal(x, x0))
+        pair_ms = (a1 - a0) * 1e3 / nrep
+        del x, x0
+        return {
+            "workload": f"ntt+intt_2^{logn}_fp",
+            "pair_ms": pair_ms,
+            "elems_per_s_pair": N / (pair_ms * 1e-3),
+            "roundtrip_bit_exact": ok,
+            "passes_per_transform": int(nl.value // (2 * nrep)),
+            "pass_kernel_avg_ms": nms.value / max(1, nl.value),
+            "roofline_frac_pair": (2 * NTT_BYTES_PER_ELEM * N) / (pair_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+        }
 
-    # ---- NTT + iNTT pair at 2^ntt_logn (configs[2]); rank-local, reported under extra
-    N = 1 << args.ntt_logn
-    x = torch.randint(-(2**63), 2**63 - 1, (N, 4), dtype=torch.int64, device="cuda", generator=gen)
-    x[:, 3] &= 0x0FFFFFFFFFFFFFFF
-    x0 = x.clone()
-    xp = ctypes.c_void_p(x.data_ptr())
-    for _ in range(2):
-        H.check(L.halo_ntt_dev(H.FP, xp, args.ntt_logn, 1, 0, ctypes.c_void_p(stream)))
-        H.check(L.halo_ntt_dev(H.FP, xp, args.ntt_logn, 1, 1, ctypes.c_void_p(stream)))
-    torch.cuda.synchronize()
-    ntt_ok = bool(torch.equal(x, x0))
-    L.halo_profile_reset()
-    L.halo_profile_enable(1)
-    nrep = 10
-    torch.cuda.synchronize()
-    a0 = time.perf_counter()
-    for _ in range(nrep):
-        H.check(L.halo_ntt_dev(H.FP, xp, args.ntt_logn, 1, 0, ctypes.c_void_p(stream)))
-        H.check(L.halo_ntt_dev(H.FP, xp, args.ntt_logn, 1, 1, ctypes.c_void_p(stream)))
-    torch.cuda.synchronize()
-    a1 = time.perf_counter()
-    L.halo_profile_enable(0)
-    nl = ctypes.c_size_t(0)
-    nms = ctypes.c_double(0)
-    H.check(L.halo_profile_read(b"ntt_pass", ctypes.byref(nl), ctypes.byref(nms)))
-    ntt_ok = ntt_ok and bool(torch.equal(x, x0))
-    ntt_pair_ms = (a1 - a0) * 1e3 / nrep
+    ntt_main = measure_ntt(args.ntt_logn)
+    ntt_main["workload"] += " (BASELINE.json configs[2])"
+    sizes = {}
+    for lg in [int(v) for v in args.sizes.split(",") if v.strip()]:
+        e, a_ms, ok, lt, _ = measure_msm(lg, 4, 2, check_sync=False)
+        sizes[f"msm_2^{lg}"] = {
+            "points_per_s": (1 << lg) * world * 4 / e,
+            "ms_per_msm": e * 1e3 / 4,
+            "k_acc_ms": a_ms,
+            "single_latency_ms": lt[0] if lt else None,
+            "roofline_frac": MSM_BYTES_PER_POINT * (1 << lg) * world * 4 / e / 1e9 / HBM_PEAK_GBS,
+        }
+        sizes[f"ntt_2^{lg}"] = measure_ntt(lg, nrep=4)
+        torch.cuda.empty_cache()
 
     if rank != 0:
         if world > 1:
@@ -192,7 +222,7 @@ def main():
 
     cpu = None
     if not args.no_cpu and world == 1:
-        cpu = cpu_baseline(L, H, curve, n, scalars[0], out_check=True, budget_s=args.cpu_seconds)
+        cpu = cpu_baseline(L, H, curve, n, scalars0, out_check=True, budget_s=args.cpu_seconds)
 
     line = {
         "metric": "MSM points/sec (Pippenger, Pallas, 2^20 points, resident SRS)",
@@ -210,7 +240,7 @@ def main():
         "config": {
             "workload": f"msm_2^{args.logn}_pallas_resident_srs (BASELINE.json configs[1]; point-partitioned across ranks)",
             "points_per_rank": n,
-            "window_bits": L.halo_msm_window_bits(n),
+            "window_bits": window_bits,
             "parallelism": f"point-partition x{world}, RCCL all-gather of partial sums",
             "pipelining": "steps enqueued back to back: step k's reduction tail overlaps step k+1's accumulation",
         },
@@ -230,14 +260,8 @@ def main():
         "extra": {
             "msm_single_latency_ms": min(lat) if lat else None,
             "pipelined_equals_sync": sync_ok,
-            "ntt": {
-                "workload": f"ntt+intt_2^{args.ntt_logn}_fp (BASELINE.json configs[2])",
-                "pair_ms": ntt_pair_ms,
-                "elems_per_s_pair": N / (ntt_pair_ms * 1e-3),
-                "roundtrip_bit_exact": ntt_ok,
-                "pass_kernel_avg_ms": nms.value / max(1, nl.value),
-                "roofline_frac_pair": (2 * NTT_BYTES_PER_ELEM * N) / (ntt_pair_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-            }
+            "ntt": ntt_main,
+            "sizes": sizes,
         },
     }
     print(json.dumps(line))

@@ -61,6 +61,7 @@ SIGNATURES = {
     "halo_pcdl_commit": [ctypes.c_int, _vp, _sz, _sz, _vp, _vp],
     "halo_msm_dev": [ctypes.c_int, _vp, _vp, _sz, _vp, _vp],
     "halo_msm_window_bits": [_sz],
+    "halo_srs_window_bits": [ctypes.c_int],
     "halo_msm_dev_async": [ctypes.c_int, _vp, _vp, _sz, _vp, _vp],
     "halo_msm_join": [_vp],
     "halo_srs_read": [ctypes.c_int, _sz, _sz, _vp],

@@ -17,6 +17,7 @@
 //                 one workgroup per window forms sum_j (acc_j + jL sum_j) and tree-reduces in LDS.
 //   7. final    : Horner over the windows (+ w * S for hiding commitments), XYZZ -> affine -> ark.
 #include <algorithm>
+#include <cstdlib>
 
 #include "dispatch.hpp"
 #include "msm.hpp"
@@ -26,7 +27,6 @@
 namespace halo {
 
 constexpr uint32_t DIGIT_NONE = 0xffffffffu;
-constexpr int MSM_TASK_K = 64;   // max entries per accumulation task
 constexpr int MSM_SEG_L = 32;    // columns of the bucket reduction grid (k_rowcol)
 
 // ---------------------------------------------------------------------------------------------
@@ -142,57 +142,104 @@ __global__ void k_digits(const uint4* scalars, size_t n, int c, int W, uint32_t*
 // ---------------------------------------------------------------------------------------------
 // 3-5. tasks, accumulation, merge
 // ---------------------------------------------------------------------------------------------
-struct Task {
-    uint32_t begin, end;
-};
-
-// Task slots without a prefix scan: bucket b owns slots [b + bstart[b] / K, b + 1 + bstart[b + 1] / K)
-// (disjoint, since ceil(cnt / K) <= floor(cnt / K) + 1).  Its first ceil(cnt / K) slots get chunks
-// of <= K consecutive sorted entries, the rest are empty (identity partials).  task_off[b] = the
-// first slot, task_off[nb] = total slot count (read by k_acc on the device).
-__global__ void k_tasks(const uint32_t* bstart, size_t nb, uint32_t* task_off, Task* tasks) {
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= nb) return;
-    uint32_t b = bstart[t];
-    const uint32_t e = bstart[t + 1];
-    uint32_t o = (uint32_t)t + b / MSM_TASK_K;
-    const uint32_t o_end = (uint32_t)t + 1 + e / MSM_TASK_K;
-    task_off[t] = o;
-    if (t == nb - 1) task_off[nb] = o_end;
-    for (; b < e; b += MSM_TASK_K) tasks[o++] = Task{b, min(e, b + (uint32_t)MSM_TASK_K)};
-    for (; o < o_end; o++) tasks[o] = Task{0, 0};
-}
-
+// Uniform chunks: thread t accumulates the sorted entries [t K, t K + K) (every lane does the same
+// number of mixed additions, whatever the bucket sizes).  A chunk may cross bucket boundaries: its
+// first segment's sum goes to first[t], its last segment's (when there are >= 2) to last[t], and the
+// buckets strictly inside the chunk are complete, so they go straight to bucket_sums.  k_merge then
+// completes the buckets that straddle chunk boundaries.
 template <class Cv>
-__global__ __launch_bounds__(256, 4) void k_acc(const Task* tasks, const uint32_t* ntasks_total, const uint32_t* sorted,
-                                             const uint4* bases, uint32_t n_per_window, size_t stride,
-                                             uint4* partials) {
+__global__ __launch_bounds__(256, 4) void k_acc(const uint32_t* keys, const uint32_t* vals, const uint32_t* count,
+                                             uint32_t K, const uint4* bases, uint32_t n_per_window, size_t stride,
+                                             uint4* first, uint4* last, uint4* bucket_sums) {
     using F = typename Cv::Base;
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= *ntasks_total) return;
-    const Task tk = tasks[t];
+    const uint32_t cnt = *count;
+    const size_t beg = t * K;
+    if (beg >= cnt) return;
+    const uint32_t end = (uint32_t)min((size_t)cnt, beg + K);
+    uint32_t cur = keys[beg];
+    bool first_done = false;
     XYZZ<F> acc = xyzz_id<F>();
-    for (uint32_t e = tk.begin; e < tk.end; e++) {
-        const uint32_t v = sorted[e];
+    for (uint32_t e = (uint32_t)beg; e < end; e++) {
+        const uint32_t k = keys[e];
+        if (k != cur) {  // bucket boundary inside the chunk
+            if (!first_done) {
+                xyzz_store(first + 8 * t, acc);
+                first_done = true;
+            } else {
+                xyzz_store(bucket_sums + 8 * (size_t)cur, acc);
+            }
+            acc = xyzz_id<F>();
+            cur = k;
+        }
+        const uint32_t v = vals[e];
         size_t idx = v & 0x7fffffffu;
         if (stride) idx = (idx / n_per_window) * stride + idx % n_per_window;  // window-shifted SRS
         Affine<F> p = aff_load<F>(bases + 4 * idx);
         if (v & 0x80000000u) p.y = fe_neg(p.y);
         acc = xyzz_madd(acc, p);
     }
-    xyzz_store(partials + 8 * t, acc);
+    xyzz_store((first_done ? last : first) + 8 * t, acc);
 }
 
+// Skew guard: sums of MSM_GROUP consecutive chunk partials whose entries all belong to one bucket
+// (level 1: groups of 64 chunks from first[]; level 2: groups of 64 level-1 groups), so that a huge
+// bucket (all-equal scalars) is merged in O(chunks / 4096 + 128) sequential adds, not O(chunks).
+constexpr uint32_t MSM_GROUP = 64;
 template <class Cv>
-__global__ __launch_bounds__(256) void k_merge(const uint32_t* task_off, size_t nb, const uint4* partials, uint4* bucket_sums) {
+__global__ __launch_bounds__(MSM_GROUP) void k_group_sums(const uint32_t* keys, const uint32_t* count, uint32_t K,
+                                                          uint32_t span, const uint4* src, uint4* out) {
     using F = typename Cv::Base;
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= nb) return;
-    const uint32_t b = task_off[t], e = task_off[t + 1];
+    __shared__ uint4 red[MSM_GROUP * 8];
+    const uint32_t g = blockIdx.x, i = threadIdx.x;
+    const uint32_t cnt = *count;
+    const size_t e0 = (size_t)g * MSM_GROUP * span * K, e1 = e0 + (size_t)MSM_GROUP * span * K;
+    if (e1 > cnt || keys[e0] != keys[e1 - 1]) return;  // not one bucket throughout: never used
+    xyzz_store(red + 8 * i, xyzz_load<F>(src + 8 * ((size_t)g * MSM_GROUP + i)));
+    for (uint32_t off = MSM_GROUP / 2; off > 0; off >>= 1) {
+        __syncthreads();
+        if (i < off) xyzz_store(red + 8 * i, xyzz_add(xyzz_load<F>(red + 8 * i), xyzz_load<F>(red + 8 * (i + off))));
+    }
+    __syncthreads();
+    if (i == 0) xyzz_store(out + 8 * (size_t)g, xyzz_load<F>(red));
+}
+
+// Buckets that touch a chunk boundary (or are empty): bucket b's entries [s, e) lie in chunks
+// t0 = s / K .. t1 = (e - 1) / K; chunk t contributes first[t] when b is its first segment, else
+// last[t]; whole groups strictly inside (t0, t1) come from the group sums.  A bucket strictly
+// inside one chunk was written by k_acc.
+template <class Cv>
+__global__ __launch_bounds__(256) void k_merge(const uint32_t* bstart, const uint32_t* keys, const uint32_t* count,
+                                               uint32_t K, size_t nb, const uint4* first, const uint4* last,
+                                               const uint4* g1, const uint4* g2, uint4* bucket_sums) {
+    using F = typename Cv::Base;
+    const size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    const uint32_t s = bstart[b], e = bstart[b + 1];
+    if (s == e) {
+        xyzz_store(bucket_sums + 8 * b, xyzz_id<F>());
+        return;
+    }
+    const uint32_t cnt = *count;
+    const uint32_t t0 = s / K, t1 = (e - 1) / K;
+    auto chunk_last = [&](uint32_t t) { return min(cnt, (t + 1) * K) - 1; };
+    if (t0 == t1 && keys[(size_t)t0 * K] != b && keys[chunk_last(t0)] != b) return;  // interior: done
+    constexpr uint32_t G2 = MSM_GROUP * MSM_GROUP;
     XYZZ<F> acc = xyzz_id<F>();
-    if (e > b) acc = xyzz_load<F>(partials + 8 * (size_t)b);
-    for (uint32_t k = b + 1; k < e; k++) acc = xyzz_add(acc, xyzz_load<F>(partials + 8 * (size_t)k));
-    xyzz_store(bucket_sums + 8 * t, acc);
+    for (uint32_t t = t0; t <= t1;) {
+        if (t > t0 && t % G2 == 0 && t + G2 <= t1) {
+            acc = xyzz_add(acc, xyzz_load<F>(g2 + 8 * (size_t)(t / G2)));
+            t += G2;
+        } else if (t > t0 && t % MSM_GROUP == 0 && t + MSM_GROUP <= t1) {
+            acc = xyzz_add(acc, xyzz_load<F>(g1 + 8 * (size_t)(t / MSM_GROUP)));
+            t += MSM_GROUP;
+        } else {
+            const uint4* src = (keys[(size_t)t * K] == b) ? first : last;
+            acc = xyzz_add(acc, xyzz_load<F>(src + 8 * (size_t)t));
+            t++;
+        }
+    }
+    xyzz_store(bucket_sums + 8 * b, acc);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -395,8 +442,9 @@ int msm_window_bits(size_t n) {
 static unsigned grid_for(size_t n, unsigned thr) { return (unsigned)std::max<size_t>(1, (n + thr - 1) / thr); }
 
 struct MsmScratch {
-    DevBuf digits, bstart, task_off, tasks, partials, bucket_sums, seg_acc, seg_sum, bits, window_sums,
-        scan_tmp, conv;
+    DevBuf digits, bstart, partials, bucket_sums, seg_acc, seg_sum, bits, window_sums, scan_tmp, conv;
+    const uint32_t* skeys = nullptr;   // sorted keys of the current MSM (sort scratch)
+    const uint32_t* scount = nullptr;  // device count of valid entries
     SortScratch sort;
     hipEvent_t acc_done = nullptr, tail_done = nullptr;
     bool tail_pending = false;
@@ -449,10 +497,20 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
     const uint32_t key_bits = NB > 1 ? ilog2(NB - 1) + 1 : 1;
     HALO_CHECK(M.digits.reserve((size_t)W * nn * 4));
     HALO_CHECK(M.bstart.reserve((NB + 1) * 4));
-    HALO_CHECK(M.task_off.reserve((NB + 1) * 4));
-    const size_t max_tasks = NB + (size_t)W * nn / MSM_TASK_K + 1;
-    HALO_CHECK(M.tasks.reserve(max_tasks * sizeof(Task)));
-    HALO_CHECK(M.partials.reserve(max_tasks * 128));
+    // chunk length K: >= 4 rounds of resident lanes (256 CUs x 16 waves x 64), 16 <= K <= 64.  Every
+    // lane does the same number of mixed additions; several rounds absorb the CU slots held by the
+    // previous MSM's tail kernels, which one exact round would not (measured: K = 60 at 2^20 is 1
+    // round and 15% slower than K = 16).
+    const size_t E = (size_t)W * nn;
+    const size_t lanes = (size_t)st->num_cu * 16 * 64 * 4;
+    const uint32_t K = (uint32_t)std::max<size_t>(16, std::min<size_t>(64, (E + lanes - 1) / lanes));
+    const size_t nchunks = (E + K - 1) / K;
+    const size_t ng1 = nchunks / MSM_GROUP, ng2 = nchunks / (MSM_GROUP * MSM_GROUP);
+    HALO_CHECK(M.partials.reserve((std::max<size_t>(nchunks, 1) * 2 + ng1 + ng2 + 2) * 128));
+    uint4* P_first = M.partials.as<uint4>();
+    uint4* P_last = P_first + 8 * std::max<size_t>(nchunks, 1);
+    uint4* P_g1 = P_last + 8 * std::max<size_t>(nchunks, 1);
+    uint4* P_g2 = P_g1 + 8 * (ng1 + 1);
     HALO_CHECK(M.bucket_sums.reserve(NB * 128));
     HALO_CHECK(M.seg_acc.reserve((size_t)SW * H * 128));  // row sums
     HALO_CHECK(M.seg_sum.reserve((size_t)SW * L * 128));  // column sums
@@ -465,14 +523,15 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
         HALO_HIP(hipGetLastError());
         uint32_t *skeys = nullptr, *svals = nullptr;
         const uint32_t* scount = nullptr;
-        HALO_CHECK(msm_radix_sort(M.digits.as<const uint32_t>(), (size_t)W * nn, SN, B, key_bits, M.sort, &skeys,
-                                  &svals, &scount, M.bstart.as<uint32_t>(), NB, s));
-        hipLaunchKernelGGL(k_tasks, dim3(grid_for(NB, 256)), dim3(256), 0, s, M.bstart.as<const uint32_t>(), NB,
-                           M.task_off.as<uint32_t>(), M.tasks.as<Task>());
+        HALO_CHECK(msm_radix_sort(M.digits.as<const uint32_t>(), E, SN, B, key_bits, M.sort, &skeys, &svals, &scount,
+                                  nullptr, NB, s));
         ProfScope prof("msm_acc", s);
-        HALO_LAUNCH(prof, k_acc<Cv>, dim3(grid_for(max_tasks, 256)), dim3(256), 0, s, M.tasks.as<const Task>(),
-                    M.task_off.as<const uint32_t>() + NB, (const uint32_t*)svals, bases_int, (uint32_t)nn,
-                    (shifted && shift_stride != nn) ? shift_stride : (size_t)0, M.partials.as<uint4>());
+        HALO_LAUNCH(prof, k_acc<Cv>, dim3(grid_for(nchunks, 256)), dim3(256), 0, s, (const uint32_t*)skeys,
+                    (const uint32_t*)svals, scount, K, bases_int, (uint32_t)nn,
+                    (shifted && shift_stride != nn) ? shift_stride : (size_t)0, P_first, P_last,
+                    M.bucket_sums.as<uint4>());
+        M.skeys = skeys;
+        M.scount = scount;
         HALO_HIP(hipGetLastError());
     } else {
         HALO_HIP(hipMemsetAsync(M.window_sums.ptr, 0, (size_t)SW * 128, s));
@@ -482,8 +541,16 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
     HALO_HIP(hipEventRecord(M.acc_done, s));
     HALO_HIP(hipStreamWaitEvent(ts, M.acc_done, 0));
     if (n > 0) {
-        hipLaunchKernelGGL(k_merge<Cv>, dim3(grid_for(NB, 256)), dim3(256), 0, ts, M.task_off.as<const uint32_t>(), NB,
-                           M.partials.as<const uint4>(), M.bucket_sums.as<uint4>());
+        HALO_CHECK(msm_bucket_starts(M.skeys, M.scount, NB, E, M.bstart.as<uint32_t>(), ts));
+        if (ng1)
+            hipLaunchKernelGGL(k_group_sums<Cv>, dim3((unsigned)ng1), dim3(MSM_GROUP), 0, ts, (const uint32_t*)M.skeys,
+                               M.scount, K, 1u, (const uint4*)P_first, P_g1);
+        if (ng2)
+            hipLaunchKernelGGL(k_group_sums<Cv>, dim3((unsigned)ng2), dim3(MSM_GROUP), 0, ts, (const uint32_t*)M.skeys,
+                               M.scount, K, MSM_GROUP, (const uint4*)P_g1, P_g2);
+        hipLaunchKernelGGL(k_merge<Cv>, dim3(grid_for(NB, 256)), dim3(256), 0, ts, M.bstart.as<const uint32_t>(),
+                           (const uint32_t*)M.skeys, M.scount, K, NB, P_first, P_last, P_g1, P_g2,
+                           M.bucket_sums.as<uint4>());
         const uint32_t nrb = (H + (256 / L) - 1) / (256 / L);
         hipLaunchKernelGGL(k_rowcol<Cv>, dim3(nrb + L, SW), dim3(256), 0, ts, M.bucket_sums.as<const uint4>(), L, H,
                            M.seg_acc.as<uint4>(), M.seg_sum.as<uint4>());
@@ -626,6 +693,15 @@ static int check_curve(halo_curve_t c) {
 }
 
 extern "C" int halo_msm_window_bits(size_t n) { return msm_window_bits(n); }
+
+extern "C" int halo_srs_window_bits(halo_curve_t curve) {
+    clear_error();
+    if (curve != HALO_PALLAS && curve != HALO_VESTA) return set_error(HALO_EINVAL, "unknown curve id %d", (int)curve);
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    return st->srs[curve].shifted_c;
+}
 
 extern "C" int halo_point_sum(halo_curve_t curve, const halo_wrapped_point_t* pts, size_t k, halo_wrapped_point_t* out) {
     clear_error();

@@ -56,6 +56,9 @@ DeviceState* current_state() {
     if (!g_states[dev]) {
         g_states[dev] = new DeviceState();
         g_states[dev]->device = dev;
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
+            g_states[dev]->num_cu = cus;
     }
     return g_states[dev];
 }

@@ -60,6 +60,7 @@ struct SrsState {
 
 struct DeviceState {
     int device = -1;
+    int num_cu = 256;              // compute units (MI355X: 256), sizes one-round launches
     std::mutex mu;                 // serialises API calls on this device
     SrsState srs[2];               // per curve
     // scratch

@@ -4,7 +4,7 @@
 // per point per window).  On MI355X the buckets are instead formed by sorting the W*n digit entries
 // by bucket key, so the accumulation kernel reads each bucket's points as one contiguous run.
 //
-// Design (per 8-bit digit pass, tiles of 4096 entries, 256 threads):
+// Design (per 8-bit digit pass, tiles of 8192 entries, 512 threads):
 //   k_rs_hist    : per-tile LDS histogram of the digit -> hist[tile][digit] (coalesced)
 //   colscan/chunkscan : digit-major exclusive prefix of that table without transposing it
 //                  -> every tile's global run start per digit
@@ -24,9 +24,9 @@
 
 namespace halo {
 
-constexpr int RS_THREADS = 256;
+constexpr int RS_THREADS = 512;
 constexpr int RS_ROUNDS = 16;
-constexpr int RS_TILE = RS_THREADS * RS_ROUNDS;  // 4096
+constexpr int RS_TILE = RS_THREADS * RS_ROUNDS;  // 8192: runs average 32 entries (128 B) per digit
 constexpr int RS_BINS = 256;
 constexpr uint32_t RS_NONE = 0xffffffffu;
 
@@ -63,7 +63,7 @@ HALO_DEV size_t rs_limit(const RsIn& in) { return in.pass == 0 ? in.E : (size_t)
 
 __global__ __launch_bounds__(RS_THREADS) void k_rs_hist(RsIn in, uint32_t ntiles, uint32_t* hist) {
     __shared__ uint32_t h[RS_BINS];
-    h[threadIdx.x] = 0;
+    if (threadIdx.x < RS_BINS) h[threadIdx.x] = 0;
     __syncthreads();
     const size_t limit = rs_limit(in);
     const size_t base = (size_t)blockIdx.x * RS_TILE;
@@ -73,7 +73,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_hist(RsIn in, uint32_t ntiles
             atomicAdd(&h[(k >> in.shift) & 255u], 1u);
     }
     __syncthreads();
-    hist[(size_t)blockIdx.x * RS_BINS + threadIdx.x] = h[threadIdx.x];  // tile-major: coalesced
+    if (threadIdx.x < RS_BINS) hist[(size_t)blockIdx.x * RS_BINS + threadIdx.x] = h[threadIdx.x];  // tile-major
 }
 
 // Offsets from the tile-major histogram without a transposed copy.  k_rs_colscan: per chunk of
@@ -125,7 +125,7 @@ __global__ __launch_bounds__(RS_BINS) void k_rs_chunkscan(uint32_t* chunk, uint3
     for (uint32_t c = 0; c < nchunks; c++) chunk[(size_t)c * RS_BINS + d] += base;
 }
 
-// Each wave owns a contiguous quarter of the tile (1024 entries, 16 rounds of 64), so ranking is
+// Each wave owns a contiguous eighth of the tile (1024 entries, 16 rounds of 64), so ranking is
 // wave-local (ballots + a wave-private LDS run counter per digit) and the workgroup needs only
 // three barriers: after the per-wave histograms, after the prefix, after staging.
 __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(RsIn in, const uint32_t* tile_off, const uint32_t* chunk_off,
@@ -150,16 +150,18 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(RsIn in, const uint32
         V[r] = 0;
         if (rs_fetch(in, wbase + (size_t)r * 64 + lane, limit, K[r], V[r])) validmask |= 1u << r;
     }
-    goff[tid] = tile_off[(size_t)blockIdx.x * RS_BINS + tid] + chunk_off[(size_t)(blockIdx.x / RS_CH) * RS_BINS + tid];
+    if (tid < RS_BINS) {
+        goff[tid] = tile_off[(size_t)blockIdx.x * RS_BINS + tid] + chunk_off[(size_t)(blockIdx.x / RS_CH) * RS_BINS + tid];
 #pragma unroll
-    for (int w = 0; w < WAVES; w++) wpos[w][tid] = 0;
+        for (int w = 0; w < WAVES; w++) wpos[w][tid] = 0;
+    }
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < R; r++)
         if ((validmask >> r) & 1u) atomicAdd(&wpos[wave][(K[r] >> in.shift) & 255u], 1u);
     __syncthreads();
     // thread tid = digit: tile-local exclusive prefix over digits (wave-0 shuffle scan of 4 digits/lane)
-    {
+    if (tid < RS_BINS) {
         uint32_t cnt = 0;
 #pragma unroll
         for (int w = 0; w < WAVES; w++) cnt += wpos[w][tid];
@@ -189,7 +191,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(RsIn in, const uint32
         if (lane == 63) total = incl;
     }
     __syncthreads();
-    {
+    if (tid < RS_BINS) {
         uint32_t p = lstart[tid];
 #pragma unroll
         for (int w = 0; w < WAVES; w++) {
@@ -371,8 +373,14 @@ int msm_radix_sort(const uint32_t* digits, size_t E, size_t npw, uint32_t B, uin
     *keys_out = S.keys[cur ^ 1].as<uint32_t>();
     *vals_out = S.vals[cur ^ 1].as<uint32_t>();
     *count_out = S.count.as<const uint32_t>();
-    hipLaunchKernelGGL(k_bucket_starts, dim3((unsigned)((E + 1 + 255) / 256)), dim3(256), 0, s, *keys_out,
-                       S.count.as<const uint32_t>(), NB, E, bstart);
+    if (bstart) HALO_CHECK(msm_bucket_starts(*keys_out, S.count.as<const uint32_t>(), NB, E, bstart, s));
+    HALO_HIP(hipGetLastError());
+    return HALO_OK;
+}
+
+int msm_bucket_starts(const uint32_t* keys, const uint32_t* count, size_t NB, size_t E, uint32_t* bstart, hipStream_t s) {
+    hipLaunchKernelGGL(k_bucket_starts, dim3((unsigned)((E + 1 + 255) / 256)), dim3(256), 0, s, keys, count, NB, E,
+                       bstart);
     HALO_HIP(hipGetLastError());
     return HALO_OK;
 }

@@ -127,6 +127,9 @@ int halo_point_sum_dev(halo_curve_t curve, const void* d_pts, size_t k, size_t s
                        void* stream);
 /* Window size the device MSM uses for n points. */
 int halo_msm_window_bits(size_t n);
+/* Window size of the resident SRS's window-shifted copies (halo_srs_precompute_windows), or 0 when
+ * they are not built (MSMs against the resident SRS then use halo_msm_window_bits). */
+int halo_srs_window_bits(halo_curve_t curve);
 
 /* ------------------------------------------------------------------ a5/a6/a7: NTT
  * Radix-2 domain of size N = 2^log_n, omega = 5^((p-1)/N) (ark-poly Radix2EvaluationDomain,

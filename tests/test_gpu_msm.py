@@ -51,6 +51,9 @@ def test_msm_vs_c_oracle(hal, corc, cname, cid):
             sc[1] = fe([c.scalar - 1], c.scalar)[0]             # r - 1
             sc[2] = sc[3]                                       # repeated scalar
             sc[4] = fe([1 << 15], c.scalar)[0]                  # digit on a window boundary
+            sc[5] = fe([(c.scalar - 1) // 2], c.scalar)[0]      # largest scalar kept as is
+            sc[6] = fe([(c.scalar + 1) // 2], c.scalar)[0]      # smallest scalar folded to p - s
+            sc[7] = fe([1], c.scalar)[0]
         exp = corc.msm(cname, g[:n], sc) if n else np.zeros(8, dtype=np.uint64)
         assert np.array_equal(group.point_dot_affine(sc, g[:n], cname), exp), n
 
@@ -116,6 +119,8 @@ def test_pcdl_commit_reference_srs(hal, golden, corc, cname, cid):
         group.PublicParams.upload(cname, g, S, Hh, precompute_windows=pre)
         for d in (0, 1, 255, 4095, n - 1):
             coeffs = rand_sc(d + 1, d)
+            if d >= 7:  # scalars around p / 2 (k_digits folds s > p / 2 to p - s), 0, 1, p - 1
+                coeffs[:8] = fe([(r - 1) // 2, (r + 1) // 2, 0, 1, r - 1, r - 2, (r - 1) // 2 + 2, 1 << 254], r)
             exp = corc.msm(cname, g[: d + 1], coeffs)
             assert np.array_equal(pcdl.commit(coeffs, d, None, cname), exp), (pre, d)
         w = rand_sc(1, 9)
@@ -175,6 +180,29 @@ def test_msm_2p22_synthetic_srs_known_logs(hal):
     for j in range(n):
         acc += int.from_bytes(sb[32 * j:32 * j + 32], "little") * int.from_bytes(kb[32 * j:32 * j + 32], "little")
     acc = acc * pow(1 << 256, -1, r) % r  # scalars are Montgomery: s = S / 2^256
+    assert list(got) == P.point_to_wrapped(c, P.mul_fast(c, acc, c.generator))
+
+
+def test_msm_2p20_all_equal_scalars_shifted(hal):
+    """Worst-case bucket skew on the window-shifted path: every scalar equal, so each window's digit
+    puts all 2^20 points in one bucket (exercises the chunk-group merge, k_group_sums).  Expected:
+    (s * sum_j k_j) G over the synthetic SRS; also a half-skewed mix (two distinct scalars)."""
+    c = P.PALLAS
+    r = c.scalar
+    n = 1 << 20
+    seed = 5
+    group.PublicParams.synthesize("pallas", n, seed, precompute_windows=True)
+    k = synth_scalars_np(seed, n)
+    kb = k.tobytes()
+    ks = [int.from_bytes(kb[32 * j:32 * j + 32], "little") for j in range(n)]
+    s1 = fe([r - 12345], r)[0]
+    s2 = fe([(1 << 200) + 7], r)[0]
+    sc = np.ascontiguousarray(np.repeat(s1[None, :], n, axis=0))
+    got = pcdl.commit(sc, n - 1, None, "pallas")
+    assert list(got) == P.point_to_wrapped(c, P.mul_fast(c, (r - 12345) * sum(ks) % r, c.generator))
+    sc[n // 3:] = s2
+    got = pcdl.commit(sc, n - 1, None, "pallas")
+    acc = ((r - 12345) * sum(ks[: n // 3]) + ((1 << 200) + 7) * sum(ks[n // 3:])) % r
     assert list(got) == P.point_to_wrapped(c, P.mul_fast(c, acc, c.generator))
 
 
