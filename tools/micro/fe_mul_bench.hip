@@ -51,12 +51,49 @@ __device__ __forceinline__ Fe<C> fe_mul_asm(const Fe<C>& a, const Fe<C>& b) {
     return r;
 }
 
+// two interleaved chains per column (independent neighbours: no dependent-mad hazard nop)
+template <class C>
+__device__ __forceinline__ Fe<C> fe_mul_asm2(const Fe<C>& a, const Fe<C>& b) {
+    uint32_t m[NLIMB];
+    Fe<C> r;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 2 * NLIMB - 1; k++) {
+        uint64_t acc2 = 0;
+        int par = 0;
+#pragma unroll
+        for (int i = 0; i < NLIMB; i++) {
+            const int j = k - i;
+            if (j < 0 || j >= NLIMB) continue;
+            if (par++ & 1) acc2 = mad64(a.v[i], b.v[j], acc2); else acc = mad64(a.v[i], b.v[j], acc);
+        }
+#pragma unroll
+        for (int i = 0; i < NLIMB; i++) {
+            const int j = k - i;
+            if (i >= k || j < 1 || j >= NLIMB || C::P[j] == 0) continue;
+            if (par++ & 1) acc2 = mad64s(m[i], C::P[j], acc2); else acc = mad64s(m[i], C::P[j], acc);
+        }
+        acc += acc2;
+        if (k < NLIMB) {
+            const uint32_t mk = (0u - (uint32_t)acc) & LIMB_MASK;
+            m[k] = mk;
+            acc += mk;
+            acc >>= LIMB_BITS;
+        } else {
+            r.v[k - NLIMB] = (uint32_t)acc & LIMB_MASK;
+            acc >>= LIMB_BITS;
+        }
+    }
+    r.v[NLIMB - 1] = (uint32_t)acc;
+    return r;
+}
+
 template <int V>
 __global__ void bench(uint4* d, int iters) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     Fe<FqCfg> a = fe_load<FqCfg>(d + 4 * i), b = fe_load<FqCfg>(d + 4 * i + 2);
     for (int k = 0; k < iters; k++) {
-        Fe<FqCfg> c = V == 0 ? fe_mul(a, b) : fe_mul_asm(a, b);
+        Fe<FqCfg> c = V == 0 ? fe_mul(a, b) : (V == 1 ? fe_mul_asm(a, b) : fe_mul_asm2(a, b));
         b = a;
         a = c;
     }
@@ -88,6 +125,8 @@ int main() {
         double t0 = timeit(bench<0>, d, blocks, threads, iters);
         CHECK(hipMemcpy(d, h.data(), h.size() * 4, hipMemcpyHostToDevice));
         double t1 = timeit(bench<1>, d, blocks, threads, iters);
+        CHECK(hipMemcpy(d, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+        double t2 = timeit(bench<2>, d, blocks, threads, iters);
         std::vector<uint32_t> o0(n * 16), o1(n * 16);
         CHECK(hipMemcpy(d, h.data(), h.size() * 4, hipMemcpyHostToDevice));
         hipLaunchKernelGGL(bench<0>, dim3(blocks), dim3(threads), 0, 0, d, 7);
@@ -95,8 +134,13 @@ int main() {
         CHECK(hipMemcpy(d, h.data(), h.size() * 4, hipMemcpyHostToDevice));
         hipLaunchKernelGGL(bench<1>, dim3(blocks), dim3(threads), 0, 0, d, 7);
         CHECK(hipMemcpy(o1.data(), d, h.size() * 4, hipMemcpyDeviceToHost));
-        printf("waves/SIMD %d: compiler %.3e modmul/s, asm-chain %.3e modmul/s, same=%d\n", wps,
-               n * (double)iters / (t0 * 1e-3), n * (double)iters / (t1 * 1e-3), (int)(o0 == o1));
+        std::vector<uint32_t> o2(n * 16);
+        CHECK(hipMemcpy(d, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+        hipLaunchKernelGGL(bench<2>, dim3(blocks), dim3(threads), 0, 0, d, 7);
+        CHECK(hipMemcpy(o2.data(), d, h.size() * 4, hipMemcpyDeviceToHost));
+        printf("waves/SIMD %d: fe_mul %.3e, asm-chain %.3e, asm-2chain %.3e modmul/s, same=%d%d\n", wps,
+               n * (double)iters / (t0 * 1e-3), n * (double)iters / (t1 * 1e-3), n * (double)iters / (t2 * 1e-3),
+               (int)(o0 == o1), (int)(o0 == o2));
         CHECK(hipFree(d));
     }
     return 0;
