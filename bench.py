@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--sizes", default="24", help="extra MSM / NTT sizes (log2, comma separated) under extra.sizes")
+    ap.add_argument("--dist-ntt-logn", type=int, default=24, help="distributed single NTT size (N > 1 only; 0 = off)")
     return ap.parse_args()
 
 
@@ -199,6 +200,41 @@ def main():
         sizes[f"ntt_2^{lg}"] = measure_ntt(lg, nrep=4)
         torch.cuda.empty_cache()
 
+    # ---- distributed single NTT (four-step, RCCL all-to-all; halo_amd.dist.sharded_ntt), N > 1 only
+    dist_ntt = None
+    if world > 1 and args.dist_ntt_logn:
+        from halo_amd.dist import GpuNttOps, sharded_ntt, torch_alltoall
+        lg = args.dist_ntt_logn
+        per = (1 << lg) // world
+        xl = torch.randint(-(2**63), 2**63 - 1, (per, 4), dtype=torch.int64, device="cuda", generator=gen)
+        xl[:, 3] &= 0x0FFFFFFFFFFFFFFF
+        ops = GpuNttOps(H.FP)
+        a2a = torch_alltoall(dist)
+        y = sharded_ntt(xl, lg, False, ops, rank, world, a2a)
+        z = sharded_ntt(y, lg, True, ops, rank, world, a2a)
+        torch.cuda.synchronize()
+        ok = torch.tensor([int(torch.equal(z, xl))], device="cuda")
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        reps = 5
+        dist.barrier()
+        torch.cuda.synchronize()
+        a0 = time.perf_counter()
+        for _ in range(reps):
+            y = sharded_ntt(xl, lg, False, ops, rank, world, a2a)
+            z = sharded_ntt(y, lg, True, ops, rank, world, a2a)
+        torch.cuda.synchronize()
+        dist.barrier()
+        tt = torch.tensor([time.perf_counter() - a0], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        pair_ms = float(tt.item()) * 1e3 / reps
+        dist_ntt = {
+            "workload": f"distributed ntt+intt_2^{lg}_fp over {world} ranks (four-step, 3 RCCL all-to-alls each way)",
+            "pair_ms": pair_ms,
+            "elems_per_s_pair": (1 << lg) / (pair_ms * 1e-3),
+            "roundtrip_bit_exact": bool(ok.item()),
+        }
+        del xl, y, z
+
     if rank != 0:
         if world > 1:
             dist.barrier()
@@ -262,6 +298,7 @@ def main():
             "pipelined_equals_sync": sync_ok,
             "ntt": ntt_main,
             "sizes": sizes,
+            "dist_ntt": dist_ntt,
         },
     }
     print(json.dumps(line))

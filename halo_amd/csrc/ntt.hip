@@ -300,6 +300,60 @@ __global__ void k_fold(const uint4* in, size_t len, uint4* out, size_t N) {
     fe_to_ark(out + 2 * i, acc);
 }
 
+// Four-step twiddle: x[a][b] (ark) *= omega^((row0 + a)(col0 + b) mod N), omega from the two-level
+// tables (lo: omega^e for e < 2^lo_bits, hi: omega^(e 2^lo_bits)).
+template <class F>
+__global__ void k_twiddle_mat(uint4* x, size_t rows, size_t cols, size_t row0, size_t col0, uint32_t logn,
+                              const uint4* lo, const uint4* hi, uint32_t lo_bits) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= rows * cols) return;
+    const size_t a = i / cols, b = i % cols;
+    const uint64_t mask = ((uint64_t)1 << logn) - 1;
+    const uint64_t e = (uint64_t)(((unsigned __int128)(row0 + a) * (col0 + b)) & mask);
+    Fe<F> w = fe_load<F>(lo + 2 * (e & (((uint64_t)1 << lo_bits) - 1)));
+    const uint64_t eh = e >> lo_bits;
+    if (eh) w = fe_mul(w, fe_load<F>(hi + 2 * eh));
+    fe_to_ark(x + 2 * i, fe_mul(fe_from_ark<F>(x + 2 * i), w));
+}
+
+// Batched transpose of 32-byte elements through LDS tiles (32 x 32 elements, padded).
+__global__ __launch_bounds__(256) void k_transpose32(const uint4* src, uint4* dst, size_t rows, size_t cols) {
+    __shared__ uint4 t[32][33][2];
+    const size_t s = blockIdx.z;
+    const size_t r0 = (size_t)blockIdx.y * 32, c0 = (size_t)blockIdx.x * 32;
+    const uint4* S = src + 2 * s * rows * cols;
+    uint4* D = dst + 2 * s * rows * cols;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+    for (int k = ty; k < 32; k += 8) {
+        const size_t r = r0 + k, c = c0 + tx;
+        if (r < rows && c < cols) {
+            t[k][tx][0] = S[2 * (r * cols + c)];
+            t[k][tx][1] = S[2 * (r * cols + c) + 1];
+        }
+    }
+    __syncthreads();
+    for (int k = ty; k < 32; k += 8) {
+        const size_t c = c0 + k, r = r0 + tx;
+        if (r < rows && c < cols) {
+            D[2 * (c * rows + r)] = t[tx][k][0];
+            D[2 * (c * rows + r) + 1] = t[tx][k][1];
+        }
+    }
+}
+
+// Transpose of matrices whose elements are runs of `run` 32-byte values (block permutation)
+__global__ void k_transpose_runs(const uint4* src, uint4* dst, size_t batch, size_t rows, size_t cols, size_t run) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // destination 32-byte element
+    const size_t per = rows * cols * run;
+    if (i >= batch * per) return;
+    const size_t s = i / per, rem = i % per;
+    const size_t j = rem % run, q = rem / run;  // q = c * rows + r in the destination
+    const size_t c = q / rows, r = q % rows;
+    const size_t from = s * per + (r * cols + c) * run + j;
+    dst[2 * i] = src[2 * from];
+    dst[2 * i + 1] = src[2 * from + 1];
+}
+
 // ---------------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------------
@@ -561,4 +615,47 @@ extern "C" int halo_ntt_dev(halo_field_t field, void* d_data, unsigned log_n, si
     HALO_CHECK(st->scratch[5].reserve(batch * N * 32));
     return ntt_device_dispatch(st, field, d_data, d_data, st->scratch[4].ptr, log_n, batch, inverse, s,
                                st->scratch[5].ptr);
+}
+
+extern "C" int halo_ntt_twiddle_dev(halo_field_t field, void* d_data, unsigned log_n, size_t rows, size_t cols,
+                                    size_t row0, size_t col0, int inverse, void* stream) {
+    clear_error();
+    HALO_CHECK(check_field(field));
+    if (!d_data && rows * cols) return set_error(HALO_EINVAL, "halo_ntt_twiddle_dev: null buffer");
+    if (log_n == 0 || log_n > 30) return set_error(HALO_EINVAL, "halo_ntt_twiddle_dev: log_n %u out of range", log_n);
+    if (!rows || !cols) return HALO_OK;
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    hipStream_t s = (hipStream_t)stream;
+    const size_t cnt = rows * cols;
+    const unsigned thr = 256, blocks = (unsigned)((cnt + thr - 1) / thr);
+    DISPATCH_FIELD(field, F, {
+        DeviceState::Twiddles* tw = nullptr;
+        HALO_CHECK(get_twiddles<F>(st, field, log_n, inverse ? 1 : 0, &tw, s));
+        hipLaunchKernelGGL(k_twiddle_mat<F>, dim3(blocks), dim3(thr), 0, s, (uint4*)d_data, rows, cols, row0, col0,
+                           log_n, tw->lo.as<const uint4>(), tw->hi.as<const uint4>(), (uint32_t)tw->lo_bits);
+    });
+    HALO_HIP(hipGetLastError());
+    return HALO_OK;
+}
+
+extern "C" int halo_transpose_dev(const void* d_src, void* d_dst, size_t batch, size_t rows, size_t cols, size_t run,
+                                  void* stream) {
+    clear_error();
+    if (!batch || !rows || !cols || !run) return HALO_OK;
+    if (!d_src || !d_dst || d_src == d_dst) return set_error(HALO_EINVAL, "halo_transpose_dev: bad buffers");
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    if (run == 1 && batch <= 65535 && (rows + 31) / 32 <= 65535) {
+        dim3 grid((unsigned)((cols + 31) / 32), (unsigned)((rows + 31) / 32), (unsigned)batch);
+        hipLaunchKernelGGL(k_transpose32, grid, dim3(256), 0, (hipStream_t)stream, (const uint4*)d_src,
+                           (uint4*)d_dst, rows, cols);
+    } else {
+        const size_t total = batch * rows * cols * run;
+        hipLaunchKernelGGL(k_transpose_runs, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                           (const uint4*)d_src, (uint4*)d_dst, batch, rows, cols, run);
+    }
+    HALO_HIP(hipGetLastError());
+    return HALO_OK;
 }

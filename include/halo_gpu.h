@@ -151,6 +151,15 @@ int halo_poly_mul(halo_field_t field, const halo_fe_t* a, size_t la, const halo_
 /* Batched device NTT: `batch` contiguous transforms of size 2^log_n at d_data, in place. */
 int halo_ntt_dev(halo_field_t field, void* d_data, unsigned log_n, size_t batch, int inverse,
                  void* stream);
+/* Distributed-NTT building blocks (four-step decomposition, halo_amd/dist.py sharded_ntt; SURVEY
+ * §8e).  halo_ntt_twiddle_dev: element (a, b) of the rows x cols matrix at d_data (ark format) is
+ * multiplied by omega_N^((row0 + a)(col0 + b)) (omega^-1 when inverse), N = 2^log_n.
+ * halo_transpose_dev: for `batch` consecutive rows x cols matrices whose elements are runs of `run`
+ * 32-byte field elements: dst[s][b][a] = src[s][a][b]. */
+int halo_ntt_twiddle_dev(halo_field_t field, void* d_data, unsigned log_n, size_t rows, size_t cols, size_t row0,
+                         size_t col0, int inverse, void* stream);
+int halo_transpose_dev(const void* d_src, void* d_dst, size_t batch, size_t rows, size_t cols, size_t run,
+                       void* stream);
 
 /* ------------------------------------------------------------------ a8: evaluation / dots */
 /* DensePolynomial::evaluate (Horner; pcdl.rs:49,471), k polynomials at one point z. */

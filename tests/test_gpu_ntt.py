@@ -157,3 +157,54 @@ def test_poly_mul_edge(hal):
     assert poly.poly_mul(np.zeros((0, 4), dtype=np.uint64), fe([1, 2], m)).shape == (0, 4)
     assert unfe(poly.poly_mul(fe([3], m), fe([5], m)), m) == [15]
     assert unfe(poly.poly_mul(fe([m - 1, 1], m), fe([1, 1], m)), m) == [m - 1, 0, 1]  # (X-1)(X+1) = X^2 - 1
+
+
+def test_sharded_ntt_virtual_ranks(hal, corc):
+    """The distributed four-step NTT (halo_amd.dist) with the device primitives (batched NTT,
+    twiddle, transposes) and P virtual ranks on one GPU, bit-exact vs the oracle NTT."""
+    import torch
+
+    from halo_amd import _lib as H
+    from halo_amd.dist import GpuNttOps, sharded_ntt_virtual
+
+    ops = GpuNttOps(H.FP)
+    rng = np.random.default_rng(11)
+    for logn, world in ((6, 2), (9, 4), (12, 8), (16, 4)):
+        N = 1 << logn
+        x = rng.integers(0, 2**62, size=(N, 4), dtype=np.uint64)
+        xd = torch.from_numpy(x.view(np.int64).copy()).cuda()
+        y = sharded_ntt_virtual(xd, logn, False, ops, world)
+        assert np.array_equal(y.cpu().numpy().view(np.uint64), corc.ntt("fp", x)), (logn, world)
+        z = sharded_ntt_virtual(y, logn, True, ops, world)
+        assert np.array_equal(z.cpu().numpy().view(np.uint64), x), (logn, world)
+
+
+def test_transpose_and_twiddle_dev(hal, corc):
+    import ctypes
+
+    import pasta as P
+    import torch
+
+    from halo_amd import _lib as H
+    L = H.load()
+    rng = np.random.default_rng(3)
+    for (b, r, c, run) in ((1, 37, 45, 1), (3, 64, 33, 1), (2, 5, 7, 3)):
+        x = torch.from_numpy(rng.integers(0, 2**62, size=(b * r * c * run, 4), dtype=np.int64)).cuda()
+        y = torch.empty_like(x)
+        H.check(L.halo_transpose_dev(ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(y.data_ptr()), b, r, c, run, None))
+        exp = x.view(b, r, c, run, 4).permute(0, 2, 1, 3, 4).reshape(-1, 4)
+        assert torch.equal(y, exp)
+    m = P.FP_MODULUS
+    logn, rows, cols, row0, col0 = 10, 6, 9, 5, 3
+    x = rng.integers(0, 2**62, size=(rows * cols, 4), dtype=np.uint64)
+    for inv in (0, 1):
+        d = torch.from_numpy(x.view(np.int64).copy()).cuda()
+        H.check(L.halo_ntt_twiddle_dev(H.FP, ctypes.c_void_p(d.data_ptr()), logn, rows, cols, row0, col0, inv, None))
+        w = pow(5, (m - 1) >> logn, m)
+        if inv:
+            w = pow(w, -1, m)
+        got = d.cpu().numpy().view(np.uint64)
+        for i in range(rows * cols):
+            a, bb = divmod(i, cols)
+            v = P.from_mont(P.limbs_to_int(x[i]), m) * pow(w, (row0 + a) * (col0 + bb), m) % m
+            assert P.from_mont(P.limbs_to_int(got[i]), m) == v
