@@ -571,3 +571,126 @@ extern "C" int halo_ipa_fold_host(halo_curve_t curve, halo_wrapped_point_t* gs, 
     HALO_CHECK(copy_d2h(zs, st->scratch[3].ptr, m * 32, s));
     return HALO_OK;
 }
+
+// ---------------------------------------------------------------------------------------------
+// h(X) coefficients and the decider commitment.
+//
+// HPoly::get_poly (crates/accumulation/src/pcdl.rs:198-219) builds
+//   h(X) = prod_{i < lg n} (1 + xi_{lg n - i} X^(2^i))
+// with lg n growing FFT multiplications; its coefficient j is simply the product of
+// xi_{lg n - b} over the set bits b of j (the identity pcdl.rs:735-758 tests).  Generated directly:
+// j = hi * 2^LB + lo, coef[j] = T_lo[lo] * T_hi[hi] (two small tables, one multiplication per
+// coefficient).  The ASDL combination sum_i alpha_i h_i(X) (acc.rs:89) folds alpha_i into T_hi,i.
+// ---------------------------------------------------------------------------------------------
+template <class F>
+__global__ void k_hpoly_tables(const uint4* xis_ark, size_t k, uint32_t lg_n, uint32_t lb, const uint4* alphas_ark,
+                               uint4* t_lo, uint4* t_hi) {
+    const size_t nlo = (size_t)1 << lb, nhi = (size_t)1 << (lg_n - lb);
+    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= k * (nlo + nhi)) return;
+    const size_t i = idx / (nlo + nhi), x = idx % (nlo + nhi);
+    const uint4* xi = xis_ark + 2 * i * (lg_n + 1);
+    Fe<F> v = fe_one<F>();
+    if (x < nlo) {
+        for (uint32_t b = 0; b < lb; b++)
+            if ((x >> b) & 1) v = fe_mul(v, fe_from_ark<F>(xi + 2 * (lg_n - b)));
+        fe_store(t_lo + 2 * (i * nlo + x), v);
+    } else {
+        const size_t y = x - nlo;
+        if (alphas_ark) v = fe_from_ark<F>(alphas_ark + 2 * i);
+        for (uint32_t b = 0; b < lg_n - lb; b++)
+            if ((y >> b) & 1) v = fe_mul(v, fe_from_ark<F>(xi + 2 * (lg_n - lb - b)));
+        fe_store(t_hi + 2 * (i * nhi + y), v);
+    }
+}
+
+template <class F>
+__global__ void k_hpoly_coeffs(const uint4* t_lo, const uint4* t_hi, size_t k, uint32_t lg_n, uint32_t lb,
+                               uint4* out_ark) {
+    const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >> lg_n) return;
+    const size_t nlo = (size_t)1 << lb, nhi = (size_t)1 << (lg_n - lb);
+    const size_t lo = j & (nlo - 1), hi = j >> lb;
+    Fe<F> acc = fe_zero<F>();
+    for (size_t i = 0; i < k; i++)
+        acc = fe_add(acc, fe_mul(fe_load<F>(t_lo + 2 * (i * nlo + lo)), fe_load<F>(t_hi + 2 * (i * nhi + hi))));
+    fe_to_ark(out_ark + 2 * j, acc);
+}
+
+// k h-polynomials (xis: k rows of n_xis ark elements) -> sum_i alpha_i h_i coefficients (ark) at d_out
+// (2^(n_xis - 1) entries), on stream s.  Uses scratch[6] for the xis/alphas and tables.
+static int hpoly_device(DeviceState* st, int field, const halo_fe_t* xis, size_t k, size_t n_xis,
+                        const halo_fe_t* alphas, void* d_out, hipStream_t s) {
+    const uint32_t lg_n = (uint32_t)(n_xis - 1);
+    const uint32_t lb = lg_n / 2;
+    const size_t nlo = (size_t)1 << lb, nhi = (size_t)1 << (lg_n - lb);
+    const size_t in_elems = k * n_xis + (alphas ? k : 0);
+    HALO_CHECK(st->scratch[6].reserve((in_elems + k * (nlo + nhi)) * 32));
+    uint4* d_xis = st->scratch[6].as<uint4>();
+    uint4* d_alpha = alphas ? d_xis + 2 * k * n_xis : nullptr;
+    uint4* t_lo = d_xis + 2 * in_elems;
+    uint4* t_hi = t_lo + 2 * k * nlo;
+    HALO_CHECK(copy_h2d(d_xis, xis, k * n_xis * 32, s));
+    if (alphas) HALO_CHECK(copy_h2d(d_alpha, alphas, k * 32, s));
+    DISPATCH_FIELD(field, F, {
+        hipLaunchKernelGGL(k_hpoly_tables<F>, dim3(gridn(k * (nlo + nhi), 128)), dim3(128), 0, s, (const uint4*)d_xis, k,
+                           lg_n, lb, (const uint4*)d_alpha, t_lo, t_hi);
+        hipLaunchKernelGGL(k_hpoly_coeffs<F>, dim3(gridn((size_t)1 << lg_n, 256)), dim3(256), 0, s, (const uint4*)t_lo,
+                           (const uint4*)t_hi, k, lg_n, lb, (uint4*)d_out);
+    });
+    HALO_HIP(hipGetLastError());
+    return HALO_OK;
+}
+
+extern "C" int halo_hpoly_combine(halo_field_t field, const halo_fe_t* xis, size_t k, size_t n_xis,
+                                  const halo_fe_t* alphas, halo_fe_t* out, size_t* out_len) {
+    clear_error();
+    HALO_CHECK(check_field_i(field));
+    if (n_xis < 1 || n_xis > 29) return set_error(HALO_EINVAL, "halo_hpoly: n_xis %zu out of range [1, 29]", n_xis);
+    if (!k || !xis || !out) return set_error(HALO_EINVAL, "halo_hpoly: null buffer or k = 0");
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    hipStream_t s = 0;
+    const size_t n = (size_t)1 << (n_xis - 1);
+    HALO_CHECK(st->scratch[7].reserve(n * 32));
+    HALO_CHECK(hpoly_device(st, field, xis, k, n_xis, alphas, st->scratch[7].ptr, s));
+    HALO_CHECK(copy_d2h(out, st->scratch[7].ptr, n * 32, s));
+    if (out_len) {  // DensePolynomial trims trailing zeros
+        size_t m = n;
+        while (m > 0 && !(out[m - 1].l[0] | out[m - 1].l[1] | out[m - 1].l[2] | out[m - 1].l[3])) m--;
+        *out_len = m;
+    }
+    return HALO_OK;
+}
+
+extern "C" int halo_hpoly_coeffs(halo_field_t field, const halo_fe_t* xis, size_t n_xis, halo_fe_t* out) {
+    return halo_hpoly_combine(field, xis, 1, n_xis, nullptr, out, nullptr);
+}
+
+// pcdl::check step 5 (pcdl.rs:579): U' = pedersen::commit(None, &pp.Gs[0..d+1], &h.get_poly().coeffs),
+// computed without leaving the device (h coefficients -> resident-SRS MSM).
+extern "C" int halo_pcdl_decider_commit(halo_curve_t curve, const halo_fe_t* xis, size_t n_xis, size_t d,
+                                        halo_wrapped_point_t* out) {
+    clear_error();
+    if (curve != HALO_PALLAS && curve != HALO_VESTA) return set_error(HALO_EINVAL, "unknown curve id %d", (int)curve);
+    if (n_xis < 1 || n_xis > 29) return set_error(HALO_EINVAL, "halo_pcdl_decider_commit: n_xis %zu out of range", n_xis);
+    if (!xis || !out) return set_error(HALO_EINVAL, "halo_pcdl_decider_commit: null buffer");
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    SrsState& srs = st->srs[curve];
+    const size_t n = (size_t)1 << (n_xis - 1);
+    if (d + 1 > srs.n)
+        return set_error(HALO_ESRSRANGE, "range end index %zu out of range for slice of length %zu", d + 1, srs.n);
+    // all coefficients are products of nonzero challenges: no trailing zeros, ms.len() = n
+    if (d + 1 < n)
+        return set_error(HALO_ELENGTH, "ms must be larger than Gs: (Gs: %zu), (ms: %zu)", d + 1, n);
+    hipStream_t s = 0;
+    HALO_CHECK(st->scratch[7].reserve(n * 32 + 64));
+    const int field = (curve == HALO_PALLAS) ? HALO_FP : HALO_FQ;
+    HALO_CHECK(hpoly_device(st, field, xis, 1, n_xis, nullptr, st->scratch[7].ptr, s));
+    char* d_out = (char*)st->scratch[7].ptr + n * 32;
+    HALO_CHECK(msm_srs_device(st, curve, st->scratch[7].ptr, n, nullptr, d_out, s));
+    return copy_d2h(out, d_out, 64, s);
+}

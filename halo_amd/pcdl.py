@@ -84,3 +84,44 @@ def ipa_rounds(cs, z, H_prime, challenge: Callable, inverse: Callable, curve="pa
         ses.fold(xi, inverse(xi))
     U, c = ses.end()
     return Ls, Rs, U, c
+
+
+class HPoly:
+    """pcdl.rs:184-229 HPoly: h(X) = prod_{i < lg n} (1 + xi_{lg n - i} X^(2^i)) from the round
+    challenges xis (ark Montgomery scalars, xis[0] unused by h as in the reference)."""
+
+    def __init__(self, xis, curve="pallas"):
+        self.curve = _curve(curve)
+        self.field = H.FP if self.curve == 0 else H.FQ
+        self.xis = H.fe_array(xis)
+
+    def get_poly(self) -> np.ndarray:
+        """Coefficients (2^(len(xis) - 1) of them), generated on the device (halo_hpoly_coeffs)."""
+        H.ensure_device()
+        n = 1 << (len(self.xis) - 1)
+        out = np.zeros((n, 4), dtype=np.uint64)
+        H.check(H.load().halo_hpoly_coeffs(self.field, H.ptr(self.xis), len(self.xis), H.ptr(out)))
+        return out
+
+    @staticmethod
+    def combine(hs: list["HPoly"], alphas) -> np.ndarray:
+        """sum_i alphas[i] * h_i(X) (acc.rs:89), trimmed like DensePolynomial."""
+        H.ensure_device()
+        k = len(hs)
+        xis = np.ascontiguousarray(np.concatenate([h.xis for h in hs]))
+        a = H.fe_array(alphas, k)
+        n = 1 << (len(hs[0].xis) - 1)
+        out = np.zeros((n, 4), dtype=np.uint64)
+        m = ctypes.c_size_t(0)
+        H.check(H.load().halo_hpoly_combine(hs[0].field, H.ptr(xis), k, len(hs[0].xis), H.ptr(a), H.ptr(out),
+                                            ctypes.byref(m)))
+        return out[: m.value]
+
+
+def decider_commit(xis, d: int, curve="pallas") -> np.ndarray:
+    """pcdl.rs:579 (check step 5): pedersen::commit(None, &pp.Gs[0..d+1], &h.get_poly().coeffs)."""
+    H.ensure_device()
+    x = H.fe_array(xis)
+    out = np.zeros(8, dtype=np.uint64)
+    H.check(H.load().halo_pcdl_decider_commit(_curve(curve), H.ptr(x), len(x), d, H.ptr(out)))
+    return out

@@ -161,6 +161,19 @@ int halo_ntt_twiddle_dev(halo_field_t field, void* d_data, unsigned log_n, size_
 int halo_transpose_dev(const void* d_src, void* d_dst, size_t batch, size_t rows, size_t cols, size_t run,
                        void* stream);
 
+/* ------------------------------------------------------------------ f4: h(X) and the decider MSM
+ * HPoly::get_poly (pcdl.rs:198-219): coefficients of h(X) = prod_{i<lg n} (1 + xi_{lg n-i} X^(2^i)),
+ * lg n = n_xis - 1, generated directly (coef[j] = product of xi_{lg n-b} over the set bits b of j). */
+int halo_hpoly_coeffs(halo_field_t field, const halo_fe_t* xis, size_t n_xis, halo_fe_t* out);
+/* sum_i alphas[i] * h_i(X) over k h-polynomials (xis: k rows of n_xis; acc.rs:89); alphas NULL = 1;
+ * *out_len (if not NULL) = trimmed length. */
+int halo_hpoly_combine(halo_field_t field, const halo_fe_t* xis, size_t k, size_t n_xis, const halo_fe_t* alphas,
+                       halo_fe_t* out, size_t* out_len);
+/* pcdl::check step 5 (pcdl.rs:579): pedersen::commit(None, &pp.Gs[0..d+1], &h.get_poly().coeffs)
+ * against the resident SRS, the coefficients never leaving the device. */
+int halo_pcdl_decider_commit(halo_curve_t curve, const halo_fe_t* xis, size_t n_xis, size_t d,
+                             halo_wrapped_point_t* out);
+
 /* ------------------------------------------------------------------ a8: evaluation / dots */
 /* DensePolynomial::evaluate (Horner; pcdl.rs:49,471), k polynomials at one point z. */
 int halo_poly_eval_batch(halo_field_t field, const halo_fe_t* const* polys, const size_t* lens,

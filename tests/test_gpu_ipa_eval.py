@@ -147,3 +147,52 @@ def test_scalar_dot_and_powers(hal, corc, tag):
     z = 31337
     pw = group.construct_powers(fe([z], m), 1000, tag)
     assert unfe(pw, m) == P.construct_powers(z, 1000, m)
+
+
+# ---- h(X) coefficients (HPoly::get_poly) and the decider commitment --------
+@pytest.mark.parametrize("tag,cname", [("fp", "pallas"), ("fq", "vesta")])
+def test_hpoly_golden(hal, golden, tag, cname):
+    """pcdl.rs:735-758 test_construct_h_with_degree_7 on the device."""
+    got = pcdl.HPoly(golden[f"hpoly_{tag}_xis"], cname).get_poly()
+    assert np.array_equal(got, golden[f"hpoly_{tag}_coeffs"])
+
+
+@pytest.mark.parametrize("cname", ["pallas", "vesta"])
+def test_hpoly_random_and_combine(hal, cname):
+    c = P.CURVES[cname]
+    r = c.scalar
+    rnd = random.Random(17)
+    for lg in (1, 2, 5, 11, 14):
+        xis = [rnd.randrange(1, r) for _ in range(lg + 1)]
+        assert unfe(pcdl.HPoly(fe(xis, r), cname).get_poly(), r) == P.h_coeffs(xis, r), lg
+    lg = 9
+    hs_x = [[rnd.randrange(1, r) for _ in range(lg + 1)] for _ in range(3)]
+    alphas = [rnd.randrange(r) for _ in range(3)]
+    got = pcdl.HPoly.combine([pcdl.HPoly(fe(x, r), cname) for x in hs_x], fe(alphas, r))
+    exp = [sum(a * h for a, h in zip(alphas, col)) % r for col in zip(*[P.h_coeffs(x, r) for x in hs_x])]
+    while exp and exp[-1] == 0:
+        exp.pop()
+    assert unfe(got, r) == exp
+
+
+@pytest.mark.parametrize("cname,cid", CURVES)
+def test_decider_commit_equals_folded_U(hal, golden, corc, cname, cid):
+    """pcdl::check step 5 (pcdl.rs:579): U == pedersen::commit(Gs[0..d+1], h.get_poly().coeffs) for
+    the U that the IPA fold produces from the same challenges (the identity test_u_check pins)."""
+    c = P.CURVES[cname]
+    r = c.scalar
+    # the reference's own u-check case: xis = [0, 1, 2, 3] over G[0..8]
+    g = corc.srs_generate(cname, 1 << 12)
+    group.PublicParams.upload(cname, g, precompute_windows=False)
+    assert np.array_equal(pcdl.decider_commit(fe([0, 1, 2, 3], r), 7, cname), golden[f"ucheck_{cname}_U"][0])
+    # random challenges over 2^12 bases: fold on the device, then the decider MSM
+    rnd = random.Random(5)
+    lg = 12
+    xis = [rnd.randrange(1, r) for _ in range(lg + 1)]
+    ses = pcdl.IpaSession(np.zeros((1 << lg, 4), dtype=np.uint64), fe([5], r), g[0], cname)
+    for xi in xis[1:]:
+        ses.fold(fe([xi], r), fe([P.inv(xi, r)], r))
+    U, _ = ses.end()
+    assert np.array_equal(pcdl.decider_commit(fe(xis, r), (1 << lg) - 1, cname), U)
+    with pytest.raises(AssertionError, match=r"ms must be larger than Gs: \(Gs: 8\), \(ms: 4096\)"):
+        pcdl.decider_commit(fe(xis, r), 7, cname)
