@@ -694,3 +694,85 @@ extern "C" int halo_pcdl_decider_commit(halo_curve_t curve, const halo_fe_t* xis
     HALO_CHECK(msm_srs_device(st, curve, st->scratch[7].ptr, n, nullptr, d_out, s));
     return copy_d2h(out, d_out, 64, s);
 }
+
+// ---------------------------------------------------------------------------------------------
+// Trace::new's interpolate + commit batch (crates/plonk/src/circuit/trace.rs
+// :165-192): k evaluation vectors on the 2^log_n domain -> Evals::from_vec_and_domain (rotate right
+// by one, poly.rs:21-31) -> interpolate_by_ref (iNTT, trailing zeros trimmed) -> pcdl::commit(poly,
+// d, None).  One batched iNTT, then k resident-SRS MSMs enqueued back to back (pipelined: each
+// MSM's reduction tail overlaps the next one's accumulation), one host sync at the end.
+// ---------------------------------------------------------------------------------------------
+__global__ void k_rotate_right(const uint4* in, uint4* out, size_t k, size_t n) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= k * n) return;
+    const size_t r = i / n, j = i % n;
+    const size_t from = r * n + (j == 0 ? n - 1 : j - 1);
+    out[2 * i] = in[2 * from];
+    out[2 * i + 1] = in[2 * from + 1];
+}
+
+// lens[r] = 1 + index of the last nonzero element of row r (0 if all zero); one block per row
+__global__ __launch_bounds__(256) void k_row_lengths(const uint4* a, size_t n, uint32_t* lens) {
+    __shared__ uint32_t best;
+    if (threadIdx.x == 0) best = 0;
+    __syncthreads();
+    const uint4* row = a + 2 * (size_t)blockIdx.x * n;
+    uint32_t m = 0;
+    for (size_t j = threadIdx.x; j < n; j += 256) {
+        const uint4 x = row[2 * j], y = row[2 * j + 1];
+        if (x.x | x.y | x.z | x.w | y.x | y.y | y.z | y.w) m = (uint32_t)j + 1;
+    }
+    if (m) atomicMax(&best, m);
+    __syncthreads();
+    if (threadIdx.x == 0) lens[blockIdx.x] = best;
+}
+
+extern "C" int halo_trace_commit_batch(halo_curve_t curve, const halo_fe_t* evals, size_t k, unsigned log_n, size_t d,
+                                       halo_fe_t* coeffs_out, size_t* lens_out, halo_wrapped_point_t* commits_out) {
+    clear_error();
+    if (curve != HALO_PALLAS && curve != HALO_VESTA) return set_error(HALO_EINVAL, "unknown curve id %d", (int)curve);
+    if (!k) return HALO_OK;
+    if (!evals || !commits_out) return set_error(HALO_EINVAL, "halo_trace_commit_batch: null buffer");
+    if (log_n > 28) return set_error(HALO_EINVAL, "log_n %u too large", log_n);
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    SrsState& srs = st->srs[curve];
+    if (!srs.n) return set_error(HALO_ESRSRANGE, "no resident SRS: call halo_srs_upload first");
+    const size_t n = (size_t)1 << log_n, D = srs.n - 1, nc = d + 1;
+    if (!is_pow2(nc)) return set_error(HALO_ENOTPOW2, "n (%zu) is not a power of two", nc);
+    if (d > D) return set_error(HALO_ESRSRANGE, "d (%zu) <= D (%zu) (pp_len = %zu)", d, D, D + 1);
+    const int field = (curve == HALO_PALLAS) ? HALO_FP : HALO_FQ;
+    hipStream_t s = 0;
+    const size_t bytes = k * n * 32;
+    HALO_CHECK(st->scratch[0].reserve(bytes));
+    HALO_CHECK(st->scratch[1].reserve(bytes));
+    HALO_CHECK(st->scratch[2].reserve(bytes));
+    HALO_CHECK(st->scratch[3].reserve(bytes));
+    HALO_CHECK(st->scratch[7].reserve(k * (64 + 4)));
+    uint4* A = st->scratch[0].as<uint4>();
+    uint4* B = st->scratch[1].as<uint4>();
+    HALO_CHECK(copy_h2d(A, evals, bytes, s));
+    hipLaunchKernelGGL(k_rotate_right, dim3(gridn(k * n, 256)), dim3(256), 0, s, (const uint4*)A, B, k, n);
+    HALO_HIP(hipGetLastError());
+    // batched in-place iNTT of the k rows of B (ping-pong through scratch 2 and 3)
+    HALO_CHECK(ntt_device_dispatch(st, field, B, B, st->scratch[2].ptr, log_n, k, 1, s, st->scratch[3].ptr));
+    uint32_t* d_lens = (uint32_t*)((char*)st->scratch[7].ptr + k * 64);
+    hipLaunchKernelGGL(k_row_lengths, dim3((unsigned)k), dim3(256), 0, s, (const uint4*)B, n, d_lens);
+    HALO_HIP(hipGetLastError());
+    std::vector<uint32_t> lens(k);
+    HALO_CHECK(copy_d2h(lens.data(), d_lens, k * 4, s));
+    for (size_t r = 0; r < k; r++) {
+        const size_t p_deg = lens[r] ? lens[r] - 1 : 0;
+        if (p_deg > d) return set_error(HALO_EDEGREE, "p_deg (%zu) <= d (%zu)", p_deg, d);
+    }
+    uint4* d_commits = st->scratch[7].as<uint4>();
+    for (size_t r = 0; r < k; r++)
+        HALO_CHECK(msm_srs_device(st, curve, B + 2 * r * n, lens[r], nullptr, d_commits + 4 * r, s, true));
+    HALO_CHECK(msm_join(st, s));
+    HALO_CHECK(copy_d2h(commits_out, d_commits, k * 64, s));
+    if (coeffs_out) HALO_CHECK(copy_d2h(coeffs_out, B, bytes, s));
+    if (lens_out)
+        for (size_t r = 0; r < k; r++) lens_out[r] = lens[r];
+    return HALO_OK;
+}

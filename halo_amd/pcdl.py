@@ -125,3 +125,24 @@ def decider_commit(xis, d: int, curve="pallas") -> np.ndarray:
     out = np.zeros(8, dtype=np.uint64)
     H.check(H.load().halo_pcdl_decider_commit(_curve(curve), H.ptr(x), len(x), d, H.ptr(out)))
     return out
+
+
+def trace_commit_batch(evals, d: int, curve="pallas", want_coeffs: bool = False):
+    """Trace::new's interpolate + commit (crates/plonk/src/circuit/trace.rs:165-192) for k evaluation
+    vectors at once: Evals::from_vec_and_domain -> interpolate_by_ref -> pcdl::commit(poly, d, None).
+    evals: (k, n, 4) ark scalars.  Returns the k commitments (k, 8) and, if asked, the trimmed
+    coefficient vectors."""
+    H.ensure_device()
+    e = np.ascontiguousarray(np.asarray(evals, dtype=np.uint64))
+    k, n = e.shape[0], e.shape[1]
+    log_n = n.bit_length() - 1
+    if 1 << log_n != n:
+        raise ValueError("domain size must be a power of two")
+    commits = np.zeros((k, 8), dtype=np.uint64)
+    coeffs = np.zeros((k, n, 4), dtype=np.uint64) if want_coeffs else None
+    lens = (ctypes.c_size_t * k)()
+    H.check(H.load().halo_trace_commit_batch(_curve(curve), H.ptr(e), k, log_n, d,
+                                             H.ptr(coeffs) if want_coeffs else None, lens, H.ptr(commits)))
+    if want_coeffs:
+        return commits, [coeffs[i, : lens[i]] for i in range(k)]
+    return commits

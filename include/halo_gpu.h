@@ -174,6 +174,14 @@ int halo_hpoly_combine(halo_field_t field, const halo_fe_t* xis, size_t k, size_
 int halo_pcdl_decider_commit(halo_curve_t curve, const halo_fe_t* xis, size_t n_xis, size_t d,
                              halo_wrapped_point_t* out);
 
+/* ------------------------------------------------------------------ f2: Trace::new batch
+ * trace.rs:165-192: k evaluation vectors (k x 2^log_n, row-major) -> Evals::from_vec_and_domain
+ * (rotate right by one) -> interpolate (iNTT) -> pcdl::commit(poly, d, None) each; the pcdl::commit
+ * assertions and messages apply per row.  coeffs_out (k x 2^log_n, untrimmed) and lens_out (trimmed
+ * lengths) are optional. */
+int halo_trace_commit_batch(halo_curve_t curve, const halo_fe_t* evals, size_t k, unsigned log_n, size_t d,
+                            halo_fe_t* coeffs_out, size_t* lens_out, halo_wrapped_point_t* commits_out);
+
 /* ------------------------------------------------------------------ a8: evaluation / dots */
 /* DensePolynomial::evaluate (Horner; pcdl.rs:49,471), k polynomials at one point z. */
 int halo_poly_eval_batch(halo_field_t field, const halo_fe_t* const* polys, const size_t* lens,

@@ -241,3 +241,32 @@ def test_srs_read_roundtrip(hal, corc):
     group.PublicParams.upload("vesta", g, precompute_windows=False)
     assert group.PublicParams.len("vesta") == 1000
     assert np.array_equal(group.PublicParams.read("vesta", 100, 50), g[100:150])
+
+
+@pytest.mark.parametrize("cname,cid", CURVES)
+def test_trace_commit_batch(hal, corc, cname, cid):
+    """SURVEY f2 (trace.rs:165-192): batched from_vec_and_domain -> interpolate -> pcdl::commit,
+    against the per-polynomial path (poly.Evals + pcdl.commit) and the oracle MSM; includes an
+    all-zero row, a row of low degree, and the degree assertion."""
+    from halo_amd import poly
+    c = P.CURVES[cname]
+    r = c.scalar
+    n = 1 << 10
+    g = corc.srs_generate(cname, n)
+    for pre in (False, True):
+        group.PublicParams.upload(cname, g, precompute_windows=pre)
+        ev = np.stack([rand_sc(n, 100 + i) for i in range(5)])
+        ev[1] = 0
+        # row 2: evaluations of a constant polynomial (degree 0 after interpolation)
+        ev[2] = fe([7], r)[0]
+        commits, coeffs = pcdl.trace_commit_batch(ev, n - 1, cname, want_coeffs=True)
+        dom = poly.Domain(n, "fp" if cname == "pallas" else "fq")
+        for i in range(5):
+            p = poly.Evals.from_vec_and_domain(ev[i], dom).interpolate_by_ref()
+            assert np.array_equal(coeffs[i], p), i
+            assert np.array_equal(commits[i], pcdl.commit(p, n - 1, None, cname)), i
+            exp = corc.msm(cname, g[: len(p)], p) if len(p) else np.zeros(8, dtype=np.uint64)
+            assert np.array_equal(commits[i], exp), i
+        assert len(coeffs[1]) == 0 and len(coeffs[2]) == 1
+    with pytest.raises(AssertionError, match=r"p_deg \(1023\) <= d \(511\)"):
+        pcdl.trace_commit_batch(ev, 511, cname)
