@@ -11,7 +11,7 @@
 #pragma once
 #include "fields.hpp"
 
-namespace halo {
+HALO_ARITH_BEGIN
 
 struct PallasCurve {
     using Base = FqCfg;
@@ -231,6 +231,57 @@ HALO_DEV void aff_to_wrapped(uint4* p, const Affine<F>& a) {
     fe_to_ark(p + 2, a.y);
 }
 
+// Jacobian (x = X/Z^2, y = Y/Z^3): used for long doubling chains (Horner), where dbl-2009-l
+// (1M + 5S) is ~30 % cheaper than the XYZZ doubling (6M + 3S).
+template <class F>
+struct Jac {
+    Fe<F> X, Y, Z;
+};
+
+// XYZZ -> Jacobian without inversion: Z = ZZZ, X = X ZZ^2, Y = Y ZZZ^2 (uses ZZ^3 = ZZZ^2)
+template <class F>
+HALO_DEV Jac<F> jac_from_xyzz(const XYZZ<F>& p) {
+    Jac<F> r;
+    if (xyzz_is_id(p)) {
+        r.X = fe_one<F>();
+        r.Y = fe_one<F>();
+        r.Z = fe_zero<F>();
+        return r;
+    }
+    r.X = fe_mul(p.X, fe_sqr(p.ZZ));
+    r.Y = fe_mul(p.Y, fe_sqr(p.ZZZ));
+    r.Z = p.ZZZ;
+    return r;
+}
+
+template <class F>
+HALO_DEV XYZZ<F> jac_to_xyzz(const Jac<F>& j) {
+    XYZZ<F> r;
+    r.X = j.X;
+    r.Y = j.Y;
+    r.ZZ = fe_sqr(j.Z);
+    r.ZZZ = fe_mul(r.ZZ, j.Z);
+    return r;
+}
+
+// dbl-2009-l (a = 0): A = X^2, B = Y^2, C = B^2, D = 2((X + B)^2 - A - C), E = 3A, F = E^2,
+// X3 = F - 2D, Y3 = E (D - X3) - 8C, Z3 = 2 Y Z.  The identity (Z = 0) maps to itself.
+template <class F>
+HALO_DEV Jac<F> jac_dbl(const Jac<F>& p) {
+    const Fe<F> A = fe_sqr(p.X);
+    const Fe<F> B = fe_sqr(p.Y);
+    const Fe<F> C = fe_sqr(B);
+    const Fe<F> D = fe_dbl(fe_sub(fe_sub(fe_sqr(fe_add(p.X, B)), A), C));
+    const Fe<F> E = fe_add(A, fe_dbl(A));
+    const Fe<F> Fv = fe_sqr(E);
+    Jac<F> r;
+    r.X = fe_sub(Fv, fe_dbl(D));
+    const Fe<F> C8 = fe_dbl(fe_dbl(fe_dbl(C)));
+    r.Y = fe_sub(fe_mul(E, fe_sub(D, r.X)), C8);
+    r.Z = fe_dbl(fe_mul(p.Y, p.Z));
+    return r;
+}
+
 // Variable-base scalar multiplication k * P (k canonical, 8 x u32 words), left-to-right binary.
 template <class F>
 HALO_DEV XYZZ<F> xyzz_scalar_mul(const Affine<F>& P, const uint32_t (&k)[8]) {
@@ -242,4 +293,4 @@ HALO_DEV XYZZ<F> xyzz_scalar_mul(const Affine<F>& P, const uint32_t (&k)[8]) {
     return acc;
 }
 
-}  // namespace halo
+HALO_ARITH_END  // namespace halo

@@ -25,9 +25,19 @@
 
 #include "consts.hpp"
 
-namespace halo {
+// Arithmetic namespace: translation units compiled with HALO_MAD_ILP (latency-bound kernels, see
+// msm_tail.hip) get the same code in the inline namespace halo::ilp with split column sums.
+#ifdef HALO_MAD_ILP
+#define HALO_ARITH_BEGIN namespace halo { inline namespace ilp {
+#define HALO_ARITH_END } }
+#else
+#define HALO_ARITH_BEGIN namespace halo {
+#define HALO_ARITH_END }
+#endif
 
 #define HALO_DEV __device__ __forceinline__
+
+HALO_ARITH_BEGIN
 
 // Column accumulation acc + a * b as ONE v_mad_u64_u32 per product.  Written as inline asm so that
 // the compiler keeps each column as a single dependent chain instead of splitting it into partial
@@ -35,16 +45,24 @@ namespace halo {
 // chain form issues ~12% fewer VALU instructions per multiplication and is ~10% faster
 // (tools/micro/fe_mul_bench.hip); latency-bound single-wave code loses a little.
 HALO_DEV uint64_t mad_acc(uint32_t a, uint32_t b, uint64_t c) {
+#ifdef HALO_MAD_ILP
+    return (uint64_t)a * b + c;
+#else
     uint64_t d, cc;
     asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(cc) : "v"(a), "v"(b), "v"(c));
     return d;
+#endif
 }
 // acc + a * K for a compile-time constant K (SGPR operand)
 template <uint32_t K>
 HALO_DEV uint64_t mad_acc_k(uint32_t a, uint64_t c) {
+#ifdef HALO_MAD_ILP
+    return (uint64_t)a * K + c;
+#else
     uint64_t d, cc;
     asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(cc) : "v"(a), "s"(K), "v"(c));
     return d;
+#endif
 }
 
 template <class C>
@@ -415,4 +433,4 @@ HALO_DEV void fe_ark_to_canonical_words(const uint4* p, uint32_t (&w)[8]) {
     fe_pack(x, w);
 }
 
-}  // namespace halo
+HALO_ARITH_END  // namespace halo

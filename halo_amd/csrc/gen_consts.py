@@ -64,12 +64,63 @@ def field_block(struct: str, p: int) -> str:
     return "".join(out)
 
 
-def curve_block(struct: str, base: int) -> str:
+# GLV endomorphism phi(x, y) = (beta x, y) = lambda (x, y) (beta: cube root of unity in the base
+# field, lambda: in the scalar field; the matching pair, checked against the oracle in
+# tests/test_oracle.py::test_glv_constants) and the short lattice basis (a_i, b_i) with
+# a_i + b_i lambda = 0 mod r from the half extended Euclid of (r, lambda).
+GLV = {
+    "PallasCurveCfg": dict(
+        lam=0x397E65A7D7C1AD71AEE24B27E308F0A61259527EC1D4752E619D1840AF55F1B1,
+        beta=0x2D33357CB532458ED3552A23A8554E5005270D29D19FC7D27B7FD22F0201B547),
+    "VestaCurveCfg": dict(
+        lam=0x12CCCA834ACDBA712CAAD5DC57AAB1B01D1F8BD237AD31491DAD5EBDFDFE4AB9,
+        beta=0x06819A58283E528E511DB4D81CF70F5A0FED467D47C033AF2AA9D2E050AA0E4F),
+}
+
+
+def glv_basis(r: int, lam: int):
+    import math
+    r0, t0, r1, t1 = r, 0, lam, 1
+    sq = math.isqrt(r)
+    seq = [(r0, t0), (r1, t1)]
+    while r1 >= sq:
+        qq = r0 // r1
+        r0, r1 = r1, r0 - qq * r1
+        t0, t1 = t1, t0 - qq * t1
+        seq.append((r1, t1))
+    (rl1, tl1), (rl, tl) = seq[-1], seq[-2]
+    qq = r0 // r1
+    r2, t2 = r0 - qq * r1, t0 - qq * t1
+    v1 = (rl1, -tl1)
+    v2 = min([(rl, -tl), (r2, -t2)], key=lambda v: v[0] ** 2 + v[1] ** 2)
+    return v1, v2
+
+
+def words32(x: int, n: int) -> str:
+    assert 0 <= x < (1 << (32 * n))
+    return ", ".join(hex((x >> (32 * i)) & 0xFFFFFFFF) for i in range(n))
+
+
+def curve_block(struct: str, base: int, scalar: int) -> str:
     # short Weierstrass y^2 = x^3 + 5; generator (-1, 2)
     out = [f"struct {struct} {{\n"]
     out.append(arr("B", 5 * RP % base))
     out.append(arr("GX", (base - 1) * RP % base))
     out.append(arr("GY", 2 * RP % base))
+    g = GLV[struct]
+    lam, beta = g["lam"], g["beta"]
+    assert pow(beta, 3, base) == 1 and pow(lam, 3, scalar) == 1
+    out.append(arr("BETA", beta * RP % base))  # internal Montgomery form
+    (a1, b1), (a2, b2) = glv_basis(scalar, lam)
+    det = a1 * b2 - a2 * b1
+    assert abs(det) == scalar and (a1 + b1 * lam) % scalar == 0 and (a2 + b2 * lam) % scalar == 0
+    # c1 = round(b2 k / det), c2 = round(-b1 k / det) ~ (k * G) >> 384 with G = round(2^384 * num / det)
+    g1 = (b2 * (1 << 384) + det // 2) // det
+    g2 = (-b1 * (1 << 384) + det // 2) // det
+    for name, v in (("GLV_A1", a1), ("GLV_B1", b1), ("GLV_A2", a2), ("GLV_B2", b2), ("GLV_G1", g1), ("GLV_G2", g2)):
+        nw = 9 if name in ("GLV_G1", "GLV_G2") else 5
+        out.append(f"    static constexpr uint32_t {name}[{nw}] = {{{words32(abs(v), nw)}}};  // magnitude\n")
+        out.append(f"    static constexpr int {name}_NEG = {1 if v < 0 else 0};\n")
     out.append("};\n")
     return "".join(out)
 
@@ -85,8 +136,8 @@ def main() -> None:
     print(f"constexpr int MAX_LOG_DOMAIN = {MAXLOG};")
     print(field_block("FpCfg", FP))
     print(field_block("FqCfg", FQ))
-    print(curve_block("PallasCurveCfg", FQ))
-    print(curve_block("VestaCurveCfg", FP))
+    print(curve_block("PallasCurveCfg", FQ, FP))
+    print(curve_block("VestaCurveCfg", FP, FQ))
     print("}  // namespace halo")
 
 

@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "dispatch.hpp"
+#include "glv.hpp"
 #include "msm.hpp"
 #include "runtime.hpp"
 
@@ -147,77 +148,143 @@ __global__ void k_pointwise_mul(uint4* a, const uint4* b, size_t n) {
 // ---------------------------------------------------------------------------------------------
 // IPA fold
 // ---------------------------------------------------------------------------------------------
+
+// G'[j] = G_l[j] + xi G_r[j] for j < m, c'[j] = c_l + xi^-1 c_r, z'[j] = z_l + xi z_r.
 // gs: internal affine (2m points), cs/zs: ark scalars (2m).  xi / xi_inv: ark.
+// xi G_r = k1 G_r + k2 phi(G_r), phi(x, y) = (beta x, y) (GLV): one interleaved NAF double-and-add
+// of ~128 doublings (digit schedule wave-uniform, in LDS) instead of 255.  The affine conversion
+// shares one inversion per workgroup (Montgomery's trick over prefix / suffix product scans).
+constexpr int FOLD_THREADS = 128;
 template <class Cv>
-__global__ __launch_bounds__(128) void k_ipa_fold(uint4* gs, uint4* cs, uint4* zs, size_t m, const uint4* xi_ark,
-                                                  const uint4* xi_inv_ark) {
+__global__ __launch_bounds__(FOLD_THREADS, 4) void k_ipa_fold(uint4* gs, uint4* cs, uint4* zs, size_t m,
+                                                           const uint4* xi_ark, const uint4* xi_inv_ark) {
     using F = typename Cv::Base;
     using S = typename Cv::Scalar;
-    __shared__ int8_t naf[260];
-    __shared__ int naf_top_s;
-    if (threadIdx.x == 0) {
-        // non-adjacent form of the canonical xi
-        uint32_t k[9];
+    constexpr int ND = 132;
+    __shared__ int8_t naf1[ND], naf2[ND];
+    __shared__ int top_s, neg1_s, neg2_s;
+    __shared__ uint32_t pre[FOLD_THREADS][NLIMB], suf[FOLD_THREADS][NLIMB];
+    __shared__ uint32_t tinv[NLIMB];
+    const int tid = threadIdx.x;
+    if (tid == 0) {
         uint32_t w8[8];
         fe_ark_to_canonical_words<S>(xi_ark, w8);
-        for (int i = 0; i < 8; i++) k[i] = w8[i];
-        k[8] = 0;
-        int top = -1;
-        for (int i = 0; i < 258; i++) {
-            int d = 0;
-            if (k[0] & 1u) {
-                d = 2 - (int)(k[0] & 3u);  // +1 or -1
-                // k -= d
-                if (d == 1) {
-                    k[0] -= 1;
-                } else {
-                    uint32_t c = 1;
-                    for (int q = 0; q < 9 && c; q++) {
-                        k[q] += 1;
-                        c = (k[q] == 0);
-                    }
-                }
-            }
-            naf[i] = (int8_t)d;
-            if (d) top = i;
-            for (int q = 0; q < 8; q++) k[q] = (k[q] >> 1) | (k[q + 1] << 31);
-            k[8] >>= 1;
-        }
-        naf_top_s = top;
+        bool n1, n2;
+        uint32_t k1[5], k2[5];
+        glv::decompose<typename Cv::K>(w8, n1, k1, n2, k2);
+        const int t1 = glv::naf_digits(k1, naf1, ND), t2 = glv::naf_digits(k2, naf2, ND);
+        top_s = t1 > t2 ? t1 : t2;
+        neg1_s = n1;
+        neg2_s = n2;
     }
     __syncthreads();
-    const int naf_top = naf_top_s;
-    const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= m) return;
-    // scalars
-    const Fe<S> xi = fe_from_ark<S>(xi_ark);
-    const Fe<S> xinv = fe_from_ark<S>(xi_inv_ark);
-    fe_to_ark(cs + 2 * j, fe_add(fe_from_ark<S>(cs + 2 * j), fe_mul(fe_from_ark<S>(cs + 2 * (j + m)), xinv)));
-    fe_to_ark(zs + 2 * j, fe_add(fe_from_ark<S>(zs + 2 * j), fe_mul(fe_from_ark<S>(zs + 2 * (j + m)), xi)));
-    // G_l[j] + xi * G_r[j]: every lane shares xi, so the NAF digit schedule (in LDS, computed once
-    // per workgroup) is wave-uniform: 255 doublings + ~85 mixed additions, no divergence.
-    const Affine<F> gr = aff_load<F>(gs + 4 * (j + m));
-    const Affine<F> grn = aff_neg(gr);
+    const int top = top_s;
+    const size_t j = (size_t)blockIdx.x * FOLD_THREADS + tid;
+    const bool live = j < m;
     XYZZ<F> acc = xyzz_id<F>();
-    for (int i = naf_top; i >= 0; i--) {
-        acc = xyzz_dbl(acc);
-        const int d = __builtin_amdgcn_readfirstlane((int)naf[i]);
-        if (d > 0) acc = xyzz_madd(acc, gr);
-        else if (d < 0) acc = xyzz_madd(acc, grn);
+    if (live) {
+        const Fe<S> xi = fe_from_ark<S>(xi_ark);
+        const Fe<S> xinv = fe_from_ark<S>(xi_inv_ark);
+        fe_to_ark(cs + 2 * j, fe_add(fe_from_ark<S>(cs + 2 * j), fe_mul(fe_from_ark<S>(cs + 2 * (j + m)), xinv)));
+        fe_to_ark(zs + 2 * j, fe_add(fe_from_ark<S>(zs + 2 * j), fe_mul(fe_from_ark<S>(zs + 2 * (j + m)), xi)));
+        const Affine<F> gr = aff_load<F>(gs + 4 * (j + m));
+        Affine<F> p1 = gr, p2;
+        p2.x = fe_mul(gr.x, fe_from_const<F>(Cv::K::BETA));
+        p2.y = gr.y;
+        if (aff_is_id(gr)) p2 = gr;
+        const int s1 = neg1_s ? -1 : 1, s2 = neg2_s ? -1 : 1;
+        for (int i = top; i >= 0; i--) {
+            acc = xyzz_dbl(acc);
+            const int d1 = __builtin_amdgcn_readfirstlane((int)naf1[i] * s1);
+            const int d2 = __builtin_amdgcn_readfirstlane((int)naf2[i] * s2);
+            if (d1) {
+                Affine<F> q = p1;
+                if (d1 < 0) q.y = fe_neg(q.y);
+                acc = xyzz_madd(acc, q);
+            }
+            if (d2) {
+                Affine<F> q = p2;
+                if (d2 < 0) q.y = fe_neg(q.y);
+                acc = xyzz_madd(acc, q);
+            }
+        }
+        acc = xyzz_madd(acc, aff_load<F>(gs + 4 * j));
     }
-    acc = xyzz_madd(acc, aff_load<F>(gs + 4 * j));
-    aff_store(gs + 4 * j, xyzz_to_aff(acc));
+    // batched affine conversion: z = ZZ * ZZZ (1 for identity / idle lanes)
+    const bool id = xyzz_is_id(acc);
+    const Fe<F> z = (live && !id) ? fe_mul(acc.ZZ, acc.ZZZ) : fe_one<F>();
+    // inclusive prefix and suffix products (Hillis-Steele in LDS)
+    Fe<F> pv = z, sv = z;
+    for (int off = 1; off < FOLD_THREADS; off <<= 1) {
+        for (int l = 0; l < NLIMB; l++) {
+            pre[tid][l] = pv.v[l];
+            suf[tid][l] = sv.v[l];
+        }
+        __syncthreads();
+        if (tid >= off) {
+            Fe<F> o;
+            for (int l = 0; l < NLIMB; l++) o.v[l] = pre[tid - off][l];
+            pv = fe_mul(pv, o);
+        }
+        if (tid + off < FOLD_THREADS) {
+            Fe<F> o;
+            for (int l = 0; l < NLIMB; l++) o.v[l] = suf[tid + off][l];
+            sv = fe_mul(sv, o);
+        }
+        __syncthreads();
+    }
+    for (int l = 0; l < NLIMB; l++) {
+        pre[tid][l] = pv.v[l];
+        suf[tid][l] = sv.v[l];
+    }
+    __syncthreads();
+    if (tid == FOLD_THREADS - 1) {
+        const Fe<F> t = fe_inv(pv);  // inverse of the product of all z
+        for (int l = 0; l < NLIMB; l++) tinv[l] = t.v[l];
+    }
+    __syncthreads();
+    if (!live) return;
+    Fe<F> inv;
+    for (int l = 0; l < NLIMB; l++) inv.v[l] = tinv[l];
+    if (tid > 0) {
+        Fe<F> o;
+        for (int l = 0; l < NLIMB; l++) o.v[l] = pre[tid - 1][l];
+        inv = fe_mul(inv, o);
+    }
+    if (tid + 1 < FOLD_THREADS) {
+        Fe<F> o;
+        for (int l = 0; l < NLIMB; l++) o.v[l] = suf[tid + 1][l];
+        inv = fe_mul(inv, o);
+    }
+    Affine<F> r;
+    if (id) {
+        r.x = fe_zero<F>();
+        r.y = fe_zero<F>();
+    } else {
+        r.x = fe_mul(acc.X, fe_mul(inv, acc.ZZZ));  // X / ZZ
+        r.y = fe_mul(acc.Y, fe_mul(inv, acc.ZZ));   // Y / ZZZ
+    }
+    aff_store(gs + 4 * j, r);
 }
 
+// 2^i P (i < count) as XYZZ from a WrappedPoint: one doubling chain (one thread)
 template <class Cv>
-__global__ __launch_bounds__(64) void k_pow2_table_from_wrapped(const uint4* P_wrapped, uint4* out_aff, int count) {
+__global__ __launch_bounds__(64) void k_pow2_xyzz_from_wrapped(const uint4* P_wrapped, uint4* out_xyzz, int count) {
     using F = typename Cv::Base;
     if (threadIdx.x != 0) return;
     XYZZ<F> p = xyzz_from_aff(aff_from_wrapped<F>(P_wrapped));
     for (int i = 0; i < count; i++) {
-        aff_store(out_aff + 4 * i, xyzz_to_aff(p));
+        xyzz_store(out_xyzz + 8 * i, p);
         p = xyzz_dbl(p);
     }
+}
+
+// XYZZ -> internal affine, one inversion per lane (all lanes in parallel)
+template <class Cv>
+__global__ __launch_bounds__(64) void k_xyzz_to_aff_ipa(const uint4* in, uint4* out, int count) {
+    using F = typename Cv::Base;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < count) aff_store(out + 4 * i, xyzz_to_aff(xyzz_load<F>(in + 8 * i)));
 }
 
 template <class Cv>
@@ -432,7 +499,9 @@ extern "C" int halo_ipa_begin(halo_curve_t curve, const halo_fe_t* cs, size_t n,
         DISPATCH_CURVE(curve, Cv, {
             hipLaunchKernelGGL(k_powers<typename Cv::Scalar>, dim3(gridn((n + run - 1) / run, 128)), dim3(128), 0, s,
                                (const uint4*)sm, n, run, ses->zs.as<uint4>());
-            hipLaunchKernelGGL(k_pow2_table_from_wrapped<Cv>, dim3(1), dim3(64), 0, s, (const uint4*)(sm + 64),
+            hipLaunchKernelGGL(k_pow2_xyzz_from_wrapped<Cv>, dim3(1), dim3(64), 0, s, (const uint4*)(sm + 64),
+                               ses->tmp.as<uint4>(), 256);
+            hipLaunchKernelGGL(k_xyzz_to_aff_ipa<Cv>, dim3(4), dim3(64), 0, s, (const uint4*)ses->tmp.ptr,
                                ses->htab.as<uint4>(), 256);
         });
         if (hipGetLastError() != hipSuccess) rc = set_error(HALO_EDEVICE, "ipa begin launch failed");
@@ -484,7 +553,7 @@ extern "C" int halo_ipa_fold(halo_ipa_session* ses, const halo_fe_t* xi, const h
     const size_t m = ses->m;
     DISPATCH_CURVE(ses->curve, Cv, {
         ProfScope prof("ipa_fold", s);
-        HALO_LAUNCH(prof, k_ipa_fold<Cv>, dim3(gridn(m, 128)), dim3(128), 0, s, ses->gs.as<uint4>(), ses->cs.as<uint4>(),
+        HALO_LAUNCH(prof, k_ipa_fold<Cv>, dim3(gridn(m, FOLD_THREADS)), dim3(FOLD_THREADS), 0, s, ses->gs.as<uint4>(), ses->cs.as<uint4>(),
                     ses->zs.as<uint4>(), m, (const uint4*)(sm + 384), (const uint4*)(sm + 416));
     });
     HALO_HIP(hipGetLastError());

@@ -17,9 +17,11 @@
 //                 one workgroup per window forms sum_j (acc_j + jL sum_j) and tree-reduces in LDS.
 //   7. final    : Horner over the windows (+ w * S for hiding commitments), XYZZ -> affine -> ark.
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 
 #include "dispatch.hpp"
+#include "glv.hpp"
 #include "msm.hpp"
 #include "runtime.hpp"
 #include "sort.hpp"
@@ -139,6 +141,49 @@ __global__ void k_digits(const uint4* scalars, size_t n, int c, int W, uint32_t*
     }
 }
 
+// GLV recoding (bases not window-shifted): s = k1 + lambda k2 with |k1|, |k2| < 2^128, so each
+// scalar gives W = ceil(129 / c) signed digits for point i (k1) and W for phi(G_i) (k2, entry
+// n + i): the same number of bucket additions as W = ceil(255 / c) digits of s, but the Horner
+// over the window sums needs ~128 doublings instead of ~255 (the latency of small MSMs).
+template <class Cv>
+__global__ void k_digits_glv(const uint4* scalars, size_t n, int c, int W, uint32_t* digits) {
+    using S = typename Cv::Scalar;
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t w8[8];
+    fe_ark_to_canonical_words<S>(scalars + 2 * i, w8);
+    bool neg[2];
+    uint32_t mag[2][5];
+    glv::decompose<typename Cv::K>(w8, neg[0], mag[0], neg[1], mag[1]);
+    const uint32_t half = 1u << (c - 1);
+    const uint32_t full = 1u << c;
+    for (int h = 0; h < 2; h++) {
+        const uint32_t nflip = neg[h] ? 0x80000000u : 0u;
+        uint32_t carry = 0;
+        for (int w = 0; w < W; w++) {
+            const int bit = w * c;
+            uint32_t raw = 0;
+            if (bit < 160) {
+                const int q = bit >> 5, sh = bit & 31;
+                const uint64_t lo = mag[h][q];
+                const uint64_t hi = (q + 1 < 5) ? mag[h][q + 1] : 0;
+                raw = (uint32_t)(((hi << 32) | lo) >> sh) & (full - 1);
+            }
+            const uint32_t v = raw + carry;
+            uint32_t out;
+            if (v > half) {
+                carry = 1;
+                const uint32_t m = full - v;
+                out = (m == 0) ? DIGIT_NONE : (((m - 1) | 0x80000000u) ^ nflip);
+            } else {
+                carry = 0;
+                out = (v == 0) ? DIGIT_NONE : ((v - 1) | nflip);
+            }
+            digits[(size_t)w * 2 * n + (size_t)h * n + i] = out;
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // 3-5. tasks, accumulation, merge
 // ---------------------------------------------------------------------------------------------
@@ -150,7 +195,7 @@ __global__ void k_digits(const uint4* scalars, size_t n, int c, int W, uint32_t*
 template <class Cv>
 __global__ __launch_bounds__(256, 4) void k_acc(const uint32_t* keys, const uint32_t* vals, const uint32_t* count,
                                              uint32_t K, const uint4* bases, uint32_t n_per_window, size_t stride,
-                                             uint4* first, uint4* last, uint4* bucket_sums) {
+                                             uint32_t glv_n, uint4* first, uint4* last, uint4* bucket_sums) {
     using F = typename Cv::Base;
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t cnt = *count;
@@ -175,212 +220,14 @@ __global__ __launch_bounds__(256, 4) void k_acc(const uint32_t* keys, const uint
         const uint32_t v = vals[e];
         size_t idx = v & 0x7fffffffu;
         if (stride) idx = (idx / n_per_window) * stride + idx % n_per_window;  // window-shifted SRS
+        const bool phi = glv_n && idx >= glv_n;                               // GLV: phi(G_i)
+        if (phi) idx -= glv_n;
         Affine<F> p = aff_load<F>(bases + 4 * idx);
+        if (phi) p.x = fe_mul(p.x, fe_from_const<F>(Cv::K::BETA));
         if (v & 0x80000000u) p.y = fe_neg(p.y);
         acc = xyzz_madd(acc, p);
     }
     xyzz_store((first_done ? last : first) + 8 * t, acc);
-}
-
-// Skew guard: sums of MSM_GROUP consecutive chunk partials whose entries all belong to one bucket
-// (level 1: groups of 64 chunks from first[]; level 2: groups of 64 level-1 groups), so that a huge
-// bucket (all-equal scalars) is merged in O(chunks / 4096 + 128) sequential adds, not O(chunks).
-constexpr uint32_t MSM_GROUP = 64;
-template <class Cv>
-__global__ __launch_bounds__(MSM_GROUP) void k_group_sums(const uint32_t* keys, const uint32_t* count, uint32_t K,
-                                                          uint32_t span, const uint4* src, uint4* out) {
-    using F = typename Cv::Base;
-    __shared__ uint4 red[MSM_GROUP * 8];
-    const uint32_t g = blockIdx.x, i = threadIdx.x;
-    const uint32_t cnt = *count;
-    const size_t e0 = (size_t)g * MSM_GROUP * span * K, e1 = e0 + (size_t)MSM_GROUP * span * K;
-    if (e1 > cnt || keys[e0] != keys[e1 - 1]) return;  // not one bucket throughout: never used
-    xyzz_store(red + 8 * i, xyzz_load<F>(src + 8 * ((size_t)g * MSM_GROUP + i)));
-    for (uint32_t off = MSM_GROUP / 2; off > 0; off >>= 1) {
-        __syncthreads();
-        if (i < off) xyzz_store(red + 8 * i, xyzz_add(xyzz_load<F>(red + 8 * i), xyzz_load<F>(red + 8 * (i + off))));
-    }
-    __syncthreads();
-    if (i == 0) xyzz_store(out + 8 * (size_t)g, xyzz_load<F>(red));
-}
-
-// Buckets that touch a chunk boundary (or are empty): bucket b's entries [s, e) lie in chunks
-// t0 = s / K .. t1 = (e - 1) / K; chunk t contributes first[t] when b is its first segment, else
-// last[t]; whole groups strictly inside (t0, t1) come from the group sums.  A bucket strictly
-// inside one chunk was written by k_acc.
-template <class Cv>
-__global__ __launch_bounds__(256) void k_merge(const uint32_t* bstart, const uint32_t* keys, const uint32_t* count,
-                                               uint32_t K, size_t nb, const uint4* first, const uint4* last,
-                                               const uint4* g1, const uint4* g2, uint4* bucket_sums) {
-    using F = typename Cv::Base;
-    const size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= nb) return;
-    const uint32_t s = bstart[b], e = bstart[b + 1];
-    if (s == e) {
-        xyzz_store(bucket_sums + 8 * b, xyzz_id<F>());
-        return;
-    }
-    const uint32_t cnt = *count;
-    const uint32_t t0 = s / K, t1 = (e - 1) / K;
-    auto chunk_last = [&](uint32_t t) { return min(cnt, (t + 1) * K) - 1; };
-    if (t0 == t1 && keys[(size_t)t0 * K] != b && keys[chunk_last(t0)] != b) return;  // interior: done
-    constexpr uint32_t G2 = MSM_GROUP * MSM_GROUP;
-    XYZZ<F> acc = xyzz_id<F>();
-    for (uint32_t t = t0; t <= t1;) {
-        if (t > t0 && t % G2 == 0 && t + G2 <= t1) {
-            acc = xyzz_add(acc, xyzz_load<F>(g2 + 8 * (size_t)(t / G2)));
-            t += G2;
-        } else if (t > t0 && t % MSM_GROUP == 0 && t + MSM_GROUP <= t1) {
-            acc = xyzz_add(acc, xyzz_load<F>(g1 + 8 * (size_t)(t / MSM_GROUP)));
-            t += MSM_GROUP;
-        } else {
-            const uint4* src = (keys[(size_t)t * K] == b) ? first : last;
-            acc = xyzz_add(acc, xyzz_load<F>(src + 8 * (size_t)t));
-            t++;
-        }
-    }
-    xyzz_store(bucket_sums + 8 * b, acc);
-}
-
-// ---------------------------------------------------------------------------------------------
-// 6. per-window reduction  S_w = sum_{i<B} (i + 1) BS[w][i], organised for low dependency depth
-//    (every stage is latency-bound: a lone XYZZ add is ~14 dependent modmuls).  View the buckets as
-//    H rows x L columns, i = h L + l:
-//      sum_i (i + 1) BS_i = sum_h R_h + L sum_h h R_h + sum_l l C_l,
-//      R_h = sum_l BS[h L + l] (row sums), C_l = sum_h BS[h L + l] (column sums),
-//      sum_h h R_h = sum_j 2^j U_j, U_j = sum_{h : bit j of h} R_h, and likewise V_j for the columns.
-//    k_rowcol: R and C (tree sums, depth ~12); k_bitterms: sum_h R_h, U_j, V_j (independent tree
-//    sums, depth ~12); k_bitcombine: lane k doubles its term (<= log B times), then a tree sum.
-//    ~2.1 B adds in total at depth ~40 (a running-sum reduction needs 2 B adds at depth 2 B / #threads).
-// ---------------------------------------------------------------------------------------------
-template <class F>
-HALO_DEV void lds_tree_sum(uint4* red, uint32_t tid, uint32_t n) {  // red[0] = sum of red[0..n), n pow2
-    for (uint32_t off = n >> 1; off > 0; off >>= 1) {
-        __syncthreads();
-        if (tid < off) xyzz_store(red + 8 * tid, xyzz_add(xyzz_load<F>(red + 8 * tid), xyzz_load<F>(red + 8 * (tid + off))));
-    }
-    __syncthreads();
-}
-
-// grid (ceil(H / (256 / L)) + L, SW), 256 threads
-template <class Cv>
-__global__ __launch_bounds__(256) void k_rowcol(const uint4* bucket_sums, uint32_t L, uint32_t H, uint4* rows,
-                                                uint4* cols) {
-    using F = typename Cv::Base;
-    __shared__ uint4 red[256 * 8];
-    const uint32_t w = blockIdx.y, tid = threadIdx.x;
-    const uint32_t B = L * H;
-    const uint4* bs = bucket_sums + 8 * (size_t)w * B;
-    const uint32_t rpb = 256 / L;  // rows per block
-    const uint32_t nrb = (H + rpb - 1) / rpb;
-    if (blockIdx.x < nrb) {
-        const uint32_t h = blockIdx.x * rpb + tid / L, l = tid % L;
-        XYZZ<F> v = xyzz_id<F>();
-        if (h < H) v = xyzz_load<F>(bs + 8 * ((size_t)h * L + l));
-        xyzz_store(red + 8 * tid, v);
-        // tree over the L lanes of each row (rows are contiguous groups of L threads)
-        for (uint32_t off = L >> 1; off > 0; off >>= 1) {
-            __syncthreads();
-            if (l < off)
-                xyzz_store(red + 8 * tid, xyzz_add(xyzz_load<F>(red + 8 * tid), xyzz_load<F>(red + 8 * (tid + off))));
-        }
-        __syncthreads();
-        if (l == 0 && h < H) xyzz_store(rows + 8 * ((size_t)w * H + h), xyzz_load<F>(red + 8 * tid));
-    } else {
-        const uint32_t l = blockIdx.x - nrb;
-        XYZZ<F> acc = xyzz_id<F>();
-        for (uint32_t h = tid; h < H; h += 256) acc = xyzz_add(acc, xyzz_load<F>(bs + 8 * ((size_t)h * L + l)));
-        xyzz_store(red + 8 * tid, acc);
-        lds_tree_sum<F>(red, tid, 256);
-        if (tid == 0) xyzz_store(cols + 8 * ((size_t)w * L + l), xyzz_load<F>(red));
-    }
-}
-
-// grid (1 + logH + logL, SW), 256 threads.  out[w * NT + k]:
-//   k == 0             : sum_h R_h
-//   1 <= k <= logH     : U_{k-1} = sum_{h : bit k-1} R_h
-//   k >  logH          : V_{k-1-logH} = sum_{l : bit k-1-logH} C_l
-template <class Cv>
-__global__ __launch_bounds__(256) void k_bitterms(const uint4* rows, const uint4* cols, uint32_t H, uint32_t L,
-                                                  uint32_t logH, uint4* out) {
-    using F = typename Cv::Base;
-    __shared__ uint4 red[256 * 8];
-    const uint32_t k = blockIdx.x, w = blockIdx.y, tid = threadIdx.x;
-    const uint32_t NT = gridDim.x;
-    const bool is_col = k > logH;
-    const uint32_t cnt = is_col ? L : H;
-    const uint4* src = is_col ? cols + 8 * (size_t)w * L : rows + 8 * (size_t)w * H;
-    const uint32_t bit = is_col ? (k - 1 - logH) : (k - 1);
-    XYZZ<F> acc = xyzz_id<F>();
-    for (uint32_t j = tid; j < cnt; j += 256) {
-        if (k != 0 && !((j >> bit) & 1u)) continue;
-        acc = xyzz_add(acc, xyzz_load<F>(src + 8 * j));
-    }
-    xyzz_store(red + 8 * tid, acc);
-    lds_tree_sum<F>(red, tid, 256);
-    if (tid == 0) xyzz_store(out + 8 * ((size_t)w * NT + k), xyzz_load<F>(red));
-}
-
-// grid SW, 64 threads: S_w = T_0 + sum_j 2^(j + logL) U_j + sum_j 2^j V_j
-template <class Cv>
-__global__ __launch_bounds__(64) void k_bitcombine(const uint4* terms, uint32_t NT, uint32_t logH, uint32_t logL,
-                                                   uint4* window_sums) {
-    using F = typename Cv::Base;
-    __shared__ uint4 red[64 * 8];
-    const uint32_t w = blockIdx.x, k = threadIdx.x;
-    XYZZ<F> v = xyzz_id<F>();
-    if (k < NT) {
-        v = xyzz_load<F>(terms + 8 * ((size_t)w * NT + k));
-        const uint32_t d = (k == 0) ? 0 : (k <= logH ? (k - 1 + logL) : (k - 1 - logH));
-        for (uint32_t i = 0; i < d; i++) v = xyzz_dbl(v);
-    }
-    xyzz_store(red + 8 * k, v);
-    for (uint32_t off = 32; off > 0; off >>= 1) {
-        __syncthreads();
-        if (k < off) xyzz_store(red + 8 * k, xyzz_add(xyzz_load<F>(red + 8 * k), xyzz_load<F>(red + 8 * (k + off))));
-    }
-    __syncthreads();
-    if (k == 0) xyzz_store(window_sums + 8 * w, xyzz_load<F>(red));
-}
-
-// ---------------------------------------------------------------------------------------------
-// 7. final: Horner over the windows (wave 0), hiding term w * S from the table 2^i S (waves 1-4),
-//    XYZZ -> affine -> ark WrappedPoint.
-// ---------------------------------------------------------------------------------------------
-template <class Cv>
-__global__ __launch_bounds__(320) void k_final(const uint4* window_sums, int W, int c,
-                                               const uint4* hide_table /* 256 internal affine 2^i S, or null */,
-                                               const uint4* hide_scalar /* ark or null */, uint4* out_wrapped) {
-    using F = typename Cv::Base;
-    using S = typename Cv::Scalar;
-    __shared__ uint4 red[256 * 8];
-    __shared__ uint32_t kw[8];
-    const int tid = threadIdx.x;
-    XYZZ<F> horner = xyzz_id<F>();
-    if (tid == 0) {
-        for (int w = W - 1; w >= 0; w--) {
-            if (w != W - 1)
-                for (int k = 0; k < c; k++) horner = xyzz_dbl(horner);
-            horner = xyzz_add(horner, xyzz_load<F>(window_sums + 8 * w));
-        }
-    }
-    if (tid == 64 && hide_table && hide_scalar) fe_ark_to_canonical_words<S>(hide_scalar, kw);
-    __syncthreads();
-    if (tid >= 64) {
-        const int i = tid - 64;
-        XYZZ<F> v = xyzz_id<F>();
-        if (hide_table && hide_scalar && ((kw[i >> 5] >> (i & 31)) & 1u))
-            v = xyzz_from_aff(aff_load<F>(hide_table + 4 * i));
-        xyzz_store(red + 8 * i, v);
-    }
-    __syncthreads();
-    for (int off = 128; off > 0; off >>= 1) {
-        const int i = tid - 64;
-        if (tid >= 64 && i < off)
-            xyzz_store(red + 8 * i, xyzz_add(xyzz_load<F>(red + 8 * i), xyzz_load<F>(red + 8 * (i + off))));
-        __syncthreads();
-    }
-    if (tid == 0) aff_to_wrapped(out_wrapped, xyzz_to_aff(xyzz_add(horner, xyzz_load<F>(red))));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -455,18 +302,24 @@ struct MsmScratch {
 struct MsmPipe {
     MsmScratch set[2];
     int next = 0;
-    hipStream_t tail = nullptr;
+    hipStream_t tail[2] = {nullptr, nullptr};  // one per scratch set: consecutive tails run concurrently
 };
 static MsmPipe g_msm_pipe[64];  // per device
 
 static int pipe_init(MsmPipe& P) {
-    if (P.tail) return HALO_OK;
-    HALO_HIP(hipStreamCreateWithFlags(&P.tail, hipStreamNonBlocking));
+    if (P.tail[0]) return HALO_OK;
+    HALO_HIP(hipStreamCreateWithFlags(&P.tail[0], hipStreamNonBlocking));
+    HALO_HIP(hipStreamCreateWithFlags(&P.tail[1], hipStreamNonBlocking));
     for (auto& m : P.set) {
         HALO_HIP(hipEventCreateWithFlags(&m.acc_done, hipEventDisableTiming));
         HALO_HIP(hipEventCreateWithFlags(&m.tail_done, hipEventDisableTiming));
     }
     return HALO_OK;
+}
+
+template <class Cv>
+constexpr int curve_id() {
+    return std::is_same<Cv, PallasCurve>::value ? HALO_PALLAS : HALO_VESTA;
 }
 
 // bases_int: n internal affine points, or (shifted) W * n window-shifted points (single bucket set).
@@ -476,18 +329,22 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
                         uint4* d_out_wrapped, hipStream_t s, bool async) {
     MsmPipe& PP = g_msm_pipe[st->device & 63];
     HALO_CHECK(pipe_init(PP));
-    MsmScratch& M = PP.set[PP.next];
+    const int set = PP.next;
+    MsmScratch& M = PP.set[set];
     PP.next ^= 1;
     // the previous user of this scratch set must have finished its tail
     if (M.tail_pending) HALO_HIP(hipStreamWaitEvent(s, M.tail_done, 0));
-    const hipStream_t ts = PP.tail;
+    const hipStream_t ts = PP.tail[set];
     const size_t nn = std::max<size_t>(n, 1);
-    const int c = c_req ? c_req : msm_window_bits(nn);
-    const int W = msm_windows(c);
+    // non-shifted bases: GLV (2n half-size scalars, ~128-bit windows) -- see k_digits_glv
+    const bool glv = !shifted;
+    const size_t NP = glv ? 2 * nn : nn;  // digit entries per window
+    const int c = c_req ? c_req : msm_window_bits(NP);
+    const int W = glv ? (129 + c - 1) / c : msm_windows(c);
     const uint32_t B = 1u << (c - 1);
     // sort geometry: SW windows of SN entries each (shifted: one window over all W * n digits)
     const int SW = shifted ? 1 : W;
-    const size_t SN = shifted ? (size_t)W * nn : nn;
+    const size_t SN = shifted ? (size_t)W * nn : NP;
     const size_t NB = (size_t)SW * B;
     const uint32_t L = std::min<uint32_t>(MSM_SEG_L, B);
     const uint32_t logL = ilog2(L);
@@ -495,13 +352,13 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
     const uint32_t logH = ilog2(H);
     const uint32_t NT = 1 + logH + logL;  // reduction bit terms per window (<= 64)
     const uint32_t key_bits = NB > 1 ? ilog2(NB - 1) + 1 : 1;
-    HALO_CHECK(M.digits.reserve((size_t)W * nn * 4));
+    HALO_CHECK(M.digits.reserve((size_t)W * NP * 4));
     HALO_CHECK(M.bstart.reserve((NB + 1) * 4));
     // chunk length K: >= 4 rounds of resident lanes (256 CUs x 16 waves x 64), 16 <= K <= 64.  Every
     // lane does the same number of mixed additions; several rounds absorb the CU slots held by the
     // previous MSM's tail kernels, which one exact round would not (measured: K = 60 at 2^20 is 1
     // round and 15% slower than K = 16).
-    const size_t E = (size_t)W * nn;
+    const size_t E = (size_t)W * NP;
     const size_t lanes = (size_t)st->num_cu * 16 * 64 * 4;
     const uint32_t K = (uint32_t)std::max<size_t>(16, std::min<size_t>(64, (E + lanes - 1) / lanes));
     const size_t nchunks = (E + K - 1) / K;
@@ -518,8 +375,12 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
     HALO_CHECK(M.window_sums.reserve((size_t)W * 128));
 
     if (n > 0) {
-        hipLaunchKernelGGL(k_digits<typename Cv::Scalar>, dim3(grid_for(n, 256)), dim3(256), 0, s, scalars_ark, n, c,
-                           W, M.digits.as<uint32_t>());
+        if (glv)
+            hipLaunchKernelGGL(k_digits_glv<Cv>, dim3(grid_for(n, 256)), dim3(256), 0, s, scalars_ark, n, c, W,
+                               M.digits.as<uint32_t>());
+        else
+            hipLaunchKernelGGL(k_digits<typename Cv::Scalar>, dim3(grid_for(n, 256)), dim3(256), 0, s, scalars_ark, n,
+                               c, W, M.digits.as<uint32_t>());
         HALO_HIP(hipGetLastError());
         uint32_t *skeys = nullptr, *svals = nullptr;
         const uint32_t* scount = nullptr;
@@ -528,8 +389,8 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
         ProfScope prof("msm_acc", s);
         HALO_LAUNCH(prof, k_acc<Cv>, dim3(grid_for(nchunks, 256)), dim3(256), 0, s, (const uint32_t*)skeys,
                     (const uint32_t*)svals, scount, K, bases_int, (uint32_t)nn,
-                    (shifted && shift_stride != nn) ? shift_stride : (size_t)0, P_first, P_last,
-                    M.bucket_sums.as<uint4>());
+                    (shifted && shift_stride != nn) ? shift_stride : (size_t)0, glv ? (uint32_t)nn : 0u, P_first,
+                    P_last, M.bucket_sums.as<uint4>());
         M.skeys = skeys;
         M.scount = scount;
         HALO_HIP(hipGetLastError());
@@ -540,27 +401,36 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
     // caller's next MSM
     HALO_HIP(hipEventRecord(M.acc_done, s));
     HALO_HIP(hipStreamWaitEvent(ts, M.acc_done, 0));
-    if (n > 0) {
-        HALO_CHECK(msm_bucket_starts(M.skeys, M.scount, NB, E, M.bstart.as<uint32_t>(), ts));
-        if (ng1)
-            hipLaunchKernelGGL(k_group_sums<Cv>, dim3((unsigned)ng1), dim3(MSM_GROUP), 0, ts, (const uint32_t*)M.skeys,
-                               M.scount, K, 1u, (const uint4*)P_first, P_g1);
-        if (ng2)
-            hipLaunchKernelGGL(k_group_sums<Cv>, dim3((unsigned)ng2), dim3(MSM_GROUP), 0, ts, (const uint32_t*)M.skeys,
-                               M.scount, K, MSM_GROUP, (const uint4*)P_g1, P_g2);
-        hipLaunchKernelGGL(k_merge<Cv>, dim3(grid_for(NB, 256)), dim3(256), 0, ts, M.bstart.as<const uint32_t>(),
-                           (const uint32_t*)M.skeys, M.scount, K, NB, P_first, P_last, P_g1, P_g2,
-                           M.bucket_sums.as<uint4>());
-        const uint32_t nrb = (H + (256 / L) - 1) / (256 / L);
-        hipLaunchKernelGGL(k_rowcol<Cv>, dim3(nrb + L, SW), dim3(256), 0, ts, M.bucket_sums.as<const uint4>(), L, H,
-                           M.seg_acc.as<uint4>(), M.seg_sum.as<uint4>());
-        hipLaunchKernelGGL(k_bitterms<Cv>, dim3(NT, SW), dim3(256), 0, ts, M.seg_acc.as<const uint4>(),
-                           M.seg_sum.as<const uint4>(), H, L, logH, M.bits.as<uint4>());
-        hipLaunchKernelGGL(k_bitcombine<Cv>, dim3(SW), dim3(64), 0, ts, M.bits.as<const uint4>(), NT, logH, logL,
-                           M.window_sums.as<uint4>());
-    }
-    hipLaunchKernelGGL(k_final<Cv>, dim3(1), dim3(320), 0, ts, M.window_sums.as<const uint4>(), SW, c, hide_table,
-                       hide_scalar, d_out_wrapped);
+    MsmTailArgs ta;
+    ta.n = n;
+    ta.skeys = M.skeys;
+    ta.scount = M.scount;
+    ta.K = K;
+    ta.NB = NB;
+    ta.E = E;
+    ta.first = P_first;
+    ta.last = P_last;
+    ta.g1 = P_g1;
+    ta.g2 = P_g2;
+    ta.ng1 = ng1;
+    ta.ng2 = ng2;
+    ta.bstart = M.bstart.as<uint32_t>();
+    ta.bucket_sums = M.bucket_sums.as<uint4>();
+    ta.rows = M.seg_acc.as<uint4>();
+    ta.cols = M.seg_sum.as<uint4>();
+    ta.terms = M.bits.as<uint4>();
+    ta.window_sums = M.window_sums.as<uint4>();
+    ta.L = L;
+    ta.H = H;
+    ta.logH = logH;
+    ta.logL = logL;
+    ta.NT = NT;
+    ta.SW = SW;
+    ta.c = c;
+    ta.hide_table = hide_table;
+    ta.hide_scalar = hide_scalar;
+    ta.out_wrapped = d_out_wrapped;
+    HALO_CHECK(msm_tail_launch(curve_id<Cv>(), ta, ts));
     HALO_HIP(hipGetLastError());
     HALO_HIP(hipEventRecord(M.tail_done, ts));
     M.tail_pending = true;

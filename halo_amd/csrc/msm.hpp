@@ -23,4 +23,24 @@ int convert_internal_to_wrapped(int curve, const void* in, void* out, size_t n, 
 int ntt_device_dispatch(DeviceState* st, int field, const void* d_in, void* d_out, void* d_tmp, unsigned logn,
                         size_t batch, int inverse, hipStream_t s, void* d_tmp2 = nullptr);
 
+// chunk-partial group size of the skew guard (msm_tail.hip k_group_sums)
+constexpr uint32_t MSM_GROUP = 64;
+
+// Inputs of the MSM's reduction tail (msm_tail.hip), launched on the tail stream.
+struct MsmTailArgs {
+    size_t n, NB, E, ng1, ng2;
+    const uint32_t* skeys;
+    const uint32_t* scount;
+    uint32_t K;
+    uint4 *first, *last, *g1, *g2;
+    uint32_t* bstart;
+    uint4 *bucket_sums, *rows, *cols, *terms, *window_sums;
+    uint32_t L, H, logH, logL, NT;
+    int SW, c;
+    const uint4* hide_table;
+    const uint4* hide_scalar;
+    uint4* out_wrapped;
+};
+int msm_tail_launch(int curve, const MsmTailArgs& a, hipStream_t ts);
+
 }  // namespace halo

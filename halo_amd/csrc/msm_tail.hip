@@ -1,0 +1,263 @@
+// MSM reduction tail: chunk-partial merge and the bucket reduction
+// sum_i (i + 1) B_i per window, Horner over windows, hiding term, affine output.
+//
+// Every kernel here is latency-bound (a few waves doing dependent chains of curve additions), so this
+// translation unit is compiled with HALO_MAD_ILP: the field multiplication keeps the compiler's
+// split column sums (shorter dependency chains: 418 vs 523 ns per dependent modmul on one wave,
+// tools/micro/fe_mul_bench.hip) instead of the single-chain form that wins in the throughput
+// kernels.  The arithmetic lives in the inline namespace halo::ilp here (fields.hpp), so the two
+// variants never collide.
+#include <algorithm>
+
+#include "dispatch.hpp"
+#include "msm.hpp"
+#include "runtime.hpp"
+#include "sort.hpp"
+
+#ifndef HALO_MAD_ILP
+#error "msm_tail.hip must be compiled with -DHALO_MAD_ILP (see Makefile)"
+#endif
+
+namespace halo {
+
+// Skew guard: sums of MSM_GROUP consecutive chunk partials whose entries all belong to one bucket
+// (level 1: groups of 64 chunks from first[]; level 2: groups of 64 level-1 groups), so that a huge
+// bucket (all-equal scalars) is merged in O(chunks / 4096 + 128) sequential adds, not O(chunks).
+template <class Cv>
+__global__ __launch_bounds__(MSM_GROUP) void k_group_sums(const uint32_t* keys, const uint32_t* count, uint32_t K,
+                                                          uint32_t span, const uint4* src, uint4* out) {
+    using F = typename Cv::Base;
+    __shared__ uint4 red[MSM_GROUP * 8];
+    const uint32_t g = blockIdx.x, i = threadIdx.x;
+    const uint32_t cnt = *count;
+    const size_t e0 = (size_t)g * MSM_GROUP * span * K, e1 = e0 + (size_t)MSM_GROUP * span * K;
+    if (e1 > cnt || keys[e0] != keys[e1 - 1]) return;  // not one bucket throughout: never used
+    xyzz_store(red + 8 * i, xyzz_load<F>(src + 8 * ((size_t)g * MSM_GROUP + i)));
+    for (uint32_t off = MSM_GROUP / 2; off > 0; off >>= 1) {
+        __syncthreads();
+        if (i < off) xyzz_store(red + 8 * i, xyzz_add(xyzz_load<F>(red + 8 * i), xyzz_load<F>(red + 8 * (i + off))));
+    }
+    __syncthreads();
+    if (i == 0) xyzz_store(out + 8 * (size_t)g, xyzz_load<F>(red));
+}
+
+// Buckets that touch a chunk boundary (or are empty): bucket b's entries [s, e) lie in chunks
+// t0 = s / K .. t1 = (e - 1) / K; chunk t contributes first[t] when b is its first segment, else
+// last[t]; whole groups strictly inside (t0, t1) come from the group sums.  A bucket strictly
+// inside one chunk was written by k_acc.
+template <class Cv>
+__global__ __launch_bounds__(256) void k_merge(const uint32_t* bstart, const uint32_t* keys, const uint32_t* count,
+                                               uint32_t K, size_t nb, const uint4* first, const uint4* last,
+                                               const uint4* g1, const uint4* g2, uint4* bucket_sums) {
+    using F = typename Cv::Base;
+    const size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    const uint32_t s = bstart[b], e = bstart[b + 1];
+    if (s == e) {
+        xyzz_store(bucket_sums + 8 * b, xyzz_id<F>());
+        return;
+    }
+    const uint32_t cnt = *count;
+    const uint32_t t0 = s / K, t1 = (e - 1) / K;
+    auto chunk_last = [&](uint32_t t) { return min(cnt, (t + 1) * K) - 1; };
+    if (t0 == t1 && keys[(size_t)t0 * K] != b && keys[chunk_last(t0)] != b) return;  // interior: done
+    constexpr uint32_t G2 = MSM_GROUP * MSM_GROUP;
+    XYZZ<F> acc = xyzz_id<F>();
+    for (uint32_t t = t0; t <= t1;) {
+        if (t > t0 && t % G2 == 0 && t + G2 <= t1) {
+            acc = xyzz_add(acc, xyzz_load<F>(g2 + 8 * (size_t)(t / G2)));
+            t += G2;
+        } else if (t > t0 && t % MSM_GROUP == 0 && t + MSM_GROUP <= t1) {
+            acc = xyzz_add(acc, xyzz_load<F>(g1 + 8 * (size_t)(t / MSM_GROUP)));
+            t += MSM_GROUP;
+        } else {
+            const uint4* src = (keys[(size_t)t * K] == b) ? first : last;
+            acc = xyzz_add(acc, xyzz_load<F>(src + 8 * (size_t)t));
+            t++;
+        }
+    }
+    xyzz_store(bucket_sums + 8 * b, acc);
+}
+
+// ---------------------------------------------------------------------------------------------
+// 6. per-window reduction  S_w = sum_{i<B} (i + 1) BS[w][i], organised for low dependency depth
+//    (every stage is latency-bound: a lone XYZZ add is ~14 dependent modmuls).  View the buckets as
+//    H rows x L columns, i = h L + l:
+//      sum_i (i + 1) BS_i = sum_h R_h + L sum_h h R_h + sum_l l C_l,
+//      R_h = sum_l BS[h L + l] (row sums), C_l = sum_h BS[h L + l] (column sums),
+//      sum_h h R_h = sum_j 2^j U_j, U_j = sum_{h : bit j of h} R_h, and likewise V_j for the columns.
+//    k_rowcol: R and C (tree sums, depth ~12); k_bitterms: sum_h R_h, U_j, V_j (independent tree
+//    sums, depth ~12); k_bitcombine: lane k doubles its term (<= log B times), then a tree sum.
+//    ~2.1 B adds in total at depth ~40 (a running-sum reduction needs 2 B adds at depth 2 B / #threads).
+// ---------------------------------------------------------------------------------------------
+template <class F>
+HALO_DEV void lds_tree_sum(uint4* red, uint32_t tid, uint32_t n) {  // red[0] = sum of red[0..n), n pow2
+    for (uint32_t off = n >> 1; off > 0; off >>= 1) {
+        __syncthreads();
+        if (tid < off) xyzz_store(red + 8 * tid, xyzz_add(xyzz_load<F>(red + 8 * tid), xyzz_load<F>(red + 8 * (tid + off))));
+    }
+    __syncthreads();
+}
+
+// grid (ceil(H / (256 / L)) + L, SW), 256 threads
+template <class Cv>
+__global__ __launch_bounds__(256) void k_rowcol(const uint4* bucket_sums, uint32_t L, uint32_t H, uint4* rows,
+                                                uint4* cols) {
+    using F = typename Cv::Base;
+    __shared__ uint4 red[256 * 8];
+    const uint32_t w = blockIdx.y, tid = threadIdx.x;
+    const uint32_t B = L * H;
+    const uint4* bs = bucket_sums + 8 * (size_t)w * B;
+    const uint32_t rpb = 256 / L;  // rows per block
+    const uint32_t nrb = (H + rpb - 1) / rpb;
+    if (blockIdx.x < nrb) {
+        const uint32_t h = blockIdx.x * rpb + tid / L, l = tid % L;
+        XYZZ<F> v = xyzz_id<F>();
+        if (h < H) v = xyzz_load<F>(bs + 8 * ((size_t)h * L + l));
+        xyzz_store(red + 8 * tid, v);
+        // tree over the L lanes of each row (rows are contiguous groups of L threads)
+        for (uint32_t off = L >> 1; off > 0; off >>= 1) {
+            __syncthreads();
+            if (l < off)
+                xyzz_store(red + 8 * tid, xyzz_add(xyzz_load<F>(red + 8 * tid), xyzz_load<F>(red + 8 * (tid + off))));
+        }
+        __syncthreads();
+        if (l == 0 && h < H) xyzz_store(rows + 8 * ((size_t)w * H + h), xyzz_load<F>(red + 8 * tid));
+    } else {
+        const uint32_t l = blockIdx.x - nrb;
+        XYZZ<F> acc = xyzz_id<F>();
+        for (uint32_t h = tid; h < H; h += 256) acc = xyzz_add(acc, xyzz_load<F>(bs + 8 * ((size_t)h * L + l)));
+        xyzz_store(red + 8 * tid, acc);
+        lds_tree_sum<F>(red, tid, 256);
+        if (tid == 0) xyzz_store(cols + 8 * ((size_t)w * L + l), xyzz_load<F>(red));
+    }
+}
+
+// grid (1 + logH + logL, SW), 256 threads.  out[w * NT + k]:
+//   k == 0             : sum_h R_h
+//   1 <= k <= logH     : U_{k-1} = sum_{h : bit k-1} R_h
+//   k >  logH          : V_{k-1-logH} = sum_{l : bit k-1-logH} C_l
+template <class Cv>
+__global__ __launch_bounds__(256) void k_bitterms(const uint4* rows, const uint4* cols, uint32_t H, uint32_t L,
+                                                  uint32_t logH, uint4* out) {
+    using F = typename Cv::Base;
+    __shared__ uint4 red[256 * 8];
+    const uint32_t k = blockIdx.x, w = blockIdx.y, tid = threadIdx.x;
+    const uint32_t NT = gridDim.x;
+    const bool is_col = k > logH;
+    const uint32_t cnt = is_col ? L : H;
+    const uint4* src = is_col ? cols + 8 * (size_t)w * L : rows + 8 * (size_t)w * H;
+    const uint32_t bit = is_col ? (k - 1 - logH) : (k - 1);
+    XYZZ<F> acc = xyzz_id<F>();
+    for (uint32_t j = tid; j < cnt; j += 256) {
+        if (k != 0 && !((j >> bit) & 1u)) continue;
+        acc = xyzz_add(acc, xyzz_load<F>(src + 8 * j));
+    }
+    xyzz_store(red + 8 * tid, acc);
+    lds_tree_sum<F>(red, tid, 256);
+    if (tid == 0) xyzz_store(out + 8 * ((size_t)w * NT + k), xyzz_load<F>(red));
+}
+
+// grid SW, 64 threads: S_w = T_0 + sum_j 2^(j + logL) U_j + sum_j 2^j V_j
+template <class Cv>
+__global__ __launch_bounds__(64) void k_bitcombine(const uint4* terms, uint32_t NT, uint32_t logH, uint32_t logL,
+                                                   uint4* window_sums) {
+    using F = typename Cv::Base;
+    __shared__ uint4 red[64 * 8];
+    const uint32_t w = blockIdx.x, k = threadIdx.x;
+    XYZZ<F> v = xyzz_id<F>();
+    if (k < NT) {
+        v = xyzz_load<F>(terms + 8 * ((size_t)w * NT + k));
+        const uint32_t d = (k == 0) ? 0 : (k <= logH ? (k - 1 + logL) : (k - 1 - logH));
+        for (uint32_t i = 0; i < d; i++) v = xyzz_dbl(v);
+    }
+    xyzz_store(red + 8 * k, v);
+    for (uint32_t off = 32; off > 0; off >>= 1) {
+        __syncthreads();
+        if (k < off) xyzz_store(red + 8 * k, xyzz_add(xyzz_load<F>(red + 8 * k), xyzz_load<F>(red + 8 * (k + off))));
+    }
+    __syncthreads();
+    if (k == 0) xyzz_store(window_sums + 8 * w, xyzz_load<F>(red));
+}
+
+// ---------------------------------------------------------------------------------------------
+// 7. final: Horner over the windows (wave 0), hiding term w * S from the table 2^i S (waves 1-4),
+//    XYZZ -> affine -> ark WrappedPoint.
+// ---------------------------------------------------------------------------------------------
+template <class Cv>
+__global__ __launch_bounds__(320) void k_final(const uint4* window_sums, int W, int c,
+                                               const uint4* hide_table /* 256 internal affine 2^i S, or null */,
+                                               const uint4* hide_scalar /* ark or null */, uint4* out_wrapped) {
+    using F = typename Cv::Base;
+    using S = typename Cv::Scalar;
+    __shared__ uint4 red[256 * 8];
+    __shared__ uint32_t kw[8];
+    const int tid = threadIdx.x;
+    XYZZ<F> horner = xyzz_id<F>();
+    if (tid == 0) {
+        // Horner over the windows; the c doublings per window run in Jacobian coordinates
+        for (int w = W - 1; w >= 0; w--) {
+            if (w != W - 1 && !xyzz_is_id(horner)) {
+                Jac<F> j = jac_from_xyzz(horner);
+                for (int k = 0; k < c; k++) j = jac_dbl(j);
+                horner = jac_to_xyzz(j);
+            }
+            horner = xyzz_add(horner, xyzz_load<F>(window_sums + 8 * w));
+        }
+    }
+    if (tid == 64 && hide_table && hide_scalar) fe_ark_to_canonical_words<S>(hide_scalar, kw);
+    __syncthreads();
+    if (tid >= 64) {
+        const int i = tid - 64;
+        XYZZ<F> v = xyzz_id<F>();
+        if (hide_table && hide_scalar && ((kw[i >> 5] >> (i & 31)) & 1u))
+            v = xyzz_from_aff(aff_load<F>(hide_table + 4 * i));
+        xyzz_store(red + 8 * i, v);
+    }
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+        const int i = tid - 64;
+        if (tid >= 64 && i < off)
+            xyzz_store(red + 8 * i, xyzz_add(xyzz_load<F>(red + 8 * i), xyzz_load<F>(red + 8 * (i + off))));
+        __syncthreads();
+    }
+    if (tid == 0) aff_to_wrapped(out_wrapped, xyzz_to_aff(xyzz_add(horner, xyzz_load<F>(red))));
+}
+
+
+static unsigned grid_for_t(size_t n, unsigned thr) { return (unsigned)std::max<size_t>(1, (n + thr - 1) / thr); }
+
+template <class Cv>
+static int tail_launch_t(const MsmTailArgs& a, hipStream_t ts) {
+    if (a.n > 0) {
+        HALO_CHECK(msm_bucket_starts(a.skeys, a.scount, a.NB, a.E, a.bstart, ts));
+        if (a.ng1)
+            hipLaunchKernelGGL(k_group_sums<Cv>, dim3((unsigned)a.ng1), dim3(MSM_GROUP), 0, ts, a.skeys, a.scount, a.K,
+                               1u, (const uint4*)a.first, a.g1);
+        if (a.ng2)
+            hipLaunchKernelGGL(k_group_sums<Cv>, dim3((unsigned)a.ng2), dim3(MSM_GROUP), 0, ts, a.skeys, a.scount, a.K,
+                               MSM_GROUP, (const uint4*)a.g1, a.g2);
+        hipLaunchKernelGGL(k_merge<Cv>, dim3(grid_for_t(a.NB, 256)), dim3(256), 0, ts, (const uint32_t*)a.bstart,
+                           a.skeys, a.scount, a.K, a.NB, (const uint4*)a.first, (const uint4*)a.last,
+                           (const uint4*)a.g1, (const uint4*)a.g2, a.bucket_sums);
+        const uint32_t nrb = (a.H + (256 / a.L) - 1) / (256 / a.L);
+        hipLaunchKernelGGL(k_rowcol<Cv>, dim3(nrb + a.L, a.SW), dim3(256), 0, ts, (const uint4*)a.bucket_sums, a.L,
+                           a.H, a.rows, a.cols);
+        hipLaunchKernelGGL(k_bitterms<Cv>, dim3(a.NT, a.SW), dim3(256), 0, ts, (const uint4*)a.rows,
+                           (const uint4*)a.cols, a.H, a.L, a.logH, a.terms);
+        hipLaunchKernelGGL(k_bitcombine<Cv>, dim3(a.SW), dim3(64), 0, ts, (const uint4*)a.terms, a.NT, a.logH, a.logL,
+                           a.window_sums);
+    }
+    hipLaunchKernelGGL(k_final<Cv>, dim3(1), dim3(320), 0, ts, (const uint4*)a.window_sums, a.SW, a.c, a.hide_table,
+                       a.hide_scalar, a.out_wrapped);
+    HALO_HIP(hipGetLastError());
+    return HALO_OK;
+}
+
+int msm_tail_launch(int curve, const MsmTailArgs& a, hipStream_t ts) {
+    int rc;
+    DISPATCH_CURVE(curve, Cv, { rc = tail_launch_t<Cv>(a, ts); });
+    return rc;
+}
+
+}  // namespace halo

@@ -1,0 +1,47 @@
+"""Times a full device-resident IPA opening (pcdl.rs:392-438 round loop): lg n rounds of L/R MSMs +
+fold, with a stand-in transcript (fixed pseudo-random challenges)."""
+import ctypes, random, sys, time
+sys.path.insert(0, '/root/repo')
+import numpy as np
+from halo_amd import _lib as H
+H.ensure_device(0)
+L = H.load()
+R = 0x40000000000000000000000000000000224698FC0994A8DD8C46EB2100000001
+
+
+def fe1(v):
+    m = v * (1 << 256) % R
+    return np.array([(m >> (64 * i)) & (2**64 - 1) for i in range(4)], dtype=np.uint64)
+
+
+for lg in [int(x) for x in (sys.argv[1:] or ['16', '20'])]:
+    n = 1 << lg
+    H.check(L.halo_srs_synthesize(0, n, 77))
+    rnd = random.Random(lg)
+    cs = np.array([[rnd.getrandbits(62) for _ in range(4)] for _ in range(n)], dtype=np.uint64)
+    z = fe1(12345)
+    Hp = np.zeros(8, dtype=np.uint64)
+    H.check(L.halo_srs_read(0, 1, 1, H.ptr(Hp)))
+    for rep in range(2):
+        s = ctypes.c_void_p()
+        H.check(L.halo_ipa_begin(0, H.ptr(cs), n, H.ptr(z), H.ptr(Hp), ctypes.byref(s)))
+        Lp = np.zeros(8, dtype=np.uint64); Rp = np.zeros(8, dtype=np.uint64)
+        H.check(L.halo_profile_reset()); H.check(L.halo_profile_enable(1))
+        t_lr = t_fold = 0.0
+        t0 = time.perf_counter()
+        for r in range(lg):
+            a = time.perf_counter()
+            H.check(L.halo_ipa_round_lr(s, H.ptr(Lp), H.ptr(Rp)))
+            b = time.perf_counter()
+            xi = rnd.randrange(1, R)
+            H.check(L.halo_ipa_fold(s, H.ptr(fe1(xi)), H.ptr(fe1(pow(xi, -1, R)))))
+            c = time.perf_counter()
+            t_lr += b - a; t_fold += c - b
+        t1 = time.perf_counter()
+        U = np.zeros(8, dtype=np.uint64); c0 = np.zeros(4, dtype=np.uint64)
+        H.check(L.halo_ipa_end(s, H.ptr(U), H.ptr(c0)))
+        nl = ctypes.c_size_t(0); ms = ctypes.c_double(0)
+        H.check(L.halo_profile_read(b"ipa_fold", ctypes.byref(nl), ctypes.byref(ms)))
+        H.check(L.halo_profile_enable(0))
+        print(f"open 2^{lg}: total {1e3*(t1-t0):.2f} ms (L/R rounds {1e3*t_lr:.2f} ms, folds {1e3*t_fold:.2f} ms; "
+              f"fold kernels {ms.value:.2f} ms over {nl.value})", flush=True)

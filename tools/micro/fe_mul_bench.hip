@@ -112,7 +112,57 @@ double timeit(K kern, uint4* d, int blocks, int threads, int iters) {
     return ms;
 }
 
+// compiler-scheduled column sums (split chains, more ILP)
+template <class C>
+__device__ __forceinline__ Fe<C> fe_mul_c(const Fe<C>& a, const Fe<C>& b) {
+    uint32_t m[NLIMB];
+    Fe<C> r;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 2 * NLIMB - 1; k++) {
+#pragma unroll
+        for (int i = 0; i < NLIMB; i++) {
+            const int j = k - i;
+            if (j < 0 || j >= NLIMB) continue;
+            acc += (uint64_t)a.v[i] * b.v[j];
+        }
+#pragma unroll
+        for (int i = 0; i < NLIMB; i++) {
+            const int j = k - i;
+            if (i >= k || j < 1 || j >= NLIMB || C::P[j] == 0) continue;
+            acc += (uint64_t)m[i] * C::P[j];
+        }
+        if (k < NLIMB) {
+            const uint32_t mk = (0u - (uint32_t)acc) & LIMB_MASK;
+            m[k] = mk;
+            acc += mk;
+            acc >>= LIMB_BITS;
+        } else {
+            r.v[k - NLIMB] = (uint32_t)acc & LIMB_MASK;
+            acc >>= LIMB_BITS;
+        }
+    }
+    r.v[NLIMB - 1] = (uint32_t)acc;
+    return r;
+}
+template <int V>
+__global__ void lat(uint4* d, int iters) {
+    const int i = threadIdx.x;
+    Fe<FqCfg> a = fe_load<FqCfg>(d + 4 * i), b = fe_load<FqCfg>(d + 4 * i + 2);
+    for (int k = 0; k < iters; k++) a = V == 0 ? fe_mul_c(a, b) : fe_mul_asm(a, b);
+    fe_store(d + 4 * i, a);
+}
+
 int main() {
+    {
+        uint4* d; CHECK(hipMalloc(&d, 64 * 4 * sizeof(uint4)));
+        CHECK(hipMemset(d, 1, 64 * 4 * sizeof(uint4)));
+        for (int v = 0; v < 2; v++) {
+            double t = timeit(v == 0 ? lat<0> : lat<1>, d, 1, 64, 4096);
+            printf("single-wave dependent chain: %s %.1f ns per modmul\n", v == 0 ? "compiler-split" : "asm-chain", t * 1e6 / 4096);
+        }
+        CHECK(hipFree(d));
+    }
     const int threads = 256;
     for (int wps : {1, 2, 4, 8}) {
         const int blocks = 256 * wps;  // wps waves per SIMD
