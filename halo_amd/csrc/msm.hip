@@ -231,6 +231,50 @@ __global__ __launch_bounds__(256, 4) void k_acc(const uint32_t* keys, const uint
 }
 
 // ---------------------------------------------------------------------------------------------
+// 7. final: Horner over the windows (wave 0), hiding term w * S from the table 2^i S (waves 1-4),
+//    XYZZ -> affine -> ark WrappedPoint.
+// ---------------------------------------------------------------------------------------------
+template <class Cv>
+__global__ __launch_bounds__(320) void k_final(const uint4* window_sums, int W, int c,
+                                               const uint4* hide_table /* 256 internal affine 2^i S, or null */,
+                                               const uint4* hide_scalar /* ark or null */, uint4* out_wrapped) {
+    using F = typename Cv::Base;
+    using S = typename Cv::Scalar;
+    __shared__ uint4 red[256 * 8];
+    __shared__ uint32_t kw[8];
+    const int tid = threadIdx.x;
+    XYZZ<F> horner = xyzz_id<F>();
+    if (tid == 0) {
+        // Horner over the windows; the c doublings per window run in Jacobian coordinates
+        for (int w = W - 1; w >= 0; w--) {
+            if (w != W - 1 && !xyzz_is_id(horner)) {
+                Jac<F> j = jac_from_xyzz(horner);
+                for (int k = 0; k < c; k++) j = jac_dbl(j);
+                horner = jac_to_xyzz(j);
+            }
+            horner = xyzz_add(horner, xyzz_load<F>(window_sums + 8 * w));
+        }
+    }
+    if (tid == 64 && hide_table && hide_scalar) fe_ark_to_canonical_words<S>(hide_scalar, kw);
+    __syncthreads();
+    if (tid >= 64) {
+        const int i = tid - 64;
+        XYZZ<F> v = xyzz_id<F>();
+        if (hide_table && hide_scalar && ((kw[i >> 5] >> (i & 31)) & 1u))
+            v = xyzz_from_aff(aff_load<F>(hide_table + 4 * i));
+        xyzz_store(red + 8 * i, v);
+    }
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+        const int i = tid - 64;
+        if (tid >= 64 && i < off)
+            xyzz_store(red + 8 * i, xyzz_add(xyzz_load<F>(red + 8 * i), xyzz_load<F>(red + 8 * (i + off))));
+        __syncthreads();
+    }
+    if (tid == 0) aff_to_wrapped(out_wrapped, xyzz_to_aff(xyzz_add(horner, xyzz_load<F>(red))));
+}
+
+// ---------------------------------------------------------------------------------------------
 // SRS precomputation: window-shifted bases 2^(c w) G_i (w < W) and the hiding table 2^i S
 // ---------------------------------------------------------------------------------------------
 template <class Cv>
@@ -431,6 +475,8 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
     ta.hide_scalar = hide_scalar;
     ta.out_wrapped = d_out_wrapped;
     HALO_CHECK(msm_tail_launch(curve_id<Cv>(), ta, ts));
+    hipLaunchKernelGGL(k_final<Cv>, dim3(1), dim3(320), 0, ts, M.window_sums.as<const uint4>(), SW, c, hide_table,
+                       hide_scalar, d_out_wrapped);
     HALO_HIP(hipGetLastError());
     HALO_HIP(hipEventRecord(M.tail_done, ts));
     M.tail_pending = true;

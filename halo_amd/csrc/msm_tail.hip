@@ -1,5 +1,6 @@
 // MSM reduction tail: chunk-partial merge and the bucket reduction
-// sum_i (i + 1) B_i per window, Horner over windows, hiding term, affine output.
+// sum_i (i + 1) B_i per window (k_final, the single-wave Horner, stays in msm.hip: measured faster
+// with the single-chain multiplication).
 //
 // Every kernel here is latency-bound (a few waves doing dependent chains of curve additions), so this
 // translation unit is compiled with HALO_MAD_ILP: the field multiplication keeps the compiler's
@@ -17,6 +18,7 @@
 #ifndef HALO_MAD_ILP
 #error "msm_tail.hip must be compiled with -DHALO_MAD_ILP (see Makefile)"
 #endif
+
 
 namespace halo {
 
@@ -180,50 +182,6 @@ __global__ __launch_bounds__(64) void k_bitcombine(const uint4* terms, uint32_t 
     if (k == 0) xyzz_store(window_sums + 8 * w, xyzz_load<F>(red));
 }
 
-// ---------------------------------------------------------------------------------------------
-// 7. final: Horner over the windows (wave 0), hiding term w * S from the table 2^i S (waves 1-4),
-//    XYZZ -> affine -> ark WrappedPoint.
-// ---------------------------------------------------------------------------------------------
-template <class Cv>
-__global__ __launch_bounds__(320) void k_final(const uint4* window_sums, int W, int c,
-                                               const uint4* hide_table /* 256 internal affine 2^i S, or null */,
-                                               const uint4* hide_scalar /* ark or null */, uint4* out_wrapped) {
-    using F = typename Cv::Base;
-    using S = typename Cv::Scalar;
-    __shared__ uint4 red[256 * 8];
-    __shared__ uint32_t kw[8];
-    const int tid = threadIdx.x;
-    XYZZ<F> horner = xyzz_id<F>();
-    if (tid == 0) {
-        // Horner over the windows; the c doublings per window run in Jacobian coordinates
-        for (int w = W - 1; w >= 0; w--) {
-            if (w != W - 1 && !xyzz_is_id(horner)) {
-                Jac<F> j = jac_from_xyzz(horner);
-                for (int k = 0; k < c; k++) j = jac_dbl(j);
-                horner = jac_to_xyzz(j);
-            }
-            horner = xyzz_add(horner, xyzz_load<F>(window_sums + 8 * w));
-        }
-    }
-    if (tid == 64 && hide_table && hide_scalar) fe_ark_to_canonical_words<S>(hide_scalar, kw);
-    __syncthreads();
-    if (tid >= 64) {
-        const int i = tid - 64;
-        XYZZ<F> v = xyzz_id<F>();
-        if (hide_table && hide_scalar && ((kw[i >> 5] >> (i & 31)) & 1u))
-            v = xyzz_from_aff(aff_load<F>(hide_table + 4 * i));
-        xyzz_store(red + 8 * i, v);
-    }
-    __syncthreads();
-    for (int off = 128; off > 0; off >>= 1) {
-        const int i = tid - 64;
-        if (tid >= 64 && i < off)
-            xyzz_store(red + 8 * i, xyzz_add(xyzz_load<F>(red + 8 * i), xyzz_load<F>(red + 8 * (i + off))));
-        __syncthreads();
-    }
-    if (tid == 0) aff_to_wrapped(out_wrapped, xyzz_to_aff(xyzz_add(horner, xyzz_load<F>(red))));
-}
-
 
 static unsigned grid_for_t(size_t n, unsigned thr) { return (unsigned)std::max<size_t>(1, (n + thr - 1) / thr); }
 
@@ -248,8 +206,6 @@ static int tail_launch_t(const MsmTailArgs& a, hipStream_t ts) {
         hipLaunchKernelGGL(k_bitcombine<Cv>, dim3(a.SW), dim3(64), 0, ts, (const uint4*)a.terms, a.NT, a.logH, a.logL,
                            a.window_sums);
     }
-    hipLaunchKernelGGL(k_final<Cv>, dim3(1), dim3(320), 0, ts, (const uint4*)a.window_sums, a.SW, a.c, a.hide_table,
-                       a.hide_scalar, a.out_wrapped);
     HALO_HIP(hipGetLastError());
     return HALO_OK;
 }
