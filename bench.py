@@ -48,6 +48,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--sizes", default="24", help="extra MSM / NTT sizes (log2, comma separated) under extra.sizes")
     ap.add_argument("--dist-ntt-logn", type=int, default=24, help="distributed single NTT size (N > 1 only; 0 = off)")
+    ap.add_argument("--ipa", type=int, default=1, help="measure the 2^logn IPA opening (extra.ipa_open)")
     return ap.parse_args()
 
 
@@ -146,6 +147,53 @@ def main():
 
     elapsed, acc_avg_ms, sync_ok, lat, scalars0 = measure_msm(args.logn, args.steps, args.warmup)
     window_bits = L.halo_srs_window_bits(curve)
+
+    # ---- IPA opening (pcdl::open_without_eval round loop, pcdl.rs:392-438) at 2^logn:
+    # lg n rounds of L/R MSMs + fold over the device-resident (G, c, z), host stand-in transcript
+    def measure_ipa(logn):
+        n_ = 1 << logn
+        R = 0x40000000000000000000000000000000224698FC0994A8DD8C46EB2100000001
+
+        def fe1(v):
+            m = v * (1 << 256) % R
+            return np.array([(m >> (64 * i)) & (2**64 - 1) for i in range(4)], dtype=np.uint64)
+
+        rng = np.random.default_rng(99)
+        cs = rng.integers(0, 2**62, size=(n_, 4), dtype=np.uint64)
+        hp = np.zeros(8, dtype=np.uint64)
+        H.check(L.halo_srs_read(curve, 1, 1, H.ptr(hp)))
+        z = fe1(12345)
+        best = None
+        for _ in range(2):
+            ses = ctypes.c_void_p()
+            H.check(L.halo_ipa_begin(curve, H.ptr(cs), n_, H.ptr(z), H.ptr(hp), ctypes.byref(ses)))
+            Lp = np.zeros(8, dtype=np.uint64)
+            Rp = np.zeros(8, dtype=np.uint64)
+            L.halo_profile_reset()
+            L.halo_profile_enable(1)
+            a0 = time.perf_counter()
+            for r in range(logn):
+                H.check(L.halo_ipa_round_lr(ses, H.ptr(Lp), H.ptr(Rp)))
+                xi = (int.from_bytes(Lp.tobytes()[:16], "little") ^ (r + 1)) % R or 1
+                H.check(L.halo_ipa_fold(ses, H.ptr(fe1(xi)), H.ptr(fe1(pow(xi, -1, R)))))
+            U = np.zeros(8, dtype=np.uint64)
+            c0 = np.zeros(4, dtype=np.uint64)
+            H.check(L.halo_ipa_end(ses, H.ptr(U), H.ptr(c0)))
+            dt = (time.perf_counter() - a0) * 1e3
+            L.halo_profile_enable(0)
+            nl = ctypes.c_size_t(0)
+            fms = ctypes.c_double(0)
+            H.check(L.halo_profile_read(b"ipa_fold", ctypes.byref(nl), ctypes.byref(fms)))
+            if best is None or dt < best[0]:
+                best = (dt, fms.value)
+        return {
+            "workload": f"pcdl open round loop 2^{logn} (lg n rounds: L/R MSMs + GLV fold), device-resident",
+            "open_ms": best[0],
+            "fold_kernels_ms": best[1],
+            "rounds": logn,
+        }
+
+    ipa = measure_ipa(args.logn) if args.ipa else None
 
     # ---- NTT + iNTT pairs (configs[2] at 2^22, and the other BASELINE sizes); rank-local, under extra
     def measure_ntt(logn, nrep=10):
@@ -299,6 +347,7 @@ def main():
             "ntt": ntt_main,
             "sizes": sizes,
             "dist_ntt": dist_ntt,
+            "ipa_open": ipa,
         },
     }
     print(json.dumps(line))
