@@ -233,6 +233,34 @@ def main():
             "roofline_frac_pair": (2 * NTT_BYTES_PER_ELEM * N) / (pair_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
         }
 
+    # ---- evaluation algebra: pointwise product of two 2^23-element evaluation vectors
+    # (the prover's 8n domain at n = 2^20), HBM-streaming: 64 B read + 32 B written per element
+    def measure_evals(logn, nrep=20):
+        N = 1 << logn
+        a = torch.randint(-(2**63), 2**63 - 1, (N, 4), dtype=torch.int64, device="cuda", generator=gen)
+        b = torch.randint(-(2**63), 2**63 - 1, (N, 4), dtype=torch.int64, device="cuda", generator=gen)
+        a[:, 3] &= 0x0FFFFFFFFFFFFFFF
+        b[:, 3] &= 0x0FFFFFFFFFFFFFFF
+        o = torch.empty_like(a)
+        res = {}
+        for name, op in (("mul", 2), ("add", 0)):
+            for _ in range(2):
+                H.check(L.halo_evals_op_dev(H.FP, op, ctypes.c_void_p(a.data_ptr()), ctypes.c_void_p(b.data_ptr()),
+                                            None, 0, ctypes.c_void_p(o.data_ptr()), N, sp))
+            torch.cuda.synchronize()
+            a0 = time.perf_counter()
+            for _ in range(nrep):
+                H.check(L.halo_evals_op_dev(H.FP, op, ctypes.c_void_p(a.data_ptr()), ctypes.c_void_p(b.data_ptr()),
+                                            None, 0, ctypes.c_void_p(o.data_ptr()), N, sp))
+            torch.cuda.synchronize()
+            ms = (time.perf_counter() - a0) * 1e3 / nrep
+            gbs = 96 * N / (ms * 1e-3) / 1e9
+            res[name] = {"ms": ms, "achieved_GBps": gbs, "roofline_frac": gbs / HBM_PEAK_GBS}
+        del a, b, o
+        return {"workload": f"Evals pointwise op over 2^{logn} Fp elements (96 B/element)", **res}
+
+    evals = measure_evals(23)
+
     ntt_main = measure_ntt(args.ntt_logn)
     ntt_main["workload"] += " (BASELINE.json configs[2])"
     sizes = {}
@@ -348,6 +376,7 @@ def main():
             "sizes": sizes,
             "dist_ntt": dist_ntt,
             "ipa_open": ipa,
+            "evals_op": evals,
         },
     }
     print(json.dumps(line))

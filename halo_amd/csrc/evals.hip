@@ -1,0 +1,184 @@
+// SURVEY §8f row f1 (first slice): the prover's elementwise polynomial-evaluation algebra and the
+// vanishing-polynomial division, device-resident.
+//
+//   Evals ops (crates/group/src/poly.rs:90-327): pointwise add / sub / mul of two evaluation
+//   vectors, scale / add_scalar / sub_scalar by one scalar, and x^e (the Poseidon S-box x^7 of the
+//   gate evaluation, protocol.rs:591-1011).
+//   DensePolynomial::divide_by_vanishing_poly (ark-poly 0.5.0, called at protocol.rs:256): for
+//   Z_H = X^n - 1, quotient q[j] = sum_{k >= 1} c[j + k n] and remainder r[j] = c[j] + q[j] (j < n),
+//   both trimmed.
+//
+// These are HBM-streaming kernels (one read per operand, one write): every lane handles whole
+// 32-byte elements with two dwordx4 accesses, consecutive lanes consecutive elements.  Values stay
+// in the ark format (Montgomery R = 2^256): additions are format-agnostic; a product of two ark
+// values through the R' = 2^261 multiplier carries 2^-5 too many, fixed by one multiplication by
+// 2^266 mod p (ARK_MUL_FIX, computed on the host side of the launch).
+#include <algorithm>
+
+#include "dispatch.hpp"
+#include "runtime.hpp"
+
+namespace halo {
+
+enum EvalsOp { EV_ADD = 0, EV_SUB = 1, EV_MUL = 2, EV_SCALE = 3, EV_ADD_SCALAR = 4, EV_SUB_SCALAR = 5, EV_POW = 6 };
+
+template <class F>
+__global__ __launch_bounds__(256) void k_evals_op(int op, const uint4* a, const uint4* b, Fe<F> s, uint32_t e,
+                                                  Fe<F> fix, uint4* out, size_t n) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const Fe<F> x = fe_load<F>(a + 2 * i);
+    Fe<F> r;
+    switch (op) {
+        case EV_ADD: r = fe_add(x, fe_load<F>(b + 2 * i)); break;
+        case EV_SUB: r = fe_sub(x, fe_load<F>(b + 2 * i)); break;
+        case EV_MUL: r = fe_mul(fe_mul(x, fe_load<F>(b + 2 * i)), fix); break;
+        case EV_SCALE: r = fe_mul(fe_mul(x, s), fix); break;
+        case EV_ADD_SCALAR: r = fe_add(x, s); break;
+        case EV_SUB_SCALAR: r = fe_sub(x, s); break;
+        default: {  // EV_POW: internal domain, square-and-multiply
+            const Fe<F> xi = fe_mul(x, fe_from_const<F>(F::ARK2INT));
+            Fe<F> acc = fe_one<F>();
+            for (int bit = 31; bit >= 0; bit--) {
+                acc = fe_sqr(acc);
+                if ((e >> bit) & 1u) acc = fe_mul(acc, xi);
+            }
+            r = fe_mul(acc, fe_from_const<F>(F::INT2ARK));
+        }
+    }
+    fe_store(out + 2 * i, fe_canon(r));
+}
+
+// q[j] = sum_{k >= 1, j + k n < len} c[j + k n]  (j < len - n);  r[j] = c[j] + q[j]  (j < n)
+template <class F>
+__global__ __launch_bounds__(256) void k_div_vanishing(const uint4* c, size_t len, size_t n, uint4* q, uint4* r) {
+    const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t qn = len - n;
+    if (j < qn) {
+        Fe<F> acc = fe_zero<F>();
+        for (size_t k = j + n; k < len; k += n) acc = fe_add(acc, fe_load<F>(c + 2 * k));
+        fe_store(q + 2 * j, fe_canon(acc));
+    }
+    if (j < n) {
+        Fe<F> acc = fe_load<F>(c + 2 * j);
+        for (size_t k = j + n; k < len; k += n) acc = fe_add(acc, fe_load<F>(c + 2 * k));
+        fe_store(r + 2 * j, fe_canon(acc));
+    }
+}
+
+template <class F>
+static Fe<F> host_fe_raw(const uint32_t (&k)[NLIMB]) {
+    Fe<F> r;
+    for (int i = 0; i < NLIMB; i++) r.v[i] = k[i];
+    return r;
+}
+
+// host: packs an ark scalar (4 x u64) into the 9 x 29-bit limb form (ark words used as-is)
+template <class F>
+static Fe<F> host_fe_from_words(const halo_fe_t& w) {
+    Fe<F> r;
+    for (int i = 0; i < NLIMB; i++) {
+        const int bit = 29 * i;
+        const int q = bit / 64, s = bit % 64;
+        uint64_t v = w.l[q] >> s;
+        if (s > 35 && q + 1 < 4) v |= w.l[q + 1] << (64 - s);
+        r.v[i] = (uint32_t)v & ((i == NLIMB - 1) ? 0xffffffffu : LIMB_MASK);
+    }
+    return r;
+}
+
+static int evals_launch(int field, int op, const void* a, const void* b, const halo_fe_t* scalar, uint32_t e,
+                        void* out, size_t n, hipStream_t s) {
+    if (!n) return HALO_OK;
+    const unsigned thr = 256, blocks = (unsigned)((n + thr - 1) / thr);
+    DISPATCH_FIELD(field, F, {
+        halo_fe_t zero = {{0, 0, 0, 0}};
+        const Fe<F> sv = host_fe_from_words<F>(scalar ? *scalar : zero);
+        const Fe<F> fix = host_fe_raw<F>(F::ARK_MUL_FIX);
+        hipLaunchKernelGGL(k_evals_op<F>, dim3(blocks), dim3(thr), 0, s, op, (const uint4*)a, (const uint4*)b, sv, e,
+                           fix, (uint4*)out, n);
+    });
+    HALO_HIP(hipGetLastError());
+    return HALO_OK;
+}
+
+static int check_evals_args(halo_field_t field, int op, const void* a, const void* b, const halo_fe_t* scalar,
+                            const void* out, size_t n) {
+    if (field != HALO_FP && field != HALO_FQ) return set_error(HALO_EINVAL, "unknown field id %d", (int)field);
+    if (op < EV_ADD || op > EV_POW) return set_error(HALO_EINVAL, "unknown evals op %d", op);
+    if (n && (!a || !out)) return set_error(HALO_EINVAL, "halo_evals_op: null buffer");
+    if (n && op <= EV_MUL && !b) return set_error(HALO_EINVAL, "halo_evals_op: op %d needs a second operand", op);
+    if (op >= EV_SCALE && op <= EV_SUB_SCALAR && !scalar) return set_error(HALO_EINVAL, "halo_evals_op: null scalar");
+    return HALO_OK;
+}
+
+}  // namespace halo
+
+using namespace halo;
+
+extern "C" int halo_evals_op_dev(halo_field_t field, int op, const void* d_a, const void* d_b, const halo_fe_t* scalar,
+                                 uint32_t exponent, void* d_out, size_t n, void* stream) {
+    clear_error();
+    HALO_CHECK(check_evals_args(field, op, d_a, d_b, scalar, d_out, n));
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    return evals_launch(field, op, d_a, d_b, scalar, exponent, d_out, n, (hipStream_t)stream);
+}
+
+extern "C" int halo_evals_op(halo_field_t field, int op, const halo_fe_t* a, const halo_fe_t* b, const halo_fe_t* scalar,
+                             uint32_t exponent, halo_fe_t* out, size_t n) {
+    clear_error();
+    HALO_CHECK(check_evals_args(field, op, a, b, scalar, out, n));
+    if (!n) return HALO_OK;
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    hipStream_t s = 0;
+    HALO_CHECK(st->scratch[0].reserve(n * 32));
+    HALO_CHECK(st->scratch[1].reserve(n * 32));
+    HALO_CHECK(copy_h2d(st->scratch[0].ptr, a, n * 32, s));
+    if (op <= EV_MUL) HALO_CHECK(copy_h2d(st->scratch[1].ptr, b, n * 32, s));
+    HALO_CHECK(evals_launch(field, op, st->scratch[0].ptr, st->scratch[1].ptr, scalar, exponent, st->scratch[0].ptr, n, s));
+    return copy_d2h(out, st->scratch[0].ptr, n * 32, s);
+}
+
+static size_t trimmed(const halo_fe_t* c, size_t len) {
+    while (len > 0 && !(c[len - 1].l[0] | c[len - 1].l[1] | c[len - 1].l[2] | c[len - 1].l[3])) len--;
+    return len;
+}
+
+extern "C" int halo_divide_by_vanishing(halo_field_t field, const halo_fe_t* coeffs, size_t len, size_t n,
+                                        halo_fe_t* quotient, size_t* q_len, halo_fe_t* remainder, size_t* r_len) {
+    clear_error();
+    if (field != HALO_FP && field != HALO_FQ) return set_error(HALO_EINVAL, "unknown field id %d", (int)field);
+    if (!n || (len && !coeffs) || !quotient || !remainder || !q_len || !r_len)
+        return set_error(HALO_EINVAL, "halo_divide_by_vanishing: null argument");
+    len = trimmed(coeffs, len);
+    if (len < n) {  // quotient zero, remainder = self
+        for (size_t j = 0; j < len; j++) remainder[j] = coeffs[j];
+        *q_len = 0;
+        *r_len = len;
+        return HALO_OK;
+    }
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    hipStream_t s = 0;
+    const size_t qn = len - n;
+    HALO_CHECK(st->scratch[0].reserve(len * 32));
+    HALO_CHECK(st->scratch[1].reserve(std::max<size_t>(qn, 1) * 32));
+    HALO_CHECK(st->scratch[2].reserve(n * 32));
+    HALO_CHECK(copy_h2d(st->scratch[0].ptr, coeffs, len * 32, s));
+    const size_t threads = std::max(qn, n);
+    DISPATCH_FIELD(field, F, {
+        hipLaunchKernelGGL(k_div_vanishing<F>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
+                           st->scratch[0].as<const uint4>(), len, n, st->scratch[1].as<uint4>(),
+                           st->scratch[2].as<uint4>());
+    });
+    HALO_HIP(hipGetLastError());
+    if (qn) HALO_CHECK(copy_d2h(quotient, st->scratch[1].ptr, qn * 32, s));
+    HALO_CHECK(copy_d2h(remainder, st->scratch[2].ptr, n * 32, s));
+    *q_len = trimmed(quotient, qn);
+    *r_len = trimmed(remainder, n);
+    return HALO_OK;
+}

@@ -64,6 +64,72 @@ class Evals:
 
     interpolate = interpolate_by_ref
 
+    # ---- elementwise algebra (poly.rs:90-327), on the device (halo_evals_op) ----
+    def _op(self, op: int, other=None, scalar=None, e: int = 0) -> "Evals":
+        H.ensure_device()
+        n = len(self.evals)
+        b = None
+        if other is not None:
+            b = other.evals if isinstance(other, Evals) else H.fe_array(other)
+            assert len(b) == n, "evaluation vectors of different lengths"
+        sc = H.fe_array(scalar, 1) if scalar is not None else None
+        out = np.zeros((n, 4), dtype=np.uint64)
+        H.check(H.load().halo_evals_op(self.domain.field, op, H.ptr(self.evals), H.ptr(b), H.ptr(sc), e, H.ptr(out), n))
+        return Evals(out, self.domain)
+
+    def __add__(self, other):
+        return self._op(0, other)
+
+    def __sub__(self, other):
+        return self._op(1, other)
+
+    def __mul__(self, other):
+        return self._op(2, other)
+
+    def scale(self, s):
+        return self._op(3, scalar=s)
+
+    def add_scalar(self, s):
+        return self._op(4, scalar=s)
+
+    def sub_scalar(self, s):
+        return self._op(5, scalar=s)
+
+    def pow(self, e: int):
+        return self._op(6, e=e)
+
+
+def divide_by_vanishing_poly(coeffs, domain: Domain):
+    """``DensePolynomial::divide_by_vanishing_poly`` (ark-poly 0.5.0, protocol.rs:256): division by
+    X^n - 1 -> (quotient, remainder), both trimmed."""
+    H.ensure_device()
+    c = H.fe_array(coeffs) if len(coeffs) else np.zeros((0, 4), dtype=np.uint64)
+    n = domain.n
+    q = np.zeros((max(len(c) - n, 0) + 1, 4), dtype=np.uint64)
+    r = np.zeros((n, 4), dtype=np.uint64)
+    ql, rl = ctypes.c_size_t(0), ctypes.c_size_t(0)
+    H.check(H.load().halo_divide_by_vanishing(domain.field, H.ptr(c) if len(c) else None, len(c), n, H.ptr(q),
+                                              ctypes.byref(ql), H.ptr(r), ctypes.byref(rl)))
+    return q[: ql.value].copy(), r[: rl.value].copy()
+
+
+def t_split(t, n: int, parts: int):
+    """protocol.rs:509-517: t (degree < parts * n) zero-padded and cut into `parts` chunks of n."""
+    t = H.fe_array(t) if len(t) else np.zeros((0, 4), dtype=np.uint64)
+    deg = max(len(t) - 1, 0)
+    if not deg < parts * n:
+        raise AssertionError(f"{deg} < {parts * n}")
+    pad = np.zeros((parts * n, 4), dtype=np.uint64)
+    pad[: len(t)] = t
+    out = []
+    for i in range(parts):
+        chunk = pad[i * n:(i + 1) * n]
+        m = len(chunk)
+        while m > 0 and not chunk[m - 1].any():
+            m -= 1
+        out.append(chunk[:m].copy())
+    return out
+
 
 def poly_mul(a, b, field="fp") -> np.ndarray:
     """``&DensePolynomial * &DensePolynomial`` (FFT multiplication), trimmed."""

@@ -182,6 +182,19 @@ int halo_pcdl_decider_commit(halo_curve_t curve, const halo_fe_t* xis, size_t n_
 int halo_trace_commit_batch(halo_curve_t curve, const halo_fe_t* evals, size_t k, unsigned log_n, size_t d,
                             halo_fe_t* coeffs_out, size_t* lens_out, halo_wrapped_point_t* commits_out);
 
+/* ------------------------------------------------------------------ f1: evaluation algebra
+ * Evals ops (crates/group/src/poly.rs:90-327), elementwise over n ark scalars:
+ *   op 0 add (a + b), 1 sub (a - b), 2 mul (a * b), 3 scale (a * scalar), 4 add_scalar, 5 sub_scalar,
+ *   6 pow (a^exponent, e.g. the Poseidon S-box x^7).  out may alias a or b. */
+int halo_evals_op(halo_field_t field, int op, const halo_fe_t* a, const halo_fe_t* b, const halo_fe_t* scalar,
+                  uint32_t exponent, halo_fe_t* out, size_t n);
+int halo_evals_op_dev(halo_field_t field, int op, const void* d_a, const void* d_b, const halo_fe_t* scalar,
+                      uint32_t exponent, void* d_out, size_t n, void* stream);
+/* DensePolynomial::divide_by_vanishing_poly (ark-poly 0.5.0; protocol.rs:256): division by
+ * X^n - 1; quotient (room for len - n) and remainder (room for n), both trimmed. */
+int halo_divide_by_vanishing(halo_field_t field, const halo_fe_t* coeffs, size_t len, size_t n, halo_fe_t* quotient,
+                             size_t* q_len, halo_fe_t* remainder, size_t* r_len);
+
 /* ------------------------------------------------------------------ a8: evaluation / dots */
 /* DensePolynomial::evaluate (Horner; pcdl.rs:49,471), k polynomials at one point z. */
 int halo_poly_eval_batch(halo_field_t field, const halo_fe_t* const* polys, const size_t* lens,

@@ -208,3 +208,59 @@ def test_transpose_and_twiddle_dev(hal, corc):
             a, bb = divmod(i, cols)
             v = P.from_mont(P.limbs_to_int(x[i]), m) * pow(w, (row0 + a) * (col0 + bb), m) % m
             assert P.from_mont(P.limbs_to_int(got[i]), m) == v
+
+
+# ---- evaluation algebra and vanishing division ---------------------------------------
+@pytest.mark.parametrize("tag", ["fp", "fq"])
+def test_evals_ops_vs_python(hal, tag):
+    m = P.FIELDS[tag]
+    dom = poly.Domain(1 << 10, tag)
+    rnd = random.Random(3)
+    a = [rnd.randrange(m) for _ in range(dom.n)]
+    b = [rnd.randrange(m) for _ in range(dom.n)]
+    a[0], b[1] = m - 1, 0
+    A = poly.Evals(fe(a, m), dom)
+    B = poly.Evals(fe(b, m), dom)
+    s = rnd.randrange(m)
+    chk = {
+        "add": ((A + B), [(x + y) % m for x, y in zip(a, b)]),
+        "sub": ((A - B), [(x - y) % m for x, y in zip(a, b)]),
+        "mul": ((A * B), [(x * y) % m for x, y in zip(a, b)]),
+        "scale": (A.scale(fe([s], m)[0]), [(x * s) % m for x in a]),
+        "add_scalar": (A.add_scalar(fe([s], m)[0]), [(x + s) % m for x in a]),
+        "sub_scalar": (A.sub_scalar(fe([s], m)[0]), [(x - s) % m for x in a]),
+        "pow7": (A.pow(7), [pow(x, 7, m) for x in a]),
+    }
+    for name, (got, exp) in chk.items():
+        assert [P.from_mont(P.limbs_to_int(r), m) for r in got.evals] == exp, name
+
+
+@pytest.mark.parametrize("tag", ["fp", "fq"])
+def test_divide_by_vanishing_poly(hal, tag):
+    """ark-poly divide_by_vanishing_poly (protocol.rs:256): p = q (X^n - 1) + r with deg r < n,
+    checked against Python long division, incl. len < n, len = n, len > 2n, trailing zeros."""
+    m = P.FIELDS[tag]
+    rnd = random.Random(9)
+    n = 64
+    dom = poly.Domain(n, tag)
+    for ln in (0, 5, n, n + 1, 2 * n + 3, 8 * n, 8 * n - 7):
+        c = [rnd.randrange(m) for _ in range(ln)]
+        if ln > 3:
+            c[-1] = rnd.randrange(1, m)
+        q, r = poly.divide_by_vanishing_poly(fe(c, m) if ln else [], dom)
+        # Python: quotient q[j] = sum_{k>=1} c[j + k n], remainder c[j] + q[j]
+        qe = [sum(c[j + k * n] for k in range(1, (ln - j - 1) // n + 1)) % m for j in range(max(ln - n, 0))]
+        re = [(c[j] + (qe[j] if j < len(qe) else 0)) % m for j in range(min(ln, n))] if ln >= n else c[:]
+        while qe and qe[-1] == 0:
+            qe.pop()
+        while re and re[-1] == 0:
+            re.pop()
+        assert [P.from_mont(P.limbs_to_int(x), m) for x in q] == qe, ln
+        assert [P.from_mont(P.limbs_to_int(x), m) for x in r] == re, ln
+        # and the defining identity at a random point
+        if ln:
+            z = rnd.randrange(m)
+            ev = lambda cs: sum(v * pow(z, i, m) for i, v in enumerate(cs)) % m
+            assert ev(c) == (ev(qe) * (pow(z, n, m) - 1) + ev(re)) % m
+    ts = poly.t_split(fe([rnd.randrange(m) for _ in range(3 * n - 2)], m), n, 3)
+    assert [len(t) for t in ts] == [n, n, n - 2]
