@@ -79,6 +79,7 @@ SIGNATURES = {
     "halo_hpoly_combine": [ctypes.c_int, _vp, _sz, _sz, _vp, _vp, ctypes.POINTER(_sz)],
     "halo_pcdl_decider_commit": [ctypes.c_int, _vp, _sz, _sz, _vp],
     "halo_trace_commit_batch": [ctypes.c_int, _vp, _sz, ctypes.c_uint, _sz, _vp, _vp, _vp],
+    "halo_srs_load_bincode": [ctypes.c_int, _vp, _vp, _sz, _vp, _sz, _sz],
     "halo_evals_op": [ctypes.c_int, ctypes.c_int, _vp, _vp, _vp, ctypes.c_uint32, _vp, _sz],
     "halo_evals_op_dev": [ctypes.c_int, ctypes.c_int, _vp, _vp, _vp, ctypes.c_uint32, _vp, _sz, _vp],
     "halo_divide_by_vanishing": [ctypes.c_int, _vp, _sz, _sz, _vp, ctypes.POINTER(_sz), _vp, ctypes.POINTER(_sz)],

@@ -18,6 +18,7 @@
 //   7. final    : Horner over the windows (+ w * S for hiding commitments), XYZZ -> affine -> ark.
 #include <algorithm>
 #include <type_traits>
+#include <vector>
 #include <cstdlib>
 
 #include "dispatch.hpp"
@@ -695,6 +696,30 @@ extern "C" int halo_msm(halo_curve_t curve, const halo_wrapped_point_t* bases, s
 }
 
 // SRS management --------------------------------------------------------------------------------
+// Installs n WrappedPoints already in device memory (d_wrapped, may be scratch[0]) as the resident
+// SRS of `curve`, plus (S, H) when given (host WrappedPoints).
+static int srs_install(DeviceState* st, int curve, const void* d_wrapped, size_t n, const halo_wrapped_point_t* S,
+                       const halo_wrapped_point_t* H, hipStream_t s) {
+    SrsState& srs = st->srs[curve];
+    HALO_CHECK(srs.gs.reserve(std::max<size_t>(n, 1) * 64));
+    HALO_CHECK(convert_wrapped_to_internal(curve, d_wrapped, srs.gs.ptr, n, s));
+    srs.n = n;
+    srs.shifted_c = 0;
+    if (S && H) {
+        HALO_CHECK(st->scratch[1].reserve(256));
+        char* tmp = (char*)st->scratch[1].ptr;
+        HALO_CHECK(copy_h2d(tmp, S, 64, s));
+        HALO_CHECK(copy_h2d(tmp + 64, H, 64, s));
+        HALO_CHECK(convert_wrapped_to_internal(curve, tmp, tmp + 128, 2, s));
+        HALO_CHECK(copy_d2h(srs.S, tmp + 128, 64, s));
+        HALO_CHECK(copy_d2h(srs.H, tmp + 192, 64, s));
+        srs.has_sh = true;
+        HALO_CHECK(build_s_table(st, curve, s));
+    }
+    HALO_HIP(hipStreamSynchronize(s));
+    return HALO_OK;
+}
+
 extern "C" int halo_srs_upload(halo_curve_t curve, const halo_wrapped_point_t* gs, size_t n,
                                const halo_wrapped_point_t* S, const halo_wrapped_point_t* H) {
     clear_error();
@@ -704,25 +729,135 @@ extern "C" int halo_srs_upload(halo_curve_t curve, const halo_wrapped_point_t* g
     if (!st) return HALO_EDEVICE;
     std::lock_guard<std::mutex> g(st->mu);
     hipStream_t s = 0;
-    SrsState& srs = st->srs[curve];
-    HALO_CHECK(srs.gs.reserve(std::max<size_t>(n, 1) * 64));
     HALO_CHECK(st->scratch[0].reserve(std::max<size_t>(n, 2) * 64));
     HALO_CHECK(copy_h2d(st->scratch[0].ptr, gs, n * 64, s));
-    HALO_CHECK(convert_wrapped_to_internal(curve, st->scratch[0].ptr, srs.gs.ptr, n, s));
-    srs.n = n;
-    srs.shifted_c = 0;
-    if (S && H) {
-        HALO_CHECK(st->scratch[1].reserve(128));
-        HALO_CHECK(copy_h2d(st->scratch[0].ptr, S, 64, s));
-        HALO_CHECK(copy_h2d((char*)st->scratch[0].ptr + 64, H, 64, s));
-        HALO_CHECK(convert_wrapped_to_internal(curve, st->scratch[0].ptr, st->scratch[1].ptr, 2, s));
-        HALO_CHECK(copy_d2h(srs.S, st->scratch[1].ptr, 64, s));
-        HALO_CHECK(copy_d2h(srs.H, (char*)st->scratch[1].ptr + 64, 64, s));
-        srs.has_sh = true;
-        HALO_CHECK(build_s_table(st, curve, s));
+    return srs_install(st, curve, st->scratch[0].ptr, n, S, H, s);
+}
+
+// ---------------------------------------------------------------------------------------------
+// the SRS wire format (bincode-v2 `standard()` Vec<WrappedPoint> per block,
+// pp.rs:36-53; (S, H) tuple in sh.bin) decoded on the device.  A block whose records are all in the
+// fixed 72-byte form (every u64 limb as 0xFD + 8 LE bytes -- what the reference's generator writes
+// for Montgomery limbs >= 2^32) is decoded by k_decode_points, one record per lane; any other
+// record (a small limb gets a shorter varint) sends that block through the sequential host decoder.
+// Every point is then checked on the curve on the device (wrappers.rs:606 `assert!(is_on_curve)`).
+// ---------------------------------------------------------------------------------------------
+__global__ void k_decode_points(const uint8_t* rec0, size_t count, uint4* out, uint32_t* bad) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const uint8_t* r = rec0 + 72 * i;
+    uint32_t w[16];
+    bool ok = true;
+#pragma unroll
+    for (int l = 0; l < 8; l++) {
+        const uint8_t* f = r + 9 * l;
+        ok &= (f[0] == 0xFD);
+        w[2 * l] = (uint32_t)f[1] | ((uint32_t)f[2] << 8) | ((uint32_t)f[3] << 16) | ((uint32_t)f[4] << 24);
+        w[2 * l + 1] = (uint32_t)f[5] | ((uint32_t)f[6] << 8) | ((uint32_t)f[7] << 16) | ((uint32_t)f[8] << 24);
     }
-    HALO_HIP(hipStreamSynchronize(s));
-    return HALO_OK;
+    if (!ok) atomicOr(bad, 1u);
+    out[4 * i] = make_uint4(w[0], w[1], w[2], w[3]);
+    out[4 * i + 1] = make_uint4(w[4], w[5], w[6], w[7]);
+    out[4 * i + 2] = make_uint4(w[8], w[9], w[10], w[11]);
+    out[4 * i + 3] = make_uint4(w[12], w[13], w[14], w[15]);
+}
+
+template <class Cv>
+__global__ void k_check_on_curve(const uint4* pts_wrapped, size_t n, uint32_t* bad) {
+    using F = typename Cv::Base;
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const Affine<F> a = aff_from_wrapped<F>(pts_wrapped + 4 * i);
+    // y^2 == x^3 + 5 (the identity (0, 0) is not on the curve, as for ark's Affine::new_unchecked)
+    const Fe<F> lhs = fe_sqr(a.y);
+    const Fe<F> rhs = fe_add(fe_mul(fe_sqr(a.x), a.x), fe_from_const<F>(Cv::K::B));
+    if (!fe_eq(lhs, rhs)) atomicAdd(bad, 1u);
+}
+
+// bincode-v2 standard() unsigned varint
+static bool bc_varint(const uint8_t* b, size_t len, size_t& off, uint64_t& v) {
+    if (off >= len) return false;
+    const uint8_t t = b[off];
+    if (t < 251) {
+        v = t;
+        off += 1;
+        return true;
+    }
+    const int width = t == 251 ? 2 : t == 252 ? 4 : t == 253 ? 8 : 0;
+    if (!width || off + 1 + width > len) return false;
+    v = 0;
+    for (int i = 0; i < width; i++) v |= (uint64_t)b[off + 1 + i] << (8 * i);
+    off += 1 + width;
+    return true;
+}
+
+static bool bc_point(const uint8_t* b, size_t len, size_t& off, halo_wrapped_point_t& p) {
+    for (int l = 0; l < 4; l++)
+        if (!bc_varint(b, len, off, p.x[l])) return false;
+    for (int l = 0; l < 4; l++)
+        if (!bc_varint(b, len, off, p.y[l])) return false;
+    return true;
+}
+
+extern "C" int halo_srs_load_bincode(halo_curve_t curve, const uint8_t* const* blocks, const size_t* block_lens,
+                                     size_t nblocks, const uint8_t* sh, size_t sh_len, size_t n) {
+    clear_error();
+    HALO_CHECK(check_curve(curve));
+    if (!is_pow2(n)) return set_error(HALO_ENOTPOW2, "assertion failed: n.is_power_of_two()");
+    if (nblocks && (!blocks || !block_lens)) return set_error(HALO_EINVAL, "halo_srs_load_bincode: null blocks");
+    halo_wrapped_point_t SH[2];
+    if (sh) {
+        size_t off = 0;
+        if (!bc_point(sh, sh_len, off, SH[0]) || !bc_point(sh, sh_len, off, SH[1]))
+            return set_error(HALO_EINVAL, "Failed to get SH data for curve %s", curve == HALO_PALLAS ? "pallas" : "vesta");
+    }
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    hipStream_t s = 0;
+    HALO_CHECK(st->scratch[0].reserve(std::max<size_t>(n, 2) * 64));
+    HALO_CHECK(st->scratch[2].reserve(16));
+    uint4* d_pts = st->scratch[0].as<uint4>();
+    uint32_t* d_bad = st->scratch[2].as<uint32_t>();
+    size_t have = 0;
+    std::vector<halo_wrapped_point_t> host_pts;
+    for (size_t bi = 0; bi < nblocks && have < n; bi++) {
+        const uint8_t* b = blocks[bi];
+        const size_t len = block_lens[bi];
+        size_t off = 0;
+        uint64_t count = 0;
+        if (!b || !bc_varint(b, len, off, count)) return set_error(HALO_EINVAL, "Failed to decode G_BLOCKS_NO %zu", bi);
+        const size_t take = std::min<size_t>(count, n - have);
+        bool fast = (len - off) >= 72 * take;
+        if (fast && take) {
+            HALO_CHECK(st->scratch[3].reserve(72 * take));
+            HALO_HIP(hipMemsetAsync(d_bad, 0, 4, s));
+            HALO_CHECK(copy_h2d(st->scratch[3].ptr, b + off, 72 * take, s));
+            hipLaunchKernelGGL(k_decode_points, dim3(grid_for(take, 256)), dim3(256), 0, s,
+                               st->scratch[3].as<const uint8_t>(), take, d_pts + 4 * have, d_bad);
+            HALO_HIP(hipGetLastError());
+            uint32_t bad = 0;
+            HALO_CHECK(copy_d2h(&bad, d_bad, 4, s));
+            fast = (bad == 0);
+        }
+        if (!fast) {  // general varints: sequential host decode of this block
+            host_pts.resize(take);
+            for (size_t i = 0; i < take; i++)
+                if (!bc_point(b, len, off, host_pts[i])) return set_error(HALO_EINVAL, "Failed to decode G_BLOCKS_NO %zu", bi);
+            HALO_CHECK(copy_h2d(d_pts + 4 * have, host_pts.data(), take * 64, s));
+        }
+        have += take;
+    }
+    if (have < n) return set_error(HALO_ESRSRANGE, "assertion failed: n <= N (%zu points available)", have);
+    HALO_HIP(hipMemsetAsync(d_bad, 0, 4, s));
+    DISPATCH_CURVE(curve, Cv, {
+        hipLaunchKernelGGL(k_check_on_curve<Cv>, dim3(grid_for(n, 256)), dim3(256), 0, s, (const uint4*)d_pts, n, d_bad);
+    });
+    HALO_HIP(hipGetLastError());
+    uint32_t bad = 0;
+    HALO_CHECK(copy_d2h(&bad, d_bad, 4, s));
+    if (bad) return set_error(HALO_EINVAL, "assertion failed: affine.is_on_curve() (%u points)", bad);
+    return srs_install(st, curve, d_pts, n, sh ? &SH[0] : nullptr, sh ? &SH[1] : nullptr, s);
 }
 
 extern "C" int halo_srs_len(halo_curve_t curve, size_t* n) {

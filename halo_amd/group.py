@@ -78,6 +78,28 @@ class PublicParams:
             H.check(L.halo_srs_precompute_windows(_curve(curve)))
 
     @staticmethod
+    def load_bincode(curve, blocks, sh=None, n: int | None = None, precompute_windows: bool = True) -> None:
+        """PublicParams::new(n) from the wire format (pp.rs:26-61): `blocks` = the gs-XX.bin byte
+        strings in order, `sh` = sh.bin; decoded and curve-checked on the device."""
+        H.ensure_device()
+        bl = [bytes(b) for b in blocks]
+        k = len(bl)
+        arrs = [np.frombuffer(b, dtype=np.uint8) for b in bl]
+        ptrs = (ctypes.c_void_p * max(k, 1))(*[a.ctypes.data for a in arrs])
+        lens = (ctypes.c_size_t * max(k, 1))(*[len(b) for b in bl])
+        sha = np.frombuffer(bytes(sh), dtype=np.uint8) if sh is not None else None
+        if n is None:
+            n = 0
+            for b in bl:  # count prefix of each block (bincode varint)
+                t = b[0]
+                n += t if t < 251 else int.from_bytes(b[1:1 + {251: 2, 252: 4, 253: 8}[t]], "little")
+        L = H.load()
+        H.check(L.halo_srs_load_bincode(_curve(curve), ctypes.cast(ptrs, ctypes.c_void_p), ctypes.cast(lens, ctypes.c_void_p),
+                                        k, H.ptr(sha) if sha is not None else None, len(sha) if sha is not None else 0, n))
+        if precompute_windows:
+            H.check(L.halo_srs_precompute_windows(_curve(curve)))
+
+    @staticmethod
     def len(curve) -> int:
         H.ensure_device()
         n = ctypes.c_size_t(0)

@@ -73,6 +73,13 @@ int halo_stream_sync(void* stream);
  * `Vec<WrappedPoint>` of crates/group/.precompute/<curve>/gs-XX.bin (or any prefix of it). */
 int halo_srs_upload(halo_curve_t curve, const halo_wrapped_point_t* gs, size_t n,
                     const halo_wrapped_point_t* S, const halo_wrapped_point_t* H);
+/* f3: PublicParams::new(n) from the wire format (pp.rs:26-61): `blocks` are the gs-XX.bin files
+ * (bincode-v2 standard() Vec<WrappedPoint>, decoded in order until n points), `sh` is sh.bin
+ * ((S, H); may be NULL).  Decoded and curve-checked on the device; the reference's panics map to
+ * HALO_ENOTPOW2 ("assertion failed: n.is_power_of_two()"), HALO_ESRSRANGE (n > available points),
+ * HALO_EINVAL ("Failed to decode G_BLOCKS_NO i", "assertion failed: affine.is_on_curve()"). */
+int halo_srs_load_bincode(halo_curve_t curve, const uint8_t* const* blocks, const size_t* block_lens, size_t nblocks,
+                          const uint8_t* sh, size_t sh_len, size_t n);
 /* Current resident SRS length (0 if none). */
 int halo_srs_len(halo_curve_t curve, size_t* n);
 /* Synthetic SRS for sizes beyond the reference's N = 2^20 (crates/group/src/consts.rs:1):

@@ -4,7 +4,8 @@ checkout is mounted read-only at /root/reference:
 
     python3 tests/golden/make_golden.py
 
-Two kinds of arrays are written (all uint64, loaded with numpy's default allow_pickle=False):
+Two kinds of arrays are written (uint64, and uint8 for raw wire bytes; loaded with numpy's default
+allow_pickle=False):
 
 1. Data copied from the reference's own committed artefacts (the reference is Rust and cannot be
    built or run here -- SURVEY §8c -- so these are the only reference-produced values available):
@@ -12,6 +13,8 @@ Two kinds of arrays are written (all uint64, loaded with numpy's default allow_p
                            (bincode Vec<WrappedPoint>, pp.rs:36-53) -- first 64 of block 0, first 8 of
                            block 1 and the last 8 of block 63;
    * ref_sh_<curve>      : (S, H) from sh.bin;
+   * ref_gs_<curve>_b00_head_bytes / ref_sh_<curve>_bytes : raw bytes (length prefix + first 64
+                           records of gs-00.bin; all of sh.bin) for the device bincode loader;
    * ref_omega_fp16 / ref_omega_fq16 : IVC_FP_CIRCUIT.omega / IVC_FQ_CIRCUIT.omega
                            (crates/plonk/src/frontend/ivc/mod.rs:55,112), Montgomery limbs.
 2. Golden vectors computed by the pure-Python oracle (oracle/pasta.py) from seeded inputs on top of
@@ -55,6 +58,12 @@ def main():
         out[f"ref_srs_{cname}_b01_first8"] = np.array(b1, dtype=np.uint64)
         out[f"ref_srs_{cname}_b63_last8"] = np.array(b63[n63 - 8:], dtype=np.uint64)
         out[f"ref_sh_{cname}"] = np.array(P.decode_sh(open(d + "sh.bin", "rb").read()), dtype=np.uint64)
+        # raw wire bytes (uint8) for the bincode loader test: the varint length prefix and the first
+        # 64 records of gs-00.bin verbatim, and the whole sh.bin
+        raw = open(d + "gs-00.bin", "rb").read()
+        _, off = P.bincode_varint(raw, 0)
+        out[f"ref_gs_{cname}_b00_head_bytes"] = np.frombuffer(raw[: off + 64 * 72], dtype=np.uint8).copy()
+        out[f"ref_sh_{cname}_bytes"] = np.frombuffer(open(d + "sh.bin", "rb").read(), dtype=np.uint8).copy()
     ivc = open(f"{REF}/plonk/src/frontend/ivc/mod.rs").read()
     for tag, name in (("fp", "IVC_FP_CIRCUIT"), ("fq", "IVC_FQ_CIRCUIT")):
         block = ivc[ivc.index(f"pub const {name}"):]

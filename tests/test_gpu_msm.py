@@ -270,3 +270,47 @@ def test_trace_commit_batch(hal, corc, cname, cid):
         assert len(coeffs[1]) == 0 and len(coeffs[2]) == 1
     with pytest.raises(AssertionError, match=r"p_deg \(1023\) <= d \(511\)"):
         pcdl.trace_commit_batch(ev, 511, cname)
+
+
+@pytest.mark.parametrize("cname,cid", CURVES)
+def test_srs_load_bincode(hal, golden, corc, cname, cid):
+    """SURVEY f3 (pp.rs:26-61): the reference's own gs-00.bin bytes (length prefix + first 64
+    records, verbatim) and sh.bin decode on the device to the golden points / (S, H); general
+    varints take the host path and an off-curve point is rejected like wrappers.rs:606."""
+    c = P.CURVES[cname]
+    head = golden[f"ref_gs_{cname}_b00_head_bytes"].tobytes()
+    sh = golden[f"ref_sh_{cname}_bytes"].tobytes()
+    group.PublicParams.load_bincode(cname, [head], sh, n=64, precompute_windows=False)
+    assert np.array_equal(group.PublicParams.read(cname, 0, 64), golden[f"ref_srs_{cname}_b00_first64"])
+    # (S, H) installed: the hiding term of pcdl::commit uses S (compare with the upload path)
+    w = rand_sc(1, 3)
+    coeffs = rand_sc(64, 4)
+    got = pcdl.commit(coeffs, 63, w, cname)
+    S, Hh = golden[f"ref_sh_{cname}"]
+    group.PublicParams.upload(cname, golden[f"ref_srs_{cname}_b00_first64"], S, Hh, precompute_windows=False)
+    assert np.array_equal(got, pcdl.commit(coeffs, 63, w, cname))
+    # two blocks re-encoded by a bincode varint encoder (32 + 32 points)
+
+    def enc_varint(v):
+        if v < 251:
+            return bytes([v])
+        for tag, width in ((251, 2), (252, 4), (253, 8)):
+            if v < 1 << (8 * width):
+                return bytes([tag]) + v.to_bytes(width, "little")
+        raise ValueError
+
+    pts = golden[f"ref_srs_{cname}_b00_first64"]
+
+    def block(points):
+        return enc_varint(len(points)) + b"".join(enc_varint(int(l)) for p in points for l in p)
+    group.PublicParams.load_bincode(cname, [block(pts[:32]), block(pts[32:])], sh, n=64,
+                                    precompute_windows=False)
+    assert np.array_equal(group.PublicParams.read(cname, 0, 64), pts)
+    bad = pts[:4].copy()
+    bad[2] = [1, 0, 0, 0, 2, 0, 0, 0]  # small limbs (1-byte varints), not on the curve
+    with pytest.raises(Exception, match="is_on_curve"):
+        group.PublicParams.load_bincode(cname, [block(bad)], sh, n=4, precompute_windows=False)
+    with pytest.raises(Exception, match="is_power_of_two"):
+        group.PublicParams.load_bincode(cname, [head], sh, n=48, precompute_windows=False)
+    with pytest.raises(Exception, match="n <= N"):
+        group.PublicParams.load_bincode(cname, [block(pts[:16])], sh, n=32, precompute_windows=False)
