@@ -34,6 +34,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 MSM_BYTES_PER_POINT = 96
 NTT_BYTES_PER_ELEM = 64  # read + write 32 B per transform
+MODMUL_PEAK = 1.77e11  # 255-bit Montgomery multiplications/s, 1 MI355X, 8 waves/SIMD (fe_mul_bench)
 
 
 def parse():
@@ -336,6 +337,9 @@ def main():
     if not args.no_cpu and world == 1:
         cpu = cpu_baseline(L, H, curve, n, scalars0, out_check=True, budget_s=args.cpu_seconds)
 
+    madds = n * (-(-255 // window_bits)) if window_bits else 0  # one mixed addition per nonzero digit
+    valu_achieved = madds * 10 / (acc_avg_ms * 1e-3) if acc_avg_ms > 0 else 0.0
+
     line = {
         "metric": "MSM points/sec (Pippenger, Pallas, 2^20 points, resident SRS)",
         "value": value,
@@ -369,6 +373,16 @@ def main():
             "note": "the MSM is bound by 255-bit modular multiplication on the VALU, not HBM (SURVEY §7 hard part 1)",
         },
         "cpu_baseline": cpu,
+        "compute_roofline": {
+            "bound": "valu",
+            "kernel": "k_acc",
+            "unit": "modmul/s",
+            "achieved": valu_achieved,
+            "peak": MODMUL_PEAK,
+            "frac": valu_achieved / MODMUL_PEAK,
+            "note": "XYZZ mixed additions (8M + 2S, counted as 10 modmul) per launch / mean launch time, against the "
+                    "measured single-chain Montgomery multiplication rate of one MI355X (tools/micro/fe_mul_bench.hip)",
+        },
         "extra": {
             "msm_single_latency_ms": min(lat) if lat else None,
             "pipelined_equals_sync": sync_ok,
