@@ -276,6 +276,17 @@ def main():
         }
         sizes[f"ntt_2^{lg}"] = measure_ntt(lg, nrep=4)
         torch.cuda.empty_cache()
+        if world > 1 and (world & (world - 1)) == 0:
+            # BASELINE configs[4]: one 2^lg-point MSM partitioned across the ranks (strong scaling)
+            lr = lg - (world.bit_length() - 1)
+            e, a_ms, ok, lt, _ = measure_msm(lr, 4, 2, check_sync=False)
+            sizes[f"msm_2^{lg}_partitioned"] = {
+                "points_per_s": (1 << lg) * 4 / e,
+                "ms_per_msm": e * 1e3 / 4,
+                "points_per_rank": 1 << lr,
+                "scaling": "strong",
+            }
+            torch.cuda.empty_cache()
 
     # ---- distributed single NTT (four-step, RCCL all-to-all; halo_amd.dist.sharded_ntt), N > 1 only
     dist_ntt = None
