@@ -22,9 +22,11 @@
 
 namespace halo {
 
-constexpr int NTT_E = 1024;  // elements per workgroup (LDS-resident R-point DFTs)
+constexpr int NTT_E = 1024;        // elements per workgroup for passes with R <= 256
+constexpr int NTT_E_BIG = 2048;    // ... and for the two-pass split of 2^17..2^22 (R up to 2048)
+constexpr int NTT_EPT = 4;         // elements per thread (radix-4 register groups)
 constexpr int NTT_MAX_LOG_R_MULTI = 8;
-constexpr int NTT_TW_MAX = 256;  // stage-twiddle table entries (stages 0..7)
+constexpr int NTT_TW_MAX = 2048;  // stage-twiddle table entries (stages 0..10), read through L1/L2
 constexpr unsigned NTT_FULL_TABLE_MAX_LOG = 24;  // per-pass twiddle tables up to 2^24
 
 struct NttPassArgs {
@@ -44,30 +46,35 @@ struct NttPassArgs {
     size_t stride;              // elements between consecutive transforms of a batch
 };
 
-// LDS layout: limb-major (SoA), limb l of position p at smem[l * NTT_E + swz(p)].  swz XORs the
-// bank bits with a linear function of p >> 5, chosen (by exhaustive check over every access pattern
-// of the load, group and store phases for r = 1..8) so that every ds_read_b32 / ds_write_b32 is
-// conflict-free.
-template <int EPT>
+// LDS layout: limb-major (SoA), limb l of position p at smem[l * NE + swz(p)].  swz XORs the bank
+// bits with a linear function of p >> 5, chosen (by exhaustive check over every access pattern of
+// the load, group and store phases, tools: see DESIGN.md) so that every ds_read_b32 / ds_write_b32
+// is conflict-free: for NE = 1024 over r = 1..8, for NE = 2048 over r = 9..11.  (A 4096-element
+// variant for 2 x 12-bit passes at 2^24 was measured 47 % slower than 3 x 8 bits: one 1024-thread
+// block per CU and 32-byte strided column loads; not kept.)
+template <int NE>
 struct NttSwz;
 template <>
-struct NttSwz<8> {
-    static constexpr uint32_t C[5] = {25, 18, 15, 10, 30};
-};
-template <>
-struct NttSwz<4> {
+struct NttSwz<1024> {
+    static constexpr int NB = 5;
     static constexpr uint32_t C[5] = {31, 22, 5, 27, 10};
 };
-template <int EPT>
+template <>
+struct NttSwz<2048> {
+    static constexpr int NB = 6;
+    static constexpr uint32_t C[6] = {10, 29, 31, 20, 30, 17};
+};
+
+template <int NE>
 HALO_DEV uint32_t ntt_swz_hi(uint32_t hi) {  // linear map of (p >> 5) onto the bank bits
     uint32_t m = 0;
 #pragma unroll
-    for (int b = 0; b < 5; b++) m ^= ((hi >> b) & 1u) ? NttSwz<EPT>::C[b] : 0u;
+    for (int b = 0; b < NttSwz<NE>::NB; b++) m ^= ((hi >> b) & 1u) ? NttSwz<NE>::C[b] : 0u;
     return m;
 }
-template <int EPT>
+template <int NE>
 HALO_DEV uint32_t ntt_swz(uint32_t p) {
-    return p ^ ntt_swz_hi<EPT>(p >> 5);
+    return p ^ ntt_swz_hi<NE>(p >> 5);
 }
 
 template <class F>
@@ -106,14 +113,8 @@ HALO_DEV Fe<C> fe_reduce_q(const Fe<C>& x) {
 // (< 2p except raw ark words), stage 0 doubles that bound, every later stage adds at most 2p
 // (u + t and u - t + 2p with t = v w < 2p), so after 8 stages they are < 22p: still valid
 // Montgomery inputs (< 64p), reduced once at the end of the pass (fe_reduce_q, < 32p).
-template <class F, bool TWG>
-HALO_DEV Fe<F> ntt_stage_tw(const uint32_t* twl, const uint4* twg, uint32_t idx) {
-    if (TWG) return fe_load<F>(twg + 2 * idx);
-    return lds_get_soa<F>(twl, idx, NTT_TW_MAX);
-}
-
-template <class F, int EPT, int LG, bool TWG>
-HALO_DEV void ntt_group(Fe<F> (&v)[EPT], uint32_t s, uint32_t G, uint32_t k0, const uint32_t* twl, const uint4* twg) {
+template <class F, int EPT, int LG>
+HALO_DEV void ntt_group(Fe<F> (&v)[EPT], uint32_t s, uint32_t G, uint32_t k0, const uint4* twg) {
 #pragma unroll
     for (int g = 0; g < LG; g++) {
         if ((uint32_t)g >= G) break;
@@ -125,7 +126,7 @@ HALO_DEV void ntt_group(Fe<F> (&v)[EPT], uint32_t s, uint32_t G, uint32_t k0, co
             Fe<F> t = v[m2];
             if (sp != 0) {
                 const uint32_t k = k0 + ((uint32_t)(m & ((1 << g) - 1)) << s);
-                t = fe_mul(t, ntt_stage_tw<F, TWG>(twl, twg, (1u << sp) - 1u + k));
+                t = fe_mul(t, fe_load<F>(twg + 2 * ((1u << sp) - 1u + k)));
             }
             // stage 0 (no multiplication): t is a pass input, < 4p even for non-canonical ark words
             v[m2] = (sp == 0) ? fe_sub_k<4>(v[m], t) : fe_sub_k<2>(v[m], t);
@@ -138,28 +139,28 @@ HALO_DEV void ntt_group(Fe<F> (&v)[EPT], uint32_t s, uint32_t G, uint32_t k0, co
 // owns T = NTT_E / R consecutive columns.  Each thread holds EPT elements in registers; the first
 // LG stages are done straight from the global loads, the rest in groups of LG stages through LDS,
 // and a final coalesced store phase writes y[(j / Ns) Ns R + (j mod Ns) + k Ns].
-template <class F, int EPT, bool TWG>
-__global__ __launch_bounds__(NTT_E / EPT) void k_ntt_pass(NttPassArgs a) {
-    constexpr int LG = (EPT == 8) ? 3 : 2;
-    constexpr uint32_t TH = NTT_E / EPT;
+template <class F, int NE>
+__global__ __launch_bounds__(NE / NTT_EPT) void k_ntt_pass(NttPassArgs a) {
+    constexpr int EPT = NTT_EPT;
+    constexpr int LG = 2;
+    constexpr uint32_t TH = NE / EPT;
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t* data = smem;
-    uint32_t* twl = smem + NTT_E * NLIMB;
     const uint32_t r = a.log_r;
     const uint32_t R = 1u << r;
     const size_t N = (size_t)1 << a.logn;
     const size_t NJ = N >> r;
-    const uint32_t T = (uint32_t)((NJ < (size_t)(NTT_E >> r)) ? NJ : (NTT_E >> r));
+    const uint32_t T = (uint32_t)((NJ < (size_t)(NE >> r)) ? NJ : (NE >> r));
     const uint32_t EB = T * R;  // elements in this block
     const size_t Ns = (size_t)1 << a.log_ns;
-    const size_t j0 = (size_t)blockIdx.x * T;
+    // XCD-aware order for the wide passes (few columns per block): blocks b, b + 8, ... run on one
+    // XCD, so give them consecutive column groups -- neighbouring columns share 128-B lines in L2
+    uint32_t bx = blockIdx.x;
+    if (NE >= NTT_E_BIG && (gridDim.x & 7) == 0) bx = (bx & 7) * (gridDim.x >> 3) + (bx >> 3);
+    const size_t j0 = (size_t)bx * T;
     const uint4* in = a.in + (size_t)blockIdx.y * a.stride * 2;
     uint4* out = a.out + (size_t)blockIdx.y * a.stride * 2;
     const uint32_t tau = threadIdx.x;
-
-    // stage twiddles (entries < R - 1) into LDS
-    if (!TWG)
-        for (uint32_t x = tau; x + 1 < R; x += TH) lds_put_soa(twl, x, NTT_TW_MAX, fe_load<F>(a.stage_tw + 2 * x));
 
     // ---- load + pre-twiddle + first LG stages (positions base + m)
     uint32_t base;
@@ -199,14 +200,14 @@ __global__ __launch_bounds__(NTT_E / EPT) void k_ntt_pass(NttPassArgs a) {
             v[m] = fe_zero<F>();
         }
     }
-    __syncthreads();  // stage twiddles visible
-    const uint32_t G0 = r < (uint32_t)LG ? r : (uint32_t)LG;
-    ntt_group<F, EPT, LG, TWG>(v, 0, G0, 0, twl, a.stage_tw);
+    // odd r on the wide blocks: the single-stage group goes first, so later groups stay in range
+    const uint32_t G0 = (NE >= NTT_E_BIG && (r & 1)) ? 1u : (r < (uint32_t)LG ? r : (uint32_t)LG);
+    ntt_group<F, EPT, LG>(v, 0, G0, 0, a.stage_tw);
     {
-        const uint32_t pb = ntt_swz<EPT>(base);
+        const uint32_t pb = ntt_swz<NE>(base);
 #pragma unroll
         for (int m = 0; m < EPT; m++)
-            if (base + m < EB) lds_put_soa(data, pb ^ (uint32_t)m, NTT_E, v[m]);
+            if (base + m < EB) lds_put_soa(data, pb ^ (uint32_t)m, NE, v[m]);
     }
     __syncthreads();
 
@@ -215,19 +216,19 @@ __global__ __launch_bounds__(NTT_E / EPT) void k_ntt_pass(NttPassArgs a) {
         const uint32_t G = (r - s) < (uint32_t)LG ? (r - s) : (uint32_t)LG;
         const uint32_t h = 1u << s;
         const uint32_t gb = (tau & (h - 1)) | ((tau >> s) << (s + LG));
-        const uint32_t shb = ntt_swz_hi<EPT>(gb >> 5);
+        const uint32_t shb = ntt_swz_hi<NE>(gb >> 5);
 #pragma unroll
         for (int m = 0; m < EPT; m++) {
             const uint32_t pos = gb + (uint32_t)m * h;
-            const uint32_t ph = (pos ^ shb) ^ ntt_swz_hi<EPT>(((uint32_t)m * h) >> 5);
-            if (pos < EB) v[m] = lds_get_soa<F>(data, ph, NTT_E);
+            const uint32_t ph = (pos ^ shb) ^ ntt_swz_hi<NE>(((uint32_t)m * h) >> 5);
+            if (pos < EB) v[m] = lds_get_soa<F>(data, ph, NE);
         }
-        ntt_group<F, EPT, LG, TWG>(v, s, G, tau & (h - 1), twl, a.stage_tw);
+        ntt_group<F, EPT, LG>(v, s, G, tau & (h - 1), a.stage_tw);
 #pragma unroll
         for (int m = 0; m < EPT; m++) {
             const uint32_t pos = gb + (uint32_t)m * h;
-            const uint32_t ph = (pos ^ shb) ^ ntt_swz_hi<EPT>(((uint32_t)m * h) >> 5);
-            if (pos < EB) lds_put_soa(data, ph, NTT_E, v[m]);
+            const uint32_t ph = (pos ^ shb) ^ ntt_swz_hi<NE>(((uint32_t)m * h) >> 5);
+            if (pos < EB) lds_put_soa(data, ph, NE, v[m]);
         }
         __syncthreads();
     }
@@ -250,7 +251,7 @@ __global__ __launch_bounds__(NTT_E / EPT) void k_ntt_pass(NttPassArgs a) {
         }
         const size_t j = j0 + t;
         const size_t dst = ((j >> a.log_ns) << (a.log_ns + r)) + (j & (Ns - 1)) + (size_t)k * Ns;
-        Fe<F> x = lds_get_soa<F>(data, ntt_swz<EPT>(t * R + k), NTT_E);
+        Fe<F> x = lds_get_soa<F>(data, ntt_swz<NE>(t * R + k), NE);
         if (a.out_ark) {
             fe_store(out + 2 * dst, fe_canon(fe_mul(x, oc)));
         } else {
@@ -374,26 +375,22 @@ static int launch_pow_table(uint4* out, size_t count, const Fe<F>& base, uint64_
     return HALO_OK;
 }
 
-// k_ntt_pass variant: bit 1 = 8 elements per thread (radix-8 register groups; else radix-4),
-// bit 0 = stage twiddles read from global (L1/L2) instead of staged in LDS.  HALO_NTT_CFG overrides
-// the default (kept for measurement).
-static int ntt_cfg() {
-    static const int v = [] {
-        const char* e = getenv("HALO_NTT_CFG");
-        return e ? (atoi(e) & 3) : 1;
-    }();
-    return v;
-}
-
+// Pass split: N <= 2^8 in one pass; 2^17..2^22 in two passes of up to 11 bits on 2048-element
+// blocks (one fewer pass than the 8-bit split: one pre-twiddle multiplication and one HBM round
+// trip per element saved; measured A/B on one box: 2^20 pair 0.28 -> 0.25 ms, 2^22 equal at
+// 1.03 ms, where the single-column 11-bit pass loses on its strided 32-B loads what it saves in
+// work); everything else in passes of <= 8 bits on 1024-element blocks.
+constexpr unsigned NTT_MAX_LOG_R_BIG = 11;
 static std::vector<unsigned> ntt_radices(unsigned logn) {
     std::vector<unsigned> r;
-    const unsigned loge = 10;  // log2(NTT_E)
-    if (logn <= NTT_MAX_LOG_R_MULTI || logn <= loge) {
-        // one pass (R = N <= NTT_E): r > 8 would overflow the stage-twiddle table
-        if (logn <= NTT_MAX_LOG_R_MULTI) {
-            r.push_back(logn);
-            return r;
-        }
+    if (logn <= NTT_MAX_LOG_R_MULTI) {
+        r.push_back(logn);
+        return r;
+    }
+    if (logn >= 17 && logn <= 2 * NTT_MAX_LOG_R_BIG) {
+        r.push_back((logn + 1) / 2);
+        r.push_back(logn / 2);
+        return r;
     }
     const unsigned passes = (logn + NTT_MAX_LOG_R_MULTI - 1) / NTT_MAX_LOG_R_MULTI;
     unsigned left = logn;
@@ -426,7 +423,7 @@ static int get_twiddles(DeviceState* st, int field, unsigned logn, int inverse, 
     HALO_CHECK(launch_pow_table<F>(t->hi.as<uint4>(), nhi, w, (uint64_t)nlo, s));
     // stage twiddles omega_{2^(s+1)}^k (the same for every N; kept per table for simplicity)
     HALO_CHECK(t->stage.reserve(NTT_TW_MAX * 32));
-    for (unsigned sg = 0; sg < 8; sg++) {
+    for (unsigned sg = 0; sg < NTT_MAX_LOG_R_BIG; sg++) {
         const Fe<F> ws = host_fe<F>(inverse ? F::OMEGA_INV[sg + 1] : F::OMEGA[sg + 1]);
         HALO_CHECK(launch_pow_table<F>(t->stage.as<uint4>() + 2 * (((size_t)1 << sg) - 1), (size_t)1 << sg, ws, 1, s));
     }
@@ -497,18 +494,15 @@ static int ntt_device(DeviceState* st, int field, const void* d_in, void* d_out,
         for (int l = 0; l < NLIMB; l++) a.out_const[l] = inverse ? F::NINV_ARK[logn][l] : F::ONE[l];
         a.stride = N;
         const size_t NJ = N >> lr;
-        const size_t T = std::min(NJ, (size_t)(NTT_E >> lr));
-        const int cfg = ntt_cfg();
-        const bool twg = cfg & 1;
-        const size_t lds = (size_t)(NTT_E + (twg ? 0 : NTT_TW_MAX)) * NLIMB * 4;
+        const size_t NE = lr > NTT_MAX_LOG_R_MULTI ? NTT_E_BIG : NTT_E;
+        const size_t T = std::min(NJ, NE >> lr);
+        const size_t lds = NE * NLIMB * 4;
         dim3 grid((unsigned)(NJ / T), (unsigned)batch);
         ProfScope prof("ntt_pass", s);
-        switch (cfg) {
-            case 0: HALO_LAUNCH(prof, (k_ntt_pass<F, 4, false>), grid, dim3(NTT_E / 4), lds, s, a); break;
-            case 1: HALO_LAUNCH(prof, (k_ntt_pass<F, 4, true>), grid, dim3(NTT_E / 4), lds, s, a); break;
-            case 2: HALO_LAUNCH(prof, (k_ntt_pass<F, 8, false>), grid, dim3(NTT_E / 8), lds, s, a); break;
-            default: HALO_LAUNCH(prof, (k_ntt_pass<F, 8, true>), grid, dim3(NTT_E / 8), lds, s, a); break;
-        }
+        if (NE == NTT_E_BIG)
+            HALO_LAUNCH(prof, (k_ntt_pass<F, NTT_E_BIG>), grid, dim3(NTT_E_BIG / NTT_EPT), lds, s, a);
+        else
+            HALO_LAUNCH(prof, (k_ntt_pass<F, NTT_E>), grid, dim3(NTT_E / NTT_EPT), lds, s, a);
         HALO_HIP(hipGetLastError());
         log_ns += lr;
     }
