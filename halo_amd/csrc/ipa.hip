@@ -461,18 +461,21 @@ extern "C" int halo_poly_mul(halo_field_t field, const halo_fe_t* a, size_t la, 
 }
 
 // ------------------------------------------------------------------------------------------ IPA
-extern "C" int halo_ipa_begin(halo_curve_t curve, const halo_fe_t* cs, size_t n, const halo_fe_t* z,
-                              const halo_wrapped_point_t* H_prime, halo_ipa_session** out) {
-    clear_error();
+// Session start shared by halo_ipa_begin (G = resident SRS prefix, z powers generated on the
+// device) and halo_ipa_begin_vectors (explicit G, c, z: a shard of a distributed opening or its
+// final collapsed rounds, halo_amd/dist.py).
+static int ipa_begin(halo_curve_t curve, size_t n, const halo_wrapped_point_t* gs_host, const halo_fe_t* cs,
+                     const halo_fe_t* zs_host, const halo_fe_t* z, const halo_wrapped_point_t* H_prime,
+                     halo_ipa_session** out) {
     if (curve != HALO_PALLAS && curve != HALO_VESTA) return set_error(HALO_EINVAL, "unknown curve");
-    if (!cs || !z || !H_prime || !out) return set_error(HALO_EINVAL, "halo_ipa_begin: null argument");
+    if (!cs || !(z || zs_host) || !H_prime || !out) return set_error(HALO_EINVAL, "halo_ipa_begin: null argument");
     if (n <= 1) return set_error(HALO_EINVAL, "assertion failed: n > 1");
     if (!is_pow2(n)) return set_error(HALO_ENOTPOW2, "n (%zu) is not a power of two", n);
     DeviceState* st = current_state();
     if (!st) return HALO_EDEVICE;
     std::lock_guard<std::mutex> g(st->mu);
     SrsState& srs = st->srs[curve];
-    if (n > srs.n) return set_error(HALO_ESRSRANGE, "d (%zu) <= D (%zu)", n - 1, srs.n ? srs.n - 1 : 0);
+    if (!gs_host && n > srs.n) return set_error(HALO_ESRSRANGE, "d (%zu) <= D (%zu)", n - 1, srs.n ? srs.n - 1 : 0);
     auto* ses = new halo_ipa_session();
     ses->curve = curve;
     ses->n = n;
@@ -486,25 +489,35 @@ extern "C" int halo_ipa_begin(halo_curve_t curve, const halo_fe_t* cs, size_t n,
         if ((rc = ses->zs.reserve(n * 32))) break;
         if ((rc = ses->htab.reserve(256 * 64))) break;
         if ((rc = ses->small.reserve(512))) break;
-        if ((rc = ses->tmp.reserve(4096 * 32))) break;
-        if (hipMemcpyAsync(ses->gs.ptr, srs.gs.ptr, n * 64, hipMemcpyDeviceToDevice, s) != hipSuccess) {
+        if ((rc = ses->tmp.reserve(std::max<size_t>(4096 * 32, gs_host ? n * 64 : 0)))) break;
+        if (gs_host) {
+            if ((rc = copy_h2d(ses->tmp.ptr, gs_host, n * 64, s))) break;
+            if ((rc = convert_wrapped_to_internal(curve, ses->tmp.ptr, ses->gs.ptr, n, s))) break;
+        } else if (hipMemcpyAsync(ses->gs.ptr, srs.gs.ptr, n * 64, hipMemcpyDeviceToDevice, s) != hipSuccess) {
             rc = set_error(HALO_EDEVICE, "copy of the SRS prefix failed");
             break;
         }
         if ((rc = copy_h2d(ses->cs.ptr, cs, n * 32, s))) break;
         char* sm = (char*)ses->small.ptr;
-        if ((rc = copy_h2d(sm, z, 32, s))) break;
+        if (zs_host) {
+            if ((rc = copy_h2d(ses->zs.ptr, zs_host, n * 32, s))) break;
+        } else {
+            if ((rc = copy_h2d(sm, z, 32, s))) break;
+        }
         if ((rc = copy_h2d(sm + 64, H_prime, 64, s))) break;
         const size_t run = 16;
         DISPATCH_CURVE(curve, Cv, {
-            hipLaunchKernelGGL(k_powers<typename Cv::Scalar>, dim3(gridn((n + run - 1) / run, 128)), dim3(128), 0, s,
-                               (const uint4*)sm, n, run, ses->zs.as<uint4>());
+            if (!zs_host)
+                hipLaunchKernelGGL(k_powers<typename Cv::Scalar>, dim3(gridn((n + run - 1) / run, 128)), dim3(128), 0,
+                                   s, (const uint4*)sm, n, run, ses->zs.as<uint4>());
             hipLaunchKernelGGL(k_pow2_xyzz_from_wrapped<Cv>, dim3(1), dim3(64), 0, s, (const uint4*)(sm + 64),
                                ses->tmp.as<uint4>(), 256);
             hipLaunchKernelGGL(k_xyzz_to_aff_ipa<Cv>, dim3(4), dim3(64), 0, s, (const uint4*)ses->tmp.ptr,
                                ses->htab.as<uint4>(), 256);
         });
         if (hipGetLastError() != hipSuccess) rc = set_error(HALO_EDEVICE, "ipa begin launch failed");
+        if (!rc && gs_host && hipStreamSynchronize(s) != hipSuccess)  // tmp held the staged bases
+            rc = set_error(HALO_EDEVICE, "ipa begin: synchronisation failed");
     } while (0);
     if (rc) {
         delete ses;
@@ -512,6 +525,20 @@ extern "C" int halo_ipa_begin(halo_curve_t curve, const halo_fe_t* cs, size_t n,
     }
     *out = ses;
     return HALO_OK;
+}
+
+extern "C" int halo_ipa_begin(halo_curve_t curve, const halo_fe_t* cs, size_t n, const halo_fe_t* z,
+                              const halo_wrapped_point_t* H_prime, halo_ipa_session** out) {
+    clear_error();
+    return ipa_begin(curve, n, nullptr, cs, nullptr, z, H_prime, out);
+}
+
+extern "C" int halo_ipa_begin_vectors(halo_curve_t curve, const halo_wrapped_point_t* gs, const halo_fe_t* cs,
+                                      const halo_fe_t* zs, size_t n, const halo_wrapped_point_t* H_prime,
+                                      halo_ipa_session** out) {
+    clear_error();
+    if (!gs || !zs) return set_error(HALO_EINVAL, "halo_ipa_begin_vectors: null argument");
+    return ipa_begin(curve, n, gs, cs, zs, nullptr, H_prime, out);
 }
 
 extern "C" int halo_ipa_round_lr(halo_ipa_session* ses, halo_wrapped_point_t* L, halo_wrapped_point_t* R) {

@@ -186,3 +186,176 @@ def torch_alltoall(dist):
         dist.all_to_all_single(recv, send)
         return recv
     return f
+
+
+# ---------------------------------------------------------------------------------------------
+# Distributed polynomial evaluation (SURVEY §8e "Poly eval"): rank r holds the coefficient block
+# [lo_r, hi_r) (shard_range) and evaluates it at z; p(z) = sum_r z^lo_r v_r.  With equal blocks
+# lo_r = r * per, so the combine is the evaluation of the polynomial (v_0 .. v_{P-1}) at z^per:
+# one all-gather of 32 B per rank and two tiny device calls (x^e, Horner), no host field math.
+# ---------------------------------------------------------------------------------------------
+class PolyOps:
+    """Device primitives of the distributed evaluation: Horner of k polynomials at one point and
+    z^e."""
+
+    def __init__(self, field="fp"):
+        self.field = field
+
+    def eval_batch(self, polys, z):
+        from .poly import evaluate_batch
+
+        return evaluate_batch(polys, z, self.field)
+
+    def pow(self, z, e: int):
+        from . import _lib as H
+        from .group import _field
+
+        zz = H.fe_array(z, 1)
+        w = np.zeros((1, 4), dtype=np.uint64)
+        H.check(H.load().halo_evals_op(_field(self.field), 6, H.ptr(zz), None, None, e, H.ptr(w), 1))
+        return w[0]
+
+
+def poly_eval_partial(coeffs_local, z, ops: PolyOps) -> np.ndarray:
+    """v_r = sum_i coeffs_local[i] z^i (this rank's block, unshifted)."""
+    if len(coeffs_local) == 0:
+        return np.zeros(4, dtype=np.uint64)
+    return np.asarray(ops.eval_batch([coeffs_local], z)[0], dtype=np.uint64)
+
+
+def poly_eval_combine(parts, n_total: int, z, ops: PolyOps) -> np.ndarray:
+    """p(z) = sum_r (z^per)^r v_r for the equal blocks of shard_range."""
+    world = len(parts)
+    if world == 1:
+        return np.asarray(parts[0], dtype=np.uint64)
+    per = (n_total + world - 1) // world
+    return np.asarray(ops.eval_batch([np.stack(parts)], ops.pow(z, per))[0], dtype=np.uint64)
+
+
+def sharded_poly_eval(coeffs_local, n_total: int, z, dist, ops: PolyOps | None = None) -> np.ndarray:
+    """DensePolynomial::evaluate (pcdl.rs:49,471) of a polynomial whose coefficients are split into
+    contiguous blocks over the ranks (rank r holds coeffs[shard_range(n_total, r, P)])."""
+    ops = ops or PolyOps()
+    rank, world = dist.get_rank(), dist.get_world_size()
+    lo, hi = shard_range(n_total, rank, world)
+    if len(coeffs_local) != hi - lo:
+        raise ValueError("coefficient block does not match shard_range")
+    parts = [None] * world
+    dist.all_gather_object(parts, poly_eval_partial(coeffs_local, z, ops))
+    return poly_eval_combine(parts, n_total, z, ops)
+
+
+# ---------------------------------------------------------------------------------------------
+# Distributed IPA opening (SURVEY §8e "IPA fold ... shards by j"): the round loop of
+# open_without_eval (pcdl.rs:404-438) over P ranks.  Rank r holds the strided shard
+# G[i P + r], c[i P + r], z[i P + r] (i < n / P).  While the half-length m is a multiple of P the
+# fold pairs j and j + m lie on the same rank (local i and i + m / P), so every fold is local and
+# the local session is the single-GPU one.  L and R are linear in the shards: L = sum_r L_r with
+# each L_r carrying its own <c_r, z_l>_r H' term, so a round all-gathers two points per rank and
+# sums them on the device, and every rank runs the same transcript.  After lg(n / P) rounds each
+# rank holds one element; the P elements are all-gathered (global order j = r) and the last lg P
+# rounds run on one session, replicated on every rank (all ranks return the same proof).
+# ---------------------------------------------------------------------------------------------
+def ipa_shard(vec, rank: int, world: int):
+    """Rank r's strided shard vec[r::P] of an IPA vector."""
+    return np.ascontiguousarray(np.asarray(vec)[rank::world])
+
+
+class IpaOps:
+    """Per-rank session primitives the distributed opening is written against."""
+
+    def begin(self, gs, cs, zs, H_prime):
+        raise NotImplementedError
+
+    def round_lr(self, ses):  # -> (L, R) WrappedPoints of this shard (H' terms included)
+        raise NotImplementedError
+
+    def fold(self, ses, xi, xi_inv):
+        raise NotImplementedError
+
+    def final(self, ses):  # -> (g (1, 8), c (1, 4), z (1, 4)) once fully folded
+        raise NotImplementedError
+
+    def point_sum(self, pts):  # (k, 8) WrappedPoints -> (8,)
+        raise NotImplementedError
+
+
+class GpuIpaOps(IpaOps):
+    def __init__(self, curve="pallas"):
+        self.curve = curve
+
+    def begin(self, gs, cs, zs, H_prime):
+        from .pcdl import IpaSession
+
+        return IpaSession.from_vectors(gs, cs, zs, H_prime, self.curve)
+
+    def round_lr(self, ses):
+        return ses.round_lr()
+
+    def fold(self, ses, xi, xi_inv):
+        ses.fold(xi, xi_inv)
+
+    def final(self, ses):
+        _, gs, cs, zs = ses.state()
+        ses.end()
+        return gs[:1], cs[:1], zs[:1]
+
+    def point_sum(self, pts):
+        from .group import point_sum
+
+        return point_sum(pts, self.curve)
+
+
+def _ipa_loop(sessions, ops: IpaOps, gather, challenge, inverse, xi, Ls, Rs, rounds: int):
+    for _ in range(rounds):
+        parts = gather([ops.round_lr(s) for s in sessions])
+        L = ops.point_sum(np.stack([p[0] for p in parts]))
+        R = ops.point_sum(np.stack([p[1] for p in parts]))
+        Ls.append(L)
+        Rs.append(R)
+        xi = challenge(xi, L, R)
+        xinv = inverse(xi)
+        for s in sessions:
+            ops.fold(s, xi, xinv)
+    return xi
+
+
+def sharded_ipa_rounds(local_shards, H_prime, challenge: Callable, inverse: Callable, ops: IpaOps, world: int,
+                       gather: Callable):
+    """Distributed pcdl round loop.  ``local_shards``: the (gs, cs, zs) strided shards (ipa_shard)
+    this process holds -- one with a real communicator, all P with virtual ranks; ``gather(objs)``
+    returns the list of every rank's objs in rank order (torch_gather_objects(dist), or identity for
+    virtual ranks).  Returns (Ls, Rs, U, c) exactly as the single-session ipa_rounds does."""
+    if world < 1 or world & (world - 1):
+        raise ValueError("world size must be a power of two")
+    n_loc = len(local_shards[0][1])
+    if n_loc < 1 or n_loc & (n_loc - 1):
+        raise ValueError("n / P must be a power of two")
+    Ls, Rs = [], []
+    xi = None
+    if n_loc >= 2:
+        sessions = [ops.begin(g, c, z, H_prime) for g, c, z in local_shards]
+        xi = _ipa_loop(sessions, ops, gather, challenge, inverse, xi, Ls, Rs, n_loc.bit_length() - 1)
+        finals = gather([ops.final(s) for s in sessions])
+    else:
+        finals = gather([(np.asarray(g).reshape(-1, 8)[:1], np.asarray(c).reshape(-1, 4)[:1],
+                          np.asarray(z).reshape(-1, 4)[:1]) for g, c, z in local_shards])
+    G = np.concatenate([f[0] for f in finals])
+    C = np.concatenate([f[1] for f in finals])
+    Z = np.concatenate([f[2] for f in finals])
+    if world > 1:
+        ses = ops.begin(G, C, Z, H_prime)
+        _ipa_loop([ses], ops, lambda objs: objs, challenge, inverse, xi, Ls, Rs, world.bit_length() - 1)
+        G, C, _ = ops.final(ses)
+    return Ls, Rs, np.asarray(G[0], dtype=np.uint64), np.asarray(C[0], dtype=np.uint64)
+
+
+def torch_gather_objects(dist):
+    """gather() for sharded_ipa_rounds over a torch.distributed group (gloo or RCCL)."""
+
+    def f(objs):
+        out = [None] * dist.get_world_size()
+        dist.all_gather_object(out, list(objs))
+        return [o for part in out for o in part]
+
+    return f

@@ -40,6 +40,26 @@ class IpaSession:
         H.check(H.load().halo_ipa_begin(self.curve, H.ptr(cs), self.n, H.ptr(zz), H.ptr(hp), ctypes.byref(s)))
         self._s = s
 
+    @classmethod
+    def from_vectors(cls, gs, cs, zs, H_prime, curve="pallas") -> "IpaSession":
+        """Session over explicit (G, c, z) of length n (a shard of a distributed opening,
+        halo_amd.dist.sharded_ipa_rounds)."""
+        H.ensure_device()
+        self = cls.__new__(cls)
+        self.curve = _curve(curve)
+        g = H.point_array(gs)
+        c = H.fe_array(cs)
+        z = H.fe_array(zs)
+        if not (len(g) == len(c) == len(z)):
+            raise ValueError("G, c and z must have the same length")
+        self.n = len(c)
+        hp = H.point_array(H_prime)
+        s = ctypes.c_void_p()
+        H.check(H.load().halo_ipa_begin_vectors(self.curve, H.ptr(g), H.ptr(c), H.ptr(z), self.n, H.ptr(hp),
+                                                ctypes.byref(s)))
+        self._s = s
+        return self
+
     def round_lr(self):
         L = np.zeros(8, dtype=np.uint64)
         R = np.zeros(8, dtype=np.uint64)

@@ -221,6 +221,12 @@ int halo_construct_powers(halo_field_t field, const halo_fe_t* z, size_t n, halo
 typedef struct halo_ipa_session halo_ipa_session;
 int halo_ipa_begin(halo_curve_t curve, const halo_fe_t* cs, size_t n, const halo_fe_t* z,
                    const halo_wrapped_point_t* H_prime, halo_ipa_session** out);
+/* Session over explicit vectors G (WrappedPoints), c, z of length n (power of two >= 2) instead of
+ * the SRS prefix and the powers of z: one rank's shard of a distributed opening (the
+ * strided split G[i P + r] keeps every fold pair on one rank) and its collapsed final rounds. */
+int halo_ipa_begin_vectors(halo_curve_t curve, const halo_wrapped_point_t* gs, const halo_fe_t* cs,
+                           const halo_fe_t* zs, size_t n, const halo_wrapped_point_t* H_prime,
+                           halo_ipa_session** out);
 /* L = <c_r, G_l> + H' <c_r, z_l>,  R = <c_l, G_r> + H' <c_l, z_r>  (pcdl.rs:412-418) */
 int halo_ipa_round_lr(halo_ipa_session* s, halo_wrapped_point_t* L, halo_wrapped_point_t* R);
 /* G_l[j] = G_l[j] + xi G_r[j] (affine), c_l[j] += xi^-1 c_r[j], z_l[j] += xi z_r[j]; m /= 2

@@ -155,3 +155,220 @@ def test_sharded_ntt_gloo(corc, world, logn):
     back = np.array([v for _, _, z in out for v in z], dtype=np.uint64).reshape(N, 4)
     assert np.array_equal(got, exp)
     assert np.array_equal(back, x)
+
+
+# ---------------------------------------------------------------------------------------------
+# distributed IPA opening (strided shards, per-round all-gather of 2 points): oracle-backed
+# session primitives on CPU, gloo world 2 and 4, against the single-session oracle loop
+# ---------------------------------------------------------------------------------------------
+def _oracle_mods():
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pasta as P
+    return P
+
+
+class OracleIpaOps:
+    """halo_amd.dist.IpaOps on the CPU: pure-Python restatement of pcdl.rs:404-438."""
+
+    def __init__(self, cname):
+        self.P = P = _oracle_mods()
+        self.c = P.CURVES[cname]
+
+    def _ints(self, a):
+        P, r = self.P, self.c.scalar
+        return [P.from_mont(P.limbs_to_int(x), r) for x in np.asarray(a, dtype=np.uint64).reshape(-1, 4)]
+
+    def _fe(self, xs):
+        P, r = self.P, self.c.scalar
+        return np.array([P.int_to_limbs(P.to_mont(x % r, r)) for x in xs], dtype=np.uint64).reshape(-1, 4)
+
+    def begin(self, gs, cs, zs, H_prime):
+        P, c = self.P, self.c
+        G = [P.wrapped_to_point(c, list(g)) for g in np.asarray(gs, dtype=np.uint64).reshape(-1, 8)]
+        return {"G": G, "C": self._ints(cs), "Z": self._ints(zs),
+                "H": P.wrapped_to_point(c, list(np.asarray(H_prime, dtype=np.uint64)))}
+
+    def round_lr(self, s):
+        P, c, r = self.P, self.c, self.c.scalar
+        G, C, Z, Hp = s["G"], s["C"], s["Z"], s["H"]
+        m = len(G) // 2
+        L = P.add(c, P.msm(c, G[:m], C[m:]), P.mul_fast(c, P.scalar_dot(C[m:], Z[:m], r), Hp))
+        R = P.add(c, P.msm(c, G[m:], C[:m]), P.mul_fast(c, P.scalar_dot(C[:m], Z[m:], r), Hp))
+        return (np.array(P.point_to_wrapped(c, L), dtype=np.uint64), np.array(P.point_to_wrapped(c, R), dtype=np.uint64))
+
+    def fold(self, s, xi, xi_inv):
+        x = self._ints(xi)[0]
+        _, _, _, _, s["G"], s["C"], s["Z"] = self.P.ipa_round(self.c, s["G"], s["C"], s["Z"], x)
+
+    def final(self, s):
+        P, c = self.P, self.c
+        return (np.array([P.point_to_wrapped(c, s["G"][0])], dtype=np.uint64), self._fe(s["C"][:1]),
+                self._fe(s["Z"][:1]))
+
+    def point_sum(self, pts):
+        P, c = self.P, self.c
+        acc = None
+        for p in pts:
+            acc = P.add(c, acc, P.wrapped_to_point(c, list(p)))
+        return np.array(P.point_to_wrapped(c, acc), dtype=np.uint64)
+
+
+def ipa_transcript(cname):
+    """Deterministic stand-in for the Poseidon transcript (the distributed loop only needs every
+    rank to derive the same xi from (xi_prev, L, R))."""
+    import hashlib
+    P = _oracle_mods()
+    r = P.CURVES[cname].scalar
+
+    def challenge(xi_prev, L, R):
+        h = hashlib.sha3_256((b"" if xi_prev is None else np.asarray(xi_prev).tobytes()) + L.tobytes() + R.tobytes())
+        v = int.from_bytes(h.digest(), "little") % r or 1
+        return np.array(P.int_to_limbs(P.to_mont(v, r)), dtype=np.uint64)
+
+    def inverse(x):
+        v = P.from_mont(P.limbs_to_int(x), r)
+        return np.array(P.int_to_limbs(P.to_mont(P.inv(v, r), r)), dtype=np.uint64)
+
+    return challenge, inverse
+
+
+def ipa_instance(cname, n, seed=5):
+    """(G, c, z-powers, H') of an opening of length n: G from the reference SRS recipe (C oracle)."""
+    import random
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import corc
+    P = _oracle_mods()
+    c = P.CURVES[cname]
+    r = c.scalar
+    rng = random.Random(seed)
+    g = corc.srs_generate(cname, n)
+    cs = [rng.randrange(r) for _ in range(n)]
+    z = rng.randrange(r)
+    zs = P.construct_powers(z, n, r)
+    Hp = P.mul_fast(c, rng.randrange(r), c.generator)
+    fe = lambda xs: np.array([P.int_to_limbs(P.to_mont(x, r)) for x in xs], dtype=np.uint64).reshape(-1, 4)
+    return g, fe(cs), fe(zs), np.array(P.point_to_wrapped(c, Hp), dtype=np.uint64)
+
+
+def _ipa_worker(rank, world, port, cname, n, q):
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+
+    from halo_amd.dist import ipa_shard, sharded_ipa_rounds, torch_gather_objects
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g, cs, zs, Hp = ipa_instance(cname, n)
+    shard = (ipa_shard(g, rank, world), ipa_shard(cs, rank, world), ipa_shard(zs, rank, world))
+    ch, inv = ipa_transcript(cname)
+    Ls, Rs, U, c = sharded_ipa_rounds([shard], Hp, ch, inv, OracleIpaOps(cname), world, torch_gather_objects(dist))
+    q.put((rank, [x.tolist() for x in Ls], [x.tolist() for x in Rs], U.tolist(), c.tolist()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def single_session_ipa(cname, g, cs, zs, Hp):
+    """The unsharded round loop (world 1 of the same code path, oracle primitives)."""
+    sys.path.insert(0, ROOT)
+    from halo_amd.dist import sharded_ipa_rounds
+    ch, inv = ipa_transcript(cname)
+    return sharded_ipa_rounds([(g, cs, zs)], Hp, ch, inv, OracleIpaOps(cname), 1, lambda objs: objs)
+
+
+@pytest.mark.parametrize("world,n,cname", [(2, 16, "pallas"), (4, 16, "vesta"), (4, 4, "pallas")])
+def test_sharded_ipa_gloo(corc, world, n, cname):
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_ipa_worker, args=(r, world, port, cname, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=300) for _ in range(world)])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    g, cs, zs, Hp = ipa_instance(cname, n)
+    Ls, Rs, U, c = single_session_ipa(cname, g, cs, zs, Hp)
+    assert len(Ls) == n.bit_length() - 1
+    for _, ls, rs, u, cc in out:  # every rank returns the unsharded proof
+        assert ls == [x.tolist() for x in Ls]
+        assert rs == [x.tolist() for x in Rs]
+        assert u == U.tolist() and cc == c.tolist()
+    # and the unsharded loop itself is the reference round loop (the restatement of pcdl.rs:404-438)
+    P = _oracle_mods()
+    cv = P.CURVES[cname]
+    G = [P.wrapped_to_point(cv, list(x)) for x in g]
+    Cs = OracleIpaOps(cname)._ints(cs)
+    Zs = OracleIpaOps(cname)._ints(zs)
+    Hpt = P.wrapped_to_point(cv, list(Hp))
+    challenge, _ = ipa_transcript(cname)
+    xi = None
+    for k in range(n.bit_length() - 1):
+        m = len(G) // 2
+        L = P.add(cv, P.msm(cv, G[:m], Cs[m:]), P.mul_fast(cv, P.scalar_dot(Cs[m:], Zs[:m], cv.scalar), Hpt))
+        assert Ls[k].tolist() == P.point_to_wrapped(cv, L)
+        xi = challenge(xi, Ls[k], Rs[k])
+        _, _, _, _, G, Cs, Zs = P.ipa_round(cv, G, Cs, Zs, OracleIpaOps(cname)._ints(xi)[0])
+    assert U.tolist() == P.point_to_wrapped(cv, G[0])
+
+
+# ---------------------------------------------------------------------------------------------
+# distributed polynomial evaluation: block partials + combine at z^per, gloo world 2 and 3
+# ---------------------------------------------------------------------------------------------
+class OraclePolyOps:
+    def __init__(self, field):
+        self.P = _oracle_mods()
+        self.m = self.P.FIELDS[field]
+
+    def _i(self, x):
+        return self.P.from_mont(self.P.limbs_to_int(np.asarray(x, dtype=np.uint64).reshape(4)), self.m)
+
+    def _f(self, v):
+        return np.array(self.P.int_to_limbs(self.P.to_mont(v, self.m)), dtype=np.uint64)
+
+    def eval_batch(self, polys, z):
+        zi = self._i(z)
+        return [self._f(self.P.horner([self._i(c) for c in np.asarray(p).reshape(-1, 4)], zi, self.m)) for p in polys]
+
+    def pow(self, z, e):
+        return self._f(pow(self._i(z), e, self.m))
+
+
+def _eval_worker(rank, world, port, n, q):
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+
+    from halo_amd.dist import shard_range, sharded_poly_eval
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(11)
+    coeffs = rng.integers(0, 2**62, size=(n, 4), dtype=np.uint64)
+    z = rng.integers(0, 2**62, size=4, dtype=np.uint64)
+    lo, hi = shard_range(n, rank, world)
+    v = sharded_poly_eval(coeffs[lo:hi], n, z, dist, OraclePolyOps("fp"))
+    q.put((rank, v.tolist()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n", [(2, 37), (3, 100)])
+def test_sharded_poly_eval_gloo(world, n):
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_eval_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=120) for _ in range(world)])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    rng = np.random.default_rng(11)
+    coeffs = rng.integers(0, 2**62, size=(n, 4), dtype=np.uint64)
+    z = rng.integers(0, 2**62, size=4, dtype=np.uint64)
+    exp = OraclePolyOps("fp").eval_batch([coeffs], z)[0].tolist()
+    for _, v in out:
+        assert v == exp

@@ -196,3 +196,49 @@ def test_decider_commit_equals_folded_U(hal, golden, corc, cname, cid):
     assert np.array_equal(pcdl.decider_commit(fe(xis, r), (1 << lg) - 1, cname), U)
     with pytest.raises(AssertionError, match=r"ms must be larger than Gs: \(Gs: 8\), \(ms: 4096\)"):
         pcdl.decider_commit(fe(xis, r), 7, cname)
+
+
+# ---------------------------------------------------------------------------------------------
+# distributed opening and evaluation, P virtual ranks on one GPU (the gather is the
+# identity over the P local sessions; tests/test_dist.py runs the same code over gloo ranks)
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("cname,cid", CURVES)
+@pytest.mark.parametrize("n,world", [(64, 4), (1024, 8), (16, 2)])
+def test_sharded_ipa_virtual_ranks(hal, corc, cname, cid, n, world):
+    """Strided shards + per-round point sums + collapsed final rounds == the single session."""
+    from halo_amd.dist import GpuIpaOps, ipa_shard, sharded_ipa_rounds
+
+    c = P.CURVES[cname]
+    r = c.scalar
+    g = corc.srs_generate(cname, n)
+    group.PublicParams.upload(cname, g, precompute_windows=False)
+    rng = random.Random(n + world)
+    cs = fe([rng.randrange(r) for _ in range(n)], r)
+    z = rng.randrange(r)
+    zs = fe(P.construct_powers(z, n, r), r)
+    Hp = np.array(P.point_to_wrapped(c, P.mul_fast(c, rng.randrange(r), c.generator)), dtype=np.uint64)
+    challenge, inverse = transcript(cname)
+    Ls, Rs, U, cfin = pcdl.ipa_rounds(cs, fe([z], r), Hp, challenge, inverse, cname)
+    shards = [(ipa_shard(g[:n], k, world), ipa_shard(cs, k, world), ipa_shard(zs, k, world)) for k in range(world)]
+    Ls2, Rs2, U2, c2 = sharded_ipa_rounds(shards, Hp, challenge, inverse, GpuIpaOps(cname), world, lambda o: o)
+    assert len(Ls2) == len(Ls)
+    for a, b in zip(Ls + Rs, Ls2 + Rs2):
+        assert np.array_equal(a, b)
+    assert np.array_equal(U, U2)
+    assert np.array_equal(cfin, c2)
+
+
+@pytest.mark.parametrize("n,world", [(1000, 3), (1 << 16, 8), (5, 8)])
+def test_sharded_poly_eval_virtual_ranks(hal, n, world):
+    from halo_amd.dist import PolyOps, poly_eval_combine, poly_eval_partial, shard_range
+
+    rng = np.random.default_rng(n)
+    m = P.FIELDS["fp"]
+    coeffs = fe([int(x) for x in rng.integers(0, 2**62, size=n)], m)
+    z = fe([int(rng.integers(1, 2**62))], m)[0]
+    ops = PolyOps("fp")
+    parts = [poly_eval_partial(coeffs[slice(*shard_range(n, k, world))], z, ops) for k in range(world)]
+    got = poly_eval_combine(parts, n, z, ops)
+    exp = poly.evaluate_batch([coeffs], z, "fp")[0]
+    assert np.array_equal(got, exp)
+    assert unfe(exp, m) == [P.horner(unfe(coeffs, m), unfe(z, m)[0], m)]
