@@ -50,6 +50,9 @@ def parse():
     ap.add_argument("--sizes", default="24", help="extra MSM / NTT sizes (log2, comma separated) under extra.sizes")
     ap.add_argument("--dist-ntt-logn", type=int, default=24, help="distributed single NTT size (N > 1 only; 0 = off)")
     ap.add_argument("--ipa", type=int, default=1, help="measure the 2^logn IPA opening (extra.ipa_open)")
+    ap.add_argument("--dist-ipa", type=int, default=1, help="N > 1: the sharded 2^logn opening (extra.dist_ipa)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="rehearsal only: every rank on cuda:0 over gloo (multi-rank runs on a one-GPU box)")
     return ap.parse_args()
 
 
@@ -65,11 +68,16 @@ def main():
     from halo_amd import _lib as H
     from halo_amd.dist import allgather_points
 
+    if args.same_device:
+        local = 0
     H.ensure_device(local)
     torch.cuda.set_device(local)
     L = H.load()
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.same_device:  # RCCL refuses two ranks on one GPU: rehearse the protocol over gloo
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     curve = H.CURVES[args.curve]
     n = 1 << args.logn
     gen = torch.Generator(device="cuda")
@@ -323,6 +331,64 @@ def main():
         }
         del xl, y, z
 
+    # ---- distributed IPA opening (strided shards, halo_amd.dist.sharded_ipa_rounds), N > 1 only:
+    # every rank holds the same synthetic 2^logn SRS; rank r opens with the shard G[i P + r]
+    dist_ipa = None
+    if world > 1 and args.ipa and args.dist_ipa:
+        from halo_amd.dist import GpuIpaOps, ipa_shard, sharded_ipa_rounds, torch_gather_objects
+        n_ = 1 << args.logn
+        H.check(L.halo_srs_synthesize(curve, n_, 777))
+        G = np.zeros((n_, 8), dtype=np.uint64)
+        H.check(L.halo_srs_read(curve, 0, n_, H.ptr(G)))
+        Rm = 0x40000000000000000000000000000000224698FC0994A8DD8C46EB2100000001
+
+        def fe1(v):
+            m = v * (1 << 256) % Rm
+            return np.array([(m >> (64 * i)) & (2**64 - 1) for i in range(4)], dtype=np.uint64)
+
+        rng = np.random.default_rng(99)
+        cs = rng.integers(0, 2**62, size=(n_, 4), dtype=np.uint64)
+        z = 12345
+        zs = np.zeros((n_, 4), dtype=np.uint64)
+        H.check(L.halo_construct_powers(H.FP, H.ptr(fe1(z)), n_, H.ptr(zs)))
+        hp = G[1].copy()
+        ks = {"k": 0}
+
+        def challenge(xi_prev, Lp, Rp):
+            ks["k"] += 1
+            return fe1((int.from_bytes(Lp.tobytes()[:16], "little") ^ ks["k"]) % Rm or 1)
+
+        def inverse(x):
+            v = int.from_bytes(x.tobytes(), "little") * pow(1 << 256, -1, Rm) % Rm
+            return fe1(pow(v, -1, Rm))
+
+        shard = (ipa_shard(G, rank, world), ipa_shard(cs, rank, world), ipa_shard(zs, rank, world))
+        gather = torch_gather_objects(dist)
+        best = None
+        for _ in range(2):
+            ks["k"] = 0
+            dist.barrier()
+            torch.cuda.synchronize()
+            a0 = time.perf_counter()
+            Ls, Rs, U, c0 = sharded_ipa_rounds([shard], hp, challenge, inverse, GpuIpaOps(args.curve), world, gather)
+            torch.cuda.synchronize()
+            tt = torch.tensor([time.perf_counter() - a0], dtype=torch.float64, device="cuda")
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            best = float(tt.item()) if best is None else min(best, float(tt.item()))
+        same = None
+        if rank == 0:  # the unsharded opening of the same instance on one GPU must give the same proof
+            ks["k"] = 0
+            Ls1, Rs1, U1, c1 = sharded_ipa_rounds([(G, cs, zs)], hp, challenge, inverse, GpuIpaOps(args.curve), 1,
+                                                  lambda o: o)
+            same = all(np.array_equal(a_, b_) for a_, b_ in zip(Ls + Rs + [U, c0], Ls1 + Rs1 + [U1, c1]))
+        dist_ipa = {
+            "workload": f"pcdl open 2^{args.logn} sharded over {world} ranks (strided G/c/z shards, "
+                        f"per-round all-gather of L_r, R_r, last lg P rounds collapsed)",
+            "open_ms": best * 1e3,
+            "matches_single_gpu": same,
+        }
+        del G, cs, zs
+
     if rank != 0:
         if world > 1:
             dist.barrier()
@@ -400,6 +466,7 @@ def main():
             "ntt": ntt_main,
             "sizes": sizes,
             "dist_ntt": dist_ntt,
+            "dist_ipa": dist_ipa,
             "ipa_open": ipa,
             "evals_op": evals,
         },

@@ -161,6 +161,8 @@ _initialized = set()
 def ensure_device(device: int | None = None) -> None:
     """halo_init on first use (device from HALO_DEVICE / LOCAL_RANK, default 0)."""
     if device is None:
+        if _initialized:  # the process already chose its device (e.g. bench.py's explicit one)
+            return
         device = int(os.environ.get("HALO_DEVICE", os.environ.get("LOCAL_RANK", "0")))
     if device in _initialized:
         return
