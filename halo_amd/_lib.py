@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libhalo_gpu.so")
+LIB_PATH = os.environ.get("HALO_LIB") or os.path.join(_HERE, "lib", "libhalo_gpu.so")  # HALO_LIB: A/B builds
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "halo_gpu.h")
 
 PALLAS, VESTA = 0, 1
