@@ -411,8 +411,11 @@ def main():
             traffic = None
 
     cpu = None
+    cpu_ntt = cpu_fold = None
     if not args.no_cpu and world == 1:
         cpu = cpu_baseline(L, H, curve, n, scalars0, out_check=True, budget_s=args.cpu_seconds)
+        cpu_ntt = cpu_ntt_baseline(L, H, args.ntt_logn, sp, ntt_main)
+        cpu_fold = cpu_fold_baseline(L, H, curve, 13, ipa)
 
     madds = n * (-(-255 // window_bits)) if window_bits else 0  # one mixed addition per nonzero digit
     valu_achieved = madds * 10 / (acc_avg_ms * 1e-3) if acc_avg_ms > 0 else 0.0
@@ -469,6 +472,8 @@ def main():
             "dist_ipa": dist_ipa,
             "ipa_open": ipa,
             "evals_op": evals,
+            "cpu_ntt": cpu_ntt,
+            "cpu_ipa_fold": cpu_fold,
         },
     }
     print(json.dumps(line))
@@ -506,6 +511,87 @@ def cpu_baseline(L, H, curve, n, scalars_dev, out_check, budget_s):
         "sample": f"{reps} x full 2^{n.bit_length() - 1}-point MSM (same bases/scalars as the GPU), C restatement of "
                   f"ark-ec 0.5 msm_bigint_wnaf, c={corc.msm_window_size(n)}, OpenMP over windows",
         "gpu_matches_cpu": bool(np.array_equal(cpu_out, gpu_out)) if out_check else None,
+    }
+
+
+def _cpu_threads():
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    return min(threads, 16)
+
+
+def cpu_ntt_baseline(L, H, logn, sp, gpu_ntt):
+    """Rank 0, N=1 only: the C restatement of ark-poly's radix-2 FFT (oracle/oracle.c) on host cores,
+    NTT + iNTT pair at the bench size, on the same input as one GPU forward transform (bit-exact check)."""
+    import torch
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import corc  # noqa: E402  (oracle: only the cpu_baseline legs may load it)
+
+    N = 1 << logn
+    rng = np.random.default_rng(7)
+    x = rng.integers(0, 2**63, size=(N, 4), dtype=np.uint64)
+    x[:, 3] &= np.uint64(0x0FFFFFFFFFFFFFFF)
+    d = torch.from_numpy(x.view(np.int64).copy()).cuda()
+    H.check(L.halo_ntt_dev(H.FP, ctypes.c_void_p(d.data_ptr()), logn, 1, 0, sp))
+    torch.cuda.synchronize()
+    y_gpu = d.cpu().numpy().view(np.uint64)
+    threads = _cpu_threads()
+    t0 = time.perf_counter()
+    y = corc.ntt("fp", x, inverse=False, threads=threads)
+    z = corc.ntt("fp", y, inverse=True, threads=threads)
+    dt = time.perf_counter() - t0
+    return {
+        "workload": f"ntt+intt_2^{logn}_fp",
+        "pair_ms": dt * 1e3,
+        "elems_per_s_pair": N / dt,
+        "cores": threads,
+        "kind": "port",
+        "sample": f"1 x NTT + iNTT at 2^{logn} (C restatement of ark-poly 0.5 radix-2 DIF/DIT + derange, OpenMP)",
+        "gpu_matches_cpu": bool(np.array_equal(y, y_gpu)) and bool(np.array_equal(z, x)),
+        "gpu_over_cpu": (dt * 1e3) / gpu_ntt["pair_ms"] if gpu_ntt else None,
+    }
+
+
+def cpu_fold_baseline(L, H, curve, logm, ipa):
+    """Rank 0, N=1 only: one IPA fold round (pcdl.rs:427-435: G' = G_l + xi G_r with per-element
+    scalar multiplication and affine conversion, c' and z' folds) over 2^logm element pairs, C
+    restatement on host cores vs the device fold of the same inputs (halo_ipa_fold_host)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import corc  # noqa: E402  (oracle: only the cpu_baseline legs may load it)
+
+    m = 1 << logm
+    cname = "pallas" if curve == 0 else "vesta"
+    gs = np.zeros((2 * m, 8), dtype=np.uint64)
+    H.check(L.halo_srs_read(curve, 0, 2 * m, H.ptr(gs)))
+    rng = np.random.default_rng(11)
+
+    def fes(k):
+        a = rng.integers(0, 2**63, size=(k, 4), dtype=np.uint64)
+        a[:, 3] &= np.uint64(0x0FFFFFFFFFFFFFFF)
+        return np.ascontiguousarray(a)
+
+    cs, zs, xi = fes(2 * m), fes(2 * m), fes(1)[0]
+    xi_inv = corc.field_inv("fp" if curve == 0 else "fq", xi)
+    g_gpu, c_gpu, z_gpu = gs.copy(), cs.copy(), zs.copy()
+    H.check(L.halo_ipa_fold_host(curve, H.ptr(g_gpu), H.ptr(c_gpu), H.ptr(z_gpu), m, H.ptr(xi), H.ptr(xi_inv)))
+    threads = _cpu_threads()
+    t0 = time.perf_counter()
+    g2, c2, z2 = corc.ipa_fold(cname, gs, cs, zs, xi, xi_inv, threads=threads)
+    dt = time.perf_counter() - t0
+    ok = np.array_equal(g2, g_gpu[:m]) and np.array_equal(c2, c_gpu[:m]) and np.array_equal(z2, z_gpu[:m])
+    gpu_rate = None
+    if ipa and ipa.get("fold_kernels_ms"):
+        gpu_rate = ((1 << ipa["rounds"]) - 1) / (ipa["fold_kernels_ms"] * 1e-3)
+    return {
+        "workload": f"IPA fold round, {m} element pairs ({cname})",
+        "elements_per_s": m / dt,
+        "cores": threads,
+        "kind": "port",
+        "sample": f"1 x fold of 2^{logm} pairs (C restatement of pcdl.rs:427-435: per-element variable-base "
+                  f"scalar multiplication + affine conversion), OpenMP",
+        "gpu_matches_cpu": bool(ok),
+        "gpu_elements_per_s": gpu_rate,
+        "gpu_note": "device fold rate over the whole 2^logn opening (extra.ipa_open.fold_kernels_ms)",
     }
 
 
