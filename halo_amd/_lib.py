@@ -83,12 +83,16 @@ SIGNATURES = {
     "halo_evals_op": [ctypes.c_int, ctypes.c_int, _vp, _vp, _vp, ctypes.c_uint32, _vp, _sz],
     "halo_evals_op_dev": [ctypes.c_int, ctypes.c_int, _vp, _vp, _vp, ctypes.c_uint32, _vp, _sz, _vp],
     "halo_divide_by_vanishing": [ctypes.c_int, _vp, _sz, _sz, _vp, ctypes.POINTER(_sz), _vp, ctypes.POINTER(_sz)],
+    "halo_divide_by_vanishing_dev": [ctypes.c_int, _vp, _sz, _sz, _vp, _vp, _vp],
+    "halo_evals_scan_dev": [ctypes.c_int, ctypes.c_int, _vp, _vp, _sz, _vp],
     "halo_ntt_twiddle_dev": [ctypes.c_int, _vp, ctypes.c_uint, _sz, _sz, _sz, _sz, ctypes.c_int, _vp],
     "halo_transpose_dev": [_vp, _vp, _sz, _sz, _sz, _sz, _vp],
     "halo_poly_eval_batch": [ctypes.c_int, _vp, _vp, _sz, _vp, _vp],
+    "halo_poly_eval_batch_dev": [ctypes.c_int, _vp, _vp, _sz, _vp, _vp, _vp],
     "halo_scalar_dot": [ctypes.c_int, _vp, _vp, _sz, _vp],
     "halo_construct_powers": [ctypes.c_int, _vp, _sz, _vp],
     "halo_ipa_begin": [ctypes.c_int, _vp, _sz, _vp, _vp, ctypes.POINTER(_vp)],
+    "halo_ipa_begin_dev": [ctypes.c_int, _vp, _sz, _vp, _vp, ctypes.POINTER(_vp)],
     "halo_ipa_begin_vectors": [ctypes.c_int, _vp, _vp, _vp, _sz, _vp, ctypes.POINTER(_vp)],
     "halo_ipa_round_lr": [_vp, _vp, _vp],
     "halo_ipa_fold": [_vp, _vp, _vp],
@@ -177,7 +181,9 @@ def ptr(a: np.ndarray | None):
     if a is None:
         return None
     assert a.flags["C_CONTIGUOUS"], "arrays passed to libhalo_gpu must be C-contiguous"
-    return ctypes.c_void_p(a.ctypes.data)
+    # data_as keeps a reference to the array in the returned pointer object, so a temporary
+    # (e.g. ``ptr(fe(x))`` inside a call's argument list) stays alive until the call returns
+    return a.ctypes.data_as(ctypes.c_void_p)
 
 
 def fe_array(a, n: int | None = None) -> np.ndarray:

@@ -66,6 +66,84 @@ __global__ __launch_bounds__(256) void k_div_vanishing(const uint4* c, size_t le
     }
 }
 
+// Running product (protocol.rs:143-154, the permutation accumulator z): inclusive prefix product
+// out[i] = prod_{j <= i} in[j] (reverse: suffix product prod_{j >= i} in[j]), ark in / out.  Three
+// phases: per-block scan (SCAN_EPT elements per thread, then a Hillis-Steele scan of the thread
+// products in LDS), a one-block scan of the block totals, and a multiply by each block's exclusive
+// prefix.  Internal Montgomery form inside (one conversion in, one out).
+constexpr int SCAN_THREADS = 256, SCAN_EPT = 8, SCAN_BLOCK = SCAN_THREADS * SCAN_EPT;
+
+HALO_DEV size_t scan_idx(size_t i, size_t n, int reverse) { return reverse ? n - 1 - i : i; }
+
+template <class F>
+HALO_DEV void lds_scan_mul(uint4* red, uint32_t tid, Fe<F>& v) {  // inclusive scan of v over the block
+    fe_store(red + 2 * tid, v);
+    __syncthreads();
+    for (uint32_t off = 1; off < SCAN_THREADS; off <<= 1) {
+        Fe<F> t = v;
+        if (tid >= off) t = fe_mul(fe_load<F>(red + 2 * (tid - off)), v);
+        __syncthreads();
+        v = t;
+        fe_store(red + 2 * tid, v);
+        __syncthreads();
+    }
+}
+
+template <class F>
+__global__ __launch_bounds__(SCAN_THREADS) void k_scan_block(const uint4* in, uint4* out, size_t n, int reverse,
+                                                             uint4* totals) {
+    __shared__ uint4 red[SCAN_THREADS * 2];
+    const uint32_t tid = threadIdx.x;
+    const size_t base = (size_t)blockIdx.x * SCAN_BLOCK + (size_t)tid * SCAN_EPT;
+    Fe<F> x[SCAN_EPT];
+    Fe<F> run = fe_one<F>();
+#pragma unroll
+    for (int e = 0; e < SCAN_EPT; e++) {
+        x[e] = fe_one<F>();
+        if (base + e < n) x[e] = fe_from_ark<F>(in + 2 * scan_idx(base + e, n, reverse));
+        run = fe_mul(run, x[e]);
+    }
+    Fe<F> incl = run;
+    lds_scan_mul<F>(red, tid, incl);
+    Fe<F> p = fe_one<F>();  // exclusive prefix of this thread inside the block
+    if (tid > 0) p = fe_load<F>(red + 2 * (tid - 1));
+#pragma unroll
+    for (int e = 0; e < SCAN_EPT; e++) {
+        p = fe_mul(p, x[e]);
+        if (base + e < n) fe_to_ark(out + 2 * scan_idx(base + e, n, reverse), p);
+    }
+    if (tid == SCAN_THREADS - 1) fe_store(totals + 2 * blockIdx.x, fe_reduce_2p(incl));
+}
+
+// one block: totals[b] <- exclusive prefix product of the block totals (internal form)
+template <class F>
+__global__ __launch_bounds__(SCAN_THREADS) void k_scan_totals(uint4* totals, uint32_t nb) {
+    __shared__ uint4 red[SCAN_THREADS * 2];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t per = (nb + SCAN_THREADS - 1) / SCAN_THREADS;
+    const uint32_t b0 = tid * per;
+    Fe<F> run = fe_one<F>();
+    for (uint32_t b = b0; b < min(nb, b0 + per); b++) run = fe_mul(run, fe_load<F>(totals + 2 * b));
+    Fe<F> incl = run;
+    lds_scan_mul<F>(red, tid, incl);
+    Fe<F> p = fe_one<F>();
+    if (tid > 0) p = fe_load<F>(red + 2 * (tid - 1));
+    for (uint32_t b = b0; b < min(nb, b0 + per); b++) {
+        const Fe<F> t = fe_load<F>(totals + 2 * b);
+        fe_store(totals + 2 * b, fe_reduce_2p(p));
+        p = fe_mul(p, t);
+    }
+}
+
+template <class F>
+__global__ __launch_bounds__(256) void k_scan_apply(uint4* out, size_t n, int reverse, const uint4* totals) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x + SCAN_BLOCK;  // block 0 is final
+    if (i >= n) return;
+    const size_t j = scan_idx(i, n, reverse);
+    const Fe<F> t = fe_load<F>(totals + 2 * (i / SCAN_BLOCK));
+    fe_to_ark(out + 2 * j, fe_mul(fe_from_ark<F>(out + 2 * j), t));
+}
+
 template <class F>
 static Fe<F> host_fe_raw(const uint32_t (&k)[NLIMB]) {
     Fe<F> r;
@@ -180,5 +258,53 @@ extern "C" int halo_divide_by_vanishing(halo_field_t field, const halo_fe_t* coe
     HALO_CHECK(copy_d2h(remainder, st->scratch[2].ptr, n * 32, s));
     *q_len = trimmed(quotient, qn);
     *r_len = trimmed(remainder, n);
+    return HALO_OK;
+}
+
+extern "C" int halo_evals_scan_dev(halo_field_t field, int reverse, const void* d_in, void* d_out, size_t n,
+                                   void* stream) {
+    clear_error();
+    if (field != HALO_FP && field != HALO_FQ) return set_error(HALO_EINVAL, "unknown field id %d", (int)field);
+    if (n && (!d_in || !d_out)) return set_error(HALO_EINVAL, "halo_evals_scan_dev: null buffer");
+    if (!n) return HALO_OK;
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    const size_t nb = (n + SCAN_BLOCK - 1) / SCAN_BLOCK;
+    if (nb > (size_t)SCAN_THREADS * 4096) return set_error(HALO_EINVAL, "halo_evals_scan_dev: n too large");
+    hipStream_t s = (hipStream_t)stream;
+    DevBuf* tot;
+    {
+        std::lock_guard<std::mutex> g(st->mu);
+        tot = &st->scan_tmp;
+        HALO_CHECK(tot->reserve(nb * 32));
+    }
+    DISPATCH_FIELD(field, F, {
+        hipLaunchKernelGGL(k_scan_block<F>, dim3((unsigned)nb), dim3(SCAN_THREADS), 0, s, (const uint4*)d_in,
+                           (uint4*)d_out, n, reverse, tot->as<uint4>());
+        if (nb > 1) {
+            hipLaunchKernelGGL(k_scan_totals<F>, dim3(1), dim3(SCAN_THREADS), 0, s, tot->as<uint4>(), (uint32_t)nb);
+            hipLaunchKernelGGL(k_scan_apply<F>, dim3((unsigned)((n - SCAN_BLOCK + 255) / 256)), dim3(256), 0, s,
+                               (uint4*)d_out, n, reverse, tot->as<const uint4>());
+        }
+    });
+    HALO_HIP(hipGetLastError());
+    return HALO_OK;
+}
+
+extern "C" int halo_divide_by_vanishing_dev(halo_field_t field, const void* d_coeffs, size_t len, size_t n,
+                                            void* d_quotient, void* d_remainder, void* stream) {
+    clear_error();
+    if (field != HALO_FP && field != HALO_FQ) return set_error(HALO_EINVAL, "unknown field id %d", (int)field);
+    if (!n || len < n || !d_coeffs || !d_remainder || (len > n && !d_quotient))
+        return set_error(HALO_EINVAL, "halo_divide_by_vanishing_dev: bad argument (len %zu, n %zu)", len, n);
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    const size_t threads = std::max(len - n, n);
+    DISPATCH_FIELD(field, F, {
+        hipLaunchKernelGGL(k_div_vanishing<F>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                           (hipStream_t)stream, (const uint4*)d_coeffs, len, n, (uint4*)d_quotient,
+                           (uint4*)d_remainder);
+    });
+    HALO_HIP(hipGetLastError());
     return HALO_OK;
 }

@@ -15,6 +15,7 @@
 //  * group::scalar_dot / construct_powers (crates/group/src/group.rs:43-45,58-66).
 //  * &Poly * &Poly (protocol.rs:132-139, pcdl.rs:215): NTT, pointwise product, iNTT, trim.
 #include <algorithm>
+#include <cstring>
 #include <vector>
 
 #include "dispatch.hpp"
@@ -415,6 +416,48 @@ extern "C" int halo_poly_eval_batch(halo_field_t field, const halo_fe_t* const* 
     return copy_d2h(out, part + (size_t)k * nchunks * 32, k * 32, s);
 }
 
+// Device-resident variant (the prover's 78 evaluations at xi, protocol.rs:315-323): d_polys is a
+// host array of k device pointers (ark coefficients), results (ark) to d_out[k].  Stream-ordered;
+// the pointer table is staged through a per-device buffer, so calls on one stream may be queued back
+// to back.
+extern "C" int halo_poly_eval_batch_dev(halo_field_t field, const void* const* d_polys, const size_t* lens, size_t k,
+                                        const halo_fe_t* z, void* d_out, void* stream) {
+    clear_error();
+    HALO_CHECK(check_field_i(field));
+    if (!z || (k && (!d_polys || !lens || !d_out))) return set_error(HALO_EINVAL, "halo_poly_eval_batch_dev: null buffer");
+    if (!k) return HALO_OK;
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    hipStream_t s = (hipStream_t)stream;
+    size_t maxlen = 0;
+    for (size_t i = 0; i < k; i++) {
+        if (lens[i] && !d_polys[i]) return set_error(HALO_EINVAL, "halo_poly_eval_batch_dev: null polynomial %zu", i);
+        maxlen = std::max(maxlen, lens[i]);
+    }
+    const size_t chunk = 32;
+    const int nchunks = (int)std::max<size_t>(1, (maxlen + chunk * RED_THREADS - 1) / (chunk * RED_THREADS));
+    const size_t meta_bytes = k * (sizeof(void*) + sizeof(size_t)) + 32;
+    HALO_CHECK(st->eval_meta[0].reserve(meta_bytes));
+    HALO_CHECK(st->eval_meta[1].reserve((size_t)k * nchunks * 32));
+    std::vector<unsigned char> host(meta_bytes);
+    memcpy(host.data(), d_polys, k * sizeof(void*));
+    memcpy(host.data() + k * sizeof(void*), lens, k * sizeof(size_t));
+    memcpy(host.data() + k * (sizeof(void*) + sizeof(size_t)), z, 32);
+    char* meta = (char*)st->eval_meta[0].ptr;
+    HALO_CHECK(copy_h2d(meta, host.data(), meta_bytes, s));
+    char* part = (char*)st->eval_meta[1].ptr;
+    DISPATCH_FIELD(field, F, {
+        hipLaunchKernelGGL(k_eval_chunks<F>, dim3(nchunks, (unsigned)k), dim3(RED_THREADS), 0, s,
+                           (const uint4* const*)meta, (const size_t*)(meta + k * sizeof(void*)),
+                           (const uint4*)(meta + k * (sizeof(void*) + sizeof(size_t))), chunk, nchunks, (uint4*)part);
+        hipLaunchKernelGGL(k_sum_internal_to_ark<F>, dim3((unsigned)k), dim3(RED_THREADS), 0, s, (const uint4*)part,
+                           nchunks, (uint4*)d_out);
+    });
+    HALO_HIP(hipGetLastError());
+    return HALO_OK;
+}
+
 extern "C" int halo_poly_mul(halo_field_t field, const halo_fe_t* a, size_t la, const halo_fe_t* b, size_t lb,
                              halo_fe_t* out, size_t* out_len) {
     clear_error();
@@ -466,7 +509,7 @@ extern "C" int halo_poly_mul(halo_field_t field, const halo_fe_t* a, size_t la, 
 // final collapsed rounds, halo_amd/dist.py).
 static int ipa_begin(halo_curve_t curve, size_t n, const halo_wrapped_point_t* gs_host, const halo_fe_t* cs,
                      const halo_fe_t* zs_host, const halo_fe_t* z, const halo_wrapped_point_t* H_prime,
-                     halo_ipa_session** out) {
+                     halo_ipa_session** out, bool cs_on_device = false) {
     if (curve != HALO_PALLAS && curve != HALO_VESTA) return set_error(HALO_EINVAL, "unknown curve");
     if (!cs || !(z || zs_host) || !H_prime || !out) return set_error(HALO_EINVAL, "halo_ipa_begin: null argument");
     if (n <= 1) return set_error(HALO_EINVAL, "assertion failed: n > 1");
@@ -497,7 +540,14 @@ static int ipa_begin(halo_curve_t curve, size_t n, const halo_wrapped_point_t* g
             rc = set_error(HALO_EDEVICE, "copy of the SRS prefix failed");
             break;
         }
-        if ((rc = copy_h2d(ses->cs.ptr, cs, n * 32, s))) break;
+        if (cs_on_device) {
+            if (hipMemcpyAsync(ses->cs.ptr, cs, n * 32, hipMemcpyDeviceToDevice, s) != hipSuccess) {
+                rc = set_error(HALO_EDEVICE, "copy of the coefficients failed");
+                break;
+            }
+        } else if ((rc = copy_h2d(ses->cs.ptr, cs, n * 32, s))) {
+            break;
+        }
         char* sm = (char*)ses->small.ptr;
         if (zs_host) {
             if ((rc = copy_h2d(ses->zs.ptr, zs_host, n * 32, s))) break;
@@ -531,6 +581,14 @@ extern "C" int halo_ipa_begin(halo_curve_t curve, const halo_fe_t* cs, size_t n,
                               const halo_wrapped_point_t* H_prime, halo_ipa_session** out) {
     clear_error();
     return ipa_begin(curve, n, nullptr, cs, nullptr, z, H_prime, out);
+}
+
+// Device-resident coefficients (the prover's opened polynomials never leave HBM): d_cs holds n ark
+// coefficients on the device, ordered on the null stream.
+extern "C" int halo_ipa_begin_dev(halo_curve_t curve, const void* d_cs, size_t n, const halo_fe_t* z,
+                                  const halo_wrapped_point_t* H_prime, halo_ipa_session** out) {
+    clear_error();
+    return ipa_begin(curve, n, nullptr, (const halo_fe_t*)d_cs, nullptr, z, H_prime, out, true);
 }
 
 extern "C" int halo_ipa_begin_vectors(halo_curve_t curve, const halo_wrapped_point_t* gs, const halo_fe_t* cs,

@@ -65,6 +65,8 @@ struct DeviceState {
     SrsState srs[2];               // per curve
     // scratch
     DevBuf scratch[8];
+    DevBuf scan_tmp;     // halo_evals_scan_dev block totals
+    DevBuf eval_meta[2]; // halo_poly_eval_batch_dev: pointer/length tables, partial sums
     // NTT twiddle caches: key (field, log, inverse)
     struct Twiddles {
         int field, logn, inverse;

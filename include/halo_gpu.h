@@ -201,11 +201,22 @@ int halo_evals_op_dev(halo_field_t field, int op, const void* d_a, const void* d
  * X^n - 1; quotient (room for len - n) and remainder (room for n), both trimmed. */
 int halo_divide_by_vanishing(halo_field_t field, const halo_fe_t* coeffs, size_t len, size_t n, halo_fe_t* quotient,
                              size_t* q_len, halo_fe_t* remainder, size_t* r_len);
+/* Device-resident variant (no trimming): d_coeffs has len >= n entries; quotient len - n entries
+ * (may be null when len == n), remainder n entries. */
+int halo_divide_by_vanishing_dev(halo_field_t field, const void* d_coeffs, size_t len, size_t n,
+                                 void* d_quotient, void* d_remainder, void* stream);
+/* Running product of the permutation argument (protocol.rs:143-154): inclusive prefix product
+ * out[i] = prod_{j<=i} in[j] over n device elements (reverse != 0: suffix product prod_{j>=i}). */
+int halo_evals_scan_dev(halo_field_t field, int reverse, const void* d_in, void* d_out, size_t n, void* stream);
 
 /* ------------------------------------------------------------------ a8: evaluation / dots */
 /* DensePolynomial::evaluate (Horner; pcdl.rs:49,471), k polynomials at one point z. */
 int halo_poly_eval_batch(halo_field_t field, const halo_fe_t* const* polys, const size_t* lens,
                          size_t k, const halo_fe_t* z, halo_fe_t* out);
+/* Device-resident variant: d_polys is a host array of k device pointers (ark coefficients);
+ * d_out receives k device field elements.  Stream-ordered. */
+int halo_poly_eval_batch_dev(halo_field_t field, const void* const* d_polys, const size_t* lens, size_t k,
+                             const halo_fe_t* z, void* d_out, void* stream);
 /* group::scalar_dot (crates/group/src/group.rs:43-45). */
 int halo_scalar_dot(halo_field_t field, const halo_fe_t* xs, const halo_fe_t* ys, size_t n,
                     halo_fe_t* out);
@@ -221,6 +232,9 @@ int halo_construct_powers(halo_field_t field, const halo_fe_t* z, size_t n, halo
 typedef struct halo_ipa_session halo_ipa_session;
 int halo_ipa_begin(halo_curve_t curve, const halo_fe_t* cs, size_t n, const halo_fe_t* z,
                    const halo_wrapped_point_t* H_prime, halo_ipa_session** out);
+/* As halo_ipa_begin with the n coefficients already on the device (ark format; null stream order). */
+int halo_ipa_begin_dev(halo_curve_t curve, const void* d_cs, size_t n, const halo_fe_t* z,
+                       const halo_wrapped_point_t* H_prime, halo_ipa_session** out);
 /* Session over explicit vectors G (WrappedPoints), c, z of length n (power of two >= 2) instead of
  * the SRS prefix and the powers of z: one rank's shard of a distributed opening (the
  * strided split G[i P + r] keeps every fold pair on one rank) and its collapsed final rounds. */

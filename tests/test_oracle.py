@@ -177,3 +177,22 @@ def test_h_coeffs(golden, tag):
         term[0], term[1 << i] = 1, xis[3 - i]
         h = P.poly_mul(h, term, m)
     assert h == P.h_coeffs(xis, m)
+
+
+def test_prover_pipeline_runs_on_cpu_restatement():
+    """The generic naive_prover pipeline (halo_amd.prover) on the CPU restatement backend at n = 8:
+    the checker side of tests/test_gpu_prover.py must itself run (no GPU needed)."""
+    import pasta as P
+    import prover_ref
+
+    from halo_amd import prover
+
+    c = P.PALLAS
+    n = 8
+    srs = np.array([P.point_to_wrapped(c, P.mul_fast(c, 1000 + i, c.generator)) for i in range(n)], dtype=np.uint64)
+    B = prover_ref.RefBackend("pallas", srs, srs[1])
+    out = prover.naive_prover(B, prover.synthetic_witness(B, n, seed=3), n, prover.Challenges(B.m))
+    assert len(out["C_ws"]) == 16 and len(out["C_ts"]) == 16 and len(out["vs"]) == 91
+    assert len(out["q_r"]["Ls"]) == 3 and len(out["acc"]["Rs"]) == 3
+    # the opened polynomial's evaluation is the one the instance reports
+    assert out["q_r"]["v"] == out["q_r"]["v"] % B.m

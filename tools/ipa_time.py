@@ -28,6 +28,7 @@ for lg in [int(x) for x in (sys.argv[1:] or ['16', '20'])]:
         Lp = np.zeros(8, dtype=np.uint64); Rp = np.zeros(8, dtype=np.uint64)
         H.check(L.halo_profile_reset()); H.check(L.halo_profile_enable(1))
         t_lr = t_fold = 0.0
+        per = []
         t0 = time.perf_counter()
         for r in range(lg):
             a = time.perf_counter()
@@ -37,6 +38,7 @@ for lg in [int(x) for x in (sys.argv[1:] or ['16', '20'])]:
             H.check(L.halo_ipa_fold(s, H.ptr(fe1(xi)), H.ptr(fe1(pow(xi, -1, R)))))
             c = time.perf_counter()
             t_lr += b - a; t_fold += c - b
+            per.append((round(1e3 * (b - a), 2), round(1e3 * (c - b), 2)))
         t1 = time.perf_counter()
         U = np.zeros(8, dtype=np.uint64); c0 = np.zeros(4, dtype=np.uint64)
         H.check(L.halo_ipa_end(s, H.ptr(U), H.ptr(c0)))
@@ -45,3 +47,4 @@ for lg in [int(x) for x in (sys.argv[1:] or ['16', '20'])]:
         H.check(L.halo_profile_enable(0))
         print(f"open 2^{lg}: total {1e3*(t1-t0):.2f} ms (L/R rounds {1e3*t_lr:.2f} ms, folds {1e3*t_fold:.2f} ms; "
               f"fold kernels {ms.value:.2f} ms over {nl.value})", flush=True)
+        print("  per round (lr ms, fold ms):", per, flush=True)

@@ -1,0 +1,21 @@
+"""Times the device-resident naive_prover pipeline (halo_amd.prover) at n = 2^logn on one GPU."""
+import json, sys, time
+sys.path.insert(0, '/root/repo')
+from halo_amd import _lib as H
+from halo_amd import prover
+H.ensure_device(0)
+L = H.load()
+for arg in (sys.argv[1:] or ['16', '20']):
+    logn = int(arg)
+    n = 1 << logn
+    for curve in ('pallas',):
+        cid = H.CURVES[curve]
+        H.check(L.halo_srs_synthesize(cid, n, 99))
+        H.check(L.halo_srs_precompute_windows(cid))
+        B = prover.DeviceBackend(curve)
+        wit = prover.synthetic_witness(B, n, seed=1)
+        B.sync()
+        for rep in range(2):
+            out = prover.naive_prover(B, wit, n, prover.Challenges(B.m))
+            print(json.dumps({"logn": logn, "curve": curve, "rep": rep,
+                              "times_ms": {k: round(v * 1e3, 2) for k, v in out["times"].items()}}), flush=True)
