@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--dist-ntt-logn", type=int, default=24, help="distributed single NTT size (N > 1 only; 0 = off)")
     ap.add_argument("--ipa", type=int, default=1, help="measure the 2^logn IPA opening (extra.ipa_open)")
     ap.add_argument("--dist-ipa", type=int, default=1, help="N > 1: the sharded 2^logn opening (extra.dist_ipa)")
+    ap.add_argument("--prove", type=int, default=20, help="log2 n of the naive_prover pipeline (extra.prove; 0 = off)")
+    ap.add_argument("--prove-cpu", type=int, default=16, help="log2 n of the prover's CPU-baseline comparison")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal only: every rank on cuda:0 over gloo (multi-rank runs on a one-GPU box)")
     return ap.parse_args()
@@ -203,6 +205,27 @@ def main():
         }
 
     ipa = measure_ipa(args.logn) if args.ipa else None
+
+    # ---- BASELINE configs[3]: the naive_prover hot path (halo_amd.prover, protocol.rs:64-330) on the
+    # device at n = 2^prove_logn, and at 2^prove_cpu_logn beside the C restatement of the same
+    # pipeline on the host cores (bit-exact check of every commitment, evaluation and opening)
+    def measure_prove(logn, reps=2):
+        from halo_amd import prover
+        n_ = 1 << logn
+        H.check(L.halo_srs_synthesize(curve, n_, 0x505256 + logn))
+        H.check(L.halo_srs_precompute_windows(curve))
+        B = prover.DeviceBackend(args.curve)
+        wit = prover.synthetic_witness(B, n_, seed=1)
+        B.sync()
+        best = None
+        for _ in range(reps):
+            out = prover.naive_prover(B, wit, n_, prover.Challenges(B.m))
+            if best is None or out["times"]["total"] < best["times"]["total"]:
+                best = out
+        del wit
+        torch.cuda.empty_cache()
+        return best
+
 
     # ---- NTT + iNTT pairs (configs[2] at 2^22, and the other BASELINE sizes); rank-local, under extra
     def measure_ntt(logn, nrep=10):
@@ -417,6 +440,22 @@ def main():
         cpu_ntt = cpu_ntt_baseline(L, H, args.ntt_logn, sp, ntt_main)
         cpu_fold = cpu_fold_baseline(L, H, curve, 13, ipa)
 
+    # after the MSM CPU leg (which reads the MSM's resident SRS back)
+    prove = None
+    if args.prove and world == 1:
+        main_out = measure_prove(args.prove)
+        prove = {
+            "workload": f"naive_prover hot path at n = 2^{args.prove} (BASELINE.json configs[3]): 17 iNTT(n) + "
+                        f"42 NTT(8n), 33 commits, 14 + 3 FFT products, gate constraints over 8n, quotient, "
+                        f"3 IPA openings, 91 evaluations; synthetic witness, stand-in transcript",
+            "n": 1 << args.prove,
+            "ms": {k: v * 1e3 for k, v in main_out["times"].items()},
+        }
+        if not args.no_cpu and args.prove_cpu:
+            small = measure_prove(args.prove_cpu)
+            prove["at_cpu_size"] = {"n": 1 << args.prove_cpu, "gpu_ms": {k: v * 1e3 for k, v in small["times"].items()}}
+            prove["cpu"] = cpu_prove_baseline(L, H, curve, args.curve, args.prove_cpu, small)
+
     madds = n * (-(-255 // window_bits)) if window_bits else 0  # one mixed addition per nonzero digit
     valu_achieved = madds * 10 / (acc_avg_ms * 1e-3) if acc_avg_ms > 0 else 0.0
 
@@ -473,6 +512,7 @@ def main():
             "ipa_open": ipa,
             "evals_op": evals,
             "cpu_ntt": cpu_ntt,
+            "prove": prove,
             "cpu_ipa_fold": cpu_fold,
         },
     }
@@ -549,6 +589,43 @@ def cpu_ntt_baseline(L, H, logn, sp, gpu_ntt):
         "sample": f"1 x NTT + iNTT at 2^{logn} (C restatement of ark-poly 0.5 radix-2 DIF/DIT + derange, OpenMP)",
         "gpu_matches_cpu": bool(np.array_equal(y, y_gpu)) and bool(np.array_equal(z, x)),
         "gpu_over_cpu": (dt * 1e3) / gpu_ntt["pair_ms"] if gpu_ntt else None,
+    }
+
+
+def cpu_prove_baseline(L, H, curve, cname, logn, gpu_out):
+    """Rank 0, N=1 only: the same naive_prover pipeline on the C restatement backend
+    (oracle/prover_ref.py CRefBackend over oracle.c, OpenMP) with the SRS the GPU run used; every
+    commitment, evaluation and opening is compared with the GPU proof."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import prover_ref  # noqa: E402  (oracle: only the cpu_baseline legs may load it)
+
+    from halo_amd import prover
+
+    n = 1 << logn
+    srs = np.zeros((n, 8), dtype=np.uint64)
+    H.check(L.halo_srs_read(curve, 0, n, H.ptr(srs)))
+    threads = _cpu_threads()
+    B = prover_ref.CRefBackend(cname, srs, srs[1], threads=threads)
+    wit = prover.synthetic_witness(B, n, seed=1)
+    out = prover.naive_prover(B, wit, n, prover.Challenges(B.m))
+
+    def same(a, b):
+        return len(a) == len(b) and all(np.array_equal(x, y) for x, y in zip(a, b))
+
+    ok = same(out["C_ws"], gpu_out["C_ws"]) and np.array_equal(out["C_z"], gpu_out["C_z"]) \
+        and same(out["C_ts"], gpu_out["C_ts"]) and out["vs"] == gpu_out["vs"]
+    for k in ("q_r", "q_r_omega", "acc"):
+        a, b = out[k], gpu_out[k]
+        ok = ok and np.array_equal(a["C"], b["C"]) and a["v"] == b["v"] and same(a["Ls"], b["Ls"]) \
+            and same(a["Rs"], b["Rs"]) and np.array_equal(a["U"], b["U"]) and a["c"] == b["c"]
+    return {
+        "n": n,
+        "ms": {k: v * 1e3 for k, v in out["times"].items()},
+        "cores": threads,
+        "kind": "port",
+        "sample": f"1 x the naive_prover pipeline at 2^{logn} on the C restatement (ark-style NTT, Pippenger, "
+                  f"per-element fold and division) with OpenMP",
+        "gpu_matches_cpu": bool(ok),
     }
 
 

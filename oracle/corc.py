@@ -45,6 +45,9 @@ def lib():
         L.orc_msm_window_size.argtypes = [ctypes.c_size_t]
         L.orc_msm_window_size.restype = ctypes.c_int
         L.orc_max_threads.restype = ctypes.c_int
+        L.orc_evals_op.argtypes = [ctypes.c_int, ctypes.c_int, u64p, u64p, u64p, ctypes.c_uint32, ctypes.c_size_t,
+                                   u64p, ctypes.c_int]
+        L.orc_perm_acc.argtypes = [ctypes.c_int, u64p, u64p, ctypes.c_size_t, u64p]
         _lib = L
     return _lib
 
@@ -110,6 +113,25 @@ def ipa_fold(curve: str, gs: np.ndarray, cs: np.ndarray, zs: np.ndarray, xi: np.
     lib().orc_ipa_fold(CURVE_ID[curve], _p(gs), _p(cs), _p(zs), m, _p(np.ascontiguousarray(xi)),
                        _p(np.ascontiguousarray(xi_inv)), threads)
     return gs[:m], cs[:m], zs[:m]
+
+
+def evals_op(field: str, op: int, a: np.ndarray, b=None, s=None, e: int = 0, threads: int = 0) -> np.ndarray:
+    """Elementwise Evals op over Montgomery words (0 add, 1 sub, 2 mul, 3 scale, 4 add_scalar,
+    5 sub_scalar, 6 pow)."""
+    a = np.ascontiguousarray(a)
+    out = np.empty_like(a)
+    bp = _p(np.ascontiguousarray(b)) if b is not None else None
+    sp = _p(np.ascontiguousarray(s)) if s is not None else None
+    lib().orc_evals_op(FIELD_ID[field], op, _p(a), bp, sp, e, len(a), _p(out), threads)
+    return out
+
+
+def perm_acc(field: str, f: np.ndarray, g: np.ndarray) -> np.ndarray:
+    """z[0] = 1, z[i] = z[i-1] f[i] / g[i] (sequential; protocol.rs:143-154)."""
+    f, g = np.ascontiguousarray(f), np.ascontiguousarray(g)
+    out = np.empty_like(f)
+    lib().orc_perm_acc(FIELD_ID[field], _p(f), _p(g), len(f), _p(out))
+    return out
 
 
 def srs_generate(curve: str, n: int, threads: int = 0) -> np.ndarray:

@@ -565,3 +565,48 @@ void orc_srs_generate(int curve, size_t n, int threads, uint64_t *out) {
 }
 
 int orc_max_threads(void) { return omp_get_max_threads(); }
+
+/* ----------------------------------------------------------------------------- prover helpers
+ * Vectorised Evals ops for the CPU restatement of the prover pipeline (oracle/prover_ref.py,
+ * CRefBackend), on Montgomery words: op 0 a+b, 1 a-b, 2 a*b, 3 a*s, 4 a+s, 5 a-s, 6 a^e. */
+void orc_evals_op(int fid, int op, const uint64_t *a, const uint64_t *b, const uint64_t *s, uint32_t e, size_t n,
+                  uint64_t *out, int threads) {
+    const field_t *F = field_of(fid);
+    if (threads > 0) omp_set_num_threads(threads);
+    fe sv = f_zero();
+    if (s) memcpy(sv.l, s, 32);
+#pragma omp parallel for schedule(static)
+    for (size_t i = 0; i < n; i++) {
+        fe x, y, r;
+        memcpy(x.l, a + 4 * i, 32);
+        if (op <= 2) memcpy(y.l, b + 4 * i, 32);
+        switch (op) {
+            case 0: r = f_add(F, x, y); break;
+            case 1: r = f_sub(F, x, y); break;
+            case 2: r = f_mul(F, x, y); break;
+            case 3: r = f_mul(F, x, sv); break;
+            case 4: r = f_add(F, x, sv); break;
+            case 5: r = f_sub(F, x, sv); break;
+            default: /* x^e as e - 1 multiplications, like the reference's sbox closure w*w*...*w */
+                r = x;
+                for (uint32_t k = 1; k < e; k++) r = f_mul(F, r, x);
+                if (e == 0) r = f_one(F);
+        }
+        memcpy(out + 4 * i, r.l, 32);
+    }
+}
+
+/* z[0] = 1, z[i] = z[i-1] * f[i] / g[i] (protocol.rs:143-154, sequential, one inversion each) */
+void orc_perm_acc(int fid, const uint64_t *f, const uint64_t *g, size_t n, uint64_t *z) {
+    const field_t *F = field_of(fid);
+    fe acc = f_one(F);
+    for (size_t i = 0; i < n; i++) {
+        if (i) {
+            fe fi, gi;
+            memcpy(fi.l, f + 4 * i, 32);
+            memcpy(gi.l, g + 4 * i, 32);
+            acc = f_mul(F, f_mul(F, acc, fi), f_inv(F, gi));
+        }
+        memcpy(z + 4 * i, acc.l, 32);
+    }
+}

@@ -184,3 +184,210 @@ class RefBackend:
             xis.append(x)
         self.last_xis = xis
         return [Ls, Rs, self._w(gs[0]), cs[0]]
+
+
+# ---------------------------------------------------------------------------------------------
+# C-backed restatement (oracle.c through corc): the same pipeline at sizes the pure-Python backend
+# cannot reach -- the CPU side of bench.py's extra.prove (BASELINE configs[3]) and its bit-exact
+# check of the device pipeline at 2^12..2^16.  Vectors are (len, 4) uint64 Montgomery arrays.
+# ---------------------------------------------------------------------------------------------
+class CEvals:
+    __slots__ = ("B", "v")
+
+    def __init__(self, B, v):
+        self.B, self.v = B, v
+
+    def _bin(self, o, op_vec, op_s):
+        B = self.B
+        if isinstance(o, CEvals):
+            return CEvals(B, B.C.evals_op(B.fname, op_vec, self.v, o.v, threads=B.threads))
+        return CEvals(B, B.C.evals_op(B.fname, op_s, self.v, s=B.fe(int(o)), threads=B.threads))
+
+    def __add__(self, o):
+        return self._bin(o, 0, 4)
+
+    __radd__ = __add__
+
+    def __sub__(self, o):
+        return self._bin(o, 1, 5)
+
+    def __mul__(self, o):
+        return self._bin(o, 2, 3)
+
+    __rmul__ = __mul__
+
+
+class CRefBackend:
+    def __init__(self, curve: str, srs_wrapped: np.ndarray, h_wrapped: np.ndarray, threads: int = 0):
+        import corc
+
+        self.C = corc
+        self.curve = curve
+        self.c = P.CURVES[curve]
+        self.m = self.c.scalar
+        self.fname = "fp" if curve == "pallas" else "fq"
+        self.threads = threads
+        self.srs = np.ascontiguousarray(srs_wrapped)
+        self.H_point = P.wrapped_to_point(self.c, [int(x) for x in h_wrapped])
+        self.last_xis = []
+
+    def fe(self, x):
+        v = (x % self.m) * (1 << 256) % self.m
+        return np.array([(v >> (64 * i)) & (2**64 - 1) for i in range(4)], dtype=np.uint64)
+
+    def to_int(self, a):
+        return P.limbs_to_int([int(x) for x in a]) * pow(1 << 256, -1, self.m) % self.m
+
+    def sync(self):
+        pass
+
+    def random_vec(self, n, rng):
+        a = rng.integers(0, 2**63, size=(n, 4), dtype=np.uint64)
+        a[:, 3] &= np.uint64(0x0FFFFFFFFFFFFFFF)
+        return a
+
+    def sparse_vec(self, n, entries):
+        out = np.zeros((n, 4), dtype=np.uint64)
+        for i, x in entries.items():
+            out[i] = self.fe(x)
+        return out
+
+    def ones(self, n):
+        return CEvals(self, np.tile(self.fe(1), (n, 1)))
+
+    def length(self, p):
+        return len(p)
+
+    def omega(self, n):
+        return pow(5, (self.m - 1) // n, self.m)
+
+    def _add(self, a, b):
+        return self.C.evals_op(self.fname, 0, a, b, threads=self.threads)
+
+    def ntt(self, p, N):
+        v = p.v if isinstance(p, CEvals) else p
+        x = np.zeros((N, 4), dtype=np.uint64)
+        k = min(N, len(v))
+        x[:k] = v[:k]
+        for s in range(N, len(v), N):
+            j = min(N, len(v) - s)
+            x[:j] = self._add(x[:j], v[s:s + j])
+        return CEvals(self, self.C.ntt(self.fname, x, inverse=False, threads=self.threads))
+
+    def intt(self, e):
+        v = e.v if isinstance(e, CEvals) else e
+        return self.C.ntt(self.fname, v, inverse=True, threads=self.threads)
+
+    def shift_left(self, e, k):
+        if isinstance(e, CEvals):
+            return CEvals(self, np.roll(e.v, -k, axis=0))
+        return np.roll(e, -k, axis=0)
+
+    def shift_right(self, e, k):
+        if isinstance(e, CEvals):
+            return CEvals(self, np.roll(e.v, k, axis=0))
+        return np.roll(e, k, axis=0)
+
+    def sbox(self, x):
+        return CEvals(self, self.C.evals_op(self.fname, 6, x.v, e=7, threads=self.threads))
+
+    def poly_add(self, a, b, op=0):
+        n = max(len(a), len(b))
+        out = np.zeros((n, 4), dtype=np.uint64)
+        out[:len(a)] = a
+        out[:len(b)] = self.C.evals_op(self.fname, op, np.ascontiguousarray(out[:len(b)]), b, threads=self.threads)
+        return out
+
+    def poly_sub(self, a, b):
+        return self.poly_add(a, b, op=1)
+
+    def poly_scale(self, a, s):
+        return self.C.evals_op(self.fname, 3, a, s=self.fe(s), threads=self.threads)
+
+    def poly_add_const(self, a, s):
+        out = a.copy()
+        out[:1] = self.C.evals_op(self.fname, 4, a[:1], s=self.fe(s))
+        return out
+
+    def poly_mul(self, a, b):
+        rl = len(a) + len(b) - 1
+        N = 1 << (rl - 1).bit_length()
+        fa, fb = self.ntt(a, N), self.ntt(b, N)
+        return self.intt(self.C.evals_op(self.fname, 2, fa.v, fb.v, threads=self.threads))[:rl].copy()
+
+    def divide_by_vanishing(self, f, n):
+        L = len(f)
+        q = np.zeros((L - n, 4), dtype=np.uint64)
+        top = ((L - n - 1) // n) * n  # q[j] = f[j + n] + q[j + n], from the top chunk down
+        for c in range(top, -1, -n):
+            k = min(n, L - n - c)
+            nxt = np.zeros((k, 4), dtype=np.uint64)
+            if c + n < L - n:
+                j = min(k, L - n - c - n)
+                nxt[:j] = q[c + n:c + n + j]
+            q[c:c + k] = self._add(np.ascontiguousarray(f[c + n:c + n + k]), nxt)
+        return q
+
+    def resize(self, p, N):
+        out = np.zeros((N, 4), dtype=np.uint64)
+        out[:min(N, len(p))] = p[:min(N, len(p))]
+        return out
+
+    def split(self, p, n):
+        return [np.ascontiguousarray(p[i:i + n]) for i in range(0, len(p), n)]
+
+    def permutation_accumulator(self, f_ev, g_ev):
+        return CEvals(self, self.C.perm_acc(self.fname, f_ev.v, g_ev.v))
+
+    def commit_many(self, polys):
+        return [self.C.msm(self.curve, self.srs[:len(p)], p, threads=self.threads) for p in polys]
+
+    def eval_many(self, polys, z):
+        zf = self.fe(z)
+        return [self.to_int(self.C.poly_eval(self.fname, p, zf)) for p in polys]
+
+    def h_mul(self, k):
+        return P.mul(self.c, k, self.H_point)
+
+    def point_combine(self, points, scalars):
+        acc = P.INF
+        for w, k in zip(points, scalars):
+            acc = P.add(self.c, acc, P.mul(self.c, k, P.wrapped_to_point(self.c, [int(x) for x in w])))
+        return np.array(P.point_to_wrapped(self.c, acc), dtype=np.uint64)
+
+    def _doubling(self, factors):  # [1] -> products over the bits of the index (h(X), powers of z)
+        v = self.fe(1)[None, :].copy()
+        for f in factors:
+            v = np.concatenate([v, self.C.evals_op(self.fname, 3, v, s=self.fe(f), threads=self.threads)])
+        return v
+
+    def hpoly(self, xis_rows, alphas):
+        out = None
+        for row, a in zip(xis_rows, alphas):
+            lg = len(row) - 1
+            h = self._doubling([row[lg - b] for b in range(lg)])  # coef[k] = prod_{bit b of k} xi_{lg-b}
+            h = self.C.evals_op(self.fname, 3, h, s=self.fe(a), threads=self.threads)
+            out = h if out is None else self._add(out, h)
+        return out
+
+    def ipa(self, p, n, z, h_prime, chal):
+        cs = self.resize(p, n)
+        gs = self.srs[:n].copy()
+        lg = n.bit_length() - 1
+        zs = self._doubling([pow(z, 1 << i, self.m) for i in range(lg)])
+        Ls, Rs, xis = [], [], []
+        while len(gs) > 1:
+            m = len(gs) // 2
+            dl = self.to_int(self.C.scalar_dot(self.fname, cs[m:], zs[:m]))
+            dr = self.to_int(self.C.scalar_dot(self.fname, cs[:m], zs[m:]))
+            L = P.wrapped_to_point(self.c, [int(x) for x in self.C.msm(self.curve, gs[:m], cs[m:], threads=self.threads)])
+            R = P.wrapped_to_point(self.c, [int(x) for x in self.C.msm(self.curve, gs[m:], cs[:m], threads=self.threads)])
+            Ls.append(np.array(P.point_to_wrapped(self.c, P.add(self.c, L, P.mul(self.c, dl, h_prime))), dtype=np.uint64))
+            Rs.append(np.array(P.point_to_wrapped(self.c, P.add(self.c, R, P.mul(self.c, dr, h_prime))), dtype=np.uint64))
+            x = chal()
+            gs, cs, zs = self.C.ipa_fold(self.curve, gs, cs, zs, self.fe(x), self.fe(pow(x, -1, self.m)),
+                                         threads=self.threads)
+            gs, cs, zs = np.ascontiguousarray(gs), np.ascontiguousarray(cs), np.ascontiguousarray(zs)
+            xis.append(x)
+        self.last_xis = xis
+        return [Ls, Rs, gs[0].copy(), self.to_int(cs[0])]
