@@ -316,6 +316,149 @@ static int dot_device(int field, const void* x, const void* y, size_t n, void* o
     return HALO_OK;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Tail rounds of the opening (length <= IPA_TAIL_N): instead of folding G (one ~128-doubling scalar
+// multiplication per element per round, a ~1 ms dependent chain however few elements are left) the
+// session keeps G0 = G at the switch round and the fold weights w (G_j[i] = sum_u w[u] G0[i + u len],
+// fold: w' = interleave(w, xi w)).  L and R are then direct sums over G0 with expanded scalars
+//   k = j + u len:  s[k] = c[m + j] w[u] (j < m, -> L),  c[j - m] w[u] (j >= m, -> R),
+// evaluated from a table 2^(8 win) G0[k] (win < 32, built once): every (k, win) term is an 8-bit
+// double-and-add (~16 dependent curve operations), then block trees.  U = sum_u w[u] G0[u] at the end.
+// c and z keep their ordinary elementwise folds (pcdl.rs:430-435).
+constexpr size_t IPA_TAIL_N = 2048;
+constexpr int TAIL_WIN = 32, TAIL_THREADS = 256;
+
+template <class Cv>
+__global__ __launch_bounds__(64) void k_tail_table(const uint4* gs, size_t n0, uint4* table) {
+    using F = typename Cv::Base;
+    const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n0) return;
+    XYZZ<F> p = xyzz_from_aff(aff_load<F>(gs + 4 * k));
+    for (int w = 0; w < TAIL_WIN; w++) {
+        xyzz_store(table + 8 * ((size_t)w * n0 + k), p);
+        if (w + 1 < TAIL_WIN)
+            for (int b = 0; b < 8; b++) p = xyzz_dbl(p);
+    }
+}
+
+// mode 0: L/R scalars of the current round (len = 2m); mode 1: U's scalars s[k] = w[k]
+template <class Cv>
+__global__ __launch_bounds__(256) void k_tail_scalars(const uint4* cs, const uint4* w, size_t n0, size_t len, size_t m,
+                                                      int mode, uint32_t* scal, uint8_t* side) {
+    using S = typename Cv::Scalar;
+    const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n0) return;
+    Fe<S> v;
+    uint8_t sd = 0;
+    if (mode == 0) {
+        const size_t j = k % len, u = k / len;
+        const size_t ci = (j < m) ? m + j : j - m;
+        sd = (j < m) ? 0 : 1;
+        v = fe_mul(fe_from_ark<S>(cs + 2 * ci), fe_from_ark<S>(w + 2 * u));
+    } else {
+        v = fe_from_ark<S>(w + 2 * k);
+    }
+    Fe<S> one_raw = fe_zero<S>();  // internal (x 2^261) -> canonical: Montgomery product with 1
+    one_raw.v[0] = 1;
+    uint32_t w8[8];
+    fe_pack(fe_canon(fe_mul(v, one_raw)), w8);
+#pragma unroll
+    for (int q = 0; q < 8; q++) scal[8 * k + q] = w8[q];
+    side[k] = sd;
+}
+
+template <class F>
+HALO_DEV void tail_tree(uint4* red, int tid, XYZZ<F> v, uint4* out) {
+    xyzz_store(red + 8 * tid, v);
+    for (int off = TAIL_THREADS / 2; off > 0; off >>= 1) {
+        __syncthreads();
+        if (tid < off) xyzz_store(red + 8 * tid, xyzz_add(xyzz_load<F>(red + 8 * tid), xyzz_load<F>(red + 8 * (tid + off))));
+    }
+    __syncthreads();
+    if (tid == 0) xyzz_store(out, xyzz_load<F>(red));
+    __syncthreads();
+}
+
+// terms t = win * n0 + k; block partial sums part[block][side]
+template <class Cv>
+__global__ __launch_bounds__(TAIL_THREADS) void k_tail_msm(const uint4* table, const uint32_t* scal, const uint8_t* side,
+                                                            size_t n0, uint4* part) {
+    using F = typename Cv::Base;
+    __shared__ uint4 red[TAIL_THREADS * 8];
+    const int tid = threadIdx.x;
+    const size_t t = (size_t)blockIdx.x * TAIL_THREADS + tid;
+    XYZZ<F> acc = xyzz_id<F>();
+    int sd = 0;
+    if (t < (size_t)TAIL_WIN * n0) {
+        const size_t win = t / n0, k = t % n0;
+        const uint32_t d = (scal[8 * k + (win >> 2)] >> (8 * (win & 3))) & 255u;
+        sd = side[k];
+        if (d) {
+            const XYZZ<F> q = xyzz_load<F>(table + 8 * t);
+            const int top = 31 - __clz(d);
+            acc = q;
+            for (int b = top - 1; b >= 0; b--) {
+                acc = xyzz_dbl(acc);
+                if ((d >> b) & 1u) acc = xyzz_add(acc, q);
+            }
+        }
+    }
+    tail_tree<F>(red, tid, sd == 0 ? acc : xyzz_id<F>(), part + 8 * (2 * (size_t)blockIdx.x));
+    tail_tree<F>(red, tid, sd == 1 ? acc : xyzz_id<F>(), part + 8 * (2 * (size_t)blockIdx.x + 1));
+}
+
+// block b (0: L, 1: R): sum of the partials + dot_b * H' (from the 2^i H' table), -> WrappedPoint
+template <class Cv>
+__global__ __launch_bounds__(TAIL_THREADS) void k_tail_final(const uint4* part, int nblk, const uint4* htab,
+                                                              const uint4* dots_ark, uint4* out_wrapped) {
+    using F = typename Cv::Base;
+    using S = typename Cv::Scalar;
+    __shared__ uint4 red[TAIL_THREADS * 8];
+    __shared__ uint4 sum_s[8];
+    __shared__ uint32_t kw[8];
+    const int tid = threadIdx.x, b = blockIdx.x;
+    XYZZ<F> acc = xyzz_id<F>();
+    for (int i = tid; i < nblk; i += TAIL_THREADS) acc = xyzz_add(acc, xyzz_load<F>(part + 8 * (2 * (size_t)i + b)));
+    tail_tree<F>(red, tid, acc, sum_s);
+    XYZZ<F> hv = xyzz_id<F>();
+    if (htab) {
+        if (tid == 0) fe_ark_to_canonical_words<S>(dots_ark + 2 * b, kw);
+        __syncthreads();
+        if ((kw[tid >> 5] >> (tid & 31)) & 1u) hv = xyzz_from_aff(aff_load<F>(htab + 4 * tid));
+        tail_tree<F>(red, tid, hv, red + 8 * TAIL_THREADS - 8);  // slot read back below
+    }
+    if (tid == 0) {
+        XYZZ<F> r = xyzz_load<F>(sum_s);
+        if (htab) r = xyzz_add(r, xyzz_load<F>(red + 8 * TAIL_THREADS - 8));
+        aff_to_wrapped(out_wrapped + 4 * b, xyzz_to_aff(r));
+    }
+}
+
+template <class S>
+__global__ void k_set_one_ark(uint4* out) {
+    if (threadIdx.x == 0) fe_to_ark(out, fe_one<S>());
+}
+
+// c / z folds (pcdl.rs:430-435) and the weight update w' = interleave(w, xi w)
+template <class Cv>
+__global__ __launch_bounds__(256) void k_tail_fold(uint4* cs, uint4* zs, size_t m, const uint4* xi_ark,
+                                                   const uint4* xi_inv_ark, const uint4* w_in, uint4* w_out,
+                                                   size_t wlen) {
+    using S = typename Cv::Scalar;
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const Fe<S> xi = fe_from_ark<S>(xi_ark);
+    if (i < m) {
+        const Fe<S> xinv = fe_from_ark<S>(xi_inv_ark);
+        fe_to_ark(cs + 2 * i, fe_add(fe_from_ark<S>(cs + 2 * i), fe_mul(fe_from_ark<S>(cs + 2 * (i + m)), xinv)));
+        fe_to_ark(zs + 2 * i, fe_add(fe_from_ark<S>(zs + 2 * i), fe_mul(fe_from_ark<S>(zs + 2 * (i + m)), xi)));
+    }
+    if (i < wlen) {
+        const Fe<S> wv = fe_from_ark<S>(w_in + 2 * i);
+        fe_to_ark(w_out + 2 * (2 * i), wv);
+        fe_to_ark(w_out + 2 * (2 * i + 1), fe_mul(wv, xi));
+    }
+}
+
 }  // namespace halo
 
 using namespace halo;
@@ -325,6 +468,11 @@ struct halo_ipa_session {
     size_t n, m;
     DevBuf gs, cs, zs, htab, small, tmp;
     hipStream_t s;
+    // tail rounds (length <= IPA_TAIL_N, sessions over the SRS only): see k_tail_table
+    bool allow_tail = false, tail = false;
+    size_t n0 = 0, wlen = 0;
+    DevBuf table, w[2], scal, side, part;
+    int wcur = 0;
 };
 
 static int check_field_i(halo_field_t f) {
@@ -521,6 +669,10 @@ static int ipa_begin(halo_curve_t curve, size_t n, const halo_wrapped_point_t* g
     if (!gs_host && n > srs.n) return set_error(HALO_ESRSRANGE, "d (%zu) <= D (%zu)", n - 1, srs.n ? srs.n - 1 : 0);
     auto* ses = new halo_ipa_session();
     ses->curve = curve;
+    {
+        const char* e = getenv("HALO_IPA_TAIL");
+        ses->allow_tail = !gs_host && !(e && e[0] == '0');
+    }
     ses->n = n;
     ses->m = n / 2;
     ses->s = 0;
@@ -599,6 +751,49 @@ extern "C" int halo_ipa_begin_vectors(halo_curve_t curve, const halo_wrapped_poi
     return ipa_begin(curve, n, gs, cs, zs, nullptr, H_prime, out);
 }
 
+// Switch to the tail rounds: G0 = current G (length 2m), table 2^(8 win) G0, w = [1].
+static int ipa_enter_tail(halo_ipa_session* ses, hipStream_t s) {
+    const size_t n0 = 2 * ses->m;
+    const size_t nblk = (TAIL_WIN * n0 + TAIL_THREADS - 1) / TAIL_THREADS;
+    HALO_CHECK(ses->table.reserve((size_t)TAIL_WIN * n0 * 128));
+    HALO_CHECK(ses->w[0].reserve(n0 * 32));
+    HALO_CHECK(ses->w[1].reserve(n0 * 32));
+    HALO_CHECK(ses->scal.reserve(n0 * 32));
+    HALO_CHECK(ses->side.reserve(n0));
+    HALO_CHECK(ses->part.reserve(nblk * 2 * 128));
+    DISPATCH_CURVE(ses->curve, Cv, {
+        hipLaunchKernelGGL(k_tail_table<Cv>, dim3(gridn(n0, 64)), dim3(64), 0, s, ses->gs.as<const uint4>(), n0,
+                           ses->table.as<uint4>());
+        hipLaunchKernelGGL(k_set_one_ark<typename Cv::Scalar>, dim3(1), dim3(64), 0, s, ses->w[0].as<uint4>());
+    });
+    HALO_HIP(hipGetLastError());
+    ses->n0 = n0;
+    ses->wlen = 1;
+    ses->wcur = 0;
+    ses->tail = true;
+    return HALO_OK;
+}
+
+// mode 0: L, R of the current round -> small[256..384) (with the dot * H' terms from small[128..192));
+// mode 1: U = sum_u w[u] G0[u] -> small[256..320)
+static int ipa_tail_sums(halo_ipa_session* ses, int mode, hipStream_t s) {
+    const size_t n0 = ses->n0, m = ses->m;
+    const size_t nblk = (TAIL_WIN * n0 + TAIL_THREADS - 1) / TAIL_THREADS;
+    char* sm = (char*)ses->small.ptr;
+    DISPATCH_CURVE(ses->curve, Cv, {
+        hipLaunchKernelGGL(k_tail_scalars<Cv>, dim3(gridn(n0, 256)), dim3(256), 0, s, ses->cs.as<const uint4>(),
+                           ses->w[ses->wcur].as<const uint4>(), n0, 2 * m, m, mode, ses->scal.as<uint32_t>(),
+                           ses->side.as<uint8_t>());
+        hipLaunchKernelGGL(k_tail_msm<Cv>, dim3((unsigned)nblk), dim3(TAIL_THREADS), 0, s, ses->table.as<const uint4>(),
+                           ses->scal.as<const uint32_t>(), ses->side.as<const uint8_t>(), n0, ses->part.as<uint4>());
+        hipLaunchKernelGGL(k_tail_final<Cv>, dim3(mode == 0 ? 2 : 1), dim3(TAIL_THREADS), 0, s,
+                           ses->part.as<const uint4>(), (int)nblk, mode == 0 ? ses->htab.as<const uint4>() : nullptr,
+                           (const uint4*)(sm + 128), (uint4*)(sm + 256));
+    });
+    HALO_HIP(hipGetLastError());
+    return HALO_OK;
+}
+
 extern "C" int halo_ipa_round_lr(halo_ipa_session* ses, halo_wrapped_point_t* L, halo_wrapped_point_t* R) {
     clear_error();
     if (!ses || !L || !R) return set_error(HALO_EINVAL, "halo_ipa_round_lr: null argument");
@@ -613,8 +808,14 @@ extern "C" int halo_ipa_round_lr(halo_ipa_session* ses, halo_wrapped_point_t* L,
     const char* cs = ses->cs.as<const char>();
     const char* zs = ses->zs.as<const char>();
     const char* gs = ses->gs.as<const char>();
+    if (!ses->tail && ses->allow_tail && 2 * m <= IPA_TAIL_N) HALO_CHECK(ipa_enter_tail(ses, s));
     HALO_CHECK(dot_device(sf, cs + m * 32, zs, m, sm + 128, ses->tmp.ptr, s));        // <c_r, z_l>
     HALO_CHECK(dot_device(sf, cs, zs + m * 32, m, sm + 160, ses->tmp.ptr, s));        // <c_l, z_r>
+    if (ses->tail) {
+        HALO_CHECK(ipa_tail_sums(ses, 0, s));
+        HALO_CHECK(copy_d2h(L, sm + 256, 64, s));
+        return copy_d2h(R, sm + 320, 64, s);
+    }
     // L and R are independent: the second MSM's accumulation overlaps the first one's tail
     HALO_CHECK(msm_device(st, ses->curve, gs, cs + m * 32, m, ses->htab.ptr, sm + 128, sm + 256, s, true));   // L
     HALO_CHECK(msm_device(st, ses->curve, gs + m * 64, cs, m, ses->htab.ptr, sm + 160, sm + 320, s, true));   // R
@@ -636,6 +837,20 @@ extern "C" int halo_ipa_fold(halo_ipa_session* ses, const halo_fe_t* xi, const h
     HALO_CHECK(copy_h2d(sm + 384, xi, 32, s));
     HALO_CHECK(copy_h2d(sm + 416, xi_inv, 32, s));
     const size_t m = ses->m;
+    if (ses->tail) {
+        DISPATCH_CURVE(ses->curve, Cv, {
+            hipLaunchKernelGGL(k_tail_fold<Cv>, dim3(gridn(std::max(m, ses->wlen), 256)), dim3(256), 0, s,
+                               ses->cs.as<uint4>(), ses->zs.as<uint4>(), m, (const uint4*)(sm + 384),
+                               (const uint4*)(sm + 416), ses->w[ses->wcur].as<const uint4>(),
+                               ses->w[ses->wcur ^ 1].as<uint4>(), ses->wlen);
+        });
+        HALO_HIP(hipGetLastError());
+        HALO_HIP(hipStreamSynchronize(s));
+        ses->wcur ^= 1;
+        ses->wlen *= 2;
+        ses->m /= 2;
+        return HALO_OK;
+    }
     DISPATCH_CURVE(ses->curve, Cv, {
         ProfScope prof("ipa_fold", s);
         HALO_LAUNCH(prof, k_ipa_fold<Cv>, dim3(gridn(m, FOLD_THREADS)), dim3(FOLD_THREADS), 0, s, ses->gs.as<uint4>(), ses->cs.as<uint4>(),
@@ -656,6 +871,8 @@ extern "C" int halo_ipa_state(halo_ipa_session* ses, size_t* m, halo_wrapped_poi
     hipStream_t s = ses->s;
     const size_t len = std::max<size_t>(2 * ses->m, 1);
     if (m) *m = ses->m;
+    if (gs && ses->tail)
+        return set_error(HALO_EINVAL, "halo_ipa_state: G is not materialised in the tail rounds (HALO_IPA_TAIL=0)");
     if (gs) {
         HALO_CHECK(ses->tmp.reserve(std::max<size_t>(len * 64, 4096 * 32)));
         HALO_CHECK(convert_internal_to_wrapped(ses->curve, ses->gs.ptr, ses->tmp.ptr, len, s));
@@ -679,11 +896,17 @@ extern "C" int halo_ipa_end(halo_ipa_session* ses, halo_wrapped_point_t* U, halo
         std::lock_guard<std::mutex> g(st->mu);
         hipStream_t s = ses->s;
         char* sm = (char*)ses->small.ptr;
-        DISPATCH_CURVE(ses->curve, Cv, {
-            hipLaunchKernelGGL(k_copy_first_wrapped<Cv>, dim3(1), dim3(64), 0, s, ses->gs.as<const uint4>(),
-                               ses->cs.as<const uint4>(), (uint4*)(sm + 256), (uint4*)(sm + 320));
-        });
-        if (hipGetLastError() != hipSuccess) rc = set_error(HALO_EDEVICE, "ipa end launch failed");
+        if (ses->tail) {
+            rc = ipa_tail_sums(ses, 1, s);
+            if (!rc && hipMemcpyAsync(sm + 320, ses->cs.ptr, 32, hipMemcpyDeviceToDevice, s) != hipSuccess)
+                rc = set_error(HALO_EDEVICE, "ipa end copy failed");
+        } else {
+            DISPATCH_CURVE(ses->curve, Cv, {
+                hipLaunchKernelGGL(k_copy_first_wrapped<Cv>, dim3(1), dim3(64), 0, s, ses->gs.as<const uint4>(),
+                                   ses->cs.as<const uint4>(), (uint4*)(sm + 256), (uint4*)(sm + 320));
+            });
+            if (hipGetLastError() != hipSuccess) rc = set_error(HALO_EDEVICE, "ipa end launch failed");
+        }
         if (!rc && U) rc = copy_d2h(U, sm + 256, 64, s);
         if (!rc && c) rc = copy_d2h(c, sm + 320, 32, s);
     }
