@@ -71,3 +71,28 @@ def test_permutation_accumulator_scan_large(hal):
         if i in checks:
             assert dev.to_int(z[i]) == num * pow(den, -1, m) % m, i
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("logn", [12, 13])
+def test_ipa_open_tail_switch_vs_c_restatement(hal, logn):
+    """An SRS-based opening longer than the tail threshold (2048): ordinary rounds (MSM L/R + GLV
+    fold) switch to the tail rounds (direct sums over G0 with fold weights) mid-opening; Ls, Rs, U, c
+    against the C restatement of pcdl.rs:404-438."""
+    from prover_ref import CRefBackend
+
+    n = 1 << logn
+    L = hal.load()
+    hal.check(L.halo_srs_synthesize(0, n, 777 + logn))
+    srs = np.zeros((n, 8), dtype=np.uint64)
+    hal.check(L.halo_srs_read(0, 0, n, hal.ptr(srs)))
+    dev = prover.DeviceBackend("pallas")
+    ref = CRefBackend("pallas", srs, srs[1])
+    rng = np.random.default_rng(logn)
+    p_dev = dev.random_vec(n, rng)
+    p_ref = p_dev.cpu().numpy().view(np.uint64).copy()
+    z, xi0 = 0x1234567, 0xABCDEF
+    a = dev.ipa(p_dev, n, z, dev.h_mul(xi0), prover.Challenges(dev.m, seed=5))
+    b = ref.ipa(p_ref, n, z, ref.h_mul(xi0), prover.Challenges(ref.m, seed=5))
+    assert all(np.array_equal(x, y) for x, y in zip(a[0], b[0]))
+    assert all(np.array_equal(x, y) for x, y in zip(a[1], b[1]))
+    assert np.array_equal(a[2], b[2]) and a[3] == b[3]
