@@ -470,6 +470,7 @@ struct halo_ipa_session {
     hipStream_t s;
     // tail rounds (length <= IPA_TAIL_N, sessions over the SRS only): see k_tail_table
     bool allow_tail = false, tail = false;
+    bool srs_round0 = false;  // G is still the SRS prefix (no fold yet): L/R on the resident shifted SRS
     size_t n0 = 0, wlen = 0;
     DevBuf table, w[2], scal, side, part;
     int wcur = 0;
@@ -672,6 +673,7 @@ static int ipa_begin(halo_curve_t curve, size_t n, const halo_wrapped_point_t* g
     {
         const char* e = getenv("HALO_IPA_TAIL");
         ses->allow_tail = !gs_host && !(e && e[0] == '0');
+        ses->srs_round0 = !gs_host && srs.shifted_c != 0;
     }
     ses->n = n;
     ses->m = n / 2;
@@ -808,7 +810,11 @@ extern "C" int halo_ipa_round_lr(halo_ipa_session* ses, halo_wrapped_point_t* L,
     const char* cs = ses->cs.as<const char>();
     const char* zs = ses->zs.as<const char>();
     const char* gs = ses->gs.as<const char>();
-    if (!ses->tail && ses->allow_tail && 2 * m <= IPA_TAIL_N) HALO_CHECK(ipa_enter_tail(ses, s));
+    static const size_t tail_n = [] {
+        const char* e = getenv("HALO_IPA_TAIL_N");  // A/B knob; default IPA_TAIL_N
+        return e ? (size_t)atoll(e) : IPA_TAIL_N;
+    }();
+    if (!ses->tail && ses->allow_tail && 2 * m <= tail_n) HALO_CHECK(ipa_enter_tail(ses, s));
     HALO_CHECK(dot_device(sf, cs + m * 32, zs, m, sm + 128, ses->tmp.ptr, s));        // <c_r, z_l>
     HALO_CHECK(dot_device(sf, cs, zs + m * 32, m, sm + 160, ses->tmp.ptr, s));        // <c_l, z_r>
     if (ses->tail) {
@@ -817,8 +823,13 @@ extern "C" int halo_ipa_round_lr(halo_ipa_session* ses, halo_wrapped_point_t* L,
         return copy_d2h(R, sm + 320, 64, s);
     }
     // L and R are independent: the second MSM's accumulation overlaps the first one's tail
-    HALO_CHECK(msm_device(st, ses->curve, gs, cs + m * 32, m, ses->htab.ptr, sm + 128, sm + 256, s, true));   // L
-    HALO_CHECK(msm_device(st, ses->curve, gs + m * 64, cs, m, ses->htab.ptr, sm + 160, sm + 320, s, true));   // R
+    if (ses->srs_round0) {  // G_l = SRS[0, m), G_r = SRS[m, 2m): resident window-shifted copies, no Horner
+        HALO_CHECK(msm_srs_range_device(st, ses->curve, 0, cs + m * 32, m, ses->htab.ptr, sm + 128, sm + 256, s, true));
+        HALO_CHECK(msm_srs_range_device(st, ses->curve, m, cs, m, ses->htab.ptr, sm + 160, sm + 320, s, true));
+    } else {
+        HALO_CHECK(msm_device(st, ses->curve, gs, cs + m * 32, m, ses->htab.ptr, sm + 128, sm + 256, s, true));   // L
+        HALO_CHECK(msm_device(st, ses->curve, gs + m * 64, cs, m, ses->htab.ptr, sm + 160, sm + 320, s, true));   // R
+    }
     HALO_CHECK(msm_join(st, s));
     HALO_CHECK(copy_d2h(L, sm + 256, 64, s));
     HALO_CHECK(copy_d2h(R, sm + 320, 64, s));
@@ -837,6 +848,7 @@ extern "C" int halo_ipa_fold(halo_ipa_session* ses, const halo_fe_t* xi, const h
     HALO_CHECK(copy_h2d(sm + 384, xi, 32, s));
     HALO_CHECK(copy_h2d(sm + 416, xi_inv, 32, s));
     const size_t m = ses->m;
+    ses->srs_round0 = false;
     if (ses->tail) {
         DISPATCH_CURVE(ses->curve, Cv, {
             hipLaunchKernelGGL(k_tail_fold<Cv>, dim3(gridn(std::max(m, ses->wlen), 256)), dim3(256), 0, s,

@@ -528,6 +528,22 @@ int msm_srs_device(DeviceState* st, int curve, const void* scalars_ark, size_t n
     return rc;
 }
 
+int msm_srs_range_device(DeviceState* st, int curve, size_t offset, const void* scalars_ark, size_t n,
+                         const void* hide_table, const void* hide_scalar, void* d_out_wrapped, hipStream_t s,
+                         bool async) {
+    SrsState& srs = st->srs[curve];
+    if (!srs.shifted_c) return set_error(HALO_EINVAL, "msm_srs_range_device: no window-shifted SRS");
+    if (offset + n > srs.n) return set_error(HALO_ESRSRANGE, "range [%zu, %zu) exceeds the SRS (%zu)", offset, offset + n, srs.n);
+    int rc;
+    // window w of point offset + i lives at shifted[w * srs.n + offset + i]: shift the base pointer
+    DISPATCH_CURVE(curve, Cv, {
+        rc = msm_device_t<Cv>(st, srs.shifted.as<const uint4>() + 4 * offset, true, srs.n, (const uint4*)scalars_ark, n,
+                              srs.shifted_c, (const uint4*)hide_table, (const uint4*)hide_scalar,
+                              (uint4*)d_out_wrapped, s, async);
+    });
+    return rc;
+}
+
 int convert_wrapped_to_internal(int curve, const void* in, void* out, size_t n, hipStream_t s) {
     if (!n) return HALO_OK;
     DISPATCH_CURVE(curve, Cv, {

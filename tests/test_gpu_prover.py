@@ -73,8 +73,8 @@ def test_permutation_accumulator_scan_large(hal):
     torch.cuda.synchronize()
 
 
-@pytest.mark.parametrize("logn", [12, 13])
-def test_ipa_open_tail_switch_vs_c_restatement(hal, logn):
+@pytest.mark.parametrize("logn,windows", [(12, False), (13, False), (13, True)])
+def test_ipa_open_tail_switch_vs_c_restatement(hal, logn, windows):
     """An SRS-based opening longer than the tail threshold (2048): ordinary rounds (MSM L/R + GLV
     fold) switch to the tail rounds (direct sums over G0 with fold weights) mid-opening; Ls, Rs, U, c
     against the C restatement of pcdl.rs:404-438."""
@@ -83,6 +83,8 @@ def test_ipa_open_tail_switch_vs_c_restatement(hal, logn):
     n = 1 << logn
     L = hal.load()
     hal.check(L.halo_srs_synthesize(0, n, 777 + logn))
+    if windows:  # round 1's L / R then run on the resident window-shifted SRS (SRS ranges [0, m), [m, 2m))
+        hal.check(L.halo_srs_precompute_windows(0))
     srs = np.zeros((n, 8), dtype=np.uint64)
     hal.check(L.halo_srs_read(0, 0, n, hal.ptr(srs)))
     dev = prover.DeviceBackend("pallas")

@@ -17,6 +17,7 @@ def fe1(v):
 for lg in [int(x) for x in (sys.argv[1:] or ['16', '20'])]:
     n = 1 << lg
     H.check(L.halo_srs_synthesize(0, n, 77))
+    H.check(L.halo_srs_precompute_windows(0))  # as bench.py: round 1 L/R on the shifted SRS
     rnd = random.Random(lg)
     cs = np.array([[rnd.getrandbits(62) for _ in range(4)] for _ in range(n)], dtype=np.uint64)
     z = fe1(12345)
