@@ -144,6 +144,176 @@ __global__ __launch_bounds__(256) void k_scan_apply(uint4* out, size_t n, int re
     fe_to_ark(out + 2 * j, fe_mul(fe_from_ark<F>(out + 2 * j), t));
 }
 
+// ---------------------------------------------------------------------------------------------
+// Fused gate-constraint evaluation over the 8n domain (protocol.rs:170-191 with the constraint
+// polynomials of protocol.rs:591-1011, written from their *_generic forms): one pass reads the 16
+// w, 3 shifted w (w_omega = w shifted by the domain ratio), 15 r, 10 q and the public-input
+// evaluations of element i and writes f_gc[i] -- instead of ~250 separate Evals kernels, each a
+// full read/write of 256 MiB at n = 2^20.  Internal Montgomery form inside.
+// ---------------------------------------------------------------------------------------------
+struct GateArgs {
+    const uint4* w[16];
+    const uint4* r[15];
+    const uint4* q[10];
+    const uint4* pi;
+    uint4 mds[9][2];  // ark words of the Poseidon MDS matrix (row-major)
+};
+
+template <class F>
+HALO_DEV Fe<F> fe_from_ark_words(const uint4 (&a)[2]) {
+    return fe_mul(fe_load<F>(a), fe_from_const<F>(F::ARK2INT));
+}
+
+template <class F>
+HALO_DEV Fe<F> pow7(const Fe<F>& x) {
+    const Fe<F> x2 = fe_sqr(x), x3 = fe_mul(x2, x), x6 = fe_sqr(x3);
+    return fe_mul(x6, x);
+}
+
+// Three passes keep the live register set of each kernel small (one fused kernel needed 512 VGPRs and
+// spilled): poseidon -> t0; q6 aa + q7 am + q8 eq -> t1; then the range check and the f_gc sum.
+#define GATE_PROLOGUE                                                        \
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;         \
+    if (i >= N) return;                                                      \
+    const size_t in = (i + shift) & (N - 1);                                 \
+    auto W = [&](int k) { return fe_from_ark<F>(a.w[k] + 2 * i); };          \
+    auto NW = [&](int k) { return fe_from_ark<F>(a.w[k] + 2 * in); };        \
+    auto R = [&](int k) { return fe_from_ark<F>(a.r[k] + 2 * i); };          \
+    auto Q = [&](int k) { return fe_from_ark<F>(a.q[k] + 2 * i); };          \
+    const Fe<F> one = fe_one<F>();                                           \
+    (void)NW; (void)R; (void)Q; (void)one;
+
+// poseidon_constraints_generic (protocol.rs:623-648) -> t (internal packed)
+template <class F>
+__global__ __launch_bounds__(256) void k_gate_poseidon(const GateArgs a, size_t N, uint32_t shift, uint4* t) {
+    GATE_PROLOGUE
+    Fe<F> pos = fe_zero<F>();
+#pragma unroll 1
+    for (int rd = 0; rd < 5; rd++) {
+        const int b = 3 * rd;
+        const Fe<F> s0 = pow7(W(b)), s1 = pow7(W(b + 1)), s2 = pow7(W(b + 2));
+#pragma unroll 1
+        for (int row = 0; row < 3; row++) {
+            const Fe<F> nxt = (rd < 4) ? W(b + 3 + row) : NW(row);
+            Fe<F> u = fe_add(R(b + row), fe_mul(s0, fe_from_ark_words<F>(a.mds[3 * row + 0])));
+            u = fe_add(u, fe_mul(s1, fe_from_ark_words<F>(a.mds[3 * row + 1])));
+            u = fe_add(u, fe_mul(s2, fe_from_ark_words<F>(a.mds[3 * row + 2])));
+            pos = fe_add(pos, fe_sub(nxt, u));
+        }
+    }
+    fe_store(t + 2 * i, pos);
+}
+
+// q6 * affine_add + q7 * affine_mul + q8 * eq  -> t (internal packed)
+template <class F>
+__global__ __launch_bounds__(256) void k_gate_affine(const GateArgs a, size_t N, uint32_t shift, uint4* t) {
+    GATE_PROLOGUE
+    // affine_add_constraints_generic (protocol.rs:705-761)
+    Fe<F> aa;
+    {
+        const Fe<F> xp = W(0), yp = W(1), xq = W(2), yq = W(3), xr = W(4), yr = W(5);
+        const Fe<F> al = W(6), be = W(7), ga = W(8), de = W(9), lam = W(10);
+        const Fe<F> xq_xp = fe_sub(xq, xp), yq_yp = fe_sub(yq, yp);
+        aa = fe_mul(xq_xp, fe_sub(fe_mul(xq_xp, lam), yq_yp));
+        const Fe<F> yp2 = fe_add(yp, yp), xpxp = fe_mul(xp, xp);
+        const Fe<F> xpxp3 = fe_add(fe_add(xpxp, xpxp), xpxp);
+        aa = fe_add(aa, fe_mul(fe_sub(one, fe_mul(xq_xp, al)), fe_sub(fe_mul(yp2, lam), xpxp3)));
+        const Fe<F> xpxq = fe_mul(xp, xq), xpxq_d = fe_mul(xpxq, fe_sub(xq, xp));
+        const Fe<F> ll_x = fe_sub(fe_sub(fe_sub(fe_mul(lam, lam), xp), xq), xr);
+        aa = fe_add(aa, fe_mul(xpxq_d, ll_x));
+        const Fe<F> l_y = fe_sub(fe_sub(fe_mul(lam, fe_sub(xp, xr)), yp), yr);
+        aa = fe_add(aa, fe_mul(xpxq_d, l_y));
+        const Fe<F> xpxq_s = fe_mul(xpxq, fe_add(yq, yp));
+        aa = fe_add(aa, fe_mul(xpxq_s, ll_x));
+        aa = fe_add(aa, fe_mul(xpxq_s, l_y));
+        const Fe<F> l_xpb = fe_sub(one, fe_mul(xp, be));
+        aa = fe_add(aa, fe_mul(l_xpb, fe_sub(xr, xq)));
+        aa = fe_add(aa, fe_mul(l_xpb, fe_sub(yr, yq)));
+        const Fe<F> l_xqg = fe_sub(one, fe_mul(xq, ga));
+        aa = fe_add(aa, fe_mul(l_xqg, fe_sub(xr, xp)));
+        aa = fe_add(aa, fe_mul(l_xqg, fe_sub(yr, yp)));
+        const Fe<F> l_ad = fe_sub(fe_sub(one, fe_mul(fe_sub(xq, xp), al)), fe_mul(fe_add(yq, yp), de));
+        aa = fe_add(aa, fe_mul(l_ad, xr));
+        aa = fe_add(aa, fe_mul(l_ad, yr));
+    }
+
+    // affine_mul_constraints_generic (protocol.rs:851-937), two_pow_i = r[0]
+    Fe<F> am;
+    {
+        const Fe<F> xp = W(0), yp = W(1), av = W(2), xg = W(3), yg = W(4), bv = W(5), xq = W(6), yq = W(7);
+        const Fe<F> xr = W(8), yr = W(9), bq = W(10), lq = W(11), ar = W(12), gr = W(13), dr = W(14), lr = W(15);
+        const Fe<F> xpxp = fe_mul(xp, xp), xp2 = fe_add(xp, xp), llq = fe_mul(lq, lq);
+        const Fe<F> xpxp3 = fe_add(fe_add(xpxp, xpxp), xpxp), yp2 = fe_add(yp, yp);
+        const Fe<F> l_xpb = fe_sub(one, fe_mul(xp, bq));
+        am = fe_mul(l_xpb, xq);
+        am = fe_add(am, fe_mul(l_xpb, yq));
+        am = fe_add(am, fe_sub(fe_mul(yp2, lq), xpxp3));
+        am = fe_add(am, fe_sub(fe_sub(llq, xp2), xq));
+        am = fe_add(am, fe_sub(fe_sub(fe_mul(lq, fe_sub(xp, xq)), yp), yq));
+        const Fe<F> xg_xq = fe_sub(xg, xq), yg_yq = fe_sub(yg, yq);
+        am = fe_add(am, fe_mul(xg_xq, fe_sub(fe_mul(xg_xq, lr), yg_yq)));
+        const Fe<F> yq2 = fe_add(yq, yq), xqxq = fe_mul(xq, xq);
+        const Fe<F> xqxq3 = fe_add(fe_add(xqxq, xqxq), xqxq);
+        am = fe_add(am, fe_mul(fe_sub(one, fe_mul(xg_xq, ar)), fe_sub(fe_mul(yq2, lr), xqxq3)));
+        const Fe<F> xqxg = fe_mul(xq, xg), xqxg_d = fe_mul(xqxg, fe_sub(xg, xq));
+        const Fe<F> ll_x = fe_sub(fe_sub(fe_sub(fe_mul(lr, lr), xq), xg), xr);
+        am = fe_add(am, fe_mul(xqxg_d, ll_x));
+        const Fe<F> l_y = fe_sub(fe_sub(fe_mul(lr, fe_sub(xq, xr)), yq), yr);
+        am = fe_add(am, fe_mul(xqxg_d, l_y));
+        const Fe<F> xqxg_s = fe_mul(xqxg, fe_add(yg, yq));
+        am = fe_add(am, fe_mul(xqxg_s, ll_x));
+        am = fe_add(am, fe_mul(xqxg_s, l_y));
+        am = fe_add(am, fe_mul(l_xpb, fe_sub(xr, xg)));
+        am = fe_add(am, fe_mul(l_xpb, fe_sub(yr, yg)));
+        const Fe<F> l_xgg = fe_sub(one, fe_mul(xg, gr));
+        am = fe_add(am, fe_mul(l_xgg, fe_sub(xr, xq)));
+        am = fe_add(am, fe_mul(l_xgg, fe_sub(yr, yq)));
+        const Fe<F> l_ad = fe_sub(fe_sub(one, fe_mul(fe_sub(xg, xq), ar)), fe_mul(fe_add(yg, yq), dr));
+        am = fe_add(am, fe_mul(l_ad, xr));
+        am = fe_add(am, fe_mul(l_ad, yr));
+        am = fe_add(am, fe_mul(bv, fe_sub(bv, one)));
+        const Fe<F> one_b = fe_sub(one, bv);
+        am = fe_add(am, fe_sub(NW(0), fe_add(fe_mul(bv, xr), fe_mul(one_b, xq))));
+        am = fe_add(am, fe_sub(NW(1), fe_add(fe_mul(bv, yr), fe_mul(one_b, yq))));
+        am = fe_sub(fe_add(am, NW(2)), fe_add(av, fe_mul(bv, R(0))));
+    }
+
+    // eq_generic (protocol.rs:1001-1011)
+    Fe<F> eq;
+    {
+        const Fe<F> ab = fe_sub(W(0), W(1)), e = W(3);
+        eq = fe_add(fe_mul(ab, e), fe_sub(fe_add(fe_mul(ab, W(4)), e), W(2)));
+    }
+
+    Fe<F> acc = fe_mul(Q(6), aa);
+    acc = fe_add(acc, fe_mul(Q(7), am));
+    acc = fe_add(acc, fe_mul(Q(8), eq));
+    fe_store(t + 2 * i, acc);
+}
+
+// range check and f_gc (protocol.rs:179-190) with the two partial vectors
+template <class F>
+__global__ __launch_bounds__(256) void k_gate_final(const GateArgs a, size_t N, uint32_t shift, const uint4* t0,
+                                                    const uint4* t1, uint4* out) {
+    GATE_PROLOGUE
+    // range_check_generic (protocol.rs:966-990)
+    Fe<F> rc = fe_sub(NW(0), W(0));
+    for (int k = 0; k < 15; k++) rc = fe_sub(rc, fe_mul(W(1 + k), R(k)));
+
+    // f_gc (protocol.rs:179-190)
+    const Fe<F> w0 = W(0), w1 = W(1);
+    Fe<F> f = fe_mul(w0, Q(0));
+    f = fe_add(f, fe_mul(Q(1), w1));
+    f = fe_add(f, fe_mul(Q(2), W(2)));
+    f = fe_add(f, fe_mul(fe_mul(Q(3), w0), w1));
+    f = fe_add(f, Q(4));
+    f = fe_add(f, fe_mul(Q(5), fe_load<F>(t0 + 2 * i)));
+    f = fe_add(f, fe_load<F>(t1 + 2 * i));
+    f = fe_add(f, fe_mul(Q(9), rc));
+    f = fe_add(f, fe_from_ark<F>(a.pi + 2 * i));
+    fe_to_ark(out + 2 * i, f);
+}
+
 template <class F>
 static Fe<F> host_fe_raw(const uint32_t (&k)[NLIMB]) {
     Fe<F> r;
@@ -304,6 +474,46 @@ extern "C" int halo_divide_by_vanishing_dev(halo_field_t field, const void* d_co
         hipLaunchKernelGGL(k_div_vanishing<F>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
                            (hipStream_t)stream, (const uint4*)d_coeffs, len, n, (uint4*)d_quotient,
                            (uint4*)d_remainder);
+    });
+    HALO_HIP(hipGetLastError());
+    return HALO_OK;
+}
+
+extern "C" int halo_gate_constraints_dev(halo_field_t field, const void* const* d_w, const void* const* d_r,
+                                         const void* const* d_q, const void* d_pi, const halo_fe_t* mds, size_t n,
+                                         unsigned shift, void* d_out, void* stream) {
+    clear_error();
+    if (field != HALO_FP && field != HALO_FQ) return set_error(HALO_EINVAL, "unknown field id %d", (int)field);
+    if (!d_w || !d_r || !d_q || !d_pi || !mds || !d_out || !is_pow2(n))
+        return set_error(HALO_EINVAL, "halo_gate_constraints_dev: bad argument");
+    GateArgs a;
+    for (int k = 0; k < 16; k++) a.w[k] = (const uint4*)d_w[k];
+    for (int k = 0; k < 15; k++) a.r[k] = (const uint4*)d_r[k];
+    for (int k = 0; k < 10; k++) a.q[k] = (const uint4*)d_q[k];
+    a.pi = (const uint4*)d_pi;
+    for (int k = 0; k < 9; k++) {
+        a.mds[k][0] = make_uint4((uint32_t)mds[k].l[0], (uint32_t)(mds[k].l[0] >> 32), (uint32_t)mds[k].l[1],
+                                 (uint32_t)(mds[k].l[1] >> 32));
+        a.mds[k][1] = make_uint4((uint32_t)mds[k].l[2], (uint32_t)(mds[k].l[2] >> 32), (uint32_t)mds[k].l[3],
+                                 (uint32_t)(mds[k].l[3] >> 32));
+    }
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    DevBuf* tmp;
+    {
+        std::lock_guard<std::mutex> g(st->mu);
+        tmp = &st->gate_tmp;
+        HALO_CHECK(tmp->reserve(2 * n * 32));
+    }
+    uint4* t0 = tmp->as<uint4>();
+    uint4* t1 = t0 + 2 * n;
+    const dim3 grid((unsigned)((n + 255) / 256));
+    hipStream_t s = (hipStream_t)stream;
+    DISPATCH_FIELD(field, F, {
+        hipLaunchKernelGGL(k_gate_poseidon<F>, grid, dim3(256), 0, s, a, n, (uint32_t)shift, t0);
+        hipLaunchKernelGGL(k_gate_affine<F>, grid, dim3(256), 0, s, a, n, (uint32_t)shift, t1);
+        hipLaunchKernelGGL(k_gate_final<F>, grid, dim3(256), 0, s, a, n, (uint32_t)shift, (const uint4*)t0,
+                           (const uint4*)t1, (uint4*)d_out);
     });
     HALO_HIP(hipGetLastError());
     return HALO_OK;

@@ -66,6 +66,7 @@ struct DeviceState {
     // scratch
     DevBuf scratch[8];
     DevBuf scan_tmp;     // halo_evals_scan_dev block totals
+    DevBuf gate_tmp;     // halo_gate_constraints_dev partial vectors
     DevBuf eval_meta[2]; // halo_poly_eval_batch_dev: pointer/length tables, partial sums
     // NTT twiddle caches: key (field, log, inverse)
     struct Twiddles {

@@ -9,9 +9,10 @@ backend ``B``; with ``DeviceBackend`` every data-parallel step runs in libhalo_g
 * round 3: the 14 growing FFT products of f' and g', their NTTs mod X^n - 1, the permutation
   accumulator z as prefix/suffix product scans (no per-element inversion), 2 iNTTs, 1 commitment
   (protocol.rs:126-161),
-* round 4: the gate-constraint evaluation over the 8n domain (protocol.rs:591-1011, transcribed from
-  the ``*_generic`` forms onto device ``Evals`` algebra), iNTT(8n), f_cc1 / f_cc2 products, the
-  vanishing division, t_split and 16 commitments (protocol.rs:170-265),
+* round 4: the gate-constraint evaluation over the 8n domain (protocol.rs:591-1011: on the device
+  three fused passes, halo_gate_constraints_dev; on the CPU backends the ``*_generic`` forms
+  transcribed below over ``Evals`` algebra), iNTT(8n), f_cc1 / f_cc2 products, the vanishing
+  division, t_split and 16 commitments (protocol.rs:170-265),
 * round 5: the geometric combinations, two ``Instance::open`` (commit + evaluation + IPA opening),
   ``acc::prover`` (h(X) of three instances, one more IPA opening; acc.rs:178-204) and the 91
   polynomial evaluations of the proof (protocol.rs:273-323).
@@ -206,7 +207,9 @@ def naive_prover(B, wit, n: int, chal: Challenges, acc_prev=None):
     q_evals = [B.ntt(p, N8) for p in wit["qs"]]
     w_evals = [B.ntt(p, N8) for p in wit["ws"]]
     r_evals = [B.ntt(p, N8) for p in wit["rs"]]
-    w_omega_evals = [B.shift_left(w_evals[i], CONSTRAINT_DEGREE_MULTIPLIER) for i in range(3)]
+    fused_gates = hasattr(B, "gate_constraints")  # the device reads w_omega as w shifted in place
+    w_omega_evals = None if fused_gates else [B.shift_left(w_evals[i], CONSTRAINT_DEGREE_MULTIPLIER)
+                                              for i in range(3)]
     pi_evals = B.ntt(pi_poly, N8)
     B.sync()
     times["round0"] = time.perf_counter() - t0
@@ -242,17 +245,19 @@ def naive_prover(B, wit, n: int, chal: Challenges, acc_prev=None):
     # ---- round 4 (protocol.rs:170-265)
     t4 = time.perf_counter()
     alpha = chal()
-    one = B.ones(N8)
-    sbox = B.sbox
-    poseidon = poseidon_constraints(wit["mds"], r_evals, w_evals, w_omega_evals, sbox)
-    affine_add = affine_add_constraints(w_evals, one)
-    affine_mul = affine_mul_constraints(w_evals, w_omega_evals, r_evals[0], one)
-    eq = eq_constraints(w_evals)
-    range_check = range_check_constraints(w_evals, w_omega_evals, r_evals)
-    q, w = q_evals, w_evals
-    f_gc_evals = (w[0] * q[0] + q[1] * w[1] + q[2] * w[2] + q[3] * w[0] * w[1] + q[4] + q[5] * poseidon
-                  + q[6] * affine_add + q[7] * affine_mul + q[8] * eq + q[9] * range_check + pi_evals)
-    del poseidon, affine_add, affine_mul, eq, range_check, one
+    if fused_gates:
+        f_gc_evals = B.gate_constraints(w_evals, r_evals, q_evals, pi_evals, wit["mds"], CONSTRAINT_DEGREE_MULTIPLIER)
+    else:
+        one = B.ones(N8)
+        poseidon = poseidon_constraints(wit["mds"], r_evals, w_evals, w_omega_evals, B.sbox)
+        affine_add = affine_add_constraints(w_evals, one)
+        affine_mul = affine_mul_constraints(w_evals, w_omega_evals, r_evals[0], one)
+        eq = eq_constraints(w_evals)
+        range_check = range_check_constraints(w_evals, w_omega_evals, r_evals)
+        q, w = q_evals, w_evals
+        f_gc_evals = (w[0] * q[0] + q[1] * w[1] + q[2] * w[2] + q[3] * w[0] * w[1] + q[4] + q[5] * poseidon
+                      + q[6] * affine_add + q[7] * affine_mul + q[8] * eq + q[9] * range_check + pi_evals)
+        del poseidon, affine_add, affine_mul, eq, range_check, one
     f_gc = B.intt(f_gc_evals)
     del f_gc_evals
     e1 = B.sparse_vec(n, {0: 1})
@@ -429,6 +434,20 @@ class DeviceBackend:
 
     def sbox(self, x):
         return DevEvals(self, self._op(6, x.t, None, None, 7, self._empty(x.t.shape[0])))
+
+    def gate_constraints(self, w, r, q, pi, mds, shift):
+        """protocol.rs:170-191 fused on the device (halo_gate_constraints_dev): one pass per group of
+        constraint polynomials instead of ~250 Evals kernels; w_omega = w[0..3] shifted by `shift`."""
+        N = w[0].t.shape[0]
+        vp = ctypes.c_void_p
+        dw = (vp * 16)(*[e.t.data_ptr() for e in w])
+        dr = (vp * 15)(*[e.t.data_ptr() for e in r])
+        dq = (vp * 10)(*[e.t.data_ptr() for e in q])
+        m9 = np.ascontiguousarray(np.stack([self.fe(x) for row in mds for x in row]))
+        out = self._empty(N)
+        self.H.check(self.L.halo_gate_constraints_dev(self.field, dw, dr, dq, self._p(pi.t), self.H.ptr(m9), N, shift,
+                                                      self._p(out), self.sp))
+        return DevEvals(self, out)
 
     # -- polynomials (coefficient tensors; lengths may differ)
     def poly_add(self, a, b, sub=False):

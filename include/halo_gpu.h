@@ -205,6 +205,13 @@ int halo_divide_by_vanishing(halo_field_t field, const halo_fe_t* coeffs, size_t
  * (may be null when len == n), remainder n entries. */
 int halo_divide_by_vanishing_dev(halo_field_t field, const void* d_coeffs, size_t len, size_t n,
                                  void* d_quotient, void* d_remainder, void* stream);
+/* Gate-constraint evaluation of naive_prover round 4 (protocol.rs:170-191 with the constraint
+ * polynomials of protocol.rs:591-1011), fused into one pass over the n-point (8x) domain: d_w (16),
+ * d_r (15), d_q (10) device evaluation vectors, d_pi the public-input evaluations, w_omega = d_w[0..3]
+ * shifted left by `shift`; mds = the 3 x 3 Poseidon MDS matrix (row-major, ark).  d_out = f_gc. */
+int halo_gate_constraints_dev(halo_field_t field, const void* const* d_w, const void* const* d_r,
+                              const void* const* d_q, const void* d_pi, const halo_fe_t* mds, size_t n,
+                              unsigned shift, void* d_out, void* stream);
 /* Running product of the permutation argument (protocol.rs:143-154): inclusive prefix product
  * out[i] = prod_{j<=i} in[j] over n device elements (reverse != 0: suffix product prod_{j>=i}). */
 int halo_evals_scan_dev(halo_field_t field, int reverse, const void* d_in, void* d_out, size_t n, void* stream);
