@@ -64,6 +64,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    # 8 hardware queues (HIP's default is 4): the MSM tail streams and the concurrent IPA sessions'
+    # streams then map onto distinct queues instead of serialising behind each other (measured: two
+    # concurrent 2^16 openings 56 ms on 4 queues, 38 ms on 8; the MSM pipeline is unchanged)
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
     import torch
     import torch.distributed as dist
 

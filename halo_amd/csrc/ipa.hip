@@ -474,6 +474,11 @@ struct halo_ipa_session {
     size_t n0 = 0, wlen = 0;
     DevBuf table, w[2], scal, side, part;
     int wcur = 0;
+    uint8_t* pinned = nullptr;  // 128 B L|R (D2H) + 64 B xi|xi_inv (H2D): async copies, several sessions in flight
+    ~halo_ipa_session() {
+        if (s) (void)hipStreamDestroy(s);
+        if (pinned) (void)hipHostFree(pinned);
+    }
 };
 
 static int check_field_i(halo_field_t f) {
@@ -677,7 +682,12 @@ static int ipa_begin(halo_curve_t curve, size_t n, const halo_wrapped_point_t* g
     }
     ses->n = n;
     ses->m = n / 2;
-    ses->s = 0;
+    ses->s = nullptr;
+    if (hipStreamCreateWithFlags(&ses->s, hipStreamNonBlocking) != hipSuccess ||
+        hipHostMalloc((void**)&ses->pinned, 256, hipHostMallocDefault) != hipSuccess) {
+        delete ses;
+        return set_error(HALO_EDEVICE, "halo_ipa_begin: stream / pinned buffer allocation failed");
+    }
     hipStream_t s = ses->s;
     int rc = HALO_OK;
     do {
@@ -694,7 +704,13 @@ static int ipa_begin(halo_curve_t curve, size_t n, const halo_wrapped_point_t* g
             rc = set_error(HALO_EDEVICE, "copy of the SRS prefix failed");
             break;
         }
-        if (cs_on_device) {
+        if (cs_on_device) {  // the producer ran on the null stream: order the session's stream after it
+            hipEvent_t ev;
+            if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess || hipEventRecord(ev, 0) != hipSuccess ||
+                hipStreamWaitEvent(s, ev, 0) != hipSuccess || hipEventDestroy(ev) != hipSuccess) {
+                rc = set_error(HALO_EDEVICE, "halo_ipa_begin_dev: stream ordering failed");
+                break;
+            }
             if (hipMemcpyAsync(ses->cs.ptr, cs, n * 32, hipMemcpyDeviceToDevice, s) != hipSuccess) {
                 rc = set_error(HALO_EDEVICE, "copy of the coefficients failed");
                 break;
@@ -796,13 +812,9 @@ static int ipa_tail_sums(halo_ipa_session* ses, int mode, hipStream_t s) {
     return HALO_OK;
 }
 
-extern "C" int halo_ipa_round_lr(halo_ipa_session* ses, halo_wrapped_point_t* L, halo_wrapped_point_t* R) {
-    clear_error();
-    if (!ses || !L || !R) return set_error(HALO_EINVAL, "halo_ipa_round_lr: null argument");
+// Enqueues one round's L and R (with their H' terms) and their D2H copy into ses->pinned.
+static int ipa_round_launch(DeviceState* st, halo_ipa_session* ses) {
     if (ses->m == 0) return set_error(HALO_EINVAL, "halo_ipa_round_lr: no rounds left");
-    DeviceState* st = current_state();
-    if (!st) return HALO_EDEVICE;
-    std::lock_guard<std::mutex> g(st->mu);
     hipStream_t s = ses->s;
     const size_t m = ses->m;
     const int sf = ses->curve == HALO_PALLAS ? HALO_FP : HALO_FQ;
@@ -819,34 +831,29 @@ extern "C" int halo_ipa_round_lr(halo_ipa_session* ses, halo_wrapped_point_t* L,
     HALO_CHECK(dot_device(sf, cs, zs + m * 32, m, sm + 160, ses->tmp.ptr, s));        // <c_l, z_r>
     if (ses->tail) {
         HALO_CHECK(ipa_tail_sums(ses, 0, s));
-        HALO_CHECK(copy_d2h(L, sm + 256, 64, s));
-        return copy_d2h(R, sm + 320, 64, s);
-    }
-    // L and R are independent: the second MSM's accumulation overlaps the first one's tail
-    if (ses->srs_round0) {  // G_l = SRS[0, m), G_r = SRS[m, 2m): resident window-shifted copies, no Horner
-        HALO_CHECK(msm_srs_range_device(st, ses->curve, 0, cs + m * 32, m, ses->htab.ptr, sm + 128, sm + 256, s, true));
-        HALO_CHECK(msm_srs_range_device(st, ses->curve, m, cs, m, ses->htab.ptr, sm + 160, sm + 320, s, true));
     } else {
-        HALO_CHECK(msm_device(st, ses->curve, gs, cs + m * 32, m, ses->htab.ptr, sm + 128, sm + 256, s, true));   // L
-        HALO_CHECK(msm_device(st, ses->curve, gs + m * 64, cs, m, ses->htab.ptr, sm + 160, sm + 320, s, true));   // R
+        // L and R are independent: the second MSM's accumulation overlaps the first one's tail
+        if (ses->srs_round0) {  // G_l = SRS[0, m), G_r = SRS[m, 2m): resident window-shifted copies, no Horner
+            HALO_CHECK(msm_srs_range_device(st, ses->curve, 0, cs + m * 32, m, ses->htab.ptr, sm + 128, sm + 256, s, true));
+            HALO_CHECK(msm_srs_range_device(st, ses->curve, m, cs, m, ses->htab.ptr, sm + 160, sm + 320, s, true));
+        } else {
+            HALO_CHECK(msm_device(st, ses->curve, gs, cs + m * 32, m, ses->htab.ptr, sm + 128, sm + 256, s, true));
+            HALO_CHECK(msm_device(st, ses->curve, gs + m * 64, cs, m, ses->htab.ptr, sm + 160, sm + 320, s, true));
+        }
+        HALO_CHECK(msm_join(st, s));
     }
-    HALO_CHECK(msm_join(st, s));
-    HALO_CHECK(copy_d2h(L, sm + 256, 64, s));
-    HALO_CHECK(copy_d2h(R, sm + 320, 64, s));
+    HALO_HIP(hipMemcpyAsync(ses->pinned, sm + 256, 128, hipMemcpyDeviceToHost, s));
     return HALO_OK;
 }
 
-extern "C" int halo_ipa_fold(halo_ipa_session* ses, const halo_fe_t* xi, const halo_fe_t* xi_inv) {
-    clear_error();
-    if (!ses || !xi || !xi_inv) return set_error(HALO_EINVAL, "halo_ipa_fold: null argument");
+// Enqueues one fold with challenge xi (pcdl.rs:427-435); the session advances to the next round.
+static int ipa_fold_launch(halo_ipa_session* ses, const halo_fe_t* xi, const halo_fe_t* xi_inv) {
     if (ses->m == 0) return set_error(HALO_EINVAL, "halo_ipa_fold: no rounds left");
-    DeviceState* st = current_state();
-    if (!st) return HALO_EDEVICE;
-    std::lock_guard<std::mutex> g(st->mu);
     hipStream_t s = ses->s;
     char* sm = (char*)ses->small.ptr;
-    HALO_CHECK(copy_h2d(sm + 384, xi, 32, s));
-    HALO_CHECK(copy_h2d(sm + 416, xi_inv, 32, s));
+    memcpy(ses->pinned + 128, xi, 32);
+    memcpy(ses->pinned + 160, xi_inv, 32);
+    HALO_HIP(hipMemcpyAsync(sm + 384, ses->pinned + 128, 64, hipMemcpyHostToDevice, s));
     const size_t m = ses->m;
     ses->srs_round0 = false;
     if (ses->tail) {
@@ -857,20 +864,66 @@ extern "C" int halo_ipa_fold(halo_ipa_session* ses, const halo_fe_t* xi, const h
                                ses->w[ses->wcur ^ 1].as<uint4>(), ses->wlen);
         });
         HALO_HIP(hipGetLastError());
-        HALO_HIP(hipStreamSynchronize(s));
         ses->wcur ^= 1;
         ses->wlen *= 2;
-        ses->m /= 2;
-        return HALO_OK;
+    } else {
+        DISPATCH_CURVE(ses->curve, Cv, {
+            ProfScope prof("ipa_fold", s);
+            HALO_LAUNCH(prof, k_ipa_fold<Cv>, dim3(gridn(m, FOLD_THREADS)), dim3(FOLD_THREADS), 0, s, ses->gs.as<uint4>(),
+                        ses->cs.as<uint4>(), ses->zs.as<uint4>(), m, (const uint4*)(sm + 384),
+                        (const uint4*)(sm + 416));
+        });
+        HALO_HIP(hipGetLastError());
     }
-    DISPATCH_CURVE(ses->curve, Cv, {
-        ProfScope prof("ipa_fold", s);
-        HALO_LAUNCH(prof, k_ipa_fold<Cv>, dim3(gridn(m, FOLD_THREADS)), dim3(FOLD_THREADS), 0, s, ses->gs.as<uint4>(), ses->cs.as<uint4>(),
-                    ses->zs.as<uint4>(), m, (const uint4*)(sm + 384), (const uint4*)(sm + 416));
-    });
-    HALO_HIP(hipGetLastError());
-    HALO_HIP(hipStreamSynchronize(s));
     ses->m /= 2;
+    return HALO_OK;
+}
+
+extern "C" int halo_ipa_round_lr(halo_ipa_session* ses, halo_wrapped_point_t* L, halo_wrapped_point_t* R) {
+    clear_error();
+    if (!ses || !L || !R) return set_error(HALO_EINVAL, "halo_ipa_round_lr: null argument");
+    return halo_ipa_round_lr_multi(&ses, 1, L, R);
+}
+
+// k independent openings advanced in lockstep: every session's round is enqueued on its own stream
+// before any is waited for, so their latency-bound kernels overlap on the device.
+extern "C" int halo_ipa_round_lr_multi(halo_ipa_session* const* ses, size_t k, halo_wrapped_point_t* L,
+                                       halo_wrapped_point_t* R) {
+    clear_error();
+    if (!ses || !L || !R) return set_error(HALO_EINVAL, "halo_ipa_round_lr_multi: null argument");
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    for (size_t i = 0; i < k; i++) {
+        if (!ses[i]) return set_error(HALO_EINVAL, "halo_ipa_round_lr_multi: null session %zu", i);
+        HALO_CHECK(ipa_round_launch(st, ses[i]));
+    }
+    for (size_t i = 0; i < k; i++) {
+        HALO_HIP(hipStreamSynchronize(ses[i]->s));
+        memcpy(&L[i], ses[i]->pinned, 64);
+        memcpy(&R[i], ses[i]->pinned + 64, 64);
+    }
+    return HALO_OK;
+}
+
+extern "C" int halo_ipa_fold(halo_ipa_session* ses, const halo_fe_t* xi, const halo_fe_t* xi_inv) {
+    clear_error();
+    if (!ses || !xi || !xi_inv) return set_error(HALO_EINVAL, "halo_ipa_fold: null argument");
+    return halo_ipa_fold_multi(&ses, 1, xi, xi_inv);
+}
+
+extern "C" int halo_ipa_fold_multi(halo_ipa_session* const* ses, size_t k, const halo_fe_t* xi,
+                                   const halo_fe_t* xi_inv) {
+    clear_error();
+    if (!ses || !xi || !xi_inv) return set_error(HALO_EINVAL, "halo_ipa_fold_multi: null argument");
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    for (size_t i = 0; i < k; i++) {
+        if (!ses[i]) return set_error(HALO_EINVAL, "halo_ipa_fold_multi: null session %zu", i);
+        HALO_CHECK(ipa_fold_launch(ses[i], &xi[i], &xi_inv[i]));
+    }
+    for (size_t i = 0; i < k; i++) HALO_HIP(hipStreamSynchronize(ses[i]->s));
     return HALO_OK;
 }
 

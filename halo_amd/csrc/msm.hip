@@ -333,6 +333,10 @@ int msm_window_bits(size_t n) {
 
 static unsigned grid_for(size_t n, unsigned thr) { return (unsigned)std::max<size_t>(1, (n + thr - 1) / thr); }
 
+// Four scratch sets: consecutive MSMs of one stream pipeline (tail of k overlaps k+1), and
+// independent streams (concurrent IPA openings: L and R of two sessions per round) do not wait for
+// each other's scratch.
+constexpr int MSM_SETS = 4;
 struct MsmScratch {
     DevBuf digits, bstart, partials, bucket_sums, seg_acc, seg_sum, bits, window_sums, scan_tmp, conv;
     const uint32_t* skeys = nullptr;   // sorted keys of the current MSM (sort scratch)
@@ -340,21 +344,21 @@ struct MsmScratch {
     SortScratch sort;
     hipEvent_t acc_done = nullptr, tail_done = nullptr;
     bool tail_pending = false;
+    hipStream_t owner = nullptr;  // stream the set's last MSM was enqueued on (msm_join)
 };
 // Two scratch sets per device: MSM k+1's digit/sort/accumulation phase (throughput-bound, whole
 // GPU) runs on the caller's stream while MSM k's reduction tail (latency-bound, a few waves) runs
 // on the per-device tail stream.
 struct MsmPipe {
-    MsmScratch set[2];
+    MsmScratch set[MSM_SETS];
     int next = 0;
-    hipStream_t tail[2] = {nullptr, nullptr};  // one per scratch set: consecutive tails run concurrently
+    hipStream_t tail[MSM_SETS] = {};  // one per scratch set: consecutive tails run concurrently
 };
 static MsmPipe g_msm_pipe[64];  // per device
 
 static int pipe_init(MsmPipe& P) {
     if (P.tail[0]) return HALO_OK;
-    HALO_HIP(hipStreamCreateWithFlags(&P.tail[0], hipStreamNonBlocking));
-    HALO_HIP(hipStreamCreateWithFlags(&P.tail[1], hipStreamNonBlocking));
+    for (auto& t : P.tail) HALO_HIP(hipStreamCreateWithFlags(&t, hipStreamNonBlocking));
     for (auto& m : P.set) {
         HALO_HIP(hipEventCreateWithFlags(&m.acc_done, hipEventDisableTiming));
         HALO_HIP(hipEventCreateWithFlags(&m.tail_done, hipEventDisableTiming));
@@ -376,7 +380,7 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
     HALO_CHECK(pipe_init(PP));
     const int set = PP.next;
     MsmScratch& M = PP.set[set];
-    PP.next ^= 1;
+    PP.next = (PP.next + 1) % MSM_SETS;
     // the previous user of this scratch set must have finished its tail
     if (M.tail_pending) HALO_HIP(hipStreamWaitEvent(s, M.tail_done, 0));
     const hipStream_t ts = PP.tail[set];
@@ -481,6 +485,7 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
     HALO_HIP(hipGetLastError());
     HALO_HIP(hipEventRecord(M.tail_done, ts));
     M.tail_pending = true;
+    M.owner = s;
     if (!async) HALO_HIP(hipStreamWaitEvent(s, M.tail_done, 0));
     return HALO_OK;
 }
@@ -491,11 +496,11 @@ DevBuf& msm_next_conv_buffer(DeviceState* st) {
     return PP.set[PP.next].conv;
 }
 
-// Makes `s` wait (device-side) for every MSM tail still in flight on this device.
+// Makes `s` wait (device-side) for the tails of the MSMs enqueued on `s` that are still in flight.
 int msm_join(DeviceState* st, hipStream_t s) {
     MsmPipe& PP = g_msm_pipe[st->device & 63];
     for (auto& m : PP.set)
-        if (m.tail_pending) HALO_HIP(hipStreamWaitEvent(s, m.tail_done, 0));
+        if (m.tail_pending && m.owner == s) HALO_HIP(hipStreamWaitEvent(s, m.tail_done, 0));
     return HALO_OK;
 }
 

@@ -11,7 +11,7 @@ int msm_window_bits(size_t n);
 int msm_device(DeviceState* st, int curve, const void* bases_int, const void* scalars_ark, size_t n,
                const void* hide_table, const void* hide_scalar, void* d_out_wrapped, hipStream_t s,
                bool async = false);
-// Makes stream s wait for every MSM reduction tail still in flight (async MSMs).
+// Makes stream s wait for the reduction tails of the async MSMs enqueued on s.
 int msm_join(DeviceState* st, hipStream_t s);
 // MSM over the resident SRS prefix (window-shifted copies when precomputed); optional hiding
 // scalar (ark, device pointer) times S.

@@ -279,8 +279,7 @@ def naive_prover(B, wit, n: int, chal: Challenges, acc_prev=None):
     r_omega = geometric_polys(B, zeta, wit["ws"][0:3] + [z])
     xi = chal()
     omega = B.omega(n)
-    q_r = instance_open(B, r, d, xi, chal)
-    q_r_omega = instance_open(B, r_omega, d, xi * omega % m, chal)
+    q_r, q_r_omega = instances_open(B, [(r, xi), (r_omega, xi * omega % m)], d)
     if acc_prev is None:
         acc_prev = synthetic_accumulator(B, n, chal)
     acc_next = acc_prover(B, [acc_prev, q_r, q_r_omega], d, chal)
@@ -296,19 +295,31 @@ def naive_prover(B, wit, n: int, chal: Challenges, acc_prev=None):
     }
 
 
-def ipa_open(B, p, C, d: int, z: int, v: int, chal: Challenges):
-    """pcdl::open_without_eval with w = None (pcdl.rs:326-453): xi_0, H' = xi_0 H, lg n rounds of
-    (L, R, xi, fold).  Returns (Ls, Rs, U, c, xis)."""
-    xi0 = chal()
-    return tuple(B.ipa(p, d + 1, z, B.h_mul(xi0), chal)) + ([xi0],)
+def open_seed(z: int, v: int) -> int:
+    """Stand-in for the opening's own transcript (open_without_eval starts a fresh PCDL sponge that
+    absorbs C', z, v; pcdl.rs:336,387-389): its challenge stream is seeded by (z, v)."""
+    return (z * 0x9E3779B97F4A7C15 + v) & ((1 << 64) - 1)
 
 
-def instance_open(B, p, d: int, z: int, chal: Challenges):
-    """Instance::open (pcdl.rs:41-51): C = commit(p), v = p(z), pi = open(p, C, d, z)."""
-    C = B.commit_many([p])[0]
-    v = B.eval_many([p], z)[0]
-    Ls, Rs, U, c, xi0 = ipa_open(B, p, C, d, z, v, chal)
-    return {"C": C, "v": v, "Ls": Ls, "Rs": Rs, "U": U, "c": c, "xis": xi0 + B.last_xis}
+def ipa_open_many(B, items, d: int):
+    """pcdl::open_without_eval with w = None (pcdl.rs:326-453) for independent openings
+    items = [(p, z, v)]: per opening xi_0 from its own transcript, H' = xi_0 H, lg n rounds of
+    (L, R, xi, fold).  The device backend advances all openings in lockstep on their own streams.
+    Returns [(Ls, Rs, U, c, [xi_0] + xis)]."""
+    chals = [Challenges(B.m, seed=open_seed(z, v)) for (_, z, v) in items]
+    xi0s = [ch() for ch in chals]
+    jobs = [(p, d + 1, z, B.h_mul(x0)) for (p, z, _), x0 in zip(items, xi0s)]
+    outs = B.ipa_many(jobs, chals)
+    return [(Ls, Rs, U, c, [x0] + xis) for (Ls, Rs, U, c, xis), x0 in zip(outs, xi0s)]
+
+
+def instances_open(B, polys_points, d: int):
+    """Instance::open (pcdl.rs:41-51) for independent (p, z): C = commit(p), v = p(z), pi = open."""
+    Cs = B.commit_many([p for p, _ in polys_points])
+    vs = [B.eval_many([p], z)[0] for p, z in polys_points]
+    opens = ipa_open_many(B, [(p, z, v) for (p, z), v in zip(polys_points, vs)], d)
+    return [{"C": C, "v": v, "Ls": o[0], "Rs": o[1], "U": o[2], "c": o[3], "xis": o[4]}
+            for C, v, o in zip(Cs, vs, opens)]
 
 
 def synthetic_accumulator(B, n: int, chal: Challenges):
@@ -328,7 +339,7 @@ def acc_prover(B, qs, d: int, chal: Challenges):
     z = chal()
     h = B.hpoly([q["xis"] for q in qs], alphas)
     v = B.eval_many([h], z)[0]
-    Ls, Rs, U, c, xi0 = ipa_open(B, h, C, d, z, v, chal)
+    Ls, Rs, U, c, _ = ipa_open_many(B, [(h, z, v)], d)[0]
     return {"C": C, "z": z, "v": v, "Ls": Ls, "Rs": Rs, "U": U, "c": c}
 
 
@@ -350,7 +361,6 @@ class DeviceBackend:
         self.m = SCALAR_MODULUS[curve]
         self.stream = torch.cuda.current_stream().cuda_stream
         self.sp = ctypes.c_void_p(self.stream)
-        self.last_xis = []
         hp = np.zeros(8, dtype=np.uint64)
         H.check(self.L.halo_srs_read(self.curve, 1, 1, H.ptr(hp)))  # H = Gs[1] of the resident SRS
         self.H_point = hp
@@ -560,27 +570,45 @@ class DeviceBackend:
                                                ctypes.byref(ln)))
         return self.torch.from_numpy(out.view(np.int64)).cuda()
 
-    def ipa(self, p, n: int, z: int, h_prime, chal):
-        cs = self.resize(p, n)
-        self.sync()  # sessions run on the null stream
-        ses = ctypes.c_void_p()
-        self.H.check(self.L.halo_ipa_begin_dev(self.curve, self._p(cs), n, self.H.ptr(self.fe(z)),
-                                               self.H.ptr(np.ascontiguousarray(h_prime)), ctypes.byref(ses)))
-        Ls, Rs, xis = [], [], []
+    def ipa_many(self, jobs, chals):
+        """jobs = [(p, n, z, H')] with one challenge stream each; all sessions advance in lockstep
+        (halo_ipa_round_lr_multi / halo_ipa_fold_multi: one host round trip per round for all)."""
+        k = len(jobs)
+        n = jobs[0][1]
+        assert all(j[1] == n for j in jobs)
+        css = [self.resize(p, n) for (p, _, _, _) in jobs]
+        self.sync()  # the coefficients were produced on the caller's stream
+        sess = (ctypes.c_void_p * k)()
+        for i, ((_, _, z, hp), cs) in enumerate(zip(jobs, css)):
+            s = ctypes.c_void_p()
+            self.H.check(self.L.halo_ipa_begin_dev(self.curve, self._p(cs), n, self.H.ptr(self.fe(z)),
+                                                   self.H.ptr(np.ascontiguousarray(hp)), ctypes.byref(s)))
+            sess[i] = s.value
+        Ls = [[] for _ in range(k)]
+        Rs = [[] for _ in range(k)]
+        xis = [[] for _ in range(k)]
+        Lb = np.zeros((k, 8), dtype=np.uint64)
+        Rb = np.zeros((k, 8), dtype=np.uint64)
         for _ in range(n.bit_length() - 1):
-            Lp = np.zeros(8, dtype=np.uint64)
-            Rp = np.zeros(8, dtype=np.uint64)
-            self.H.check(self.L.halo_ipa_round_lr(ses, self.H.ptr(Lp), self.H.ptr(Rp)))
-            x = chal()
-            self.H.check(self.L.halo_ipa_fold(ses, self.H.ptr(self.fe(x)), self.H.ptr(self.fe(pow(x, -1, self.m)))))
-            Ls.append(Lp)
-            Rs.append(Rp)
-            xis.append(x)
-        U = np.zeros(8, dtype=np.uint64)
-        c0 = np.zeros(4, dtype=np.uint64)
-        self.H.check(self.L.halo_ipa_end(ses, self.H.ptr(U), self.H.ptr(c0)))
-        self.last_xis = xis
-        return [Ls, Rs, U, self.to_int(c0)]
+            self.H.check(self.L.halo_ipa_round_lr_multi(sess, k, self.H.ptr(Lb), self.H.ptr(Rb)))
+            xs = [ch() for ch in chals]
+            xa = np.ascontiguousarray(np.stack([self.fe(x) for x in xs]))
+            xia = np.ascontiguousarray(np.stack([self.fe(pow(x, -1, self.m)) for x in xs]))
+            self.H.check(self.L.halo_ipa_fold_multi(sess, k, self.H.ptr(xa), self.H.ptr(xia)))
+            for i in range(k):
+                Ls[i].append(Lb[i].copy())
+                Rs[i].append(Rb[i].copy())
+                xis[i].append(xs[i])
+        outs = []
+        for i in range(k):
+            U = np.zeros(8, dtype=np.uint64)
+            c0 = np.zeros(4, dtype=np.uint64)
+            self.H.check(self.L.halo_ipa_end(ctypes.c_void_p(sess[i]), self.H.ptr(U), self.H.ptr(c0)))
+            outs.append((Ls[i], Rs[i], U, self.to_int(c0), xis[i]))
+        return outs
+
+    def ipa(self, p, n: int, z: int, h_prime, chal):
+        return self.ipa_many([(p, n, z, h_prime)], [chal])[0]
 
 
 class DevEvals:

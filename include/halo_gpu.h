@@ -253,6 +253,12 @@ int halo_ipa_round_lr(halo_ipa_session* s, halo_wrapped_point_t* L, halo_wrapped
 /* G_l[j] = G_l[j] + xi G_r[j] (affine), c_l[j] += xi^-1 c_r[j], z_l[j] += xi z_r[j]; m /= 2
  * (pcdl.rs:427-437). */
 int halo_ipa_fold(halo_ipa_session* s, const halo_fe_t* xi, const halo_fe_t* xi_inv);
+/* k independent openings advanced in lockstep (each session has its own stream; all k rounds /
+ * folds are enqueued before any is waited for, so the openings overlap on the device): L[i], R[i]
+ * of session i; xi[i], xi_inv[i] for session i. */
+int halo_ipa_round_lr_multi(halo_ipa_session* const* ses, size_t k, halo_wrapped_point_t* L,
+                            halo_wrapped_point_t* R);
+int halo_ipa_fold_multi(halo_ipa_session* const* ses, size_t k, const halo_fe_t* xi, const halo_fe_t* xi_inv);
 /* Current half-length m, and the folded vectors (length 2m) copied back to the host (any of the
  * output pointers may be NULL). */
 int halo_ipa_state(halo_ipa_session* s, size_t* m, halo_wrapped_point_t* gs, halo_fe_t* cs,

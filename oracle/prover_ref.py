@@ -53,7 +53,6 @@ class RefBackend:
         self.m = self.c.scalar
         self.srs = [P.wrapped_to_point(self.c, [int(x) for x in row]) for row in srs_wrapped]
         self.H_point = P.wrapped_to_point(self.c, [int(x) for x in h_wrapped])
-        self.last_xis = []
         self._rinv = pow(1 << 256, -1, self.m)
 
     # -- helpers
@@ -182,8 +181,10 @@ class RefBackend:
             Ls.append(self._w(P.add(self.c, L, P.mul(self.c, dl, h_prime))))
             Rs.append(self._w(P.add(self.c, R, P.mul(self.c, dr, h_prime))))
             xis.append(x)
-        self.last_xis = xis
-        return [Ls, Rs, self._w(gs[0]), cs[0]]
+        return (Ls, Rs, self._w(gs[0]), cs[0], xis)
+
+    def ipa_many(self, jobs, chals):
+        return [self.ipa(p, n, z, hp, ch) for (p, n, z, hp), ch in zip(jobs, chals)]
 
 
 # ---------------------------------------------------------------------------------------------
@@ -229,7 +230,6 @@ class CRefBackend:
         self.threads = threads
         self.srs = np.ascontiguousarray(srs_wrapped)
         self.H_point = P.wrapped_to_point(self.c, [int(x) for x in h_wrapped])
-        self.last_xis = []
 
     def fe(self, x):
         v = (x % self.m) * (1 << 256) % self.m
@@ -389,5 +389,7 @@ class CRefBackend:
                                          threads=self.threads)
             gs, cs, zs = np.ascontiguousarray(gs), np.ascontiguousarray(cs), np.ascontiguousarray(zs)
             xis.append(x)
-        self.last_xis = xis
-        return [Ls, Rs, gs[0].copy(), self.to_int(cs[0])]
+        return (Ls, Rs, gs[0].copy(), self.to_int(cs[0]), xis)
+
+    def ipa_many(self, jobs, chals):
+        return [self.ipa(p, n, z, hp, ch) for (p, n, z, hp), ch in zip(jobs, chals)]
