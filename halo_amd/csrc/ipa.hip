@@ -212,6 +212,8 @@ __global__ __launch_bounds__(FOLD_THREADS, 4) void k_ipa_fold(uint4* gs, uint4* 
         acc = xyzz_madd(acc, aff_load<F>(gs + 4 * j));
     }
     // batched affine conversion: z = ZZ * ZZZ (1 for identity / idle lanes)
+    // (measured and rejected: a Jacobian accumulator (dbl-2009-l + madd-2007-bl, ~27 % fewer
+    // multiplications) was 13 % slower -- its fully reduced additions cost more than they save)
     const bool id = xyzz_is_id(acc);
     const Fe<F> z = (live && !id) ? fe_mul(acc.ZZ, acc.ZZZ) : fe_one<F>();
     // inclusive prefix and suffix products (Hillis-Steele in LDS)
