@@ -461,6 +461,22 @@ __global__ __launch_bounds__(256) void k_tail_fold(uint4* cs, uint4* zs, size_t 
     }
 }
 
+// Weighted rounds (sessions over the resident SRS, length > IPA_TAIL_N): G is never folded.  With
+// len = 2m and the fold weights w (as in the tail rounds, G_i = sum_u w[u] SRS[i + u len]),
+//   L = sum_{u, i < m} c[m + i] w[u] SRS[u len + i],   R = sum_{u, i < m} c[i] w[u] SRS[u len + m + i],
+// two MSMs of n/2 terms over the resident window-shifted SRS (msm_srs_range_device, block map
+// blk_lg = lg m).  Term j = u m + i of both: sl[j] = c[m + i] w[u], sr[j] = c[i] w[u].
+template <class S>
+__global__ __launch_bounds__(256) void k_weighted_scalars(const uint4* cs, const uint4* w, size_t m, int lgm,
+                                                          size_t total, uint4* sl, uint4* sr) {
+    const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= total) return;
+    const size_t u = j >> lgm, i = j & (m - 1);
+    const Fe<S> wu = fe_from_ark<S>(w + 2 * u);
+    fe_to_ark(sl + 2 * j, fe_mul(fe_from_ark<S>(cs + 2 * (m + i)), wu));
+    fe_to_ark(sr + 2 * j, fe_mul(fe_from_ark<S>(cs + 2 * i), wu));
+}
+
 }  // namespace halo
 
 using namespace halo;
@@ -473,6 +489,7 @@ struct halo_ipa_session {
     // tail rounds (length <= IPA_TAIL_N, sessions over the SRS only): see k_tail_table
     bool allow_tail = false, tail = false;
     bool srs_round0 = false;  // G is still the SRS prefix (no fold yet): L/R on the resident shifted SRS
+    bool weighted = false;    // G is never folded: L/R over the resident shifted SRS (k_weighted_scalars)
     size_t n0 = 0, wlen = 0;
     DevBuf table, w[2], scal, side, part;
     int wcur = 0;
@@ -663,6 +680,14 @@ extern "C" int halo_poly_mul(halo_field_t field, const halo_fe_t* a, size_t la, 
 // Session start shared by halo_ipa_begin (G = resident SRS prefix, z powers generated on the
 // device) and halo_ipa_begin_vectors (explicit G, c, z: a shard of a distributed opening or its
 // final collapsed rounds, halo_amd/dist.py).
+static size_t ipa_tail_n() {
+    static const size_t tail_n = [] {
+        const char* e = getenv("HALO_IPA_TAIL_N");  // A/B knob; default IPA_TAIL_N
+        return e ? (size_t)atoll(e) : IPA_TAIL_N;
+    }();
+    return tail_n;
+}
+
 static int ipa_begin(halo_curve_t curve, size_t n, const halo_wrapped_point_t* gs_host, const halo_fe_t* cs,
                      const halo_fe_t* zs_host, const halo_fe_t* z, const halo_wrapped_point_t* H_prime,
                      halo_ipa_session** out, bool cs_on_device = false) {
@@ -679,8 +704,11 @@ static int ipa_begin(halo_curve_t curve, size_t n, const halo_wrapped_point_t* g
     ses->curve = curve;
     {
         const char* e = getenv("HALO_IPA_TAIL");
+        const char* ew = getenv("HALO_IPA_WEIGHTED");  // A/B knob: 0 = fold G every round
         ses->allow_tail = !gs_host && !(e && e[0] == '0');
-        ses->srs_round0 = !gs_host && srs.shifted_c != 0;
+        ses->weighted = !gs_host && srs.shifted_c != 0 && n > ipa_tail_n() && !(ew && ew[0] == '0');
+        if (ses->weighted) ses->allow_tail = false;
+        ses->srs_round0 = !gs_host && srs.shifted_c != 0 && !ses->weighted;
     }
     ses->n = n;
     ses->m = n / 2;
@@ -693,7 +721,17 @@ static int ipa_begin(halo_curve_t curve, size_t n, const halo_wrapped_point_t* g
     hipStream_t s = ses->s;
     int rc = HALO_OK;
     do {
-        if ((rc = ses->gs.reserve(n * 64))) break;
+        if (!ses->weighted && (rc = ses->gs.reserve(n * 64))) break;
+        if (ses->weighted) {  // w = [1]; scal holds the two n/2-term scalar vectors of a round
+            if ((rc = ses->w[0].reserve(n * 32)) || (rc = ses->w[1].reserve(n * 32)) || (rc = ses->scal.reserve(n * 32)))
+                break;
+            DISPATCH_CURVE(curve, Cv, {
+                hipLaunchKernelGGL(k_set_one_ark<typename Cv::Scalar>, dim3(1), dim3(64), 0, s, ses->w[0].as<uint4>());
+            });
+            ses->n0 = n;
+            ses->wlen = 1;
+            ses->wcur = 0;
+        }
         if ((rc = ses->cs.reserve(n * 32))) break;
         if ((rc = ses->zs.reserve(n * 32))) break;
         if ((rc = ses->htab.reserve(256 * 64))) break;
@@ -702,7 +740,8 @@ static int ipa_begin(halo_curve_t curve, size_t n, const halo_wrapped_point_t* g
         if (gs_host) {
             if ((rc = copy_h2d(ses->tmp.ptr, gs_host, n * 64, s))) break;
             if ((rc = convert_wrapped_to_internal(curve, ses->tmp.ptr, ses->gs.ptr, n, s))) break;
-        } else if (hipMemcpyAsync(ses->gs.ptr, srs.gs.ptr, n * 64, hipMemcpyDeviceToDevice, s) != hipSuccess) {
+        } else if (!ses->weighted &&
+                   hipMemcpyAsync(ses->gs.ptr, srs.gs.ptr, n * 64, hipMemcpyDeviceToDevice, s) != hipSuccess) {
             rc = set_error(HALO_EDEVICE, "copy of the SRS prefix failed");
             break;
         }
@@ -824,15 +863,30 @@ static int ipa_round_launch(DeviceState* st, halo_ipa_session* ses) {
     const char* cs = ses->cs.as<const char>();
     const char* zs = ses->zs.as<const char>();
     const char* gs = ses->gs.as<const char>();
-    static const size_t tail_n = [] {
-        const char* e = getenv("HALO_IPA_TAIL_N");  // A/B knob; default IPA_TAIL_N
-        return e ? (size_t)atoll(e) : IPA_TAIL_N;
-    }();
-    if (!ses->tail && ses->allow_tail && 2 * m <= tail_n) HALO_CHECK(ipa_enter_tail(ses, s));
+    if (!ses->tail && ses->allow_tail && 2 * m <= ipa_tail_n()) HALO_CHECK(ipa_enter_tail(ses, s));
     HALO_CHECK(dot_device(sf, cs + m * 32, zs, m, sm + 128, ses->tmp.ptr, s));        // <c_r, z_l>
     HALO_CHECK(dot_device(sf, cs, zs + m * 32, m, sm + 160, ses->tmp.ptr, s));        // <c_l, z_r>
     if (ses->tail) {
         HALO_CHECK(ipa_tail_sums(ses, 0, s));
+    } else if (ses->weighted) {
+        const size_t half = ses->n0 / 2;  // = wlen * m terms per side
+        const uint32_t lgm = ilog2(m);
+        const char* sl = cs + m * 32;     // round 0 (w = [1]): the scalars are c_r, c_l themselves
+        const char* sr = cs;
+        if (ses->wlen > 1) {
+            char* sb = (char*)ses->scal.ptr;
+            DISPATCH_CURVE(ses->curve, Cv, {
+                hipLaunchKernelGGL(k_weighted_scalars<typename Cv::Scalar>, dim3(gridn(half, 256)), dim3(256), 0, s,
+                                   (const uint4*)cs, ses->w[ses->wcur].as<const uint4>(), m, (int)lgm, half, (uint4*)sb,
+                                   (uint4*)(sb + half * 32));
+            });
+            HALO_HIP(hipGetLastError());
+            sl = sb;
+            sr = sb + half * 32;
+        }
+        HALO_CHECK(msm_srs_range_device(st, ses->curve, 0, sl, half, ses->htab.ptr, sm + 128, sm + 256, s, true, lgm));
+        HALO_CHECK(msm_srs_range_device(st, ses->curve, m, sr, half, ses->htab.ptr, sm + 160, sm + 320, s, true, lgm));
+        HALO_CHECK(msm_join(st, s));
     } else {
         // L and R are independent: the second MSM's accumulation overlaps the first one's tail
         if (ses->srs_round0) {  // G_l = SRS[0, m), G_r = SRS[m, 2m): resident window-shifted copies, no Horner
@@ -858,7 +912,7 @@ static int ipa_fold_launch(halo_ipa_session* ses, const halo_fe_t* xi, const hal
     HALO_HIP(hipMemcpyAsync(sm + 384, ses->pinned + 128, 64, hipMemcpyHostToDevice, s));
     const size_t m = ses->m;
     ses->srs_round0 = false;
-    if (ses->tail) {
+    if (ses->tail || ses->weighted) {
         DISPATCH_CURVE(ses->curve, Cv, {
             hipLaunchKernelGGL(k_tail_fold<Cv>, dim3(gridn(std::max(m, ses->wlen), 256)), dim3(256), 0, s,
                                ses->cs.as<uint4>(), ses->zs.as<uint4>(), m, (const uint4*)(sm + 384),
@@ -938,8 +992,10 @@ extern "C" int halo_ipa_state(halo_ipa_session* ses, size_t* m, halo_wrapped_poi
     hipStream_t s = ses->s;
     const size_t len = std::max<size_t>(2 * ses->m, 1);
     if (m) *m = ses->m;
-    if (gs && ses->tail)
-        return set_error(HALO_EINVAL, "halo_ipa_state: G is not materialised in the tail rounds (HALO_IPA_TAIL=0)");
+    if (gs && (ses->tail || ses->weighted))
+        return set_error(HALO_EINVAL,
+                         "halo_ipa_state: G is not materialised in the weighted / tail rounds (HALO_IPA_WEIGHTED=0, "
+                         "HALO_IPA_TAIL=0)");
     if (gs) {
         HALO_CHECK(ses->tmp.reserve(std::max<size_t>(len * 64, 4096 * 32)));
         HALO_CHECK(convert_internal_to_wrapped(ses->curve, ses->gs.ptr, ses->tmp.ptr, len, s));
@@ -963,8 +1019,16 @@ extern "C" int halo_ipa_end(halo_ipa_session* ses, halo_wrapped_point_t* U, halo
         std::lock_guard<std::mutex> g(st->mu);
         hipStream_t s = ses->s;
         char* sm = (char*)ses->small.ptr;
-        if (ses->tail) {
-            rc = ipa_tail_sums(ses, 1, s);
+        if (ses->tail || ses->weighted) {
+            // U = G_0 = sum_u w[u] G0[u] (len = 1 once every round ran)
+            if (ses->m != 0)
+                rc = set_error(HALO_EINVAL, "halo_ipa_end: U needs every round in the weighted / tail rounds (m = %zu)",
+                               ses->m);
+            else if (ses->tail)
+                rc = ipa_tail_sums(ses, 1, s);
+            else
+                rc = msm_srs_range_device(st, ses->curve, 0, ses->w[ses->wcur].ptr, ses->n0, nullptr, nullptr, sm + 256,
+                                          s, false);
             if (!rc && hipMemcpyAsync(sm + 320, ses->cs.ptr, 32, hipMemcpyDeviceToDevice, s) != hipSuccess)
                 rc = set_error(HALO_EDEVICE, "ipa end copy failed");
         } else {

@@ -196,7 +196,8 @@ __global__ void k_digits_glv(const uint4* scalars, size_t n, int c, int W, uint3
 template <class Cv>
 __global__ __launch_bounds__(256, 4) void k_acc(const uint32_t* keys, const uint32_t* vals, const uint32_t* count,
                                              uint32_t K, const uint4* bases, uint32_t n_per_window, size_t stride,
-                                             uint32_t glv_n, uint4* first, uint4* last, uint4* bucket_sums) {
+                                             uint32_t blk_lg, uint32_t glv_n, uint4* first, uint4* last,
+                                             uint4* bucket_sums) {
     using F = typename Cv::Base;
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t cnt = *count;
@@ -220,7 +221,12 @@ __global__ __launch_bounds__(256, 4) void k_acc(const uint32_t* keys, const uint
         }
         const uint32_t v = vals[e];
         size_t idx = v & 0x7fffffffu;
-        if (stride) idx = (idx / n_per_window) * stride + idx % n_per_window;  // window-shifted SRS
+        if (stride) {  // window-shifted SRS: entry w * n_per_window + i -> point w * stride + i
+            const uint32_t w = (uint32_t)idx / n_per_window;
+            uint32_t i = (uint32_t)idx - w * n_per_window;
+            if (blk_lg < 32) i += (i >> blk_lg) << blk_lg;  // blocks of 2^blk_lg at stride 2^(blk_lg+1)
+            idx = (size_t)w * stride + i;
+        }
         const bool phi = glv_n && idx >= glv_n;                               // GLV: phi(G_i)
         if (phi) idx -= glv_n;
         Affine<F> p = aff_load<F>(bases + 4 * idx);
@@ -235,44 +241,48 @@ __global__ __launch_bounds__(256, 4) void k_acc(const uint32_t* keys, const uint
 // 7. final: Horner over the windows (wave 0), hiding term w * S from the table 2^i S (waves 1-4),
 //    XYZZ -> affine -> ark WrappedPoint.
 // ---------------------------------------------------------------------------------------------
+// The hiding term w * S = sum of the 2^i S table entries over the set bits of w (an 8-level tree),
+// -> hide_out (XYZZ).  Launched on the tail stream when the MSM starts, so it runs beside the
+// digit / sort / accumulation phase instead of on the tail's critical path.
 template <class Cv>
-__global__ __launch_bounds__(320) void k_final(const uint4* window_sums, int W, int c,
-                                               const uint4* hide_table /* 256 internal affine 2^i S, or null */,
-                                               const uint4* hide_scalar /* ark or null */, uint4* out_wrapped) {
+__global__ __launch_bounds__(256) void k_hide_term(const uint4* hide_table /* 256 internal affine 2^i S */,
+                                                   const uint4* hide_scalar /* ark */, uint4* hide_out) {
     using F = typename Cv::Base;
     using S = typename Cv::Scalar;
     __shared__ uint4 red[256 * 8];
     __shared__ uint32_t kw[8];
-    const int tid = threadIdx.x;
-    XYZZ<F> horner = xyzz_id<F>();
-    if (tid == 0) {
-        // Horner over the windows; the c doublings per window run in Jacobian coordinates
-        for (int w = W - 1; w >= 0; w--) {
-            if (w != W - 1 && !xyzz_is_id(horner)) {
-                Jac<F> j = jac_from_xyzz(horner);
-                for (int k = 0; k < c; k++) j = jac_dbl(j);
-                horner = jac_to_xyzz(j);
-            }
-            horner = xyzz_add(horner, xyzz_load<F>(window_sums + 8 * w));
-        }
-    }
-    if (tid == 64 && hide_table && hide_scalar) fe_ark_to_canonical_words<S>(hide_scalar, kw);
+    const int i = threadIdx.x;
+    if (i == 0) fe_ark_to_canonical_words<S>(hide_scalar, kw);
     __syncthreads();
-    if (tid >= 64) {
-        const int i = tid - 64;
-        XYZZ<F> v = xyzz_id<F>();
-        if (hide_table && hide_scalar && ((kw[i >> 5] >> (i & 31)) & 1u))
-            v = xyzz_from_aff(aff_load<F>(hide_table + 4 * i));
-        xyzz_store(red + 8 * i, v);
-    }
-    __syncthreads();
+    XYZZ<F> v = xyzz_id<F>();
+    if ((kw[i >> 5] >> (i & 31)) & 1u) v = xyzz_from_aff(aff_load<F>(hide_table + 4 * i));
+    xyzz_store(red + 8 * i, v);
     for (int off = 128; off > 0; off >>= 1) {
-        const int i = tid - 64;
-        if (tid >= 64 && i < off)
-            xyzz_store(red + 8 * i, xyzz_add(xyzz_load<F>(red + 8 * i), xyzz_load<F>(red + 8 * (i + off))));
         __syncthreads();
+        if (i < off) xyzz_store(red + 8 * i, xyzz_add(xyzz_load<F>(red + 8 * i), xyzz_load<F>(red + 8 * (i + off))));
     }
-    if (tid == 0) aff_to_wrapped(out_wrapped, xyzz_to_aff(xyzz_add(horner, xyzz_load<F>(red))));
+    __syncthreads();
+    if (i == 0) xyzz_store(hide_out, xyzz_load<F>(red));
+}
+
+// Horner over the window sums (one lane; the c doublings per window run in Jacobian coordinates),
+// plus the precomputed hiding term (or null), -> affine -> ark WrappedPoint.
+template <class Cv>
+__global__ __launch_bounds__(64) void k_final(const uint4* window_sums, int W, int c, const uint4* hide_xyzz,
+                                              uint4* out_wrapped) {
+    using F = typename Cv::Base;
+    if (threadIdx.x != 0) return;
+    XYZZ<F> horner = xyzz_id<F>();
+    for (int w = W - 1; w >= 0; w--) {
+        if (w != W - 1 && !xyzz_is_id(horner)) {
+            Jac<F> j = jac_from_xyzz(horner);
+            for (int k = 0; k < c; k++) j = jac_dbl(j);
+            horner = jac_to_xyzz(j);
+        }
+        horner = xyzz_add(horner, xyzz_load<F>(window_sums + 8 * w));
+    }
+    if (hide_xyzz) horner = xyzz_add(horner, xyzz_load<F>(hide_xyzz));
+    aff_to_wrapped(out_wrapped, xyzz_to_aff(horner));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -345,7 +355,7 @@ struct MsmScratch {
     const uint32_t* skeys = nullptr;   // sorted keys of the current MSM (sort scratch)
     const uint32_t* scount = nullptr;  // device count of valid entries
     SortScratch sort;
-    hipEvent_t acc_done = nullptr, tail_done = nullptr;
+    hipEvent_t acc_done = nullptr, tail_done = nullptr, start = nullptr;
     bool tail_pending = false;
     hipStream_t owner = nullptr;  // stream the set's last MSM was enqueued on (msm_join)
 };
@@ -395,6 +405,7 @@ static int pipe_init(MsmPipe& P) {
     for (auto& m : P.set) {
         HALO_HIP(hipEventCreateWithFlags(&m.acc_done, hipEventDisableTiming));
         HALO_HIP(hipEventCreateWithFlags(&m.tail_done, hipEventDisableTiming));
+        HALO_HIP(hipEventCreateWithFlags(&m.start, hipEventDisableTiming));
     }
     return HALO_OK;
 }
@@ -408,7 +419,7 @@ constexpr int curve_id() {
 template <class Cv>
 static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, size_t shift_stride,
                         const uint4* scalars_ark, size_t n, int c_req, const uint4* hide_table, const uint4* hide_scalar,
-                        uint4* d_out_wrapped, hipStream_t s, bool async) {
+                        uint4* d_out_wrapped, hipStream_t s, bool async, uint32_t blk_lg = 32) {
     MsmPipe& PP = g_msm_pipe[st->device & 63];
     HALO_CHECK(pipe_init(PP));
     const int set = msm_pick_set(PP, s, true);
@@ -453,7 +464,17 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
     HALO_CHECK(M.seg_acc.reserve((size_t)SW * H * 128));  // row sums
     HALO_CHECK(M.seg_sum.reserve((size_t)SW * L * 128));  // column sums
     HALO_CHECK(M.bits.reserve((size_t)SW * NT * 128));
-    HALO_CHECK(M.window_sums.reserve((size_t)W * 128));
+    HALO_CHECK(M.window_sums.reserve((size_t)(W + 1) * 128));  // + the hiding term's slot
+
+    // the hiding term (k_hide_term) runs on the tail stream beside the accumulation phase
+    uint4* hide_slot = nullptr;
+    if (hide_table && hide_scalar) {
+        hide_slot = M.window_sums.as<uint4>() + 8 * (size_t)W;
+        HALO_HIP(hipEventRecord(M.start, s));
+        HALO_HIP(hipStreamWaitEvent(ts, M.start, 0));
+        hipLaunchKernelGGL(k_hide_term<Cv>, dim3(1), dim3(256), 0, ts, hide_table, hide_scalar, hide_slot);
+        HALO_HIP(hipGetLastError());
+    }
 
     if (n > 0) {
         if (glv)
@@ -470,7 +491,8 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
         ProfScope prof("msm_acc", s);
         HALO_LAUNCH(prof, k_acc<Cv>, dim3(grid_for(nchunks, 256)), dim3(256), 0, s, (const uint32_t*)skeys,
                     (const uint32_t*)svals, scount, K, bases_int, (uint32_t)nn,
-                    (shifted && shift_stride != nn) ? shift_stride : (size_t)0, glv ? (uint32_t)nn : 0u, P_first,
+                    (shifted && (shift_stride != nn || blk_lg < 32)) ? shift_stride : (size_t)0, blk_lg,
+                    glv ? (uint32_t)nn : 0u, P_first,
                     P_last, M.bucket_sums.as<uint4>());
         M.skeys = skeys;
         M.scount = scount;
@@ -512,8 +534,8 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
     ta.hide_scalar = hide_scalar;
     ta.out_wrapped = d_out_wrapped;
     HALO_CHECK(msm_tail_launch(curve_id<Cv>(), ta, ts));
-    hipLaunchKernelGGL(k_final<Cv>, dim3(1), dim3(320), 0, ts, M.window_sums.as<const uint4>(), SW, c, hide_table,
-                       hide_scalar, d_out_wrapped);
+    hipLaunchKernelGGL(k_final<Cv>, dim3(1), dim3(64), 0, ts, M.window_sums.as<const uint4>(), SW, c,
+                       (const uint4*)hide_slot, d_out_wrapped);
     HALO_HIP(hipGetLastError());
     HALO_HIP(hipEventRecord(M.tail_done, ts));
     M.tail_pending = true;
@@ -567,16 +589,20 @@ int msm_srs_device(DeviceState* st, int curve, const void* scalars_ark, size_t n
 
 int msm_srs_range_device(DeviceState* st, int curve, size_t offset, const void* scalars_ark, size_t n,
                          const void* hide_table, const void* hide_scalar, void* d_out_wrapped, hipStream_t s,
-                         bool async) {
+                         bool async, uint32_t blk_lg) {
     SrsState& srs = st->srs[curve];
     if (!srs.shifted_c) return set_error(HALO_EINVAL, "msm_srs_range_device: no window-shifted SRS");
-    if (offset + n > srs.n) return set_error(HALO_ESRSRANGE, "range [%zu, %zu) exceeds the SRS (%zu)", offset, offset + n, srs.n);
+    // highest point touched: offset + map(n - 1), map(i) = i + (i >> blk_lg) << blk_lg
+    const size_t last = n ? (n - 1) + (blk_lg < 32 ? ((n - 1) >> blk_lg) << blk_lg : 0) : 0;
+    if (n && offset + last >= srs.n)
+        return set_error(HALO_ESRSRANGE, "range [%zu, %zu] exceeds the SRS (%zu)", offset, offset + last, srs.n);
+    if (n >= (1u << 31)) return set_error(HALO_EINVAL, "msm_srs_range_device: n too large");
     int rc;
     // window w of point offset + i lives at shifted[w * srs.n + offset + i]: shift the base pointer
     DISPATCH_CURVE(curve, Cv, {
         rc = msm_device_t<Cv>(st, srs.shifted.as<const uint4>() + 4 * offset, true, srs.n, (const uint4*)scalars_ark, n,
                               srs.shifted_c, (const uint4*)hide_table, (const uint4*)hide_scalar,
-                              (uint4*)d_out_wrapped, s, async);
+                              (uint4*)d_out_wrapped, s, async, blk_lg);
     });
     return rc;
 }

@@ -19,9 +19,12 @@ int msm_srs_device(DeviceState* st, int curve, const void* scalars_ark, size_t n
                    void* d_out_wrapped, hipStream_t s, bool async = false);
 // MSM over the resident SRS range [offset, offset + n) with a caller hiding table (2^i P, i < 256,
 // internal affine) and scalar; uses the window-shifted copies (returns HALO_EINVAL without them).
+// blk_lg < 32: scalar i goes with point offset + i + ((i >> blk_lg) << blk_lg), i.e. the blocks
+// [2b B, 2b B + B) (B = 2^blk_lg) of the range -- the even half-blocks an IPA round's G_l / G_r
+// occupy in the unfolded SRS.
 int msm_srs_range_device(DeviceState* st, int curve, size_t offset, const void* scalars_ark, size_t n,
                          const void* hide_table, const void* hide_scalar, void* d_out_wrapped, hipStream_t s,
-                         bool async);
+                         bool async, uint32_t blk_lg = 32);
 int srs_precompute_windows(DeviceState* st, int curve, hipStream_t s);
 int convert_wrapped_to_internal(int curve, const void* in, void* out, size_t n, hipStream_t s);
 int convert_internal_to_wrapped(int curve, const void* in, void* out, size_t n, hipStream_t s);

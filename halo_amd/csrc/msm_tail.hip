@@ -64,19 +64,23 @@ __global__ __launch_bounds__(256) void k_merge(const uint32_t* bstart, const uin
     auto chunk_last = [&](uint32_t t) { return min(cnt, (t + 1) * K) - 1; };
     if (t0 == t1 && keys[(size_t)t0 * K] != b && keys[chunk_last(t0)] != b) return;  // interior: done
     constexpr uint32_t G2 = MSM_GROUP * MSM_GROUP;
-    XYZZ<F> acc = xyzz_id<F>();
-    for (uint32_t t = t0; t <= t1;) {
-        if (t > t0 && t % G2 == 0 && t + G2 <= t1) {
-            acc = xyzz_add(acc, xyzz_load<F>(g2 + 8 * (size_t)(t / G2)));
+    // chunk t0's partial starts the sum (no addition to the identity); the loop picks each further
+    // source first, then runs ONE addition, so lanes that take different sources do not execute
+    // several inlined copies of it
+    XYZZ<F> acc = xyzz_load<F>(((keys[(size_t)t0 * K] == b) ? first : last) + 8 * (size_t)t0);
+    for (uint32_t t = t0 + 1; t <= t1;) {
+        const uint4* src;
+        if (t % G2 == 0 && t + G2 <= t1) {
+            src = g2 + 8 * (size_t)(t / G2);
             t += G2;
-        } else if (t > t0 && t % MSM_GROUP == 0 && t + MSM_GROUP <= t1) {
-            acc = xyzz_add(acc, xyzz_load<F>(g1 + 8 * (size_t)(t / MSM_GROUP)));
+        } else if (t % MSM_GROUP == 0 && t + MSM_GROUP <= t1) {
+            src = g1 + 8 * (size_t)(t / MSM_GROUP);
             t += MSM_GROUP;
         } else {
-            const uint4* src = (keys[(size_t)t * K] == b) ? first : last;
-            acc = xyzz_add(acc, xyzz_load<F>(src + 8 * (size_t)t));
+            src = ((keys[(size_t)t * K] == b) ? first : last) + 8 * (size_t)t;
             t++;
         }
+        acc = xyzz_add(acc, xyzz_load<F>(src));
     }
     xyzz_store(bucket_sums + 8 * b, acc);
 }

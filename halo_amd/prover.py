@@ -279,15 +279,24 @@ def naive_prover(B, wit, n: int, chal: Challenges, acc_prev=None):
     r_omega = geometric_polys(B, zeta, wit["ws"][0:3] + [z])
     xi = chal()
     omega = B.omega(n)
-    q_r, q_r_omega = instances_open(B, [(r, xi), (r_omega, xi * omega % m)], d)
     if acc_prev is None:
         acc_prev = synthetic_accumulator(B, n, chal)
+    B.sync()
+    t5a = time.perf_counter()
+    q_r, q_r_omega = instances_open(B, [(r, xi), (r_omega, xi * omega % m)], d)
+    B.sync()
+    t5b = time.perf_counter()
     acc_next = acc_prover(B, [acc_prev, q_r, q_r_omega], d, chal)
+    B.sync()
+    t5c = time.perf_counter()
     at_xi = wit["ws"] + wit["rs"] + wit["qs"] + ts + wit["ids"] + wit["sigmas"] + [z] + w_omegas
     vs = B.eval_many(at_xi, xi)
     vs.append(B.eval_many([z], xi * omega % m)[0])
     B.sync()
     times["round5"] = time.perf_counter() - t5
+    times["r5_open"] = t5b - t5a    # two Instance::open (concurrent openings)
+    times["r5_acc"] = t5c - t5b     # acc::prover (h(X), one opening)
+    times["r5_other"] = times["round5"] - times["r5_open"] - times["r5_acc"]
     times["total"] = time.perf_counter() - t0
     return {
         "C_ws": C_ws, "C_z": C_z, "C_ts": C_ts, "vs": vs,

@@ -73,22 +73,30 @@ def test_permutation_accumulator_scan_large(hal):
     torch.cuda.synchronize()
 
 
-@pytest.mark.parametrize("logn,windows", [(12, False), (13, False), (13, True)])
-def test_ipa_open_tail_switch_vs_c_restatement(hal, logn, windows):
-    """An SRS-based opening longer than the tail threshold (2048): ordinary rounds (MSM L/R + GLV
-    fold) switch to the tail rounds (direct sums over G0 with fold weights) mid-opening; Ls, Rs, U, c
-    against the C restatement of pcdl.rs:404-438."""
+@pytest.mark.parametrize("curve,logn,mode", [
+    ("pallas", 12, "fold"), ("pallas", 13, "fold"), ("pallas", 13, "fold_srs_round0"),
+    ("pallas", 12, "weighted"), ("pallas", 14, "weighted"), ("vesta", 13, "weighted"),
+])
+def test_ipa_open_tail_switch_vs_c_restatement(hal, monkeypatch, curve, logn, mode):
+    """An SRS-based opening longer than the tail threshold (2048), against the C restatement of
+    pcdl.rs:404-438 (Ls, Rs, U, c).  fold: ordinary rounds (MSM L/R + GLV fold of G) switch to the
+    tail rounds (direct sums over G0 with fold weights) mid-opening; fold_srs_round0: the same with
+    round 1's L / R on the resident window-shifted SRS (ranges [0, m), [m, 2m)); weighted (the default
+    with the shifted SRS): G is never folded, every round's L / R are block-mapped MSMs over the
+    shifted SRS with scalars c * w, and U = sum w[u] G[u] at the end."""
     from prover_ref import CRefBackend
 
     n = 1 << logn
     L = hal.load()
-    hal.check(L.halo_srs_synthesize(0, n, 777 + logn))
-    if windows:  # round 1's L / R then run on the resident window-shifted SRS (SRS ranges [0, m), [m, 2m))
-        hal.check(L.halo_srs_precompute_windows(0))
+    cid = hal.CURVES[curve]
+    hal.check(L.halo_srs_synthesize(cid, n, 777 + logn))
+    if mode != "fold":
+        hal.check(L.halo_srs_precompute_windows(cid))
+    monkeypatch.setenv("HALO_IPA_WEIGHTED", "1" if mode == "weighted" else "0")
     srs = np.zeros((n, 8), dtype=np.uint64)
-    hal.check(L.halo_srs_read(0, 0, n, hal.ptr(srs)))
-    dev = prover.DeviceBackend("pallas")
-    ref = CRefBackend("pallas", srs, srs[1])
+    hal.check(L.halo_srs_read(cid, 0, n, hal.ptr(srs)))
+    dev = prover.DeviceBackend(curve)
+    ref = CRefBackend(curve, srs, srs[1])
     rng = np.random.default_rng(logn)
     p_dev = dev.random_vec(n, rng)
     p_ref = p_dev.cpu().numpy().view(np.uint64).copy()

@@ -12,11 +12,11 @@ rm -rf $O && mkdir -p $O
 timeout -k 10 400 python bench.py > $O/bench_full.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
 tail -n 1 $O/bench_full.json > $O/bench.json
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 bench.py --no-cpu --sizes "" --ipa 0 > $O/trace.log 2>&1 || { tail -20 $O/trace.log; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 bench.py --no-cpu --sizes "" --ipa 0 --prove 0 > $O/trace.log 2>&1 || { tail -20 $O/trace.log; exit 1; }
 cp $(find $O/trace -name "*kernel_stats.csv" | head -1) $O/kernel_stats.csv
 grep '^{' $O/trace.log | tail -n 1 > $O/bench_traced.json
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_f -o run -- python3 bench.py --no-cpu --sizes "" --ipa 0 --steps 3 --warmup 1 > /dev/null 2>&1 || exit 1
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_w -o run -- python3 bench.py --no-cpu --sizes "" --ipa 0 --steps 3 --warmup 1 > /dev/null 2>&1 || exit 1
-python3 tools/make_pmc_summary.py $O/pmc_f $O/pmc_w $O/pmc_summary.json "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes) of 'python3 bench.py --no-cpu --sizes \"\" --ipa 0 --steps 3 --warmup 1', ${tag}" > /dev/null
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_f -o run -- python3 bench.py --no-cpu --sizes "" --ipa 0 --prove 0 --steps 3 --warmup 1 > /dev/null 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_w -o run -- python3 bench.py --no-cpu --sizes "" --ipa 0 --prove 0 --steps 3 --warmup 1 > /dev/null 2>&1 || exit 1
+python3 tools/make_pmc_summary.py $O/pmc_f $O/pmc_w $O/pmc_summary.json "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes) of 'python3 bench.py --no-cpu --sizes \"\" --ipa 0 --prove 0 --steps 3 --warmup 1', ${tag}" > /dev/null
 rm -rf $O/trace $O/pmc_f/*/ $O/pmc_w/*/ 2>/dev/null
 python3 tools/kstats.py $O/kernel_stats.csv > $O/kstats.txt; head -n 30 $O/kstats.txt

@@ -40,9 +40,9 @@ for lg in [int(x) for x in (sys.argv[1:] or ['16', '20'])]:
             c = time.perf_counter()
             t_lr += b - a; t_fold += c - b
             per.append((round(1e3 * (b - a), 2), round(1e3 * (c - b), 2)))
-        t1 = time.perf_counter()
         U = np.zeros(8, dtype=np.uint64); c0 = np.zeros(4, dtype=np.uint64)
-        H.check(L.halo_ipa_end(s, H.ptr(U), H.ptr(c0)))
+        H.check(L.halo_ipa_end(s, H.ptr(U), H.ptr(c0)))  # weighted rounds: U is one more MSM
+        t1 = time.perf_counter()
         nl = ctypes.c_size_t(0); ms = ctypes.c_double(0)
         H.check(L.halo_profile_read(b"ipa_fold", ctypes.byref(nl), ctypes.byref(ms)))
         H.check(L.halo_profile_enable(0))
