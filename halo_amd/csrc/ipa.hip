@@ -275,10 +275,12 @@ template <class Cv>
 __global__ __launch_bounds__(64) void k_pow2_xyzz_from_wrapped(const uint4* P_wrapped, uint4* out_xyzz, int count) {
     using F = typename Cv::Base;
     if (threadIdx.x != 0) return;
-    XYZZ<F> p = xyzz_from_aff(aff_from_wrapped<F>(P_wrapped));
+    // the doubling chain runs in Jacobian coordinates (dbl-2009-l: 1M + 5S, vs 6M + 3S in XYZZ); the
+    // per-entry XYZZ conversion (Z^2, Z^3) is off the chain's dependency path
+    Jac<F> j = jac_from_xyzz(xyzz_from_aff(aff_from_wrapped<F>(P_wrapped)));
     for (int i = 0; i < count; i++) {
-        xyzz_store(out_xyzz + 8 * i, p);
-        p = xyzz_dbl(p);
+        xyzz_store(out_xyzz + 8 * i, jac_to_xyzz(j));
+        j = jac_dbl(j);
     }
 }
 
@@ -331,11 +333,11 @@ constexpr size_t IPA_TAIL_N = 2048;
 constexpr int TAIL_WIN = 32, TAIL_THREADS = 256;
 
 template <class Cv>
-__global__ __launch_bounds__(64) void k_tail_table(const uint4* gs, size_t n0, uint4* table) {
+__global__ __launch_bounds__(64) void k_tail_table(const uint4* gs, int gs_xyzz, size_t n0, uint4* table) {
     using F = typename Cv::Base;
     const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n0) return;
-    XYZZ<F> p = xyzz_from_aff(aff_load<F>(gs + 4 * k));
+    XYZZ<F> p = gs_xyzz ? xyzz_load<F>(gs + 8 * k) : xyzz_from_aff(aff_load<F>(gs + 4 * k));
     for (int w = 0; w < TAIL_WIN; w++) {
         xyzz_store(table + 8 * ((size_t)w * n0 + k), p);
         if (w + 1 < TAIL_WIN)
@@ -419,21 +421,14 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail_final(const uint4* part, 
     __shared__ uint4 sum_s[8];
     __shared__ uint32_t kw[8];
     const int tid = threadIdx.x, b = blockIdx.x;
-    XYZZ<F> acc = xyzz_id<F>();
+    if (htab && tid == 0) fe_ark_to_canonical_words<S>(dots_ark + 2 * b, kw);
+    __syncthreads();
+    // lane tid: its partials plus, for bit tid of dot_b, the table entry 2^tid H' -- one tree
+    XYZZ<F> acc = (htab && ((kw[tid >> 5] >> (tid & 31)) & 1u)) ? xyzz_from_aff(aff_load<F>(htab + 4 * tid))
+                                                               : xyzz_id<F>();
     for (int i = tid; i < nblk; i += TAIL_THREADS) acc = xyzz_add(acc, xyzz_load<F>(part + 8 * (2 * (size_t)i + b)));
     tail_tree<F>(red, tid, acc, sum_s);
-    XYZZ<F> hv = xyzz_id<F>();
-    if (htab) {
-        if (tid == 0) fe_ark_to_canonical_words<S>(dots_ark + 2 * b, kw);
-        __syncthreads();
-        if ((kw[tid >> 5] >> (tid & 31)) & 1u) hv = xyzz_from_aff(aff_load<F>(htab + 4 * tid));
-        tail_tree<F>(red, tid, hv, red + 8 * TAIL_THREADS - 8);  // slot read back below
-    }
-    if (tid == 0) {
-        XYZZ<F> r = xyzz_load<F>(sum_s);
-        if (htab) r = xyzz_add(r, xyzz_load<F>(red + 8 * TAIL_THREADS - 8));
-        aff_to_wrapped(out_wrapped + 4 * b, xyzz_to_aff(r));
-    }
+    if (tid == 0) aff_to_wrapped(out_wrapped + 4 * b, xyzz_to_aff(xyzz_load<F>(sum_s)));
 }
 
 template <class S>
@@ -489,9 +484,11 @@ struct halo_ipa_session {
     // tail rounds (length <= IPA_TAIL_N, sessions over the SRS only): see k_tail_table
     bool allow_tail = false, tail = false;
     bool srs_round0 = false;  // G is still the SRS prefix (no fold yet): L/R on the resident shifted SRS
+    bool gs_xyzz = false;     // gs holds XYZZ points (materialised for the tail table only)
     bool weighted = false;    // G is never folded: L/R over the resident shifted SRS (k_weighted_scalars)
     size_t n0 = 0, wlen = 0;
     DevBuf table, w[2], scal, side, part;
+    BatchScratch mat;  // weighted -> tail switch (msm_shared_batch)
     int wcur = 0;
     uint8_t* pinned = nullptr;  // 128 B L|R (D2H) + 64 B xi|xi_inv (H2D): async copies, several sessions in flight
     ~halo_ipa_session() {
@@ -688,6 +685,15 @@ static size_t ipa_tail_n() {
     return tail_n;
 }
 
+// Length at which weighted rounds materialise G = sum_u w[u] SRS[i + u len] (one batched MSM with
+// the fold weights as shared scalars, msm_shared_batch) and continue as tail rounds: a weighted
+// round costs two n/2-term MSMs whatever the length, a tail round at this length ~0.6 ms.
+constexpr size_t IPA_MAT_N = 1024;
+static size_t ipa_mat_n() {
+    const char* e = getenv("HALO_IPA_MAT_N");  // A/B knob (read per round); 0 keeps the weighted rounds to the end
+    return e ? (size_t)atoll(e) : IPA_MAT_N;
+}
+
 static int ipa_begin(halo_curve_t curve, size_t n, const halo_wrapped_point_t* gs_host, const halo_fe_t* cs,
                      const halo_fe_t* zs_host, const halo_fe_t* z, const halo_wrapped_point_t* H_prime,
                      halo_ipa_session** out, bool cs_on_device = false) {
@@ -821,7 +827,8 @@ static int ipa_enter_tail(halo_ipa_session* ses, hipStream_t s) {
     HALO_CHECK(ses->side.reserve(n0));
     HALO_CHECK(ses->part.reserve(nblk * 2 * 128));
     DISPATCH_CURVE(ses->curve, Cv, {
-        hipLaunchKernelGGL(k_tail_table<Cv>, dim3(gridn(n0, 64)), dim3(64), 0, s, ses->gs.as<const uint4>(), n0,
+        hipLaunchKernelGGL(k_tail_table<Cv>, dim3(gridn(n0, 64)), dim3(64), 0, s, ses->gs.as<const uint4>(),
+                           (int)ses->gs_xyzz, n0,
                            ses->table.as<uint4>());
         hipLaunchKernelGGL(k_set_one_ark<typename Cv::Scalar>, dim3(1), dim3(64), 0, s, ses->w[0].as<uint4>());
     });
@@ -862,8 +869,19 @@ static int ipa_round_launch(DeviceState* st, halo_ipa_session* ses) {
     char* sm = (char*)ses->small.ptr;  // [0,32) z, [64,128) H', [128,160) dot_l, [160,192) dot_r, [256,320) L, [320,384) R
     const char* cs = ses->cs.as<const char>();
     const char* zs = ses->zs.as<const char>();
-    const char* gs = ses->gs.as<const char>();
+    if (ses->weighted && 2 * m <= ipa_mat_n()) {
+        // G (length 2m) = sum_u w[u] SRS[i + u 2m]: from here on an ordinary (tail) session
+        const char* e = getenv("HALO_IPA_TAIL");
+        ses->allow_tail = !(e && e[0] == '0');
+        const bool to_tail = ses->allow_tail && 2 * m <= ipa_tail_n();  // the tail table reads XYZZ directly
+        HALO_CHECK(ses->gs.reserve(2 * m * 128));
+        HALO_CHECK(msm_shared_batch(st, ses->curve, st->srs[ses->curve].gs.ptr, ses->w[ses->wcur].ptr, ses->wlen,
+                                    2 * m, ses->gs.ptr, to_tail, ses->mat, s));
+        ses->gs_xyzz = to_tail;
+        ses->weighted = false;
+    }
     if (!ses->tail && ses->allow_tail && 2 * m <= ipa_tail_n()) HALO_CHECK(ipa_enter_tail(ses, s));
+    const char* gs = ses->gs.as<const char>();  // (materialised above in a weighted session)
     HALO_CHECK(dot_device(sf, cs + m * 32, zs, m, sm + 128, ses->tmp.ptr, s));        // <c_r, z_l>
     HALO_CHECK(dot_device(sf, cs, zs + m * 32, m, sm + 160, ses->tmp.ptr, s));        // <c_l, z_r>
     if (ses->tail) {

@@ -607,6 +607,181 @@ int msm_srs_range_device(DeviceState* st, int curve, size_t offset, const void* 
     return rc;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Batched MSM with shared scalars (the IPA's switch from weighted to tail rounds, ipa.hip):
+//   out[i] = sum_{u < T} w[u] bases[i + u len],  i < len.
+// Every output has the same digit lists, so there is no sort: one workgroup groups the (window,
+// scalar) digits by bucket (counting sort in LDS, k_batch_lists), and k_batch_expand replicates that
+// order for every output (key = (i W + win) B + b, value = base index i + u len) -- exactly the
+// sorted layout k_acc and the reduction tail take, with SW = len W windows of B buckets.  A batched
+// Horner (one lane per output) finishes.
+// ---------------------------------------------------------------------------------------------
+constexpr int BATCH_C_MAX = 8;  // window bits: at most 32 windows of 128 buckets
+
+__global__ __launch_bounds__(256) void k_batch_lists(const uint32_t* digits, uint32_t T, int W, uint32_t B,
+                                                     uint32_t len, uint32_t* ent, uint32_t* ekey, uint32_t* tot) {
+    __shared__ uint32_t cnt[(1 << (BATCH_C_MAX - 1)) + 1];
+    __shared__ uint32_t base;
+    const uint32_t tid = threadIdx.x;
+    if (tid == 0) base = 0;
+    for (int w = 0; w < W; w++) {
+        for (uint32_t b = tid; b < B; b += blockDim.x) cnt[b] = 0;
+        __syncthreads();
+        for (uint32_t u = tid; u < T; u += blockDim.x) {
+            const uint32_t d = digits[(size_t)w * T + u];
+            if (d != DIGIT_NONE) atomicAdd(&cnt[d & 0x7fffffffu], 1u);
+        }
+        __syncthreads();
+        if (tid == 0) {  // exclusive scan over the B buckets, continuing after the previous windows
+            uint32_t run = base;
+            for (uint32_t b = 0; b < B; b++) {
+                const uint32_t c = cnt[b];
+                cnt[b] = run;
+                run += c;
+            }
+            cnt[B] = run;
+        }
+        __syncthreads();
+        for (uint32_t u = tid; u < T; u += blockDim.x) {
+            const uint32_t d = digits[(size_t)w * T + u];
+            if (d == DIGIT_NONE) continue;
+            const uint32_t b = d & 0x7fffffffu;
+            const uint32_t pos = atomicAdd(&cnt[b], 1u);
+            ent[pos] = u | (d & 0x80000000u);
+            ekey[pos] = (uint32_t)w * B + b;
+        }
+        __syncthreads();
+        if (tid == 0) base = cnt[B];
+        __syncthreads();
+    }
+    if (tid == 0) {
+        tot[0] = base;        // entries per output
+        tot[1] = base * len;  // entries in total (k_acc's count)
+    }
+}
+
+__global__ __launch_bounds__(256) void k_batch_expand(const uint32_t* ent, const uint32_t* ekey, const uint32_t* tot,
+                                                      uint32_t len, uint32_t WB, uint32_t* keys, uint32_t* vals) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t per = tot[0];
+    if (per == 0 || p >= per * len) return;
+    const uint32_t i = p / per, r = p - i * per;
+    const uint32_t e = ent[r];
+    keys[p] = i * WB + ekey[r];
+    vals[p] = (i + (e & 0x7fffffffu) * len) | (e & 0x80000000u);
+}
+
+template <class Cv>
+__global__ __launch_bounds__(64) void k_batch_horner(const uint4* window_sums, uint32_t len, int W, int c,
+                                                     uint4* out, int xyzz_out) {
+    using F = typename Cv::Base;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= len) return;
+    const uint4* ws = window_sums + 8 * (size_t)i * W;
+    XYZZ<F> h = xyzz_id<F>();
+    for (int w = W - 1; w >= 0; w--) {
+        if (w != W - 1 && !xyzz_is_id(h)) {
+            Jac<F> j = jac_from_xyzz(h);
+            for (int k = 0; k < c; k++) j = jac_dbl(j);
+            h = jac_to_xyzz(j);
+        }
+        h = xyzz_add(h, xyzz_load<F>(ws + 8 * w));
+    }
+    if (xyzz_out)
+        xyzz_store(out + 8 * (size_t)i, h);
+    else
+        aff_store(out + 4 * (size_t)i, xyzz_to_aff(h));
+}
+
+template <class Cv>
+static int msm_shared_batch_t(DeviceState* st, const uint4* bases, const uint4* w_ark, size_t T, size_t len,
+                              uint4* out, bool xyzz_out, BatchScratch& S, hipStream_t s) {
+    // window bits: about T / 4 buckets per window, so that the per-window reduction (2 B additions)
+    // stays below the accumulation (T mixed additions)
+    const int c = std::max(5, std::min(BATCH_C_MAX, (int)ilog2(std::max<size_t>(T, 2)) - 1)), W = msm_windows(c);
+    const uint32_t B = 1u << (c - 1);
+    const size_t SW = len * (size_t)W, NB = SW * B, E = SW * T;
+    if (!T || !len) return set_error(HALO_EINVAL, "msm_shared_batch: empty batch");
+    if (E >= (1ull << 32) || T * len >= (1ull << 31))
+        return set_error(HALO_EINVAL, "msm_shared_batch: batch too large (len %zu, T %zu)", len, T);
+    const uint32_t L = std::min<uint32_t>(MSM_SEG_L, B), logL = ilog2(L), H = B / L, logH = ilog2(H);
+    const uint32_t NT = 1 + logH + logL;
+    const size_t lanes = (size_t)st->num_cu * 16 * 64 * 4;
+    const uint32_t K = (uint32_t)std::max<size_t>(16, std::min<size_t>(64, (E + lanes - 1) / lanes));
+    const size_t nchunks = (E + K - 1) / K;
+    const size_t ng1 = nchunks / MSM_GROUP, ng2 = nchunks / (MSM_GROUP * MSM_GROUP);
+    HALO_CHECK(S.digits.reserve((size_t)W * T * 4));
+    HALO_CHECK(S.lists.reserve((size_t)W * T * 8 + 16));
+    HALO_CHECK(S.keys.reserve(E * 4));
+    HALO_CHECK(S.vals.reserve(E * 4));
+    HALO_CHECK(S.bstart.reserve((NB + 1) * 4));
+    HALO_CHECK(S.partials.reserve((nchunks * 2 + ng1 + ng2 + 2) * 128));
+    HALO_CHECK(S.bucket_sums.reserve(NB * 128));
+    HALO_CHECK(S.window_sums.reserve(SW * 128));
+    uint32_t* ent = S.lists.as<uint32_t>();
+    uint32_t* ekey = ent + (size_t)W * T;
+    uint32_t* tot = ekey + (size_t)W * T;
+    uint4* P_first = S.partials.as<uint4>();
+    uint4* P_last = P_first + 8 * nchunks;
+    uint4* P_g1 = P_last + 8 * nchunks;
+    uint4* P_g2 = P_g1 + 8 * (ng1 + 1);
+
+    hipLaunchKernelGGL(k_digits<typename Cv::Scalar>, dim3(grid_for(T, 256)), dim3(256), 0, s, w_ark, T, c, W,
+                       S.digits.as<uint32_t>());
+    hipLaunchKernelGGL(k_batch_lists, dim3(1), dim3(256), 0, s, S.digits.as<const uint32_t>(), (uint32_t)T, W, B,
+                       (uint32_t)len, ent, ekey, tot);
+    hipLaunchKernelGGL(k_batch_expand, dim3(grid_for(E, 256)), dim3(256), 0, s, (const uint32_t*)ent,
+                       (const uint32_t*)ekey, (const uint32_t*)tot, (uint32_t)len, (uint32_t)(W * B),
+                       S.keys.as<uint32_t>(), S.vals.as<uint32_t>());
+    hipLaunchKernelGGL(k_acc<Cv>, dim3(grid_for(nchunks, 256)), dim3(256), 0, s, S.keys.as<const uint32_t>(),
+                       S.vals.as<const uint32_t>(), (const uint32_t*)(tot + 1), K, bases, 1u, (size_t)0, 32u, 0u,
+                       P_first, P_last, S.bucket_sums.as<uint4>());
+    HALO_HIP(hipGetLastError());
+    MsmTailArgs ta;
+    ta.n = T;
+    ta.skeys = S.keys.as<const uint32_t>();
+    ta.scount = tot + 1;
+    ta.K = K;
+    ta.NB = NB;
+    ta.E = E;
+    ta.first = P_first;
+    ta.last = P_last;
+    ta.g1 = P_g1;
+    ta.g2 = P_g2;
+    ta.ng1 = ng1;
+    ta.ng2 = ng2;
+    ta.bstart = S.bstart.as<uint32_t>();
+    ta.bucket_sums = S.bucket_sums.as<uint4>();
+    ta.rows = ta.cols = ta.terms = nullptr;  // k_batch_window_sums needs no grid scratch
+    ta.window_sums = S.window_sums.as<uint4>();
+    ta.L = L;
+    ta.H = H;
+    ta.logH = logH;
+    ta.logL = logL;
+    ta.NT = NT;
+    ta.SW = (int)SW;
+    ta.c = c;
+    ta.hide_table = nullptr;
+    ta.hide_scalar = nullptr;
+    ta.out_wrapped = nullptr;
+    ta.batch_windows = true;
+    HALO_CHECK(msm_tail_launch(curve_id<Cv>(), ta, s));
+    hipLaunchKernelGGL(k_batch_horner<Cv>, dim3(grid_for(len, 64)), dim3(64), 0, s, S.window_sums.as<const uint4>(),
+                       (uint32_t)len, W, c, out, (int)xyzz_out);
+    HALO_HIP(hipGetLastError());
+    return HALO_OK;
+}
+
+int msm_shared_batch(DeviceState* st, int curve, const void* bases_int, const void* w_ark, size_t T, size_t len,
+                     void* out, bool xyzz_out, BatchScratch& S, hipStream_t s) {
+    int rc;
+    DISPATCH_CURVE(curve, Cv, {
+        rc = msm_shared_batch_t<Cv>(st, (const uint4*)bases_int, (const uint4*)w_ark, T, len, (uint4*)out, xyzz_out,
+                                    S, s);
+    });
+    return rc;
+}
+
 int convert_wrapped_to_internal(int curve, const void* in, void* out, size_t n, hipStream_t s) {
     if (!n) return HALO_OK;
     DISPATCH_CURVE(curve, Cv, {

@@ -25,6 +25,14 @@ int msm_srs_device(DeviceState* st, int curve, const void* scalars_ark, size_t n
 int msm_srs_range_device(DeviceState* st, int curve, size_t offset, const void* scalars_ark, size_t n,
                          const void* hide_table, const void* hide_scalar, void* d_out_wrapped, hipStream_t s,
                          bool async, uint32_t blk_lg = 32);
+// Batched MSM with shared scalars: out[i] = sum_{u < T} w[u] bases[i + u len] for i < len
+// (internal affine bases, ark scalars; outputs internal affine, or XYZZ (128 B) when xyzz_out;
+// stream-ordered on s).
+struct BatchScratch {
+    DevBuf digits, lists, keys, vals, bstart, partials, bucket_sums, window_sums;
+};
+int msm_shared_batch(DeviceState* st, int curve, const void* bases_int, const void* w_ark, size_t T, size_t len,
+                     void* out, bool xyzz_out, BatchScratch& S, hipStream_t s);
 int srs_precompute_windows(DeviceState* st, int curve, hipStream_t s);
 int convert_wrapped_to_internal(int curve, const void* in, void* out, size_t n, hipStream_t s);
 int convert_internal_to_wrapped(int curve, const void* in, void* out, size_t n, hipStream_t s);
@@ -48,6 +56,7 @@ struct MsmTailArgs {
     const uint4* hide_table;
     const uint4* hide_scalar;
     uint4* out_wrapped;
+    bool batch_windows = false;  // SW windows of 128 buckets: k_batch_window_sums instead of the grid reduction
 };
 int msm_tail_launch(int curve, const MsmTailArgs& a, hipStream_t ts);
 

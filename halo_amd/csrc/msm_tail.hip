@@ -186,6 +186,48 @@ __global__ __launch_bounds__(64) void k_bitcombine(const uint4* terms, uint32_t 
     if (k == 0) xyzz_store(window_sums + 8 * w, xyzz_load<F>(red));
 }
 
+// Many small windows (msm_shared_batch: SW = len * W windows of B = 16..128 buckets): 8 lanes per
+// window, lane k owns the G = B / 8 buckets [G k, G k + G): a running sum gives R = sum B_b and
+// S = sum (b - G k + 1) B_b over the segment (2 G additions), the lane adds G k R (lg G doublings
+// and a 3-bit multiple), and a 3-level tree over the 8 lanes gives sum_b (b + 1) B_b.
+constexpr uint32_t BATCH_SEGS = 8;
+template <class Cv>
+__global__ __launch_bounds__(256) void k_batch_window_sums(const uint4* bucket_sums, uint32_t SW, uint32_t B,
+                                                           uint4* window_sums) {
+    using F = typename Cv::Base;
+    __shared__ uint4 red[256 * 8];
+    const uint32_t tid = threadIdx.x;
+    const size_t t = (size_t)blockIdx.x * blockDim.x + tid;
+    const uint32_t k = tid % BATCH_SEGS, G = B / BATCH_SEGS;
+    const size_t w = t / BATCH_SEGS;
+    XYZZ<F> v = xyzz_id<F>();
+    if (w < SW) {
+        const uint4* bs = bucket_sums + 8 * (w * B + (size_t)k * G);
+        XYZZ<F> R = xyzz_id<F>(), S = xyzz_id<F>();
+        for (int j = (int)G - 1; j >= 0; j--) {
+            R = xyzz_add(R, xyzz_load<F>(bs + 8 * j));
+            S = xyzz_add(S, R);
+        }
+        if (k) {
+            XYZZ<F> X = R;
+            for (uint32_t g = G; g > 1; g >>= 1) X = xyzz_dbl(X);  // G R
+            XYZZ<F> Y = xyzz_id<F>();
+            for (int bit = 2; bit >= 0; bit--) {
+                Y = xyzz_dbl(Y);
+                if ((k >> bit) & 1u) Y = xyzz_add(Y, X);
+            }
+            S = xyzz_add(S, Y);
+        }
+        v = S;
+    }
+    xyzz_store(red + 8 * tid, v);
+    for (uint32_t off = BATCH_SEGS / 2; off > 0; off >>= 1) {
+        __syncthreads();
+        if (k < off) xyzz_store(red + 8 * tid, xyzz_add(xyzz_load<F>(red + 8 * tid), xyzz_load<F>(red + 8 * (tid + off))));
+    }
+    __syncthreads();
+    if (k == 0 && w < SW) xyzz_store(window_sums + 8 * w, xyzz_load<F>(red + 8 * tid));
+}
 
 static unsigned grid_for_t(size_t n, unsigned thr) { return (unsigned)std::max<size_t>(1, (n + thr - 1) / thr); }
 
@@ -202,6 +244,15 @@ static int tail_launch_t(const MsmTailArgs& a, hipStream_t ts) {
         hipLaunchKernelGGL(k_merge<Cv>, dim3(grid_for_t(a.NB, 256)), dim3(256), 0, ts, (const uint32_t*)a.bstart,
                            a.skeys, a.scount, a.K, a.NB, (const uint4*)a.first, (const uint4*)a.last,
                            (const uint4*)a.g1, (const uint4*)a.g2, a.bucket_sums);
+        if (a.batch_windows) {
+            const uint32_t B = a.L * a.H;
+            if (B < 2 * BATCH_SEGS || B > 1024 || (B & (B - 1)))
+                return set_error(HALO_EINVAL, "batched window sums: %u buckets per window", B);
+            hipLaunchKernelGGL(k_batch_window_sums<Cv>, dim3(grid_for_t((size_t)a.SW * BATCH_SEGS, 256)), dim3(256), 0, ts,
+                               (const uint4*)a.bucket_sums, (uint32_t)a.SW, B, a.window_sums);
+            HALO_HIP(hipGetLastError());
+            return HALO_OK;
+        }
         const uint32_t nrb = (a.H + (256 / a.L) - 1) / (256 / a.L);
         hipLaunchKernelGGL(k_rowcol<Cv>, dim3(nrb + a.L, a.SW), dim3(256), 0, ts, (const uint4*)a.bucket_sums, a.L,
                            a.H, a.rows, a.cols);

@@ -76,6 +76,7 @@ def test_permutation_accumulator_scan_large(hal):
 @pytest.mark.parametrize("curve,logn,mode", [
     ("pallas", 12, "fold"), ("pallas", 13, "fold"), ("pallas", 13, "fold_srs_round0"),
     ("pallas", 12, "weighted"), ("pallas", 14, "weighted"), ("vesta", 13, "weighted"),
+    ("pallas", 13, "weighted_to_end"), ("pallas", 15, "weighted"), ("pallas", 12, "weighted_fold_after"),
 ])
 def test_ipa_open_tail_switch_vs_c_restatement(hal, monkeypatch, curve, logn, mode):
     """An SRS-based opening longer than the tail threshold (2048), against the C restatement of
@@ -83,7 +84,9 @@ def test_ipa_open_tail_switch_vs_c_restatement(hal, monkeypatch, curve, logn, mo
     tail rounds (direct sums over G0 with fold weights) mid-opening; fold_srs_round0: the same with
     round 1's L / R on the resident window-shifted SRS (ranges [0, m), [m, 2m)); weighted (the default
     with the shifted SRS): G is never folded, every round's L / R are block-mapped MSMs over the
-    shifted SRS with scalars c * w, and U = sum w[u] G[u] at the end."""
+    shifted SRS with scalars c * w until the length reaches 1024, where G is materialised by one
+    batched shared-scalar MSM and the tail rounds finish; weighted_to_end: no switch, U = sum w[u] G[u]
+    at the end; weighted_fold_after: the materialised G continues with ordinary rounds."""
     from prover_ref import CRefBackend
 
     n = 1 << logn
@@ -92,7 +95,11 @@ def test_ipa_open_tail_switch_vs_c_restatement(hal, monkeypatch, curve, logn, mo
     hal.check(L.halo_srs_synthesize(cid, n, 777 + logn))
     if mode != "fold":
         hal.check(L.halo_srs_precompute_windows(cid))
-    monkeypatch.setenv("HALO_IPA_WEIGHTED", "1" if mode == "weighted" else "0")
+    monkeypatch.setenv("HALO_IPA_WEIGHTED", "1" if mode.startswith("weighted") else "0")
+    if mode == "weighted_to_end":  # no switch to the tail rounds: U = sum w[u] G[u] over the SRS
+        monkeypatch.setenv("HALO_IPA_MAT_N", "0")
+    if mode == "weighted_fold_after":  # materialised G (affine) continues with L/R MSMs + GLV folds
+        monkeypatch.setenv("HALO_IPA_TAIL", "0")
     srs = np.zeros((n, 8), dtype=np.uint64)
     hal.check(L.halo_srs_read(cid, 0, n, hal.ptr(srs)))
     dev = prover.DeviceBackend(curve)
