@@ -330,6 +330,7 @@ static int dot_device(int field, const void* x, const void* y, size_t n, void* o
 // double-and-add (~16 dependent curve operations), then block trees.  U = sum_u w[u] G0[u] at the end.
 // c and z keep their ordinary elementwise folds (pcdl.rs:430-435).
 constexpr size_t IPA_TAIL_N = 2048;
+constexpr int IPA_HTAB = 128;  // entries 2^i H' of the session's hiding table (GLV split of the scalar)
 constexpr int TAIL_WIN = 32, TAIL_THREADS = 256;
 
 template <class Cv>
@@ -420,12 +421,29 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail_final(const uint4* part, 
     __shared__ uint4 red[TAIL_THREADS * 8];
     __shared__ uint4 sum_s[8];
     __shared__ uint32_t kw[8];
+    __shared__ uint32_t neg[2];
     const int tid = threadIdx.x, b = blockIdx.x;
-    if (htab && tid == 0) fe_ark_to_canonical_words<S>(dots_ark + 2 * b, kw);
+    if (htab && tid == 0) {  // dot_b = k1 + lambda k2: lanes 0-127 k1 with 2^i H', 128-255 k2 with phi(2^i H')
+        uint32_t w8[8], k1[5], k2[5];
+        bool n1, n2;
+        fe_ark_to_canonical_words<S>(dots_ark + 2 * b, w8);
+        glv::decompose<typename Cv::K>(w8, n1, k1, n2, k2);
+        for (int q = 0; q < 4; q++) {
+            kw[q] = k1[q];
+            kw[4 + q] = k2[q];
+        }
+        neg[0] = n1;
+        neg[1] = n2;
+    }
     __syncthreads();
-    // lane tid: its partials plus, for bit tid of dot_b, the table entry 2^tid H' -- one tree
-    XYZZ<F> acc = (htab && ((kw[tid >> 5] >> (tid & 31)) & 1u)) ? xyzz_from_aff(aff_load<F>(htab + 4 * tid))
-                                                               : xyzz_id<F>();
+    // lane tid: its partials plus, for bit tid of (k1 | k2), the table entry -- one tree
+    XYZZ<F> acc = xyzz_id<F>();
+    if (htab && ((kw[tid >> 5] >> (tid & 31)) & 1u)) {
+        Affine<F> p = aff_load<F>(htab + 4 * (tid & 127));
+        if (tid >= 128) p.x = fe_mul(p.x, fe_from_const<F>(Cv::K::BETA));
+        if (neg[tid >> 7]) p.y = fe_neg(p.y);
+        acc = xyzz_from_aff(p);
+    }
     for (int i = tid; i < nblk; i += TAIL_THREADS) acc = xyzz_add(acc, xyzz_load<F>(part + 8 * (2 * (size_t)i + b)));
     tail_tree<F>(red, tid, acc, sum_s);
     if (tid == 0) aff_to_wrapped(out_wrapped + 4 * b, xyzz_to_aff(xyzz_load<F>(sum_s)));
@@ -777,10 +795,11 @@ static int ipa_begin(halo_curve_t curve, size_t n, const halo_wrapped_point_t* g
             if (!zs_host)
                 hipLaunchKernelGGL(k_powers<typename Cv::Scalar>, dim3(gridn((n + run - 1) / run, 128)), dim3(128), 0,
                                    s, (const uint4*)sm, n, run, ses->zs.as<uint4>());
+            // 2^i H' for i < 128: the hiding terms use the GLV split of their scalar (k_hide_term)
             hipLaunchKernelGGL(k_pow2_xyzz_from_wrapped<Cv>, dim3(1), dim3(64), 0, s, (const uint4*)(sm + 64),
-                               ses->tmp.as<uint4>(), 256);
-            hipLaunchKernelGGL(k_xyzz_to_aff_ipa<Cv>, dim3(4), dim3(64), 0, s, (const uint4*)ses->tmp.ptr,
-                               ses->htab.as<uint4>(), 256);
+                               ses->tmp.as<uint4>(), IPA_HTAB);
+            hipLaunchKernelGGL(k_xyzz_to_aff_ipa<Cv>, dim3(IPA_HTAB / 64), dim3(64), 0, s, (const uint4*)ses->tmp.ptr,
+                               ses->htab.as<uint4>(), IPA_HTAB);
         });
         if (hipGetLastError() != hipSuccess) rc = set_error(HALO_EDEVICE, "ipa begin launch failed");
         if (!rc && gs_host && hipStreamSynchronize(s) != hipSuccess)  // tmp held the staged bases
@@ -902,17 +921,21 @@ static int ipa_round_launch(DeviceState* st, halo_ipa_session* ses) {
             sl = sb;
             sr = sb + half * 32;
         }
-        HALO_CHECK(msm_srs_range_device(st, ses->curve, 0, sl, half, ses->htab.ptr, sm + 128, sm + 256, s, true, lgm));
-        HALO_CHECK(msm_srs_range_device(st, ses->curve, m, sr, half, ses->htab.ptr, sm + 160, sm + 320, s, true, lgm));
+        HALO_CHECK(msm_srs_range_device(st, ses->curve, 0, sl, half, ses->htab.ptr, sm + 128, sm + 256, s, true, lgm,
+                                        true));
+        HALO_CHECK(msm_srs_range_device(st, ses->curve, m, sr, half, ses->htab.ptr, sm + 160, sm + 320, s, true, lgm,
+                                        true));
         HALO_CHECK(msm_join(st, s));
     } else {
         // L and R are independent: the second MSM's accumulation overlaps the first one's tail
         if (ses->srs_round0) {  // G_l = SRS[0, m), G_r = SRS[m, 2m): resident window-shifted copies, no Horner
-            HALO_CHECK(msm_srs_range_device(st, ses->curve, 0, cs + m * 32, m, ses->htab.ptr, sm + 128, sm + 256, s, true));
-            HALO_CHECK(msm_srs_range_device(st, ses->curve, m, cs, m, ses->htab.ptr, sm + 160, sm + 320, s, true));
+            HALO_CHECK(msm_srs_range_device(st, ses->curve, 0, cs + m * 32, m, ses->htab.ptr, sm + 128, sm + 256, s, true,
+                                            32, true));
+            HALO_CHECK(msm_srs_range_device(st, ses->curve, m, cs, m, ses->htab.ptr, sm + 160, sm + 320, s, true, 32,
+                                            true));
         } else {
-            HALO_CHECK(msm_device(st, ses->curve, gs, cs + m * 32, m, ses->htab.ptr, sm + 128, sm + 256, s, true));
-            HALO_CHECK(msm_device(st, ses->curve, gs + m * 64, cs, m, ses->htab.ptr, sm + 160, sm + 320, s, true));
+            HALO_CHECK(msm_device(st, ses->curve, gs, cs + m * 32, m, ses->htab.ptr, sm + 128, sm + 256, s, true, true));
+            HALO_CHECK(msm_device(st, ses->curve, gs + m * 64, cs, m, ses->htab.ptr, sm + 160, sm + 320, s, true, true));
         }
         HALO_CHECK(msm_join(st, s));
     }

@@ -241,21 +241,48 @@ __global__ __launch_bounds__(256, 4) void k_acc(const uint32_t* keys, const uint
 // 7. final: Horner over the windows (wave 0), hiding term w * S from the table 2^i S (waves 1-4),
 //    XYZZ -> affine -> ark WrappedPoint.
 // ---------------------------------------------------------------------------------------------
-// The hiding term w * S = sum of the 2^i S table entries over the set bits of w (an 8-level tree),
-// -> hide_out (XYZZ).  Launched on the tail stream when the MSM starts, so it runs beside the
-// digit / sort / accumulation phase instead of on the tail's critical path.
+// The hiding term w * P = sum of the 2^i P table entries over the set bits of w (an 8-level tree),
+// -> hide_out (XYZZ).  glv: the table holds 2^i P for i < 128 only and w = k1 + lambda k2
+// (|k1|, |k2| < 2^128, glv.hpp): lanes 0-127 take the bits of k1 with 2^i P, lanes 128-255 those of
+// k2 with phi(2^i P) = (beta x, y) -- the IPA's 2^i H' table, whose doubling chain is then half as
+// long.  Launched on the tail stream when the MSM starts, so it runs beside the digit / sort /
+// accumulation phase instead of on the tail's critical path.
 template <class Cv>
-__global__ __launch_bounds__(256) void k_hide_term(const uint4* hide_table /* 256 internal affine 2^i S */,
-                                                   const uint4* hide_scalar /* ark */, uint4* hide_out) {
+__global__ __launch_bounds__(256) void k_hide_term(const uint4* hide_table /* internal affine 2^i P */,
+                                                   const uint4* hide_scalar /* ark */, int glv, uint4* hide_out) {
     using F = typename Cv::Base;
     using S = typename Cv::Scalar;
     __shared__ uint4 red[256 * 8];
     __shared__ uint32_t kw[8];
+    __shared__ uint32_t neg[2];
     const int i = threadIdx.x;
-    if (i == 0) fe_ark_to_canonical_words<S>(hide_scalar, kw);
+    if (i == 0) {
+        uint32_t w8[8];
+        fe_ark_to_canonical_words<S>(hide_scalar, w8);
+        if (glv) {
+            bool n1, n2;
+            uint32_t k1[5], k2[5];
+            glv::decompose<typename Cv::K>(w8, n1, k1, n2, k2);
+            for (int q = 0; q < 4; q++) {
+                kw[q] = k1[q];
+                kw[4 + q] = k2[q];
+            }
+            neg[0] = n1;
+            neg[1] = n2;
+        } else {
+            for (int q = 0; q < 8; q++) kw[q] = w8[q];
+        }
+    }
     __syncthreads();
     XYZZ<F> v = xyzz_id<F>();
-    if ((kw[i >> 5] >> (i & 31)) & 1u) v = xyzz_from_aff(aff_load<F>(hide_table + 4 * i));
+    if ((kw[i >> 5] >> (i & 31)) & 1u) {
+        Affine<F> p = aff_load<F>(hide_table + 4 * (glv ? (i & 127) : i));
+        if (glv) {
+            if (i >= 128) p.x = fe_mul(p.x, fe_from_const<F>(Cv::K::BETA));
+            if (neg[i >> 7]) p.y = fe_neg(p.y);
+        }
+        v = xyzz_from_aff(p);
+    }
     xyzz_store(red + 8 * i, v);
     for (int off = 128; off > 0; off >>= 1) {
         __syncthreads();
@@ -419,7 +446,8 @@ constexpr int curve_id() {
 template <class Cv>
 static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, size_t shift_stride,
                         const uint4* scalars_ark, size_t n, int c_req, const uint4* hide_table, const uint4* hide_scalar,
-                        uint4* d_out_wrapped, hipStream_t s, bool async, uint32_t blk_lg = 32) {
+                        uint4* d_out_wrapped, hipStream_t s, bool async, uint32_t blk_lg = 32,
+                        bool hide_glv = false) {
     MsmPipe& PP = g_msm_pipe[st->device & 63];
     HALO_CHECK(pipe_init(PP));
     const int set = msm_pick_set(PP, s, true);
@@ -472,7 +500,8 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
         hide_slot = M.window_sums.as<uint4>() + 8 * (size_t)W;
         HALO_HIP(hipEventRecord(M.start, s));
         HALO_HIP(hipStreamWaitEvent(ts, M.start, 0));
-        hipLaunchKernelGGL(k_hide_term<Cv>, dim3(1), dim3(256), 0, ts, hide_table, hide_scalar, hide_slot);
+        hipLaunchKernelGGL(k_hide_term<Cv>, dim3(1), dim3(256), 0, ts, hide_table, hide_scalar, (int)hide_glv,
+                           hide_slot);
         HALO_HIP(hipGetLastError());
     }
 
@@ -559,11 +588,13 @@ int msm_join(DeviceState* st, hipStream_t s) {
 }
 
 int msm_device(DeviceState* st, int curve, const void* bases_int, const void* scalars_ark, size_t n,
-               const void* hide_table, const void* hide_scalar, void* d_out_wrapped, hipStream_t s, bool async) {
+               const void* hide_table, const void* hide_scalar, void* d_out_wrapped, hipStream_t s, bool async,
+               bool hide_glv) {
     int rc;
     DISPATCH_CURVE(curve, Cv, {
         rc = msm_device_t<Cv>(st, (const uint4*)bases_int, false, 0, (const uint4*)scalars_ark, n, 0,
-                              (const uint4*)hide_table, (const uint4*)hide_scalar, (uint4*)d_out_wrapped, s, async);
+                              (const uint4*)hide_table, (const uint4*)hide_scalar, (uint4*)d_out_wrapped, s, async,
+                              32, hide_glv);
     });
     return rc;
 }
@@ -589,7 +620,7 @@ int msm_srs_device(DeviceState* st, int curve, const void* scalars_ark, size_t n
 
 int msm_srs_range_device(DeviceState* st, int curve, size_t offset, const void* scalars_ark, size_t n,
                          const void* hide_table, const void* hide_scalar, void* d_out_wrapped, hipStream_t s,
-                         bool async, uint32_t blk_lg) {
+                         bool async, uint32_t blk_lg, bool hide_glv) {
     SrsState& srs = st->srs[curve];
     if (!srs.shifted_c) return set_error(HALO_EINVAL, "msm_srs_range_device: no window-shifted SRS");
     // highest point touched: offset + map(n - 1), map(i) = i + (i >> blk_lg) << blk_lg
@@ -602,7 +633,7 @@ int msm_srs_range_device(DeviceState* st, int curve, size_t offset, const void* 
     DISPATCH_CURVE(curve, Cv, {
         rc = msm_device_t<Cv>(st, srs.shifted.as<const uint4>() + 4 * offset, true, srs.n, (const uint4*)scalars_ark, n,
                               srs.shifted_c, (const uint4*)hide_table, (const uint4*)hide_scalar,
-                              (uint4*)d_out_wrapped, s, async, blk_lg);
+                              (uint4*)d_out_wrapped, s, async, blk_lg, hide_glv);
     });
     return rc;
 }

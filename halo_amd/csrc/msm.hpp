@@ -7,10 +7,11 @@ namespace halo {
 int msm_window_bits(size_t n);
 // MSM over device-resident internal-format affine bases (64 B each) and ark-format scalars.
 // Writes one ark WrappedPoint (64 B) to d_out_wrapped (device).  Optional hiding term
-// hide_scalar * P where hide_table = {2^i P : i < 256} (internal affine; both device pointers).
+// hide_scalar * P where hide_table = {2^i P : i < 256} (internal affine; both device pointers), or
+// with hide_glv {2^i P : i < 128} and the GLV split of the scalar (k_hide_term).
 int msm_device(DeviceState* st, int curve, const void* bases_int, const void* scalars_ark, size_t n,
                const void* hide_table, const void* hide_scalar, void* d_out_wrapped, hipStream_t s,
-               bool async = false);
+               bool async = false, bool hide_glv = false);
 // Makes stream s wait for the reduction tails of the async MSMs enqueued on s.
 int msm_join(DeviceState* st, hipStream_t s);
 // MSM over the resident SRS prefix (window-shifted copies when precomputed); optional hiding
@@ -24,7 +25,7 @@ int msm_srs_device(DeviceState* st, int curve, const void* scalars_ark, size_t n
 // occupy in the unfolded SRS.
 int msm_srs_range_device(DeviceState* st, int curve, size_t offset, const void* scalars_ark, size_t n,
                          const void* hide_table, const void* hide_scalar, void* d_out_wrapped, hipStream_t s,
-                         bool async, uint32_t blk_lg = 32);
+                         bool async, uint32_t blk_lg = 32, bool hide_glv = false);
 // Batched MSM with shared scalars: out[i] = sum_{u < T} w[u] bases[i + u len] for i < len
 // (internal affine bases, ark scalars; outputs internal affine, or XYZZ (128 B) when xyzz_out;
 // stream-ordered on s).

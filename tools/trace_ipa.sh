@@ -11,7 +11,7 @@ import csv, sys
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r['Start_Timestamp']))
 if len(sys.argv) > 2 and sys.argv[2]:
     ws = [r for r in rows if sys.argv[2] in r['Kernel_Name']]
-    t0 = int(ws[-1]['Start_Timestamp']); t1 = t0 + 8000000
+    t0 = int(ws[-1]['Start_Timestamp']); t1 = t0 + 6000000
 else:
     ws = [r for r in rows if 'k_weighted_scalars' in r['Kernel_Name']]
     k = len(ws) - 6
