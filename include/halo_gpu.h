@@ -260,9 +260,12 @@ int halo_ipa_round_lr_multi(halo_ipa_session* const* ses, size_t k, halo_wrapped
                             halo_wrapped_point_t* R);
 int halo_ipa_fold_multi(halo_ipa_session* const* ses, size_t k, const halo_fe_t* xi, const halo_fe_t* xi_inv);
 /* Current half-length m, and the folded vectors (length 2m) copied back to the host (any of the
- * output pointers may be NULL). */
+ * output pointers may be NULL).  Sessions over the resident SRS do not materialise G in their
+ * weighted / tail rounds (the default; HALO_IPA_WEIGHTED=0 and HALO_IPA_TAIL=0 keep G folded every
+ * round): asking for gs there is HALO_EINVAL. */
 int halo_ipa_state(halo_ipa_session* s, size_t* m, halo_wrapped_point_t* gs, halo_fe_t* cs,
                    halo_fe_t* zs);
+/* U = G_0 and c_0 after the last round (in weighted / tail rounds U is only defined then). */
 int halo_ipa_end(halo_ipa_session* s, halo_wrapped_point_t* U, halo_fe_t* c);
 /* One stateless fold over host vectors of length 2m (the loop body of pcdl.rs:427-435), in place
  * on the left halves. */
