@@ -313,6 +313,26 @@ def main():
 
     evals = measure_evals(23)
 
+    # ---- measured HBM copy peak (reported beside the 8 TB/s spec figure): device-to-
+    # device copy of 1 GiB, read + write bytes over the copy time
+    def measure_copy(nbytes=1 << 30, nrep=10):
+        src = torch.empty(nbytes // 8, dtype=torch.int64, device="cuda")
+        src.fill_(1)
+        dst = torch.empty_like(src)
+        for _ in range(2):
+            dst.copy_(src)
+        torch.cuda.synchronize()
+        a0 = time.perf_counter()
+        for _ in range(nrep):
+            dst.copy_(src)
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - a0) * 1e3 / nrep
+        del src, dst
+        return {"workload": "device-to-device copy of 1 GiB (torch copy kernel)", "ms": ms,
+                "GBps": 2 * nbytes / (ms * 1e-3) / 1e9, "frac_of_spec": 2 * nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+
+    hbm_copy = measure_copy()
+
     ntt_main = measure_ntt(args.ntt_logn)
     ntt_main["workload"] += " (BASELINE.json configs[2])"
     sizes = {}
@@ -531,6 +551,7 @@ def main():
             "dist_ipa": dist_ipa,
             "ipa_open": ipa,
             "evals_op": evals,
+            "hbm_copy": hbm_copy,
             "cpu_ntt": cpu_ntt,
             "prove": prove,
             "cpu_ipa_fold": cpu_fold,
@@ -563,10 +584,18 @@ def cpu_baseline(L, H, curve, n, scalars_dev, out_check, budget_s):
         if time.perf_counter() - t0 >= budget_s or reps >= 5:
             break
     dt = (time.perf_counter() - t0) / reps
+    # the same restatement on one thread, over a 2^16-point prefix of the same inputs
+    n1 = min(n, 1 << 16)
+    t1 = time.perf_counter()
+    corc.msm("pallas" if curve == 0 else "vesta", np.ascontiguousarray(bases[:n1]), np.ascontiguousarray(sc[:n1]),
+             threads=1)
+    one_thread = n1 / (time.perf_counter() - t1)
     return {
         "value": n / dt,
         "unit": "points/s",
         "cores": threads,
+        "single_thread": {"value": one_thread, "unit": "points/s", "sample": f"1 x 2^{n1.bit_length() - 1}-point "
+                          "prefix of the same MSM, 1 thread"},
         "kind": "port",
         "sample": f"{reps} x full 2^{n.bit_length() - 1}-point MSM (same bases/scalars as the GPU), C restatement of "
                   f"ark-ec 0.5 msm_bigint_wnaf, c={corc.msm_window_size(n)}, OpenMP over windows",
