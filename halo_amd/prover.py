@@ -6,9 +6,10 @@ backend ``B``; with ``DeviceBackend`` every data-parallel step runs in libhalo_g
 
 * round 0: 17 iNTTs of size n and 42 NTTs of size 8n (protocol.rs:76-106),
 * round 1: 16 commitments (pcdl::commit = resident-SRS MSM, protocol.rs:114),
-* round 3: the 14 growing FFT products of f' and g', their NTTs mod X^n - 1, the permutation
-  accumulator z as prefix/suffix product scans (no per-element inversion), 2 iNTTs, 1 commitment
-  (protocol.rs:126-161),
+* round 3: f' and g' (on the CPU backends the reference's 14 growing FFT products; on the device
+  the same polynomials through the 8n domain: 16 NTT(8n), pointwise products, 2 iNTT(8n), and their
+  n-domain evaluations as strided reads), the permutation accumulator z as prefix/suffix product
+  scans (no per-element inversion), 2 iNTTs, 1 commitment (protocol.rs:126-161),
 * round 4: the gate-constraint evaluation over the 8n domain (protocol.rs:591-1011: on the device
   three fused passes, halo_gate_constraints_dev; on the CPU backends the ``*_generic`` forms
   transcribed below over ``Evals`` algebra), iNTT(8n), f_cc1 / f_cc2 products, the vanishing
@@ -227,13 +228,16 @@ def naive_prover(B, wit, n: int, chal: Challenges, acc_prev=None):
     def perm_factor(other, i):
         return B.poly_add_const(B.poly_add(wit["ws"][i], B.poly_scale(other[i], beta)), gamma)
 
-    f_prime = perm_factor(wit["ids"], 0)
-    g_prime = perm_factor(wit["sigmas"], 0)
-    for i in range(1, S_POLYS):
-        f_prime = B.poly_mul(f_prime, perm_factor(wit["ids"], i))
-        g_prime = B.poly_mul(g_prime, perm_factor(wit["sigmas"], i))
-    f_ev = B.ntt(f_prime, n)
-    g_ev = B.ntt(g_prime, n)
+    if hasattr(B, "perm_products"):  # the same f', g' via the 8n evaluations (see DeviceBackend.perm_products)
+        f_prime, g_prime, f_ev, g_ev = B.perm_products(w_evals, wit["ws"], wit["ids"], wit["sigmas"], beta, gamma, n)
+    else:
+        f_prime = perm_factor(wit["ids"], 0)
+        g_prime = perm_factor(wit["sigmas"], 0)
+        for i in range(1, S_POLYS):
+            f_prime = B.poly_mul(f_prime, perm_factor(wit["ids"], i))
+            g_prime = B.poly_mul(g_prime, perm_factor(wit["sigmas"], i))
+        f_ev = B.ntt(f_prime, n)
+        g_ev = B.ntt(g_prime, n)
     z_vals = B.permutation_accumulator(f_ev, g_ev)              # z[0] = 1, z[i] = z[i-1] f[i] / g[i]
     z_evals = B.shift_right(z_vals, 1)                          # from_vec_and_domain
     z_omega = B.intt(B.shift_left(z_evals, 1))
@@ -499,6 +503,32 @@ class DeviceBackend:
         fa, fb = self.ntt(a, N), self.ntt(b, N)
         prod = self._op(2, fa.t, fb.t, None, 0, fa.t)
         return self.intt(prod)[:rl].contiguous()
+
+    def perm_products(self, w_evals, ws, ids, sigmas, beta, gamma, n):
+        """protocol.rs:132-141 computed through the 8n domain: f' = prod_i (w_i + beta id_i + gamma) (and
+        g' with sigma_i) has degree < 8n, so its 8n evaluations are the pointwise product of the factors'
+        8n evaluations (w_i's are round 0's w_evals; one NTT(8n) per id_i / sigma_i), one iNTT(8n) gives
+        the coefficients (the same polynomial the reference's 7 growing FFT products give), and
+        f'(omega_n^j) = F[8 j], so f_ev / g_ev are strided reads instead of two more NTTs."""
+        N8 = CONSTRAINT_DEGREE_MULTIPLIER * n
+        assert S_POLYS <= CONSTRAINT_DEGREE_MULTIPLIER
+        outs = []
+        wg = [w_evals[i] + gamma for i in range(S_POLYS)]  # shared by both products
+        for other in (ids, sigmas):
+            acc = None
+            deg = 0
+            for i in range(S_POLYS):
+                t = self.ntt(other[i], N8) * beta + wg[i]
+                deg += max(ws[i].shape[0], other[i].shape[0]) - 1
+                acc = t if acc is None else acc * t
+            assert deg < N8
+            outs.append((acc, deg + 1))
+        (F, lf), (G, lg) = outs
+        f_prime = self.intt(F)[:lf].contiguous()
+        g_prime = self.intt(G)[:lg].contiguous()
+        f_ev = DevEvals(self, F.t[::CONSTRAINT_DEGREE_MULTIPLIER].contiguous())
+        g_ev = DevEvals(self, G.t[::CONSTRAINT_DEGREE_MULTIPLIER].contiguous())
+        return f_prime, g_prime, f_ev, g_ev
 
     def divide_by_vanishing(self, f, n):
         L = f.shape[0]
