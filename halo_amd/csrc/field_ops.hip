@@ -2,6 +2,7 @@
 // field library).
 #include "curve.hpp"
 #include "dispatch.hpp"
+#include "glv.hpp"
 #include "runtime.hpp"
 
 namespace halo {
@@ -28,10 +29,51 @@ __global__ __launch_bounds__(256) void k_field_op(int op, const uint4* a, const 
     fe_to_ark(out + 2 * i, r);
 }
 
+// k P for one lane: GLV split k = k1 + lambda k2 (|k1|, |k2| < 2^128, glv.hpp) and a joint 4-bit
+// fixed window over k1 (table d P, d < 16, in LDS) and k2 (the same entries through
+// phi(X, Y, ZZ, ZZZ) = (beta X, Y, ZZ, ZZZ)): ~132 doublings + ~66 additions on the lane's dependent
+// chain instead of 256 + ~128 (a lone scalar multiplication is latency-bound: H' = xi_0 H, the
+// accumulator's combination).
+constexpr int CURVE_OP_SMUL_THREADS = 8;
+template <class Cv>
+HALO_DEV XYZZ<typename Cv::Base> scalar_mul_glv(const Affine<typename Cv::Base>& P, const uint32_t (&k)[8],
+                                               uint4* tab /* 16 XYZZ of this lane */) {
+    using F = typename Cv::Base;
+    bool n1, n2;
+    uint32_t k1[5], k2[5];
+    glv::decompose<typename Cv::K>(k, n1, k1, n2, k2);
+    const XYZZ<F> p1 = xyzz_from_aff(P);
+    xyzz_store(tab, xyzz_id<F>());
+    xyzz_store(tab + 8, p1);
+    for (int d = 2; d < 16; d++)
+        xyzz_store(tab + 8 * d, (d & 1) ? xyzz_madd(xyzz_load<F>(tab + 8 * (d - 1)), P) : xyzz_dbl(xyzz_load<F>(tab + 8 * (d / 2))));
+    const Fe<F> beta = fe_from_const<F>(Cv::K::BETA);
+    XYZZ<F> acc = xyzz_id<F>();
+    for (int w = 32; w >= 0; w--) {  // 33 windows cover 132 bits
+        if (w != 32)
+            for (int b = 0; b < 4; b++) acc = xyzz_dbl(acc);
+        const int q = (4 * w) >> 5, sh = (4 * w) & 31;
+        const uint32_t d1 = (k1[q] >> sh) & 15u, d2 = (k2[q] >> sh) & 15u;
+        if (d1) {
+            XYZZ<F> t = xyzz_load<F>(tab + 8 * d1);
+            if (n1) t.Y = fe_neg(t.Y);
+            acc = xyzz_add(acc, t);
+        }
+        if (d2) {
+            XYZZ<F> t = xyzz_load<F>(tab + 8 * d2);
+            t.X = fe_mul(t.X, beta);
+            if (n2) t.Y = fe_neg(t.Y);
+            acc = xyzz_add(acc, t);
+        }
+    }
+    return acc;
+}
+
 template <class Cv>
 __global__ __launch_bounds__(64) void k_curve_op(int op, const uint4* a, const uint4* b, const uint4* k, uint4* out, size_t n) {
     using F = typename Cv::Base;
     using S = typename Cv::Scalar;
+    extern __shared__ uint4 smul_tab[];  // op 2: 16 XYZZ (128 B) per lane
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     Affine<F> p = aff_from_wrapped<F>(a + 4 * i);
@@ -43,7 +85,7 @@ __global__ __launch_bounds__(64) void k_curve_op(int op, const uint4* a, const u
     } else {
         uint32_t w[8];
         fe_ark_to_canonical_words<S>(k + 2 * i, w);
-        r = xyzz_scalar_mul(p, w);
+        r = scalar_mul_glv<Cv>(p, w, smul_tab + 16 * 8 * threadIdx.x);
     }
     aff_to_wrapped(out + 4 * i, xyzz_to_aff(r));
 }
@@ -96,9 +138,10 @@ extern "C" int halo_curve_op(halo_curve_t curve, int op, const halo_wrapped_poin
     HALO_CHECK(copy_h2d(st->scratch[0].ptr, a, pb, s));
     if (b) HALO_CHECK(copy_h2d(st->scratch[1].ptr, b, pb, s));
     if (k) HALO_CHECK(copy_h2d(st->scratch[2].ptr, k, kb, s));
-    const unsigned threads = 64, blocks = (unsigned)((n + threads - 1) / threads);
+    const unsigned threads = op == 2 ? CURVE_OP_SMUL_THREADS : 64, blocks = (unsigned)((n + threads - 1) / threads);
+    const size_t smem = op == 2 ? (size_t)threads * 16 * 128 : 0;
     DISPATCH_CURVE(curve, Cv, {
-        hipLaunchKernelGGL(k_curve_op<Cv>, dim3(blocks), dim3(threads), 0, s, op, st->scratch[0].as<const uint4>(),
+        hipLaunchKernelGGL(k_curve_op<Cv>, dim3(blocks), dim3(threads), smem, s, op, st->scratch[0].as<const uint4>(),
                            st->scratch[1].as<const uint4>(), st->scratch[2].as<const uint4>(),
                            st->scratch[3].as<uint4>(), n);
     });

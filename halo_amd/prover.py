@@ -321,7 +321,8 @@ def ipa_open_many(B, items, d: int):
     Returns [(Ls, Rs, U, c, [xi_0] + xis)]."""
     chals = [Challenges(B.m, seed=open_seed(z, v)) for (_, z, v) in items]
     xi0s = [ch() for ch in chals]
-    jobs = [(p, d + 1, z, B.h_mul(x0)) for (p, z, _), x0 in zip(items, xi0s)]
+    hps = B.h_mul_many(xi0s) if hasattr(B, "h_mul_many") else [B.h_mul(x0) for x0 in xi0s]
+    jobs = [(p, d + 1, z, hp) for (p, z, _), hp in zip(items, hps)]
     outs = B.ipa_many(jobs, chals)
     return [(Ls, Rs, U, c, [x0] + xis) for (Ls, Rs, U, c, xis), x0 in zip(outs, xi0s)]
 
@@ -587,6 +588,15 @@ class DeviceBackend:
         self.H.check(self.L.halo_curve_op(self.curve, 2, self.H.ptr(self.H_point), None, self.H.ptr(self.fe(k)), 1,
                                           self.H.ptr(out)))
         return out
+
+    def h_mul_many(self, ks):
+        """[k H for k in ks] in one device call (the lanes run concurrently)."""
+        pts = np.ascontiguousarray(np.stack([self.H_point] * len(ks)))
+        kk = np.ascontiguousarray(np.stack([self.fe(k) for k in ks]))
+        out = np.zeros_like(pts)
+        self.H.check(self.L.halo_curve_op(self.curve, 2, self.H.ptr(pts), None, self.H.ptr(kk), len(ks),
+                                          self.H.ptr(out)))
+        return list(out)
 
     def point_combine(self, points, scalars):
         pts = np.ascontiguousarray(np.stack(points))
