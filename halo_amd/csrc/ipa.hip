@@ -415,7 +415,8 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail_msm(const uint4* table, c
 // block b (0: L, 1: R): sum of the partials + dot_b * H' (from the 2^i H' table), -> WrappedPoint
 template <class Cv>
 __global__ __launch_bounds__(TAIL_THREADS) void k_tail_final(const uint4* part, int nblk, const uint4* htab,
-                                                              const uint4* dots_ark, uint4* out_wrapped) {
+                                                              const uint4* dots_ark, uint4* out_wrapped,
+                                                              int xyzz_out) {
     using F = typename Cv::Base;
     using S = typename Cv::Scalar;
     __shared__ uint4 red[TAIL_THREADS * 8];
@@ -446,7 +447,12 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail_final(const uint4* part, 
     }
     for (int i = tid; i < nblk; i += TAIL_THREADS) acc = xyzz_add(acc, xyzz_load<F>(part + 8 * (2 * (size_t)i + b)));
     tail_tree<F>(red, tid, acc, sum_s);
-    if (tid == 0) aff_to_wrapped(out_wrapped + 4 * b, xyzz_to_aff(xyzz_load<F>(sum_s)));
+    if (tid == 0) {
+        if (xyzz_out)  // 128 B per side, converted on the host (host_xyzz_to_wrapped)
+            xyzz_store(out_wrapped + 8 * b, xyzz_load<F>(sum_s));
+        else
+            aff_to_wrapped(out_wrapped + 4 * b, xyzz_to_aff(xyzz_load<F>(sum_s)));
+    }
 }
 
 template <class S>
@@ -508,7 +514,7 @@ struct halo_ipa_session {
     DevBuf table, w[2], scal, side, part;
     BatchScratch mat;  // weighted -> tail switch (msm_shared_batch)
     int wcur = 0;
-    uint8_t* pinned = nullptr;  // 128 B L|R (D2H) + 64 B xi|xi_inv (H2D): async copies, several sessions in flight
+    uint8_t* pinned = nullptr;  // [128, 192) xi|xi_inv (H2D), [256, 512) L|R XYZZ (D2H): async, several sessions in flight
     ~halo_ipa_session() {
         if (s) (void)hipStreamDestroy(s);
         if (pinned) (void)hipHostFree(pinned);
@@ -738,7 +744,7 @@ static int ipa_begin(halo_curve_t curve, size_t n, const halo_wrapped_point_t* g
     ses->m = n / 2;
     ses->s = nullptr;
     if (hipStreamCreateWithFlags(&ses->s, hipStreamNonBlocking) != hipSuccess ||
-        hipHostMalloc((void**)&ses->pinned, 256, hipHostMallocDefault) != hipSuccess) {
+        hipHostMalloc((void**)&ses->pinned, 512, hipHostMallocDefault) != hipSuccess) {
         delete ses;
         return set_error(HALO_EDEVICE, "halo_ipa_begin: stream / pinned buffer allocation failed");
     }
@@ -759,7 +765,7 @@ static int ipa_begin(halo_curve_t curve, size_t n, const halo_wrapped_point_t* g
         if ((rc = ses->cs.reserve(n * 32))) break;
         if ((rc = ses->zs.reserve(n * 32))) break;
         if ((rc = ses->htab.reserve(256 * 64))) break;
-        if ((rc = ses->small.reserve(512))) break;
+        if ((rc = ses->small.reserve(1024))) break;
         if ((rc = ses->tmp.reserve(std::max<size_t>(4096 * 32, gs_host ? n * 64 : 0)))) break;
         if (gs_host) {
             if ((rc = copy_h2d(ses->tmp.ptr, gs_host, n * 64, s))) break;
@@ -873,7 +879,7 @@ static int ipa_tail_sums(halo_ipa_session* ses, int mode, hipStream_t s) {
                            ses->scal.as<const uint32_t>(), ses->side.as<const uint8_t>(), n0, ses->part.as<uint4>());
         hipLaunchKernelGGL(k_tail_final<Cv>, dim3(mode == 0 ? 2 : 1), dim3(TAIL_THREADS), 0, s,
                            ses->part.as<const uint4>(), (int)nblk, mode == 0 ? ses->htab.as<const uint4>() : nullptr,
-                           (const uint4*)(sm + 128), (uint4*)(sm + 256));
+                           (const uint4*)(sm + 128), (uint4*)(sm + (mode == 0 ? 512 : 256)), (int)(mode == 0));
     });
     HALO_HIP(hipGetLastError());
     return HALO_OK;
@@ -885,7 +891,7 @@ static int ipa_round_launch(DeviceState* st, halo_ipa_session* ses) {
     hipStream_t s = ses->s;
     const size_t m = ses->m;
     const int sf = ses->curve == HALO_PALLAS ? HALO_FP : HALO_FQ;
-    char* sm = (char*)ses->small.ptr;  // [0,32) z, [64,128) H', [128,160) dot_l, [160,192) dot_r, [256,320) L, [320,384) R
+    char* sm = (char*)ses->small.ptr;  // [0,32) z, [64,128) H', [128,192) dots, [256,384) U|c, [512,768) L|R XYZZ
     const char* cs = ses->cs.as<const char>();
     const char* zs = ses->zs.as<const char>();
     if (ses->weighted && 2 * m <= ipa_mat_n()) {
@@ -921,25 +927,28 @@ static int ipa_round_launch(DeviceState* st, halo_ipa_session* ses) {
             sl = sb;
             sr = sb + half * 32;
         }
-        HALO_CHECK(msm_srs_range_device(st, ses->curve, 0, sl, half, ses->htab.ptr, sm + 128, sm + 256, s, true, lgm,
-                                        true));
-        HALO_CHECK(msm_srs_range_device(st, ses->curve, m, sr, half, ses->htab.ptr, sm + 160, sm + 320, s, true, lgm,
-                                        true));
+        HALO_CHECK(msm_srs_range_device(st, ses->curve, 0, sl, half, ses->htab.ptr, sm + 128, sm + 512, s, true, lgm,
+                                        true, true));
+        HALO_CHECK(msm_srs_range_device(st, ses->curve, m, sr, half, ses->htab.ptr, sm + 160, sm + 640, s, true, lgm,
+                                        true, true));
         HALO_CHECK(msm_join(st, s));
     } else {
         // L and R are independent: the second MSM's accumulation overlaps the first one's tail
         if (ses->srs_round0) {  // G_l = SRS[0, m), G_r = SRS[m, 2m): resident window-shifted copies, no Horner
-            HALO_CHECK(msm_srs_range_device(st, ses->curve, 0, cs + m * 32, m, ses->htab.ptr, sm + 128, sm + 256, s, true,
-                                            32, true));
-            HALO_CHECK(msm_srs_range_device(st, ses->curve, m, cs, m, ses->htab.ptr, sm + 160, sm + 320, s, true, 32,
-                                            true));
+            HALO_CHECK(msm_srs_range_device(st, ses->curve, 0, cs + m * 32, m, ses->htab.ptr, sm + 128, sm + 512, s, true,
+                                            32, true, true));
+            HALO_CHECK(msm_srs_range_device(st, ses->curve, m, cs, m, ses->htab.ptr, sm + 160, sm + 640, s, true, 32,
+                                            true, true));
         } else {
-            HALO_CHECK(msm_device(st, ses->curve, gs, cs + m * 32, m, ses->htab.ptr, sm + 128, sm + 256, s, true, true));
-            HALO_CHECK(msm_device(st, ses->curve, gs + m * 64, cs, m, ses->htab.ptr, sm + 160, sm + 320, s, true, true));
+            HALO_CHECK(msm_device(st, ses->curve, gs, cs + m * 32, m, ses->htab.ptr, sm + 128, sm + 512, s, true, true,
+                                  true));
+            HALO_CHECK(msm_device(st, ses->curve, gs + m * 64, cs, m, ses->htab.ptr, sm + 160, sm + 640, s, true, true,
+                                  true));
         }
         HALO_CHECK(msm_join(st, s));
     }
-    HALO_HIP(hipMemcpyAsync(ses->pinned, sm + 256, 128, hipMemcpyDeviceToHost, s));
+    // L, R as packed XYZZ (128 B each): the affine conversion runs on the host (host_xyzz_to_wrapped)
+    HALO_HIP(hipMemcpyAsync(ses->pinned + 256, sm + 512, 256, hipMemcpyDeviceToHost, s));
     return HALO_OK;
 }
 
@@ -997,8 +1006,8 @@ extern "C" int halo_ipa_round_lr_multi(halo_ipa_session* const* ses, size_t k, h
     }
     for (size_t i = 0; i < k; i++) {
         HALO_HIP(hipStreamSynchronize(ses[i]->s));
-        memcpy(&L[i], ses[i]->pinned, 64);
-        memcpy(&R[i], ses[i]->pinned + 64, 64);
+        host_xyzz_to_wrapped(ses[i]->curve, ses[i]->pinned + 256, &L[i]);
+        host_xyzz_to_wrapped(ses[i]->curve, ses[i]->pinned + 384, &R[i]);
     }
     return HALO_OK;
 }

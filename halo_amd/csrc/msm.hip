@@ -296,7 +296,7 @@ __global__ __launch_bounds__(256) void k_hide_term(const uint4* hide_table /* in
 // plus the precomputed hiding term (or null), -> affine -> ark WrappedPoint.
 template <class Cv>
 __global__ __launch_bounds__(64) void k_final(const uint4* window_sums, int W, int c, const uint4* hide_xyzz,
-                                              uint4* out_wrapped) {
+                                              uint4* out_wrapped, int xyzz_out) {
     using F = typename Cv::Base;
     if (threadIdx.x != 0) return;
     XYZZ<F> horner = xyzz_id<F>();
@@ -309,7 +309,10 @@ __global__ __launch_bounds__(64) void k_final(const uint4* window_sums, int W, i
         horner = xyzz_add(horner, xyzz_load<F>(window_sums + 8 * w));
     }
     if (hide_xyzz) horner = xyzz_add(horner, xyzz_load<F>(hide_xyzz));
-    aff_to_wrapped(out_wrapped, xyzz_to_aff(horner));
+    if (xyzz_out)  // 128 B packed XYZZ: the host converts (halo_ipa_round_lr, no inversion on the lane)
+        xyzz_store(out_wrapped, horner);
+    else
+        aff_to_wrapped(out_wrapped, xyzz_to_aff(horner));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -447,7 +450,7 @@ template <class Cv>
 static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, size_t shift_stride,
                         const uint4* scalars_ark, size_t n, int c_req, const uint4* hide_table, const uint4* hide_scalar,
                         uint4* d_out_wrapped, hipStream_t s, bool async, uint32_t blk_lg = 32,
-                        bool hide_glv = false) {
+                        bool hide_glv = false, bool out_xyzz = false) {
     MsmPipe& PP = g_msm_pipe[st->device & 63];
     HALO_CHECK(pipe_init(PP));
     const int set = msm_pick_set(PP, s, true);
@@ -564,7 +567,7 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
     ta.out_wrapped = d_out_wrapped;
     HALO_CHECK(msm_tail_launch(curve_id<Cv>(), ta, ts));
     hipLaunchKernelGGL(k_final<Cv>, dim3(1), dim3(64), 0, ts, M.window_sums.as<const uint4>(), SW, c,
-                       (const uint4*)hide_slot, d_out_wrapped);
+                       (const uint4*)hide_slot, d_out_wrapped, (int)out_xyzz);
     HALO_HIP(hipGetLastError());
     HALO_HIP(hipEventRecord(M.tail_done, ts));
     M.tail_pending = true;
@@ -589,12 +592,12 @@ int msm_join(DeviceState* st, hipStream_t s) {
 
 int msm_device(DeviceState* st, int curve, const void* bases_int, const void* scalars_ark, size_t n,
                const void* hide_table, const void* hide_scalar, void* d_out_wrapped, hipStream_t s, bool async,
-               bool hide_glv) {
+               bool hide_glv, bool out_xyzz) {
     int rc;
     DISPATCH_CURVE(curve, Cv, {
         rc = msm_device_t<Cv>(st, (const uint4*)bases_int, false, 0, (const uint4*)scalars_ark, n, 0,
                               (const uint4*)hide_table, (const uint4*)hide_scalar, (uint4*)d_out_wrapped, s, async,
-                              32, hide_glv);
+                              32, hide_glv, out_xyzz);
     });
     return rc;
 }
@@ -620,7 +623,7 @@ int msm_srs_device(DeviceState* st, int curve, const void* scalars_ark, size_t n
 
 int msm_srs_range_device(DeviceState* st, int curve, size_t offset, const void* scalars_ark, size_t n,
                          const void* hide_table, const void* hide_scalar, void* d_out_wrapped, hipStream_t s,
-                         bool async, uint32_t blk_lg, bool hide_glv) {
+                         bool async, uint32_t blk_lg, bool hide_glv, bool out_xyzz) {
     SrsState& srs = st->srs[curve];
     if (!srs.shifted_c) return set_error(HALO_EINVAL, "msm_srs_range_device: no window-shifted SRS");
     // highest point touched: offset + map(n - 1), map(i) = i + (i >> blk_lg) << blk_lg
@@ -633,7 +636,7 @@ int msm_srs_range_device(DeviceState* st, int curve, size_t offset, const void* 
     DISPATCH_CURVE(curve, Cv, {
         rc = msm_device_t<Cv>(st, srs.shifted.as<const uint4>() + 4 * offset, true, srs.n, (const uint4*)scalars_ark, n,
                               srs.shifted_c, (const uint4*)hide_table, (const uint4*)hide_scalar,
-                              (uint4*)d_out_wrapped, s, async, blk_lg, hide_glv);
+                              (uint4*)d_out_wrapped, s, async, blk_lg, hide_glv, out_xyzz);
     });
     return rc;
 }
@@ -811,6 +814,125 @@ int msm_shared_batch(DeviceState* st, int curve, const void* bases_int, const vo
                                     S, s);
     });
     return rc;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Host-side XYZZ -> affine (the IPA's per-round L and R): the lane-side conversion is one ~300-modmul
+// dependent chain (Fermat inversion) at the end of the reduction tail; on the host it is a few
+// microseconds.  A packed internal coordinate is an integer < 2p congruent to v 2^261, so
+// x = X / ZZ and y = Y / ZZZ need no change of representation; 4 x 64-bit Montgomery arithmetic
+// (R = 2^256) then yields x R mod p, which is the ark word form directly.
+// ---------------------------------------------------------------------------------------------
+namespace {
+struct HostMont {
+    uint64_t p[4], pinv, r2[4], one[4];
+    explicit HostMont(const uint64_t (&m)[4]) {
+        for (int i = 0; i < 4; i++) p[i] = m[i];
+        uint64_t inv = 1;  // p[0]^-1 mod 2^64 by Newton's iteration
+        for (int i = 0; i < 6; i++) inv *= 2 - p[0] * inv;
+        pinv = 0 - inv;
+        uint64_t x[4] = {1, 0, 0, 0};
+        for (int i = 0; i < 512; i++) {  // 2^256 mod p (= one), then 2^512 mod p (= r2)
+            dbl(x);
+            if (i == 255)
+                for (int k = 0; k < 4; k++) one[k] = x[k];
+        }
+        for (int k = 0; k < 4; k++) r2[k] = x[k];
+    }
+    bool geq_p(const uint64_t (&a)[4]) const {
+        for (int i = 3; i >= 0; i--)
+            if (a[i] != p[i]) return a[i] > p[i];
+        return true;
+    }
+    void sub_p(uint64_t (&a)[4]) const {
+        unsigned __int128 b = 0;
+        for (int i = 0; i < 4; i++) {
+            const unsigned __int128 d = (unsigned __int128)a[i] - p[i] - b;
+            a[i] = (uint64_t)d;
+            b = (d >> 64) & 1;
+        }
+    }
+    void dbl(uint64_t (&a)[4]) const {  // a < p (p < 2^255): 2a < 2^256
+        uint64_t c = 0;
+        for (int i = 0; i < 4; i++) {
+            const uint64_t t = (a[i] << 1) | c;
+            c = a[i] >> 63;
+            a[i] = t;
+        }
+        if (geq_p(a)) sub_p(a);
+    }
+    void mul(const uint64_t (&a)[4], const uint64_t (&b)[4], uint64_t (&out)[4]) const {  // a b R^-1 mod p (CIOS)
+        uint64_t t[6] = {0, 0, 0, 0, 0, 0};
+        for (int i = 0; i < 4; i++) {
+            unsigned __int128 c = 0;
+            for (int j = 0; j < 4; j++) {
+                c += (unsigned __int128)a[j] * b[i] + t[j];
+                t[j] = (uint64_t)c;
+                c >>= 64;
+            }
+            c += t[4];
+            t[4] = (uint64_t)c;
+            t[5] = (uint64_t)(c >> 64);
+            const uint64_t m = t[0] * pinv;
+            c = ((unsigned __int128)m * p[0] + t[0]) >> 64;
+            for (int j = 1; j < 4; j++) {
+                c += (unsigned __int128)m * p[j] + t[j];
+                t[j - 1] = (uint64_t)c;
+                c >>= 64;
+            }
+            c += t[4];
+            t[3] = (uint64_t)c;
+            t[4] = t[5] + (uint64_t)(c >> 64);
+        }
+        uint64_t r[4] = {t[0], t[1], t[2], t[3]};
+        if (t[4] || geq_p(r)) sub_p(r);
+        for (int i = 0; i < 4; i++) out[i] = r[i];
+    }
+    void inv(const uint64_t (&a)[4], uint64_t (&out)[4]) const {  // Montgomery domain, a^(p-2)
+        const uint64_t e[4] = {p[0] - 2, p[1], p[2], p[3]};
+        uint64_t r[4] = {one[0], one[1], one[2], one[3]};
+        for (int i = 255; i >= 0; i--) {
+            mul(r, r, r);
+            if ((e[i >> 6] >> (i & 63)) & 1) mul(r, a, r);
+        }
+        for (int i = 0; i < 4; i++) out[i] = r[i];
+    }
+};
+
+template <class F>
+void host_xyzz_to_wrapped_t(const void* xyzz, void* wrapped) {
+    static const HostMont M(F::MODULUS64);
+    const uint64_t* q = (const uint64_t*)xyzz;
+    uint64_t c[4][4];  // X, Y, ZZ, ZZZ reduced below p
+    for (int k = 0; k < 4; k++) {
+        for (int i = 0; i < 4; i++) c[k][i] = q[4 * k + i];
+        if (M.geq_p(c[k])) M.sub_p(c[k]);
+    }
+    uint64_t* out = (uint64_t*)wrapped;
+    if (!(c[2][0] | c[2][1] | c[2][2] | c[2][3])) {  // ZZ = 0: the identity, WrappedPoint (0, 0)
+        for (int i = 0; i < 8; i++) out[i] = 0;
+        return;
+    }
+    uint64_t m[4][4], t[4], iv[4], u[4], x[4], y[4];
+    for (int k = 0; k < 4; k++) M.mul(c[k], M.r2, m[k]);  // to the Montgomery domain
+    M.mul(m[2], m[3], t);
+    M.inv(t, iv);  // (ZZ ZZZ)^-1
+    M.mul(m[0], m[3], u);
+    M.mul(u, iv, x);  // X / ZZ, times R
+    M.mul(m[1], m[2], u);
+    M.mul(u, iv, y);  // Y / ZZZ, times R
+    for (int i = 0; i < 4; i++) {
+        out[i] = x[i];
+        out[4 + i] = y[i];
+    }
+}
+}  // namespace
+
+void host_xyzz_to_wrapped(int curve, const void* xyzz, void* wrapped) {
+    if (curve == HALO_PALLAS)
+        host_xyzz_to_wrapped_t<PallasCurve::Base>(xyzz, wrapped);
+    else
+        host_xyzz_to_wrapped_t<VestaCurve::Base>(xyzz, wrapped);
 }
 
 int convert_wrapped_to_internal(int curve, const void* in, void* out, size_t n, hipStream_t s) {

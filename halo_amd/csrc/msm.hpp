@@ -8,10 +8,11 @@ int msm_window_bits(size_t n);
 // MSM over device-resident internal-format affine bases (64 B each) and ark-format scalars.
 // Writes one ark WrappedPoint (64 B) to d_out_wrapped (device).  Optional hiding term
 // hide_scalar * P where hide_table = {2^i P : i < 256} (internal affine; both device pointers), or
-// with hide_glv {2^i P : i < 128} and the GLV split of the scalar (k_hide_term).
+// with hide_glv {2^i P : i < 128} and the GLV split of the scalar (k_hide_term).  out_xyzz: the
+// result is written as 128 B packed XYZZ instead of an affine WrappedPoint (host_xyzz_to_wrapped).
 int msm_device(DeviceState* st, int curve, const void* bases_int, const void* scalars_ark, size_t n,
                const void* hide_table, const void* hide_scalar, void* d_out_wrapped, hipStream_t s,
-               bool async = false, bool hide_glv = false);
+               bool async = false, bool hide_glv = false, bool out_xyzz = false);
 // Makes stream s wait for the reduction tails of the async MSMs enqueued on s.
 int msm_join(DeviceState* st, hipStream_t s);
 // MSM over the resident SRS prefix (window-shifted copies when precomputed); optional hiding
@@ -25,7 +26,7 @@ int msm_srs_device(DeviceState* st, int curve, const void* scalars_ark, size_t n
 // occupy in the unfolded SRS.
 int msm_srs_range_device(DeviceState* st, int curve, size_t offset, const void* scalars_ark, size_t n,
                          const void* hide_table, const void* hide_scalar, void* d_out_wrapped, hipStream_t s,
-                         bool async, uint32_t blk_lg = 32, bool hide_glv = false);
+                         bool async, uint32_t blk_lg = 32, bool hide_glv = false, bool out_xyzz = false);
 // Batched MSM with shared scalars: out[i] = sum_{u < T} w[u] bases[i + u len] for i < len
 // (internal affine bases, ark scalars; outputs internal affine, or XYZZ (128 B) when xyzz_out;
 // stream-ordered on s).
@@ -35,6 +36,9 @@ struct BatchScratch {
 int msm_shared_batch(DeviceState* st, int curve, const void* bases_int, const void* w_ark, size_t T, size_t len,
                      void* out, bool xyzz_out, BatchScratch& S, hipStream_t s);
 int srs_precompute_windows(DeviceState* st, int curve, hipStream_t s);
+// Host conversion of a 128-B packed XYZZ point (internal format, each coordinate < 2p) to an ark
+// WrappedPoint: one inversion in 4 x 64-bit Montgomery arithmetic on the CPU (identity -> (0, 0)).
+void host_xyzz_to_wrapped(int curve, const void* xyzz, void* wrapped);
 int convert_wrapped_to_internal(int curve, const void* in, void* out, size_t n, hipStream_t s);
 int convert_internal_to_wrapped(int curve, const void* in, void* out, size_t n, hipStream_t s);
 int ntt_device_dispatch(DeviceState* st, int field, const void* d_in, void* d_out, void* d_tmp, unsigned logn,
