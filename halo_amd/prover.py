@@ -12,8 +12,9 @@ backend ``B``; with ``DeviceBackend`` every data-parallel step runs in libhalo_g
   scans (no per-element inversion), 2 iNTTs, 1 commitment (protocol.rs:126-161),
 * round 4: the gate-constraint evaluation over the 8n domain (protocol.rs:591-1011: on the device
   three fused passes, halo_gate_constraints_dev; on the CPU backends the ``*_generic`` forms
-  transcribed below over ``Evals`` algebra), iNTT(8n), f_cc1 / f_cc2 products, the vanishing
-  division, t_split and 16 commitments (protocol.rs:170-265),
+  transcribed below over ``Evals`` algebra), iNTT(8n), f_cc1 / f_cc2 products (on the device f_cc2 on
+  one evaluation domain, z_omega's evaluations as a rotation of z's), the vanishing division, t_split
+  and 16 commitments (protocol.rs:170-265),
 * round 5: the geometric combinations, two ``Instance::open`` (commit + evaluation + IPA opening),
   ``acc::prover`` (h(X) of three instances, one more IPA opening; acc.rs:178-204) and the 91
   polynomial evaluations of the proof (protocol.rs:273-323).
@@ -267,7 +268,10 @@ def naive_prover(B, wit, n: int, chal: Challenges, acc_prev=None):
     e1 = B.sparse_vec(n, {0: 1})
     l1 = B.intt(B.shift_right(e1, 1))                           # lagrange_basis_poly(1, domain)
     f_cc1 = B.poly_mul(l1, B.poly_add_const(z, m - 1))
-    f_cc2 = B.poly_sub(B.poly_mul(z, f_prime), B.poly_mul(z_omega, g_prime))
+    if hasattr(B, "perm_cc2"):  # the same polynomial through one evaluation domain (DeviceBackend.perm_cc2)
+        f_cc2 = B.perm_cc2(z, z_omega, f_prime, g_prime, n)
+    else:
+        f_cc2 = B.poly_sub(B.poly_mul(z, f_prime), B.poly_mul(z_omega, g_prime))
     f = B.poly_add(B.poly_add(f_gc, B.poly_scale(f_cc1, alpha)), B.poly_scale(f_cc2, alpha * alpha % m))
     t = B.divide_by_vanishing(f, n)
     assert B.length(t) <= T_POLYS * n, f"{B.length(t)} < {T_POLYS * n}"
@@ -530,6 +534,19 @@ class DeviceBackend:
         f_ev = DevEvals(self, F.t[::CONSTRAINT_DEGREE_MULTIPLIER].contiguous())
         g_ev = DevEvals(self, G.t[::CONSTRAINT_DEGREE_MULTIPLIER].contiguous())
         return f_prime, g_prime, f_ev, g_ev
+
+    def perm_cc2(self, z, z_omega, f_prime, g_prime, n):
+        """z f' - z_omega g' (protocol.rs:198-199) on one N-point domain covering both products: NTT z,
+        f', g', pointwise Z F - Z_omega G, one iNTT (4 transforms instead of the reference's two FFT
+        products, 6).  z_omega(X) = z(omega_n X) (round 3 interpolates z's evaluations shifted by one),
+        so its N-point evaluations are z's rotated by N / n."""
+        rl = max(z.shape[0] + f_prime.shape[0] - 1, z_omega.shape[0] + g_prime.shape[0] - 1)
+        N = 1 << (rl - 1).bit_length()
+        assert N % n == 0 and z.shape[0] <= n and z_omega.shape[0] <= n
+        Z = self.ntt(z, N)
+        Zw = DevEvals(self, self.torch.roll(Z.t, -(N // n), 0))
+        P = Z * self.ntt(f_prime, N) - Zw * self.ntt(g_prime, N)
+        return self.intt(P)[:rl].contiguous()
 
     def divide_by_vanishing(self, f, n):
         L = f.shape[0]
