@@ -186,6 +186,11 @@ HALO_DEV Fe<F> pow7(const Fe<F>& x) {
 // poseidon_constraints_generic (protocol.rs:623-648) -> t (internal packed)
 template <class F>
 __global__ __launch_bounds__(256) void k_gate_poseidon(const GateArgs a, size_t N, uint32_t shift, uint4* t) {
+    // the 9 MDS entries converted to the internal form once per workgroup (LDS), not at each of their
+    // 45 uses (one multiplication each)
+    __shared__ uint4 mds[9][2];
+    if (threadIdx.x < 9) fe_store(mds[threadIdx.x], fe_from_ark_words<F>(a.mds[threadIdx.x]));
+    __syncthreads();
     GATE_PROLOGUE
     Fe<F> pos = fe_zero<F>();
 #pragma unroll 1
@@ -195,9 +200,9 @@ __global__ __launch_bounds__(256) void k_gate_poseidon(const GateArgs a, size_t 
 #pragma unroll 1
         for (int row = 0; row < 3; row++) {
             const Fe<F> nxt = (rd < 4) ? W(b + 3 + row) : NW(row);
-            Fe<F> u = fe_add(R(b + row), fe_mul(s0, fe_from_ark_words<F>(a.mds[3 * row + 0])));
-            u = fe_add(u, fe_mul(s1, fe_from_ark_words<F>(a.mds[3 * row + 1])));
-            u = fe_add(u, fe_mul(s2, fe_from_ark_words<F>(a.mds[3 * row + 2])));
+            Fe<F> u = fe_add(R(b + row), fe_mul(s0, fe_load<F>(mds[3 * row + 0])));
+            u = fe_add(u, fe_mul(s1, fe_load<F>(mds[3 * row + 1])));
+            u = fe_add(u, fe_mul(s2, fe_load<F>(mds[3 * row + 2])));
             pos = fe_add(pos, fe_sub(nxt, u));
         }
     }
