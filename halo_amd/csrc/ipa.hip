@@ -514,8 +514,16 @@ struct halo_ipa_session {
     DevBuf table, w[2], scal, side, part;
     BatchScratch mat;  // weighted -> tail switch (msm_shared_batch)
     int wcur = 0;
+    hipStream_t aux = nullptr;        // builds the 2^i H' table beside round 1's accumulation
+    hipEvent_t htab_ready = nullptr;  // recorded on aux after the table
+    bool htab_waited = false;         // round 1 waited for it (later rounds follow a host sync of round 1)
     uint8_t* pinned = nullptr;  // [128, 192) xi|xi_inv (H2D), [256, 512) L|R XYZZ (D2H): async, several sessions in flight
     ~halo_ipa_session() {
+        if (aux) {
+            (void)hipStreamSynchronize(aux);
+            (void)hipStreamDestroy(aux);
+        }
+        if (htab_ready) (void)hipEventDestroy(htab_ready);
         if (s) (void)hipStreamDestroy(s);
         if (pinned) (void)hipHostFree(pinned);
     }
@@ -743,7 +751,14 @@ static int ipa_begin(halo_curve_t curve, size_t n, const halo_wrapped_point_t* g
     ses->n = n;
     ses->m = n / 2;
     ses->s = nullptr;
+    // the side stream for the H' table only when the runtime has hardware queues to spare
+    // (GPU_MAX_HW_QUEUES >= 8, as bench.py sets): with HIP's default 4 the extra stream shares a queue
+    // with the session's and the MSM tail streams, which cost ~0.3 ms per 2^16 round
+    const char* hwq = getenv("GPU_MAX_HW_QUEUES");
+    const bool use_aux = hwq && atoi(hwq) >= 8;
     if (hipStreamCreateWithFlags(&ses->s, hipStreamNonBlocking) != hipSuccess ||
+        (use_aux && hipStreamCreateWithFlags(&ses->aux, hipStreamNonBlocking) != hipSuccess) ||
+        hipEventCreateWithFlags(&ses->htab_ready, hipEventDisableTiming) != hipSuccess ||
         hipHostMalloc((void**)&ses->pinned, 512, hipHostMallocDefault) != hipSuccess) {
         delete ses;
         return set_error(HALO_EDEVICE, "halo_ipa_begin: stream / pinned buffer allocation failed");
@@ -764,7 +779,7 @@ static int ipa_begin(halo_curve_t curve, size_t n, const halo_wrapped_point_t* g
         }
         if ((rc = ses->cs.reserve(n * 32))) break;
         if ((rc = ses->zs.reserve(n * 32))) break;
-        if ((rc = ses->htab.reserve(256 * 64))) break;
+        if ((rc = ses->htab.reserve(IPA_HTAB * (64 + 128)))) break;  // affine table + XYZZ chain scratch
         if ((rc = ses->small.reserve(1024))) break;
         if ((rc = ses->tmp.reserve(std::max<size_t>(4096 * 32, gs_host ? n * 64 : 0)))) break;
         if (gs_host) {
@@ -801,13 +816,28 @@ static int ipa_begin(halo_curve_t curve, size_t n, const halo_wrapped_point_t* g
             if (!zs_host)
                 hipLaunchKernelGGL(k_powers<typename Cv::Scalar>, dim3(gridn((n + run - 1) / run, 128)), dim3(128), 0,
                                    s, (const uint4*)sm, n, run, ses->zs.as<uint4>());
-            // 2^i H' for i < 128: the hiding terms use the GLV split of their scalar (k_hide_term)
-            hipLaunchKernelGGL(k_pow2_xyzz_from_wrapped<Cv>, dim3(1), dim3(64), 0, s, (const uint4*)(sm + 64),
-                               ses->tmp.as<uint4>(), IPA_HTAB);
-            hipLaunchKernelGGL(k_xyzz_to_aff_ipa<Cv>, dim3(IPA_HTAB / 64), dim3(64), 0, s, (const uint4*)ses->tmp.ptr,
+        });
+        // 2^i H' for i < 128 (the hiding terms use the GLV split of their scalar, k_hide_term): a
+        // ~1 ms one-lane doubling chain, built on the side stream while round 1's digits, sort and
+        // accumulation run; the hiding-term kernels wait for htab_ready
+        const hipStream_t hs = ses->aux ? ses->aux : s;
+        if (ses->aux) {
+            hipEvent_t h_in;
+            if (hipEventCreateWithFlags(&h_in, hipEventDisableTiming) != hipSuccess || hipEventRecord(h_in, s) != hipSuccess ||
+                hipStreamWaitEvent(ses->aux, h_in, 0) != hipSuccess || hipEventDestroy(h_in) != hipSuccess) {
+                rc = set_error(HALO_EDEVICE, "halo_ipa_begin: stream ordering failed");
+                break;
+            }
+        }
+        uint4* chain = ses->htab.as<uint4>() + 4 * IPA_HTAB;  // XYZZ scratch after the affine table
+        DISPATCH_CURVE(curve, Cv, {
+            hipLaunchKernelGGL(k_pow2_xyzz_from_wrapped<Cv>, dim3(1), dim3(64), 0, hs, (const uint4*)(sm + 64), chain,
+                               IPA_HTAB);
+            hipLaunchKernelGGL(k_xyzz_to_aff_ipa<Cv>, dim3(IPA_HTAB / 64), dim3(64), 0, hs, (const uint4*)chain,
                                ses->htab.as<uint4>(), IPA_HTAB);
         });
-        if (hipGetLastError() != hipSuccess) rc = set_error(HALO_EDEVICE, "ipa begin launch failed");
+        if (hipGetLastError() != hipSuccess || hipEventRecord(ses->htab_ready, hs) != hipSuccess)
+            rc = set_error(HALO_EDEVICE, "ipa begin launch failed");
         if (!rc && gs_host && hipStreamSynchronize(s) != hipSuccess)  // tmp held the staged bases
             rc = set_error(HALO_EDEVICE, "ipa begin: synchronisation failed");
     } while (0);
@@ -907,9 +937,15 @@ static int ipa_round_launch(DeviceState* st, halo_ipa_session* ses) {
     }
     if (!ses->tail && ses->allow_tail && 2 * m <= ipa_tail_n()) HALO_CHECK(ipa_enter_tail(ses, s));
     const char* gs = ses->gs.as<const char>();  // (materialised above in a weighted session)
+    // only round 1 orders its hiding terms after the side-stream table: every later round starts after
+    // the host has synchronised on round 1's results, which needed the table (a cross-stream wait in
+    // every round cost ~0.3 ms per 2^16 round)
+    hipEvent_t hr = ses->htab_waited ? nullptr : ses->htab_ready;
+    ses->htab_waited = true;
     HALO_CHECK(dot_device(sf, cs + m * 32, zs, m, sm + 128, ses->tmp.ptr, s));        // <c_r, z_l>
     HALO_CHECK(dot_device(sf, cs, zs + m * 32, m, sm + 160, ses->tmp.ptr, s));        // <c_l, z_r>
     if (ses->tail) {
+        if (hr) HALO_HIP(hipStreamWaitEvent(s, hr, 0));
         HALO_CHECK(ipa_tail_sums(ses, 0, s));
     } else if (ses->weighted) {
         const size_t half = ses->n0 / 2;  // = wlen * m terms per side
@@ -928,22 +964,22 @@ static int ipa_round_launch(DeviceState* st, halo_ipa_session* ses) {
             sr = sb + half * 32;
         }
         HALO_CHECK(msm_srs_range_device(st, ses->curve, 0, sl, half, ses->htab.ptr, sm + 128, sm + 512, s, true, lgm,
-                                        true, true));
+                                        true, true, hr));
         HALO_CHECK(msm_srs_range_device(st, ses->curve, m, sr, half, ses->htab.ptr, sm + 160, sm + 640, s, true, lgm,
-                                        true, true));
+                                        true, true, hr));
         HALO_CHECK(msm_join(st, s));
     } else {
         // L and R are independent: the second MSM's accumulation overlaps the first one's tail
         if (ses->srs_round0) {  // G_l = SRS[0, m), G_r = SRS[m, 2m): resident window-shifted copies, no Horner
             HALO_CHECK(msm_srs_range_device(st, ses->curve, 0, cs + m * 32, m, ses->htab.ptr, sm + 128, sm + 512, s, true,
-                                            32, true, true));
+                                            32, true, true, hr));
             HALO_CHECK(msm_srs_range_device(st, ses->curve, m, cs, m, ses->htab.ptr, sm + 160, sm + 640, s, true, 32,
-                                            true, true));
+                                            true, true, hr));
         } else {
             HALO_CHECK(msm_device(st, ses->curve, gs, cs + m * 32, m, ses->htab.ptr, sm + 128, sm + 512, s, true, true,
-                                  true));
+                                  true, hr));
             HALO_CHECK(msm_device(st, ses->curve, gs + m * 64, cs, m, ses->htab.ptr, sm + 160, sm + 640, s, true, true,
-                                  true));
+                                  true, hr));
         }
         HALO_CHECK(msm_join(st, s));
     }

@@ -456,7 +456,7 @@ template <class Cv>
 static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, size_t shift_stride,
                         const uint4* scalars_ark, size_t n, int c_req, const uint4* hide_table, const uint4* hide_scalar,
                         uint4* d_out_wrapped, hipStream_t s, bool async, uint32_t blk_lg = 32,
-                        bool hide_glv = false, bool out_xyzz = false) {
+                        bool hide_glv = false, bool out_xyzz = false, hipEvent_t hide_ready = nullptr) {
     MsmPipe& PP = g_msm_pipe[st->device & 63];
     HALO_CHECK(pipe_init(PP));
     const int set = msm_pick_set(PP, s, true);
@@ -509,6 +509,7 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
         hide_slot = M.window_sums.as<uint4>() + 8 * (size_t)W;
         HALO_HIP(hipEventRecord(M.start, s));
         HALO_HIP(hipStreamWaitEvent(ts, M.start, 0));
+        if (hide_ready) HALO_HIP(hipStreamWaitEvent(ts, hide_ready, 0));  // table built on a side stream
         hipLaunchKernelGGL(k_hide_term<Cv>, dim3(1), dim3(256), 0, ts, hide_table, hide_scalar, (int)hide_glv,
                            hide_slot);
         HALO_HIP(hipGetLastError());
@@ -598,12 +599,12 @@ int msm_join(DeviceState* st, hipStream_t s) {
 
 int msm_device(DeviceState* st, int curve, const void* bases_int, const void* scalars_ark, size_t n,
                const void* hide_table, const void* hide_scalar, void* d_out_wrapped, hipStream_t s, bool async,
-               bool hide_glv, bool out_xyzz) {
+               bool hide_glv, bool out_xyzz, hipEvent_t hide_ready) {
     int rc;
     DISPATCH_CURVE(curve, Cv, {
         rc = msm_device_t<Cv>(st, (const uint4*)bases_int, false, 0, (const uint4*)scalars_ark, n, 0,
                               (const uint4*)hide_table, (const uint4*)hide_scalar, (uint4*)d_out_wrapped, s, async,
-                              32, hide_glv, out_xyzz);
+                              32, hide_glv, out_xyzz, hide_ready);
     });
     return rc;
 }
@@ -629,7 +630,8 @@ int msm_srs_device(DeviceState* st, int curve, const void* scalars_ark, size_t n
 
 int msm_srs_range_device(DeviceState* st, int curve, size_t offset, const void* scalars_ark, size_t n,
                          const void* hide_table, const void* hide_scalar, void* d_out_wrapped, hipStream_t s,
-                         bool async, uint32_t blk_lg, bool hide_glv, bool out_xyzz) {
+                         bool async, uint32_t blk_lg, bool hide_glv, bool out_xyzz,
+                         hipEvent_t hide_ready) {
     SrsState& srs = st->srs[curve];
     if (!srs.shifted_c) return set_error(HALO_EINVAL, "msm_srs_range_device: no window-shifted SRS");
     // highest point touched: offset + map(n - 1), map(i) = i + (i >> blk_lg) << blk_lg
@@ -642,7 +644,7 @@ int msm_srs_range_device(DeviceState* st, int curve, size_t offset, const void* 
     DISPATCH_CURVE(curve, Cv, {
         rc = msm_device_t<Cv>(st, srs.shifted.as<const uint4>() + 4 * offset, true, srs.n, (const uint4*)scalars_ark, n,
                               srs.shifted_c, (const uint4*)hide_table, (const uint4*)hide_scalar,
-                              (uint4*)d_out_wrapped, s, async, blk_lg, hide_glv, out_xyzz);
+                              (uint4*)d_out_wrapped, s, async, blk_lg, hide_glv, out_xyzz, hide_ready);
     });
     return rc;
 }

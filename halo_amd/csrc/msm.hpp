@@ -10,9 +10,10 @@ int msm_window_bits(size_t n);
 // hide_scalar * P where hide_table = {2^i P : i < 256} (internal affine; both device pointers), or
 // with hide_glv {2^i P : i < 128} and the GLV split of the scalar (k_hide_term).  out_xyzz: the
 // result is written as 128 B packed XYZZ instead of an affine WrappedPoint (host_xyzz_to_wrapped).
+// hide_ready: event after which the hiding table is complete (built on another stream).
 int msm_device(DeviceState* st, int curve, const void* bases_int, const void* scalars_ark, size_t n,
                const void* hide_table, const void* hide_scalar, void* d_out_wrapped, hipStream_t s,
-               bool async = false, bool hide_glv = false, bool out_xyzz = false);
+               bool async = false, bool hide_glv = false, bool out_xyzz = false, hipEvent_t hide_ready = nullptr);
 // Makes stream s wait for the reduction tails of the async MSMs enqueued on s.
 int msm_join(DeviceState* st, hipStream_t s);
 // MSM over the resident SRS prefix (window-shifted copies when precomputed); optional hiding
@@ -26,7 +27,8 @@ int msm_srs_device(DeviceState* st, int curve, const void* scalars_ark, size_t n
 // occupy in the unfolded SRS.
 int msm_srs_range_device(DeviceState* st, int curve, size_t offset, const void* scalars_ark, size_t n,
                          const void* hide_table, const void* hide_scalar, void* d_out_wrapped, hipStream_t s,
-                         bool async, uint32_t blk_lg = 32, bool hide_glv = false, bool out_xyzz = false);
+                         bool async, uint32_t blk_lg = 32, bool hide_glv = false, bool out_xyzz = false,
+                         hipEvent_t hide_ready = nullptr);
 // Batched MSM with shared scalars: out[i] = sum_{u < T} w[u] bases[i + u len] for i < len
 // (internal affine bases, ark scalars; outputs internal affine, or XYZZ (128 B) when xyzz_out;
 // stream-ordered on s).
