@@ -75,6 +75,7 @@ SIGNATURES = {
     "halo_interpolate": [ctypes.c_int, _vp, ctypes.c_uint, _vp, ctypes.POINTER(_sz)],
     "halo_poly_mul": [ctypes.c_int, _vp, _sz, _vp, _sz, _vp, ctypes.POINTER(_sz)],
     "halo_ntt_dev": [ctypes.c_int, _vp, ctypes.c_uint, _sz, ctypes.c_int, _vp],
+    "halo_ntt_dev_zero_tail": [ctypes.c_int, _vp, ctypes.c_uint, _sz, _sz, _vp],
     "halo_hpoly_coeffs": [ctypes.c_int, _vp, _sz, _vp],
     "halo_hpoly_combine": [ctypes.c_int, _vp, _sz, _sz, _vp, _vp, ctypes.POINTER(_sz)],
     "halo_pcdl_decider_commit": [ctypes.c_int, _vp, _sz, _sz, _vp],

@@ -44,7 +44,7 @@ void host_xyzz_to_wrapped(int curve, const void* xyzz, void* wrapped);
 int convert_wrapped_to_internal(int curve, const void* in, void* out, size_t n, hipStream_t s);
 int convert_internal_to_wrapped(int curve, const void* in, void* out, size_t n, hipStream_t s);
 int ntt_device_dispatch(DeviceState* st, int field, const void* d_in, void* d_out, void* d_tmp, unsigned logn,
-                        size_t batch, int inverse, hipStream_t s, void* d_tmp2 = nullptr);
+                        size_t batch, int inverse, hipStream_t s, void* d_tmp2 = nullptr, unsigned prune = 0);
 
 // chunk-partial group size of the skew guard (msm_tail.hip k_group_sums)
 constexpr uint32_t MSM_GROUP = 64;

@@ -18,6 +18,7 @@
 #include <cstdlib>
 
 #include "dispatch.hpp"
+#include "msm.hpp"
 #include "runtime.hpp"
 
 namespace halo {
@@ -38,6 +39,10 @@ struct NttPassArgs {
     const uint4* stage_tw;  // entry 2^s - 1 + k = omega_{2^(s+1)}^k (s < 8, k < 2^s)
     uint32_t logn, log_r, log_ns, lo_bits;
     uint32_t in_ark, out_ark;
+    // pass 0 of a forward transform whose inputs beyond N / 2^prune are zero: the first `prune`
+    // radix-2 stages only replicate each nonzero input across its 2^prune-element group (b = 0 in every
+    // butterfly), so the pass loads one element per group and starts at stage `prune`
+    uint32_t prune;
     // Output multiplier.  The first pass takes the ark words (x 2^256 mod p) directly as internal
     // values, i.e. as x 2^-5 in Montgomery form with R' = 2^261; the transform is linear, so the last
     // pass multiplies by 2^261 (forward) or 2^261 / N (inverse) and emits ark words again: the
@@ -177,7 +182,8 @@ __global__ __launch_bounds__(NE / NTT_EPT) void k_ntt_pass(NttPassArgs a) {
         const uint32_t pos = base + m;
         if (pos < EB) {
             const uint32_t t = pos >> r;
-            const uint32_t rho = r ? (__brev(pos & (R - 1)) >> (32 - r)) : 0;
+            const uint32_t pl = a.prune ? (pos & ~((1u << a.prune) - 1u)) : pos;  // the group's nonzero input
+            const uint32_t rho = r ? (__brev(pl & (R - 1)) >> (32 - r)) : 0;
             const size_t j = j0 + t;
             const uint4* src = in + 2 * (j + (size_t)rho * NJ);
             Fe<F> x = fe_load<F>(src);  // ark words are used as internal values (see out_const)
@@ -202,7 +208,7 @@ __global__ __launch_bounds__(NE / NTT_EPT) void k_ntt_pass(NttPassArgs a) {
     }
     // odd r on the wide blocks: the single-stage group goes first, so later groups stay in range
     const uint32_t G0 = (NE >= NTT_E_BIG && (r & 1)) ? 1u : (r < (uint32_t)LG ? r : (uint32_t)LG);
-    ntt_group<F, EPT, LG>(v, 0, G0, 0, a.stage_tw);
+    if (!a.prune) ntt_group<F, EPT, LG>(v, 0, G0, 0, a.stage_tw);  // (pruned: host guarantees prune >= G0)
     {
         const uint32_t pb = ntt_swz<NE>(base);
 #pragma unroll
@@ -212,7 +218,7 @@ __global__ __launch_bounds__(NE / NTT_EPT) void k_ntt_pass(NttPassArgs a) {
     __syncthreads();
 
     // ---- remaining stages in groups of LG through LDS
-    for (uint32_t s = G0; s < r; s += LG) {
+    for (uint32_t s = a.prune ? a.prune : G0; s < r; s += LG) {
         const uint32_t G = (r - s) < (uint32_t)LG ? (r - s) : (uint32_t)LG;
         const uint32_t h = 1u << s;
         const uint32_t gb = (tau & (h - 1)) | ((tau >> s) << (s + LG));
@@ -455,7 +461,7 @@ static int get_twiddles(DeviceState* st, int field, unsigned logn, int inverse, 
 // d_in, d_tmp2 (same size) takes that pass's output instead.  Buffers hold batch * N elements.
 template <class F>
 static int ntt_device(DeviceState* st, int field, const void* d_in, void* d_out, void* d_tmp, void* d_tmp2,
-                      unsigned logn, size_t batch, int inverse, hipStream_t s) {
+                      unsigned logn, size_t batch, int inverse, hipStream_t s, unsigned prune = 0) {
     if (logn > 30) return set_error(HALO_EINVAL, "NTT domain 2^%u too large", logn);
     const size_t N = (size_t)1 << logn;
     if (logn == 0) {
@@ -491,6 +497,16 @@ static int ntt_device(DeviceState* st, int field, const void* d_in, void* d_out,
         a.lo_bits = (uint32_t)tw->lo_bits;
         a.in_ark = (p == 0);
         a.out_ark = (p == P - 1);
+        a.prune = 0;
+        if (p == 0 && prune && !inverse) {  // only when it covers the pass's first register group
+            const bool big = lr > NTT_MAX_LOG_R_MULTI;
+            const unsigned g0 = (big && (lr & 1)) ? 1u : std::min(lr, 2u);
+            unsigned pr = std::min(prune, lr);
+            // one column per wide block: a trailing single-stage group would reach past the column,
+            // so the stages left after the pruned ones must pair up (as G0 = 1 arranges for odd r)
+            if (big && ((lr - pr) & 1)) pr--;
+            if (pr >= g0 && pr < lr) a.prune = pr;
+        }
         for (int l = 0; l < NLIMB; l++) a.out_const[l] = inverse ? F::NINV_ARK[logn][l] : F::ONE[l];
         a.stride = N;
         const size_t NJ = N >> lr;
@@ -510,9 +526,11 @@ static int ntt_device(DeviceState* st, int field, const void* d_in, void* d_out,
 }
 
 int ntt_device_dispatch(DeviceState* st, int field, const void* d_in, void* d_out, void* d_tmp, unsigned logn,
-                        size_t batch, int inverse, hipStream_t s, void* d_tmp2) {
+                        size_t batch, int inverse, hipStream_t s, void* d_tmp2, unsigned prune) {
     int rc;
-    DISPATCH_FIELD(field, F, { rc = ntt_device<F>(st, field, d_in, d_out, d_tmp, d_tmp2, logn, batch, inverse, s); });
+    DISPATCH_FIELD(field, F, {
+        rc = ntt_device<F>(st, field, d_in, d_out, d_tmp, d_tmp2, logn, batch, inverse, s, prune);
+    });
     return rc;
 }
 
@@ -609,6 +627,28 @@ extern "C" int halo_ntt_dev(halo_field_t field, void* d_data, unsigned log_n, si
     HALO_CHECK(st->scratch[5].reserve(batch * N * 32));
     return ntt_device_dispatch(st, field, d_data, d_data, st->scratch[4].ptr, log_n, batch, inverse, s,
                                st->scratch[5].ptr);
+}
+
+// Forward device NTT of data whose elements at index >= nonzero_len are zero (the prover's
+// evaluate_over_domain of a degree < n polynomial on the 8n domain): those elements are not read,
+// and the first pass skips the lg(N / 2^ceil(lg nonzero_len)) stages that only replicate values.
+extern "C" int halo_ntt_dev_zero_tail(halo_field_t field, void* d_data, unsigned log_n, size_t batch,
+                                      size_t nonzero_len, void* stream) {
+    clear_error();
+    HALO_CHECK(check_field(field));
+    if (!d_data) return set_error(HALO_EINVAL, "halo_ntt_dev_zero_tail: null buffer");
+    const size_t N = (size_t)1 << log_n;
+    if (nonzero_len > N) return set_error(HALO_EINVAL, "halo_ntt_dev_zero_tail: nonzero_len > N");
+    unsigned lg_nz = 0;
+    while (((size_t)1 << lg_nz) < std::max<size_t>(nonzero_len, 1)) lg_nz++;
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    hipStream_t s = (hipStream_t)stream;
+    HALO_CHECK(st->scratch[4].reserve(batch * N * 32));
+    HALO_CHECK(st->scratch[5].reserve(batch * N * 32));
+    return ntt_device_dispatch(st, field, d_data, d_data, st->scratch[4].ptr, log_n, batch, 0, s, st->scratch[5].ptr,
+                               log_n - lg_nz);
 }
 
 extern "C" int halo_ntt_twiddle_dev(halo_field_t field, void* d_data, unsigned log_n, size_t rows, size_t cols,

@@ -434,7 +434,10 @@ class DeviceBackend:
         for s in range(N, L, N):
             k = min(N, L - s)
             self._op(0, x[:k], p[s:s + k], None, 0, x[:k])
-        self.H.check(self.L.halo_ntt_dev(self.field, self._p(x), N.bit_length() - 1, 1, 0, self.sp))
+        if L < N:  # zero tail: the first pass skips the stages that only replicate values
+            self.H.check(self.L.halo_ntt_dev_zero_tail(self.field, self._p(x), N.bit_length() - 1, 1, L, self.sp))
+        else:
+            self.H.check(self.L.halo_ntt_dev(self.field, self._p(x), N.bit_length() - 1, 1, 0, self.sp))
         return DevEvals(self, x)
 
     def intt(self, e):

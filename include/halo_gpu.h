@@ -158,6 +158,11 @@ int halo_poly_mul(halo_field_t field, const halo_fe_t* a, size_t la, const halo_
 /* Batched device NTT: `batch` contiguous transforms of size 2^log_n at d_data, in place. */
 int halo_ntt_dev(halo_field_t field, void* d_data, unsigned log_n, size_t batch, int inverse,
                  void* stream);
+/* Forward halo_ntt_dev for inputs that are zero from index nonzero_len on (a polynomial of degree
+ * < nonzero_len evaluated over a larger domain, protocol.rs:89-106): those elements are not read and
+ * the first pass skips the stages that only replicate values. */
+int halo_ntt_dev_zero_tail(halo_field_t field, void* d_data, unsigned log_n, size_t batch,
+                           size_t nonzero_len, void* stream);
 /* Distributed-NTT building blocks (four-step decomposition, halo_amd/dist.py sharded_ntt; SURVEY
  * §8e).  halo_ntt_twiddle_dev: element (a, b) of the rows x cols matrix at d_data (ark format) is
  * multiplied by omega_N^((row0 + a)(col0 + b)) (omega^-1 when inverse), N = 2^log_n.
