@@ -408,6 +408,18 @@ static std::vector<unsigned> ntt_radices(unsigned logn) {
     return r;
 }
 
+// Stages of pass 0 (radix 2^lr) that a zero tail lets the pass skip (NttPassArgs::prune): only when
+// they cover its first register group; on one-column wide blocks a trailing single-stage group would
+// reach past the column, so the stages left after the pruned ones must pair up (as G0 = 1 arranges).
+static unsigned ntt_pass0_prune(unsigned lr, unsigned prune) {
+    if (!prune) return 0;
+    const bool big = lr > NTT_MAX_LOG_R_MULTI;
+    const unsigned g0 = (big && (lr & 1)) ? 1u : std::min(lr, 2u);
+    unsigned pr = std::min(prune, lr);
+    if (big && ((lr - pr) & 1)) pr--;
+    return (pr >= g0 && pr < lr) ? pr : 0u;
+}
+
 template <class F>
 static int get_twiddles(DeviceState* st, int field, unsigned logn, int inverse, DeviceState::Twiddles** out,
                         hipStream_t s) {
@@ -497,16 +509,7 @@ static int ntt_device(DeviceState* st, int field, const void* d_in, void* d_out,
         a.lo_bits = (uint32_t)tw->lo_bits;
         a.in_ark = (p == 0);
         a.out_ark = (p == P - 1);
-        a.prune = 0;
-        if (p == 0 && prune && !inverse) {  // only when it covers the pass's first register group
-            const bool big = lr > NTT_MAX_LOG_R_MULTI;
-            const unsigned g0 = (big && (lr & 1)) ? 1u : std::min(lr, 2u);
-            unsigned pr = std::min(prune, lr);
-            // one column per wide block: a trailing single-stage group would reach past the column,
-            // so the stages left after the pruned ones must pair up (as G0 = 1 arranges for odd r)
-            if (big && ((lr - pr) & 1)) pr--;
-            if (pr >= g0 && pr < lr) a.prune = pr;
-        }
+        a.prune = (p == 0 && !inverse) ? ntt_pass0_prune(lr, prune) : 0u;
         for (int l = 0; l < NLIMB; l++) a.out_const[l] = inverse ? F::NINV_ARK[logn][l] : F::ONE[l];
         a.stride = N;
         const size_t NJ = N >> lr;
@@ -647,6 +650,13 @@ extern "C" int halo_ntt_dev_zero_tail(halo_field_t field, void* d_data, unsigned
     hipStream_t s = (hipStream_t)stream;
     HALO_CHECK(st->scratch[4].reserve(batch * N * 32));
     HALO_CHECK(st->scratch[5].reserve(batch * N * 32));
+    // the tail's contents are ignored: zero exactly what pass 0 will read beyond nonzero_len (up to
+    // 2^ceil(lg nonzero_len) when it prunes, the whole tail otherwise)
+    const unsigned pr = log_n ? ntt_pass0_prune(ntt_radices(log_n)[0], log_n - lg_nz) : 0u;
+    const size_t read_end = pr ? (N >> pr) : N;
+    if (read_end > nonzero_len)
+        for (size_t b = 0; b < batch; b++)
+            HALO_HIP(hipMemsetAsync((char*)d_data + (b * N + nonzero_len) * 32, 0, (read_end - nonzero_len) * 32, s));
     return ntt_device_dispatch(st, field, d_data, d_data, st->scratch[4].ptr, log_n, batch, 0, s, st->scratch[5].ptr,
                                log_n - lg_nz);
 }

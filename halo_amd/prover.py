@@ -428,8 +428,9 @@ class DeviceBackend:
     def ntt(self, p, N: int):
         """evaluate_over_domain_by_ref: fold mod X^N - 1 when longer, zero-pad, forward NTT."""
         p = p.t if isinstance(p, DevEvals) else p
-        x = self.torch.zeros((N, 4), dtype=self.torch.int64, device="cuda")
         L = p.shape[0]
+        # a zero tail is cleared (only as far as it is read) by halo_ntt_dev_zero_tail itself
+        x = (self.torch.empty if L < N else self.torch.zeros)((N, 4), dtype=self.torch.int64, device="cuda")
         x[:min(L, N)] = p[:min(L, N)]
         for s in range(N, L, N):
             k = min(N, L - s)

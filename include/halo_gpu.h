@@ -159,8 +159,8 @@ int halo_poly_mul(halo_field_t field, const halo_fe_t* a, size_t la, const halo_
 int halo_ntt_dev(halo_field_t field, void* d_data, unsigned log_n, size_t batch, int inverse,
                  void* stream);
 /* Forward halo_ntt_dev for inputs that are zero from index nonzero_len on (a polynomial of degree
- * < nonzero_len evaluated over a larger domain, protocol.rs:89-106): those elements are not read and
- * the first pass skips the stages that only replicate values. */
+ * < nonzero_len evaluated over a larger domain, protocol.rs:89-106): the tail's contents are ignored
+ * (the caller need not clear it) and the first pass skips the stages that only replicate values. */
 int halo_ntt_dev_zero_tail(halo_field_t field, void* d_data, unsigned log_n, size_t batch,
                            size_t nonzero_len, void* stream);
 /* Distributed-NTT building blocks (four-step decomposition, halo_amd/dist.py sharded_ntt; SURVEY

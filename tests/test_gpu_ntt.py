@@ -269,8 +269,9 @@ def test_divide_by_vanishing_poly(hal, tag):
 @pytest.mark.parametrize("logn,nz", [(8, 32), (8, 33), (12, 100), (18, 1 << 15), (20, 1 << 17), (20, 5),
                                      (23, 1 << 20), (23, (1 << 20) - 3), (22, 1 << 20)])
 def test_ntt_zero_tail_matches_full(hal, logn, nz):
-    """halo_ntt_dev_zero_tail (first pass skips the stages that only replicate the nonzero prefix) equals
-    halo_ntt_dev on the same zero-padded input: 1-, 2- and 3-pass sizes, power-of-two and ragged prefixes."""
+    """halo_ntt_dev_zero_tail (first pass skips the stages that only replicate the nonzero prefix; the
+    tail's contents are ignored, here garbage) equals halo_ntt_dev on the zero-padded input: 1-, 2- and
+    3-pass sizes, power-of-two and ragged prefixes."""
     import torch
 
     N = 1 << logn
@@ -280,6 +281,7 @@ def test_ntt_zero_tail_matches_full(hal, logn, nz):
     v = torch.randint(0, 2**62, (nz, 4), dtype=torch.int64, device="cuda", generator=g)
     x[:nz] = v
     y = x.clone()
+    y[nz:] = torch.randint(0, 2**62, (N - nz, 4), dtype=torch.int64, device="cuda", generator=g)  # ignored tail
     s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     hal.check(L.halo_ntt_dev(0, ctypes.c_void_p(x.data_ptr()), logn, 1, 0, s))
     hal.check(L.halo_ntt_dev_zero_tail(0, ctypes.c_void_p(y.data_ptr()), logn, 1, nz, s))
