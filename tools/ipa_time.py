@@ -1,6 +1,7 @@
 """Times a full device-resident IPA opening (pcdl.rs:392-438 round loop): lg n rounds of L/R MSMs +
 fold, with a stand-in transcript (fixed pseudo-random challenges)."""
-import ctypes, random, sys, time
+import ctypes, os, random, sys, time
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")  # as bench.py
 sys.path.insert(0, '/root/repo')
 import numpy as np
 from halo_amd import _lib as H
