@@ -5,15 +5,16 @@
 // `DensePolynomial::evaluate_over_domain_by_ref` (crates/plonk/src/plonk/protocol.rs:89-106,140-141)
 // and FFT polynomial multiplication (`&Poly * &Poly`, protocol.rs:132-139, pcdl.rs:215).
 //
-// Algorithm: Stockham auto-sort, radix R = 2^r per pass (r <= 8, Σ r = log N), natural order in
-// and out, out-of-place ping-pong.  One workgroup owns T = E / R consecutive columns j of a pass
-// (E = elements per workgroup): it loads x[j + r N/R] (T-element contiguous runs), multiplies by the
-// Stockham twiddle omega_{Ns R}^(r (j mod Ns)) (two-level table, L2 resident), performs the R-point
-// DFT as r radix-2 DIT stages in LDS (bit-reversed placement on load, omega_R table in LDS), and
-// writes y[(j / Ns) Ns R + (j mod Ns) + k Ns].  Field elements live in LDS in the 9 x 29-bit limb
-// form (stride 9 dwords: conflict-free for consecutive lanes).  The first pass converts from the
-// ark ABI format and the last pass converts back (with the N^-1 scaling for the inverse); the
-// intermediate buffers hold the internal packed format.
+// Algorithm: Stockham auto-sort, radix R = 2^r per pass (Σ r = log N; the pass split is
+// `ntt_radices` below: two passes of up to 11 bits for 2^17..2^22, passes of <= 8 bits otherwise),
+// natural order in and out, out-of-place ping-pong.  One workgroup owns T = E / R consecutive
+// columns j of a pass (E = 1024 or 2048 elements per workgroup): it loads x[j + r N/R] (T-element
+// contiguous runs), multiplies by the Stockham twiddle read coalesced from the per-pass
+// pre-twiddle table, performs the R-point DFT as radix-4 register groups (two radix-2 DIT stages
+// per LDS round trip), and writes y[(j / Ns) Ns R + (j mod Ns) + k Ns].  Field elements live in LDS
+// in the 9 x 29-bit limb form, limb-major with an XOR bank swizzle (see NttSwz).  The first pass
+// takes ark words unconverted and the last pass multiplies by 2^261 (or 2^261 / N for the inverse),
+// see NttPassArgs::out_const; the intermediate buffers hold the internal packed format.
 #include <algorithm>
 #include <cstdlib>
 
