@@ -200,7 +200,10 @@ __global__ void k_digits_glv(const uint4* scalars, size_t n, int c, int W, uint3
 // buckets strictly inside the chunk are complete, so they go straight to bucket_sums.  k_merge then
 // completes the buckets that straddle chunk boundaries.
 template <class Cv>
-__global__ __launch_bounds__(256, 4) void k_acc(const uint32_t* keys, const uint32_t* vals, const uint32_t* count,
+#ifndef HALO_ACC_MINB
+#define HALO_ACC_MINB 4  // workgroups per CU the register budget is sized for (A/B builds override)
+#endif
+__global__ __launch_bounds__(256, HALO_ACC_MINB) void k_acc(const uint32_t* keys, const uint32_t* vals, const uint32_t* count,
                                              uint32_t K, const uint4* bases, uint32_t n_per_window, size_t stride,
                                              uint32_t blk_lg, uint32_t glv_n, uint4* first, uint4* last,
                                              uint4* bucket_sums) {
