@@ -136,6 +136,56 @@ HALO_DEV XYZZ<F> xyzz_madd(const XYZZ<F>& p, const Affine<F>& q) {
     return r;
 }
 
+// Bucket-accumulation form of madd-2008-s (k_acc's inner loop), same result as
+// xyzz_madd(p, negmask ? -q : q) but ~14 % fewer instructions:
+//   * the sign of q is folded into R = +-S2 - Y1 + 4p (no separate negation of y);
+//   * X is carried lazily in [0, 8p) between additions (no reduction of X3; callers reduce with
+//     xyzz_settle before storing or handing the point to the general formulas);
+//   * Y3 = R (Q - X3) + PPP (2p - Y1) is one product sum with a single Montgomery reduction.
+// Bounds: P < 10p, R < 6p, T = Q - X3 + 8p < 10p; P^2 < 100p^2 and R T + PPP (2p - Y1) < 64p^2 stay
+// below p 2^261 (~127p^2), so every product is < 2p.  CHECK_ID = false when q is known not to be the
+// identity (the resident SRS, checked when its shifted copies are built).
+template <class F, bool CHECK_ID>
+HALO_DEV XYZZ<F> xyzz_madd_acc(const XYZZ<F>& p, const Affine<F>& q, uint32_t negmask) {
+    if (CHECK_ID && aff_is_id(q)) return p;
+    if (xyzz_is_id(p)) {
+        XYZZ<F> r = xyzz_from_aff(q);
+        if (negmask) r.Y = fe_neg(q.y);
+        return r;
+    }
+    const Fe<F> U2 = fe_mul(q.x, p.ZZ);
+    const Fe<F> S2 = fe_mul(q.y, p.ZZZ);
+    const Fe<F> P = fe_sub_k<8>(U2, p.X);              // < 10p
+    const Fe<F> R = fe_sub_k_sgn<4>(S2, p.Y, negmask);  // < 6p
+    const Fe<F> PP = fe_sqr(P);
+    const Fe<F> ZZ3 = fe_mul(p.ZZ, PP);
+    if (fe_is_zero(ZZ3)) {  // U2 == X1: q = +-p
+        if (fe_is_zero(fe_reduce_8p(R))) {
+            Affine<F> qs = q;
+            if (negmask) qs.y = fe_neg(q.y);
+            return xyzz_mdbl(qs);
+        }
+        return xyzz_id<F>();
+    }
+    const Fe<F> PPP = fe_mul(P, PP);
+    const Fe<F> Q = fe_mul(p.X, PP);
+    XYZZ<F> r;
+    r.X = fe_sub_k<6>(fe_sqr(R), fe_add_nc(PPP, fe_add_nc(Q, Q)));  // < 8p
+    const Fe<F> T = fe_sub_k<8>(Q, r.X);                              // < 10p
+    r.Y = fe_mul2(R, T, PPP, fe_sub_k<2>(fe_zero<F>(), p.Y));
+    r.ZZ = ZZ3;
+    r.ZZZ = fe_mul(p.ZZZ, PPP);
+    return r;
+}
+
+// X of an xyzz_madd_acc accumulator back below 2p (storage needs < 2^256; the general formulas < 2p)
+template <class F>
+HALO_DEV XYZZ<F> xyzz_settle(const XYZZ<F>& p) {
+    XYZZ<F> r = p;
+    r.X = fe_reduce_8p(p.X);
+    return r;
+}
+
 // General addition (add-2008-s), handles identity and the doubling / inverse cases.
 template <class F>
 HALO_DEV XYZZ<F> xyzz_add(const XYZZ<F>& p, const XYZZ<F>& q) {

@@ -387,6 +387,7 @@ extern "C" int halo_evals_op(halo_field_t field, int op, const halo_fe_t* a, con
     if (!st) return HALO_EDEVICE;
     std::lock_guard<std::mutex> g(st->mu);
     hipStream_t s = 0;
+    ScratchUse su(st, s);
     HALO_CHECK(st->scratch[0].reserve(n * 32));
     HALO_CHECK(st->scratch[1].reserve(n * 32));
     HALO_CHECK(copy_h2d(st->scratch[0].ptr, a, n * 32, s));
@@ -417,6 +418,7 @@ extern "C" int halo_divide_by_vanishing(halo_field_t field, const halo_fe_t* coe
     if (!st) return HALO_EDEVICE;
     std::lock_guard<std::mutex> g(st->mu);
     hipStream_t s = 0;
+    ScratchUse su(st, s);
     const size_t qn = len - n;
     HALO_CHECK(st->scratch[0].reserve(len * 32));
     HALO_CHECK(st->scratch[1].reserve(std::max<size_t>(qn, 1) * 32));
@@ -447,6 +449,7 @@ extern "C" int halo_evals_scan_dev(halo_field_t field, int reverse, const void* 
     const size_t nb = (n + SCAN_BLOCK - 1) / SCAN_BLOCK;
     if (nb > (size_t)SCAN_THREADS * 4096) return set_error(HALO_EINVAL, "halo_evals_scan_dev: n too large");
     hipStream_t s = (hipStream_t)stream;
+    ScratchUse su(st, s);
     DevBuf* tot;
     {
         std::lock_guard<std::mutex> g(st->mu);
@@ -514,6 +517,7 @@ extern "C" int halo_gate_constraints_dev(halo_field_t field, const void* const* 
     uint4* t1 = t0 + 2 * n;
     const dim3 grid((unsigned)((n + 255) / 256));
     hipStream_t s = (hipStream_t)stream;
+    ScratchUse su(st, s);
     DISPATCH_FIELD(field, F, {
         hipLaunchKernelGGL(k_gate_poseidon<F>, grid, dim3(256), 0, s, a, n, (uint32_t)shift, t0);
         hipLaunchKernelGGL(k_gate_affine<F>, grid, dim3(256), 0, s, a, n, (uint32_t)shift, t1);

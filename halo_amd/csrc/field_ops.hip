@@ -108,6 +108,7 @@ extern "C" int halo_field_op(halo_field_t field, int op, const halo_fe_t* a, con
     HALO_CHECK(st->scratch[1].reserve(bytes));
     HALO_CHECK(st->scratch[2].reserve(bytes));
     hipStream_t s = 0;
+    ScratchUse su(st, s);
     HALO_CHECK(copy_h2d(st->scratch[0].ptr, a, bytes, s));
     if (b) HALO_CHECK(copy_h2d(st->scratch[1].ptr, b, bytes, s));
     const unsigned threads = 256, blocks = (unsigned)((n + threads - 1) / threads);
@@ -135,6 +136,7 @@ extern "C" int halo_curve_op(halo_curve_t curve, int op, const halo_wrapped_poin
     HALO_CHECK(st->scratch[2].reserve(kb));
     HALO_CHECK(st->scratch[3].reserve(pb));
     hipStream_t s = 0;
+    ScratchUse su(st, s);
     HALO_CHECK(copy_h2d(st->scratch[0].ptr, a, pb, s));
     if (b) HALO_CHECK(copy_h2d(st->scratch[1].ptr, b, pb, s));
     if (k) HALO_CHECK(copy_h2d(st->scratch[2].ptr, k, kb, s));

@@ -187,6 +187,79 @@ HALO_DEV Fe<C> fe_mul(const Fe<C>& a, const Fe<C>& b) {
     return r;
 }
 
+// Product sum a b + c d with ONE Montgomery reduction (81 + 81 + 45 mads instead of 2 x 126 and a
+// modular addition).  Every input normalized (limbs < 2^29): a column holds <= 18 products + 5
+// reduction products < 2^58, i.e. < 2^62.6.  Output < 2p when a b + c d < p 2^261 (~127 p^2).
+template <class C>
+HALO_DEV Fe<C> fe_mul2(const Fe<C>& a, const Fe<C>& b, const Fe<C>& c, const Fe<C>& d) {
+    uint32_t m[NLIMB];
+    Fe<C> r;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 2 * NLIMB - 1; k++) {
+#pragma unroll
+        for (int i = 0; i < NLIMB; i++) {
+            const int j = k - i;
+            if (j < 0 || j >= NLIMB) continue;
+            acc = mad_acc(a.v[i], b.v[j], acc);
+        }
+#pragma unroll
+        for (int i = 0; i < NLIMB; i++) {
+            const int j = k - i;
+            if (j < 0 || j >= NLIMB) continue;
+            acc = mad_acc(c.v[i], d.v[j], acc);
+        }
+        acc = fe_reduce_col<C>(m, k, acc);
+        if (k < NLIMB) {
+            const uint32_t mk = (0u - (uint32_t)acc) & LIMB_MASK;
+            m[k] = mk;
+            acc += mk;
+            acc >>= LIMB_BITS;
+        } else {
+            r.v[k - NLIMB] = (uint32_t)acc & LIMB_MASK;
+            acc >>= LIMB_BITS;
+        }
+    }
+    r.v[NLIMB - 1] = (uint32_t)acc;
+    return r;
+}
+
+// Two independent products r1 = a1 b1, r2 = a2 b2 with their column chains interleaved mad by mad:
+// a single product's column is one dependent v_mad_u64_u32 chain, whose latency 4 waves per SIMD do
+// not cover; two chains side by side do (same instruction count as two fe_mul).
+template <class C>
+HALO_DEV void fe_mul_x2(const Fe<C>& a1, const Fe<C>& b1, const Fe<C>& a2, const Fe<C>& b2, Fe<C>& r1, Fe<C>& r2) {
+    uint32_t m1[NLIMB], m2[NLIMB];
+    uint64_t acc1 = 0, acc2 = 0;
+#pragma unroll
+    for (int k = 0; k < 2 * NLIMB - 1; k++) {
+#pragma unroll
+        for (int i = 0; i < NLIMB; i++) {
+            const int j = k - i;
+            if (j < 0 || j >= NLIMB) continue;
+            acc1 = mad_acc(a1.v[i], b1.v[j], acc1);
+            acc2 = mad_acc(a2.v[i], b2.v[j], acc2);
+        }
+        acc1 = fe_reduce_col<C>(m1, k, acc1);
+        acc2 = fe_reduce_col<C>(m2, k, acc2);
+        if (k < NLIMB) {
+            const uint32_t mk1 = (0u - (uint32_t)acc1) & LIMB_MASK;
+            const uint32_t mk2 = (0u - (uint32_t)acc2) & LIMB_MASK;
+            m1[k] = mk1;
+            m2[k] = mk2;
+            acc1 = (acc1 + mk1) >> LIMB_BITS;
+            acc2 = (acc2 + mk2) >> LIMB_BITS;
+        } else {
+            r1.v[k - NLIMB] = (uint32_t)acc1 & LIMB_MASK;
+            r2.v[k - NLIMB] = (uint32_t)acc2 & LIMB_MASK;
+            acc1 >>= LIMB_BITS;
+            acc2 >>= LIMB_BITS;
+        }
+    }
+    r1.v[NLIMB - 1] = (uint32_t)acc1;
+    r2.v[NLIMB - 1] = (uint32_t)acc2;
+}
+
 // Squaring: cross products doubled up front (45 mads instead of 81).
 template <class C>
 HALO_DEV Fe<C> fe_sqr(const Fe<C>& a) {
@@ -302,6 +375,24 @@ HALO_DEV Fe<C> fe_sub_k(const Fe<C>& a, const Fe<C>& b) {
 #pragma unroll
     for (int i = 0; i < NLIMB; i++) {
         int32_t x = (int32_t)a.v[i] - (int32_t)b.v[i] + (int32_t)kp[i] + c;
+        s.v[i] = (i == NLIMB - 1) ? (uint32_t)x : ((uint32_t)x & LIMB_MASK);
+        c = x >> LIMB_BITS;
+    }
+    return s;
+}
+
+// (+-a) - b + K p: the sign of a taken from negmask (0 or ~0u), folded into the limb loop (a limb-wise
+// two's complement negation is the negation of the value; the signed carry chain absorbs it).
+// Bounds as fe_sub_k, with a + b < K p when negated.
+template <int K, class C>
+HALO_DEV Fe<C> fe_sub_k_sgn(const Fe<C>& a, const Fe<C>& b, uint32_t negmask) {
+    const uint32_t* kp = (K == 2) ? C::P2 : (K == 4) ? C::P4 : (K == 6) ? C::P6 : C::P8;
+    Fe<C> s;
+    int32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < NLIMB; i++) {
+        const int32_t ai = (int32_t)((a.v[i] ^ negmask) - negmask);
+        int32_t x = ai - (int32_t)b.v[i] + (int32_t)kp[i] + c;
         s.v[i] = (i == NLIMB - 1) ? (uint32_t)x : ((uint32_t)x & LIMB_MASK);
         c = x >> LIMB_BITS;
     }

@@ -542,6 +542,7 @@ extern "C" int halo_scalar_dot(halo_field_t field, const halo_fe_t* xs, const ha
     if (!st) return HALO_EDEVICE;
     std::lock_guard<std::mutex> g(st->mu);
     hipStream_t s = 0;
+    ScratchUse su(st, s);
     HALO_CHECK(st->scratch[0].reserve(std::max<size_t>(n, 1) * 32));
     HALO_CHECK(st->scratch[1].reserve(std::max<size_t>(n, 1) * 32));
     HALO_CHECK(st->scratch[2].reserve(2048 * 32 + 64));
@@ -561,6 +562,7 @@ extern "C" int halo_construct_powers(halo_field_t field, const halo_fe_t* z, siz
     if (!st) return HALO_EDEVICE;
     std::lock_guard<std::mutex> g(st->mu);
     hipStream_t s = 0;
+    ScratchUse su(st, s);
     HALO_CHECK(st->scratch[0].reserve(n * 32 + 32));
     char* b = (char*)st->scratch[0].ptr;
     HALO_CHECK(copy_h2d(b, z, 32, s));
@@ -583,6 +585,7 @@ extern "C" int halo_poly_eval_batch(halo_field_t field, const halo_fe_t* const* 
     if (!st) return HALO_EDEVICE;
     std::lock_guard<std::mutex> g(st->mu);
     hipStream_t s = 0;
+    ScratchUse su(st, s);
     size_t total = 0, maxlen = 0;
     for (size_t i = 0; i < k; i++) {
         if (lens[i] && !polys[i]) return set_error(HALO_EINVAL, "halo_poly_eval_batch: null polynomial %zu", i);
@@ -632,6 +635,7 @@ extern "C" int halo_poly_eval_batch_dev(halo_field_t field, const void* const* d
     if (!st) return HALO_EDEVICE;
     std::lock_guard<std::mutex> g(st->mu);
     hipStream_t s = (hipStream_t)stream;
+    ScratchUse su(st, s);
     size_t maxlen = 0;
     for (size_t i = 0; i < k; i++) {
         if (lens[i] && !d_polys[i]) return set_error(HALO_EINVAL, "halo_poly_eval_batch_dev: null polynomial %zu", i);
@@ -679,6 +683,7 @@ extern "C" int halo_poly_mul(halo_field_t field, const halo_fe_t* a, size_t la, 
     if (!st) return HALO_EDEVICE;
     std::lock_guard<std::mutex> g(st->mu);
     hipStream_t s = 0;
+    ScratchUse su(st, s);
     for (int i = 0; i < 5; i++) HALO_CHECK(st->scratch[i].reserve(N * 32));
     char* A = (char*)st->scratch[0].ptr;
     char* Bv = (char*)st->scratch[1].ptr;
@@ -1141,6 +1146,7 @@ extern "C" int halo_ipa_fold_host(halo_curve_t curve, halo_wrapped_point_t* gs, 
     if (!st) return HALO_EDEVICE;
     std::lock_guard<std::mutex> g(st->mu);
     hipStream_t s = 0;
+    ScratchUse su(st, s);
     HALO_CHECK(st->scratch[0].reserve(2 * m * 64));
     HALO_CHECK(st->scratch[1].reserve(2 * m * 64));
     HALO_CHECK(st->scratch[2].reserve(2 * m * 32));
@@ -1246,6 +1252,7 @@ extern "C" int halo_hpoly_combine(halo_field_t field, const halo_fe_t* xis, size
     if (!st) return HALO_EDEVICE;
     std::lock_guard<std::mutex> g(st->mu);
     hipStream_t s = 0;
+    ScratchUse su(st, s);
     const size_t n = (size_t)1 << (n_xis - 1);
     HALO_CHECK(st->scratch[7].reserve(n * 32));
     HALO_CHECK(hpoly_device(st, field, xis, k, n_xis, alphas, st->scratch[7].ptr, s));
@@ -1281,6 +1288,7 @@ extern "C" int halo_pcdl_decider_commit(halo_curve_t curve, const halo_fe_t* xis
     if (d + 1 < n)
         return set_error(HALO_ELENGTH, "ms must be larger than Gs: (Gs: %zu), (ms: %zu)", d + 1, n);
     hipStream_t s = 0;
+    ScratchUse su(st, s);
     HALO_CHECK(st->scratch[7].reserve(n * 32 + 64));
     const int field = (curve == HALO_PALLAS) ? HALO_FP : HALO_FQ;
     HALO_CHECK(hpoly_device(st, field, xis, 1, n_xis, nullptr, st->scratch[7].ptr, s));
@@ -1338,6 +1346,7 @@ extern "C" int halo_trace_commit_batch(halo_curve_t curve, const halo_fe_t* eval
     if (d > D) return set_error(HALO_ESRSRANGE, "d (%zu) <= D (%zu) (pp_len = %zu)", d, D, D + 1);
     const int field = (curve == HALO_PALLAS) ? HALO_FP : HALO_FQ;
     hipStream_t s = 0;
+    ScratchUse su(st, s);
     const size_t bytes = k * n * 32;
     HALO_CHECK(st->scratch[0].reserve(bytes));
     HALO_CHECK(st->scratch[1].reserve(bytes));

@@ -199,13 +199,18 @@ __global__ void k_digits_glv(const uint4* scalars, size_t n, int c, int W, uint3
 // first segment's sum goes to first[t], its last segment's (when there are >= 2) to last[t], and the
 // buckets strictly inside the chunk are complete, so they go straight to bucket_sums.  k_merge then
 // completes the buckets that straddle chunk boundaries.
-template <class Cv>
 #ifndef HALO_ACC_MINB
 #define HALO_ACC_MINB 4  // workgroups per CU the register budget is sized for (A/B builds override)
 #endif
+// CHECK_ID: bases may contain the identity (0, 0) (caller-supplied bases); the resident SRS is
+// checked once when its window-shifted copies are built.  npw_lg: log2 n_per_window when it is a
+// power of two (the window of a shifted entry is a shift, not a division), else 0xff.
+// (Measured and rejected: an LDS-DMA double buffer gathering entry e + 1's point while entry e's
+// addition runs -- no change, 1.07 ms: the kernel is bound by its multiply-add issue, not the gathers.)
+template <class Cv, bool CHECK_ID>
 __global__ __launch_bounds__(256, HALO_ACC_MINB) void k_acc(const uint32_t* keys, const uint32_t* vals, const uint32_t* count,
-                                             uint32_t K, const uint4* bases, uint32_t n_per_window, size_t stride,
-                                             uint32_t blk_lg, uint32_t glv_n, uint4* first, uint4* last,
+                                             uint32_t K, const uint4* bases, uint32_t n_per_window, uint32_t npw_lg,
+                                             size_t stride, uint32_t blk_lg, uint32_t glv_n, uint4* first, uint4* last,
                                              uint4* bucket_sums) {
     using F = typename Cv::Base;
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -220,10 +225,10 @@ __global__ __launch_bounds__(256, HALO_ACC_MINB) void k_acc(const uint32_t* keys
         const uint32_t k = keys[e];
         if (k != cur) {  // bucket boundary inside the chunk
             if (!first_done) {
-                xyzz_store(first + 8 * t, acc);
+                xyzz_store(first + 8 * t, xyzz_settle(acc));
                 first_done = true;
             } else {
-                xyzz_store(bucket_sums + 8 * (size_t)cur, acc);
+                xyzz_store(bucket_sums + 8 * (size_t)cur, xyzz_settle(acc));
             }
             acc = xyzz_id<F>();
             cur = k;
@@ -231,7 +236,7 @@ __global__ __launch_bounds__(256, HALO_ACC_MINB) void k_acc(const uint32_t* keys
         const uint32_t v = vals[e];
         size_t idx = v & 0x7fffffffu;
         if (stride) {  // window-shifted SRS: entry w * n_per_window + i -> point w * stride + i
-            const uint32_t w = (uint32_t)idx / n_per_window;
+            const uint32_t w = npw_lg < 32 ? (uint32_t)idx >> npw_lg : (uint32_t)idx / n_per_window;
             uint32_t i = (uint32_t)idx - w * n_per_window;
             if (blk_lg < 32) i += (i >> blk_lg) << blk_lg;  // blocks of 2^blk_lg at stride 2^(blk_lg+1)
             idx = (size_t)w * stride + i;
@@ -240,10 +245,9 @@ __global__ __launch_bounds__(256, HALO_ACC_MINB) void k_acc(const uint32_t* keys
         if (phi) idx -= glv_n;
         Affine<F> p = aff_load<F>(bases + 4 * idx);
         if (phi) p.x = fe_mul(p.x, fe_from_const<F>(Cv::K::BETA));
-        if (v & 0x80000000u) p.y = fe_neg(p.y);
-        acc = xyzz_madd(acc, p);
+        acc = xyzz_madd_acc<F, CHECK_ID>(acc, p, (v & 0x80000000u) ? ~0u : 0u);
     }
-    xyzz_store((first_done ? last : first) + 8 * t, acc);
+    xyzz_store((first_done ? last : first) + 8 * t, xyzz_settle(acc));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -339,6 +343,14 @@ __global__ __launch_bounds__(64) void k_shift_windows(const uint4* gs, size_t n,
         for (int k = 0; k < c; k++) p = xyzz_dbl(p);
         aff_store(out + 4 * ((size_t)w * n + i), xyzz_to_aff(p));
     }
+}
+
+// identity (0, 0) entries of an internal affine point array (k_acc may skip its identity test when 0)
+template <class Cv>
+__global__ void k_count_identity(const uint4* pts, size_t n, uint32_t* count) {
+    using F = typename Cv::Base;
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && aff_is_id(aff_load<F>(pts + 4 * i))) atomicAdd(count, 1u);
 }
 
 template <class Cv>
@@ -459,13 +471,15 @@ template <class Cv>
 static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, size_t shift_stride,
                         const uint4* scalars_ark, size_t n, int c_req, const uint4* hide_table, const uint4* hide_scalar,
                         uint4* d_out_wrapped, hipStream_t s, bool async, uint32_t blk_lg = 32,
-                        bool hide_glv = false, bool out_xyzz = false, hipEvent_t hide_ready = nullptr) {
+                        bool hide_glv = false, bool out_xyzz = false, hipEvent_t hide_ready = nullptr,
+                        int preset = -1) {
     MsmPipe& PP = g_msm_pipe[st->device & 63];
     HALO_CHECK(pipe_init(PP));
-    const int set = msm_pick_set(PP, s, true);
+    // preset: the set the caller already claimed (and waited for) to stage converted bases in
+    const int set = preset >= 0 ? preset : msm_pick_set(PP, s, true);
     MsmScratch& M = PP.set[set];
     // the previous user of this scratch set must have finished its tail
-    if (M.tail_pending) HALO_HIP(hipStreamWaitEvent(s, M.tail_done, 0));
+    if (M.tail_pending && preset < 0) HALO_HIP(hipStreamWaitEvent(s, M.tail_done, 0));
     const hipStream_t ts = PP.tail[set];
     const size_t nn = std::max<size_t>(n, 1);
     // non-shifted bases: GLV (2n half-size scalars, ~128-bit windows) -- see k_digits_glv
@@ -531,8 +545,11 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
         HALO_CHECK(msm_radix_sort(M.digits.as<const uint32_t>(), E, SN, B, key_bits, M.sort, &skeys, &svals, &scount,
                                   nullptr, NB, s));
         ProfScope prof("msm_acc", s);
-        HALO_LAUNCH(prof, k_acc<Cv>, dim3(grid_for(nchunks, 256)), dim3(256), 0, s, (const uint32_t*)skeys,
-                    (const uint32_t*)svals, scount, K, bases_int, (uint32_t)nn,
+        // the shifted copies exist only for the resident SRS, whose identity check ran when they were built
+        const bool no_id = shifted && st->srs[curve_id<Cv>()].shifted_no_id;
+        auto kacc = no_id ? k_acc<Cv, false> : k_acc<Cv, true>;
+        HALO_LAUNCH(prof, kacc, dim3(grid_for(nchunks, 256)), dim3(256), 0, s, (const uint32_t*)skeys,
+                    (const uint32_t*)svals, scount, K, bases_int, (uint32_t)nn, is_pow2(nn) ? ilog2(nn) : 0xffu,
                     (shifted && (shift_stride != nn || blk_lg < 32)) ? shift_stride : (size_t)0, blk_lg,
                     glv ? (uint32_t)nn : 0u, P_first,
                     P_last, M.bucket_sums.as<uint4>());
@@ -586,10 +603,17 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
     return HALO_OK;
 }
 
-// Conversion buffer of the scratch set the next MSM will use (for caller-supplied ark bases).
-DevBuf& msm_next_conv_buffer(DeviceState* st, hipStream_t s) {
+// Claims the scratch set of the next MSM on stream s and orders s after that set's previous tail
+// (the caller stages converted bases in its conv buffer before the MSM is enqueued; the MSM then
+// runs on the same set, msm_device's preset).
+int msm_claim_set(DeviceState* st, hipStream_t s, int* set, DevBuf** conv) {
     MsmPipe& PP = g_msm_pipe[st->device & 63];
-    return PP.set[msm_pick_set(PP, s, false)].conv;
+    HALO_CHECK(pipe_init(PP));
+    *set = msm_pick_set(PP, s, true);
+    MsmScratch& M = PP.set[*set];
+    if (M.tail_pending) HALO_HIP(hipStreamWaitEvent(s, M.tail_done, 0));
+    *conv = &M.conv;
+    return HALO_OK;
 }
 
 // Makes `s` wait (device-side) for the tails of the MSMs enqueued on `s` that are still in flight.
@@ -602,12 +626,12 @@ int msm_join(DeviceState* st, hipStream_t s) {
 
 int msm_device(DeviceState* st, int curve, const void* bases_int, const void* scalars_ark, size_t n,
                const void* hide_table, const void* hide_scalar, void* d_out_wrapped, hipStream_t s, bool async,
-               bool hide_glv, bool out_xyzz, hipEvent_t hide_ready) {
+               bool hide_glv, bool out_xyzz, hipEvent_t hide_ready, int preset) {
     int rc;
     DISPATCH_CURVE(curve, Cv, {
         rc = msm_device_t<Cv>(st, (const uint4*)bases_int, false, 0, (const uint4*)scalars_ark, n, 0,
                               (const uint4*)hide_table, (const uint4*)hide_scalar, (uint4*)d_out_wrapped, s, async,
-                              32, hide_glv, out_xyzz, hide_ready);
+                              32, hide_glv, out_xyzz, hide_ready, preset);
     });
     return rc;
 }
@@ -778,8 +802,8 @@ static int msm_shared_batch_t(DeviceState* st, const uint4* bases, const uint4* 
     hipLaunchKernelGGL(k_batch_expand, dim3(grid_for(E, 256)), dim3(256), 0, s, (const uint32_t*)ent,
                        (const uint32_t*)ekey, (const uint32_t*)tot, (uint32_t)len, (uint32_t)(W * B),
                        S.keys.as<uint32_t>(), S.vals.as<uint32_t>());
-    hipLaunchKernelGGL(k_acc<Cv>, dim3(grid_for(nchunks, 256)), dim3(256), 0, s, S.keys.as<const uint32_t>(),
-                       S.vals.as<const uint32_t>(), (const uint32_t*)(tot + 1), K, bases, 1u, (size_t)0, 32u, 0u,
+    hipLaunchKernelGGL((k_acc<Cv, true>), dim3(grid_for(nchunks, 256)), dim3(256), 0, s, S.keys.as<const uint32_t>(),
+                       S.vals.as<const uint32_t>(), (const uint32_t*)(tot + 1), K, bases, 1u, 0u, (size_t)0, 32u, 0u,
                        P_first, P_last, S.bucket_sums.as<uint4>());
     HALO_HIP(hipGetLastError());
     MsmTailArgs ta;
@@ -988,13 +1012,21 @@ int srs_precompute_windows(DeviceState* st, int curve, hipStream_t s) {
     const int c = msm_shifted_window_bits(srs.n);
     const int W = msm_windows(c);
     HALO_CHECK(srs.shifted.reserve((size_t)W * srs.n * 64));
+    HALO_CHECK(st->scratch[7].reserve(16));
+    uint32_t* d_ids = st->scratch[7].as<uint32_t>();
+    HALO_HIP(hipMemsetAsync(d_ids, 0, 4, s));
     DISPATCH_CURVE(curve, Cv, {
+        hipLaunchKernelGGL(k_count_identity<Cv>, dim3(grid_for(srs.n, 256)), dim3(256), 0, s, srs.gs.as<const uint4>(),
+                           srs.n, d_ids);
         hipLaunchKernelGGL(k_shift_windows<Cv>, dim3(grid_for(srs.n, 64)), dim3(64), 0, s, srs.gs.as<const uint4>(),
                            srs.n, c, W, srs.shifted.as<uint4>());
     });
     HALO_HIP(hipGetLastError());
+    uint32_t ids = 0;
+    HALO_CHECK(copy_d2h(&ids, d_ids, 4, s));
     HALO_HIP(hipStreamSynchronize(s));
     srs.shifted_c = c;
+    srs.shifted_no_id = (ids == 0);
     return HALO_OK;
 }
 
@@ -1046,6 +1078,7 @@ extern "C" int halo_point_sum(halo_curve_t curve, const halo_wrapped_point_t* pt
     if (!st) return HALO_EDEVICE;
     std::lock_guard<std::mutex> g(st->mu);
     hipStream_t s = 0;
+    ScratchUse su(st, s);
     HALO_CHECK(st->scratch[0].reserve(std::max<size_t>(k, 1) * 64 + 64));
     char* buf = (char*)st->scratch[0].ptr;
     HALO_CHECK(copy_h2d(buf + 64, pts, k * 64, s));
@@ -1081,6 +1114,7 @@ extern "C" int halo_srs_read(halo_curve_t curve, size_t offset, size_t n, halo_w
     if (offset + n > srs.n) return set_error(HALO_ESRSRANGE, "range [%zu, %zu) exceeds the SRS length %zu", offset, offset + n, srs.n);
     if (!n) return HALO_OK;
     hipStream_t s = 0;
+    ScratchUse su(st, s);
     HALO_CHECK(st->scratch[0].reserve(n * 64));
     HALO_CHECK(convert_internal_to_wrapped(curve, srs.gs.as<const char>() + offset * 64, st->scratch[0].ptr, n, s));
     return copy_d2h(out, st->scratch[0].ptr, n * 64, s);
@@ -1102,6 +1136,7 @@ extern "C" int halo_msm(halo_curve_t curve, const halo_wrapped_point_t* bases, s
     if (!st) return HALO_EDEVICE;
     std::lock_guard<std::mutex> g(st->mu);
     hipStream_t s = 0;
+    ScratchUse su(st, s);
     HALO_CHECK(st->scratch[0].reserve(std::max<size_t>(n, 1) * 64));
     HALO_CHECK(st->scratch[1].reserve(std::max<size_t>(n, 1) * 64));
     HALO_CHECK(st->scratch[2].reserve(std::max<size_t>(n, 1) * 32));
@@ -1147,6 +1182,7 @@ extern "C" int halo_srs_upload(halo_curve_t curve, const halo_wrapped_point_t* g
     if (!st) return HALO_EDEVICE;
     std::lock_guard<std::mutex> g(st->mu);
     hipStream_t s = 0;
+    ScratchUse su(st, s);
     HALO_CHECK(st->scratch[0].reserve(std::max<size_t>(n, 2) * 64));
     HALO_CHECK(copy_h2d(st->scratch[0].ptr, gs, n * 64, s));
     return srs_install(st, curve, st->scratch[0].ptr, n, S, H, s);
@@ -1233,6 +1269,7 @@ extern "C" int halo_srs_load_bincode(halo_curve_t curve, const uint8_t* const* b
     if (!st) return HALO_EDEVICE;
     std::lock_guard<std::mutex> g(st->mu);
     hipStream_t s = 0;
+    ScratchUse su(st, s);
     HALO_CHECK(st->scratch[0].reserve(std::max<size_t>(n, 2) * 64));
     HALO_CHECK(st->scratch[2].reserve(16));
     uint4* d_pts = st->scratch[0].as<uint4>();
@@ -1295,6 +1332,7 @@ extern "C" int halo_srs_synthesize(halo_curve_t curve, size_t n, uint64_t seed) 
     if (!st) return HALO_EDEVICE;
     std::lock_guard<std::mutex> g(st->mu);
     hipStream_t s = 0;
+    ScratchUse su(st, s);
     SrsState& srs = st->srs[curve];
     HALO_CHECK(srs.gs.reserve(std::max<size_t>(n, 1) * 64));
     if (n) {
@@ -1315,6 +1353,7 @@ extern "C" int halo_srs_precompute_windows(halo_curve_t curve) {
     DeviceState* st = current_state();
     if (!st) return HALO_EDEVICE;
     std::lock_guard<std::mutex> g(st->mu);
+    ScratchUse su(st, 0);
     return srs_precompute_windows(st, curve, 0);
 }
 
@@ -1326,6 +1365,7 @@ extern "C" int halo_msm_srs(halo_curve_t curve, const halo_fe_t* scalars, size_t
     if (!st) return HALO_EDEVICE;
     std::lock_guard<std::mutex> g(st->mu);
     hipStream_t s = 0;
+    ScratchUse su(st, s);
     HALO_CHECK(st->scratch[2].reserve(std::max<size_t>(n, 1) * 32));
     HALO_CHECK(st->scratch[3].reserve(64));
     HALO_CHECK(copy_h2d(st->scratch[2].ptr, scalars, n * 32, s));
@@ -1342,6 +1382,7 @@ extern "C" int halo_msm_dev(halo_curve_t curve, const void* d_bases, const void*
     if (!st) return HALO_EDEVICE;
     std::lock_guard<std::mutex> g(st->mu);
     hipStream_t s = (hipStream_t)stream;
+    ScratchUse su(st, s);
     HALO_CHECK(st->scratch[7].reserve(64));
     if (!d_bases) {
         HALO_CHECK(msm_srs_device(st, curve, d_scalars, n, nullptr, st->scratch[7].ptr, s));
@@ -1363,10 +1404,15 @@ extern "C" int halo_msm_dev_async(halo_curve_t curve, const void* d_bases, const
     std::lock_guard<std::mutex> g(st->mu);
     hipStream_t s = (hipStream_t)stream;
     if (!d_bases) return msm_srs_device(st, curve, d_scalars, n, nullptr, d_out, s, true);
-    DevBuf& conv = msm_next_conv_buffer(st, s);
-    HALO_CHECK(conv.reserve(std::max<size_t>(n, 1) * 64));
-    HALO_CHECK(convert_wrapped_to_internal(curve, d_bases, conv.ptr, n, s));
-    return msm_device(st, curve, conv.ptr, d_scalars, n, nullptr, nullptr, d_out, s, true);
+    // the set is claimed once: its previous tail is waited for before the conversion overwrites conv,
+    // and the MSM runs on that same set
+    int set = -1;
+    DevBuf* conv = nullptr;
+    HALO_CHECK(msm_claim_set(st, s, &set, &conv));
+    HALO_CHECK(conv->reserve(std::max<size_t>(n, 1) * 64));
+    HALO_CHECK(convert_wrapped_to_internal(curve, d_bases, conv->ptr, n, s));
+    return msm_device(st, curve, conv->ptr, d_scalars, n, nullptr, nullptr, d_out, s, true, false, false, nullptr,
+                      set);
 }
 
 extern "C" int halo_msm_join(void* stream) {
@@ -1391,6 +1437,7 @@ extern "C" int halo_pedersen_commit(halo_curve_t curve, const halo_fe_t* w, cons
     SrsState& srs = st->srs[curve];
     if (w && !srs.has_sh) return set_error(HALO_ESRSRANGE, "hiding commitment needs S: upload the SRS (S, H) first");
     hipStream_t s = 0;
+    ScratchUse su(st, s);
     const size_t n = n_ms;
     HALO_CHECK(st->scratch[0].reserve(std::max<size_t>(n, 1) * 64));
     HALO_CHECK(st->scratch[1].reserve(std::max<size_t>(n, 1) * 64));
@@ -1434,6 +1481,7 @@ extern "C" int halo_pcdl_commit(halo_curve_t curve, const halo_fe_t* coeffs, siz
     // coefficients past the degree are zero and contribute nothing to the MSM
     const size_t m = std::min(len, n);
     hipStream_t s = 0;
+    ScratchUse su(st, s);
     HALO_CHECK(st->scratch[2].reserve(std::max<size_t>(m, 1) * 32));
     HALO_CHECK(st->scratch[3].reserve(64 + 32));
     HALO_CHECK(copy_h2d(st->scratch[2].ptr, coeffs, m * 32, s));

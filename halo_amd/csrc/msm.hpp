@@ -13,7 +13,11 @@ int msm_window_bits(size_t n);
 // hide_ready: event after which the hiding table is complete (built on another stream).
 int msm_device(DeviceState* st, int curve, const void* bases_int, const void* scalars_ark, size_t n,
                const void* hide_table, const void* hide_scalar, void* d_out_wrapped, hipStream_t s,
-               bool async = false, bool hide_glv = false, bool out_xyzz = false, hipEvent_t hide_ready = nullptr);
+               bool async = false, bool hide_glv = false, bool out_xyzz = false, hipEvent_t hide_ready = nullptr,
+               int preset = -1);
+// Claims the scratch set the next MSM on stream s will use (s waits for its previous tail) and
+// returns its base-conversion buffer; pass the set to msm_device as `preset`.
+int msm_claim_set(DeviceState* st, hipStream_t s, int* set, DevBuf** conv);
 // Makes stream s wait for the reduction tails of the async MSMs enqueued on s.
 int msm_join(DeviceState* st, hipStream_t s);
 // MSM over the resident SRS prefix (window-shifted copies when precomputed); optional hiding

@@ -563,6 +563,7 @@ static int ntt_host(halo_field_t field, const halo_fe_t* in, size_t len, unsigne
     if (!st) return HALO_EDEVICE;
     std::lock_guard<std::mutex> g(st->mu);
     hipStream_t s = 0;
+    ScratchUse su(st, s);
     HALO_CHECK(st->scratch[0].reserve(std::max(len, N) * 32));
     HALO_CHECK(st->scratch[1].reserve(N * 32));
     HALO_CHECK(st->scratch[2].reserve(N * 32));
@@ -625,6 +626,7 @@ extern "C" int halo_ntt_dev(halo_field_t field, void* d_data, unsigned log_n, si
     std::lock_guard<std::mutex> g(st->mu);
     const size_t N = (size_t)1 << log_n;
     hipStream_t s = (hipStream_t)stream;
+    ScratchUse su(st, s);
     // in place: the passes ping-pong through scratch (a second scratch buffer takes the first pass
     // when the pass count is odd, so no pass reads and writes one buffer)
     HALO_CHECK(st->scratch[4].reserve(batch * N * 32));
@@ -649,6 +651,7 @@ extern "C" int halo_ntt_dev_zero_tail(halo_field_t field, void* d_data, unsigned
     if (!st) return HALO_EDEVICE;
     std::lock_guard<std::mutex> g(st->mu);
     hipStream_t s = (hipStream_t)stream;
+    ScratchUse su(st, s);
     HALO_CHECK(st->scratch[4].reserve(batch * N * 32));
     HALO_CHECK(st->scratch[5].reserve(batch * N * 32));
     // the tail's contents are ignored: zero exactly what pass 0 will read beyond nonzero_len (up to

@@ -37,6 +37,19 @@ int DevBuf::reserve(size_t n) {
     return HALO_OK;
 }
 
+ScratchUse::ScratchUse(DeviceState* st_, hipStream_t s_) : st(st_), s(s_) {
+    if (st && st->scratch_used && st->scratch_last != s) (void)hipStreamWaitEvent(s, st->scratch_ev, 0);
+}
+
+ScratchUse::~ScratchUse() {
+    if (!st) return;
+    if (!st->scratch_ev && hipEventCreateWithFlags(&st->scratch_ev, hipEventDisableTiming) != hipSuccess) return;
+    if (hipEventRecord(st->scratch_ev, s) == hipSuccess) {
+        st->scratch_last = s;
+        st->scratch_used = true;
+    }
+}
+
 DevBuf::~DevBuf() {
     // Device state lives for the process; freeing at exit can race the HIP runtime teardown.
 }

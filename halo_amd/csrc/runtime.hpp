@@ -55,6 +55,7 @@ struct SrsState {
     DevBuf s_table;     // 2^i S (i < 256), internal affine: hiding term of pedersen::commit
     DevBuf shifted;     // optional window-shifted copies
     int shifted_c = 0;  // window bits of `shifted`
+    bool shifted_no_id = false;  // no identity among the bases of `shifted` (k_acc skips its test)
     int shifted_windows = 0;
 };
 
@@ -83,6 +84,23 @@ struct DeviceState {
         DevBuf t;
     };
     std::vector<std::unique_ptr<RTable>> rt;
+    // ScratchUse state: completion event of the last scratch user and its stream
+    hipEvent_t scratch_ev = nullptr;
+    hipStream_t scratch_last = nullptr;
+    bool scratch_used = false;
+};
+
+// Shared-scratch fence: the device-global scratch buffers (scratch[], scan_tmp, gate_tmp, eval_meta)
+// are used by calls on different streams (the caller's torch stream, IPA session streams, the null
+// stream of the host-array calls).  Every call that touches them holds a ScratchUse for its stream:
+// the stream first waits for the last other-stream user's completion event, and the call records a
+// new one when it ends, so the uses are ordered on the device whatever the streams.  (The API mutex
+// only orders the enqueueing.)
+struct ScratchUse {
+    DeviceState* st;
+    hipStream_t s;
+    ScratchUse(DeviceState* st, hipStream_t s);
+    ~ScratchUse();
 };
 
 // Current device's state (calls halo_init(current device) lazily).  Returns nullptr on failure

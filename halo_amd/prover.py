@@ -336,8 +336,8 @@ def instances_open(B, polys_points, d: int):
     Cs = B.commit_many([p for p, _ in polys_points])
     vs = [B.eval_many([p], z)[0] for p, z in polys_points]
     opens = ipa_open_many(B, [(p, z, v) for (p, z), v in zip(polys_points, vs)], d)
-    return [{"C": C, "v": v, "Ls": o[0], "Rs": o[1], "U": o[2], "c": o[3], "xis": o[4]}
-            for C, v, o in zip(Cs, vs, opens)]
+    return [{"C": C, "z": z, "v": v, "Ls": o[0], "Rs": o[1], "U": o[2], "c": o[3], "xis": o[4]}
+            for C, (_, z), v, o in zip(Cs, polys_points, vs, opens)]
 
 
 def synthetic_accumulator(B, n: int, chal: Challenges):
@@ -357,8 +357,8 @@ def acc_prover(B, qs, d: int, chal: Challenges):
     z = chal()
     h = B.hpoly([q["xis"] for q in qs], alphas)
     v = B.eval_many([h], z)[0]
-    Ls, Rs, U, c, _ = ipa_open_many(B, [(h, z, v)], d)[0]
-    return {"C": C, "z": z, "v": v, "Ls": Ls, "Rs": Rs, "U": U, "c": c}
+    Ls, Rs, U, c, xis = ipa_open_many(B, [(h, z, v)], d)[0]
+    return {"C": C, "z": z, "v": v, "Ls": Ls, "Rs": Rs, "U": U, "c": c, "xis": xis}
 
 
 # ---------------------------------------------------------------------------------------------

@@ -154,3 +154,30 @@ def generator_mul(curve: str, k_canonical: np.ndarray) -> np.ndarray:
 
 def msm_window_size(n: int) -> int:
     return lib().orc_msm_window_size(n)
+
+
+def synth_scalars(seed: int, n: int) -> np.ndarray:
+    """numpy restatement of halo_synth_scalar (msm.hip synth_scalar: a splitmix64 stream per index,
+    top word masked below 2^253, zero replaced by 1): the known discrete logs k_j of the synthetic
+    SRS G_j = k_j G, canonical (not Montgomery)."""
+    j = np.arange(n, dtype=np.uint64)
+    st = np.uint64(seed) ^ (j * np.uint64(0xD1B54A32D192ED03))
+    out = np.zeros((n, 4), dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        for i in range(4):
+            st = st + np.uint64(0x9E3779B97F4A7C15)
+            z = st.copy()
+            z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+            z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+            out[:, i] = z ^ (z >> np.uint64(31))
+    out[:, 3] &= np.uint64(0x1FFFFFFFFFFFFFFF)
+    zero = (out == 0).all(axis=1)
+    out[zero, 0] = 1
+    return out
+
+
+def known_log_msm(curve: str, scalars_mont: np.ndarray, logs_canonical: np.ndarray) -> np.ndarray:
+    """MSM(G_j = k_j G, s) = (sum_j s_j k_j) G for bases with known discrete logs: one Montgomery dot
+    product (S_j k_j R^-1 = s_j k_j) and one scalar multiplication of the generator."""
+    acc = scalar_dot("fp" if curve == "pallas" else "fq", scalars_mont, logs_canonical)
+    return generator_mul(curve, acc)

@@ -314,3 +314,36 @@ def test_srs_load_bincode(hal, golden, corc, cname, cid):
         group.PublicParams.load_bincode(cname, [head], sh, n=48, precompute_windows=False)
     with pytest.raises(Exception, match="n <= N"):
         group.PublicParams.load_bincode(cname, [block(pts[:16])], sh, n=32, precompute_windows=False)
+
+
+def test_async_msm_caller_bases_concurrent_streams(hal, corc):
+    """halo_msm_dev_async over caller-supplied (ark) bases from three torch streams at once, several
+    MSMs per stream back to back: every result equals the synchronous halo_msm of the same inputs
+    (the conversion buffer of a scratch set is claimed together with the set, after its last tail)."""
+    import ctypes
+
+    import torch
+    L = hal.load()
+    g = corc.srs_generate("pallas", (1 << 14) + 128)
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    jobs = []
+    for k in range(9):
+        n = [1 << 14, 5000, 1 << 12][k % 3]
+        bases = torch.from_numpy(np.ascontiguousarray(g[(k * 37) % 100:][:n]).view(np.int64)).cuda()
+        sc = rand_sc(n, 500 + k)
+        jobs.append((bases, torch.from_numpy(sc.view(np.int64)).cuda(), n, sc))
+    outs = torch.zeros((len(jobs), 8), dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    for k, (bases, sc_d, n, _) in enumerate(jobs):
+        st = streams[k % 3]
+        hal.check(L.halo_msm_dev_async(0, ctypes.c_void_p(bases.data_ptr()), ctypes.c_void_p(sc_d.data_ptr()), n,
+                                       ctypes.c_void_p(outs[k].data_ptr()), ctypes.c_void_p(st.cuda_stream)))
+    for st in streams:
+        hal.check(L.halo_msm_join(ctypes.c_void_p(st.cuda_stream)))
+    torch.cuda.synchronize()
+    got = outs.cpu().numpy().view(np.uint64)
+    for k, (bases, _, n, sc) in enumerate(jobs):
+        exp = np.zeros(8, dtype=np.uint64)
+        b = bases.cpu().numpy().view(np.uint64)
+        hal.check(L.halo_msm(0, hal.ptr(np.ascontiguousarray(b)), n, hal.ptr(sc), n, hal.ptr(exp)))
+        assert np.array_equal(got[k], exp), k

@@ -287,3 +287,27 @@ def test_ntt_zero_tail_matches_full(hal, logn, nz):
     hal.check(L.halo_ntt_dev_zero_tail(0, ctypes.c_void_p(y.data_ptr()), logn, 1, nz, s))
     torch.cuda.synchronize()
     assert torch.equal(x, y)
+
+
+def test_ntt_dev_concurrent_streams(hal, corc):
+    """halo_ntt_dev on two torch streams at once plus host-array NTTs (null stream) in between: the
+    device-global NTT scratch is fenced per stream (ScratchUse), so every transform is bit-exact."""
+    import torch
+    L = hal.load()
+    logn = 18
+    n = 1 << logn
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    xs = [rand_fe(n, 900 + i) for i in range(6)]
+    exps = [corc.ntt("fp", x) for x in xs]
+    ds = [torch.from_numpy(x.view(np.int64)).cuda() for x in xs]
+    torch.cuda.synchronize()
+    for i, d in enumerate(ds):
+        st = s1 if i % 2 == 0 else s2
+        hal.check(L.halo_ntt_dev(0, ctypes.c_void_p(d.data_ptr()), logn, 1, 0, ctypes.c_void_p(st.cuda_stream)))
+        if i == 2:  # a host-array transform on the null stream while the others are in flight
+            h = xs[0].copy()
+            hal.check(L.halo_ntt(0, hal.ptr(h), logn, 0))
+            assert np.array_equal(h, exps[0])
+    torch.cuda.synchronize()
+    for i, d in enumerate(ds):
+        assert np.array_equal(d.cpu().numpy().view(np.uint64), exps[i]), i

@@ -196,3 +196,53 @@ def test_prover_pipeline_runs_on_cpu_restatement():
     assert len(out["q_r"]["Ls"]) == 3 and len(out["acc"]["Rs"]) == 3
     # the opened polynomial's evaluation is the one the instance reports
     assert out["q_r"]["v"] == out["q_r"]["v"] % B.m
+
+
+def test_succinct_check_and_decider_on_cpu_restatement(corc):
+    """oracle/pcdl_check.py (pcdl.rs:483-583) accepts the three openings the naive_prover pipeline
+    produces on the CPU restatement backend (q_r, q_r_omega, acc::prover's open of h), the decider
+    identity U == commit(h) holds for each, and a tampered L, c or v is rejected."""
+    import pcdl_check
+    import prover_ref
+
+    from halo_amd import prover
+
+    c = P.PALLAS
+    n = 16
+    srs = np.array([P.point_to_wrapped(c, P.mul_fast(c, 5000 + 7 * i, c.generator)) for i in range(n)], dtype=np.uint64)
+    H = srs[1]
+    B = prover_ref.RefBackend("pallas", srs, H)
+    out = prover.naive_prover(B, prover.synthetic_witness(B, n, seed=11), n, prover.Challenges(B.m))
+    for key in ("q_r", "q_r_omega", "acc"):
+        q = out[key]
+        pcdl_check.succinct_check("pallas", q["C"], n - 1, q["z"], q["v"], q["Ls"], q["Rs"], q["U"], q["c"], q["xis"], H)
+        assert pcdl_check.decider_commit_matches("pallas", q["U"], q["xis"], srs, corc.msm), key
+    q = out["q_r"]
+    with pytest.raises(AssertionError, match="C_\\(log_n\\)"):
+        pcdl_check.succinct_check("pallas", q["C"], n - 1, q["z"], (q["v"] + 1) % B.m, q["Ls"], q["Rs"], q["U"],
+                                  q["c"], q["xis"], H)
+    with pytest.raises(AssertionError, match="C_\\(log_n\\)"):
+        pcdl_check.succinct_check("pallas", q["C"], n - 1, q["z"], q["v"], [q["Rs"][0]] + q["Ls"][1:], q["Rs"],
+                                  q["U"], q["c"], q["xis"], H)
+    with pytest.raises(AssertionError, match="C_\\(log_n\\)"):
+        pcdl_check.succinct_check("pallas", q["C"], n - 1, q["z"], q["v"], q["Ls"], q["Rs"], q["U"], q["c"] + 1,
+                                  q["xis"], H)
+    m = B.m
+    xis = q["xis"]
+    z = 0x1234
+    assert pcdl_check.h_eval(xis, z, m) == P.horner(pcdl_check.h_coeffs(xis, m), z, m)
+    assert pcdl_check.h_coeffs(xis, m) == P.h_coeffs(xis, m)
+
+
+@pytest.mark.parametrize("cname", CURVES)
+def test_known_log_msm_identity(corc, cname):
+    """corc.known_log_msm (the 2^22 / 2^24 MSM checker) equals the oracle MSM over bases G_j = k_j G
+    built from the same synthetic logs (corc.synth_scalars restates halo_synth_scalar)."""
+    c = P.CURVES[cname]
+    n = 300
+    k = corc.synth_scalars(77, n)
+    assert all(P.limbs_to_int(k[j]) < c.scalar for j in range(n))
+    bases = np.stack([corc.generator_mul(cname, k[j]) for j in range(n)])
+    rng = np.random.default_rng(1)
+    sc = rng.integers(0, 2**62, size=(n, 4), dtype=np.uint64)
+    assert np.array_equal(corc.known_log_msm(cname, sc, k), corc.msm(cname, bases, sc))
