@@ -63,6 +63,7 @@ SIGNATURES = {
     "halo_msm_window_bits": [_sz],
     "halo_srs_window_bits": [ctypes.c_int],
     "halo_msm_dev_async": [ctypes.c_int, _vp, _vp, _sz, _vp, _vp],
+    "halo_msm_batch_dev": [ctypes.c_int, _vp, _vp, _sz, _vp, _vp],
     "halo_msm_join": [_vp],
     "halo_srs_read": [ctypes.c_int, _sz, _sz, _vp],
     "halo_point_sum": [ctypes.c_int, _vp, _sz, _vp],

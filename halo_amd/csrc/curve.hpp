@@ -143,11 +143,11 @@ HALO_DEV XYZZ<F> xyzz_madd(const XYZZ<F>& p, const Affine<F>& q) {
 //     xyzz_settle before storing or handing the point to the general formulas);
 //   * Y3 = R (Q - X3) + PPP (2p - Y1) is one product sum with a single Montgomery reduction.
 // Bounds: P < 10p, R < 6p, T = Q - X3 + 8p < 10p; P^2 < 100p^2 and R T + PPP (2p - Y1) < 64p^2 stay
-// below p 2^261 (~127p^2), so every product is < 2p.  CHECK_ID = false when q is known not to be the
-// identity (the resident SRS, checked when its shifted copies are built).
-template <class F, bool CHECK_ID>
+// below p 2^261 (~127p^2), so every product is < 2p.  (Measured: an instantiation without the
+// identity test of q was 15-25 % SLOWER -- worse schedule -- so the test stays.)
+template <class F>
 HALO_DEV XYZZ<F> xyzz_madd_acc(const XYZZ<F>& p, const Affine<F>& q, uint32_t negmask) {
-    if (CHECK_ID && aff_is_id(q)) return p;
+    if (aff_is_id(q)) return p;
     if (xyzz_is_id(p)) {
         XYZZ<F> r = xyzz_from_aff(q);
         if (negmask) r.Y = fe_neg(q.y);
@@ -157,9 +157,24 @@ HALO_DEV XYZZ<F> xyzz_madd_acc(const XYZZ<F>& p, const Affine<F>& q, uint32_t ne
     const Fe<F> S2 = fe_mul(q.y, p.ZZZ);
     const Fe<F> P = fe_sub_k<8>(U2, p.X);              // < 10p
     const Fe<F> R = fe_sub_k_sgn<4>(S2, p.Y, negmask);  // < 6p
+    // no branch until the end: independent products stay in one basic block, where the scheduler
+    // interleaves their dependent multiply-add chains (PP | R^2, then ZZ3 | PPP | Q, then Y3 | ZZZ3)
     const Fe<F> PP = fe_sqr(P);
+    const Fe<F> R2 = fe_sqr(R);
     const Fe<F> ZZ3 = fe_mul(p.ZZ, PP);
-    if (fe_is_zero(ZZ3)) {  // U2 == X1: q = +-p
+    const Fe<F> PPP = fe_mul(P, PP);
+    const Fe<F> Q = fe_mul(p.X, PP);
+    XYZZ<F> r;
+    r.X = fe_sub_k<6>(R2, fe_add_nc(PPP, fe_add_nc(Q, Q)));  // < 8p
+    const Fe<F> T = fe_sub_k<8>(Q, r.X);                       // < 10p
+#ifndef HALO_Y3_TWO_MULS
+    r.Y = fe_mul2(R, T, PPP, fe_sub_k<2>(fe_zero<F>(), p.Y));
+#else
+    r.Y = fe_sub(fe_mul(R, T), fe_mul(p.Y, PPP));
+#endif
+    r.ZZ = ZZ3;
+    r.ZZZ = fe_mul(p.ZZZ, PPP);
+    if (fe_is_zero(ZZ3)) {  // U2 == X1: q = +-p (ZZ1 != 0), off the common path
         if (fe_is_zero(fe_reduce_8p(R))) {
             Affine<F> qs = q;
             if (negmask) qs.y = fe_neg(q.y);
@@ -167,14 +182,6 @@ HALO_DEV XYZZ<F> xyzz_madd_acc(const XYZZ<F>& p, const Affine<F>& q, uint32_t ne
         }
         return xyzz_id<F>();
     }
-    const Fe<F> PPP = fe_mul(P, PP);
-    const Fe<F> Q = fe_mul(p.X, PP);
-    XYZZ<F> r;
-    r.X = fe_sub_k<6>(fe_sqr(R), fe_add_nc(PPP, fe_add_nc(Q, Q)));  // < 8p
-    const Fe<F> T = fe_sub_k<8>(Q, r.X);                              // < 10p
-    r.Y = fe_mul2(R, T, PPP, fe_sub_k<2>(fe_zero<F>(), p.Y));
-    r.ZZ = ZZ3;
-    r.ZZZ = fe_mul(p.ZZZ, PPP);
     return r;
 }
 

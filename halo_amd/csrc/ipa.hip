@@ -1370,8 +1370,13 @@ extern "C" int halo_trace_commit_batch(halo_curve_t curve, const halo_fe_t* eval
         if (p_deg > d) return set_error(HALO_EDEGREE, "p_deg (%zu) <= d (%zu)", p_deg, d);
     }
     uint4* d_commits = st->scratch[7].as<uint4>();
-    for (size_t r = 0; r < k; r++)
-        HALO_CHECK(msm_srs_device(st, curve, B + 2 * r * n, lens[r], nullptr, d_commits + 4 * r, s, true));
+    std::vector<const void*> ptrs(k);
+    std::vector<size_t> szs(k);
+    for (size_t r = 0; r < k; r++) {
+        ptrs[r] = B + 2 * r * n;
+        szs[r] = lens[r];
+    }
+    HALO_CHECK(msm_batch_device(st, curve, ptrs.data(), szs.data(), k, d_commits, s));
     HALO_CHECK(msm_join(st, s));
     HALO_CHECK(copy_d2h(commits_out, d_commits, k * 64, s));
     if (coeffs_out) HALO_CHECK(copy_d2h(coeffs_out, B, bytes, s));

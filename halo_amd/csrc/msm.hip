@@ -92,8 +92,9 @@ __global__ __launch_bounds__(64) void k_synth_bases(uint4* out, size_t n, uint64
 // ---------------------------------------------------------------------------------------------
 // 1. digits
 // ---------------------------------------------------------------------------------------------
+// digits[w * ld + i] (ld >= n: the leading dimension, the batched MSMs' per-polynomial stride)
 template <class S>
-__global__ void k_digits(const uint4* scalars, size_t n, int c, int W, uint32_t* digits) {
+__global__ void k_digits(const uint4* scalars, size_t n, int c, int W, uint32_t* digits, size_t ld) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint32_t w8[8];
@@ -144,7 +145,7 @@ __global__ void k_digits(const uint4* scalars, size_t n, int c, int W, uint32_t*
             carry = 0;
             out = (v == 0) ? DIGIT_NONE : ((v - 1) | nflip);
         }
-        digits[(size_t)w * n + i] = out;
+        digits[(size_t)w * ld + i] = out;
     }
 }
 
@@ -202,19 +203,17 @@ __global__ void k_digits_glv(const uint4* scalars, size_t n, int c, int W, uint3
 #ifndef HALO_ACC_MINB
 #define HALO_ACC_MINB 4  // workgroups per CU the register budget is sized for (A/B builds override)
 #endif
-// CHECK_ID: bases may contain the identity (0, 0) (caller-supplied bases); the resident SRS is
-// checked once when its window-shifted copies are built.  npw_lg: log2 n_per_window when it is a
-// power of two (the window of a shifted entry is a shift, not a division), else 0xff.
+// npw_lg: log2 n_per_window when it is a power of two (the window of a shifted entry is a shift,
+// not a division), else 0xff.
 // (Measured and rejected: an LDS-DMA double buffer gathering entry e + 1's point while entry e's
 // addition runs -- no change, 1.07 ms: the kernel is bound by its multiply-add issue, not the gathers.)
-template <class Cv, bool CHECK_ID>
-__global__ __launch_bounds__(256, HALO_ACC_MINB) void k_acc(const uint32_t* keys, const uint32_t* vals, const uint32_t* count,
-                                             uint32_t K, const uint4* bases, uint32_t n_per_window, uint32_t npw_lg,
-                                             size_t stride, uint32_t blk_lg, uint32_t glv_n, uint4* first, uint4* last,
-                                             uint4* bucket_sums) {
+// One thread's chunk: the sorted entries [t K, t K + K) (see k_acc).
+template <class Cv>
+__device__ __forceinline__ void acc_chunk(size_t t, uint32_t cnt, const uint32_t* keys, const uint32_t* vals, uint32_t K,
+                                          const uint4* bases, uint32_t n_per_window, uint32_t npw_lg, size_t stride,
+                                          uint32_t blk_lg, uint32_t glv_n, uint4* first, uint4* last,
+                                          uint4* bucket_sums) {
     using F = typename Cv::Base;
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t cnt = *count;
     const size_t beg = t * K;
     if (beg >= cnt) return;
     const uint32_t end = (uint32_t)min((size_t)cnt, beg + K);
@@ -241,13 +240,39 @@ __global__ __launch_bounds__(256, HALO_ACC_MINB) void k_acc(const uint32_t* keys
             if (blk_lg < 32) i += (i >> blk_lg) << blk_lg;  // blocks of 2^blk_lg at stride 2^(blk_lg+1)
             idx = (size_t)w * stride + i;
         }
-        const bool phi = glv_n && idx >= glv_n;                               // GLV: phi(G_i)
+        const bool phi = glv_n && idx >= glv_n;  // GLV: phi(G_i)
         if (phi) idx -= glv_n;
         Affine<F> p = aff_load<F>(bases + 4 * idx);
         if (phi) p.x = fe_mul(p.x, fe_from_const<F>(Cv::K::BETA));
-        acc = xyzz_madd_acc<F, CHECK_ID>(acc, p, (v & 0x80000000u) ? ~0u : 0u);
+        acc = xyzz_madd_acc(acc, p, (v & 0x80000000u) ? ~0u : 0u);
     }
     xyzz_store((first_done ? last : first) + 8 * t, xyzz_settle(acc));
+}
+
+// PERSIST (beside a concurrent front, HALO_BATCH_OVERLAP=1): a grid of a few workgroups per CU
+// takes blocks of 256 chunks from the atomic counter work_ctr until none is left, so the
+// accumulation never holds more than that many wave slots per SIMD; otherwise one chunk per thread.
+template <class Cv, bool PERSIST>
+__global__ __launch_bounds__(256, HALO_ACC_MINB) void k_acc(const uint32_t* keys, const uint32_t* vals, const uint32_t* count,
+                                             uint32_t K, const uint4* bases, uint32_t n_per_window, uint32_t npw_lg,
+                                             size_t stride, uint32_t blk_lg, uint32_t glv_n, uint4* first, uint4* last,
+                                             uint4* bucket_sums, uint32_t* work_ctr, uint32_t nblocks) {
+    const uint32_t cnt = *count;
+    if constexpr (!PERSIST) {
+        acc_chunk<Cv>((size_t)blockIdx.x * blockDim.x + threadIdx.x, cnt, keys, vals, K, bases, n_per_window,
+                                npw_lg, stride, blk_lg, glv_n, first, last, bucket_sums);
+    } else {
+        __shared__ uint32_t sblk;
+        for (;;) {
+            if (threadIdx.x == 0) sblk = atomicAdd(work_ctr, 1u);
+            __syncthreads();
+            const uint32_t blk = sblk;
+            __syncthreads();
+            if (blk >= nblocks) break;  // uniform per workgroup: every wave leaves
+            acc_chunk<Cv>((size_t)blk * blockDim.x + threadIdx.x, cnt, keys, vals, K, bases, n_per_window,
+                                    npw_lg, stride, blk_lg, glv_n, first, last, bucket_sums);
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -345,14 +370,6 @@ __global__ __launch_bounds__(64) void k_shift_windows(const uint4* gs, size_t n,
     }
 }
 
-// identity (0, 0) entries of an internal affine point array (k_acc may skip its identity test when 0)
-template <class Cv>
-__global__ void k_count_identity(const uint4* pts, size_t n, uint32_t* count) {
-    using F = typename Cv::Base;
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n && aff_is_id(aff_load<F>(pts + 4 * i))) atomicAdd(count, 1u);
-}
-
 template <class Cv>
 __global__ __launch_bounds__(64) void k_pow2_points(const uint4* P_int, uint4* out_xyzz, int count) {
     using F = typename Cv::Base;
@@ -402,11 +419,11 @@ static unsigned grid_for(size_t n, unsigned thr) { return (unsigned)std::max<siz
 // two sets only made back-to-back commitment batches slower.)
 constexpr int MSM_SETS = 4;
 struct MsmScratch {
-    DevBuf digits, bstart, partials, bucket_sums, seg_acc, seg_sum, bits, window_sums, scan_tmp, conv;
+    DevBuf digits, bstart, partials, bucket_sums, seg_acc, seg_sum, bits, window_sums, scan_tmp, conv, ctr;
     const uint32_t* skeys = nullptr;   // sorted keys of the current MSM (sort scratch)
     const uint32_t* scount = nullptr;  // device count of valid entries
     SortScratch sort;
-    hipEvent_t acc_done = nullptr, tail_done = nullptr, start = nullptr;
+    hipEvent_t acc_done = nullptr, tail_done = nullptr, start = nullptr, front_done = nullptr;
     bool tail_pending = false;
     hipStream_t owner = nullptr;  // stream the set's last MSM was enqueued on (msm_join)
 };
@@ -419,6 +436,8 @@ struct MsmPipe {
     int slot_next[2] = {0, 0};
     uint64_t slot_used[2] = {0, 0}, clock = 0;
     hipStream_t tail[MSM_SETS] = {};  // one per scratch set: consecutive tails run concurrently
+    hipStream_t front = nullptr;      // digits + sort of batched MSMs (halo_msm_batch_dev)
+    hipEvent_t batch_in = nullptr;    // the batch's inputs are ready (recorded on the caller's stream)
 };
 static MsmPipe g_msm_pipe[64];  // per device
 
@@ -450,13 +469,27 @@ static int msm_pick_set(MsmPipe& P, hipStream_t s, bool advance) {
     return set;
 }
 
+// persistent accumulation workgroups per CU beside a concurrent front (HALO_ACC_WGS overrides)
+static unsigned msm_acc_wgs_per_cu() {
+    static const unsigned v = [] {
+        const char* e = getenv("HALO_ACC_WGS");
+        return e ? (unsigned)std::max(1, atoi(e)) : 3u;
+    }();
+    return v;
+}
+
 static int pipe_init(MsmPipe& P) {
     if (P.tail[0]) return HALO_OK;
+    int least = 0, greatest = 0;  // the front's kernels are dispatched ahead of the accumulation's
+    HALO_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    HALO_HIP(hipStreamCreateWithPriority(&P.front, hipStreamNonBlocking, greatest));
+    HALO_HIP(hipEventCreateWithFlags(&P.batch_in, hipEventDisableTiming));
     for (auto& t : P.tail) HALO_HIP(hipStreamCreateWithFlags(&t, hipStreamNonBlocking));
     for (auto& m : P.set) {
         HALO_HIP(hipEventCreateWithFlags(&m.acc_done, hipEventDisableTiming));
         HALO_HIP(hipEventCreateWithFlags(&m.tail_done, hipEventDisableTiming));
         HALO_HIP(hipEventCreateWithFlags(&m.start, hipEventDisableTiming));
+        HALO_HIP(hipEventCreateWithFlags(&m.front_done, hipEventDisableTiming));
     }
     return HALO_OK;
 }
@@ -472,14 +505,20 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
                         const uint4* scalars_ark, size_t n, int c_req, const uint4* hide_table, const uint4* hide_scalar,
                         uint4* d_out_wrapped, hipStream_t s, bool async, uint32_t blk_lg = 32,
                         bool hide_glv = false, bool out_xyzz = false, hipEvent_t hide_ready = nullptr,
-                        int preset = -1) {
+                        int preset = -1, hipStream_t fs = nullptr) {
     MsmPipe& PP = g_msm_pipe[st->device & 63];
     HALO_CHECK(pipe_init(PP));
     // preset: the set the caller already claimed (and waited for) to stage converted bases in
     const int set = preset >= 0 ? preset : msm_pick_set(PP, s, true);
     MsmScratch& M = PP.set[set];
+    // fs: the front (digits + sort) runs on its own stream, beside the previous MSM's accumulation
+    // on s (halo_msm_batch_dev); the caller has ordered fs after the inputs
+    const hipStream_t front = fs ? fs : s;
     // the previous user of this scratch set must have finished its tail
-    if (M.tail_pending && preset < 0) HALO_HIP(hipStreamWaitEvent(s, M.tail_done, 0));
+    if (M.tail_pending && preset < 0) {
+        HALO_HIP(hipStreamWaitEvent(front, M.tail_done, 0));
+        if (front != s) HALO_HIP(hipStreamWaitEvent(s, M.tail_done, 0));
+    }
     const hipStream_t ts = PP.tail[set];
     const size_t nn = std::max<size_t>(n, 1);
     // non-shifted bases: GLV (2n half-size scalars, ~128-bit windows) -- see k_digits_glv
@@ -534,25 +573,38 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
 
     if (n > 0) {
         if (glv)
-            hipLaunchKernelGGL(k_digits_glv<Cv>, dim3(grid_for(n, 256)), dim3(256), 0, s, scalars_ark, n, c, W,
+            hipLaunchKernelGGL(k_digits_glv<Cv>, dim3(grid_for(n, 256)), dim3(256), 0, front, scalars_ark, n, c, W,
                                M.digits.as<uint32_t>());
         else
-            hipLaunchKernelGGL(k_digits<typename Cv::Scalar>, dim3(grid_for(n, 256)), dim3(256), 0, s, scalars_ark, n,
-                               c, W, M.digits.as<uint32_t>());
+            hipLaunchKernelGGL(k_digits<typename Cv::Scalar>, dim3(grid_for(n, 256)), dim3(256), 0, front, scalars_ark,
+                               n, c, W, M.digits.as<uint32_t>(), n);
         HALO_HIP(hipGetLastError());
         uint32_t *skeys = nullptr, *svals = nullptr;
         const uint32_t* scount = nullptr;
         HALO_CHECK(msm_radix_sort(M.digits.as<const uint32_t>(), E, SN, B, key_bits, M.sort, &skeys, &svals, &scount,
-                                  nullptr, NB, s));
+                                  nullptr, NB, front, front != s));
+        if (front != s) {
+            HALO_HIP(hipEventRecord(M.front_done, front));
+            HALO_HIP(hipStreamWaitEvent(s, M.front_done, 0));
+        }
+        // beside a concurrent front, the accumulation runs persistent with msm_acc_wgs_per_cu()
+        // workgroups per CU, leaving wave slots (and all of the LDS) to the front's kernels
+        const uint32_t nblocks = (uint32_t)grid_for(nchunks, 256);
+        uint32_t* work_ctr = nullptr;
+        unsigned grid = nblocks;
+        if (front != s) {
+            HALO_CHECK(M.ctr.reserve(16));
+            work_ctr = M.ctr.as<uint32_t>();
+            HALO_HIP(hipMemsetAsync(work_ctr, 0, 4, s));
+            grid = std::min<unsigned>(nblocks, (unsigned)st->num_cu * msm_acc_wgs_per_cu());
+        }
         ProfScope prof("msm_acc", s);
-        // the shifted copies exist only for the resident SRS, whose identity check ran when they were built
-        const bool no_id = shifted && st->srs[curve_id<Cv>()].shifted_no_id;
-        auto kacc = no_id ? k_acc<Cv, false> : k_acc<Cv, true>;
-        HALO_LAUNCH(prof, kacc, dim3(grid_for(nchunks, 256)), dim3(256), 0, s, (const uint32_t*)skeys,
+        auto kacc = work_ctr ? k_acc<Cv, true> : k_acc<Cv, false>;
+        HALO_LAUNCH(prof, kacc, dim3(grid), dim3(256), 0, s, (const uint32_t*)skeys,
                     (const uint32_t*)svals, scount, K, bases_int, (uint32_t)nn, is_pow2(nn) ? ilog2(nn) : 0xffu,
                     (shifted && (shift_stride != nn || blk_lg < 32)) ? shift_stride : (size_t)0, blk_lg,
                     glv ? (uint32_t)nn : 0u, P_first,
-                    P_last, M.bucket_sums.as<uint4>());
+                    P_last, M.bucket_sums.as<uint4>(), work_ctr, nblocks);
         M.skeys = skeys;
         M.scount = scount;
         HALO_HIP(hipGetLastError());
@@ -603,6 +655,128 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
     return HALO_OK;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Batched commitments as ONE MSM (halo_msm_batch_dev for small polynomials): k scalar vectors over
+// the resident window-shifted SRS share one digit pass, one sort (key = (polynomial, bucket)), one
+// accumulation and one reduction tail with a window per polynomial; k_sums_out converts each
+// polynomial's bucket-weighted sum.  At n = 2^16 one MSM is latency-bound (a few thousand
+// workgroups, a ~1 ms reduction tail); sixteen of them in one pass fill the GPU once.
+// ---------------------------------------------------------------------------------------------
+template <class Cv>
+__global__ __launch_bounds__(64) void k_sums_out(const uint4* window_sums, uint32_t k, uint4* out_wrapped) {
+    using F = typename Cv::Base;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= k) return;
+    aff_to_wrapped(out_wrapped + 4 * (size_t)i, xyzz_to_aff(xyzz_load<F>(window_sums + 8 * (size_t)i)));
+}
+
+template <class Cv>
+static int msm_multi_device_t(DeviceState* st, const void* const* scalars, const size_t* lens, size_t k,
+                              uint4* d_out, hipStream_t s) {
+    SrsState& srs = st->srs[curve_id<Cv>()];
+    MsmPipe& PP = g_msm_pipe[st->device & 63];
+    HALO_CHECK(pipe_init(PP));
+    const int set = msm_pick_set(PP, s, true);
+    MsmScratch& M = PP.set[set];
+    if (M.tail_pending) HALO_HIP(hipStreamWaitEvent(s, M.tail_done, 0));
+    size_t nmax = 1;
+    bool ragged = false;
+    for (size_t p = 0; p < k; p++) nmax = std::max(nmax, lens[p]);
+    size_t ld = 1;
+    while (ld < nmax) ld <<= 1;
+    if (ld > srs.n) ld = nmax;
+    for (size_t p = 0; p < k; p++) ragged |= lens[p] != ld;
+    const int c = srs.shifted_c, W = msm_windows(c);
+    const uint32_t B = 1u << (c - 1);
+    const size_t SN = (size_t)W * ld, E = k * SN, NB = k * (size_t)B;
+    const int SW = (int)k;
+    if (E >= (1ull << 32)) return set_error(HALO_EINVAL, "halo_msm_batch_dev: batch too large");
+    const uint32_t L = std::min<uint32_t>(MSM_SEG_L, B), logL = ilog2(L), H = B / L, logH = ilog2(H);
+    const uint32_t NT = 1 + logH + logL;
+    const uint32_t key_bits = ilog2(NB - 1) + 1;
+    const size_t lanes = (size_t)st->num_cu * 16 * 64 * 4;
+    const uint32_t K = (uint32_t)std::max<size_t>(16, std::min<size_t>(64, (E + lanes - 1) / lanes));
+    const size_t nchunks = (E + K - 1) / K;
+    const size_t ng1 = nchunks / MSM_GROUP, ng2 = nchunks / (MSM_GROUP * MSM_GROUP);
+    HALO_CHECK(M.digits.reserve(E * 4));
+    HALO_CHECK(M.bstart.reserve((NB + 1) * 4));
+    HALO_CHECK(M.partials.reserve((nchunks * 2 + ng1 + ng2 + 2) * 128));
+    HALO_CHECK(M.bucket_sums.reserve(NB * 128));
+    HALO_CHECK(M.seg_acc.reserve((size_t)SW * H * 128));
+    HALO_CHECK(M.seg_sum.reserve((size_t)SW * L * 128));
+    HALO_CHECK(M.bits.reserve((size_t)SW * NT * 128));
+    HALO_CHECK(M.window_sums.reserve((size_t)SW * 128));
+    uint4* P_first = M.partials.as<uint4>();
+    uint4* P_last = P_first + 8 * nchunks;
+    uint4* P_g1 = P_last + 8 * nchunks;
+    uint4* P_g2 = P_g1 + 8 * (ng1 + 1);
+    uint32_t* digits = M.digits.as<uint32_t>();
+    if (ragged) HALO_HIP(hipMemsetAsync(digits, 0xff, E * 4, s));  // DIGIT_NONE past each length
+    for (size_t p = 0; p < k; p++)
+        if (lens[p])
+            hipLaunchKernelGGL(k_digits<typename Cv::Scalar>, dim3(grid_for(lens[p], 256)), dim3(256), 0, s,
+                               (const uint4*)scalars[p], lens[p], c, W, digits + p * SN, ld);
+    HALO_HIP(hipGetLastError());
+    uint32_t *skeys = nullptr, *svals = nullptr;
+    const uint32_t* scount = nullptr;
+    HALO_CHECK(msm_radix_sort(digits, E, SN, B, key_bits, M.sort, &skeys, &svals, &scount, nullptr, NB, s));
+    {
+        ProfScope prof("msm_acc", s);
+        const uint32_t nblocks = (uint32_t)grid_for(nchunks, 256);
+        auto kacc = k_acc<Cv, false>;
+        HALO_LAUNCH(prof, kacc, dim3(nblocks), dim3(256), 0, s, (const uint32_t*)skeys, (const uint32_t*)svals, scount,
+                    K, srs.shifted.as<const uint4>(), (uint32_t)ld, is_pow2(ld) ? ilog2(ld) : 0xffu, srs.n, 32u, 0u,
+                    P_first, P_last, M.bucket_sums.as<uint4>(), (uint32_t*)nullptr, nblocks);
+        HALO_HIP(hipGetLastError());
+    }
+    MsmTailArgs ta;
+    ta.n = E;
+    ta.skeys = skeys;
+    ta.scount = scount;
+    ta.K = K;
+    ta.NB = NB;
+    ta.E = E;
+    ta.first = P_first;
+    ta.last = P_last;
+    ta.g1 = P_g1;
+    ta.g2 = P_g2;
+    ta.ng1 = ng1;
+    ta.ng2 = ng2;
+    ta.bstart = M.bstart.as<uint32_t>();
+    ta.bucket_sums = M.bucket_sums.as<uint4>();
+    ta.rows = M.seg_acc.as<uint4>();
+    ta.cols = M.seg_sum.as<uint4>();
+    ta.terms = M.bits.as<uint4>();
+    ta.window_sums = M.window_sums.as<uint4>();
+    ta.L = L;
+    ta.H = H;
+    ta.logH = logH;
+    ta.logL = logL;
+    ta.NT = NT;
+    ta.SW = SW;
+    ta.c = c;
+    ta.hide_table = nullptr;
+    ta.hide_scalar = nullptr;
+    ta.out_wrapped = nullptr;
+    HALO_CHECK(msm_tail_launch(curve_id<Cv>(), ta, s));
+    hipLaunchKernelGGL(k_sums_out<Cv>, dim3(grid_for(k, 64)), dim3(64), 0, s, M.window_sums.as<const uint4>(),
+                       (uint32_t)k, d_out);
+    HALO_HIP(hipGetLastError());
+    HALO_HIP(hipEventRecord(M.tail_done, s));
+    M.tail_pending = true;
+    M.owner = s;
+    return HALO_OK;
+}
+
+// polynomials up to this length take the one-MSM batch path (HALO_MSM_MULTI_MAX overrides; 0 = off)
+static size_t msm_multi_max() {
+    static const size_t v = [] {
+        const char* e = getenv("HALO_MSM_MULTI_MAX");
+        return e ? (size_t)strtoull(e, nullptr, 10) : ((size_t)1 << 18);
+    }();
+    return v;
+}
+
 // Claims the scratch set of the next MSM on stream s and orders s after that set's previous tail
 // (the caller stages converted bases in its conv buffer before the MSM is enqueued; the MSM then
 // runs on the same set, msm_device's preset).
@@ -638,7 +812,7 @@ int msm_device(DeviceState* st, int curve, const void* bases_int, const void* sc
 
 // MSM over the resident SRS prefix Gs[0..n): uses the window-shifted copies when present.
 int msm_srs_device(DeviceState* st, int curve, const void* scalars_ark, size_t n, const void* hide_scalar,
-                   void* d_out_wrapped, hipStream_t s, bool async) {
+                   void* d_out_wrapped, hipStream_t s, bool async, hipStream_t fs) {
     SrsState& srs = st->srs[curve];
     if (n > srs.n) return set_error(HALO_ESRSRANGE, "n (%zu) exceeds the resident SRS length (%zu)", n, srs.n);
     const void* table = hide_scalar ? srs.s_table.ptr : nullptr;
@@ -650,7 +824,8 @@ int msm_srs_device(DeviceState* st, int curve, const void* scalars_ark, size_t n
     DISPATCH_CURVE(curve, Cv, {
         rc = msm_device_t<Cv>(st, use_shifted ? srs.shifted.as<const uint4>() : srs.gs.as<const uint4>(), use_shifted,
                               srs.n, (const uint4*)scalars_ark, n, use_shifted ? srs.shifted_c : 0, (const uint4*)table,
-                              (const uint4*)hide_scalar, (uint4*)d_out_wrapped, s, async);
+                              (const uint4*)hide_scalar, (uint4*)d_out_wrapped, s, async, 32, false, false, nullptr,
+                              -1, fs);
     });
     return rc;
 }
@@ -796,15 +971,15 @@ static int msm_shared_batch_t(DeviceState* st, const uint4* bases, const uint4* 
     uint4* P_g2 = P_g1 + 8 * (ng1 + 1);
 
     hipLaunchKernelGGL(k_digits<typename Cv::Scalar>, dim3(grid_for(T, 256)), dim3(256), 0, s, w_ark, T, c, W,
-                       S.digits.as<uint32_t>());
+                       S.digits.as<uint32_t>(), T);
     hipLaunchKernelGGL(k_batch_lists, dim3(1), dim3(256), 0, s, S.digits.as<const uint32_t>(), (uint32_t)T, W, B,
                        (uint32_t)len, ent, ekey, tot);
     hipLaunchKernelGGL(k_batch_expand, dim3(grid_for(E, 256)), dim3(256), 0, s, (const uint32_t*)ent,
                        (const uint32_t*)ekey, (const uint32_t*)tot, (uint32_t)len, (uint32_t)(W * B),
                        S.keys.as<uint32_t>(), S.vals.as<uint32_t>());
-    hipLaunchKernelGGL((k_acc<Cv, true>), dim3(grid_for(nchunks, 256)), dim3(256), 0, s, S.keys.as<const uint32_t>(),
+    hipLaunchKernelGGL((k_acc<Cv, false>), dim3(grid_for(nchunks, 256)), dim3(256), 0, s, S.keys.as<const uint32_t>(),
                        S.vals.as<const uint32_t>(), (const uint32_t*)(tot + 1), K, bases, 1u, 0u, (size_t)0, 32u, 0u,
-                       P_first, P_last, S.bucket_sums.as<uint4>());
+                       P_first, P_last, S.bucket_sums.as<uint4>(), (uint32_t*)nullptr, (uint32_t)grid_for(nchunks, 256));
     HALO_HIP(hipGetLastError());
     MsmTailArgs ta;
     ta.n = T;
@@ -1012,21 +1187,13 @@ int srs_precompute_windows(DeviceState* st, int curve, hipStream_t s) {
     const int c = msm_shifted_window_bits(srs.n);
     const int W = msm_windows(c);
     HALO_CHECK(srs.shifted.reserve((size_t)W * srs.n * 64));
-    HALO_CHECK(st->scratch[7].reserve(16));
-    uint32_t* d_ids = st->scratch[7].as<uint32_t>();
-    HALO_HIP(hipMemsetAsync(d_ids, 0, 4, s));
     DISPATCH_CURVE(curve, Cv, {
-        hipLaunchKernelGGL(k_count_identity<Cv>, dim3(grid_for(srs.n, 256)), dim3(256), 0, s, srs.gs.as<const uint4>(),
-                           srs.n, d_ids);
         hipLaunchKernelGGL(k_shift_windows<Cv>, dim3(grid_for(srs.n, 64)), dim3(64), 0, s, srs.gs.as<const uint4>(),
                            srs.n, c, W, srs.shifted.as<uint4>());
     });
     HALO_HIP(hipGetLastError());
-    uint32_t ids = 0;
-    HALO_CHECK(copy_d2h(&ids, d_ids, 4, s));
     HALO_HIP(hipStreamSynchronize(s));
     srs.shifted_c = c;
-    srs.shifted_no_id = (ids == 0);
     return HALO_OK;
 }
 
@@ -1413,6 +1580,51 @@ extern "C" int halo_msm_dev_async(halo_curve_t curve, const void* d_bases, const
     HALO_CHECK(convert_wrapped_to_internal(curve, d_bases, conv->ptr, n, s));
     return msm_device(st, curve, conv->ptr, d_scalars, n, nullptr, nullptr, d_out, s, true, false, false, nullptr,
                       set);
+}
+
+namespace halo {
+// k commitments over the resident SRS prefix (lens[i] scalars at d_scalars[i]) -> d_out + 64 i,
+// asynchronous on s (msm_join before reading)
+int msm_batch_device(DeviceState* st, int curve, const void* const* d_scalars, const size_t* lens, size_t k, void* d_out,
+                     hipStream_t s) {
+    MsmPipe& PP = g_msm_pipe[st->device & 63];
+    HALO_CHECK(pipe_init(PP));
+    SrsState& srs = st->srs[curve];
+    size_t nmax = 0;
+    for (size_t i = 0; i < k; i++) {
+        if (lens[i] && !d_scalars[i]) return set_error(HALO_EINVAL, "halo_msm_batch_dev: null scalars %zu", i);
+        if (lens[i] > srs.n) return set_error(HALO_ESRSRANGE, "n (%zu) exceeds the resident SRS length (%zu)", lens[i], srs.n);
+        nmax = std::max(nmax, lens[i]);
+    }
+    // HALO_BATCH_OVERLAP=1: fronts on the side stream beside the accumulations (measured slower:
+    // the sort kernels starve beside k_acc's gathers); off by default
+    const char* ov = getenv("HALO_BATCH_OVERLAP");
+    const bool overlap = k > 1 && srs.shifted_c != 0 && ov && ov[0] == '1';
+    if (k > 1 && srs.shifted_c && nmax <= msm_multi_max() && !overlap) {
+        int rc;
+        DISPATCH_CURVE(curve, Cv, { rc = msm_multi_device_t<Cv>(st, d_scalars, lens, k, (uint4*)d_out, s); });
+        return rc;
+    }
+    if (overlap) {  // the fronts run on PP.front from the batch's inputs on: one event on s
+        HALO_HIP(hipEventRecord(PP.batch_in, s));
+        HALO_HIP(hipStreamWaitEvent(PP.front, PP.batch_in, 0));
+    }
+    for (size_t i = 0; i < k; i++)
+        HALO_CHECK(msm_srs_device(st, curve, d_scalars[i], lens[i], nullptr, (char*)d_out + 64 * i, s, true,
+                                  overlap ? PP.front : nullptr));
+    return HALO_OK;
+}
+}  // namespace halo
+
+extern "C" int halo_msm_batch_dev(halo_curve_t curve, const void* const* d_scalars, const size_t* lens, size_t k,
+                                  void* d_out, void* stream) {
+    clear_error();
+    HALO_CHECK(check_curve(curve));
+    if (k && (!d_scalars || !lens || !d_out)) return set_error(HALO_EINVAL, "halo_msm_batch_dev: null buffer");
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    return msm_batch_device(st, curve, d_scalars, lens, k, d_out, (hipStream_t)stream);
 }
 
 extern "C" int halo_msm_join(void* stream) {

@@ -18,12 +18,16 @@ int msm_device(DeviceState* st, int curve, const void* bases_int, const void* sc
 // Claims the scratch set the next MSM on stream s will use (s waits for its previous tail) and
 // returns its base-conversion buffer; pass the set to msm_device as `preset`.
 int msm_claim_set(DeviceState* st, hipStream_t s, int* set, DevBuf** conv);
+// k commitments over the resident SRS prefix, MSM i over lens[i] ark scalars at d_scalars[i] (device),
+// result i (WrappedPoint) at d_out + 64 i; asynchronous on s like msm_device(async) (msm_join).
+int msm_batch_device(DeviceState* st, int curve, const void* const* d_scalars, const size_t* lens, size_t k, void* d_out,
+                     hipStream_t s);
 // Makes stream s wait for the reduction tails of the async MSMs enqueued on s.
 int msm_join(DeviceState* st, hipStream_t s);
 // MSM over the resident SRS prefix (window-shifted copies when precomputed); optional hiding
 // scalar (ark, device pointer) times S.
 int msm_srs_device(DeviceState* st, int curve, const void* scalars_ark, size_t n, const void* hide_scalar,
-                   void* d_out_wrapped, hipStream_t s, bool async = false);
+                   void* d_out_wrapped, hipStream_t s, bool async = false, hipStream_t fs = nullptr);
 // MSM over the resident SRS range [offset, offset + n) with a caller hiding table (2^i P, i < 256,
 // internal affine) and scalar; uses the window-shifted copies (returns HALO_EINVAL without them).
 // blk_lg < 32: scalar i goes with point offset + i + ((i >> blk_lg) << blk_lg), i.e. the blocks

@@ -55,7 +55,6 @@ struct SrsState {
     DevBuf s_table;     // 2^i S (i < 256), internal affine: hiding term of pedersen::commit
     DevBuf shifted;     // optional window-shifted copies
     int shifted_c = 0;  // window bits of `shifted`
-    bool shifted_no_id = false;  // no identity among the bases of `shifted` (k_acc skips its test)
     int shifted_windows = 0;
 };
 

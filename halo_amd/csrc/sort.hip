@@ -25,8 +25,9 @@
 namespace halo {
 
 constexpr int RS_THREADS = 512;
-constexpr int RS_ROUNDS = 16;
-constexpr int RS_TILE = RS_THREADS * RS_ROUNDS;  // 8192: runs average 32 entries (128 B) per digit
+// Tiles of RS_THREADS x ROUNDS entries: 16 rounds (8192 entries, runs of ~32 entries = 128 B per digit,
+// 64 KB of LDS staging) by default; 8 rounds (4096 entries, 32 KB) when the sort runs beside the
+// previous MSM's accumulation (halo_msm_batch_dev), whose workgroups leave little LDS free.
 constexpr int RS_BINS = 256;
 constexpr uint32_t RS_NONE = 0xffffffffu;
 
@@ -61,13 +62,15 @@ HALO_DEV bool rs_fetch(const RsIn& in, size_t e, size_t limit, uint32_t& key, ui
 
 HALO_DEV size_t rs_limit(const RsIn& in) { return in.pass == 0 ? in.E : (size_t)*in.count; }
 
+template <int ROUNDS>
 __global__ __launch_bounds__(RS_THREADS) void k_rs_hist(RsIn in, uint32_t ntiles, uint32_t* hist) {
+    constexpr int RS_TILE = RS_THREADS * ROUNDS;
     __shared__ uint32_t h[RS_BINS];
     if (threadIdx.x < RS_BINS) h[threadIdx.x] = 0;
     __syncthreads();
     const size_t limit = rs_limit(in);
     const size_t base = (size_t)blockIdx.x * RS_TILE;
-    for (int r = 0; r < RS_ROUNDS; r++) {
+    for (int r = 0; r < ROUNDS; r++) {
         uint32_t k, v;
         if (rs_fetch(in, base + (size_t)r * RS_THREADS + threadIdx.x, limit, k, v))
             atomicAdd(&h[(k >> in.shift) & 255u], 1u);
@@ -128,8 +131,10 @@ __global__ __launch_bounds__(RS_BINS) void k_rs_chunkscan(uint32_t* chunk, uint3
 // Each wave owns a contiguous eighth of the tile (1024 entries, 16 rounds of 64), so ranking is
 // wave-local (ballots + a wave-private LDS run counter per digit) and the workgroup needs only
 // three barriers: after the per-wave histograms, after the prefix, after staging.
+template <int ROUNDS>
 __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(RsIn in, const uint32_t* tile_off, const uint32_t* chunk_off,
                                                            uint32_t* keys_out, uint32_t* vals_out) {
+    constexpr int RS_TILE = RS_THREADS * ROUNDS;
     constexpr int WAVES = RS_THREADS / 64;
     constexpr int PER_WAVE = RS_TILE / WAVES;  // 1024
     __shared__ uint32_t goff[RS_BINS];           // global start of this tile's run per digit
@@ -335,7 +340,8 @@ int device_exclusive_scan(const uint32_t* in, size_t n, uint32_t* out, DevBuf& t
 
 int msm_radix_sort(const uint32_t* digits, size_t E, size_t npw, uint32_t B, uint32_t key_bits, SortScratch& S,
                    uint32_t** keys_out, uint32_t** vals_out, const uint32_t** count_out, uint32_t* bstart, size_t NB,
-                   hipStream_t s) {
+                   hipStream_t s, bool small_tiles) {
+    const int RS_TILE = RS_THREADS * (small_tiles ? 8 : 16);
     const uint32_t ntiles = (uint32_t)std::max<size_t>(1, (E + RS_TILE - 1) / RS_TILE);
     const size_t hn = (size_t)RS_BINS * ntiles;
     HALO_CHECK(S.keys[0].reserve(std::max<size_t>(E, 1) * 4));
@@ -359,14 +365,16 @@ int msm_radix_sort(const uint32_t* digits, size_t E, size_t npw, uint32_t B, uin
         in.B = B;
         in.pass = p;
         in.shift = 8 * p;
-        hipLaunchKernelGGL(k_rs_hist, dim3(ntiles), dim3(RS_THREADS), 0, s, in, ntiles, S.hist.as<uint32_t>());
+        hipLaunchKernelGGL(small_tiles ? k_rs_hist<8> : k_rs_hist<16>, dim3(ntiles), dim3(RS_THREADS), 0, s, in, ntiles,
+                           S.hist.as<uint32_t>());
         hipLaunchKernelGGL(k_rs_colscan, dim3(nchunks), dim3(RS_BINS), 0, s, S.hist.as<uint32_t>(), ntiles,
                            S.offs.as<uint32_t>());
         // pass 0 also stores the number of valid (nonzero-digit) entries
         hipLaunchKernelGGL(k_rs_chunkscan, dim3(1), dim3(RS_BINS), 0, s, S.offs.as<uint32_t>(), nchunks,
                            p == 0 ? S.count.as<uint32_t>() : nullptr);
-        hipLaunchKernelGGL(k_rs_scatter, dim3(ntiles), dim3(RS_THREADS), 0, s, in, S.hist.as<const uint32_t>(),
-                           S.offs.as<const uint32_t>(), S.keys[cur].as<uint32_t>(), S.vals[cur].as<uint32_t>());
+        hipLaunchKernelGGL(small_tiles ? k_rs_scatter<8> : k_rs_scatter<16>, dim3(ntiles), dim3(RS_THREADS), 0, s, in,
+                           S.hist.as<const uint32_t>(), S.offs.as<const uint32_t>(), S.keys[cur].as<uint32_t>(),
+                           S.vals[cur].as<uint32_t>());
         HALO_HIP(hipGetLastError());
         cur ^= 1;
     }

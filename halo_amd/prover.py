@@ -589,10 +589,13 @@ class DeviceBackend:
 
     # -- commitments, evaluations, openings
     def commit_many(self, polys):
-        outs = self.torch.zeros((len(polys), 8), dtype=self.torch.int64, device="cuda")
-        for i, p in enumerate(polys):
-            self.H.check(self.L.halo_msm_dev_async(self.curve, None, self._p(p), p.shape[0],
-                                                   ctypes.c_void_p(outs[i].data_ptr()), self.sp))
+        """pcdl::commit of every polynomial (protocol.rs:114,263): one halo_msm_batch_dev call (small
+        polynomials as one MSM with (polynomial, bucket) keys, larger ones pipelined)."""
+        k = len(polys)
+        outs = self.torch.zeros((k, 8), dtype=self.torch.int64, device="cuda")
+        ptrs = (ctypes.c_void_p * k)(*[p.data_ptr() for p in polys])
+        lens = (ctypes.c_size_t * k)(*[p.shape[0] for p in polys])
+        self.H.check(self.L.halo_msm_batch_dev(self.curve, ptrs, lens, k, ctypes.c_void_p(outs.data_ptr()), self.sp))
         self.H.check(self.L.halo_msm_join(self.sp))
         return [o.view(np.uint64) for o in outs.cpu().numpy()]
 

@@ -126,6 +126,15 @@ int halo_msm_dev_async(halo_curve_t curve, const void* d_bases, const void* d_sc
                        void* d_out, void* stream);
 /* Makes `stream` wait (device-side, no host sync) for every asynchronous MSM still in flight. */
 int halo_msm_join(void* stream);
+/* Batched commitments over the resident SRS prefix: k independent MSMs, MSM i over d_scalars[i]
+ * (device pointer, lens[i] <= SRS length ark scalars), result i (64-B WrappedPoint) at
+ * d_out + 64 i.  Replaces a loop of pcdl::commit / pedersen::commit calls over one SRS -- the
+ * reference's commitment batches (crates/plonk/src/plonk/protocol.rs:114,263 -- 16 commits each;
+ * crates/plonk/src/plonk/trace.rs:188-192).  All inputs must be ready on `stream` at the call;
+ * asynchronous like halo_msm_dev_async (halo_msm_join before reading d_out).  Inside the batch the
+ * digit extraction and bucket sort of MSM i+1 run on a side stream beside MSM i's accumulation. */
+int halo_msm_batch_dev(halo_curve_t curve, const void* const* d_scalars, const size_t* lens, size_t k, void* d_out,
+                       void* stream);
 /* Sum of k points (host arrays) on the device: the combine step after an RCCL all-gather of
  * per-rank partial MSMs (RCCL has no elliptic-curve reduction operator). */
 int halo_point_sum(halo_curve_t curve, const halo_wrapped_point_t* pts, size_t k, halo_wrapped_point_t* out);

@@ -347,3 +347,33 @@ def test_async_msm_caller_bases_concurrent_streams(hal, corc):
         b = bases.cpu().numpy().view(np.uint64)
         hal.check(L.halo_msm(0, hal.ptr(np.ascontiguousarray(b)), n, hal.ptr(sc), n, hal.ptr(exp)))
         assert np.array_equal(got[k], exp), k
+
+
+@pytest.mark.parametrize("cname,cid", CURVES)
+def test_msm_batch_dev_one_msm_path(hal, corc, cname, cid):
+    """halo_msm_batch_dev (the commitment batches of protocol.rs:114,263 / trace.rs:188-192): k
+    polynomials of ragged lengths (including empty and length 1) over the resident window-shifted
+    SRS as one MSM with (polynomial, bucket) keys, each result bit-exact vs the oracle MSM; and the
+    per-MSM pipelined path (HALO_MSM_MULTI_MAX=0 in a subprocess is not needed: lengths above the
+    threshold take it) agrees with halo_msm_dev_async."""
+    import ctypes
+
+    import torch
+    L = hal.load()
+    n = 1 << 12
+    g = corc.srs_generate(cname, n)
+    group.PublicParams.upload(cname, g, precompute_windows=True)
+    lens = [n, 0, 1, 777, n - 1, n, 2048, 5]
+    scs = [rand_sc(max(m, 1), 40 + i)[:m] for i, m in enumerate(lens)]
+    scs[0][:3] = scs[0][3]  # repeated scalars
+    dev = [torch.from_numpy(np.ascontiguousarray(sc).view(np.int64)).cuda() if len(sc) else torch.zeros((1, 4), dtype=torch.int64, device="cuda") for sc in scs]
+    ptrs = (ctypes.c_void_p * len(lens))(*[d.data_ptr() for d in dev])
+    lns = (ctypes.c_size_t * len(lens))(*lens)
+    out = torch.zeros((len(lens), 8), dtype=torch.int64, device="cuda")
+    sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    hal.check(L.halo_msm_batch_dev(cid, ptrs, lns, len(lens), ctypes.c_void_p(out.data_ptr()), sp))
+    hal.check(L.halo_msm_join(sp))
+    got = out.cpu().numpy().view(np.uint64)
+    for i, m in enumerate(lens):
+        exp = corc.msm(cname, g[:m], scs[i]) if m else np.zeros(8, dtype=np.uint64)
+        assert np.array_equal(got[i], exp), (i, m)
