@@ -5,6 +5,7 @@ and fails loudly if that library is missing or no GPU is present.  There is no C
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
 
@@ -64,6 +65,11 @@ SIGNATURES = {
     "halo_srs_window_bits": [ctypes.c_int],
     "halo_msm_dev_async": [ctypes.c_int, _vp, _vp, _sz, _vp, _vp],
     "halo_msm_batch_dev": [ctypes.c_int, _vp, _vp, _sz, _vp, _vp],
+    "halo_shutdown": [],
+    "halo_srs_sh": [ctypes.c_int, _vp, _vp],
+    "halo_point_dot_projective": [ctypes.c_int, _vp, _sz, _vp, _sz, _vp],
+    "halo_pcdl_hiding_blind": [ctypes.c_int, _vp, _sz, _vp, _vp, _vp, _vp],
+    "halo_pcdl_hiding_combine": [ctypes.c_int, _vp, _sz, _vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "halo_msm_join": [_vp],
     "halo_srs_read": [ctypes.c_int, _sz, _sz, _vp],
     "halo_point_sum": [ctypes.c_int, _vp, _sz, _vp],
@@ -135,6 +141,10 @@ def load(path: str = LIB_PATH):
         fn.argtypes = args
         fn.restype = RESTYPES.get(name, ctypes.c_int)
     _lib = L
+    if hasattr(L, "halo_shutdown"):
+        # release streams/events before the HIP runtime tears down (registered after torch's own
+        # handlers, so it runs before them)
+        atexit.register(L.halo_shutdown)
     return L
 
 

@@ -4,6 +4,7 @@
 #include "dispatch.hpp"
 #include "glv.hpp"
 #include "runtime.hpp"
+#include "msm.hpp"
 
 namespace halo {
 
@@ -149,4 +150,153 @@ extern "C" int halo_curve_op(halo_curve_t curve, int op, const halo_wrapped_poin
     });
     HALO_HIP(hipGetLastError());
     return copy_d2h(out, st->scratch[3].ptr, pb, s);
+}
+
+// ---------------------------------------------------------------------------------------------
+// The hiding branch of pcdl::open_without_eval (crates/accumulation/src/pcdl.rs:344-371):
+//   p_bar = (X - z) q, C_bar = commit(p_bar, d, w_bar)         -> halo_pcdl_hiding_blind
+//   (the caller's transcript: alpha = rho(C, C_bar, z, v))
+//   p' = p + alpha p_bar, w' = w + alpha w_bar, C' = C + alpha C_bar - w' S  -> halo_pcdl_hiding_combine
+// q (d coefficients) and w_bar are the caller's random draws (the reference samples them from its rng).
+// ---------------------------------------------------------------------------------------------
+namespace halo {
+
+template <class S>
+__global__ void k_pbar(const uint4* q, size_t d, const uint4* z, uint4* out) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > d) return;
+    const Fe<S> a = i >= 1 ? fe_from_ark<S>(q + 2 * (i - 1)) : fe_zero<S>();
+    const Fe<S> b = i < d ? fe_from_ark<S>(q + 2 * i) : fe_zero<S>();
+    fe_to_ark(out + 2 * i, fe_sub(a, fe_mul(fe_from_ark<S>(z), b)));
+}
+
+template <class S>
+__global__ void k_axpy_pad(const uint4* p, size_t len, const uint4* pb, size_t n, const uint4* alpha, uint4* out) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const Fe<S> x = i < len ? fe_from_ark<S>(p + 2 * i) : fe_zero<S>();
+    fe_to_ark(out + 2 * i, fe_add(x, fe_mul(fe_from_ark<S>(alpha), fe_from_ark<S>(pb + 2 * i))));
+}
+
+// lane 0: alpha C_bar, lane 1: w' S (both GLV scalar multiplications run side by side); lane 0 then
+// forms C + alpha C_bar - w' S.  w' = w + alpha w_bar is computed by both lanes.
+template <class Cv>
+__global__ __launch_bounds__(64) void k_hiding_point(const uint4* C, const uint4* C_bar, const uint4* S_int,
+                                                     const uint4* alpha, const uint4* w, const uint4* w_bar,
+                                                     uint4* C_out, uint4* w_out) {
+    using F = typename Cv::Base;
+    using Sc = typename Cv::Scalar;
+    __shared__ uint4 tab[2][16 * 8];
+    __shared__ uint4 res[8];
+    const int lane = threadIdx.x;
+    if (lane >= 2) return;
+    const Fe<Sc> wp = fe_add(fe_from_ark<Sc>(w), fe_mul(fe_from_ark<Sc>(alpha), fe_from_ark<Sc>(w_bar)));
+    uint32_t kw[8];
+    if (lane == 0) {
+        fe_ark_to_canonical_words<Sc>(alpha, kw);
+    } else {
+        uint4 tmp[2];
+        fe_to_ark(tmp, wp);
+        fe_ark_to_canonical_words<Sc>(tmp, kw);
+    }
+    const Affine<F> base = lane == 0 ? aff_from_wrapped<F>(C_bar) : aff_load<F>(S_int);
+    XYZZ<F> r = scalar_mul_glv<Cv>(base, kw, tab[lane]);
+    if (lane == 1) xyzz_store(res, xyzz_neg(r));
+    __syncthreads();
+    if (lane == 0) {
+        XYZZ<F> acc = xyzz_madd(r, aff_from_wrapped<F>(C));
+        acc = xyzz_add(acc, xyzz_load<F>(res));
+        aff_to_wrapped(C_out, xyzz_to_aff(acc));
+        fe_to_ark(w_out, wp);
+    }
+}
+
+}  // namespace halo
+
+static int hiding_checks(DeviceState* st, halo_curve_t curve, size_t d) {
+    SrsState& srs = st->srs[curve];
+    if (!srs.n) return set_error(HALO_ESRSRANGE, "no resident SRS: call halo_srs_upload first");
+    if (!srs.has_sh) return set_error(HALO_ESRSRANGE, "hiding commitment needs S: upload the SRS (S, H) first");
+    const size_t n = d + 1;
+    if (n <= 1) return set_error(HALO_EINVAL, "assertion failed: n > 1");
+    if (!is_pow2(n)) return set_error(HALO_ENOTPOW2, "n (%zu) is not a power of two", n);
+    if (d > srs.n - 1) return set_error(HALO_ESRSRANGE, "assertion failed: d <= pp.D");
+    return HALO_OK;
+}
+
+extern "C" int halo_pcdl_hiding_blind(halo_curve_t curve, const halo_fe_t* q, size_t d, const halo_fe_t* z,
+                                      const halo_fe_t* w_bar, halo_fe_t* p_bar_out, halo_wrapped_point_t* C_bar_out) {
+    clear_error();
+    if ((curve != HALO_PALLAS && curve != HALO_VESTA) || !q || !z || !w_bar || !C_bar_out)
+        return set_error(HALO_EINVAL, "halo_pcdl_hiding_blind: invalid argument");
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    HALO_CHECK(hiding_checks(st, curve, d));
+    hipStream_t s = 0;
+    ScratchUse su(st, s);
+    const size_t n = d + 1;
+    HALO_CHECK(st->scratch[0].reserve(d * 32 + 64));
+    HALO_CHECK(st->scratch[1].reserve(n * 32));
+    HALO_CHECK(st->scratch[2].reserve(64 + 64));
+    char* small = st->scratch[2].as<char>();
+    HALO_CHECK(copy_h2d(st->scratch[0].ptr, q, d * 32, s));
+    HALO_CHECK(copy_h2d(small, z, 32, s));
+    HALO_CHECK(copy_h2d(small + 32, w_bar, 32, s));
+    const int field = curve == HALO_PALLAS ? HALO_FP : HALO_FQ;
+    DISPATCH_FIELD(field, Fs, {
+        hipLaunchKernelGGL(k_pbar<Fs>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, st->scratch[0].as<const uint4>(),
+                           d, (const uint4*)small, st->scratch[1].as<uint4>());
+    });
+    HALO_HIP(hipGetLastError());
+    HALO_CHECK(msm_srs_device(st, curve, st->scratch[1].ptr, n, small + 32, small + 64, s));
+    if (p_bar_out) HALO_CHECK(copy_d2h(p_bar_out, st->scratch[1].ptr, n * 32, s));
+    return copy_d2h(C_bar_out, small + 64, 64, s);
+}
+
+extern "C" int halo_pcdl_hiding_combine(halo_curve_t curve, const halo_fe_t* p, size_t len, const halo_fe_t* p_bar,
+                                        size_t d, const halo_fe_t* alpha, const halo_wrapped_point_t* C,
+                                        const halo_wrapped_point_t* C_bar, const halo_fe_t* w, const halo_fe_t* w_bar,
+                                        halo_fe_t* p_prime_out, halo_fe_t* w_prime_out,
+                                        halo_wrapped_point_t* C_prime_out) {
+    clear_error();
+    if ((curve != HALO_PALLAS && curve != HALO_VESTA) || (len && !p) || !p_bar || !alpha || !C || !C_bar || !w ||
+        !w_bar || !p_prime_out || !w_prime_out || !C_prime_out)
+        return set_error(HALO_EINVAL, "halo_pcdl_hiding_combine: invalid argument");
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    HALO_CHECK(hiding_checks(st, curve, d));
+    const size_t n = d + 1;
+    if (len > n) return set_error(HALO_EDEGREE, "p has %zu coefficients for d = %zu", len, d);
+    hipStream_t s = 0;
+    ScratchUse su(st, s);
+    HALO_CHECK(st->scratch[0].reserve(std::max<size_t>(len, 1) * 32));
+    HALO_CHECK(st->scratch[1].reserve(n * 32));
+    HALO_CHECK(st->scratch[3].reserve(n * 32));
+    HALO_CHECK(st->scratch[2].reserve(512));
+    char* sm = st->scratch[2].as<char>();  // alpha, w, w_bar | C, C_bar, S | C', w'
+    HALO_CHECK(copy_h2d(st->scratch[0].ptr, p, len * 32, s));
+    HALO_CHECK(copy_h2d(st->scratch[1].ptr, p_bar, n * 32, s));
+    HALO_CHECK(copy_h2d(sm, alpha, 32, s));
+    HALO_CHECK(copy_h2d(sm + 32, w, 32, s));
+    HALO_CHECK(copy_h2d(sm + 64, w_bar, 32, s));
+    HALO_CHECK(copy_h2d(sm + 128, C, 64, s));
+    HALO_CHECK(copy_h2d(sm + 192, C_bar, 64, s));
+    HALO_CHECK(copy_h2d(sm + 256, st->srs[curve].S, 64, s));
+    const int field = curve == HALO_PALLAS ? HALO_FP : HALO_FQ;
+    DISPATCH_FIELD(field, Fs, {
+        hipLaunchKernelGGL(k_axpy_pad<Fs>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                           st->scratch[0].as<const uint4>(), len, st->scratch[1].as<const uint4>(), n, (const uint4*)sm,
+                           st->scratch[3].as<uint4>());
+    });
+    DISPATCH_CURVE(curve, Cv, {
+        hipLaunchKernelGGL(k_hiding_point<Cv>, dim3(1), dim3(64), 0, s, (const uint4*)(sm + 128), (const uint4*)(sm + 192),
+                           (const uint4*)(sm + 256), (const uint4*)sm, (const uint4*)(sm + 32), (const uint4*)(sm + 64),
+                           (uint4*)(sm + 320), (uint4*)(sm + 384));
+    });
+    HALO_HIP(hipGetLastError());
+    HALO_CHECK(copy_d2h(p_prime_out, st->scratch[3].ptr, n * 32, s));
+    HALO_CHECK(copy_d2h(w_prime_out, sm + 384, 32, s));
+    return copy_d2h(C_prime_out, sm + 320, 64, s);
 }

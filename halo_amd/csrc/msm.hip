@@ -484,7 +484,14 @@ static int pipe_init(MsmPipe& P) {
     HALO_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
     HALO_HIP(hipStreamCreateWithPriority(&P.front, hipStreamNonBlocking, greatest));
     HALO_HIP(hipEventCreateWithFlags(&P.batch_in, hipEventDisableTiming));
-    for (auto& t : P.tail) HALO_HIP(hipStreamCreateWithFlags(&t, hipStreamNonBlocking));
+    // HALO_TAIL_PRIO=low: the tails' kernels are dispatched after the next MSM's front
+    const char* tp = getenv("HALO_TAIL_PRIO");
+    for (auto& t : P.tail) {
+        if (tp && tp[0] == 'l')
+            HALO_HIP(hipStreamCreateWithPriority(&t, hipStreamNonBlocking, least));
+        else
+            HALO_HIP(hipStreamCreateWithFlags(&t, hipStreamNonBlocking));
+    }
     for (auto& m : P.set) {
         HALO_HIP(hipEventCreateWithFlags(&m.acc_done, hipEventDisableTiming));
         HALO_HIP(hipEventCreateWithFlags(&m.tail_done, hipEventDisableTiming));
@@ -492,6 +499,35 @@ static int pipe_init(MsmPipe& P) {
         HALO_HIP(hipEventCreateWithFlags(&m.front_done, hipEventDisableTiming));
     }
     return HALO_OK;
+}
+
+// halo_shutdown: destroys the pipeline's streams and events while the HIP runtime is alive (a
+// static destructor must not outlive it); pipe_init recreates them if the library is used again
+void msm_shutdown() {
+    for (auto& P : g_msm_pipe) {
+        if (!P.tail[0]) continue;
+        for (auto& t : P.tail) {
+            (void)hipStreamSynchronize(t);
+            (void)hipStreamDestroy(t);
+            t = nullptr;
+        }
+        if (P.front) {
+            (void)hipStreamSynchronize(P.front);
+            (void)hipStreamDestroy(P.front);
+            P.front = nullptr;
+        }
+        if (P.batch_in) (void)hipEventDestroy(P.batch_in);
+        P.batch_in = nullptr;
+        for (auto& m : P.set) {
+            for (hipEvent_t* e : {&m.acc_done, &m.tail_done, &m.start, &m.front_done}) {
+                if (*e) (void)hipEventDestroy(*e);
+                *e = nullptr;
+            }
+            m.tail_pending = false;
+            m.owner = nullptr;
+        }
+        P.slot_owner[0] = P.slot_owner[1] = nullptr;
+    }
 }
 
 template <class Cv>
@@ -545,7 +581,11 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
     // round and 15% slower than K = 16).
     const size_t E = (size_t)W * NP;
     const size_t lanes = (size_t)st->num_cu * 16 * 64 * 4;
-    const uint32_t K = (uint32_t)std::max<size_t>(16, std::min<size_t>(64, (E + lanes - 1) / lanes));
+    static const uint32_t k_env = [] {
+        const char* e = getenv("HALO_ACC_K");
+        return e ? (uint32_t)atoi(e) : 0u;
+    }();
+    const uint32_t K = k_env ? k_env : (uint32_t)std::max<size_t>(16, std::min<size_t>(64, (E + lanes - 1) / lanes));
     const size_t nchunks = (E + K - 1) / K;
     const size_t ng1 = nchunks / MSM_GROUP, ng2 = nchunks / (MSM_GROUP * MSM_GROUP);
     HALO_CHECK(M.partials.reserve((std::max<size_t>(nchunks, 1) * 2 + ng1 + ng2 + 2) * 128));
@@ -1292,6 +1332,59 @@ extern "C" void halo_synth_scalar(halo_curve_t curve, uint64_t seed, uint64_t j,
     synth_scalar(seed, j, out_canonical);
 }
 
+namespace halo {
+// ark Projective (Jacobian X, Y, Z, Montgomery, 96 B) -> internal affine; Z = 0 -> (0, 0).  One
+// Fermat inversion per lane (Projective::normalize_batch of point_dot, group.rs:53-56).
+template <class Cv>
+__global__ void k_jacobian_to_internal(const uint4* in, uint4* out, size_t n) {
+    using F = typename Cv::Base;
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const Fe<F> Z = fe_from_ark<F>(in + 6 * i + 4);
+    Affine<F> a;
+    if (fe_is_zero(Z)) {
+        a.x = fe_zero<F>();
+        a.y = fe_zero<F>();
+    } else {
+        const Fe<F> zi = fe_inv(Z);
+        const Fe<F> zi2 = fe_sqr(zi);
+        a.x = fe_mul(fe_from_ark<F>(in + 6 * i), zi2);
+        a.y = fe_mul(fe_from_ark<F>(in + 6 * i + 2), fe_mul(zi2, zi));
+    }
+    aff_store(out + 4 * i, a);
+}
+}  // namespace halo
+
+// group::point_dot(xs, &[Projective]) (crates/group/src/group.rs:53-56): the bases arrive as ark
+// Projective (Jacobian) points, normalised on the device, then the MSM of halo_msm.
+extern "C" int halo_point_dot_projective(halo_curve_t curve, const halo_fe_t* scalars, size_t n_scalars,
+                                         const uint64_t (*bases)[12], size_t n_bases, halo_wrapped_point_t* out) {
+    clear_error();
+    HALO_CHECK(check_curve(curve));
+    const size_t n = std::min(n_bases, n_scalars);
+    if (!out || (n && (!bases || !scalars))) return set_error(HALO_EINVAL, "halo_point_dot_projective: null buffer");
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    hipStream_t s = 0;
+    ScratchUse su(st, s);
+    HALO_CHECK(st->scratch[0].reserve(std::max<size_t>(n, 1) * 96));
+    HALO_CHECK(st->scratch[1].reserve(std::max<size_t>(n, 1) * 64));
+    HALO_CHECK(st->scratch[2].reserve(std::max<size_t>(n, 1) * 32));
+    HALO_CHECK(st->scratch[3].reserve(64));
+    HALO_CHECK(copy_h2d(st->scratch[0].ptr, bases, n * 96, s));
+    HALO_CHECK(copy_h2d(st->scratch[2].ptr, scalars, n * 32, s));
+    if (n) {
+        DISPATCH_CURVE(curve, Cv, {
+            hipLaunchKernelGGL(k_jacobian_to_internal<Cv>, dim3(grid_for(n, 256)), dim3(256), 0, s,
+                               st->scratch[0].as<const uint4>(), st->scratch[1].as<uint4>(), n);
+        });
+        HALO_HIP(hipGetLastError());
+    }
+    HALO_CHECK(msm_device(st, curve, st->scratch[1].ptr, st->scratch[2].ptr, n, nullptr, nullptr, st->scratch[3].ptr, s));
+    return copy_d2h(out, st->scratch[3].ptr, 64, s);
+}
+
 // host arrays: bases (ark WrappedPoint), scalars (ark) -> out (host)
 extern "C" int halo_msm(halo_curve_t curve, const halo_wrapped_point_t* bases, size_t n_bases,
                         const halo_fe_t* scalars, size_t n_scalars, halo_wrapped_point_t* out) {
@@ -1480,6 +1573,27 @@ extern "C" int halo_srs_load_bincode(halo_curve_t curve, const uint8_t* const* b
     HALO_CHECK(copy_d2h(&bad, d_bad, 4, s));
     if (bad) return set_error(HALO_EINVAL, "assertion failed: affine.is_on_curve() (%u points)", bad);
     return srs_install(st, curve, d_pts, n, sh ? &SH[0] : nullptr, sh ? &SH[1] : nullptr, s);
+}
+
+// PublicParams' (S, H) (pp.rs:26-61) as ark WrappedPoints
+extern "C" int halo_srs_sh(halo_curve_t curve, halo_wrapped_point_t* S, halo_wrapped_point_t* H) {
+    clear_error();
+    HALO_CHECK(check_curve(curve));
+    if (!S || !H) return set_error(HALO_EINVAL, "halo_srs_sh: null buffer");
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    SrsState& srs = st->srs[curve];
+    if (!srs.has_sh) return set_error(HALO_ESRSRANGE, "no (S, H) uploaded");
+    hipStream_t s = 0;
+    ScratchUse su(st, s);
+    HALO_CHECK(st->scratch[0].reserve(256));
+    char* b = st->scratch[0].as<char>();
+    HALO_CHECK(copy_h2d(b, srs.S, 64, s));
+    HALO_CHECK(copy_h2d(b + 64, srs.H, 64, s));
+    HALO_CHECK(convert_internal_to_wrapped(curve, b, b + 128, 2, s));
+    HALO_CHECK(copy_d2h(S, b + 128, 64, s));
+    return copy_d2h(H, b + 192, 64, s);
 }
 
 extern "C" int halo_srs_len(halo_curve_t curve, size_t* n) {

@@ -22,6 +22,8 @@ int msm_claim_set(DeviceState* st, hipStream_t s, int* set, DevBuf** conv);
 // result i (WrappedPoint) at d_out + 64 i; asynchronous on s like msm_device(async) (msm_join).
 int msm_batch_device(DeviceState* st, int curve, const void* const* d_scalars, const size_t* lens, size_t k, void* d_out,
                      hipStream_t s);
+// Destroys the MSM pipeline's streams and events (halo_shutdown).
+void msm_shutdown();
 // Makes stream s wait for the reduction tails of the async MSMs enqueued on s.
 int msm_join(DeviceState* st, hipStream_t s);
 // MSM over the resident SRS prefix (window-shifted copies when precomputed); optional hiding

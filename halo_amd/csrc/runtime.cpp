@@ -1,5 +1,6 @@
 // Runtime: error state, device selection, per-device state, buffers.
 #include "runtime.hpp"
+#include "msm.hpp"
 
 #include <cstdio>
 #include <cstring>
@@ -194,6 +195,31 @@ int halo_init(int device) {
 const char* halo_last_error(void) { return g_last_error.c_str(); }
 
 int halo_abi_version(void) { return 100; }
+
+// Releases the library's HIP objects while the runtime is alive: pending profiling events, the MSM
+// pipeline's streams and events, the scratch fence events.  Python registers it with atexit
+// (halo_amd/_lib.py), which runs before the HIP runtime's own teardown; after it no static
+// destructor of this library touches HIP.  The library stays usable (objects are recreated).
+int halo_shutdown(void) {
+    (void)hipDeviceSynchronize();
+    {
+        std::lock_guard<std::mutex> g(g_prof_mu);
+        prof_drain();
+        g_prof.clear();
+        g_prof_on = false;
+    }
+    msm_shutdown();
+    std::lock_guard<std::mutex> g(g_states_mu);
+    for (DeviceState* st : g_states) {
+        if (!st) continue;
+        std::lock_guard<std::mutex> g2(st->mu);
+        if (st->scratch_ev) (void)hipEventDestroy(st->scratch_ev);
+        st->scratch_ev = nullptr;
+        st->scratch_used = false;
+        st->scratch_last = nullptr;
+    }
+    return HALO_OK;
+}
 
 int halo_stream_sync(void* stream) {
     HALO_HIP(hipStreamSynchronize((hipStream_t)stream));

@@ -17,6 +17,7 @@
 // entries is known only on the device (scan total) -- kernels bound themselves by it, so no host
 // round trip is needed.
 #include <algorithm>
+#include <cstdlib>
 
 #include "fields.hpp"
 #include "runtime.hpp"
@@ -341,6 +342,12 @@ int device_exclusive_scan(const uint32_t* in, size_t n, uint32_t* out, DevBuf& t
 int msm_radix_sort(const uint32_t* digits, size_t E, size_t npw, uint32_t B, uint32_t key_bits, SortScratch& S,
                    uint32_t** keys_out, uint32_t** vals_out, const uint32_t** count_out, uint32_t* bstart, size_t NB,
                    hipStream_t s, bool small_tiles) {
+    static const int tile_env = [] {
+        const char* e = getenv("HALO_SORT_ROUNDS");
+        return e ? atoi(e) : 0;
+    }();
+    if (tile_env == 8) small_tiles = true;
+    if (tile_env == 16) small_tiles = false;
     const int RS_TILE = RS_THREADS * (small_tiles ? 8 : 16);
     const uint32_t ntiles = (uint32_t)std::max<size_t>(1, (E + RS_TILE - 1) / RS_TILE);
     const size_t hn = (size_t)RS_BINS * ntiles;

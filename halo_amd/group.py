@@ -37,6 +37,16 @@ def point_dot_affine(xs, Gs, curve="pallas") -> np.ndarray:
     return out
 
 
+def point_dot(xs, Gs_projective, curve="pallas") -> np.ndarray:
+    """group.rs:53-56: sum_i xs[i] Gs[i] over ark Projective (Jacobian) bases, (n, 12) u64 Montgomery."""
+    H.ensure_device()
+    x = H.fe_array(xs)
+    g = np.ascontiguousarray(np.asarray(Gs_projective, dtype=np.uint64).reshape(-1, 12))
+    out = np.zeros(8, dtype=np.uint64)
+    H.check(H.load().halo_point_dot_projective(_curve(curve), H.ptr(x), len(x), H.ptr(g), len(g), H.ptr(out)))
+    return out
+
+
 def construct_powers(z, n: int, field="fp") -> np.ndarray:
     """group.rs:58-66 ``construct_powers``: [1, z, z^2, ..., z^(n-1)]."""
     H.ensure_device()
@@ -98,6 +108,15 @@ class PublicParams:
                                         k, H.ptr(sha) if sha is not None else None, len(sha) if sha is not None else 0, n))
         if precompute_windows:
             H.check(L.halo_srs_precompute_windows(_curve(curve)))
+
+    @staticmethod
+    def sh(curve):
+        """(S, H) of the resident PublicParams (pp.rs:26-61), WrappedPoints."""
+        H.ensure_device()
+        S = np.zeros(8, dtype=np.uint64)
+        Hp = np.zeros(8, dtype=np.uint64)
+        H.check(H.load().halo_srs_sh(_curve(curve), H.ptr(S), H.ptr(Hp)))
+        return S, Hp
 
     @staticmethod
     def len(curve) -> int:

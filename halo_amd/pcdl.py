@@ -106,6 +106,78 @@ def ipa_rounds(cs, z, H_prime, challenge: Callable, inverse: Callable, curve="pa
     return Ls, Rs, U, c
 
 
+_SCALAR = {0: 0x40000000000000000000000000000000224698FC0994A8DD8C46EB2100000001,   # Pallas: Fp
+           1: 0x40000000000000000000000000000000224698FC094CF91B992D30ED00000001}   # Vesta: Fq
+
+
+def _ark_inverse(x: np.ndarray, cid: int) -> np.ndarray:
+    """x^-1 for an ark Montgomery scalar (x R -> x^-1 R), host big integers."""
+    r = _SCALAR[cid]
+    v = int(x[0]) | int(x[1]) << 64 | int(x[2]) << 128 | int(x[3]) << 192
+    inv = pow(v * pow(1 << 256, -1, r) % r, -1, r) * (1 << 256) % r
+    return np.array([(inv >> (64 * i)) & (2**64 - 1) for i in range(4)], dtype=np.uint64)
+
+
+def open_without_eval(p, C, d: int, z, v, w=None, transcript=None, q=None, w_bar=None, curve="pallas") -> dict:
+    """pcdl::open_without_eval (pcdl.rs:326-453) on the device, hiding branch included.
+
+    p: coefficients (ark scalars, <= d + 1 of them); C its commitment; z, v ark scalars; w the
+    commitment randomness (None: non-hiding).  ``transcript`` is the caller's Fiat-Shamir sponge with
+    the reference's interface (outer_sponge.rs: absorb_g(points), absorb_fr(scalars), challenge()),
+    over WrappedPoints / ark scalars; a fresh PCDL sponge, as pcdl.rs:336 creates.  q (d coefficients)
+    and w_bar are the random draws the reference takes from its rng (pcdl.rs:347,352).
+    Returns the EvalProof: dict(Ls, Rs, U, c, C_bar, w_prime)."""
+    H.ensure_device()
+    L = H.load()
+    cid = _curve(curve)
+    n = d + 1
+    assert n > 1
+    assert n & (n - 1) == 0, f"n ({n}) is not a power of two"
+    p = H.fe_array(p) if len(p) else np.zeros((0, 4), dtype=np.uint64)
+    zz, vv = H.fe_array(z, 1)[0], H.fe_array(v, 1)[0]
+    C = H.point_array(C).reshape(8)
+    C_bar = w_prime = None
+    if w is not None:
+        qq = H.fe_array(q)
+        wb = H.fe_array(w_bar, 1)
+        p_bar = np.zeros((n, 4), dtype=np.uint64)
+        C_bar = np.zeros(8, dtype=np.uint64)
+        H.check(L.halo_pcdl_hiding_blind(cid, H.ptr(qq), d, H.ptr(zz), H.ptr(wb), H.ptr(p_bar), H.ptr(C_bar)))
+        transcript.absorb_g([C, C_bar])
+        transcript.absorb_fr([zz, vv])
+        alpha = np.ascontiguousarray(transcript.challenge(), dtype=np.uint64)
+        p_prime = np.zeros((n, 4), dtype=np.uint64)
+        w_prime = np.zeros(4, dtype=np.uint64)
+        C_prime = np.zeros(8, dtype=np.uint64)
+        H.check(L.halo_pcdl_hiding_combine(cid, H.ptr(p) if len(p) else None, len(p), H.ptr(p_bar), d, H.ptr(alpha),
+                                           H.ptr(C), H.ptr(C_bar), H.ptr(H.fe_array(w, 1)), H.ptr(wb),
+                                           H.ptr(p_prime), H.ptr(w_prime), H.ptr(C_prime)))
+        p = p_prime
+    else:
+        C_prime = C
+    transcript.absorb_g([C_prime])
+    transcript.absorb_fr([zz, vv])
+    xi = np.ascontiguousarray(transcript.challenge(), dtype=np.uint64)
+    from .group import PublicParams
+    _, Hpt = PublicParams.sh(curve)
+    H_prime = np.zeros(8, dtype=np.uint64)
+    H.check(L.halo_curve_op(cid, 2, H.ptr(Hpt), None, H.ptr(xi), 1, H.ptr(H_prime)))
+    cs = np.zeros((n, 4), dtype=np.uint64)
+    cs[: len(p)] = p[:n]
+    ses = IpaSession(cs, zz, H_prime, curve)
+    Ls, Rs = [], []
+    for _ in range(n.bit_length() - 1):
+        Lp, Rp = ses.round_lr()
+        Ls.append(Lp)
+        Rs.append(Rp)
+        transcript.absorb_fr([xi])
+        transcript.absorb_g([Lp, Rp])
+        xi = np.ascontiguousarray(transcript.challenge(), dtype=np.uint64)
+        ses.fold(xi, _ark_inverse(xi, cid))
+    U, c = ses.end()
+    return {"Ls": Ls, "Rs": Rs, "U": U, "c": c, "C_bar": C_bar, "w_prime": w_prime}
+
+
 class HPoly:
     """pcdl.rs:184-229 HPoly: h(X) = prod_{i < lg n} (1 + xi_{lg n - i} X^(2^i)) from the round
     challenges xis (ark Montgomery scalars, xis[0] unused by h as in the reference)."""

@@ -64,6 +64,10 @@ int halo_device_count(void);
 const char* halo_last_error(void);
 /* ABI version (major * 100 + minor). */
 int halo_abi_version(void);
+/* Releases the library's streams, events and pending profiling events while the HIP runtime is
+ * alive (call before process exit; the Python mirror registers it with atexit).  Idempotent; the
+ * library remains usable afterwards. */
+int halo_shutdown(void);
 /* Blocks until all work queued by this library on `stream` is complete. */
 int halo_stream_sync(void* stream);
 
@@ -82,6 +86,8 @@ int halo_srs_load_bincode(halo_curve_t curve, const uint8_t* const* blocks, cons
                           const uint8_t* sh, size_t sh_len, size_t n);
 /* Current resident SRS length (0 if none). */
 int halo_srs_len(halo_curve_t curve, size_t* n);
+/* The resident PublicParams' (S, H) (crates/group/src/pp.rs:26-61) as WrappedPoints. */
+int halo_srs_sh(halo_curve_t curve, halo_wrapped_point_t* S, halo_wrapped_point_t* H);
 /* Synthetic SRS for sizes beyond the reference's N = 2^20 (crates/group/src/consts.rs:1):
  * G_j = k_j * (-1, 2) with k_j from halo_synth_scalar(seed, j), generated on the device.
  * S, H as in the reference are left unchanged if already uploaded. */
@@ -114,6 +120,25 @@ int halo_pedersen_commit(halo_curve_t curve, const halo_fe_t* w, const halo_wrap
  * `coeffs` has `len` entries (trailing zeros allowed). */
 int halo_pcdl_commit(halo_curve_t curve, const halo_fe_t* coeffs, size_t len, size_t d,
                      const halo_fe_t* w, halo_wrapped_point_t* out);
+/* The hiding branch of pcdl::open_without_eval (crates/accumulation/src/pcdl.rs:344-371), in the
+ * two steps around the caller's transcript challenge alpha = rho(C, C_bar, z, v):
+ *   blind:   p_bar = (X - z) q (q: d coefficients, the reference's random q of degree d - 1) and the
+ *            hiding commitment C_bar = pcdl::commit(p_bar, d, w_bar); p_bar_out (d + 1, optional).
+ *   combine: p' = p + alpha p_bar (d + 1 coefficients; p has len <= d + 1), w' = w + alpha w_bar,
+ *            C' = C + alpha C_bar - w' S, over the resident SRS's S.
+ * Same assertions as the reference (n = d + 1 > 1 a power of two, d <= D); needs (S, H) uploaded. */
+int halo_pcdl_hiding_blind(halo_curve_t curve, const halo_fe_t* q, size_t d, const halo_fe_t* z,
+                           const halo_fe_t* w_bar, halo_fe_t* p_bar_out, halo_wrapped_point_t* C_bar_out);
+int halo_pcdl_hiding_combine(halo_curve_t curve, const halo_fe_t* p, size_t len, const halo_fe_t* p_bar, size_t d,
+                             const halo_fe_t* alpha, const halo_wrapped_point_t* C, const halo_wrapped_point_t* C_bar,
+                             const halo_fe_t* w, const halo_fe_t* w_bar, halo_fe_t* p_prime_out,
+                             halo_fe_t* w_prime_out, halo_wrapped_point_t* C_prime_out);
+/* group::point_dot(xs, &[Projective]) (crates/group/src/group.rs:53-56, called at
+ * crates/accumulation/src/acc.rs:166): bases are ark Projective points -- Jacobian (X, Y, Z), each
+ * coordinate 4 x u64 Montgomery, 96 B per point, Z = 0 the identity -- normalised on the device
+ * (Projective::normalize_batch), then the MSM; length = min(n_bases, n_scalars). */
+int halo_point_dot_projective(halo_curve_t curve, const halo_fe_t* scalars, size_t n_scalars,
+                              const uint64_t (*bases)[12], size_t n_bases, halo_wrapped_point_t* out);
 /* Device-pointer MSM: d_bases (n WrappedPoints, or NULL to use the resident SRS prefix) and
  * d_scalars (n halo_fe_t) in HBM; result written to host `out`.  Synchronous on `stream`. */
 int halo_msm_dev(halo_curve_t curve, const void* d_bases, const void* d_scalars, size_t n,

@@ -79,3 +79,38 @@ def decider_commit_matches(curve: str, U, xis, gs, msm) -> bool:
     sc = np.array([P.int_to_limbs(P.to_mont(x, m)) for x in hc], dtype=np.uint64).reshape(-1, 4)
     got = msm(curve, np.ascontiguousarray(gs[: len(hc)]), np.ascontiguousarray(sc))
     return [int(x) for x in got] == [int(x) for x in U]
+
+
+def succinct_check_transcript(curve: str, C, d: int, z: int, v: int, Ls, Rs, U, c: int, H, S=None, C_bar=None,
+                              w_prime=None):
+    """pcdl::succinct_check exactly as pcdl.rs:483-554: the challenges are re-derived from the
+    Poseidon PCDL transcript (oracle/poseidon.py), alpha included in the hiding case.  Returns the
+    xis (for the decider)."""
+    import poseidon
+    cv = P.CURVES[curve]
+    m = cv.scalar
+    n = d + 1
+    lg_n = n.bit_length() - 1
+    t = poseidon.Sponge(curve, poseidon.PCDL)
+    Cp = _pt(cv, C)
+    alpha = None
+    if C_bar is not None:
+        t.absorb_g([Cp, _pt(cv, C_bar)])
+        t.absorb_fr([z, v])
+        alpha = t.challenge()
+    t.absorb_g([_cprime(cv, Cp, C_bar, alpha, w_prime, S)])
+    t.absorb_fr([z, v])
+    xis = [t.challenge()]
+    for i in range(lg_n):
+        t.absorb_fr([xis[i]])
+        t.absorb_g([_pt(cv, Ls[i]), _pt(cv, Rs[i])])
+        xis.append(t.challenge())
+    succinct_check(curve, C, d, z, v, Ls, Rs, U, c, xis, H, S=S, C_bar=C_bar, w_prime=w_prime, alpha=alpha)
+    return xis
+
+
+def _cprime(cv, Cp, C_bar, alpha, w_prime, S):
+    if C_bar is None:
+        return Cp
+    return P.add(cv, P.add(cv, Cp, P.mul_fast(cv, alpha, _pt(cv, C_bar))),
+                 P.neg(cv, P.mul_fast(cv, w_prime % cv.scalar, _pt(cv, S))))

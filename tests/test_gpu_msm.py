@@ -377,3 +377,29 @@ def test_msm_batch_dev_one_msm_path(hal, corc, cname, cid):
     for i, m in enumerate(lens):
         exp = corc.msm(cname, g[:m], scs[i]) if m else np.zeros(8, dtype=np.uint64)
         assert np.array_equal(got[i], exp), (i, m)
+
+
+@pytest.mark.parametrize("cname,cid", CURVES)
+def test_point_dot_projective(hal, corc, cname, cid):
+    """group.rs:53-56 point_dot over ark Projective bases: random Jacobian representatives
+    (lambda^2 x, lambda^3 y, lambda) of the SRS points, one identity (Z = 0), against the oracle MSM
+    of the affine points."""
+    c = P.CURVES[cname]
+    q = c.base
+    n = 3000
+    g = corc.srs_generate(cname, n)
+    rng = random.Random(7)
+    jac = np.zeros((n, 12), dtype=np.uint64)
+    aff = g.copy()
+    for i in range(n):
+        pt = P.wrapped_to_point(c, [int(x) for x in g[i]])
+        if i == 17:
+            jac[i] = P.int_to_limbs(P.to_mont(1, q)) + P.int_to_limbs(P.to_mont(1, q)) + [0, 0, 0, 0]
+            aff[i] = 0
+            continue
+        lam = rng.randrange(1, q)
+        X, Y = pt[0] * lam * lam % q, pt[1] * pow(lam, 3, q) % q
+        jac[i] = P.int_to_limbs(P.to_mont(X, q)) + P.int_to_limbs(P.to_mont(Y, q)) + P.int_to_limbs(P.to_mont(lam, q))
+    sc = rand_sc(n, 77)
+    assert np.array_equal(group.point_dot(sc, jac, cname), corc.msm(cname, aff, sc))
+    assert np.array_equal(group.point_dot(sc[:100], jac, cname), corc.msm(cname, aff[:100], sc[:100]))

@@ -1,0 +1,72 @@
+"""GPU parity: pcdl::open_without_eval driven by the reference's own transcript.
+
+The device round loop (halo_amd.pcdl.open_without_eval: halo_pcdl_hiding_blind / _combine, the IPA
+session) is driven by the CPU restatement of the Poseidon PCDL sponge (oracle/poseidon.py, pinned
+to the reference's Kimchi / Mina vectors in tests/test_oracle.py), so every challenge -- alpha,
+xi_0 and the per-round xi -- is derived from the device's own C_bar, L and R exactly as
+pcdl.rs:326-453 derives them.  The resulting EvalProof (Ls, Rs, U, c, C_bar, w') must equal the
+committed fixture of tests/golden/make_transcript.py bit for bit (plain and hiding openings, n =
+16..1024, Pallas and Vesta, reference-recipe SRS and the reference's (S, H))."""
+import os
+
+import numpy as np
+import pytest
+
+import pasta as P
+import poseidon
+from halo_amd import group, pcdl
+
+pytestmark = pytest.mark.gpu
+G = np.load(os.path.join(os.path.dirname(__file__), "golden", "transcript.npz"))
+CASES = sorted({k[:-2] for k in G.files if k.startswith("open_") and k.endswith("_p")})
+
+
+class SpongeAdapter:
+    """The oracle sponge behind the reference's Sponge interface, over WrappedPoints / ark scalars."""
+
+    def __init__(self, cname):
+        self.c = P.CURVES[cname]
+        self.s = poseidon.Sponge(cname, poseidon.PCDL)
+
+    def absorb_g(self, pts):
+        self.s.absorb_g([P.wrapped_to_point(self.c, [int(x) for x in q]) for q in pts])
+
+    def absorb_fr(self, xs):
+        self.s.absorb_fr([P.from_mont(P.limbs_to_int(x), self.c.scalar) for x in xs])
+
+    def challenge(self):
+        return np.array(P.int_to_limbs(P.to_mont(self.s.challenge(), self.c.scalar)), dtype=np.uint64)
+
+
+@pytest.mark.parametrize("key", CASES)
+def test_open_without_eval_matches_transcript_fixture(hal, golden, corc, key):
+    cname = key.split("_")[1]
+    n = int(key.split("_")[2][1:])
+    hiding = key.endswith("hiding")
+    S, Hh = golden[f"ref_sh_{cname}"]
+    group.PublicParams.upload(cname, corc.srs_generate(cname, n), S, Hh, precompute_windows=True)
+    Sd, Hd = group.PublicParams.sh(cname)
+    assert np.array_equal(Sd, S) and np.array_equal(Hd, Hh)
+    z, v = G[key + "_zv"]
+    w = q = w_bar = None
+    if hiding:
+        w, w_bar = G[key + "_w"]
+        q = G[key + "_q"]
+    pi = pcdl.open_without_eval(G[key + "_p"], G[key + "_C"][0], n - 1, z, v, w=w, transcript=SpongeAdapter(cname),
+                                q=q, w_bar=w_bar, curve=cname)
+    assert np.array_equal(np.stack(pi["Ls"]), G[key + "_Ls"]), key
+    assert np.array_equal(np.stack(pi["Rs"]), G[key + "_Rs"]), key
+    assert np.array_equal(pi["U"], G[key + "_U"][0]) and np.array_equal(pi["c"], G[key + "_c"][0]), key
+    if hiding:
+        assert np.array_equal(pi["C_bar"], G[key + "_Cbar"][0]), key
+        assert np.array_equal(pi["w_prime"], G[key + "_wprime_alpha"][0]), key
+
+
+def test_hiding_assertions(hal, golden, corc):
+    S, Hh = golden["ref_sh_pallas"]
+    group.PublicParams.upload("pallas", corc.srs_generate("pallas", 64), S, Hh, precompute_windows=False)
+    q = np.zeros((10, 4), dtype=np.uint64)
+    one = np.array([1, 0, 0, 0], dtype=np.uint64)
+    with pytest.raises(AssertionError, match=r"n \(11\) is not a power of two"):
+        pcdl.open_without_eval(q, np.zeros(8, dtype=np.uint64), 10, one, one, w=one, transcript=SpongeAdapter("pallas"),
+                               q=q, w_bar=one)

@@ -246,3 +246,52 @@ def test_known_log_msm_identity(corc, cname):
     rng = np.random.default_rng(1)
     sc = rng.integers(0, 2**62, size=(n, 4), dtype=np.uint64)
     assert np.array_equal(corc.known_log_msm(cname, sc, k), corc.msm(cname, bases, sc))
+
+
+def test_poseidon_sponge_reference_vectors():
+    """oracle/poseidon.py against the reference's own Poseidon vectors: the six Kimchi vectors
+    (kimchi-vecs.json, inner_sponge.rs:315-321, Pallas sponge over Fq) and the two Mina vectors
+    (inner_sponge.rs:323-368: Vesta sponge over Fp, Pallas sponge over Fq)."""
+    import os
+
+    import poseidon
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "transcript.npz"))
+    i = 0
+    while f"kimchi_{i}_in" in g:
+        s = poseidon.InnerSponge("fq")
+        s.absorb([P.limbs_to_int(x) for x in g[f"kimchi_{i}_in"]])
+        assert s.squeeze() == P.limbs_to_int(g[f"kimchi_{i}_out"]), i
+        i += 1
+    assert i == 6
+    for tag, field in (("mina_fq", "fp"), ("mina_fp", "fq")):
+        s = poseidon.InnerSponge(field)
+        s.absorb([P.limbs_to_int(x) for x in g[f"{tag}_in"]])
+        assert s.squeeze() == P.limbs_to_int(g[f"{tag}_out"]), tag
+
+
+def test_transcript_pcdl_open_fixtures_verify(golden, corc):
+    """The committed pcdl::open fixtures (tests/golden/make_transcript.py: oracle/pcdl_ref.py with the
+    Poseidon transcript) pass the transcript-driven succinct_check (pcdl.rs:483-554, challenges
+    re-derived) and the decider U == commit(h) (pcdl.rs:579-581), hiding and plain."""
+    import os
+
+    import pcdl_check
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "transcript.npz"))
+    keys = sorted({k[:-2] for k in g.files if k.startswith("open_") and k.endswith("_p")})
+    assert len(keys) == 6
+    for key in keys:
+        cname = key.split("_")[1]
+        c = P.CURVES[cname]
+        n = int(key.split("_")[2][1:])
+        r = c.scalar
+        S, Hh = golden[f"ref_sh_{cname}"]
+        z, v = unfe(g[key + "_zv"], r)
+        hiding = key.endswith("hiding")
+        wp = unfe(g[key + "_wprime_alpha"], r)[0] if hiding else None
+        xis = pcdl_check.succinct_check_transcript(
+            cname, g[key + "_C"][0], n - 1, z, v, list(g[key + "_Ls"]), list(g[key + "_Rs"]), g[key + "_U"][0],
+            unfe(g[key + "_c"], r)[0], Hh, S=S, C_bar=g[key + "_Cbar"][0] if hiding else None, w_prime=wp)
+        assert xis == unfe(g[key + "_xis"], r), key
+        if n <= 256:
+            srs = corc.srs_generate(cname, n)
+            assert pcdl_check.decider_commit_matches(cname, g[key + "_U"][0], xis, srs, corc.msm), key
