@@ -53,6 +53,10 @@ def parse():
     ap.add_argument("--dist-ipa", type=int, default=1, help="N > 1: the sharded 2^logn opening (extra.dist_ipa)")
     ap.add_argument("--prove", type=int, default=20, help="log2 n of the naive_prover pipeline (extra.prove; 0 = off)")
     ap.add_argument("--prove-cpu", type=int, default=16, help="log2 n of the prover's CPU-baseline comparison")
+    ap.add_argument("--varbase", type=int, default=1, help="variable-base MSM at 2^logn (extra.msm_varbase)")
+    ap.add_argument("--commit-batch", type=int, default=1, help="16 x 2^16 batched commitments (extra.commit_batch)")
+    ap.add_argument("--pcdl", default="2,4,6,8,10,12,14,16,18,20",
+                    help="log2 n of the pcdl_commit / pcdl_open sweeps with w = Some (extra.pcdl; '' = off)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal only: every rank on cuda:0 over gloo (multi-rank runs on a one-GPU box)")
     return ap.parse_args()
@@ -158,9 +162,10 @@ def main():
             for j in range(warmup, total_steps):
                 if j % nbatch == i:
                     sync_ok &= bool(np.array_equal(d_out[j].cpu().numpy().view(np.uint64), out))
-        return elapsed, acc_avg_ms, sync_ok, lat, scalars[0]
+        first = d_out[0].cpu().numpy().view(np.uint64).copy() if warmup > 0 else None
+        return elapsed, acc_avg_ms, sync_ok, lat, scalars[0], (seed, first)
 
-    elapsed, acc_avg_ms, sync_ok, lat, scalars0 = measure_msm(args.logn, args.steps, args.warmup)
+    elapsed, acc_avg_ms, sync_ok, lat, scalars0, check0 = measure_msm(args.logn, args.steps, args.warmup)
     window_bits = L.halo_srs_window_bits(curve)
 
     # ---- IPA opening (pcdl::open_without_eval round loop, pcdl.rs:392-438) at 2^logn:
@@ -333,11 +338,139 @@ def main():
 
     hbm_copy = measure_copy()
 
+    # ---- variable-base MSM (group.rs:48-50 point_dot_affine over caller bases: GLV digits, no
+    # window-shifted copies), pipelined like the headline; bases = the synthetic SRS read back
+    def measure_varbase(logn, steps=10, warmup=2):
+        n_ = 1 << logn
+        seed = 0x56424153
+        H.check(L.halo_srs_synthesize(curve, n_, seed))
+        bases = torch.empty((n_, 8), dtype=torch.int64, device="cuda")
+        host = np.zeros((n_, 8), dtype=np.uint64)
+        H.check(L.halo_srs_read(curve, 0, n_, H.ptr(host)))
+        bases.copy_(torch.from_numpy(host.view(np.int64)))
+        sc = torch.randint(-(2**63), 2**63 - 1, (4, n_, 4), dtype=torch.int64, device="cuda", generator=gen)
+        sc[..., 3] &= 0x0FFFFFFFFFFFFFFF
+        outs = torch.zeros((warmup + steps, 8), dtype=torch.int64, device="cuda")
+
+        def run(first, k):
+            for i in range(first, first + k):
+                H.check(L.halo_msm_dev_async(curve, ctypes.c_void_p(bases.data_ptr()),
+                                             ctypes.c_void_p(sc[i % 4].data_ptr()), n_,
+                                             ctypes.c_void_p(outs[i].data_ptr()), sp))
+            H.check(L.halo_msm_join(sp))
+
+        run(0, warmup)
+        torch.cuda.synchronize()
+        L.halo_profile_reset()
+        L.halo_profile_enable(1)
+        a0 = time.perf_counter()
+        run(warmup, steps)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - a0
+        L.halo_profile_enable(0)
+        nl = ctypes.c_size_t(0)
+        ams = ctypes.c_double(0)
+        H.check(L.halo_profile_read(b"msm_acc", ctypes.byref(nl), ctypes.byref(ams)))
+        chk = (sc[0].cpu().numpy().view(np.uint64).copy(), (seed, outs[0].cpu().numpy().view(np.uint64).copy()))
+        del bases, sc, outs
+        return {
+            "workload": f"variable-base MSM 2^{logn} over caller-supplied bases (point_dot_affine, group.rs:48-50): "
+                        "GLV digits (2 x ceil(129/c) per scalar), no precomputation, pipelined",
+            "points_per_s": n_ * steps / dt,
+            "ms_per_msm": dt * 1e3 / steps,
+            "k_acc_ms": ams.value / max(1, nl.value),
+        }, chk
+
+    varbase, varbase_chk = measure_varbase(args.logn) if args.varbase else (None, None)
+
+    # ---- batched commitments (halo_msm_batch_dev; protocol.rs:114,263: 16 commits per round)
+    def measure_commit_batch(logn, k=16, reps=5):
+        n_ = 1 << logn
+        H.check(L.halo_srs_synthesize(curve, n_, 0x42415443))
+        H.check(L.halo_srs_precompute_windows(curve))
+        sc = torch.randint(-(2**63), 2**63 - 1, (k, n_, 4), dtype=torch.int64, device="cuda", generator=gen)
+        sc[..., 3] &= 0x0FFFFFFFFFFFFFFF
+        ptrs = (ctypes.c_void_p * k)(*[sc[i].data_ptr() for i in range(k)])
+        lens = (ctypes.c_size_t * k)(*([n_] * k))
+        out = torch.zeros((k, 8), dtype=torch.int64, device="cuda")
+        out_ref = torch.zeros((k, 8), dtype=torch.int64, device="cuda")
+        for i in range(k):  # per-MSM pipelined path, for the equality check
+            H.check(L.halo_msm_dev_async(curve, None, ctypes.c_void_p(sc[i].data_ptr()), n_,
+                                         ctypes.c_void_p(out_ref[i].data_ptr()), sp))
+        H.check(L.halo_msm_join(sp))
+        H.check(L.halo_msm_batch_dev(curve, ptrs, lens, k, ctypes.c_void_p(out.data_ptr()), sp))
+        H.check(L.halo_msm_join(sp))
+        torch.cuda.synchronize()
+        a0 = time.perf_counter()
+        for _ in range(reps):
+            H.check(L.halo_msm_batch_dev(curve, ptrs, lens, k, ctypes.c_void_p(out.data_ptr()), sp))
+            H.check(L.halo_msm_join(sp))
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - a0) * 1e3 / reps
+        same = bool(torch.equal(out, out_ref))
+        del sc
+        return {"workload": f"{k} commitments of 2^{logn} coefficients in one halo_msm_batch_dev call "
+                            "(one MSM, (polynomial, bucket) keys)", "ms_per_batch": ms,
+                "points_per_s": k * n_ / (ms * 1e-3), "equals_per_msm_path": same}
+
+    commit_batch = measure_commit_batch(16) if args.commit_batch else None
+
+    # ---- the reference's own criterion shapes (crates/accumulation/benches/pcdl.rs:35-79): pcdl_commit
+    # and pcdl_open with w = Some over n = 2^2..2^20, Pallas; host buffers in and out as the Rust API
+    # has them; the open includes v = p(z), the hiding branch and the lg n rounds with a stand-in
+    # transcript (SHA-256; the Poseidon sponge is host logic, ~us per absorb)
+    def measure_pcdl(lgs):
+        from halo_amd import pcdl as P_
+        top = max(lgs)
+        N = 1 << top
+        H.check(L.halo_srs_synthesize(curve, N, 0x50434C44))
+        G = np.zeros((N, 8), dtype=np.uint64)
+        H.check(L.halo_srs_read(curve, 0, N, H.ptr(G)))
+        H.check(L.halo_srs_upload(curve, H.ptr(G), N, H.ptr(G[0]), H.ptr(G[1])))  # S = G_0, H = G_1 (synthetic)
+        H.check(L.halo_srs_precompute_windows(curve))
+        rng = np.random.default_rng(3)
+
+        def fes(k):
+            a = rng.integers(0, 2**63, size=(k, 4), dtype=np.uint64)
+            a[:, 3] &= np.uint64(0x0FFFFFFFFFFFFFFF)
+            return np.ascontiguousarray(a)
+
+        res = {}
+        inputs = {}
+        for lg in lgs:
+            n_ = 1 << lg
+            p_, w_, z_ = fes(n_), fes(1)[0], fes(1)[0]
+            q_, wb_ = fes(n_ - 1), fes(1)[0]
+            C = P_.commit(p_, n_ - 1, w_, args.curve)
+            reps = 10 if lg <= 14 else 3
+            a0 = time.perf_counter()
+            for _ in range(reps):
+                C = P_.commit(p_, n_ - 1, w_, args.curve)
+            t_commit = (time.perf_counter() - a0) / reps
+            P_.open(p_, C, n_ - 1, z_, w=w_, transcript=P_.StandInTranscript(args.curve), q=q_, w_bar=wb_,
+                    curve=args.curve)
+            reps = 5 if lg <= 14 else 2
+            a0 = time.perf_counter()
+            for _ in range(reps):
+                pi = P_.open(p_, C, n_ - 1, z_, w=w_, transcript=P_.StandInTranscript(args.curve), q=q_, w_bar=wb_,
+                             curve=args.curve)
+            t_open = (time.perf_counter() - a0) / reps
+            res[f"2^{lg}"] = {"commit_ms": t_commit * 1e3, "open_ms": t_open * 1e3}
+            inputs[lg] = (p_, w_, z_, q_, wb_, C, pi)
+        return res, inputs, G  # G: the sweep's SRS (S = G_0, H = G_1), kept for the CPU leg
+
+    pcdl_lgs = [int(v) for v in args.pcdl.split(",") if v.strip()] if world == 1 else []
+    pcdl_sweep, pcdl_inputs, pcdl_sh = measure_pcdl(pcdl_lgs) if pcdl_lgs else (None, None, None)
+
     ntt_main = measure_ntt(args.ntt_logn)
     ntt_main["workload"] += " (BASELINE.json configs[2])"
     sizes = {}
+    size_checks = {}  # 2^lg MSM: (scalars[0] on the host, SRS seed, result), verified in the CPU leg
     for lg in [int(v) for v in args.sizes.split(",") if v.strip()]:
-        e, a_ms, ok, lt, _ = measure_msm(lg, 4, 2, check_sync=False)
+        e, a_ms, ok, lt, sc0, chk = measure_msm(lg, 4, 2, check_sync=False)
+        if world == 1 and not args.no_cpu:
+            size_checks[lg] = (sc0.cpu().numpy().view(np.uint64).copy(), chk)
+        del sc0
         sizes[f"msm_2^{lg}"] = {
             "points_per_s": (1 << lg) * world * 4 / e,
             "ms_per_msm": e * 1e3 / 4,
@@ -350,7 +483,7 @@ def main():
         if world > 1 and (world & (world - 1)) == 0:
             # BASELINE configs[4]: one 2^lg-point MSM partitioned across the ranks (strong scaling)
             lr = lg - (world.bit_length() - 1)
-            e, a_ms, ok, lt, _ = measure_msm(lr, 4, 2, check_sync=False)
+            e, a_ms, ok, lt, _, _ = measure_msm(lr, 4, 2, check_sync=False)
             sizes[f"msm_2^{lg}_partitioned"] = {
                 "points_per_s": (1 << lg) * 4 / e,
                 "ms_per_msm": e * 1e3 / 4,
@@ -464,21 +597,41 @@ def main():
     acc_bytes = MSM_BYTES_PER_POINT * n
     achieved = acc_bytes / (acc_avg_ms * 1e-3) / 1e9 if acc_avg_ms > 0 else 0.0
 
+    # PMC traffic of k_acc from the committed counter passes, used only when they were measured on
+    # this very library build (library_sha256 stamp); otherwise null with the reason
     traffic = None
+    traffic_note = "no profiles/pmc_summary.json"
     pmc_path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     if os.path.exists(pmc_path):
         try:
+            import hashlib
             pmc = json.load(open(pmc_path))
-            traffic = pmc.get("msm_acc", {}).get("hbm_bytes_per_launch")
+            lib_sha = hashlib.sha256(open(H.LIB_PATH, "rb").read()).hexdigest()
+            if pmc.get("library_sha256") == lib_sha:
+                traffic = pmc.get("msm_acc", {}).get("hbm_bytes_per_launch")
+                traffic_note = "rocprofv3 FETCH_SIZE + WRITE_SIZE (separate passes) of this library build, " \
+                               "profiles/pmc_summary.json"
+            else:
+                traffic_note = "profiles/pmc_summary.json was measured on another library build: not used"
         except (OSError, ValueError):
             traffic = None
 
     cpu = None
     cpu_ntt = cpu_fold = None
+    verified = {}
     if not args.no_cpu and world == 1:
         cpu = cpu_baseline(L, H, curve, n, scalars0, out_check=True, budget_s=args.cpu_seconds)
         cpu_ntt = cpu_ntt_baseline(L, H, args.ntt_logn, sp, ntt_main)
         cpu_fold = cpu_fold_baseline(L, H, curve, 13, ipa)
+        # known-log identity checks of the measured MSMs (oracle dot product + generator multiple)
+        verified["msm_2^%d" % args.logn] = cpu_known_log_check(args.curve, scalars0.cpu().numpy().view(np.uint64),
+                                                               check0)
+        for lg, (sc_h, chk) in size_checks.items():
+            sizes[f"msm_2^{lg}"]["verified"] = cpu_known_log_check(args.curve, sc_h, chk)
+        if varbase_chk is not None:
+            varbase["verified"] = cpu_known_log_check(args.curve, varbase_chk[0], varbase_chk[1])
+        if pcdl_sweep:
+            cpu_pcdl_baseline(args.curve, pcdl_sweep, pcdl_inputs, pcdl_sh, L, H, curve)
 
     # after the MSM CPU leg (which reads the MSM's resident SRS back)
     prove = None
@@ -491,6 +644,8 @@ def main():
             "n": 1 << args.prove,
             "ms": {k: v * 1e3 for k, v in main_out["times"].items()},
         }
+        if not args.no_cpu:
+            prove["verified"] = cpu_prove_check(L, H, curve, args.curve, 1 << args.prove, main_out)
         if not args.no_cpu and args.prove_cpu:
             small = measure_prove(args.prove_cpu)
             prove["at_cpu_size"] = {"n": 1 << args.prove_cpu, "gpu_ms": {k: v * 1e3 for k, v in small["times"].items()}}
@@ -517,6 +672,8 @@ def main():
             "points_per_rank": n,
             "window_bits": window_bits,
             "parallelism": f"point-partition x{world}, RCCL all-gather of partial sums",
+            "world_size_reported": dist.get_world_size() if world > 1 else 1,
+            "backend": dist.get_backend() if world > 1 else None,
             "pipelining": "steps enqueued back to back: step k's reduction tail overlaps step k+1's accumulation",
         },
         "roofline": {
@@ -527,6 +684,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
+            "traffic_note": traffic_note,
             "algorithmic_bytes_per_launch": acc_bytes,
             "avg_launch_ms": acc_avg_ms,
             "note": "the MSM is bound by 255-bit modular multiplication on the VALU, not HBM (SURVEY §7 hard part 1)",
@@ -555,6 +713,10 @@ def main():
             "cpu_ntt": cpu_ntt,
             "prove": prove,
             "cpu_ipa_fold": cpu_fold,
+            "msm_varbase": varbase,
+            "commit_batch": commit_batch,
+            "pcdl": pcdl_sweep,
+            "verified": verified,
         },
     }
     print(json.dumps(line))
@@ -601,6 +763,70 @@ def cpu_baseline(L, H, curve, n, scalars_dev, out_check, budget_s):
                   f"ark-ec 0.5 msm_bigint_wnaf, c={corc.msm_window_size(n)}, OpenMP over windows",
         "gpu_matches_cpu": bool(np.array_equal(cpu_out, gpu_out)) if out_check else None,
     }
+
+
+def cpu_known_log_check(cname, scalars_host, chk):
+    """The MSM result against (sum_j s_j k_j) G, k_j the synthetic SRS's discrete logs (oracle)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import corc  # noqa: E402  (oracle: the checker, CPU leg only)
+    seed, got = chk
+    if got is None:
+        return None
+    n = len(scalars_host)
+    k = corc.synth_scalars(seed, n)
+    return bool(np.array_equal(corc.known_log_msm(cname, np.ascontiguousarray(scalars_host), k), got))
+
+
+def cpu_prove_check(L, H, curve, cname, n, out):
+    """The three openings of the measured prove pass the oracle's succinct_check (pcdl.rs:483-554,
+    with the prover's challenges) and the decider U == commit(h) (pcdl.rs:579-581, oracle MSM)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import corc  # noqa: E402
+    import pcdl_check  # noqa: E402
+    srs = np.zeros((n, 8), dtype=np.uint64)
+    H.check(L.halo_srs_read(curve, 0, n, H.ptr(srs)))
+    res = {}
+    for key in ("q_r", "q_r_omega", "acc"):
+        q = out[key]
+        try:
+            pcdl_check.succinct_check(cname, q["C"], n - 1, q["z"], q["v"], q["Ls"], q["Rs"], q["U"], q["c"], q["xis"],
+                                      srs[1])
+            ok = True
+        except AssertionError:
+            ok = False
+        res[key] = ok and pcdl_check.decider_commit_matches(cname, q["U"], q["xis"], srs, corc.msm)
+    return res
+
+
+def cpu_pcdl_baseline(cname, sweep, inputs, G, L, H, curve):
+    """pcdl_commit / pcdl_open on the host cores at the small sizes (oracle: C MSM + the Python
+    restatement of open_without_eval with the Poseidon transcript), and each size's GPU commitment
+    checked against the oracle's (every size) -- added in place to `sweep`."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pasta as P  # noqa: E402
+    import pcdl_ref  # noqa: E402
+    c = P.CURVES[cname]
+    r = c.scalar
+    S, Hp = (P.wrapped_to_point(c, [int(x) for x in q]) for q in (G[0], G[1]))
+    toint = lambda a: P.from_mont(P.limbs_to_int(a), r)  # noqa: E731
+    for lg, (p_, w_, z_, q_, wb_, C, pi) in inputs.items():
+        e = sweep[f"2^{lg}"]
+        pc = [toint(x) for x in p_]
+        if lg <= 16:
+            a0 = time.perf_counter()
+            Cc = pcdl_ref.commit(cname, G, pc, toint(w_), S)
+            e["cpu_commit_ms"] = (time.perf_counter() - a0) * 1e3
+            e["commit_matches_cpu"] = bool(np.array_equal(np.array(P.point_to_wrapped(c, Cc), dtype=np.uint64), C))
+        if lg <= 10:
+            z = toint(z_)
+            a0 = time.perf_counter()
+            v = P.horner(pc, z, r)
+            ref = pcdl_ref.open_without_eval(cname, pc, Cc, (1 << lg) - 1, z, v, G, S, Hp, w=toint(w_),
+                                             q=[toint(x) for x in q_], w_bar=toint(wb_))
+            e["cpu_open_ms"] = (time.perf_counter() - a0) * 1e3
+            e["cpu_open_note"] = "Python restatement with C MSM/fold and the Poseidon sponge (not arkworks)"
+            del ref
+    return sweep
 
 
 def _cpu_threads():

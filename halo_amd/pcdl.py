@@ -178,6 +178,54 @@ def open_without_eval(p, C, d: int, z, v, w=None, transcript=None, q=None, w_bar
     return {"Ls": Ls, "Rs": Rs, "U": U, "c": c, "C_bar": C_bar, "w_prime": w_prime}
 
 
+class StandInTranscript:
+    """A stand-in for the reference's Poseidon PCDL sponge (outer_sponge.rs) with its interface, for
+    timing runs only: challenges are SHA-256 of everything absorbed, reduced mod r.  (The Fiat-Shamir
+    transcript is host logic outside the device path; tests drive the device with the restated
+    Poseidon sponge, tests/test_gpu_transcript.py.)"""
+
+    def __init__(self, curve="pallas"):
+        import hashlib
+        self._h = hashlib.sha256(b"PCDL")
+        self._r = _SCALAR[_curve(curve)]
+
+    def absorb_g(self, pts):
+        for q in pts:
+            self._h.update(np.ascontiguousarray(q, dtype=np.uint64).tobytes())
+
+    def absorb_fr(self, xs):
+        for x in xs:
+            self._h.update(np.ascontiguousarray(x, dtype=np.uint64).tobytes())
+
+    def challenge(self) -> np.ndarray:
+        d = self._h.digest()
+        self._h.update(d)
+        v = (int.from_bytes(d, "little") % self._r) or 1
+        m = v * (1 << 256) % self._r
+        return np.array([(m >> (64 * i)) & (2**64 - 1) for i in range(4)], dtype=np.uint64)
+
+
+def evaluate(p, z, curve="pallas") -> np.ndarray:
+    """DensePolynomial::evaluate (pcdl.rs:49,471) on the device (halo_poly_eval_batch)."""
+    import ctypes as _ct
+    H.ensure_device()
+    c = H.fe_array(p)
+    out = np.zeros((1, 4), dtype=np.uint64)
+    ptrs = (_ct.c_void_p * 1)(c.ctypes.data)
+    lens = (_ct.c_size_t * 1)(len(c))
+    field = H.FP if _curve(curve) == 0 else H.FQ
+    H.check(H.load().halo_poly_eval_batch(field, ptrs, lens, 1, H.ptr(H.fe_array(z, 1)), H.ptr(out)))
+    return out[0]
+
+
+def open(p, C, d: int, z, w=None, transcript=None, q=None, w_bar=None, curve="pallas") -> dict:  # noqa: A001
+    """pcdl::open (pcdl.rs:463-473): v = p(z), then open_without_eval."""
+    v = evaluate(p, z, curve)
+    pi = open_without_eval(p, C, d, z, v, w=w, transcript=transcript, q=q, w_bar=w_bar, curve=curve)
+    pi["v"] = v
+    return pi
+
+
 class HPoly:
     """pcdl.rs:184-229 HPoly: h(X) = prod_{i < lg n} (1 + xi_{lg n - i} X^(2^i)) from the round
     challenges xis (ark Montgomery scalars, xis[0] unused by h as in the reference)."""

@@ -27,8 +27,13 @@ def main():
     fdir, wdir, out, src = sys.argv[1:5]
     f = summarise(load(fdir))
     w = summarise(load(wdir))
+    import hashlib
+    import os
+    lib = os.environ.get("HALO_LIB") or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                     "halo_amd", "lib", "libhalo_gpu.so")
     res = {
         "source": src,
+        "library_sha256": hashlib.sha256(open(lib, "rb").read()).hexdigest(),
         "units": "bytes per dispatch (FETCH_SIZE / WRITE_SIZE are KiB: x1024)",
         "correction": "gfx950 FETCH_SIZE = 1/2 of wide coalesced streaming reads: x2 for the streaming kernels; "
                       "k_acc (random 64-B point gathers) reported raw",
