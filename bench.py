@@ -462,6 +462,64 @@ def main():
     pcdl_lgs = [int(v) for v in args.pcdl.split(",") if v.strip()] if world == 1 else []
     pcdl_sweep, pcdl_inputs, pcdl_sh = measure_pcdl(pcdl_lgs) if pcdl_lgs else (None, None, None)
 
+    # ---- BASELINE configs[4] as named: one 2^lg-point MSM window-partitioned across the ranks
+    # (halo_amd.dist.window_range): every rank the same SRS and scalars (broadcast from rank 0 over
+    # RCCL), rank r the windows of its range, partials all-gathered + summed on the device
+    def measure_window_partition(lg, reps=4):
+        from halo_amd.dist import window_range
+        n_ = 1 << lg
+        H.check(L.halo_srs_synthesize(curve, n_, 0x57494E44))  # same seed on every rank
+        H.check(L.halo_srs_precompute_windows(curve))
+        W = L.halo_srs_windows(curve)
+        lo, hi = window_range(W, rank, world)
+        sc = torch.empty((n_, 4), dtype=torch.int64, device="cuda")
+        if rank == 0:
+            sc.copy_(torch.randint(-(2**63), 2**63 - 1, (n_, 4), dtype=torch.int64, device="cuda", generator=gen))
+            sc[:, 3] &= 0x0FFFFFFFFFFFFFFF
+        part = torch.zeros((1, 8), dtype=torch.int64, device="cuda")
+        parts = [torch.empty_like(part) for _ in range(world)]
+        res = torch.zeros(8, dtype=torch.int64, device="cuda")
+
+        def one(bcast):
+            if bcast:
+                dist.broadcast(sc, 0)
+            H.check(L.halo_msm_srs_windows_dev(curve, ctypes.c_void_p(sc.data_ptr()), n_, lo, hi,
+                                               ctypes.c_void_p(part.data_ptr()), sp))
+            H.check(L.halo_msm_join(sp))
+            dist.all_gather(parts, part)
+            st = torch.cat(parts).contiguous()
+            H.check(L.halo_point_sum_dev(curve, ctypes.c_void_p(st.data_ptr()), world, 64,
+                                         ctypes.c_void_p(res.data_ptr()), sp))
+
+        out = {}
+        for bcast in (True, False):
+            one(True)
+            torch.cuda.synchronize()
+            dist.barrier()
+            a0 = time.perf_counter()
+            for _ in range(reps):
+                one(bcast)
+            torch.cuda.synchronize()
+            dist.barrier()
+            tt = torch.tensor([time.perf_counter() - a0], dtype=torch.float64, device="cuda")
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            out["ms_per_msm_with_broadcast" if bcast else "ms_per_msm_resident_scalars"] = float(tt.item()) * 1e3 / reps
+        # the partitioned result must equal rank 0's whole MSM of the same scalars
+        ok = None
+        if rank == 0:
+            whole = torch.zeros(8, dtype=torch.int64, device="cuda")
+            H.check(L.halo_msm_dev_async(curve, None, ctypes.c_void_p(sc.data_ptr()), n_,
+                                         ctypes.c_void_p(whole.data_ptr()), sp))
+            H.check(L.halo_msm_join(sp))
+            torch.cuda.synchronize()
+            ok = bool(torch.equal(whole, res))
+        del sc
+        return {"workload": f"one 2^{lg}-point MSM, {W} windows split over {world} ranks (window_range), scalars "
+                            f"broadcast from rank 0, partials all-gathered", "windows_of_rank0": [lo, hi],
+                "points_per_s_with_broadcast": n_ / (out["ms_per_msm_with_broadcast"] * 1e-3),
+                "points_per_s_resident_scalars": n_ / (out["ms_per_msm_resident_scalars"] * 1e-3),
+                "matches_single_gpu": ok, "scaling": "strong", **out}
+
     ntt_main = measure_ntt(args.ntt_logn)
     ntt_main["workload"] += " (BASELINE.json configs[2])"
     sizes = {}
@@ -490,6 +548,8 @@ def main():
                 "points_per_rank": 1 << lr,
                 "scaling": "strong",
             }
+            torch.cuda.empty_cache()
+            sizes[f"msm_2^{lg}_window_partitioned"] = measure_window_partition(lg)
             torch.cuda.empty_cache()
 
     # ---- distributed single NTT (four-step, RCCL all-to-all; halo_amd.dist.sharded_ntt), N > 1 only

@@ -67,6 +67,8 @@ SIGNATURES = {
     "halo_msm_batch_dev": [ctypes.c_int, _vp, _vp, _sz, _vp, _vp],
     "halo_shutdown": [],
     "halo_srs_sh": [ctypes.c_int, _vp, _vp],
+    "halo_msm_srs_windows_dev": [ctypes.c_int, _vp, _sz, ctypes.c_int, ctypes.c_int, _vp, _vp],
+    "halo_srs_windows": [ctypes.c_int],
     "halo_point_dot_projective": [ctypes.c_int, _vp, _sz, _vp, _sz, _vp],
     "halo_pcdl_hiding_blind": [ctypes.c_int, _vp, _sz, _vp, _vp, _vp, _vp],
     "halo_pcdl_hiding_combine": [ctypes.c_int, _vp, _sz, _vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],

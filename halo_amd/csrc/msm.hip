@@ -92,9 +92,11 @@ __global__ __launch_bounds__(64) void k_synth_bases(uint4* out, size_t n, uint64
 // ---------------------------------------------------------------------------------------------
 // 1. digits
 // ---------------------------------------------------------------------------------------------
-// digits[w * ld + i] (ld >= n: the leading dimension, the batched MSMs' per-polynomial stride)
+// digits[(w - w_lo) * ld + i] for the windows w_lo <= w < w_hi (ld >= n: the leading dimension, the
+// batched MSMs' per-polynomial stride; a window range: one rank's share of a window-partitioned MSM)
 template <class S>
-__global__ void k_digits(const uint4* scalars, size_t n, int c, int W, uint32_t* digits, size_t ld) {
+__global__ void k_digits(const uint4* scalars, size_t n, int c, int W, uint32_t* digits, size_t ld, int w_lo,
+                         int w_hi) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint32_t w8[8];
@@ -145,7 +147,7 @@ __global__ void k_digits(const uint4* scalars, size_t n, int c, int W, uint32_t*
             carry = 0;
             out = (v == 0) ? DIGIT_NONE : ((v - 1) | nflip);
         }
-        digits[(size_t)w * ld + i] = out;
+        if (w >= w_lo && w < w_hi) digits[(size_t)(w - w_lo) * ld + i] = out;
     }
 }
 
@@ -541,7 +543,7 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
                         const uint4* scalars_ark, size_t n, int c_req, const uint4* hide_table, const uint4* hide_scalar,
                         uint4* d_out_wrapped, hipStream_t s, bool async, uint32_t blk_lg = 32,
                         bool hide_glv = false, bool out_xyzz = false, hipEvent_t hide_ready = nullptr,
-                        int preset = -1, hipStream_t fs = nullptr) {
+                        int preset = -1, hipStream_t fs = nullptr, int w_lo = 0, int w_hi = 0) {
     MsmPipe& PP = g_msm_pipe[st->device & 63];
     HALO_CHECK(pipe_init(PP));
     // preset: the set the caller already claimed (and waited for) to stage converted bases in
@@ -561,7 +563,17 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
     const bool glv = !shifted;
     const size_t NP = glv ? 2 * nn : nn;  // digit entries per window
     const int c = c_req ? c_req : msm_window_bits(NP);
-    const int W = glv ? (129 + c - 1) / c : msm_windows(c);
+    const int W_all = glv ? (129 + c - 1) / c : msm_windows(c);
+    // window range (shifted bases only): the windows [w_lo, w_hi) of the scalars, over the shifted
+    // copies w_lo.. (the bases pointer is offset below); the partials of a partition add up
+    if (w_hi <= 0 || glv) {
+        w_lo = 0;
+        w_hi = W_all;
+    }
+    if (w_lo < 0 || w_hi > W_all || w_lo >= w_hi)
+        return set_error(HALO_EINVAL, "window range [%d, %d) outside [0, %d)", w_lo, w_hi, W_all);
+    const int W = w_hi - w_lo;
+    if (shifted && w_lo) bases_int += 4 * (size_t)w_lo * shift_stride;
     const uint32_t B = 1u << (c - 1);
     // sort geometry: SW windows of SN entries each (shifted: one window over all W * n digits)
     const int SW = shifted ? 1 : W;
@@ -617,7 +629,7 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
                                M.digits.as<uint32_t>());
         else
             hipLaunchKernelGGL(k_digits<typename Cv::Scalar>, dim3(grid_for(n, 256)), dim3(256), 0, front, scalars_ark,
-                               n, c, W, M.digits.as<uint32_t>(), n);
+                               n, c, W_all, M.digits.as<uint32_t>(), n, w_lo, w_hi);
         HALO_HIP(hipGetLastError());
         uint32_t *skeys = nullptr, *svals = nullptr;
         const uint32_t* scount = nullptr;
@@ -755,7 +767,7 @@ static int msm_multi_device_t(DeviceState* st, const void* const* scalars, const
     for (size_t p = 0; p < k; p++)
         if (lens[p])
             hipLaunchKernelGGL(k_digits<typename Cv::Scalar>, dim3(grid_for(lens[p], 256)), dim3(256), 0, s,
-                               (const uint4*)scalars[p], lens[p], c, W, digits + p * SN, ld);
+                               (const uint4*)scalars[p], lens[p], c, W, digits + p * SN, ld, 0, W);
     HALO_HIP(hipGetLastError());
     uint32_t *skeys = nullptr, *svals = nullptr;
     const uint32_t* scount = nullptr;
@@ -1011,7 +1023,7 @@ static int msm_shared_batch_t(DeviceState* st, const uint4* bases, const uint4* 
     uint4* P_g2 = P_g1 + 8 * (ng1 + 1);
 
     hipLaunchKernelGGL(k_digits<typename Cv::Scalar>, dim3(grid_for(T, 256)), dim3(256), 0, s, w_ark, T, c, W,
-                       S.digits.as<uint32_t>(), T);
+                       S.digits.as<uint32_t>(), T, 0, W);
     hipLaunchKernelGGL(k_batch_lists, dim3(1), dim3(256), 0, s, S.digits.as<const uint32_t>(), (uint32_t)T, W, B,
                        (uint32_t)len, ent, ekey, tot);
     hipLaunchKernelGGL(k_batch_expand, dim3(grid_for(E, 256)), dim3(256), 0, s, (const uint32_t*)ent,
@@ -1739,6 +1751,39 @@ extern "C" int halo_msm_batch_dev(halo_curve_t curve, const void* const* d_scala
     if (!st) return HALO_EDEVICE;
     std::lock_guard<std::mutex> g(st->mu);
     return msm_batch_device(st, curve, d_scalars, lens, k, d_out, (hipStream_t)stream);
+}
+
+// One rank's share of a window-partitioned MSM over the resident window-shifted SRS (BASELINE
+// configs[4]): the digits of windows [w_lo, w_hi) only, against the copies 2^(c w) G, w in range; the
+// partials of a partition of [0, W) sum to the MSM.  Asynchronous like halo_msm_dev_async.
+extern "C" int halo_msm_srs_windows_dev(halo_curve_t curve, const void* d_scalars, size_t n, int w_lo, int w_hi,
+                                        void* d_out, void* stream) {
+    clear_error();
+    HALO_CHECK(check_curve(curve));
+    if (!d_out || (n && !d_scalars)) return set_error(HALO_EINVAL, "halo_msm_srs_windows_dev: null buffer");
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    SrsState& srs = st->srs[curve];
+    if (!srs.shifted_c) return set_error(HALO_EINVAL, "halo_msm_srs_windows_dev: no window-shifted SRS");
+    if (n > srs.n) return set_error(HALO_ESRSRANGE, "n (%zu) exceeds the resident SRS length (%zu)", n, srs.n);
+    if (w_hi <= w_lo) return set_error(HALO_EINVAL, "empty window range [%d, %d)", w_lo, w_hi);
+    int rc;
+    DISPATCH_CURVE(curve, Cv, {
+        rc = msm_device_t<Cv>(st, srs.shifted.as<const uint4>(), true, srs.n, (const uint4*)d_scalars, n,
+                              srs.shifted_c, nullptr, nullptr, (uint4*)d_out, (hipStream_t)stream, true, 32, false,
+                              false, nullptr, -1, nullptr, w_lo, w_hi);
+    });
+    return rc;
+}
+
+extern "C" int halo_srs_windows(halo_curve_t curve) {
+    clear_error();
+    HALO_CHECK(check_curve(curve));
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    return st->srs[curve].shifted_c ? msm_windows(st->srs[curve].shifted_c) : 0;
 }
 
 extern "C" int halo_msm_join(void* stream) {

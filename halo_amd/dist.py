@@ -45,6 +45,34 @@ def sharded_msm(partial_msm: Callable[[int, int], np.ndarray], point_sum: Callab
 
 
 # ---------------------------------------------------------------------------------------------
+# Window partition (BASELINE configs[4]): every rank holds the SAME scalars (broadcast from rank 0)
+# and the same window-shifted SRS copies; rank r takes the windows window_range(W, r, P) of every
+# scalar (halo_msm_srs_windows_dev).  With the shifted copies 2^(c w) G the per-window sums are
+# already weighted, so the partials simply add: the same all-gather + point sum as point-partition.
+# It costs a scalar broadcast (32 B x n over xGMI) that point-partition does not need, and W rarely
+# divides evenly (15 windows over 8 ranks: 2 + ... + 1), so point-partition is the default
+# (DESIGN.md §6); this path is measured beside it in bench.py (extra.msm_window_partition).
+# ---------------------------------------------------------------------------------------------
+def window_range(W: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous windows [lo, hi) of rank r: the first W % P ranks take one more."""
+    base, extra = divmod(W, world)
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
+
+
+def window_partitioned_msm(partial_windows: Callable[[int, int], np.ndarray],
+                           point_sum: Callable[[np.ndarray], np.ndarray], W: int, dist, device=None) -> np.ndarray:
+    """MSM whose W windows are split across ranks: partial_windows(lo, hi) is this rank's share (the
+    scalars are replicated on every rank), partials all-gathered and summed on every rank."""
+    rank, world = dist.get_rank(), dist.get_world_size()
+    lo, hi = window_range(W, rank, world)
+    part = partial_windows(lo, hi) if hi > lo else np.zeros(8, dtype=np.uint64)
+    if world == 1:
+        return part
+    return point_sum(allgather_points(part, dist, device))
+
+
+# ---------------------------------------------------------------------------------------------
 # Distributed NTT (SURVEY §8e): one transform of N = n1 n2 elements, natural order, rank r holding
 # the contiguous block x[r N/P, (r+1) N/P) in and X[r N/P, (r+1) N/P) out.
 #

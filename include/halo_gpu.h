@@ -160,6 +160,13 @@ int halo_msm_join(void* stream);
  * digit extraction and bucket sort of MSM i+1 run on a side stream beside MSM i's accumulation. */
 int halo_msm_batch_dev(halo_curve_t curve, const void* const* d_scalars, const size_t* lens, size_t k, void* d_out,
                        void* stream);
+/* Window-partitioned MSM (BASELINE configs[4]): one rank's share -- the signed digits of windows
+ * [w_lo, w_hi) of the n scalars against the resident window-shifted copies 2^(c w) G_i -- as a 64-B
+ * partial sum at d_out (asynchronous, halo_msm_join).  Partials of a partition of [0, W) add up to
+ * the full MSM (pedersen.rs:21).  halo_srs_windows gives W (0 without the shifted copies). */
+int halo_msm_srs_windows_dev(halo_curve_t curve, const void* d_scalars, size_t n, int w_lo, int w_hi, void* d_out,
+                             void* stream);
+int halo_srs_windows(halo_curve_t curve);
 /* Sum of k points (host arrays) on the device: the combine step after an RCCL all-gather of
  * per-rank partial MSMs (RCCL has no elliptic-curve reduction operator). */
 int halo_point_sum(halo_curve_t curve, const halo_wrapped_point_t* pts, size_t k, halo_wrapped_point_t* out);

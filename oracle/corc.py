@@ -181,3 +181,32 @@ def known_log_msm(curve: str, scalars_mont: np.ndarray, logs_canonical: np.ndarr
     product (S_j k_j R^-1 = s_j k_j) and one scalar multiplication of the generator."""
     acc = scalar_dot("fp" if curve == "pallas" else "fq", scalars_mont, logs_canonical)
     return generator_mul(curve, acc)
+
+
+def window_scalars(curve: str, scalars_mont: np.ndarray, c: int, lo: int, hi: int) -> np.ndarray:
+    """The part of each scalar carried by the signed c-bit windows [lo, hi) of the device's digit
+    recoding (msm.hip k_digits: s > r/2 is replaced by r - s with every digit negated; digits in
+    [-2^(c-1), 2^(c-1)] with a carry), as Montgomery scalars: sum_{w in [lo, hi)} d_w 2^(c w) mod r.
+    The window-partitioned MSM's partial of rank r is MSM(G, window_scalars(...)) (checker only)."""
+    import pasta as P
+    r = P.CURVES[curve].scalar
+    out = np.zeros_like(scalars_mont)
+    W = -(-255 // c)
+    for j, row in enumerate(np.asarray(scalars_mont).reshape(-1, 4)):
+        s = P.from_mont(P.limbs_to_int(row), r)
+        neg = (r - s) < s
+        if neg:
+            s = r - s
+        carry, acc = 0, 0
+        for w in range(W):
+            v = ((s >> (c * w)) & ((1 << c) - 1)) + carry
+            if v > (1 << (c - 1)):
+                d, carry = v - (1 << c), 1
+            else:
+                d, carry = v, 0
+            if lo <= w < hi:
+                acc += d << (c * w)
+        if neg:
+            acc = -acc
+        out[j] = P.int_to_limbs(P.to_mont(acc % r, r))
+    return out

@@ -372,3 +372,65 @@ def test_sharded_poly_eval_gloo(world, n):
     exp = OraclePolyOps("fp").eval_batch([coeffs], z)[0].tolist()
     for _, v in out:
         assert v == exp
+
+
+def _wworker(rank, world, port, n, c, q):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import torch.distributed as dist
+
+    import corc
+    import pasta as P
+    from halo_amd.dist import window_partitioned_msm
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = corc.srs_generate("pallas", n)
+    rng = np.random.default_rng(43)
+    sc = rng.integers(0, 2**63, size=(n, 4), dtype=np.uint64)
+    sc[:, 3] &= np.uint64(0x3FFFFFFFFFFFFFFF)
+    cv = P.PALLAS
+    W = -(-255 // c)
+
+    def partial(lo, hi):  # oracle restatement of halo_msm_srs_windows_dev's share
+        return corc.msm("pallas", g, corc.window_scalars("pallas", sc, c, lo, hi))
+
+    def psum(parts):
+        acc = None
+        for p in parts:
+            acc = P.add(cv, acc, P.wrapped_to_point(cv, list(p)))
+        return np.array(P.point_to_wrapped(cv, acc), dtype=np.uint64)
+
+    res = window_partitioned_msm(partial, psum, W, dist)
+    q.put((rank, res.tolist()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_window_partitioned_msm_gloo(corc, world):
+    """BASELINE configs[4]'s protocol over gloo: windows split across ranks (replicated scalars),
+    partials all-gathered and summed == the unsharded MSM on every rank; window_range covers [0, W)."""
+    from halo_amd.dist import window_range
+    for W in (13, 15, 16):
+        for P_ in (1, 2, 3, 8):
+            rs = [window_range(W, r, P_) for r in range(P_)]
+            assert rs[0][0] == 0 and rs[-1][1] == W and all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
+    n, c = 500, 17
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_wworker, args=(r, world, port, n, c, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    g = corc.srs_generate("pallas", n)
+    rng = np.random.default_rng(43)
+    sc = rng.integers(0, 2**63, size=(n, 4), dtype=np.uint64)
+    sc[:, 3] &= np.uint64(0x3FFFFFFFFFFFFFFF)
+    exp = corc.msm("pallas", g, sc).tolist()
+    assert all(o[1] == exp for o in out)

@@ -403,3 +403,37 @@ def test_point_dot_projective(hal, corc, cname, cid):
     sc = rand_sc(n, 77)
     assert np.array_equal(group.point_dot(sc, jac, cname), corc.msm(cname, aff, sc))
     assert np.array_equal(group.point_dot(sc[:100], jac, cname), corc.msm(cname, aff[:100], sc[:100]))
+
+
+def test_window_partitioned_msm_virtual_ranks(hal, corc):
+    """BASELINE configs[4] on one GPU with P virtual ranks: halo_msm_srs_windows_dev over each rank's
+    window range, partials summed (halo_point_sum) == the whole MSM; one rank's partial equals the
+    oracle MSM of its window share of the scalars (corc.window_scalars restates the digit recoding)."""
+    import ctypes
+
+    import torch
+    from halo_amd.dist import window_range
+    L = hal.load()
+    n = 1 << 14
+    g = corc.srs_generate("pallas", n)
+    group.PublicParams.upload("pallas", g, precompute_windows=True)
+    c = L.halo_srs_window_bits(0)
+    W = L.halo_srs_windows(0)
+    assert W == -(-255 // c)
+    sc = rand_sc(n, 91)
+    sc[0] = fe([P.PALLAS.scalar - 1], P.PALLAS.scalar)[0]
+    d_sc = torch.from_numpy(sc.view(np.int64)).cuda()
+    full = pcdl.commit(sc, n - 1, None, "pallas")
+    sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for world in (2, 3, 8):
+        outs = torch.zeros((world, 8), dtype=torch.int64, device="cuda")
+        for r in range(world):
+            lo, hi = window_range(W, r, world)
+            hal.check(L.halo_msm_srs_windows_dev(0, ctypes.c_void_p(d_sc.data_ptr()), n, lo, hi,
+                                                 ctypes.c_void_p(outs[r].data_ptr()), sp))
+        hal.check(L.halo_msm_join(sp))
+        parts = outs.cpu().numpy().view(np.uint64)
+        assert np.array_equal(group.point_sum(parts, "pallas"), full), world
+        if world == 3:
+            lo, hi = window_range(W, 1, 3)
+            assert np.array_equal(parts[1], corc.msm("pallas", g, corc.window_scalars("pallas", sc, c, lo, hi)))
