@@ -141,6 +141,60 @@ HALO_DEV void ntt_group(Fe<F> (&v)[EPT], uint32_t s, uint32_t G, uint32_t k0, co
     }
 }
 
+// The stage twiddles one thread needs for a radix-4 group at stages s, s + 1 (LG = 2, EPT = 4):
+// stage s uses omega_{2^(s+1)}^k0 for both of its butterflies, stage s + 1 omega_{2^(s+2)}^(k0) and
+// ^(k0 + 2^s).  Loaded packed (3 x 32 B) BEFORE the barrier that precedes the group's LDS reads, so
+// the L2 round trip of the table overlaps the barrier wait instead of following it.
+struct NttGroupTw {
+    uint4 w[3][2];
+};
+HALO_DEV void ntt_group_tw_load(NttGroupTw& t, uint32_t s, uint32_t G, uint32_t k0, const uint4* twg) {
+    const uint32_t i0 = (1u << s) - 1u + k0;
+    t.w[0][0] = twg[2 * i0];
+    t.w[0][1] = twg[2 * i0 + 1];
+    if (G > 1) {
+        const uint32_t i1 = (2u << s) - 1u + k0, i2 = i1 + (1u << s);
+        t.w[1][0] = twg[2 * i1];
+        t.w[1][1] = twg[2 * i1 + 1];
+        t.w[2][0] = twg[2 * i2];
+        t.w[2][1] = twg[2 * i2 + 1];
+    }
+}
+template <class F>
+HALO_DEV Fe<F> ntt_tw_unpack(const uint4 (&w)[2]) {
+    uint32_t x[8] = {w[0].x, w[0].y, w[0].z, w[0].w, w[1].x, w[1].y, w[1].z, w[1].w};
+    return fe_unpack<F>(x);
+}
+// ntt_group for EPT = 4, LG = 2, s >= 1 with the twiddles already loaded (same arithmetic and bounds)
+template <class F>
+HALO_DEV void ntt_group4_pre(Fe<F> (&v)[4], uint32_t G, const NttGroupTw& t) {
+    {
+        const Fe<F> w = ntt_tw_unpack<F>(t.w[0]);
+#pragma unroll
+        for (int m = 0; m < 4; m += 2) {
+            const Fe<F> x = fe_mul(v[m + 1], w);
+            v[m + 1] = fe_sub_k<2>(v[m], x);
+            v[m] = fe_norm(fe_add_nc(v[m], x));
+        }
+    }
+    if (G > 1) {
+#pragma unroll
+        for (int m = 0; m < 2; m++) {
+            const Fe<F> x = fe_mul(v[m + 2], ntt_tw_unpack<F>(t.w[1 + m]));
+            v[m + 2] = fe_sub_k<2>(v[m], x);
+            v[m] = fe_norm(fe_add_nc(v[m], x));
+        }
+    }
+}
+
+// raw workgroup barrier: LDS writes complete, global loads left in flight (a __syncthreads() would
+// also drain them)
+HALO_DEV void ntt_lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
 // One Stockham pass: R = 2^log_r point DFTs over the columns j of the N/R x R view.  A workgroup
 // owns T = NTT_E / R consecutive columns.  Each thread holds EPT elements in registers; the first
 // LG stages are done straight from the global loads, the rest in groups of LG stages through LDS,
@@ -216,10 +270,14 @@ __global__ __launch_bounds__(NE / NTT_EPT) void k_ntt_pass(NttPassArgs a) {
         for (int m = 0; m < EPT; m++)
             if (base + m < EB) lds_put_soa(data, pb ^ (uint32_t)m, NE, v[m]);
     }
-    __syncthreads();
-
-    // ---- remaining stages in groups of LG through LDS
-    for (uint32_t s = a.prune ? a.prune : G0; s < r; s += LG) {
+    // ---- remaining stages in groups of LG through LDS; each group's twiddles are loaded before the
+    // barrier that precedes its LDS reads
+    uint32_t s = a.prune ? a.prune : G0;
+    NttGroupTw tw;
+    if (s < r) ntt_group_tw_load(tw, s, (r - s) < (uint32_t)LG ? (r - s) : (uint32_t)LG, tau & ((1u << s) - 1),
+                                 a.stage_tw);
+    ntt_lds_barrier();
+    for (; s < r; s += LG) {
         const uint32_t G = (r - s) < (uint32_t)LG ? (r - s) : (uint32_t)LG;
         const uint32_t h = 1u << s;
         const uint32_t gb = (tau & (h - 1)) | ((tau >> s) << (s + LG));
@@ -230,14 +288,19 @@ __global__ __launch_bounds__(NE / NTT_EPT) void k_ntt_pass(NttPassArgs a) {
             const uint32_t ph = (pos ^ shb) ^ ntt_swz_hi<NE>(((uint32_t)m * h) >> 5);
             if (pos < EB) v[m] = lds_get_soa<F>(data, ph, NE);
         }
-        ntt_group<F, EPT, LG>(v, s, G, tau & (h - 1), a.stage_tw);
+        ntt_group4_pre<F>(v, G, tw);
+        // (no barrier here: a thread writes back exactly the positions it read)
 #pragma unroll
         for (int m = 0; m < EPT; m++) {
             const uint32_t pos = gb + (uint32_t)m * h;
             const uint32_t ph = (pos ^ shb) ^ ntt_swz_hi<NE>(((uint32_t)m * h) >> 5);
             if (pos < EB) lds_put_soa(data, ph, NE, v[m]);
         }
-        __syncthreads();
+        const uint32_t sn = s + LG;
+        if (sn < r)
+            ntt_group_tw_load(tw, sn, (r - sn) < (uint32_t)LG ? (r - sn) : (uint32_t)LG, tau & ((1u << sn) - 1),
+                              a.stage_tw);
+        ntt_lds_barrier();
     }
 
     // ---- store y[(j / Ns) Ns R + (j mod Ns) + k Ns]

@@ -9,7 +9,8 @@ import glob
 import json
 import sys
 
-SUB, XCDS, CUS = "k_acc<", 8, 256
+import os
+SUB, XCDS, CUS = os.environ.get("KSUB", "k_acc<"), 8, 256
 
 
 def counters(d):
@@ -37,7 +38,7 @@ def main():
         a, b = counters(f"{sys.argv[1]}/{tag}/a"), counters(f"{sys.argv[1]}/{tag}/b")
         ms = durations(f"{sys.argv[1]}/{tag}/c")
         cyc = b.get("GRBM_GUI_ACTIVE", 0) / XCDS
-        r = {"k_acc_ms": ms, **a, "gui_active_cycles_per_xcd": cyc}
+        r = {"kernel_ms": ms, "kernel": SUB, **a, "gui_active_cycles_per_xcd": cyc}
         if ms and cyc:
             r["effective_clock_GHz"] = cyc / (ms * 1e6)
             r["valu_wave_instr_per_cu_clk"] = a["SQ_INSTS_VALU"] / (CUS * cyc)
