@@ -21,6 +21,7 @@
 #include <vector>
 #include <cstdlib>
 
+#include "digits.hpp"
 #include "dispatch.hpp"
 #include "glv.hpp"
 #include "msm.hpp"
@@ -29,7 +30,6 @@
 
 namespace halo {
 
-constexpr uint32_t DIGIT_NONE = 0xffffffffu;
 // Columns of the bucket reduction grid (k_rowcol): 256 x 256 at 2^16 buckets keeps the row, column
 // and bit-sliced tree depths at ~9 additions each (measured against 32 columns: single-MSM latency
 // 2.15 -> 2.02 ms at 2^20, IPA opening 36.8 -> 35.2 ms; the pipelined step unchanged).
@@ -99,56 +99,9 @@ __global__ void k_digits(const uint4* scalars, size_t n, int c, int W, uint32_t*
                          int w_hi) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    uint32_t w8[8];
-    fe_ark_to_canonical_words<S>(scalars + 2 * i, w8);
-    // s > p / 2: use p - s < 2^254 and flip every digit's sign (s P = -(p - s) P), so that
-    // W = ceil(255 / c) windows suffice (msm_windows)
-    uint32_t t8[8];
-    {
-        int64_t br = 0;
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-            const int64_t d = (int64_t)(uint32_t)(S::MODULUS64[q >> 1] >> (32 * (q & 1))) - (int64_t)w8[q] + br;
-            t8[q] = (uint32_t)d;
-            br = d >> 32;
-        }
-    }
-    bool neg = false;  // p - s < s
-#pragma unroll
-    for (int q = 7; q >= 0; q--) {
-        if (t8[q] != w8[q]) {
-            neg = t8[q] < w8[q];
-            break;
-        }
-    }
-    if (neg)
-#pragma unroll
-        for (int q = 0; q < 8; q++) w8[q] = t8[q];
-    const uint32_t nflip = neg ? 0x80000000u : 0u;
-    const uint32_t half = 1u << (c - 1);
-    const uint32_t full = 1u << c;
-    uint32_t carry = 0;
-    for (int w = 0; w < W; w++) {
-        const int bit = w * c;
-        uint32_t raw = 0;
-        if (bit < 256) {
-            const int q = bit >> 5, s = bit & 31;
-            uint64_t lo = w8[q];
-            uint64_t hi = (q + 1 < 8) ? w8[q + 1] : 0;
-            raw = (uint32_t)(((hi << 32) | lo) >> s) & (full - 1);
-        }
-        uint32_t v = raw + carry;
-        uint32_t out;
-        if (v > half) {
-            carry = 1;
-            const uint32_t mag = full - v;  // |d|, d = v - 2^c < 0
-            out = (mag == 0) ? DIGIT_NONE : (((mag - 1) | 0x80000000u) ^ nflip);
-        } else {
-            carry = 0;
-            out = (v == 0) ? DIGIT_NONE : ((v - 1) | nflip);
-        }
+    scalar_signed_digits<S>(scalars + 2 * i, c, W, [&](int w, uint32_t out) {
         if (w >= w_lo && w < w_hi) digits[(size_t)(w - w_lo) * ld + i] = out;
-    }
+    });
 }
 
 // GLV recoding (bases not window-shifted): s = k1 + lambda k2 with |k1|, |k2| < 2^128, so each
@@ -624,17 +577,22 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
     }
 
     if (n > 0) {
+        // shifted, all windows, W <= 16: digit recoding fused into the sort's first pass
+        static const bool fuse_env = !getenv("HALO_SORT_UNFUSED");
+        const bool fuse = fuse_env && shifted && w_lo == 0 && w_hi == W_all && W_all <= 16 && front == s &&
+                          n < (1ull << 31) / 16;
         if (glv)
             hipLaunchKernelGGL(k_digits_glv<Cv>, dim3(grid_for(n, 256)), dim3(256), 0, front, scalars_ark, n, c, W,
                                M.digits.as<uint32_t>());
-        else
+        else if (!fuse)
             hipLaunchKernelGGL(k_digits<typename Cv::Scalar>, dim3(grid_for(n, 256)), dim3(256), 0, front, scalars_ark,
                                n, c, W_all, M.digits.as<uint32_t>(), n, w_lo, w_hi);
         HALO_HIP(hipGetLastError());
         uint32_t *skeys = nullptr, *svals = nullptr;
         const uint32_t* scount = nullptr;
+        RsFused fz{scalars_ark, n, c, W_all, curve_id<Cv>() == HALO_PALLAS ? HALO_FP : HALO_FQ};
         HALO_CHECK(msm_radix_sort(M.digits.as<const uint32_t>(), E, SN, B, key_bits, M.sort, &skeys, &svals, &scount,
-                                  nullptr, NB, front, front != s));
+                                  nullptr, NB, front, front != s, fuse ? &fz : nullptr));
         if (front != s) {
             HALO_HIP(hipEventRecord(M.front_done, front));
             HALO_HIP(hipStreamWaitEvent(s, M.front_done, 0));

@@ -17,8 +17,11 @@
 // entries is known only on the device (scan total) -- kernels bound themselves by it, so no host
 // round trip is needed.
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 
+#include "digits.hpp"
+#include "dispatch.hpp"
 #include "fields.hpp"
 #include "runtime.hpp"
 #include "sort.hpp"
@@ -33,6 +36,9 @@ constexpr int RS_BINS = 256;
 constexpr uint32_t RS_NONE = 0xffffffffu;
 
 struct RsIn {
+    const uint4* sc = nullptr;  // fused pass 0: the ark scalars (k_rs_hist_sc / k_rs_scatter<.., S>)
+    uint32_t n_sc = 0;
+    int c = 0, W = 0;
     const uint32_t* digits;  // pass 0 only
     const uint32_t* keys;    // later passes
     const uint32_t* vals;
@@ -78,6 +84,25 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_hist(RsIn in, uint32_t ntiles
     }
     __syncthreads();
     if (threadIdx.x < RS_BINS) hist[(size_t)blockIdx.x * RS_BINS + threadIdx.x] = h[threadIdx.x];  // tile-major
+}
+
+// Fused first pass of the window-shifted MSM's sort (single bucket set): the entries are recoded
+// from the scalars here instead of being written by k_digits and read back (32 B of scalar per
+// W = 15 entries instead of 2 x 4 B per entry).  Thread = one scalar, round = window: a tile is
+// RS_THREADS scalars x W windows.  Entry key = |d| - 1, value = (w n + i) | sign, as k_digits + pass 0.
+template <class S>
+__global__ __launch_bounds__(RS_THREADS) void k_rs_hist_sc(const uint4* sc, uint32_t n, int c, int W,
+                                                         uint32_t* hist) {
+    __shared__ uint32_t h[RS_BINS];
+    if (threadIdx.x < RS_BINS) h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t i = blockIdx.x * RS_THREADS + threadIdx.x;
+    if (i < n)
+        scalar_signed_digits<S>(sc + 2 * (size_t)i, c, W, [&](int, uint32_t d) {
+            if (d != DIGIT_NONE) atomicAdd(&h[d & 255u], 1u);
+        });
+    __syncthreads();
+    if (threadIdx.x < RS_BINS) hist[(size_t)blockIdx.x * RS_BINS + threadIdx.x] = h[threadIdx.x];
 }
 
 // Offsets from the tile-major histogram without a transposed copy.  k_rs_colscan: per chunk of
@@ -132,7 +157,8 @@ __global__ __launch_bounds__(RS_BINS) void k_rs_chunkscan(uint32_t* chunk, uint3
 // Each wave owns a contiguous eighth of the tile (1024 entries, 16 rounds of 64), so ranking is
 // wave-local (ballots + a wave-private LDS run counter per digit) and the workgroup needs only
 // three barriers: after the per-wave histograms, after the prefix, after staging.
-template <int ROUNDS>
+// SF: void, or the scalar field of a fused first pass (k_rs_hist_sc's entries, in.sc != null)
+template <int ROUNDS, class SF = void>
 __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(RsIn in, const uint32_t* tile_off, const uint32_t* chunk_off,
                                                            uint32_t* keys_out, uint32_t* vals_out) {
     constexpr int RS_TILE = RS_THREADS * ROUNDS;
@@ -149,12 +175,30 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(RsIn in, const uint32
     constexpr int R = PER_WAVE / 64;
     uint32_t K[R], V[R];
     uint32_t validmask = 0;
-    // all loads of the tile issued back to back (memory-level parallelism), kept in registers
+    if constexpr (!std::is_void<SF>::value) {
+        // fused first pass: this lane's scalar, its W windows as the rounds
 #pragma unroll
-    for (int r = 0; r < R; r++) {
-        K[r] = 0;
-        V[r] = 0;
-        if (rs_fetch(in, wbase + (size_t)r * 64 + lane, limit, K[r], V[r])) validmask |= 1u << r;
+        for (int r = 0; r < R; r++) {
+            K[r] = 0;
+            V[r] = 0;
+        }
+        const uint32_t i = blockIdx.x * RS_THREADS + tid;
+        if (i < in.n_sc)
+            scalar_signed_digits<SF, R>(in.sc + 2 * (size_t)i, in.c, in.W, [&](int w, uint32_t d) {
+                if (d != DIGIT_NONE) {
+                    K[w] = d & 0x7fffffffu;
+                    V[w] = ((uint32_t)w * in.n_sc + i) | (d & 0x80000000u);
+                    validmask |= 1u << w;
+                }
+            });
+    } else {
+        // all loads of the tile issued back to back (memory-level parallelism), kept in registers
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            K[r] = 0;
+            V[r] = 0;
+            if (rs_fetch(in, wbase + (size_t)r * 64 + lane, limit, K[r], V[r])) validmask |= 1u << r;
+        }
     }
     if (tid < RS_BINS) {
         goff[tid] = tile_off[(size_t)blockIdx.x * RS_BINS + tid] + chunk_off[(size_t)(blockIdx.x / RS_CH) * RS_BINS + tid];
@@ -341,7 +385,7 @@ int device_exclusive_scan(const uint32_t* in, size_t n, uint32_t* out, DevBuf& t
 
 int msm_radix_sort(const uint32_t* digits, size_t E, size_t npw, uint32_t B, uint32_t key_bits, SortScratch& S,
                    uint32_t** keys_out, uint32_t** vals_out, const uint32_t** count_out, uint32_t* bstart, size_t NB,
-                   hipStream_t s, bool small_tiles) {
+                   hipStream_t s, bool small_tiles, const RsFused* fused) {
     static const int tile_env = [] {
         const char* e = getenv("HALO_SORT_ROUNDS");
         return e ? atoi(e) : 0;
@@ -350,14 +394,15 @@ int msm_radix_sort(const uint32_t* digits, size_t E, size_t npw, uint32_t B, uin
     if (tile_env == 16) small_tiles = false;
     const int RS_TILE = RS_THREADS * (small_tiles ? 8 : 16);
     const uint32_t ntiles = (uint32_t)std::max<size_t>(1, (E + RS_TILE - 1) / RS_TILE);
-    const size_t hn = (size_t)RS_BINS * ntiles;
+    // fused first pass: tiles of RS_THREADS scalars x W windows
+    const uint32_t ntiles0 = fused ? (uint32_t)std::max<size_t>(1, (fused->n + RS_THREADS - 1) / RS_THREADS) : ntiles;
+    const uint32_t ntmax = std::max(ntiles, ntiles0);
     HALO_CHECK(S.keys[0].reserve(std::max<size_t>(E, 1) * 4));
     HALO_CHECK(S.keys[1].reserve(std::max<size_t>(E, 1) * 4));
     HALO_CHECK(S.vals[0].reserve(std::max<size_t>(E, 1) * 4));
     HALO_CHECK(S.vals[1].reserve(std::max<size_t>(E, 1) * 4));
-    const uint32_t nchunks = (ntiles + RS_CH - 1) / RS_CH;
-    HALO_CHECK(S.hist.reserve(hn * 4));
-    HALO_CHECK(S.offs.reserve((size_t)nchunks * RS_BINS * 4));
+    HALO_CHECK(S.hist.reserve((size_t)RS_BINS * ntmax * 4));
+    HALO_CHECK(S.offs.reserve((size_t)((ntmax + RS_CH - 1) / RS_CH) * RS_BINS * 4));
     HALO_CHECK(S.count.reserve(16));
     const uint32_t passes = std::max<uint32_t>(1, (key_bits + 7) / 8);
     int cur = 0;
@@ -372,16 +417,38 @@ int msm_radix_sort(const uint32_t* digits, size_t E, size_t npw, uint32_t B, uin
         in.B = B;
         in.pass = p;
         in.shift = 8 * p;
-        hipLaunchKernelGGL(small_tiles ? k_rs_hist<8> : k_rs_hist<16>, dim3(ntiles), dim3(RS_THREADS), 0, s, in, ntiles,
-                           S.hist.as<uint32_t>());
-        hipLaunchKernelGGL(k_rs_colscan, dim3(nchunks), dim3(RS_BINS), 0, s, S.hist.as<uint32_t>(), ntiles,
+        const bool fp = fused && p == 0;
+        const uint32_t nt = fp ? ntiles0 : ntiles;
+        const uint32_t nchunks = (nt + RS_CH - 1) / RS_CH;
+        if (fp) {
+            in.sc = (const uint4*)fused->scalars;
+            in.n_sc = (uint32_t)fused->n;
+            in.c = fused->c;
+            in.W = fused->W;
+            DISPATCH_FIELD(fused->field, SF, {
+                hipLaunchKernelGGL(k_rs_hist_sc<SF>, dim3(nt), dim3(RS_THREADS), 0, s, in.sc, in.n_sc, in.c, in.W,
+                                   S.hist.as<uint32_t>());
+            });
+        } else {
+            hipLaunchKernelGGL(small_tiles ? k_rs_hist<8> : k_rs_hist<16>, dim3(nt), dim3(RS_THREADS), 0, s, in, nt,
+                               S.hist.as<uint32_t>());
+        }
+        hipLaunchKernelGGL(k_rs_colscan, dim3(nchunks), dim3(RS_BINS), 0, s, S.hist.as<uint32_t>(), nt,
                            S.offs.as<uint32_t>());
         // pass 0 also stores the number of valid (nonzero-digit) entries
         hipLaunchKernelGGL(k_rs_chunkscan, dim3(1), dim3(RS_BINS), 0, s, S.offs.as<uint32_t>(), nchunks,
                            p == 0 ? S.count.as<uint32_t>() : nullptr);
-        hipLaunchKernelGGL(small_tiles ? k_rs_scatter<8> : k_rs_scatter<16>, dim3(ntiles), dim3(RS_THREADS), 0, s, in,
-                           S.hist.as<const uint32_t>(), S.offs.as<const uint32_t>(), S.keys[cur].as<uint32_t>(),
-                           S.vals[cur].as<uint32_t>());
+        if (fp) {
+            DISPATCH_FIELD(fused->field, SF, {
+                hipLaunchKernelGGL((k_rs_scatter<16, SF>), dim3(nt), dim3(RS_THREADS), 0, s, in,
+                                   S.hist.as<const uint32_t>(), S.offs.as<const uint32_t>(), S.keys[cur].as<uint32_t>(),
+                                   S.vals[cur].as<uint32_t>());
+            });
+        } else {
+            hipLaunchKernelGGL(small_tiles ? k_rs_scatter<8> : k_rs_scatter<16>, dim3(nt), dim3(RS_THREADS), 0, s, in,
+                               S.hist.as<const uint32_t>(), S.offs.as<const uint32_t>(), S.keys[cur].as<uint32_t>(),
+                               S.vals[cur].as<uint32_t>());
+        }
         HALO_HIP(hipGetLastError());
         cur ^= 1;
     }

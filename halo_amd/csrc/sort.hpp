@@ -15,9 +15,16 @@ int device_exclusive_scan(const uint32_t* in, size_t n, uint32_t* out, DevBuf& t
 // (e / npw) * B + (|d| - 1), stable; values = (e mod npw) | sign.  key_bits = bits of the largest
 // key.  Fills bstart[0..NB] when bstart is not null (bucket b's entries are [bstart[b], bstart[b+1])
 // of the sorted arrays).
+// Fused first pass (window-shifted MSM, one bucket set, W <= 16): the entries come from the scalars
+// (digits.hpp recoding) instead of a digit array; `digits` is then unused.
+struct RsFused {
+    const void* scalars;  // ark scalars (device)
+    size_t n;
+    int c, W, field;
+};
 int msm_radix_sort(const uint32_t* digits, size_t E, size_t npw, uint32_t B, uint32_t key_bits, SortScratch& S,
                    uint32_t** keys_out, uint32_t** vals_out, const uint32_t** count_out, uint32_t* bstart, size_t NB,
-                   hipStream_t s, bool small_tiles = false);
+                   hipStream_t s, bool small_tiles = false, const RsFused* fused = nullptr);
 
 // bstart[b] (b <= NB) from the sorted keys (capacity E, device count)
 int msm_bucket_starts(const uint32_t* keys, const uint32_t* count, size_t NB, size_t E, uint32_t* bstart, hipStream_t s);
