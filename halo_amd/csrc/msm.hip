@@ -167,17 +167,29 @@ template <class Cv>
 __device__ __forceinline__ void acc_chunk(size_t t, uint32_t cnt, const uint32_t* keys, const uint32_t* vals, uint32_t K,
                                           const uint4* bases, uint32_t n_per_window, uint32_t npw_lg, size_t stride,
                                           uint32_t blk_lg, uint32_t glv_n, uint4* first, uint4* last,
-                                          uint4* bucket_sums) {
+                                          uint4* bucket_sums, uint32_t* bstart, uint32_t NB) {
     using F = typename Cv::Base;
     const size_t beg = t * K;
-    if (beg >= cnt) return;
+    if (beg >= cnt) {
+        if (t == 0)  // no entries at all: every bucket is empty
+            for (uint32_t b = 0; b <= NB; b++) bstart[b] = 0;
+        return;
+    }
     const uint32_t end = (uint32_t)min((size_t)cnt, beg + K);
     uint32_t cur = keys[beg];
+    // bucket starts (the tail's k_merge): bstart[b] = first sorted position of key b, for every b
+    // whose first position (or, for empty buckets, the next bucket's) falls in this chunk
+    {
+        const uint32_t prev = beg ? keys[beg - 1] : 0xffffffffu;
+        if (prev != cur)
+            for (uint32_t b = prev + 1; b <= cur; b++) bstart[b] = (uint32_t)beg;
+    }
     bool first_done = false;
     XYZZ<F> acc = xyzz_id<F>();
     for (uint32_t e = (uint32_t)beg; e < end; e++) {
         const uint32_t k = keys[e];
         if (k != cur) {  // bucket boundary inside the chunk
+            for (uint32_t b = cur + 1; b <= k; b++) bstart[b] = e;
             if (!first_done) {
                 xyzz_store(first + 8 * t, xyzz_settle(acc));
                 first_done = true;
@@ -202,6 +214,8 @@ __device__ __forceinline__ void acc_chunk(size_t t, uint32_t cnt, const uint32_t
         acc = xyzz_madd_acc(acc, p, (v & 0x80000000u) ? ~0u : 0u);
     }
     xyzz_store((first_done ? last : first) + 8 * t, xyzz_settle(acc));
+    if (end == cnt)
+        for (uint32_t b = cur + 1; b <= NB; b++) bstart[b] = cnt;
 }
 
 // PERSIST (beside a concurrent front, HALO_BATCH_OVERLAP=1): a grid of a few workgroups per CU
@@ -211,11 +225,12 @@ template <class Cv, bool PERSIST>
 __global__ __launch_bounds__(256, HALO_ACC_MINB) void k_acc(const uint32_t* keys, const uint32_t* vals, const uint32_t* count,
                                              uint32_t K, const uint4* bases, uint32_t n_per_window, uint32_t npw_lg,
                                              size_t stride, uint32_t blk_lg, uint32_t glv_n, uint4* first, uint4* last,
-                                             uint4* bucket_sums, uint32_t* work_ctr, uint32_t nblocks) {
+                                             uint4* bucket_sums, uint32_t* work_ctr, uint32_t nblocks, uint32_t* bstart,
+                                             uint32_t NB) {
     const uint32_t cnt = *count;
     if constexpr (!PERSIST) {
         acc_chunk<Cv>((size_t)blockIdx.x * blockDim.x + threadIdx.x, cnt, keys, vals, K, bases, n_per_window,
-                                npw_lg, stride, blk_lg, glv_n, first, last, bucket_sums);
+                                npw_lg, stride, blk_lg, glv_n, first, last, bucket_sums, bstart, NB);
     } else {
         __shared__ uint32_t sblk;
         for (;;) {
@@ -225,7 +240,7 @@ __global__ __launch_bounds__(256, HALO_ACC_MINB) void k_acc(const uint32_t* keys
             __syncthreads();
             if (blk >= nblocks) break;  // uniform per workgroup: every wave leaves
             acc_chunk<Cv>((size_t)blk * blockDim.x + threadIdx.x, cnt, keys, vals, K, bases, n_per_window,
-                                    npw_lg, stride, blk_lg, glv_n, first, last, bucket_sums);
+                                    npw_lg, stride, blk_lg, glv_n, first, last, bucket_sums, bstart, NB);
         }
     }
 }
@@ -614,7 +629,7 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
                     (const uint32_t*)svals, scount, K, bases_int, (uint32_t)nn, is_pow2(nn) ? ilog2(nn) : 0xffu,
                     (shifted && (shift_stride != nn || blk_lg < 32)) ? shift_stride : (size_t)0, blk_lg,
                     glv ? (uint32_t)nn : 0u, P_first,
-                    P_last, M.bucket_sums.as<uint4>(), work_ctr, nblocks);
+                    P_last, M.bucket_sums.as<uint4>(), work_ctr, nblocks, M.bstart.as<uint32_t>(), (uint32_t)NB);
         M.skeys = skeys;
         M.scount = scount;
         HALO_HIP(hipGetLastError());
@@ -736,7 +751,8 @@ static int msm_multi_device_t(DeviceState* st, const void* const* scalars, const
         auto kacc = k_acc<Cv, false>;
         HALO_LAUNCH(prof, kacc, dim3(nblocks), dim3(256), 0, s, (const uint32_t*)skeys, (const uint32_t*)svals, scount,
                     K, srs.shifted.as<const uint4>(), (uint32_t)ld, is_pow2(ld) ? ilog2(ld) : 0xffu, srs.n, 32u, 0u,
-                    P_first, P_last, M.bucket_sums.as<uint4>(), (uint32_t*)nullptr, nblocks);
+                    P_first, P_last, M.bucket_sums.as<uint4>(), (uint32_t*)nullptr, nblocks, M.bstart.as<uint32_t>(),
+                    (uint32_t)NB);
         HALO_HIP(hipGetLastError());
     }
     MsmTailArgs ta;
@@ -989,7 +1005,8 @@ static int msm_shared_batch_t(DeviceState* st, const uint4* bases, const uint4* 
                        S.keys.as<uint32_t>(), S.vals.as<uint32_t>());
     hipLaunchKernelGGL((k_acc<Cv, false>), dim3(grid_for(nchunks, 256)), dim3(256), 0, s, S.keys.as<const uint32_t>(),
                        S.vals.as<const uint32_t>(), (const uint32_t*)(tot + 1), K, bases, 1u, 0u, (size_t)0, 32u, 0u,
-                       P_first, P_last, S.bucket_sums.as<uint4>(), (uint32_t*)nullptr, (uint32_t)grid_for(nchunks, 256));
+                       P_first, P_last, S.bucket_sums.as<uint4>(), (uint32_t*)nullptr, (uint32_t)grid_for(nchunks, 256),
+                       S.bstart.as<uint32_t>(), (uint32_t)NB);
     HALO_HIP(hipGetLastError());
     MsmTailArgs ta;
     ta.n = T;

@@ -234,7 +234,6 @@ static unsigned grid_for_t(size_t n, unsigned thr) { return (unsigned)std::max<s
 template <class Cv>
 static int tail_launch_t(const MsmTailArgs& a, hipStream_t ts) {
     if (a.n > 0) {
-        HALO_CHECK(msm_bucket_starts(a.skeys, a.scount, a.NB, a.E, a.bstart, ts));
         if (a.ng1)
             hipLaunchKernelGGL(k_group_sums<Cv>, dim3((unsigned)a.ng1), dim3(MSM_GROUP), 0, ts, a.skeys, a.scount, a.K,
                                1u, (const uint4*)a.first, a.g1);

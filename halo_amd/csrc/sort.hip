@@ -6,8 +6,8 @@
 //
 // Design (per 8-bit digit pass, tiles of 8192 entries, 512 threads):
 //   k_rs_hist    : per-tile LDS histogram of the digit -> hist[tile][digit] (coalesced)
-//   colscan/chunkscan : digit-major exclusive prefix of that table without transposing it
-//                  -> every tile's global run start per digit
+//                  and, by the kernel's last arrivers, the digit-major exclusive prefix of that table
+//                  without transposing it -> every tile's global run start per digit
 //   k_rs_scatter : stable in-tile ranking (each wave ranks its own contiguous quarter of the tile with
 //                  ballots that find equal digits among lanes; per-wave histograms order the waves),
 //                  the tile is staged in LDS in digit order and written back as contiguous runs per
@@ -69,8 +69,97 @@ HALO_DEV bool rs_fetch(const RsIn& in, size_t e, size_t limit, uint32_t& key, ui
 
 HALO_DEV size_t rs_limit(const RsIn& in) { return in.pass == 0 ? in.E : (size_t)*in.count; }
 
+// Offsets from the tile-major histogram, by the histogram kernel's last arrivers (no separate scan
+// launches, no spinning): each workgroup publishes its row (sc1 stores, drained) and counts itself in
+// its chunk of RS_CH tiles; the chunk's last arriver scans the chunk's rows per digit (in-chunk
+// exclusive prefix, in place) and publishes the chunk total; the last chunk to finish scans the chunk
+// totals per digit and adds the digit's base (exclusive scan of the digit totals).  Tile t's run for
+// digit d then starts at hist[t][d] + chunk[t / RS_CH][d].  Pass 0 also stores the number of valid
+// entries.  Hand-off protocol (MI355X_MICROARCH.md, inter-workgroup visibility): every handed-off
+// word stored sc1 and drained before a workgroup barrier and the agent-scope counter add; the
+// consumer is the workgroup whose add returned the last count, which takes an agent-scope acquire
+// before reading.  The counters (ctr[0..nchunks), ctr[nchunks]) are reset by their last arriver.
+constexpr int RS_CH = 64;
+#define RS_RLX_AGENT __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
+HALO_DEV void rs_acquire() {  // one lane's agent acquire, then the whole workgroup waits for it
+    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+}
+// true in the workgroup whose add to *c returned total - 1 (every workgroup's stores drained first)
+HALO_DEV bool rs_last_arriver(uint32_t* c, uint32_t total, uint32_t* flag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) *flag = __hip_atomic_fetch_add(c, 1u, RS_RLX_AGENT) == total - 1;
+    __syncthreads();
+    return *flag != 0;
+}
+HALO_DEV void rs_publish_and_scan(const uint32_t* h, uint32_t tile, uint32_t ntiles, uint32_t* hist, uint32_t* chunk,
+                                  uint32_t* ctr, uint32_t* count) {
+    __shared__ uint32_t flag;
+    __shared__ uint32_t s[RS_BINS];
+    const uint32_t d = threadIdx.x;
+    if (d < RS_BINS) __hip_atomic_store(hist + (size_t)tile * RS_BINS + d, h[d], RS_RLX_AGENT);
+    const uint32_t ch = tile / RS_CH, nchunks = (ntiles + RS_CH - 1) / RS_CH;
+    const uint32_t t0 = ch * RS_CH, nt = min((uint32_t)RS_CH, ntiles - t0);
+    if (!rs_last_arriver(ctr + ch, nt, &flag)) return;
+    rs_acquire();
+    if (d < RS_BINS) {
+        uint32_t v[RS_CH];
+#pragma unroll
+        for (int i = 0; i < RS_CH; i++) v[i] = (i < (int)nt) ? hist[(size_t)(t0 + i) * RS_BINS + d] : 0u;
+        uint32_t run = 0;
+#pragma unroll
+        for (int i = 0; i < RS_CH; i++) {
+            if (i < (int)nt) hist[(size_t)(t0 + i) * RS_BINS + d] = run;  // read by the scatter launch
+            run += v[i];
+        }
+        __hip_atomic_store(chunk + (size_t)ch * RS_BINS + d, run, RS_RLX_AGENT);
+    }
+    if (d == 0) __hip_atomic_store(ctr + ch, 0u, RS_RLX_AGENT);
+    if (!rs_last_arriver(ctr + nchunks, nchunks, &flag)) return;
+    rs_acquire();
+    if (d < RS_BINS) {
+        uint32_t run = 0;
+        for (uint32_t c = 0; c < nchunks; c++) {
+            const uint32_t v = chunk[(size_t)c * RS_BINS + d];
+            chunk[(size_t)c * RS_BINS + d] = run;
+            run += v;
+        }
+        s[d] = run;
+    }
+    __syncthreads();
+    // exclusive scan of the digit totals (wave 0: 4 digits per lane)
+    if (d < 64) {
+        uint32_t c[4], sum = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            c[q] = s[d * 4 + q];
+            sum += c[q];
+        }
+        uint32_t incl = sum;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t t = __shfl_up(incl, off);
+            if ((int)d >= off) incl += t;
+        }
+        uint32_t ex = incl - sum;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            s[d * 4 + q] = ex;
+            ex += c[q];
+        }
+        if (d == 63 && count) *count = incl;
+    }
+    __syncthreads();
+    if (d < RS_BINS)
+        for (uint32_t c = 0; c < nchunks; c++) chunk[(size_t)c * RS_BINS + d] += s[d];
+    if (d == 0) __hip_atomic_store(ctr + nchunks, 0u, RS_RLX_AGENT);
+}
+
 template <int ROUNDS>
-__global__ __launch_bounds__(RS_THREADS) void k_rs_hist(RsIn in, uint32_t ntiles, uint32_t* hist) {
+__global__ __launch_bounds__(RS_THREADS) void k_rs_hist(RsIn in, uint32_t ntiles, uint32_t* hist, uint32_t* chunk,
+                                                        uint32_t* ctr, uint32_t* count) {
     constexpr int RS_TILE = RS_THREADS * ROUNDS;
     __shared__ uint32_t h[RS_BINS];
     if (threadIdx.x < RS_BINS) h[threadIdx.x] = 0;
@@ -83,7 +172,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_hist(RsIn in, uint32_t ntiles
             atomicAdd(&h[(k >> in.shift) & 255u], 1u);
     }
     __syncthreads();
-    if (threadIdx.x < RS_BINS) hist[(size_t)blockIdx.x * RS_BINS + threadIdx.x] = h[threadIdx.x];  // tile-major
+    rs_publish_and_scan(h, blockIdx.x, ntiles, hist, chunk, ctr, count);
 }
 
 // Fused first pass of the window-shifted MSM's sort (single bucket set): the entries are recoded
@@ -91,8 +180,9 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_hist(RsIn in, uint32_t ntiles
 // W = 15 entries instead of 2 x 4 B per entry).  Thread = one scalar, round = window: a tile is
 // RS_THREADS scalars x W windows.  Entry key = |d| - 1, value = (w n + i) | sign, as k_digits + pass 0.
 template <class S>
-__global__ __launch_bounds__(RS_THREADS) void k_rs_hist_sc(const uint4* sc, uint32_t n, int c, int W,
-                                                         uint32_t* hist) {
+__global__ __launch_bounds__(RS_THREADS) void k_rs_hist_sc(const uint4* sc, uint32_t n, int c, int W, uint32_t ntiles,
+                                                         uint32_t* hist, uint32_t* chunk, uint32_t* ctr,
+                                                         uint32_t* count) {
     __shared__ uint32_t h[RS_BINS];
     if (threadIdx.x < RS_BINS) h[threadIdx.x] = 0;
     __syncthreads();
@@ -102,56 +192,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_hist_sc(const uint4* sc, uint
             if (d != DIGIT_NONE) atomicAdd(&h[d & 255u], 1u);
         });
     __syncthreads();
-    if (threadIdx.x < RS_BINS) hist[(size_t)blockIdx.x * RS_BINS + threadIdx.x] = h[threadIdx.x];
-}
-
-// Offsets from the tile-major histogram without a transposed copy.  k_rs_colscan: per chunk of
-// RS_CH tiles and per digit, the exclusive prefix over the chunk's tiles (in place) and the chunk
-// total.  k_rs_chunkscan (one block, thread = digit): exclusive prefix of the chunk totals per digit
-// plus the digit's base (exclusive scan of digit totals), in place; on pass 0 it also stores the
-// number of valid entries.  Tile t's run for digit d then starts at hist[t][d] + chunk[t / RS_CH][d].
-constexpr int RS_CH = 64;
-__global__ __launch_bounds__(RS_BINS) void k_rs_colscan(uint32_t* hist, uint32_t ntiles, uint32_t* chunk) {
-    const uint32_t d = threadIdx.x, t0 = blockIdx.x * RS_CH;
-    uint32_t v[RS_CH];
-#pragma unroll
-    for (int i = 0; i < RS_CH; i++) v[i] = (t0 + i < ntiles) ? hist[(size_t)(t0 + i) * RS_BINS + d] : 0u;
-    uint32_t run = 0;
-#pragma unroll
-    for (int i = 0; i < RS_CH; i++) {
-        if (t0 + i < ntiles) hist[(size_t)(t0 + i) * RS_BINS + d] = run;
-        run += v[i];
-    }
-    chunk[(size_t)blockIdx.x * RS_BINS + d] = run;
-}
-
-__global__ __launch_bounds__(RS_BINS) void k_rs_chunkscan(uint32_t* chunk, uint32_t nchunks, uint32_t* count) {
-    __shared__ uint32_t s[RS_BINS];
-    const uint32_t d = threadIdx.x;
-    constexpr int U = 16;
-    uint32_t run = 0;
-    for (uint32_t c0 = 0; c0 < nchunks; c0 += U) {
-        uint32_t v[U];
-#pragma unroll
-        for (int i = 0; i < U; i++) v[i] = (c0 + i < nchunks) ? chunk[(size_t)(c0 + i) * RS_BINS + d] : 0u;
-#pragma unroll
-        for (int i = 0; i < U; i++) {
-            if (c0 + i < nchunks) chunk[(size_t)(c0 + i) * RS_BINS + d] = run;
-            run += v[i];
-        }
-    }
-    // exclusive scan of the digit totals
-    s[d] = run;
-    __syncthreads();
-    for (int off = 1; off < RS_BINS; off <<= 1) {
-        const uint32_t t = (d >= (uint32_t)off) ? s[d - off] : 0u;
-        __syncthreads();
-        s[d] += t;
-        __syncthreads();
-    }
-    const uint32_t base = s[d] - run;
-    if (count && d == RS_BINS - 1) *count = s[d];
-    for (uint32_t c = 0; c < nchunks; c++) chunk[(size_t)c * RS_BINS + d] += base;
+    rs_publish_and_scan(h, blockIdx.x, ntiles, hist, chunk, ctr, count);
 }
 
 // Each wave owns a contiguous eighth of the tile (1024 entries, 16 rounds of 64), so ranking is
@@ -279,6 +320,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(RsIn in, const uint32
         const uint32_t k = skey[i];
         const uint32_t dg = (k >> in.shift) & 255u;
         const uint32_t g = goff[dg] + (i - lstart[dg]);
+        if (g >= in.E) continue;  // inconsistent offsets: never write outside the arrays
         keys_out[g] = k;
         vals_out[g] = sval[i];
     }
@@ -402,8 +444,14 @@ int msm_radix_sort(const uint32_t* digits, size_t E, size_t npw, uint32_t B, uin
     HALO_CHECK(S.vals[0].reserve(std::max<size_t>(E, 1) * 4));
     HALO_CHECK(S.vals[1].reserve(std::max<size_t>(E, 1) * 4));
     HALO_CHECK(S.hist.reserve((size_t)RS_BINS * ntmax * 4));
-    HALO_CHECK(S.offs.reserve((size_t)((ntmax + RS_CH - 1) / RS_CH) * RS_BINS * 4));
+    const size_t nchmax = (ntmax + RS_CH - 1) / RS_CH;
+    HALO_CHECK(S.offs.reserve(nchmax * RS_BINS * 4));
     HALO_CHECK(S.count.reserve(16));
+    // the last-arriver counters start at zero and are reset by their last arrivers
+    // (a reallocation may return the freed address: the capacity, not the pointer, tells)
+    const size_t ctr_had = S.ctr.bytes;
+    HALO_CHECK(S.ctr.reserve((nchmax + 1) * 4));
+    if (S.ctr.bytes != ctr_had) HALO_HIP(hipMemsetAsync(S.ctr.ptr, 0, S.ctr.bytes, s));
     const uint32_t passes = std::max<uint32_t>(1, (key_bits + 7) / 8);
     int cur = 0;
     for (uint32_t p = 0; p < passes; p++) {
@@ -419,25 +467,22 @@ int msm_radix_sort(const uint32_t* digits, size_t E, size_t npw, uint32_t B, uin
         in.shift = 8 * p;
         const bool fp = fused && p == 0;
         const uint32_t nt = fp ? ntiles0 : ntiles;
-        const uint32_t nchunks = (nt + RS_CH - 1) / RS_CH;
         if (fp) {
             in.sc = (const uint4*)fused->scalars;
             in.n_sc = (uint32_t)fused->n;
             in.c = fused->c;
             in.W = fused->W;
             DISPATCH_FIELD(fused->field, SF, {
-                hipLaunchKernelGGL(k_rs_hist_sc<SF>, dim3(nt), dim3(RS_THREADS), 0, s, in.sc, in.n_sc, in.c, in.W,
-                                   S.hist.as<uint32_t>());
+                hipLaunchKernelGGL(k_rs_hist_sc<SF>, dim3(nt), dim3(RS_THREADS), 0, s, in.sc, in.n_sc, in.c, in.W, nt,
+                                   S.hist.as<uint32_t>(), S.offs.as<uint32_t>(), S.ctr.as<uint32_t>(),
+                                   S.count.as<uint32_t>());
             });
         } else {
+            // pass 0 also stores the number of valid (nonzero-digit) entries
             hipLaunchKernelGGL(small_tiles ? k_rs_hist<8> : k_rs_hist<16>, dim3(nt), dim3(RS_THREADS), 0, s, in, nt,
-                               S.hist.as<uint32_t>());
+                               S.hist.as<uint32_t>(), S.offs.as<uint32_t>(), S.ctr.as<uint32_t>(),
+                               p == 0 ? S.count.as<uint32_t>() : nullptr);
         }
-        hipLaunchKernelGGL(k_rs_colscan, dim3(nchunks), dim3(RS_BINS), 0, s, S.hist.as<uint32_t>(), nt,
-                           S.offs.as<uint32_t>());
-        // pass 0 also stores the number of valid (nonzero-digit) entries
-        hipLaunchKernelGGL(k_rs_chunkscan, dim3(1), dim3(RS_BINS), 0, s, S.offs.as<uint32_t>(), nchunks,
-                           p == 0 ? S.count.as<uint32_t>() : nullptr);
         if (fp) {
             DISPATCH_FIELD(fused->field, SF, {
                 hipLaunchKernelGGL((k_rs_scatter<16, SF>), dim3(nt), dim3(RS_THREADS), 0, s, in,

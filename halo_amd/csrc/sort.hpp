@@ -5,7 +5,7 @@
 namespace halo {
 
 struct SortScratch {
-    DevBuf keys[2], vals[2], hist, offs, count, scan_tmp;
+    DevBuf keys[2], vals[2], hist, offs, count, scan_tmp, ctr;
 };
 
 // Exclusive scan of n u32 values: out[0..n) exclusive prefix, out[n] = total.

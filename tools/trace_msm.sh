@@ -3,7 +3,7 @@ cd $GRAFT_REPO_ROOT
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 O=gpurun_out/tl_${1:-a}
 rm -rf $O && mkdir -p $O
-timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $O/t -o run -- python3 bench.py --no-cpu --sizes "" --ipa 0 --prove 0 --steps 10 --warmup 2 > $O/log 2>&1 || { tail -20 $O/log; exit 1; }
+timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $O/t -o run -- python3 bench.py --no-cpu --sizes "" --ipa 0 --prove 0 --varbase 0 --commit-batch 0 --pcdl "" --steps 10 --warmup 2 > $O/log 2>&1 || { tail -20 $O/log; exit 1; }
 f=$(find $O/t -name "*kernel_trace.csv" | head -1)
 python3 - "$f" > $O/timeline.txt <<'PY'
 import csv, sys
