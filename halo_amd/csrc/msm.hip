@@ -369,6 +369,12 @@ int msm_windows(int c) { return (255 + c - 1) / c; }
 // saves a window (c = 17 at 2^20: 15 windows instead of 16; the single bucket set of 2^16 buckets
 // keeps the reduction and the 2-pass sort cheap)
 int msm_shifted_window_bits(size_t n) {
+    static const int c_env = [] {  // HALO_SHIFT_C: window bits of the shifted copies (A/B, 8..20)
+        const char* e = getenv("HALO_SHIFT_C");
+        const int v = e ? atoi(e) : 0;
+        return (v >= 8 && v <= 20) ? v : 0;
+    }();
+    if (c_env) return c_env;
     const int c = msm_window_bits(n);
     return (msm_windows(c + 1) < msm_windows(c) && c + 1 <= 17) ? c + 1 : c;
 }
