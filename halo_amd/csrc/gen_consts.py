@@ -44,6 +44,7 @@ def field_block(struct: str, p: int) -> str:
     out.append(arr("INT2ARK", (1 << 256) % p))             # internal -> ark Montgomery
     out.append(arr("ARK_MUL_FIX", (1 << 266) % p))         # ark x ark through R' = 2^261 -> ark
     out.append(arr("ARK2CANON", 32))                        # ark Montgomery -> canonical integer
+    out.append(arr("INV_FIX", pow(RP, 3, p)))              # fe_inv: (x R')^-1 -> x^-1 R'
     # NTT domain constants: omega_N = 5^((p-1)/N) for N = 2^k, internal Montgomery form
     om = [pow(5, (p - 1) >> k, p) for k in range(MAXLOG + 1)]
     omi = [pow(w, -1, p) for w in om]
