@@ -119,12 +119,17 @@ HALO_DEV void rs_publish_and_scan(const uint32_t* h, uint32_t tile, uint32_t nti
     if (d == 0) __hip_atomic_store(ctr + ch, 0u, RS_RLX_AGENT);
     if (!rs_last_arriver(ctr + nchunks, nchunks, &flag)) return;
     rs_acquire();
+    // per digit: total over the chunks, then (after the digit scan) the chunks' exclusive prefix plus
+    // the digit's base; the loads go in batches of U so their latencies overlap
+    constexpr uint32_t U = 16;
     if (d < RS_BINS) {
         uint32_t run = 0;
-        for (uint32_t c = 0; c < nchunks; c++) {
-            const uint32_t v = chunk[(size_t)c * RS_BINS + d];
-            chunk[(size_t)c * RS_BINS + d] = run;
-            run += v;
+        for (uint32_t c0 = 0; c0 < nchunks; c0 += U) {
+            uint32_t v[U];
+#pragma unroll
+            for (uint32_t i = 0; i < U; i++) v[i] = (c0 + i < nchunks) ? chunk[(size_t)(c0 + i) * RS_BINS + d] : 0u;
+#pragma unroll
+            for (uint32_t i = 0; i < U; i++) run += v[i];
         }
         s[d] = run;
     }
@@ -152,8 +157,19 @@ HALO_DEV void rs_publish_and_scan(const uint32_t* h, uint32_t tile, uint32_t nti
         if (d == 63 && count) *count = incl;
     }
     __syncthreads();
-    if (d < RS_BINS)
-        for (uint32_t c = 0; c < nchunks; c++) chunk[(size_t)c * RS_BINS + d] += s[d];
+    if (d < RS_BINS) {
+        uint32_t run = s[d];
+        for (uint32_t c0 = 0; c0 < nchunks; c0 += U) {
+            uint32_t v[U];
+#pragma unroll
+            for (uint32_t i = 0; i < U; i++) v[i] = (c0 + i < nchunks) ? chunk[(size_t)(c0 + i) * RS_BINS + d] : 0u;
+#pragma unroll
+            for (uint32_t i = 0; i < U; i++) {
+                if (c0 + i < nchunks) chunk[(size_t)(c0 + i) * RS_BINS + d] = run;
+                run += v[i];
+            }
+        }
+    }
     if (d == 0) __hip_atomic_store(ctr + nchunks, 0u, RS_RLX_AGENT);
 }
 

@@ -2,21 +2,33 @@
 # gpurun_out/evid_<tag>/ (merged back by gpurun), then copied into profiles/ locally:
 #   bench.json           default bench.py line (with the CPU baseline)
 #   kernel_stats.csv     rocprofv3 --kernel-trace --stats of the 2^20 MSM + 2^22 NTT bench
-#   bench_traced.json    the bench line of that traced run
-#   pmc_summary.json     FETCH_SIZE / WRITE_SIZE per dispatch (separate --pmc passes)
+#   kstats.txt           its per-kernel table (tools/kstats.py)
+#   bench_traced.json    the bench line of that traced run; trace_exit.txt its exit status
+#   pmc_summary.json     FETCH_SIZE / WRITE_SIZE per dispatch (separate --pmc passes), stamped with
+#                        the library's sha256 (bench.py uses it as roofline.traffic only if it matches)
+#   pmc_kernels.txt      per-kernel SQ / LDS / HBM counters of the MSM kernels (tools/pmc_kernels.sh)
+#   prove_kstats.txt     kernel statistics of the 2^20 naive_prover pipeline (tools/prof_prove.sh)
 set -o pipefail
-tag=${1:-r01}
+tag=${1:-r02}
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/evid_${tag}
 rm -rf $O && mkdir -p $O
-timeout -k 10 400 python bench.py > $O/bench_full.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+LEGS='--varbase 0 --commit-batch 0 --pcdl'
+timeout -k 10 500 python bench.py > $O/bench_full.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
 tail -n 1 $O/bench_full.json > $O/bench.json
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 bench.py --no-cpu --sizes "" --ipa 0 --prove 0 > $O/trace.log 2>&1 || { tail -20 $O/trace.log; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 bench.py --no-cpu --sizes "" --ipa 0 --prove 0 $LEGS "" > $O/trace.log 2>&1
+rc=$?; echo "rocprofv3 --kernel-trace exit status: $rc" > $O/trace_exit.txt
+grep -n -i "segmentation\|core dumped\|abort" $O/trace.log >> $O/trace_exit.txt || true
+[ $rc -eq 0 ] || { tail -20 $O/trace.log; exit 1; }
 cp $(find $O/trace -name "*kernel_stats.csv" | head -1) $O/kernel_stats.csv
 grep '^{' $O/trace.log | tail -n 1 > $O/bench_traced.json
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_f -o run -- python3 bench.py --no-cpu --sizes "" --ipa 0 --prove 0 --steps 3 --warmup 1 > /dev/null 2>&1 || exit 1
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_w -o run -- python3 bench.py --no-cpu --sizes "" --ipa 0 --prove 0 --steps 3 --warmup 1 > /dev/null 2>&1 || exit 1
-python3 tools/make_pmc_summary.py $O/pmc_f $O/pmc_w $O/pmc_summary.json "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes) of 'python3 bench.py --no-cpu --sizes \"\" --ipa 0 --prove 0 --steps 3 --warmup 1', ${tag}" > /dev/null
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_f -o run -- python3 bench.py --no-cpu --sizes "" --ipa 0 --prove 0 $LEGS "" --steps 3 --warmup 1 > /dev/null 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_w -o run -- python3 bench.py --no-cpu --sizes "" --ipa 0 --prove 0 $LEGS "" --steps 3 --warmup 1 > /dev/null 2>&1 || exit 1
+python3 tools/make_pmc_summary.py $O/pmc_f $O/pmc_w $O/pmc_summary.json "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes) of 'python3 bench.py --no-cpu --sizes \"\" --ipa 0 --prove 0 $LEGS \"\" --steps 3 --warmup 1', ${tag}" > /dev/null
 rm -rf $O/trace $O/pmc_f/*/ $O/pmc_w/*/ 2>/dev/null
-python3 tools/kstats.py $O/kernel_stats.csv > $O/kstats.txt; head -n 30 $O/kstats.txt
+python3 tools/kstats.py $O/kernel_stats.csv > $O/kstats.txt
+bash tools/pmc_kernels.sh $tag > /dev/null && cp gpurun_out/pmc_k/$tag/summary.txt $O/pmc_kernels.txt
+rm -rf gpurun_out/pmc_k/$tag/[a-e]
+bash tools/prof_prove.sh 20 > /dev/null && cp gpurun_out/prof_prove/kstats.txt $O/prove_kstats.txt
+head -n 30 $O/kstats.txt
