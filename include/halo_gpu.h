@@ -156,8 +156,9 @@ int halo_msm_join(void* stream);
  * d_out + 64 i.  Replaces a loop of pcdl::commit / pedersen::commit calls over one SRS -- the
  * reference's commitment batches (crates/plonk/src/plonk/protocol.rs:114,263 -- 16 commits each;
  * crates/plonk/src/plonk/trace.rs:188-192).  All inputs must be ready on `stream` at the call;
- * asynchronous like halo_msm_dev_async (halo_msm_join before reading d_out).  Inside the batch the
- * digit extraction and bucket sort of MSM i+1 run on a side stream beside MSM i's accumulation. */
+ * asynchronous like halo_msm_dev_async (halo_msm_join before reading d_out).  Polynomials of up to
+ * 2^18 coefficients (HALO_MSM_MULTI_MAX) form ONE MSM whose sort keys are (polynomial, bucket); longer
+ * ones run as back-to-back pipelined MSMs. */
 int halo_msm_batch_dev(halo_curve_t curve, const void* const* d_scalars, const size_t* lens, size_t k, void* d_out,
                        void* stream);
 /* Window-partitioned MSM (BASELINE configs[4]): one rank's share -- the signed digits of windows
