@@ -387,6 +387,27 @@ int msm_window_bits(size_t n) {
 
 static unsigned grid_for(size_t n, unsigned thr) { return (unsigned)std::max<size_t>(1, (n + thr - 1) / thr); }
 
+// Chunk length K of k_acc for E sorted entries.  Large MSMs (E > 16 x the resident lanes, 256 CUs x
+// 16 waves x 64): >= 4 rounds of resident lanes, 16 <= K <= 64 -- every lane does the same number
+// of mixed additions, and several rounds absorb the CU slots held by the previous MSM's tail kernels,
+// which one exact round would not (measured: K = 60 at 2^20 is 1 round and 15 % slower than K = 16).
+// Smaller MSMs are latency-bound (a commitment, an IPA round): their critical path is a lane's K
+// dependent additions in k_acc plus k_merge's run of about E / (NB K) partials per bucket, so K =
+// ceil(sqrt(E / NB)) balances the two -- but at least ceil(E / resident lanes), one round.
+// HALO_ACC_K overrides.
+static uint32_t msm_chunk_len(const DeviceState* st, size_t E, size_t NB) {
+    static const uint32_t k_env = [] {
+        const char* e = getenv("HALO_ACC_K");
+        return e ? (uint32_t)atoi(e) : 0u;
+    }();
+    if (k_env) return k_env;
+    const size_t resident = (size_t)st->num_cu * 16 * 64;
+    if (E > 16 * resident) return (uint32_t)std::max<size_t>(16, std::min<size_t>(64, (E + 4 * resident - 1) / (4 * resident)));
+    size_t k = 1;
+    while (k * k * std::max<size_t>(NB, 1) < E) k++;
+    return (uint32_t)std::min<size_t>(16, std::max<size_t>(k, (E + resident - 1) / resident));
+}
+
 // Four scratch sets in two slots of two, a slot per issuing stream (least recently used slot
 // reassigned): consecutive MSMs of one stream alternate between their slot's two sets (the tail of
 // k overlaps k+1), two concurrent streams (two IPA openings in lockstep) never wait for each
@@ -561,17 +582,8 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
     const uint32_t key_bits = NB > 1 ? ilog2(NB - 1) + 1 : 1;
     HALO_CHECK(M.digits.reserve((size_t)W * NP * 4));
     HALO_CHECK(M.bstart.reserve((NB + 1) * 4));
-    // chunk length K: >= 4 rounds of resident lanes (256 CUs x 16 waves x 64), 16 <= K <= 64.  Every
-    // lane does the same number of mixed additions; several rounds absorb the CU slots held by the
-    // previous MSM's tail kernels, which one exact round would not (measured: K = 60 at 2^20 is 1
-    // round and 15% slower than K = 16).
     const size_t E = (size_t)W * NP;
-    const size_t lanes = (size_t)st->num_cu * 16 * 64 * 4;
-    static const uint32_t k_env = [] {
-        const char* e = getenv("HALO_ACC_K");
-        return e ? (uint32_t)atoi(e) : 0u;
-    }();
-    const uint32_t K = k_env ? k_env : (uint32_t)std::max<size_t>(16, std::min<size_t>(64, (E + lanes - 1) / lanes));
+    const uint32_t K = msm_chunk_len(st, E, NB);
     const size_t nchunks = (E + K - 1) / K;
     const size_t ng1 = nchunks / MSM_GROUP, ng2 = nchunks / (MSM_GROUP * MSM_GROUP);
     HALO_CHECK(M.partials.reserve((std::max<size_t>(nchunks, 1) * 2 + ng1 + ng2 + 2) * 128));
@@ -725,8 +737,7 @@ static int msm_multi_device_t(DeviceState* st, const void* const* scalars, const
     const uint32_t L = std::min<uint32_t>(MSM_SEG_L, B), logL = ilog2(L), H = B / L, logH = ilog2(H);
     const uint32_t NT = 1 + logH + logL;
     const uint32_t key_bits = ilog2(NB - 1) + 1;
-    const size_t lanes = (size_t)st->num_cu * 16 * 64 * 4;
-    const uint32_t K = (uint32_t)std::max<size_t>(16, std::min<size_t>(64, (E + lanes - 1) / lanes));
+    const uint32_t K = msm_chunk_len(st, E, NB);
     const size_t nchunks = (E + K - 1) / K;
     const size_t ng1 = nchunks / MSM_GROUP, ng2 = nchunks / (MSM_GROUP * MSM_GROUP);
     HALO_CHECK(M.digits.reserve(E * 4));
@@ -982,8 +993,7 @@ static int msm_shared_batch_t(DeviceState* st, const uint4* bases, const uint4* 
         return set_error(HALO_EINVAL, "msm_shared_batch: batch too large (len %zu, T %zu)", len, T);
     const uint32_t L = std::min<uint32_t>(MSM_SEG_L, B), logL = ilog2(L), H = B / L, logH = ilog2(H);
     const uint32_t NT = 1 + logH + logL;
-    const size_t lanes = (size_t)st->num_cu * 16 * 64 * 4;
-    const uint32_t K = (uint32_t)std::max<size_t>(16, std::min<size_t>(64, (E + lanes - 1) / lanes));
+    const uint32_t K = msm_chunk_len(st, E, NB);
     const size_t nchunks = (E + K - 1) / K;
     const size_t ng1 = nchunks / MSM_GROUP, ng2 = nchunks / (MSM_GROUP * MSM_GROUP);
     HALO_CHECK(S.digits.reserve((size_t)W * T * 4));
