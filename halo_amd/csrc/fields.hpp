@@ -624,13 +624,14 @@ HALO_DEV Fe<C> fe_inv(const Fe<C>& x) {
     for (int it = 0; it < ROUNDS; it++) {
         const int n = max(max(bgcd::bitlen8(a), bgcd::bitlen8(b)), 62);
         uint64_t ab = bgcd::approx(a, n), bb = bgcd::approx(b, n);
-        int64_t f0 = 1, g0 = 0, f1 = 0, g1 = 1;
+        // |f|, |g| <= 2^30 after the 30 steps (Pornin, sec. 3): 32-bit registers
+        int32_t f0 = 1, g0 = 0, f1 = 0, g1 = 1;
 #pragma unroll 2
         for (int j = 0; j < 30; j++) {
             const bool odd = ab & 1u;
             const bool sw = odd && ab < bb;
             const uint64_t ta = sw ? bb : ab, tb = sw ? ab : bb;
-            const int64_t tf0 = sw ? f1 : f0, tg0 = sw ? g1 : g0, tf1 = sw ? f0 : f1, tg1 = sw ? g0 : g1;
+            const int32_t tf0 = sw ? f1 : f0, tg0 = sw ? g1 : g0, tf1 = sw ? f0 : f1, tg1 = sw ? g0 : g1;
             ab = (odd ? ta - tb : ta) >> 1;
             bb = tb;
             f0 = odd ? tf0 - tf1 : tf0;
