@@ -206,6 +206,39 @@ def test_msm_2p20_all_equal_scalars_shifted(hal):
     assert list(got) == P.point_to_wrapped(c, P.mul_fast(c, acc, c.generator))
 
 
+@pytest.mark.gpu
+def test_msm_small_chunks_shifted_skew(hal):
+    """Latency-bound MSMs over the 2^20 window-shifted SRS take short accumulation chunks (K =
+    ceil(sqrt(entries / buckets)), msm.hip msm_chunk_len): random, all-equal, two-valued and mostly
+    zero scalars at n = 2^4 .. 2^16, checked against (sum_j s_j k_j) G."""
+    c = P.PALLAS
+    r = c.scalar
+    N = 1 << 20
+    seed = 11
+    group.PublicParams.synthesize("pallas", N, seed, precompute_windows=True)
+    k = synth_scalars_np(seed, 1 << 16)
+    kb = k.tobytes()
+    ks = [int.from_bytes(kb[32 * j:32 * j + 32], "little") for j in range(1 << 16)]
+    inv_r = pow(1 << 256, -1, r)
+    rng = np.random.default_rng(4)
+    for lg in (4, 9, 12, 16):
+        n = 1 << lg
+        cases = {"random": rand_sc(n, lg)}
+        cases["equal"] = np.ascontiguousarray(np.repeat(fe([r - 99], r)[0][None, :], n, axis=0))
+        two = cases["equal"].copy()
+        two[n // 2:] = fe([(1 << 201) + 3], r)[0]
+        cases["two"] = two
+        sparse = np.zeros((n, 4), dtype=np.uint64)
+        idx = rng.choice(n, size=max(1, n // 64), replace=False)
+        sparse[idx] = rand_sc(len(idx), lg + 100)
+        cases["sparse"] = sparse
+        for name, sc in cases.items():
+            got = pcdl.commit(sc, n - 1, None, "pallas")
+            sb = sc.tobytes()
+            acc = sum(int.from_bytes(sb[32 * j:32 * j + 32], "little") * ks[j] for j in range(n)) * inv_r % r
+            assert list(got) == P.point_to_wrapped(c, P.mul_fast(c, acc, c.generator)), (lg, name)
+
+
 def synth_scalars_np(seed: int, n: int) -> np.ndarray:
     """numpy restatement of halo_synth_scalar (splitmix64 stream per index; top word masked)."""
     M = np.uint64(0xFFFFFFFFFFFFFFFF)
