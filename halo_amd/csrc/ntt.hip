@@ -165,7 +165,11 @@ HALO_DEV Fe<F> ntt_tw_unpack(const uint4 (&w)[2]) {
     uint32_t x[8] = {w[0].x, w[0].y, w[0].z, w[0].w, w[1].x, w[1].y, w[1].z, w[1].w};
     return fe_unpack<F>(x);
 }
-// ntt_group for EPT = 4, LG = 2, s >= 1 with the twiddles already loaded (same arithmetic and bounds)
+// ntt_group for EPT = 4, LG = 2, s >= 1 with the twiddles already loaded (same arithmetic and value
+// bounds).  The first stage's sums stay limb-unnormalized (limbs < 2^30): the second stage takes them
+// as a multiplication input (a column of 9 products < 2^59 plus the reduction stays < 2^63) or as the
+// minuend of fe_sub_k (int32 limb chain, |x| < 2^31), and only the values leaving the group are
+// carry-normalized -- two fe_norm per group instead of four.
 template <class F>
 HALO_DEV void ntt_group4_pre(Fe<F> (&v)[4], uint32_t G, const NttGroupTw& t) {
     {
@@ -174,7 +178,7 @@ HALO_DEV void ntt_group4_pre(Fe<F> (&v)[4], uint32_t G, const NttGroupTw& t) {
         for (int m = 0; m < 4; m += 2) {
             const Fe<F> x = fe_mul(v[m + 1], w);
             v[m + 1] = fe_sub_k<2>(v[m], x);
-            v[m] = fe_norm(fe_add_nc(v[m], x));
+            v[m] = fe_add_nc(v[m], x);
         }
     }
     if (G > 1) {
@@ -184,6 +188,9 @@ HALO_DEV void ntt_group4_pre(Fe<F> (&v)[4], uint32_t G, const NttGroupTw& t) {
             v[m + 2] = fe_sub_k<2>(v[m], x);
             v[m] = fe_norm(fe_add_nc(v[m], x));
         }
+    } else {
+        v[0] = fe_norm(v[0]);
+        v[2] = fe_norm(v[2]);
     }
 }
 
