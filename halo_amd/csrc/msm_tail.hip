@@ -44,13 +44,16 @@ __global__ __launch_bounds__(MSM_GROUP) void k_group_sums(const uint32_t* keys, 
 }
 
 // Buckets that touch a chunk boundary (or are empty): bucket b's entries [s, e) lie in chunks
-// t0 = s / K .. t1 = (e - 1) / K; chunk t contributes first[t] when b is its first segment, else
-// last[t]; whole groups strictly inside (t0, t1) come from the group sums.  A bucket strictly
-// inside one chunk was written by k_acc.
+// t0 = s / K .. t1 = (e - 1) / K.  Chunk t0 contributes first[t0] when the bucket starts it (s = t0 K),
+// else last[t0]; every later chunk t <= t1 starts inside the bucket, so it contributes first[t] -- no
+// key lookups, the sources follow from s, e and K alone; whole aligned groups strictly inside (t0, t1]
+// come from the group sums.  A bucket strictly inside one chunk was written by k_acc.  The loop is
+// software-pipelined: the next source's 128 B are loaded before the current addition, so each
+// step's memory latency hides under the previous addition (the lane's chain is latency-bound).
 template <class Cv>
-__global__ __launch_bounds__(256) void k_merge(const uint32_t* bstart, const uint32_t* keys, const uint32_t* count,
-                                               uint32_t K, size_t nb, const uint4* first, const uint4* last,
-                                               const uint4* g1, const uint4* g2, uint4* bucket_sums) {
+__global__ __launch_bounds__(256) void k_merge(const uint32_t* bstart, const uint32_t* count, uint32_t K, size_t nb,
+                                               const uint4* first, const uint4* last, const uint4* g1, const uint4* g2,
+                                               uint4* bucket_sums) {
     using F = typename Cv::Base;
     const size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= nb) return;
@@ -61,14 +64,11 @@ __global__ __launch_bounds__(256) void k_merge(const uint32_t* bstart, const uin
     }
     const uint32_t cnt = *count;
     const uint32_t t0 = s / K, t1 = (e - 1) / K;
-    auto chunk_last = [&](uint32_t t) { return min(cnt, (t + 1) * K) - 1; };
-    if (t0 == t1 && keys[(size_t)t0 * K] != b && keys[chunk_last(t0)] != b) return;  // interior: done
+    const bool starts = s == t0 * K;  // the bucket is chunk t0's first segment
+    if (t0 == t1 && !starts && e < min(cnt, (t0 + 1) * K)) return;  // interior: done by k_acc
     constexpr uint32_t G2 = MSM_GROUP * MSM_GROUP;
-    // chunk t0's partial starts the sum (no addition to the identity); the loop picks each further
-    // source first, then runs ONE addition, so lanes that take different sources do not execute
-    // several inlined copies of it
-    XYZZ<F> acc = xyzz_load<F>(((keys[(size_t)t0 * K] == b) ? first : last) + 8 * (size_t)t0);
-    for (uint32_t t = t0 + 1; t <= t1;) {
+    uint32_t t = t0 + 1;
+    auto next_src = [&]() -> const uint4* {
         const uint4* src;
         if (t % G2 == 0 && t + G2 <= t1) {
             src = g2 + 8 * (size_t)(t / G2);
@@ -77,10 +77,23 @@ __global__ __launch_bounds__(256) void k_merge(const uint32_t* bstart, const uin
             src = g1 + 8 * (size_t)(t / MSM_GROUP);
             t += MSM_GROUP;
         } else {
-            src = ((keys[(size_t)t * K] == b) ? first : last) + 8 * (size_t)t;
+            src = first + 8 * (size_t)t;
             t++;
         }
-        acc = xyzz_add(acc, xyzz_load<F>(src));
+        return src;
+    };
+    // chunk t0's partial starts the sum (no addition to the identity); one addition per step, so
+    // lanes that take different sources do not execute several inlined copies of it
+    XYZZ<F> acc = xyzz_load<F>((starts ? first : last) + 8 * (size_t)t0);
+    if (t <= t1) {
+        XYZZ<F> nxt = xyzz_load<F>(next_src());
+        for (;;) {
+            const XYZZ<F> cur = nxt;
+            const bool more = t <= t1;
+            if (more) nxt = xyzz_load<F>(next_src());
+            acc = xyzz_add(acc, cur);
+            if (!more) break;
+        }
     }
     xyzz_store(bucket_sums + 8 * b, acc);
 }
@@ -241,7 +254,7 @@ static int tail_launch_t(const MsmTailArgs& a, hipStream_t ts) {
             hipLaunchKernelGGL(k_group_sums<Cv>, dim3((unsigned)a.ng2), dim3(MSM_GROUP), 0, ts, a.skeys, a.scount, a.K,
                                MSM_GROUP, (const uint4*)a.g1, a.g2);
         hipLaunchKernelGGL(k_merge<Cv>, dim3(grid_for_t(a.NB, 256)), dim3(256), 0, ts, (const uint32_t*)a.bstart,
-                           a.skeys, a.scount, a.K, a.NB, (const uint4*)a.first, (const uint4*)a.last,
+                           a.scount, a.K, a.NB, (const uint4*)a.first, (const uint4*)a.last,
                            (const uint4*)a.g1, (const uint4*)a.g2, a.bucket_sums);
         if (a.batch_windows) {
             const uint32_t B = a.L * a.H;
