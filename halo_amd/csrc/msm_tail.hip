@@ -22,6 +22,49 @@
 
 namespace halo {
 
+// ---------------------------------------------------------------------------------------------
+// Tree sums of XYZZ points across lanes.  Inside a wave the partner's point comes over the lane
+// crossbar (__shfl_xor: 36 dwords, no LDS round trip, no barrier), so each level costs one addition;
+// only the wave sums of a group wider than a wave meet in LDS.  Every lane of the wave must call
+// these (idle lanes pass the identity).
+// ---------------------------------------------------------------------------------------------
+template <class F>
+HALO_DEV XYZZ<F> xyzz_shfl_xor(const XYZZ<F>& p, int m) {
+    XYZZ<F> r;
+#pragma unroll
+    for (int l = 0; l < NLIMB; l++) {
+        r.X.v[l] = __shfl_xor(p.X.v[l], m);
+        r.Y.v[l] = __shfl_xor(p.Y.v[l], m);
+        r.ZZ.v[l] = __shfl_xor(p.ZZ.v[l], m);
+        r.ZZZ.v[l] = __shfl_xor(p.ZZZ.v[l], m);
+    }
+    return r;
+}
+// every lane gets the sum over its aligned group of G lanes (G a power of two <= 64)
+template <class F>
+HALO_DEV XYZZ<F> wave_group_sum(XYZZ<F> v, uint32_t G) {
+    for (uint32_t m = G >> 1; m > 0; m >>= 1) v = xyzz_add(v, xyzz_shfl_xor(v, (int)m));
+    return v;
+}
+// sum over aligned groups of G threads (G a power of two <= blockDim): valid in the group's first
+// thread.  While a group spans several waves its upper half hands its points to the lower half
+// through LDS (the number of waves that add halves each level, as in an LDS tree), then the last
+// wave of each group finishes with lane shuffles (no barriers).  red: LDS scratch for blockDim / 2
+// points.  Every thread of the block must call it.
+template <class F>
+HALO_DEV XYZZ<F> block_group_sum(XYZZ<F> v, uint32_t G, uint4* red) {
+    const uint32_t gpos = threadIdx.x & (G - 1), gbase = threadIdx.x - gpos;
+    for (uint32_t span = G; span > 64; span >>= 1) {  // active: gpos < span (wave-uniform tests)
+        const uint32_t half = span >> 1;
+        if (gpos >= half && gpos < span) xyzz_store(red + 8 * ((gbase >> 1) + gpos - half), v);
+        __syncthreads();
+        if (gpos < half) v = xyzz_add(v, xyzz_load<F>(red + 8 * ((gbase >> 1) + gpos)));
+        __syncthreads();
+    }
+    if (gpos < 64) v = wave_group_sum<F>(v, G < 64 ? G : 64u);
+    return v;
+}
+
 // Skew guard: sums of MSM_GROUP consecutive chunk partials whose entries all belong to one bucket
 // (level 1: groups of 64 chunks from first[]; level 2: groups of 64 level-1 groups), so that a huge
 // bucket (all-equal scalars) is merged in O(chunks / 4096 + 128) sequential adds, not O(chunks).
@@ -29,18 +72,13 @@ template <class Cv>
 __global__ __launch_bounds__(MSM_GROUP) void k_group_sums(const uint32_t* keys, const uint32_t* count, uint32_t K,
                                                           uint32_t span, const uint4* src, uint4* out) {
     using F = typename Cv::Base;
-    __shared__ uint4 red[MSM_GROUP * 8];
+    static_assert(MSM_GROUP == 64, "one wave per group");
     const uint32_t g = blockIdx.x, i = threadIdx.x;
     const uint32_t cnt = *count;
     const size_t e0 = (size_t)g * MSM_GROUP * span * K, e1 = e0 + (size_t)MSM_GROUP * span * K;
-    if (e1 > cnt || keys[e0] != keys[e1 - 1]) return;  // not one bucket throughout: never used
-    xyzz_store(red + 8 * i, xyzz_load<F>(src + 8 * ((size_t)g * MSM_GROUP + i)));
-    for (uint32_t off = MSM_GROUP / 2; off > 0; off >>= 1) {
-        __syncthreads();
-        if (i < off) xyzz_store(red + 8 * i, xyzz_add(xyzz_load<F>(red + 8 * i), xyzz_load<F>(red + 8 * (i + off))));
-    }
-    __syncthreads();
-    if (i == 0) xyzz_store(out + 8 * (size_t)g, xyzz_load<F>(red));
+    if (e1 > cnt || keys[e0] != keys[e1 - 1]) return;  // not one bucket throughout: never used (uniform)
+    const XYZZ<F> v = wave_group_sum<F>(xyzz_load<F>(src + 8 * ((size_t)g * MSM_GROUP + i)), 64);
+    if (i == 0) xyzz_store(out + 8 * (size_t)g, v);
 }
 
 // Buckets that touch a chunk boundary (or are empty): bucket b's entries [s, e) lie in chunks
@@ -109,46 +147,30 @@ __global__ __launch_bounds__(256) void k_merge(const uint32_t* bstart, const uin
 //    sums, depth ~12); k_bitcombine: lane k doubles its term (<= log B times), then a tree sum.
 //    ~2.1 B adds in total at depth ~40 (a running-sum reduction needs 2 B adds at depth 2 B / #threads).
 // ---------------------------------------------------------------------------------------------
-template <class F>
-HALO_DEV void lds_tree_sum(uint4* red, uint32_t tid, uint32_t n) {  // red[0] = sum of red[0..n), n pow2
-    for (uint32_t off = n >> 1; off > 0; off >>= 1) {
-        __syncthreads();
-        if (tid < off) xyzz_store(red + 8 * tid, xyzz_add(xyzz_load<F>(red + 8 * tid), xyzz_load<F>(red + 8 * (tid + off))));
-    }
-    __syncthreads();
-}
-
 // grid (ceil(H / (256 / L)) + L, SW), 256 threads
 template <class Cv>
 __global__ __launch_bounds__(256) void k_rowcol(const uint4* bucket_sums, uint32_t L, uint32_t H, uint4* rows,
                                                 uint4* cols) {
     using F = typename Cv::Base;
-    __shared__ uint4 red[256 * 8];
+    __shared__ uint4 red[128 * 8];
     const uint32_t w = blockIdx.y, tid = threadIdx.x;
     const uint32_t B = L * H;
     const uint4* bs = bucket_sums + 8 * (size_t)w * B;
     const uint32_t rpb = 256 / L;  // rows per block
     const uint32_t nrb = (H + rpb - 1) / rpb;
-    if (blockIdx.x < nrb) {
+    if (blockIdx.x < nrb) {  // (uniform per block)
         const uint32_t h = blockIdx.x * rpb + tid / L, l = tid % L;
         XYZZ<F> v = xyzz_id<F>();
         if (h < H) v = xyzz_load<F>(bs + 8 * ((size_t)h * L + l));
-        xyzz_store(red + 8 * tid, v);
         // tree over the L lanes of each row (rows are contiguous groups of L threads)
-        for (uint32_t off = L >> 1; off > 0; off >>= 1) {
-            __syncthreads();
-            if (l < off)
-                xyzz_store(red + 8 * tid, xyzz_add(xyzz_load<F>(red + 8 * tid), xyzz_load<F>(red + 8 * (tid + off))));
-        }
-        __syncthreads();
-        if (l == 0 && h < H) xyzz_store(rows + 8 * ((size_t)w * H + h), xyzz_load<F>(red + 8 * tid));
+        v = block_group_sum<F>(v, L, red);
+        if (l == 0 && h < H) xyzz_store(rows + 8 * ((size_t)w * H + h), v);
     } else {
         const uint32_t l = blockIdx.x - nrb;
         XYZZ<F> acc = xyzz_id<F>();
         for (uint32_t h = tid; h < H; h += 256) acc = xyzz_add(acc, xyzz_load<F>(bs + 8 * ((size_t)h * L + l)));
-        xyzz_store(red + 8 * tid, acc);
-        lds_tree_sum<F>(red, tid, 256);
-        if (tid == 0) xyzz_store(cols + 8 * ((size_t)w * L + l), xyzz_load<F>(red));
+        acc = block_group_sum<F>(acc, 256, red);
+        if (tid == 0) xyzz_store(cols + 8 * ((size_t)w * L + l), acc);
     }
 }
 
@@ -160,7 +182,7 @@ template <class Cv>
 __global__ __launch_bounds__(256) void k_bitterms(const uint4* rows, const uint4* cols, uint32_t H, uint32_t L,
                                                   uint32_t logH, uint4* out) {
     using F = typename Cv::Base;
-    __shared__ uint4 red[256 * 8];
+    __shared__ uint4 red[128 * 8];
     const uint32_t k = blockIdx.x, w = blockIdx.y, tid = threadIdx.x;
     const uint32_t NT = gridDim.x;
     const bool is_col = k > logH;
@@ -172,9 +194,8 @@ __global__ __launch_bounds__(256) void k_bitterms(const uint4* rows, const uint4
         if (k != 0 && !((j >> bit) & 1u)) continue;
         acc = xyzz_add(acc, xyzz_load<F>(src + 8 * j));
     }
-    xyzz_store(red + 8 * tid, acc);
-    lds_tree_sum<F>(red, tid, 256);
-    if (tid == 0) xyzz_store(out + 8 * ((size_t)w * NT + k), xyzz_load<F>(red));
+    acc = block_group_sum<F>(acc, 256, red);
+    if (tid == 0) xyzz_store(out + 8 * ((size_t)w * NT + k), acc);
 }
 
 // grid SW, 64 threads: S_w = T_0 + sum_j 2^(j + logL) U_j + sum_j 2^j V_j
@@ -182,7 +203,6 @@ template <class Cv>
 __global__ __launch_bounds__(64) void k_bitcombine(const uint4* terms, uint32_t NT, uint32_t logH, uint32_t logL,
                                                    uint4* window_sums) {
     using F = typename Cv::Base;
-    __shared__ uint4 red[64 * 8];
     const uint32_t w = blockIdx.x, k = threadIdx.x;
     XYZZ<F> v = xyzz_id<F>();
     if (k < NT) {
@@ -190,13 +210,11 @@ __global__ __launch_bounds__(64) void k_bitcombine(const uint4* terms, uint32_t 
         const uint32_t d = (k == 0) ? 0 : (k <= logH ? (k - 1 + logL) : (k - 1 - logH));
         for (uint32_t i = 0; i < d; i++) v = xyzz_dbl(v);
     }
-    xyzz_store(red + 8 * k, v);
-    for (uint32_t off = 32; off > 0; off >>= 1) {
-        __syncthreads();
-        if (k < off) xyzz_store(red + 8 * k, xyzz_add(xyzz_load<F>(red + 8 * k), xyzz_load<F>(red + 8 * (k + off))));
-    }
-    __syncthreads();
-    if (k == 0) xyzz_store(window_sums + 8 * w, xyzz_load<F>(red));
+    // NT <= 64 terms: a tree over the wave's lanes
+    uint32_t G = 1;
+    while (G < NT) G <<= 1;
+    v = wave_group_sum<F>(v, G);
+    if (k == 0) xyzz_store(window_sums + 8 * w, v);
 }
 
 // Many small windows (msm_shared_batch: SW = len * W windows of B = 16..128 buckets): 8 lanes per
@@ -208,7 +226,6 @@ template <class Cv>
 __global__ __launch_bounds__(256) void k_batch_window_sums(const uint4* bucket_sums, uint32_t SW, uint32_t B,
                                                            uint4* window_sums) {
     using F = typename Cv::Base;
-    __shared__ uint4 red[256 * 8];
     const uint32_t tid = threadIdx.x;
     const size_t t = (size_t)blockIdx.x * blockDim.x + tid;
     const uint32_t k = tid % BATCH_SEGS, G = B / BATCH_SEGS;
@@ -233,13 +250,8 @@ __global__ __launch_bounds__(256) void k_batch_window_sums(const uint4* bucket_s
         }
         v = S;
     }
-    xyzz_store(red + 8 * tid, v);
-    for (uint32_t off = BATCH_SEGS / 2; off > 0; off >>= 1) {
-        __syncthreads();
-        if (k < off) xyzz_store(red + 8 * tid, xyzz_add(xyzz_load<F>(red + 8 * tid), xyzz_load<F>(red + 8 * (tid + off))));
-    }
-    __syncthreads();
-    if (k == 0 && w < SW) xyzz_store(window_sums + 8 * w, xyzz_load<F>(red + 8 * tid));
+    v = wave_group_sum<F>(v, BATCH_SEGS);
+    if (k == 0 && w < SW) xyzz_store(window_sums + 8 * w, v);
 }
 
 static unsigned grid_for_t(size_t n, unsigned thr) { return (unsigned)std::max<size_t>(1, (n + thr - 1) / thr); }
