@@ -375,8 +375,15 @@ int msm_shifted_window_bits(size_t n) {
         return (v >= 8 && v <= 20) ? v : 0;
     }();
     if (c_env) return c_env;
-    const int c = msm_window_bits(n);
-    return (msm_windows(c + 1) < msm_windows(c) && c + 1 <= 17) ? c + 1 : c;
+    int c = msm_window_bits(n);
+    if (msm_windows(c + 1) < msm_windows(c) && c + 1 <= 17) c++;
+    // the top window holds only the 255 - (W - 1) c remaining bits, so its digits pile into the
+    // lowest 2^(top - 1) buckets: n / 2^(top - 1) extra entries each, against W n / 2^(c - 1) on
+    // average, and k_merge's longest runs (the latency of a small MSM) grow with that ratio.  Widen the
+    // window until the ratio is at most 1/2 (c = 13 at 2^16: top 8 bits, ratio 1.6 -> c = 15, top 15).
+    auto top_bits = [](int cc) { return 255 - (msm_windows(cc) - 1) * cc; };
+    while (c < 17 && (1 << (c - top_bits(c))) * 2 > msm_windows(c)) c++;
+    return c;
 }
 
 int msm_window_bits(size_t n) {
