@@ -104,6 +104,8 @@ SIGNATURES = {
     "halo_construct_powers": [ctypes.c_int, _vp, _sz, _vp],
     "halo_ipa_begin": [ctypes.c_int, _vp, _sz, _vp, _vp, ctypes.POINTER(_vp)],
     "halo_ipa_begin_dev": [ctypes.c_int, _vp, _sz, _vp, _vp, ctypes.POINTER(_vp)],
+    "halo_ipa_begin_xi": [ctypes.c_int, _vp, _sz, _vp, _vp, _vp, ctypes.POINTER(_vp)],
+    "halo_ipa_begin_dev_xi": [ctypes.c_int, _vp, _sz, _vp, _vp, _vp, ctypes.POINTER(_vp)],
     "halo_ipa_round_lr_multi": [_vp, _sz, _vp, _vp],
     "halo_ipa_fold_multi": [_vp, _sz, _vp, _vp],
     "halo_ipa_begin_vectors": [ctypes.c_int, _vp, _vp, _vp, _sz, _vp, ctypes.POINTER(_vp)],

@@ -460,6 +460,13 @@ __global__ void k_set_one_ark(uint4* out) {
     if (threadIdx.x == 0) fe_to_ark(out, fe_one<S>());
 }
 
+// x[i] *= k (ark scalars, i < count): the IPA's dots scaled by xi_0 in xi mode
+template <class S>
+__global__ void k_scale_ark(uint4* x, int count, const uint4* k) {
+    const int i = threadIdx.x;
+    if (i < count) fe_to_ark(x + 2 * i, fe_mul(fe_from_ark<S>(x + 2 * i), fe_from_ark<S>(k)));
+}
+
 // c / z folds (pcdl.rs:430-435) and the weight update w' = interleave(w, xi w)
 template <class Cv>
 __global__ __launch_bounds__(256) void k_tail_fold(uint4* cs, uint4* zs, size_t m, const uint4* xi_ark,
@@ -517,6 +524,10 @@ struct halo_ipa_session {
     hipStream_t aux = nullptr;        // builds the 2^i H' table beside round 1's accumulation
     hipEvent_t htab_ready = nullptr;  // recorded on aux after the table
     bool htab_waited = false;         // round 1 waited for it (later rounds follow a host sync of round 1)
+    // xi mode (halo_ipa_begin_xi / _dev_xi): the hiding terms use the resident 2^i H table and the
+    // dots scaled by xi_0 (dot H' = (dot xi_0) H), so there is neither H' nor a per-session table
+    bool xi_mode = false;
+    const void* htab_ptr = nullptr;  // 2^i H' (own table) or 2^i H (SrsState::h_table)
     uint8_t* pinned = nullptr;  // [128, 192) xi|xi_inv (H2D), [256, 512) L|R XYZZ (D2H): async, several sessions in flight
     ~halo_ipa_session() {
         if (aux) {
@@ -731,11 +742,36 @@ static size_t ipa_mat_n() {
     return e ? (size_t)atoll(e) : IPA_MAT_N;
 }
 
+// The 2^i H table (i < IPA_HTAB, internal affine) of xi-mode sessions, kept per device and curve and
+// rebuilt only when H changes (one ~1 ms doubling chain, then shared by every later opening).
+static int ipa_h_table(DeviceState* st, int curve, const halo_wrapped_point_t* Hpt) {
+    SrsState& srs = st->srs[curve];
+    if (srs.h_built && !memcmp(srs.h_key, Hpt, 64)) return HALO_OK;
+    HALO_CHECK(srs.h_table.reserve(IPA_HTAB * 64));
+    HALO_CHECK(st->scratch[7].reserve(IPA_HTAB * 128 + 64));
+    char* tmp = (char*)st->scratch[7].ptr;
+    const hipStream_t s = nullptr;
+    HALO_CHECK(copy_h2d(tmp + IPA_HTAB * 128, Hpt, 64, s));
+    DISPATCH_CURVE(curve, Cv, {
+        hipLaunchKernelGGL(k_pow2_xyzz_from_wrapped<Cv>, dim3(1), dim3(64), 0, s, (const uint4*)(tmp + IPA_HTAB * 128),
+                           (uint4*)tmp, IPA_HTAB);
+        hipLaunchKernelGGL(k_xyzz_to_aff_ipa<Cv>, dim3(IPA_HTAB / 64), dim3(64), 0, s, (const uint4*)tmp,
+                           srs.h_table.as<uint4>(), IPA_HTAB);
+    });
+    HALO_HIP(hipGetLastError());
+    HALO_HIP(hipStreamSynchronize(s));  // sessions on other streams read it
+    memcpy(srs.h_key, Hpt, 64);
+    srs.h_built = true;
+    return HALO_OK;
+}
+
 static int ipa_begin(halo_curve_t curve, size_t n, const halo_wrapped_point_t* gs_host, const halo_fe_t* cs,
                      const halo_fe_t* zs_host, const halo_fe_t* z, const halo_wrapped_point_t* H_prime,
-                     halo_ipa_session** out, bool cs_on_device = false) {
+                     halo_ipa_session** out, bool cs_on_device = false, const halo_fe_t* xi0 = nullptr,
+                     const halo_wrapped_point_t* Hpt = nullptr) {
     if (curve != HALO_PALLAS && curve != HALO_VESTA) return set_error(HALO_EINVAL, "unknown curve");
-    if (!cs || !(z || zs_host) || !H_prime || !out) return set_error(HALO_EINVAL, "halo_ipa_begin: null argument");
+    if (!cs || !(z || zs_host) || !(H_prime || (xi0 && Hpt)) || !out)
+        return set_error(HALO_EINVAL, "halo_ipa_begin: null argument");
     if (n <= 1) return set_error(HALO_EINVAL, "assertion failed: n > 1");
     if (!is_pow2(n)) return set_error(HALO_ENOTPOW2, "n (%zu) is not a power of two", n);
     DeviceState* st = current_state();
@@ -743,8 +779,11 @@ static int ipa_begin(halo_curve_t curve, size_t n, const halo_wrapped_point_t* g
     std::lock_guard<std::mutex> g(st->mu);
     SrsState& srs = st->srs[curve];
     if (!gs_host && n > srs.n) return set_error(HALO_ESRSRANGE, "d (%zu) <= D (%zu)", n - 1, srs.n ? srs.n - 1 : 0);
+    int rc0;
+    if (xi0 && (rc0 = ipa_h_table(st, curve, Hpt))) return rc0;
     auto* ses = new halo_ipa_session();
     ses->curve = curve;
+    ses->xi_mode = xi0 != nullptr;
     {
         const char* e = getenv("HALO_IPA_TAIL");
         const char* ew = getenv("HALO_IPA_WEIGHTED");  // A/B knob: 0 = fold G every round
@@ -784,7 +823,8 @@ static int ipa_begin(halo_curve_t curve, size_t n, const halo_wrapped_point_t* g
         }
         if ((rc = ses->cs.reserve(n * 32))) break;
         if ((rc = ses->zs.reserve(n * 32))) break;
-        if ((rc = ses->htab.reserve(IPA_HTAB * (64 + 128)))) break;  // affine table + XYZZ chain scratch
+        if (!ses->xi_mode && (rc = ses->htab.reserve(IPA_HTAB * (64 + 128)))) break;  // affine table + XYZZ chain scratch
+        ses->htab_ptr = ses->xi_mode ? srs.h_table.ptr : ses->htab.ptr;
         if ((rc = ses->small.reserve(1024))) break;
         if ((rc = ses->tmp.reserve(std::max<size_t>(4096 * 32, gs_host ? n * 64 : 0)))) break;
         if (gs_host) {
@@ -815,13 +855,19 @@ static int ipa_begin(halo_curve_t curve, size_t n, const halo_wrapped_point_t* g
         } else {
             if ((rc = copy_h2d(sm, z, 32, s))) break;
         }
-        if ((rc = copy_h2d(sm + 64, H_prime, 64, s))) break;
+        if (ses->xi_mode) {  // xi_0 at [192, 224); the 2^i H table is the SRS's
+            if ((rc = copy_h2d(sm + 192, xi0, 32, s))) break;
+            ses->htab_waited = true;
+        } else if ((rc = copy_h2d(sm + 64, H_prime, 64, s))) {
+            break;
+        }
         const size_t run = 16;
         DISPATCH_CURVE(curve, Cv, {
             if (!zs_host)
                 hipLaunchKernelGGL(k_powers<typename Cv::Scalar>, dim3(gridn((n + run - 1) / run, 128)), dim3(128), 0,
                                    s, (const uint4*)sm, n, run, ses->zs.as<uint4>());
         });
+        if (ses->xi_mode) break;  // (rc == HALO_OK: nothing more to build)
         // 2^i H' for i < 128 (the hiding terms use the GLV split of their scalar, k_hide_term): a
         // ~1 ms one-lane doubling chain, built on the side stream while round 1's digits, sort and
         // accumulation run; the hiding-term kernels wait for htab_ready
@@ -866,6 +912,21 @@ extern "C" int halo_ipa_begin_dev(halo_curve_t curve, const void* d_cs, size_t n
                                   const halo_wrapped_point_t* H_prime, halo_ipa_session** out) {
     clear_error();
     return ipa_begin(curve, n, nullptr, (const halo_fe_t*)d_cs, nullptr, z, H_prime, out, true);
+}
+
+// pcdl::open_without_eval's H' = xi_0 H (pcdl.rs:390-391) inside the session: the caller passes H and
+// xi_0 instead of H'; the hiding terms use a cached 2^i H table with the dots scaled by xi_0.
+extern "C" int halo_ipa_begin_xi(halo_curve_t curve, const halo_fe_t* cs, size_t n, const halo_fe_t* z,
+                                 const halo_wrapped_point_t* H, const halo_fe_t* xi0, halo_ipa_session** out) {
+    clear_error();
+    if (!xi0 || !H) return set_error(HALO_EINVAL, "halo_ipa_begin_xi: null argument");
+    return ipa_begin(curve, n, nullptr, cs, nullptr, z, nullptr, out, false, xi0, H);
+}
+extern "C" int halo_ipa_begin_dev_xi(halo_curve_t curve, const void* d_cs, size_t n, const halo_fe_t* z,
+                                     const halo_wrapped_point_t* H, const halo_fe_t* xi0, halo_ipa_session** out) {
+    clear_error();
+    if (!xi0 || !H) return set_error(HALO_EINVAL, "halo_ipa_begin_dev_xi: null argument");
+    return ipa_begin(curve, n, nullptr, (const halo_fe_t*)d_cs, nullptr, z, nullptr, out, true, xi0, H);
 }
 
 extern "C" int halo_ipa_begin_vectors(halo_curve_t curve, const halo_wrapped_point_t* gs, const halo_fe_t* cs,
@@ -913,7 +974,7 @@ static int ipa_tail_sums(halo_ipa_session* ses, int mode, hipStream_t s) {
         hipLaunchKernelGGL(k_tail_msm<Cv>, dim3((unsigned)nblk), dim3(TAIL_THREADS), 0, s, ses->table.as<const uint4>(),
                            ses->scal.as<const uint32_t>(), ses->side.as<const uint8_t>(), n0, ses->part.as<uint4>());
         hipLaunchKernelGGL(k_tail_final<Cv>, dim3(mode == 0 ? 2 : 1), dim3(TAIL_THREADS), 0, s,
-                           ses->part.as<const uint4>(), (int)nblk, mode == 0 ? ses->htab.as<const uint4>() : nullptr,
+                           ses->part.as<const uint4>(), (int)nblk, mode == 0 ? (const uint4*)ses->htab_ptr : nullptr,
                            (const uint4*)(sm + 128), (uint4*)(sm + (mode == 0 ? 512 : 256)), (int)(mode == 0));
     });
     HALO_HIP(hipGetLastError());
@@ -949,6 +1010,13 @@ static int ipa_round_launch(DeviceState* st, halo_ipa_session* ses) {
     ses->htab_waited = true;
     HALO_CHECK(dot_device(sf, cs + m * 32, zs, m, sm + 128, ses->tmp.ptr, s));        // <c_r, z_l>
     HALO_CHECK(dot_device(sf, cs, zs + m * 32, m, sm + 160, ses->tmp.ptr, s));        // <c_l, z_r>
+    if (ses->xi_mode) {  // dot H' = (dot xi_0) H
+        DISPATCH_CURVE(ses->curve, Cv, {
+            hipLaunchKernelGGL(k_scale_ark<typename Cv::Scalar>, dim3(1), dim3(64), 0, s, (uint4*)(sm + 128), 2,
+                               (const uint4*)(sm + 192));
+        });
+        HALO_HIP(hipGetLastError());
+    }
     if (ses->tail) {
         if (hr) HALO_HIP(hipStreamWaitEvent(s, hr, 0));
         HALO_CHECK(ipa_tail_sums(ses, 0, s));
@@ -968,22 +1036,22 @@ static int ipa_round_launch(DeviceState* st, halo_ipa_session* ses) {
             sl = sb;
             sr = sb + half * 32;
         }
-        HALO_CHECK(msm_srs_range_device(st, ses->curve, 0, sl, half, ses->htab.ptr, sm + 128, sm + 512, s, true, lgm,
+        HALO_CHECK(msm_srs_range_device(st, ses->curve, 0, sl, half, ses->htab_ptr, sm + 128, sm + 512, s, true, lgm,
                                         true, true, hr));
-        HALO_CHECK(msm_srs_range_device(st, ses->curve, m, sr, half, ses->htab.ptr, sm + 160, sm + 640, s, true, lgm,
+        HALO_CHECK(msm_srs_range_device(st, ses->curve, m, sr, half, ses->htab_ptr, sm + 160, sm + 640, s, true, lgm,
                                         true, true, hr));
         HALO_CHECK(msm_join(st, s));
     } else {
         // L and R are independent: the second MSM's accumulation overlaps the first one's tail
         if (ses->srs_round0) {  // G_l = SRS[0, m), G_r = SRS[m, 2m): resident window-shifted copies, no Horner
-            HALO_CHECK(msm_srs_range_device(st, ses->curve, 0, cs + m * 32, m, ses->htab.ptr, sm + 128, sm + 512, s, true,
+            HALO_CHECK(msm_srs_range_device(st, ses->curve, 0, cs + m * 32, m, ses->htab_ptr, sm + 128, sm + 512, s, true,
                                             32, true, true, hr));
-            HALO_CHECK(msm_srs_range_device(st, ses->curve, m, cs, m, ses->htab.ptr, sm + 160, sm + 640, s, true, 32,
+            HALO_CHECK(msm_srs_range_device(st, ses->curve, m, cs, m, ses->htab_ptr, sm + 160, sm + 640, s, true, 32,
                                             true, true, hr));
         } else {
-            HALO_CHECK(msm_device(st, ses->curve, gs, cs + m * 32, m, ses->htab.ptr, sm + 128, sm + 512, s, true, true,
+            HALO_CHECK(msm_device(st, ses->curve, gs, cs + m * 32, m, ses->htab_ptr, sm + 128, sm + 512, s, true, true,
                                   true, hr));
-            HALO_CHECK(msm_device(st, ses->curve, gs + m * 64, cs, m, ses->htab.ptr, sm + 160, sm + 640, s, true, true,
+            HALO_CHECK(msm_device(st, ses->curve, gs + m * 64, cs, m, ses->htab_ptr, sm + 160, sm + 640, s, true, true,
                                   true, hr));
         }
         HALO_CHECK(msm_join(st, s));

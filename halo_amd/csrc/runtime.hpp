@@ -53,6 +53,9 @@ struct SrsState {
     uint32_t S[16];     // internal packed (x, y)
     uint32_t H[16];
     DevBuf s_table;     // 2^i S (i < 256), internal affine: hiding term of pedersen::commit
+    DevBuf h_table;     // 2^i H (i < 128), internal affine: the IPA's H' = xi_0 H terms (halo_ipa_begin_xi)
+    uint64_t h_key[8] = {};  // the WrappedPoint H that h_table was built from
+    bool h_built = false;
     DevBuf shifted;     // optional window-shifted copies
     int shifted_c = 0;  // window bits of `shifted`
     int shifted_windows = 0;

@@ -41,6 +41,24 @@ class IpaSession:
         self._s = s
 
     @classmethod
+    def with_xi(cls, cs, z, H_point, xi0, curve="pallas") -> "IpaSession":
+        """Session whose H' = xi_0 H (pcdl.rs:390-391) is formed on the device (halo_ipa_begin_xi):
+        no host scalar multiplication, and the 2^i H table is shared by every opening under H."""
+        H.ensure_device()
+        self = cls.__new__(cls)
+        self.curve = _curve(curve)
+        c = H.fe_array(cs)
+        self.n = len(c)
+        zz = H.fe_array(z, 1)
+        hp = H.point_array(H_point)
+        x0 = H.fe_array(xi0, 1)
+        s = ctypes.c_void_p()
+        H.check(H.load().halo_ipa_begin_xi(self.curve, H.ptr(c), self.n, H.ptr(zz), H.ptr(hp), H.ptr(x0),
+                                           ctypes.byref(s)))
+        self._s = s
+        return self
+
+    @classmethod
     def from_vectors(cls, gs, cs, zs, H_prime, curve="pallas") -> "IpaSession":
         """Session over explicit (G, c, z) of length n (a shard of a distributed opening,
         halo_amd.dist.sharded_ipa_rounds)."""
@@ -160,11 +178,9 @@ def open_without_eval(p, C, d: int, z, v, w=None, transcript=None, q=None, w_bar
     xi = np.ascontiguousarray(transcript.challenge(), dtype=np.uint64)
     from .group import PublicParams
     _, Hpt = PublicParams.sh(curve)
-    H_prime = np.zeros(8, dtype=np.uint64)
-    H.check(L.halo_curve_op(cid, 2, H.ptr(Hpt), None, H.ptr(xi), 1, H.ptr(H_prime)))
     cs = np.zeros((n, 4), dtype=np.uint64)
     cs[: len(p)] = p[:n]
-    ses = IpaSession(cs, zz, H_prime, curve)
+    ses = IpaSession.with_xi(cs, zz, Hpt, xi, curve)  # H' = xi_0 H (pcdl.rs:390-391) on the device
     Ls, Rs = [], []
     for _ in range(n.bit_length() - 1):
         Lp, Rp = ses.round_lr()

@@ -325,9 +325,11 @@ def ipa_open_many(B, items, d: int):
     Returns [(Ls, Rs, U, c, [xi_0] + xis)]."""
     chals = [Challenges(B.m, seed=open_seed(z, v)) for (_, z, v) in items]
     xi0s = [ch() for ch in chals]
-    hps = B.h_mul_many(xi0s) if hasattr(B, "h_mul_many") else [B.h_mul(x0) for x0 in xi0s]
-    jobs = [(p, d + 1, z, hp) for (p, z, _), hp in zip(items, hps)]
-    outs = B.ipa_many(jobs, chals)
+    if hasattr(B, "ipa_many_xi"):  # H' = xi_0 H formed inside the device sessions
+        outs = B.ipa_many_xi([(p, d + 1, z, x0) for (p, z, _), x0 in zip(items, xi0s)], chals)
+    else:
+        hps = B.h_mul_many(xi0s) if hasattr(B, "h_mul_many") else [B.h_mul(x0) for x0 in xi0s]
+        outs = B.ipa_many([(p, d + 1, z, hp) for (p, z, _), hp in zip(items, hps)], chals)
     return [(Ls, Rs, U, c, [x0] + xis) for (Ls, Rs, U, c, xis), x0 in zip(outs, xi0s)]
 
 
@@ -643,19 +645,26 @@ class DeviceBackend:
                                                ctypes.byref(ln)))
         return self.torch.from_numpy(out.view(np.int64)).cuda()
 
-    def ipa_many(self, jobs, chals):
+    def ipa_many(self, jobs, chals, xi_mode=False):
         """jobs = [(p, n, z, H')] with one challenge stream each; all sessions advance in lockstep
-        (halo_ipa_round_lr_multi / halo_ipa_fold_multi: one host round trip per round for all)."""
+        (halo_ipa_round_lr_multi / halo_ipa_fold_multi: one host round trip per round for all).
+        xi_mode: jobs = [(p, n, z, xi_0)] and the sessions form H' = xi_0 H themselves
+        (halo_ipa_begin_dev_xi with this backend's H)."""
         k = len(jobs)
         n = jobs[0][1]
         assert all(j[1] == n for j in jobs)
         css = [self.resize(p, n) for (p, _, _, _) in jobs]
         self.sync()  # the coefficients were produced on the caller's stream
         sess = (ctypes.c_void_p * k)()
-        for i, ((_, _, z, hp), cs) in enumerate(zip(jobs, css)):
+        for i, ((_, _, z, hx), cs) in enumerate(zip(jobs, css)):
             s = ctypes.c_void_p()
-            self.H.check(self.L.halo_ipa_begin_dev(self.curve, self._p(cs), n, self.H.ptr(self.fe(z)),
-                                                   self.H.ptr(np.ascontiguousarray(hp)), ctypes.byref(s)))
+            if xi_mode:
+                self.H.check(self.L.halo_ipa_begin_dev_xi(self.curve, self._p(cs), n, self.H.ptr(self.fe(z)),
+                                                          self.H.ptr(self.H_point), self.H.ptr(self.fe(hx)),
+                                                          ctypes.byref(s)))
+            else:
+                self.H.check(self.L.halo_ipa_begin_dev(self.curve, self._p(cs), n, self.H.ptr(self.fe(z)),
+                                                       self.H.ptr(np.ascontiguousarray(hx)), ctypes.byref(s)))
             sess[i] = s.value
         Ls = [[] for _ in range(k)]
         Rs = [[] for _ in range(k)]
@@ -679,6 +688,9 @@ class DeviceBackend:
             self.H.check(self.L.halo_ipa_end(ctypes.c_void_p(sess[i]), self.H.ptr(U), self.H.ptr(c0)))
             outs.append((Ls[i], Rs[i], U, self.to_int(c0), xis[i]))
         return outs
+
+    def ipa_many_xi(self, jobs, chals):
+        return self.ipa_many(jobs, chals, xi_mode=True)
 
     def ipa(self, p, n: int, z: int, h_prime, chal):
         return self.ipa_many([(p, n, z, h_prime)], [chal])[0]

@@ -289,6 +289,14 @@ int halo_ipa_begin(halo_curve_t curve, const halo_fe_t* cs, size_t n, const halo
 /* As halo_ipa_begin with the n coefficients already on the device (ark format; null stream order). */
 int halo_ipa_begin_dev(halo_curve_t curve, const void* d_cs, size_t n, const halo_fe_t* z,
                        const halo_wrapped_point_t* H_prime, halo_ipa_session** out);
+/* The same sessions with pcdl::open_without_eval's H' = xi_0 H (pcdl.rs:390-391) formed inside:
+ * the caller passes H (WrappedPoint) and xi_0 (ark) instead of H'; the hiding terms <c, z> H' of
+ * every round use a 2^i H table (built once per H and kept) with the dots scaled by xi_0, so a
+ * session needs neither the scalar multiplication for H' nor its own 2^i H' doubling chain. */
+int halo_ipa_begin_xi(halo_curve_t curve, const halo_fe_t* cs, size_t n, const halo_fe_t* z,
+                      const halo_wrapped_point_t* H, const halo_fe_t* xi0, halo_ipa_session** out);
+int halo_ipa_begin_dev_xi(halo_curve_t curve, const void* d_cs, size_t n, const halo_fe_t* z,
+                          const halo_wrapped_point_t* H, const halo_fe_t* xi0, halo_ipa_session** out);
 /* Session over explicit vectors G (WrappedPoints), c, z of length n (power of two >= 2) instead of
  * the SRS prefix and the powers of z: one rank's shard of a distributed opening (the
  * strided split G[i P + r] keeps every fold pair on one rank) and its collapsed final rounds. */

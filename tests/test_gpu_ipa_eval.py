@@ -103,6 +103,42 @@ def test_ipa_rounds_vs_oracle(hal, corc, cname, cid, n):
     assert unfe(cfin, r) == [C[0]]
 
 
+@pytest.mark.parametrize("cname,cid", CURVES)
+@pytest.mark.parametrize("n", [2, 16, 2048, 8192])
+def test_ipa_xi_mode_equals_h_prime(hal, corc, cname, cid, n):
+    """halo_ipa_begin_xi (H' = xi_0 H formed on the device, hiding terms from the shared 2^i H table
+    scaled by xi_0) gives the same L, R, U, c as a session handed H' = xi_0 H, across the weighted
+    rounds, the materialisation at 1024 and the tail rounds; two different H in a row rebuild the
+    table."""
+    c = P.CURVES[cname]
+    r = c.scalar
+    g = corc.srs_generate(cname, n)
+    group.PublicParams.upload(cname, g, precompute_windows=False)
+    rng = random.Random(n + cid)
+    cs = fe([rng.randrange(r) for _ in range(n)], r)
+    zz = fe([rng.randrange(r)], r)
+    for trial in range(2):
+        Hpt = P.mul_fast(c, rng.randrange(1, r), c.generator)
+        Hw = np.array(P.point_to_wrapped(c, Hpt), dtype=np.uint64)
+        x0v = rng.randrange(1, r)
+        x0 = fe([x0v], r)
+        Hp = np.array(P.point_to_wrapped(c, P.mul_fast(c, x0v, Hpt)), dtype=np.uint64)
+        a = pcdl.IpaSession(cs, zz, Hp, cname)
+        b = pcdl.IpaSession.with_xi(cs, zz, Hw, x0, cname)
+        challenge, inverse = transcript(cname)
+        xi = None
+        for k in range(n.bit_length() - 1):
+            La, Ra = a.round_lr()
+            Lb, Rb = b.round_lr()
+            assert np.array_equal(La, Lb) and np.array_equal(Ra, Rb), (trial, k)
+            xi = challenge(xi, La, Ra)
+            a.fold(xi, inverse(xi))
+            b.fold(xi, inverse(xi))
+        Ua, ca = a.end()
+        Ub, cb = b.end()
+        assert np.array_equal(Ua, Ub) and np.array_equal(ca, cb), trial
+
+
 def test_ipa_fold_large_vs_c_oracle(hal, corc):
     """One fold at m = 2^14 (per-element scalar multiplication + affine normalisation)."""
     c = P.PALLAS

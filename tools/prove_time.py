@@ -4,6 +4,8 @@ os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")  # as bench.py
 sys.path.insert(0, '/root/repo')
 from halo_amd import _lib as H
 from halo_amd import prover
+if os.environ.get("NO_XI") == "1":  # A/B: H' = xi_0 H on the host side (halo_curve_op + H' sessions)
+    del prover.DeviceBackend.ipa_many_xi
 H.ensure_device(0)
 L = H.load()
 for arg in (sys.argv[1:] or ['16', '20']):
