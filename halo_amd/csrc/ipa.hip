@@ -996,8 +996,13 @@ static int ipa_round_launch(DeviceState* st, halo_ipa_session* ses) {
         ses->allow_tail = !(e && e[0] == '0');
         const bool to_tail = ses->allow_tail && 2 * m <= ipa_tail_n();  // the tail table reads XYZZ directly
         HALO_CHECK(ses->gs.reserve(2 * m * 128));
-        HALO_CHECK(msm_shared_batch(st, ses->curve, st->srs[ses->curve].gs.ptr, ses->w[ses->wcur].ptr, ses->wlen,
-                                    2 * m, ses->gs.ptr, to_tail, ses->mat, s));
+        // over the window-shifted copies (three-window Horner; HALO_MAT_SHIFTED=0: the plain SRS)
+        const SrsState& srs = st->srs[ses->curve];
+        static const bool mat_shifted = !(getenv("HALO_MAT_SHIFTED") && getenv("HALO_MAT_SHIFTED")[0] == '0');
+        const bool sh = mat_shifted && srs.shifted_c != 0;
+        HALO_CHECK(msm_shared_batch(st, ses->curve, sh ? srs.shifted.ptr : srs.gs.ptr, ses->w[ses->wcur].ptr,
+                                    ses->wlen, 2 * m, ses->gs.ptr, to_tail, ses->mat, s, sh ? srs.n : 0,
+                                    sh ? srs.shifted_c : 0));
         ses->gs_xyzz = to_tail;
         ses->weighted = false;
     }

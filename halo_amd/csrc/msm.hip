@@ -954,15 +954,31 @@ __global__ __launch_bounds__(256) void k_batch_lists(const uint32_t* digits, uin
     }
 }
 
+// entry e of the lists: scalar u = e & tmask of shifted copy e >> tlog (tlog 31: no copies)
 __global__ __launch_bounds__(256) void k_batch_expand(const uint32_t* ent, const uint32_t* ekey, const uint32_t* tot,
-                                                      uint32_t len, uint32_t WB, uint32_t* keys, uint32_t* vals) {
+                                                      uint32_t len, uint32_t WB, uint32_t tlog, uint32_t wstride,
+                                                      uint32_t* keys, uint32_t* vals) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t per = tot[0];
     if (per == 0 || p >= per * len) return;
     const uint32_t i = p / per, r = p - i * per;
-    const uint32_t e = ent[r];
+    const uint32_t e = ent[r], ee = e & 0x7fffffffu;
     keys[p] = i * WB + ekey[r];
-    vals[p] = (i + (e & 0x7fffffffu) * len) | (e & 0x80000000u);
+    vals[p] = (i + (ee & ((1u << tlog) - 1u)) * len + (ee >> tlog) * wstride) | (e & 0x80000000u);
+}
+
+// Shifted-SRS batches: the signed c_s-bit digit of (copy w, scalar u) -> three unsigned cb-bit
+// sub-digits of its magnitude, window q at sub[q][w T + u] (its sign carried along; DIGIT_NONE for 0)
+__global__ __launch_bounds__(256) void k_batch_subdigits(const uint32_t* digits, uint32_t TW, int cb, uint32_t* sub) {
+    const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= TW) return;
+    const uint32_t d = digits[e];
+    const uint32_t mag = d == DIGIT_NONE ? 0u : (d & 0x7fffffffu) + 1u, sign = d & 0x80000000u;
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+        const uint32_t v = (mag >> (cb * q)) & ((1u << cb) - 1u);
+        sub[(size_t)q * TW + e] = v ? ((v - 1u) | sign) : DIGIT_NONE;
+    }
 }
 
 template <class Cv>
@@ -989,22 +1005,30 @@ __global__ __launch_bounds__(64) void k_batch_horner(const uint4* window_sums, u
 
 template <class Cv>
 static int msm_shared_batch_t(DeviceState* st, const uint4* bases, const uint4* w_ark, size_t T, size_t len,
-                              uint4* out, bool xyzz_out, BatchScratch& S, hipStream_t s) {
-    // window bits: about T / 4 buckets per window, so that the per-window reduction (2 B additions)
-    // stays below the accumulation (T mixed additions)
-    const int c = std::max(5, std::min(BATCH_C_MAX, (int)ilog2(std::max<size_t>(T, 2)) - 1)), W = msm_windows(c);
-    const uint32_t B = 1u << (c - 1);
-    const size_t SW = len * (size_t)W, NB = SW * B, E = SW * T;
+                              uint4* out, bool xyzz_out, BatchScratch& S, hipStream_t s, size_t shift_stride, int c_s) {
     if (!T || !len) return set_error(HALO_EINVAL, "msm_shared_batch: empty batch");
-    if (E >= (1ull << 32) || T * len >= (1ull << 31))
+    // shifted: the lists run over TS = W_s T (copy, scalar) entries with three sub-digit windows of
+    // cb bits and 2^cb buckets (magnitudes 1..2^(c_s-1) < 2^(3 cb))
+    const bool shifted = shift_stride && c_s && (T & (T - 1)) == 0 &&
+                         (size_t)msm_windows(c_s) * shift_stride < (1ull << 31);
+    const int W_s = shifted ? msm_windows(c_s) : 1;
+    const int cb = shifted ? (c_s + 2) / 3 : 0;
+    // unshifted window bits: about T / 4 buckets per window, so that the per-window reduction
+    // (2 B additions) stays below the accumulation (T mixed additions)
+    const int c = shifted ? cb : std::max(5, std::min(BATCH_C_MAX, (int)ilog2(std::max<size_t>(T, 2)) - 1));
+    const int W = shifted ? 3 : msm_windows(c);
+    const uint32_t B = shifted ? 1u << cb : 1u << (c - 1);
+    const size_t TS = (size_t)W_s * T;
+    const size_t SW = len * (size_t)W, NB = SW * B, E = SW * TS;
+    if (E >= (1ull << 32) || T * len >= (1ull << 31) || B > (1u << (BATCH_C_MAX - 1)))
         return set_error(HALO_EINVAL, "msm_shared_batch: batch too large (len %zu, T %zu)", len, T);
     const uint32_t L = std::min<uint32_t>(MSM_SEG_L, B), logL = ilog2(L), H = B / L, logH = ilog2(H);
     const uint32_t NT = 1 + logH + logL;
     const uint32_t K = msm_chunk_len(st, E, NB);
     const size_t nchunks = (E + K - 1) / K;
     const size_t ng1 = nchunks / MSM_GROUP, ng2 = nchunks / (MSM_GROUP * MSM_GROUP);
-    HALO_CHECK(S.digits.reserve((size_t)W * T * 4));
-    HALO_CHECK(S.lists.reserve((size_t)W * T * 8 + 16));
+    HALO_CHECK(S.digits.reserve((size_t)(shifted ? W_s + 3 : W) * TS * 4));
+    HALO_CHECK(S.lists.reserve((size_t)W * TS * 8 + 16));
     HALO_CHECK(S.keys.reserve(E * 4));
     HALO_CHECK(S.vals.reserve(E * 4));
     HALO_CHECK(S.bstart.reserve((NB + 1) * 4));
@@ -1012,19 +1036,30 @@ static int msm_shared_batch_t(DeviceState* st, const uint4* bases, const uint4* 
     HALO_CHECK(S.bucket_sums.reserve(NB * 128));
     HALO_CHECK(S.window_sums.reserve(SW * 128));
     uint32_t* ent = S.lists.as<uint32_t>();
-    uint32_t* ekey = ent + (size_t)W * T;
-    uint32_t* tot = ekey + (size_t)W * T;
+    uint32_t* ekey = ent + (size_t)W * TS;
+    uint32_t* tot = ekey + (size_t)W * TS;
     uint4* P_first = S.partials.as<uint4>();
     uint4* P_last = P_first + 8 * nchunks;
     uint4* P_g1 = P_last + 8 * nchunks;
     uint4* P_g2 = P_g1 + 8 * (ng1 + 1);
 
-    hipLaunchKernelGGL(k_digits<typename Cv::Scalar>, dim3(grid_for(T, 256)), dim3(256), 0, s, w_ark, T, c, W,
-                       S.digits.as<uint32_t>(), T, 0, W);
-    hipLaunchKernelGGL(k_batch_lists, dim3(1), dim3(256), 0, s, S.digits.as<const uint32_t>(), (uint32_t)T, W, B,
-                       (uint32_t)len, ent, ekey, tot);
+    const uint32_t* lists_in = S.digits.as<const uint32_t>();
+    if (shifted) {
+        hipLaunchKernelGGL(k_digits<typename Cv::Scalar>, dim3(grid_for(T, 256)), dim3(256), 0, s, w_ark, T, c_s, W_s,
+                           S.digits.as<uint32_t>(), T, 0, W_s);
+        uint32_t* sub = S.digits.as<uint32_t>() + TS;
+        hipLaunchKernelGGL(k_batch_subdigits, dim3(grid_for(TS, 256)), dim3(256), 0, s, S.digits.as<const uint32_t>(),
+                           (uint32_t)TS, cb, sub);
+        lists_in = sub;
+    } else {
+        hipLaunchKernelGGL(k_digits<typename Cv::Scalar>, dim3(grid_for(T, 256)), dim3(256), 0, s, w_ark, T, c, W,
+                           S.digits.as<uint32_t>(), T, 0, W);
+    }
+    hipLaunchKernelGGL(k_batch_lists, dim3(1), dim3(256), 0, s, lists_in, (uint32_t)TS, W, B, (uint32_t)len, ent, ekey,
+                       tot);
     hipLaunchKernelGGL(k_batch_expand, dim3(grid_for(E, 256)), dim3(256), 0, s, (const uint32_t*)ent,
                        (const uint32_t*)ekey, (const uint32_t*)tot, (uint32_t)len, (uint32_t)(W * B),
+                       shifted ? (uint32_t)ilog2(T) : 31u, shifted ? (uint32_t)shift_stride : 0u,
                        S.keys.as<uint32_t>(), S.vals.as<uint32_t>());
     hipLaunchKernelGGL((k_acc<Cv, false>), dim3(grid_for(nchunks, 256)), dim3(256), 0, s, S.keys.as<const uint32_t>(),
                        S.vals.as<const uint32_t>(), (const uint32_t*)(tot + 1), K, bases, 1u, 0u, (size_t)0, 32u, 0u,
@@ -1067,11 +1102,11 @@ static int msm_shared_batch_t(DeviceState* st, const uint4* bases, const uint4* 
 }
 
 int msm_shared_batch(DeviceState* st, int curve, const void* bases_int, const void* w_ark, size_t T, size_t len,
-                     void* out, bool xyzz_out, BatchScratch& S, hipStream_t s) {
+                     void* out, bool xyzz_out, BatchScratch& S, hipStream_t s, size_t shift_stride, int c_s) {
     int rc;
     DISPATCH_CURVE(curve, Cv, {
         rc = msm_shared_batch_t<Cv>(st, (const uint4*)bases_int, (const uint4*)w_ark, T, len, (uint4*)out, xyzz_out,
-                                    S, s);
+                                    S, s, shift_stride, c_s);
     });
     return rc;
 }

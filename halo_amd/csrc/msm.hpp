@@ -45,8 +45,11 @@ int msm_srs_range_device(DeviceState* st, int curve, size_t offset, const void* 
 struct BatchScratch {
     DevBuf digits, lists, keys, vals, bstart, partials, bucket_sums, window_sums;
 };
+// shift_stride > 0: bases are the resident window-shifted SRS (copy w = 2^(c_s w) G at w shift_stride):
+// every c_s-bit digit of w[u] is split into three unsigned sub-digits, so the final Horner runs
+// over three windows (~2 c_s / 3 doublings) instead of ~255 / c windows (~255 doublings).
 int msm_shared_batch(DeviceState* st, int curve, const void* bases_int, const void* w_ark, size_t T, size_t len,
-                     void* out, bool xyzz_out, BatchScratch& S, hipStream_t s);
+                     void* out, bool xyzz_out, BatchScratch& S, hipStream_t s, size_t shift_stride = 0, int c_s = 0);
 int srs_precompute_windows(DeviceState* st, int curve, hipStream_t s);
 // Host conversion of a 128-B packed XYZZ point (internal format, each coordinate < 2p) to an ark
 // WrappedPoint: one inversion in 4 x 64-bit Montgomery arithmetic on the CPU (identity -> (0, 0)).
