@@ -326,23 +326,28 @@ static int dot_device(int field, const void* x, const void* y, size_t n, void* o
 // session keeps G0 = G at the switch round and the fold weights w (G_j[i] = sum_u w[u] G0[i + u len],
 // fold: w' = interleave(w, xi w)).  L and R are then direct sums over G0 with expanded scalars
 //   k = j + u len:  s[k] = c[m + j] w[u] (j < m, -> L),  c[j - m] w[u] (j >= m, -> R),
-// evaluated from a table 2^(8 win) G0[k] (win < 32, built once): every (k, win) term is an 8-bit
-// double-and-add (~16 dependent curve operations), then block trees.  U = sum_u w[u] G0[u] at the end.
-// c and z keep their ordinary elementwise folds (pcdl.rs:430-435).
+// evaluated from a table 2^(8 win) G0[k] (win < 16, built once): each scalar is split by GLV,
+// s = k1 + lambda k2 with |k1|, |k2| < 2^128, so every (k, win, half) term is an 8-bit
+// double-and-add (~16 dependent curve operations) of the table entry or of phi of it (x -> beta x),
+// then block trees.  The table's doubling chain is 120 doublings instead of 248.
+// U = sum_u w[u] G0[u] at the end.  c and z keep their ordinary elementwise folds (pcdl.rs:430-435).
 constexpr size_t IPA_TAIL_N = 2048;
 constexpr int IPA_HTAB = 128;  // entries 2^i H' of the session's hiding table (GLV split of the scalar)
-constexpr int TAIL_WIN = 32, TAIL_THREADS = 256;
+constexpr int TAIL_TBL = 16;                          // table windows (8 bits each: 128-bit GLV halves)
+constexpr int TAIL_WIN = 2 * TAIL_TBL, TAIL_THREADS = 256;  // terms per point: 16 windows x (k1, k2)
 
+// the doubling chain in Jacobian coordinates (dbl-2009-l: 7 multiplications against XYZZ's 9)
 template <class Cv>
 __global__ __launch_bounds__(64) void k_tail_table(const uint4* gs, int gs_xyzz, size_t n0, uint4* table) {
     using F = typename Cv::Base;
     const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n0) return;
-    XYZZ<F> p = gs_xyzz ? xyzz_load<F>(gs + 8 * k) : xyzz_from_aff(aff_load<F>(gs + 4 * k));
-    for (int w = 0; w < TAIL_WIN; w++) {
-        xyzz_store(table + 8 * ((size_t)w * n0 + k), p);
-        if (w + 1 < TAIL_WIN)
-            for (int b = 0; b < 8; b++) p = xyzz_dbl(p);
+    const XYZZ<F> p0 = gs_xyzz ? xyzz_load<F>(gs + 8 * k) : xyzz_from_aff(aff_load<F>(gs + 4 * k));
+    xyzz_store(table + 8 * k, p0);
+    Jac<F> j = jac_from_xyzz(p0);
+    for (int w = 1; w < TAIL_TBL; w++) {
+        for (int b = 0; b < 8; b++) j = jac_dbl(j);
+        xyzz_store(table + 8 * ((size_t)w * n0 + k), jac_to_xyzz(j));
     }
 }
 
@@ -365,11 +370,16 @@ __global__ __launch_bounds__(256) void k_tail_scalars(const uint4* cs, const uin
     }
     Fe<S> one_raw = fe_zero<S>();  // internal (x 2^261) -> canonical: Montgomery product with 1
     one_raw.v[0] = 1;
-    uint32_t w8[8];
+    uint32_t w8[8], k1[5], k2[5];
+    bool n1, n2;
     fe_pack(fe_canon(fe_mul(v, one_raw)), w8);
+    glv::decompose<typename Cv::K>(w8, n1, k1, n2, k2);
 #pragma unroll
-    for (int q = 0; q < 8; q++) scal[8 * k + q] = w8[q];
-    side[k] = sd;
+    for (int q = 0; q < 4; q++) {
+        scal[8 * k + q] = k1[q];
+        scal[8 * k + 4 + q] = k2[q];
+    }
+    side[k] = sd | (n1 ? 2 : 0) | (n2 ? 4 : 0);
 }
 
 template <class F>
@@ -396,10 +406,14 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail_msm(const uint4* table, c
     int sd = 0;
     if (t < (size_t)TAIL_WIN * n0) {
         const size_t win = t / n0, k = t % n0;
-        const uint32_t d = (scal[8 * k + (win >> 2)] >> (8 * (win & 3))) & 255u;
-        sd = side[k];
+        const uint32_t half = (uint32_t)win / TAIL_TBL, bw = (uint32_t)win % TAIL_TBL;
+        const uint32_t d = (scal[8 * k + 4 * half + (bw >> 2)] >> (8 * (bw & 3))) & 255u;
+        const uint32_t sk = side[k];
+        sd = sk & 1;
         if (d) {
-            const XYZZ<F> q = xyzz_load<F>(table + 8 * t);
+            XYZZ<F> q = xyzz_load<F>(table + 8 * ((size_t)bw * n0 + k));
+            if (half) q.X = fe_mul(q.X, fe_from_const<F>(Cv::K::BETA));  // phi
+            if ((sk >> (1 + half)) & 1u) q = xyzz_neg(q);
             const int top = 31 - __clz(d);
             acc = q;
             for (int b = top - 1; b >= 0; b--) {
@@ -941,7 +955,7 @@ extern "C" int halo_ipa_begin_vectors(halo_curve_t curve, const halo_wrapped_poi
 static int ipa_enter_tail(halo_ipa_session* ses, hipStream_t s) {
     const size_t n0 = 2 * ses->m;
     const size_t nblk = (TAIL_WIN * n0 + TAIL_THREADS - 1) / TAIL_THREADS;
-    HALO_CHECK(ses->table.reserve((size_t)TAIL_WIN * n0 * 128));
+    HALO_CHECK(ses->table.reserve((size_t)TAIL_TBL * n0 * 128));
     HALO_CHECK(ses->w[0].reserve(n0 * 32));
     HALO_CHECK(ses->w[1].reserve(n0 * 32));
     HALO_CHECK(ses->scal.reserve(n0 * 32));

@@ -24,7 +24,7 @@ for lg in [int(x) for x in (sys.argv[1:] or ['16', '20'])]:
     z = fe1(12345)
     Hp = np.zeros(8, dtype=np.uint64)
     H.check(L.halo_srs_read(0, 1, 1, H.ptr(Hp)))
-    for rep in range(2):
+    for rep in range(int(os.environ.get("REPS", "2"))):
         s = ctypes.c_void_p()
         H.check(L.halo_ipa_begin(0, H.ptr(cs), n, H.ptr(z), H.ptr(Hp), ctypes.byref(s)))
         Lp = np.zeros(8, dtype=np.uint64); Rp = np.zeros(8, dtype=np.uint64)
