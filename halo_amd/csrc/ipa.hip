@@ -22,6 +22,7 @@
 #include "glv.hpp"
 #include "msm.hpp"
 #include "runtime.hpp"
+#include "tree.hpp"
 
 namespace halo {
 
@@ -382,34 +383,37 @@ __global__ __launch_bounds__(256) void k_tail_scalars(const uint4* cs, const uin
     side[k] = sd | (n1 ? 2 : 0) | (n2 ? 4 : 0);
 }
 
-template <class F>
-HALO_DEV void tail_tree(uint4* red, int tid, XYZZ<F> v, uint4* out) {
-    xyzz_store(red + 8 * tid, v);
-    for (int off = TAIL_THREADS / 2; off > 0; off >>= 1) {
-        __syncthreads();
-        if (tid < off) xyzz_store(red + 8 * tid, xyzz_add(xyzz_load<F>(red + 8 * tid), xyzz_load<F>(red + 8 * (tid + off))));
-    }
-    __syncthreads();
-    if (tid == 0) xyzz_store(out, xyzz_load<F>(red));
-    __syncthreads();
-}
-
-// terms t = win * n0 + k; block partial sums part[block][side]
+// Block partial sums part[block][side].  mode 0 (L and R of a round, 2m = len): the first nbs blocks
+// take side 0's terms, the rest side 1's (each block one side: one tree, not two); the term q of a
+// side is (win, u, j) = window, fold weight, j < m, at point k = j + u 2m + side m.  mode 1 (U): terms
+// t = win n0 + k, all on side 0.
 template <class Cv>
 __global__ __launch_bounds__(TAIL_THREADS) void k_tail_msm(const uint4* table, const uint32_t* scal, const uint8_t* side,
-                                                            size_t n0, uint4* part) {
+                                                            size_t n0, size_t m, int mode, uint32_t nbs, uint4* part) {
     using F = typename Cv::Base;
-    __shared__ uint4 red[TAIL_THREADS * 8];
+    __shared__ uint4 red[TAIL_THREADS / 2 * 8];
     const int tid = threadIdx.x;
-    const size_t t = (size_t)blockIdx.x * TAIL_THREADS + tid;
     XYZZ<F> acc = xyzz_id<F>();
-    int sd = 0;
-    if (t < (size_t)TAIL_WIN * n0) {
-        const size_t win = t / n0, k = t % n0;
+    uint32_t sd = 0;
+    size_t win = 0, k = 0;
+    bool valid;
+    if (mode == 0) {
+        sd = blockIdx.x >= nbs;
+        const size_t q = (size_t)(blockIdx.x - sd * nbs) * TAIL_THREADS + tid, hn = n0 / 2;
+        valid = q < (size_t)TAIL_WIN * hn;
+        win = q / hn;
+        const size_t r = q % hn, u = r / m, j = r % m;
+        k = j + u * 2 * m + sd * m;
+    } else {
+        const size_t t = (size_t)blockIdx.x * TAIL_THREADS + tid;
+        valid = t < (size_t)TAIL_WIN * n0;
+        win = t / n0;
+        k = t % n0;
+    }
+    if (valid) {
         const uint32_t half = (uint32_t)win / TAIL_TBL, bw = (uint32_t)win % TAIL_TBL;
         const uint32_t d = (scal[8 * k + 4 * half + (bw >> 2)] >> (8 * (bw & 3))) & 255u;
         const uint32_t sk = side[k];
-        sd = sk & 1;
         if (d) {
             XYZZ<F> q = xyzz_load<F>(table + 8 * ((size_t)bw * n0 + k));
             if (half) q.X = fe_mul(q.X, fe_from_const<F>(Cv::K::BETA));  // phi
@@ -422,8 +426,11 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail_msm(const uint4* table, c
             }
         }
     }
-    tail_tree<F>(red, tid, sd == 0 ? acc : xyzz_id<F>(), part + 8 * (2 * (size_t)blockIdx.x));
-    tail_tree<F>(red, tid, sd == 1 ? acc : xyzz_id<F>(), part + 8 * (2 * (size_t)blockIdx.x + 1));
+    acc = block_group_sum<F>(acc, TAIL_THREADS, red);
+    if (tid == 0) {
+        xyzz_store(part + 8 * (2 * (size_t)blockIdx.x + sd), acc);
+        xyzz_store(part + 8 * (2 * (size_t)blockIdx.x + (sd ^ 1)), xyzz_id<F>());
+    }
 }
 
 // block b (0: L, 1: R): sum of the partials + dot_b * H' (from the 2^i H' table), -> WrappedPoint
@@ -433,8 +440,7 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail_final(const uint4* part, 
                                                               int xyzz_out) {
     using F = typename Cv::Base;
     using S = typename Cv::Scalar;
-    __shared__ uint4 red[TAIL_THREADS * 8];
-    __shared__ uint4 sum_s[8];
+    __shared__ uint4 red[TAIL_THREADS / 2 * 8];
     __shared__ uint32_t kw[8];
     __shared__ uint32_t neg[2];
     const int tid = threadIdx.x, b = blockIdx.x;
@@ -460,12 +466,12 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail_final(const uint4* part, 
         acc = xyzz_from_aff(p);
     }
     for (int i = tid; i < nblk; i += TAIL_THREADS) acc = xyzz_add(acc, xyzz_load<F>(part + 8 * (2 * (size_t)i + b)));
-    tail_tree<F>(red, tid, acc, sum_s);
+    acc = block_group_sum<F>(acc, TAIL_THREADS, red);
     if (tid == 0) {
         if (xyzz_out)  // 128 B per side, converted on the host (host_xyzz_to_wrapped)
-            xyzz_store(out_wrapped + 8 * b, xyzz_load<F>(sum_s));
+            xyzz_store(out_wrapped + 8 * b, acc);
         else
-            aff_to_wrapped(out_wrapped + 4 * b, xyzz_to_aff(xyzz_load<F>(sum_s)));
+            aff_to_wrapped(out_wrapped + 4 * b, xyzz_to_aff(acc));
     }
 }
 
@@ -954,7 +960,7 @@ extern "C" int halo_ipa_begin_vectors(halo_curve_t curve, const halo_wrapped_poi
 // Switch to the tail rounds: G0 = current G (length 2m), table 2^(8 win) G0, w = [1].
 static int ipa_enter_tail(halo_ipa_session* ses, hipStream_t s) {
     const size_t n0 = 2 * ses->m;
-    const size_t nblk = (TAIL_WIN * n0 + TAIL_THREADS - 1) / TAIL_THREADS;
+    const size_t nblk = (TAIL_WIN * n0 + TAIL_THREADS - 1) / TAIL_THREADS + 2;  // (+ mode 0's per-side rounding)
     HALO_CHECK(ses->table.reserve((size_t)TAIL_TBL * n0 * 128));
     HALO_CHECK(ses->w[0].reserve(n0 * 32));
     HALO_CHECK(ses->w[1].reserve(n0 * 32));
@@ -979,14 +985,16 @@ static int ipa_enter_tail(halo_ipa_session* ses, hipStream_t s) {
 // mode 1: U = sum_u w[u] G0[u] -> small[256..320)
 static int ipa_tail_sums(halo_ipa_session* ses, int mode, hipStream_t s) {
     const size_t n0 = ses->n0, m = ses->m;
-    const size_t nblk = (TAIL_WIN * n0 + TAIL_THREADS - 1) / TAIL_THREADS;
+    const size_t nbs = (TAIL_WIN * (n0 / 2) + TAIL_THREADS - 1) / TAIL_THREADS;  // mode 0: blocks per side
+    const size_t nblk = mode == 0 ? 2 * nbs : (TAIL_WIN * n0 + TAIL_THREADS - 1) / TAIL_THREADS;
     char* sm = (char*)ses->small.ptr;
     DISPATCH_CURVE(ses->curve, Cv, {
         hipLaunchKernelGGL(k_tail_scalars<Cv>, dim3(gridn(n0, 256)), dim3(256), 0, s, ses->cs.as<const uint4>(),
                            ses->w[ses->wcur].as<const uint4>(), n0, 2 * m, m, mode, ses->scal.as<uint32_t>(),
                            ses->side.as<uint8_t>());
         hipLaunchKernelGGL(k_tail_msm<Cv>, dim3((unsigned)nblk), dim3(TAIL_THREADS), 0, s, ses->table.as<const uint4>(),
-                           ses->scal.as<const uint32_t>(), ses->side.as<const uint8_t>(), n0, ses->part.as<uint4>());
+                           ses->scal.as<const uint32_t>(), ses->side.as<const uint8_t>(), n0, m, mode, (uint32_t)nbs,
+                           ses->part.as<uint4>());
         hipLaunchKernelGGL(k_tail_final<Cv>, dim3(mode == 0 ? 2 : 1), dim3(TAIL_THREADS), 0, s,
                            ses->part.as<const uint4>(), (int)nblk, mode == 0 ? (const uint4*)ses->htab_ptr : nullptr,
                            (const uint4*)(sm + 128), (uint4*)(sm + (mode == 0 ? 512 : 256)), (int)(mode == 0));
