@@ -755,8 +755,10 @@ static size_t ipa_tail_n() {
 
 // Length at which weighted rounds materialise G = sum_u w[u] SRS[i + u len] (one batched MSM with
 // the fold weights as shared scalars, msm_shared_batch) and continue as tail rounds: a weighted
-// round costs two n/2-term MSMs whatever the length, a tail round at this length ~0.6 ms.
-constexpr size_t IPA_MAT_N = 1024;
+// round costs two n/2-term MSMs whatever the length (~0.75 ms at 2^16), a tail round ~0.25 ms.
+// Measured (opening 2^12 / 2^16 / 2^20, ms): 1024: 6.2 / 10.4 / 29.3; 2048: 5.6 / 9.3 / 27.6;
+// 4096 (tail 4096): 6.5 / 10.7 / 27.4; 8192: 6.4 / 12.8 / 28.4.
+constexpr size_t IPA_MAT_N = 2048;
 static size_t ipa_mat_n() {
     const char* e = getenv("HALO_IPA_MAT_N");  // A/B knob (read per round); 0 keeps the weighted rounds to the end
     return e ? (size_t)atoll(e) : IPA_MAT_N;

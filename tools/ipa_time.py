@@ -26,7 +26,10 @@ for lg in [int(x) for x in (sys.argv[1:] or ['16', '20'])]:
     H.check(L.halo_srs_read(0, 1, 1, H.ptr(Hp)))
     for rep in range(int(os.environ.get("REPS", "2"))):
         s = ctypes.c_void_p()
-        H.check(L.halo_ipa_begin(0, H.ptr(cs), n, H.ptr(z), H.ptr(Hp), ctypes.byref(s)))
+        if os.environ.get("NO_XI") == "1":  # H' given (the caller's scalar multiplication)
+            H.check(L.halo_ipa_begin(0, H.ptr(cs), n, H.ptr(z), H.ptr(Hp), ctypes.byref(s)))
+        else:  # H' = xi_0 H formed in the session (the prover's path)
+            H.check(L.halo_ipa_begin_xi(0, H.ptr(cs), n, H.ptr(z), H.ptr(Hp), H.ptr(fe1(987654321)), ctypes.byref(s)))
         Lp = np.zeros(8, dtype=np.uint64); Rp = np.zeros(8, dtype=np.uint64)
         H.check(L.halo_profile_reset()); H.check(L.halo_profile_enable(1))
         t_lr = t_fold = 0.0
