@@ -759,6 +759,7 @@ static size_t ipa_tail_n() {
 // Measured (opening 2^12 / 2^16 / 2^20, ms): 1024: 6.2 / 10.4 / 29.3; 2048: 5.6 / 9.3 / 27.6;
 // 4096 (tail 4096): 6.5 / 10.7 / 27.4; 8192: 6.4 / 12.8 / 28.4.
 constexpr size_t IPA_MAT_N = 2048;
+constexpr size_t IPA_PAIR_MAX = (size_t)1 << 18;  // weighted rounds: L and R as one MSM up to this half
 static size_t ipa_mat_n() {
     const char* e = getenv("HALO_IPA_MAT_N");  // A/B knob (read per round); 0 keeps the weighted rounds to the end
     return e ? (size_t)atoll(e) : IPA_MAT_N;
@@ -1065,10 +1066,23 @@ static int ipa_round_launch(DeviceState* st, halo_ipa_session* ses) {
             sl = sb;
             sr = sb + half * 32;
         }
-        HALO_CHECK(msm_srs_range_device(st, ses->curve, 0, sl, half, ses->htab_ptr, sm + 128, sm + 512, s, true, lgm,
-                                        true, true, hr));
-        HALO_CHECK(msm_srs_range_device(st, ses->curve, m, sr, half, ses->htab_ptr, sm + 160, sm + 640, s, true, lgm,
-                                        true, true, hr));
+        // L and R as one MSM (key = (side, bucket)) while the round is latency-bound; at 2^19 terms per
+        // side two MSMs win (R's front and accumulation overlap L's reduction tail).  Measured, opening
+        // 2^14 / 2^17 / 2^18 / 2^19 / 2^20 ms, two MSMs vs one: 7.5 / 11.3 / 14.4 / 19.3 / 27.2 vs
+        // 6.9 / 10.3 / 13.2 / 17.8 / 29.0
+        static const size_t pair_max = [] {
+            const char* e = getenv("HALO_IPA_PAIR_MAX");  // A/B knob: terms per side
+            return e ? (size_t)atoll(e) : IPA_PAIR_MAX;
+        }();
+        if (half <= pair_max) {
+            HALO_CHECK(msm_srs_pair_device(st, ses->curve, sl, sr, half, lgm, ses->htab_ptr, sm + 128, sm + 160,
+                                           sm + 512, sm + 640, s, hr));
+        } else {
+            HALO_CHECK(msm_srs_range_device(st, ses->curve, 0, sl, half, ses->htab_ptr, sm + 128, sm + 512, s, true,
+                                            lgm, true, true, hr));
+            HALO_CHECK(msm_srs_range_device(st, ses->curve, m, sr, half, ses->htab_ptr, sm + 160, sm + 640, s, true,
+                                            lgm, true, true, hr));
+        }
         HALO_CHECK(msm_join(st, s));
     } else {
         // L and R are independent: the second MSM's accumulation overlaps the first one's tail

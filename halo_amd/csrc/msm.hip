@@ -167,7 +167,8 @@ template <class Cv>
 __device__ __forceinline__ void acc_chunk(size_t t, uint32_t cnt, const uint32_t* keys, const uint32_t* vals, uint32_t K,
                                           const uint4* bases, uint32_t n_per_window, uint32_t npw_lg, size_t stride,
                                           uint32_t blk_lg, uint32_t glv_n, uint4* first, uint4* last,
-                                          uint4* bucket_sums, uint32_t* bstart, uint32_t NB) {
+                                          uint4* bucket_sums, uint32_t* bstart, uint32_t NB, uint32_t key_lg,
+                                          uint32_t poly_off) {
     using F = typename Cv::Base;
     const size_t beg = t * K;
     if (beg >= cnt) {
@@ -205,7 +206,8 @@ __device__ __forceinline__ void acc_chunk(size_t t, uint32_t cnt, const uint32_t
             const uint32_t w = npw_lg < 32 ? (uint32_t)idx >> npw_lg : (uint32_t)idx / n_per_window;
             uint32_t i = (uint32_t)idx - w * n_per_window;
             if (blk_lg < 32) i += (i >> blk_lg) << blk_lg;  // blocks of 2^blk_lg at stride 2^(blk_lg+1)
-            idx = (size_t)w * stride + i;
+            // + the point offset of the entry's output (k >> key_lg: msm_srs_pair's R at offset m)
+            idx = (size_t)w * stride + i + (size_t)(k >> key_lg) * poly_off;
         }
         const bool phi = glv_n && idx >= glv_n;  // GLV: phi(G_i)
         if (phi) idx -= glv_n;
@@ -226,11 +228,11 @@ __global__ __launch_bounds__(256, HALO_ACC_MINB) void k_acc(const uint32_t* keys
                                              uint32_t K, const uint4* bases, uint32_t n_per_window, uint32_t npw_lg,
                                              size_t stride, uint32_t blk_lg, uint32_t glv_n, uint4* first, uint4* last,
                                              uint4* bucket_sums, uint32_t* work_ctr, uint32_t nblocks, uint32_t* bstart,
-                                             uint32_t NB) {
+                                             uint32_t NB, uint32_t key_lg = 31, uint32_t poly_off = 0) {
     const uint32_t cnt = *count;
     if constexpr (!PERSIST) {
         acc_chunk<Cv>((size_t)blockIdx.x * blockDim.x + threadIdx.x, cnt, keys, vals, K, bases, n_per_window,
-                                npw_lg, stride, blk_lg, glv_n, first, last, bucket_sums, bstart, NB);
+                                npw_lg, stride, blk_lg, glv_n, first, last, bucket_sums, bstart, NB, key_lg, poly_off);
     } else {
         __shared__ uint32_t sblk;
         for (;;) {
@@ -240,7 +242,7 @@ __global__ __launch_bounds__(256, HALO_ACC_MINB) void k_acc(const uint32_t* keys
             __syncthreads();
             if (blk >= nblocks) break;  // uniform per workgroup: every wave leaves
             acc_chunk<Cv>((size_t)blk * blockDim.x + threadIdx.x, cnt, keys, vals, K, bases, n_per_window,
-                                    npw_lg, stride, blk_lg, glv_n, first, last, bucket_sums, bstart, NB);
+                                    npw_lg, stride, blk_lg, glv_n, first, last, bucket_sums, bstart, NB, key_lg, poly_off);
         }
     }
 }
@@ -654,7 +656,7 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
                     (const uint32_t*)svals, scount, K, bases_int, (uint32_t)nn, is_pow2(nn) ? ilog2(nn) : 0xffu,
                     (shifted && (shift_stride != nn || blk_lg < 32)) ? shift_stride : (size_t)0, blk_lg,
                     glv ? (uint32_t)nn : 0u, P_first,
-                    P_last, M.bucket_sums.as<uint4>(), work_ctr, nblocks, M.bstart.as<uint32_t>(), (uint32_t)NB);
+                    P_last, M.bucket_sums.as<uint4>(), work_ctr, nblocks, M.bstart.as<uint32_t>(), (uint32_t)NB, 31u, 0u);
         M.skeys = skeys;
         M.scount = scount;
         HALO_HIP(hipGetLastError());
@@ -776,7 +778,7 @@ static int msm_multi_device_t(DeviceState* st, const void* const* scalars, const
         HALO_LAUNCH(prof, kacc, dim3(nblocks), dim3(256), 0, s, (const uint32_t*)skeys, (const uint32_t*)svals, scount,
                     K, srs.shifted.as<const uint4>(), (uint32_t)ld, is_pow2(ld) ? ilog2(ld) : 0xffu, srs.n, 32u, 0u,
                     P_first, P_last, M.bucket_sums.as<uint4>(), (uint32_t*)nullptr, nblocks, M.bstart.as<uint32_t>(),
-                    (uint32_t)NB);
+                    (uint32_t)NB, 31u, 0u);
         HALO_HIP(hipGetLastError());
     }
     MsmTailArgs ta;
@@ -816,6 +818,133 @@ static int msm_multi_device_t(DeviceState* st, const void* const* scalars, const
     M.tail_pending = true;
     M.owner = s;
     return HALO_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// The IPA's weighted-round pair (ipa.hip): L = sum_i sl[i] G[map(i)] and R = sum_i sr[i] G[m + map(i)],
+// map(i) = i + (i >> lg m) << lg m (the left / right halves of the 2m-blocks), each plus its hiding
+// term dot H' from the 2^i table -- ONE MSM over the window-shifted SRS with key (side, bucket): one
+// digit pass, one sort, one accumulation and one reduction tail (SW = 2) instead of two MSMs whose
+// front and accumulation run one after the other.  Outputs packed XYZZ (128 B each) at out[0], out[1].
+// ---------------------------------------------------------------------------------------------
+template <class Cv>
+static int msm_srs_pair_t(DeviceState* st, const uint4* sl, const uint4* sr, size_t half, uint32_t lgm,
+                          const uint4* hide_table, const uint4* hide_l, const uint4* hide_r, uint4* out_l,
+                          uint4* out_r, hipStream_t s, hipEvent_t hide_ready) {
+    SrsState& srs = st->srs[curve_id<Cv>()];
+    const size_t m = (size_t)1 << lgm;
+    if (!srs.shifted_c) return set_error(HALO_EINVAL, "msm_srs_pair: no window-shifted SRS");
+    if (!half || (half & (half - 1)) || half % m || 2 * half > srs.n)
+        return set_error(HALO_EINVAL, "msm_srs_pair: %zu terms per side, blocks of %zu, SRS %zu", half, m, srs.n);
+    MsmPipe& PP = g_msm_pipe[st->device & 63];
+    HALO_CHECK(pipe_init(PP));
+    const int set = msm_pick_set(PP, s, true);
+    MsmScratch& M = PP.set[set];
+    if (M.tail_pending) HALO_HIP(hipStreamWaitEvent(s, M.tail_done, 0));
+    const hipStream_t ts = PP.tail[set];
+    const int c = srs.shifted_c, W = msm_windows(c);
+    const uint32_t B = 1u << (c - 1);
+    const size_t SN = (size_t)W * half, E = 2 * SN, NB = 2 * (size_t)B;
+    const int SW = 2;
+    if (E >= (1ull << 32)) return set_error(HALO_EINVAL, "msm_srs_pair: too large");
+    const uint32_t L = std::min<uint32_t>(MSM_SEG_L, B), logL = ilog2(L), H = B / L, logH = ilog2(H);
+    const uint32_t NT = 1 + logH + logL;
+    const uint32_t key_bits = ilog2(NB - 1) + 1;
+    const uint32_t K = msm_chunk_len(st, E, NB);
+    const size_t nchunks = (E + K - 1) / K;
+    const size_t ng1 = nchunks / MSM_GROUP, ng2 = nchunks / (MSM_GROUP * MSM_GROUP);
+    HALO_CHECK(M.digits.reserve(E * 4));
+    HALO_CHECK(M.bstart.reserve((NB + 1) * 4));
+    HALO_CHECK(M.partials.reserve((nchunks * 2 + ng1 + ng2 + 2) * 128));
+    HALO_CHECK(M.bucket_sums.reserve(NB * 128));
+    HALO_CHECK(M.seg_acc.reserve((size_t)SW * H * 128));
+    HALO_CHECK(M.seg_sum.reserve((size_t)SW * L * 128));
+    HALO_CHECK(M.bits.reserve((size_t)SW * NT * 128));
+    HALO_CHECK(M.window_sums.reserve((size_t)(SW + 2) * 128));  // + the two hiding terms
+    uint4* P_first = M.partials.as<uint4>();
+    uint4* P_last = P_first + 8 * nchunks;
+    uint4* P_g1 = P_last + 8 * nchunks;
+    uint4* P_g2 = P_g1 + 8 * (ng1 + 1);
+    uint4* hide_slot = M.window_sums.as<uint4>() + 8 * SW;
+    // the hiding terms on the tail stream, beside the front and the accumulation
+    HALO_HIP(hipEventRecord(M.start, s));
+    HALO_HIP(hipStreamWaitEvent(ts, M.start, 0));
+    if (hide_ready) HALO_HIP(hipStreamWaitEvent(ts, hide_ready, 0));
+    hipLaunchKernelGGL(k_hide_term<Cv>, dim3(1), dim3(256), 0, ts, hide_table, hide_l, 1, hide_slot);
+    hipLaunchKernelGGL(k_hide_term<Cv>, dim3(1), dim3(256), 0, ts, hide_table, hide_r, 1, hide_slot + 8);
+    HALO_HIP(hipGetLastError());
+    HALO_HIP(hipEventRecord(M.front_done, ts));
+    uint32_t* digits = M.digits.as<uint32_t>();
+    hipLaunchKernelGGL(k_digits<typename Cv::Scalar>, dim3(grid_for(half, 256)), dim3(256), 0, s, sl, half, c, W,
+                       digits, half, 0, W);
+    hipLaunchKernelGGL(k_digits<typename Cv::Scalar>, dim3(grid_for(half, 256)), dim3(256), 0, s, sr, half, c, W,
+                       digits + SN, half, 0, W);
+    HALO_HIP(hipGetLastError());
+    uint32_t *skeys = nullptr, *svals = nullptr;
+    const uint32_t* scount = nullptr;
+    HALO_CHECK(msm_radix_sort(digits, E, SN, B, key_bits, M.sort, &skeys, &svals, &scount, nullptr, NB, s));
+    {
+        ProfScope prof("msm_acc", s);
+        const uint32_t nblocks = (uint32_t)grid_for(nchunks, 256);
+        auto kacc = k_acc<Cv, false>;
+        HALO_LAUNCH(prof, kacc, dim3(nblocks), dim3(256), 0, s, (const uint32_t*)skeys, (const uint32_t*)svals, scount,
+                    K, srs.shifted.as<const uint4>(), (uint32_t)half, ilog2(half), srs.n, lgm, 0u, P_first, P_last,
+                    M.bucket_sums.as<uint4>(), (uint32_t*)nullptr, nblocks, M.bstart.as<uint32_t>(), (uint32_t)NB,
+                    (uint32_t)(c - 1), (uint32_t)m);
+        HALO_HIP(hipGetLastError());
+    }
+    MsmTailArgs ta;
+    ta.n = E;
+    ta.skeys = skeys;
+    ta.scount = scount;
+    ta.K = K;
+    ta.NB = NB;
+    ta.E = E;
+    ta.first = P_first;
+    ta.last = P_last;
+    ta.g1 = P_g1;
+    ta.g2 = P_g2;
+    ta.ng1 = ng1;
+    ta.ng2 = ng2;
+    ta.bstart = M.bstart.as<uint32_t>();
+    ta.bucket_sums = M.bucket_sums.as<uint4>();
+    ta.rows = M.seg_acc.as<uint4>();
+    ta.cols = M.seg_sum.as<uint4>();
+    ta.terms = M.bits.as<uint4>();
+    ta.window_sums = M.window_sums.as<uint4>();
+    ta.L = L;
+    ta.H = H;
+    ta.logH = logH;
+    ta.logL = logL;
+    ta.NT = NT;
+    ta.SW = SW;
+    ta.c = c;
+    ta.hide_table = nullptr;
+    ta.hide_scalar = nullptr;
+    ta.out_wrapped = nullptr;
+    HALO_CHECK(msm_tail_launch(curve_id<Cv>(), ta, s));
+    HALO_HIP(hipStreamWaitEvent(s, M.front_done, 0));  // the hiding terms
+    hipLaunchKernelGGL(k_final<Cv>, dim3(1), dim3(64), 0, s, M.window_sums.as<const uint4>(), 1, c,
+                       (const uint4*)hide_slot, out_l, 1);
+    hipLaunchKernelGGL(k_final<Cv>, dim3(1), dim3(64), 0, s, M.window_sums.as<const uint4>() + 8, 1, c,
+                       (const uint4*)(hide_slot + 8), out_r, 1);
+    HALO_HIP(hipGetLastError());
+    HALO_HIP(hipEventRecord(M.tail_done, s));
+    M.tail_pending = true;
+    M.owner = s;
+    return HALO_OK;
+}
+
+int msm_srs_pair_device(DeviceState* st, int curve, const void* sl, const void* sr, size_t half, uint32_t lgm,
+                        const void* hide_table, const void* hide_l, const void* hide_r, void* out_l, void* out_r,
+                        hipStream_t s, hipEvent_t hide_ready) {
+    int rc;
+    DISPATCH_CURVE(curve, Cv, {
+        rc = msm_srs_pair_t<Cv>(st, (const uint4*)sl, (const uint4*)sr, half, lgm, (const uint4*)hide_table,
+                                (const uint4*)hide_l, (const uint4*)hide_r, (uint4*)out_l, (uint4*)out_r, s,
+                                hide_ready);
+    });
+    return rc;
 }
 
 // polynomials up to this length take the one-MSM batch path (HALO_MSM_MULTI_MAX overrides; 0 = off)
@@ -1064,7 +1193,7 @@ static int msm_shared_batch_t(DeviceState* st, const uint4* bases, const uint4* 
     hipLaunchKernelGGL((k_acc<Cv, false>), dim3(grid_for(nchunks, 256)), dim3(256), 0, s, S.keys.as<const uint32_t>(),
                        S.vals.as<const uint32_t>(), (const uint32_t*)(tot + 1), K, bases, 1u, 0u, (size_t)0, 32u, 0u,
                        P_first, P_last, S.bucket_sums.as<uint4>(), (uint32_t*)nullptr, (uint32_t)grid_for(nchunks, 256),
-                       S.bstart.as<uint32_t>(), (uint32_t)NB);
+                       S.bstart.as<uint32_t>(), (uint32_t)NB, 31u, 0u);
     HALO_HIP(hipGetLastError());
     MsmTailArgs ta;
     ta.n = T;
