@@ -1006,6 +1006,12 @@ static int ipa_tail_sums(halo_ipa_session* ses, int mode, hipStream_t s) {
     return HALO_OK;
 }
 
+static int ipa_copy_out(halo_ipa_session* ses) {
+    // L, R as packed XYZZ (128 B each): the affine conversion runs on the host (host_xyzz_to_wrapped)
+    HALO_HIP(hipMemcpyAsync(ses->pinned + 256, (char*)ses->small.ptr + 512, 256, hipMemcpyDeviceToHost, ses->s));
+    return HALO_OK;
+}
+
 // Enqueues one round's L and R (with their H' terms) and their D2H copy into ses->pinned.
 static int ipa_round_launch(DeviceState* st, halo_ipa_session* ses) {
     if (ses->m == 0) return set_error(HALO_EINVAL, "halo_ipa_round_lr: no rounds left");
@@ -1075,8 +1081,8 @@ static int ipa_round_launch(DeviceState* st, halo_ipa_session* ses) {
             return e ? (size_t)atoll(e) : IPA_PAIR_MAX;
         }();
         if (half <= pair_max) {
-            HALO_CHECK(msm_srs_pair_device(st, ses->curve, sl, sr, half, lgm, ses->htab_ptr, sm + 128, sm + 160,
-                                           sm + 512, sm + 640, s, hr));
+            const MsmPairIO io{sl, sr, sm + 128, sm + 160, sm + 512, sm + 640};
+            HALO_CHECK(msm_srs_pairs_device(st, ses->curve, 1, &io, half, lgm, ses->htab_ptr, s, hr));
         } else {
             HALO_CHECK(msm_srs_range_device(st, ses->curve, 0, sl, half, ses->htab_ptr, sm + 128, sm + 512, s, true,
                                             lgm, true, true, hr));
@@ -1099,9 +1105,7 @@ static int ipa_round_launch(DeviceState* st, halo_ipa_session* ses) {
         }
         HALO_CHECK(msm_join(st, s));
     }
-    // L, R as packed XYZZ (128 B each): the affine conversion runs on the host (host_xyzz_to_wrapped)
-    HALO_HIP(hipMemcpyAsync(ses->pinned + 256, sm + 512, 256, hipMemcpyDeviceToHost, s));
-    return HALO_OK;
+    return ipa_copy_out(ses);
 }
 
 // Enqueues one fold with challenge xi (pcdl.rs:427-435); the session advances to the next round.

@@ -27,6 +27,7 @@
 #include "msm.hpp"
 #include "runtime.hpp"
 #include "sort.hpp"
+#include "tree.hpp"
 
 namespace halo {
 
@@ -206,8 +207,8 @@ __device__ __forceinline__ void acc_chunk(size_t t, uint32_t cnt, const uint32_t
             const uint32_t w = npw_lg < 32 ? (uint32_t)idx >> npw_lg : (uint32_t)idx / n_per_window;
             uint32_t i = (uint32_t)idx - w * n_per_window;
             if (blk_lg < 32) i += (i >> blk_lg) << blk_lg;  // blocks of 2^blk_lg at stride 2^(blk_lg+1)
-            // + the point offset of the entry's output (k >> key_lg: msm_srs_pair's R at offset m)
-            idx = (size_t)w * stride + i + (size_t)(k >> key_lg) * poly_off;
+            // + the point offset of the entry's output (msm_srs_pairs: output k >> key_lg, odd = R at m)
+            idx = (size_t)w * stride + i + (size_t)((k >> key_lg) & 1u) * poly_off;
         }
         const bool phi = glv_n && idx >= glv_n;  // GLV: phi(G_i)
         if (phi) idx -= glv_n;
@@ -258,11 +259,11 @@ __global__ __launch_bounds__(256, HALO_ACC_MINB) void k_acc(const uint32_t* keys
 // long.  Launched on the tail stream when the MSM starts, so it runs beside the digit / sort /
 // accumulation phase instead of on the tail's critical path.
 template <class Cv>
-__global__ __launch_bounds__(256) void k_hide_term(const uint4* hide_table /* internal affine 2^i P */,
-                                                   const uint4* hide_scalar /* ark */, int glv, uint4* hide_out) {
+__device__ __forceinline__ void hide_term_block(const uint4* hide_table, const uint4* hide_scalar, int glv,
+                                                uint4* hide_out) {
     using F = typename Cv::Base;
     using S = typename Cv::Scalar;
-    __shared__ uint4 red[256 * 8];
+    __shared__ uint4 red[128 * 8];
     __shared__ uint32_t kw[8];
     __shared__ uint32_t neg[2];
     const int i = threadIdx.x;
@@ -293,13 +294,35 @@ __global__ __launch_bounds__(256) void k_hide_term(const uint4* hide_table /* in
         }
         v = xyzz_from_aff(p);
     }
-    xyzz_store(red + 8 * i, v);
-    for (int off = 128; off > 0; off >>= 1) {
-        __syncthreads();
-        if (i < off) xyzz_store(red + 8 * i, xyzz_add(xyzz_load<F>(red + 8 * i), xyzz_load<F>(red + 8 * (i + off))));
-    }
-    __syncthreads();
-    if (i == 0) xyzz_store(hide_out, xyzz_load<F>(red));
+    v = block_group_sum<F>(v, 256, red);
+    if (i == 0) xyzz_store(hide_out, v);
+}
+
+template <class Cv>
+__global__ __launch_bounds__(256) void k_hide_term(const uint4* hide_table /* internal affine 2^i P */,
+                                                   const uint4* hide_scalar /* ark */, int glv, uint4* hide_out) {
+    hide_term_block<Cv>(hide_table, hide_scalar, glv, hide_out);
+}
+
+// up to 8 hiding terms (msm_srs_pairs): block b -> hide_out + 8 b
+struct HideScalars {
+    const uint4* sc[8];
+};
+template <class Cv>
+__global__ __launch_bounds__(256) void k_hide_terms(const uint4* hide_table, HideScalars hs, int glv, uint4* hide_out) {
+    hide_term_block<Cv>(hide_table, hs.sc[blockIdx.x], glv, hide_out + 8 * blockIdx.x);
+}
+
+// msm_srs_pairs' outputs: out[p] = window_sums[p] + hide[p], packed XYZZ
+struct PairOuts {
+    uint4* o[8];
+};
+template <class Cv>
+__global__ __launch_bounds__(64) void k_pairs_out(const uint4* window_sums, const uint4* hide, PairOuts outs, int P) {
+    using F = typename Cv::Base;
+    const int p = threadIdx.x;
+    if (p >= P) return;
+    xyzz_store(outs.o[p], xyzz_add(xyzz_load<F>(window_sums + 8 * p), xyzz_load<F>(hide + 8 * p)));
 }
 
 // Horner over the window sums (one lane; the c doublings per window run in Jacobian coordinates),
@@ -821,32 +844,34 @@ static int msm_multi_device_t(DeviceState* st, const void* const* scalars, const
 }
 
 // ---------------------------------------------------------------------------------------------
-// The IPA's weighted-round pair (ipa.hip): L = sum_i sl[i] G[map(i)] and R = sum_i sr[i] G[m + map(i)],
+// The IPA's weighted-round pairs (ipa.hip): L = sum_i sl[i] G[map(i)] and R = sum_i sr[i] G[m + map(i)],
 // map(i) = i + (i >> lg m) << lg m (the left / right halves of the 2m-blocks), each plus its hiding
-// term dot H' from the 2^i table -- ONE MSM over the window-shifted SRS with key (side, bucket): one
-// digit pass, one sort, one accumulation and one reduction tail (SW = 2) instead of two MSMs whose
-// front and accumulation run one after the other.  Outputs packed XYZZ (128 B each) at out[0], out[1].
+// term dot H' from the 2^i table, for np <= 4 sessions in lockstep -- ONE MSM over the window-shifted
+// SRS with key (output, bucket): one digit pass, one sort, one accumulation and one reduction tail
+// (SW = 2 np) instead of 2 np MSMs whose fronts and accumulations run one after the other.  Outputs
+// packed XYZZ (128 B each).
 // ---------------------------------------------------------------------------------------------
 template <class Cv>
-static int msm_srs_pair_t(DeviceState* st, const uint4* sl, const uint4* sr, size_t half, uint32_t lgm,
-                          const uint4* hide_table, const uint4* hide_l, const uint4* hide_r, uint4* out_l,
-                          uint4* out_r, hipStream_t s, hipEvent_t hide_ready) {
+static int msm_srs_pairs_t(DeviceState* st, size_t np, const MsmPairIO* io, size_t half, uint32_t lgm,
+                           const uint4* hide_table, hipStream_t s, hipEvent_t hide_ready) {
     SrsState& srs = st->srs[curve_id<Cv>()];
     const size_t m = (size_t)1 << lgm;
-    if (!srs.shifted_c) return set_error(HALO_EINVAL, "msm_srs_pair: no window-shifted SRS");
+    if (!srs.shifted_c) return set_error(HALO_EINVAL, "msm_srs_pairs: no window-shifted SRS");
+    if (!np || np > 4) return set_error(HALO_EINVAL, "msm_srs_pairs: %zu pairs (1..4)", np);
     if (!half || (half & (half - 1)) || half % m || 2 * half > srs.n)
-        return set_error(HALO_EINVAL, "msm_srs_pair: %zu terms per side, blocks of %zu, SRS %zu", half, m, srs.n);
+        return set_error(HALO_EINVAL, "msm_srs_pairs: %zu terms per side, blocks of %zu, SRS %zu", half, m, srs.n);
     MsmPipe& PP = g_msm_pipe[st->device & 63];
     HALO_CHECK(pipe_init(PP));
     const int set = msm_pick_set(PP, s, true);
     MsmScratch& M = PP.set[set];
     if (M.tail_pending) HALO_HIP(hipStreamWaitEvent(s, M.tail_done, 0));
     const hipStream_t ts = PP.tail[set];
+    const int P = (int)(2 * np);  // outputs: L0, R0, L1, R1, ...
     const int c = srs.shifted_c, W = msm_windows(c);
     const uint32_t B = 1u << (c - 1);
-    const size_t SN = (size_t)W * half, E = 2 * SN, NB = 2 * (size_t)B;
-    const int SW = 2;
-    if (E >= (1ull << 32)) return set_error(HALO_EINVAL, "msm_srs_pair: too large");
+    const size_t SN = (size_t)W * half, E = P * SN, NB = P * (size_t)B;
+    const int SW = P;
+    if (E >= (1ull << 32)) return set_error(HALO_EINVAL, "msm_srs_pairs: too large");
     const uint32_t L = std::min<uint32_t>(MSM_SEG_L, B), logL = ilog2(L), H = B / L, logH = ilog2(H);
     const uint32_t NT = 1 + logH + logL;
     const uint32_t key_bits = ilog2(NB - 1) + 1;
@@ -860,7 +885,7 @@ static int msm_srs_pair_t(DeviceState* st, const uint4* sl, const uint4* sr, siz
     HALO_CHECK(M.seg_acc.reserve((size_t)SW * H * 128));
     HALO_CHECK(M.seg_sum.reserve((size_t)SW * L * 128));
     HALO_CHECK(M.bits.reserve((size_t)SW * NT * 128));
-    HALO_CHECK(M.window_sums.reserve((size_t)(SW + 2) * 128));  // + the two hiding terms
+    HALO_CHECK(M.window_sums.reserve((size_t)(2 * SW) * 128));  // + the hiding terms
     uint4* P_first = M.partials.as<uint4>();
     uint4* P_last = P_first + 8 * nchunks;
     uint4* P_g1 = P_last + 8 * nchunks;
@@ -870,15 +895,21 @@ static int msm_srs_pair_t(DeviceState* st, const uint4* sl, const uint4* sr, siz
     HALO_HIP(hipEventRecord(M.start, s));
     HALO_HIP(hipStreamWaitEvent(ts, M.start, 0));
     if (hide_ready) HALO_HIP(hipStreamWaitEvent(ts, hide_ready, 0));
-    hipLaunchKernelGGL(k_hide_term<Cv>, dim3(1), dim3(256), 0, ts, hide_table, hide_l, 1, hide_slot);
-    hipLaunchKernelGGL(k_hide_term<Cv>, dim3(1), dim3(256), 0, ts, hide_table, hide_r, 1, hide_slot + 8);
+    HideScalars hs{};
+    PairOuts outs{};
+    for (size_t q = 0; q < np; q++) {
+        hs.sc[2 * q] = (const uint4*)io[q].hide_l;
+        hs.sc[2 * q + 1] = (const uint4*)io[q].hide_r;
+        outs.o[2 * q] = (uint4*)io[q].out_l;
+        outs.o[2 * q + 1] = (uint4*)io[q].out_r;
+    }
+    hipLaunchKernelGGL(k_hide_terms<Cv>, dim3(P), dim3(256), 0, ts, hide_table, hs, 1, hide_slot);
     HALO_HIP(hipGetLastError());
     HALO_HIP(hipEventRecord(M.front_done, ts));
     uint32_t* digits = M.digits.as<uint32_t>();
-    hipLaunchKernelGGL(k_digits<typename Cv::Scalar>, dim3(grid_for(half, 256)), dim3(256), 0, s, sl, half, c, W,
-                       digits, half, 0, W);
-    hipLaunchKernelGGL(k_digits<typename Cv::Scalar>, dim3(grid_for(half, 256)), dim3(256), 0, s, sr, half, c, W,
-                       digits + SN, half, 0, W);
+    for (int p = 0; p < P; p++)
+        hipLaunchKernelGGL(k_digits<typename Cv::Scalar>, dim3(grid_for(half, 256)), dim3(256), 0, s,
+                           (const uint4*)(p & 1 ? io[p / 2].sr : io[p / 2].sl), half, c, W, digits + p * SN, half, 0, W);
     HALO_HIP(hipGetLastError());
     uint32_t *skeys = nullptr, *svals = nullptr;
     const uint32_t* scount = nullptr;
@@ -924,10 +955,8 @@ static int msm_srs_pair_t(DeviceState* st, const uint4* sl, const uint4* sr, siz
     ta.out_wrapped = nullptr;
     HALO_CHECK(msm_tail_launch(curve_id<Cv>(), ta, s));
     HALO_HIP(hipStreamWaitEvent(s, M.front_done, 0));  // the hiding terms
-    hipLaunchKernelGGL(k_final<Cv>, dim3(1), dim3(64), 0, s, M.window_sums.as<const uint4>(), 1, c,
-                       (const uint4*)hide_slot, out_l, 1);
-    hipLaunchKernelGGL(k_final<Cv>, dim3(1), dim3(64), 0, s, M.window_sums.as<const uint4>() + 8, 1, c,
-                       (const uint4*)(hide_slot + 8), out_r, 1);
+    hipLaunchKernelGGL(k_pairs_out<Cv>, dim3(1), dim3(64), 0, s, M.window_sums.as<const uint4>(),
+                       (const uint4*)hide_slot, outs, P);
     HALO_HIP(hipGetLastError());
     HALO_HIP(hipEventRecord(M.tail_done, s));
     M.tail_pending = true;
@@ -935,14 +964,11 @@ static int msm_srs_pair_t(DeviceState* st, const uint4* sl, const uint4* sr, siz
     return HALO_OK;
 }
 
-int msm_srs_pair_device(DeviceState* st, int curve, const void* sl, const void* sr, size_t half, uint32_t lgm,
-                        const void* hide_table, const void* hide_l, const void* hide_r, void* out_l, void* out_r,
-                        hipStream_t s, hipEvent_t hide_ready) {
+int msm_srs_pairs_device(DeviceState* st, int curve, size_t np, const MsmPairIO* io, size_t half, uint32_t lgm,
+                         const void* hide_table, hipStream_t s, hipEvent_t hide_ready) {
     int rc;
     DISPATCH_CURVE(curve, Cv, {
-        rc = msm_srs_pair_t<Cv>(st, (const uint4*)sl, (const uint4*)sr, half, lgm, (const uint4*)hide_table,
-                                (const uint4*)hide_l, (const uint4*)hide_r, (uint4*)out_l, (uint4*)out_r, s,
-                                hide_ready);
+        rc = msm_srs_pairs_t<Cv>(st, np, io, half, lgm, (const uint4*)hide_table, s, hide_ready);
     });
     return rc;
 }

@@ -45,12 +45,16 @@ int msm_srs_range_device(DeviceState* st, int curve, size_t offset, const void* 
 struct BatchScratch {
     DevBuf digits, lists, keys, vals, bstart, partials, bucket_sums, window_sums;
 };
-// The IPA weighted round's L and R (sum_i sl[i] G[map(i)], sum_i sr[i] G[m + map(i)], map(i) =
-// i + (i >> lgm) << lgm, m = 2^lgm) each plus dot H' (hide_l / hide_r ark scalars, GLV table), as one
-// MSM over the window-shifted SRS; packed XYZZ outputs; asynchronous on s (msm_join).
-int msm_srs_pair_device(DeviceState* st, int curve, const void* sl, const void* sr, size_t half, uint32_t lgm,
-                        const void* hide_table, const void* hide_l, const void* hide_r, void* out_l, void* out_r,
-                        hipStream_t s, hipEvent_t hide_ready);
+// The IPA weighted rounds' L and R (sum_i sl[i] G[map(i)], sum_i sr[i] G[m + map(i)], map(i) =
+// i + (i >> lgm) << lgm, m = 2^lgm) each plus dot H' (hide_l / hide_r ark scalars, GLV table), for
+// np <= 4 sessions with the same geometry, as one MSM over the window-shifted SRS; packed XYZZ
+// outputs; asynchronous on s (msm_join).
+struct MsmPairIO {
+    const void *sl, *sr, *hide_l, *hide_r;
+    void *out_l, *out_r;
+};
+int msm_srs_pairs_device(DeviceState* st, int curve, size_t np, const MsmPairIO* io, size_t half, uint32_t lgm,
+                         const void* hide_table, hipStream_t s, hipEvent_t hide_ready);
 // shift_stride > 0: bases are the resident window-shifted SRS (copy w = 2^(c_s w) G at w shift_stride):
 // every c_s-bit digit of w[u] is split into three unsigned sub-digits, so the final Horner runs
 // over three windows (~2 c_s / 3 doublings) instead of ~255 / c windows (~255 doublings).

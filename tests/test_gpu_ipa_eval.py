@@ -139,6 +139,49 @@ def test_ipa_xi_mode_equals_h_prime(hal, corc, cname, cid, n):
         assert np.array_equal(Ua, Ub) and np.array_equal(ca, cb), trial
 
 
+@pytest.mark.parametrize("k", [2, 3, 5])
+def test_ipa_lockstep_sessions_equal_single(hal, corc, k):
+    """halo_ipa_round_lr_multi over k sessions in lockstep (their weighted rounds share one L/R MSM,
+    up to 4 sessions per MSM) gives every session's L, R, U, c exactly as that session run alone."""
+    import ctypes
+    c = P.PALLAS
+    r = c.scalar
+    n = 1 << 13
+    L = hal.load()
+    g = corc.srs_generate("pallas", n)
+    group.PublicParams.upload("pallas", g, precompute_windows=True)
+    rng = random.Random(k)
+    Hw = np.array(P.point_to_wrapped(c, P.mul_fast(c, rng.randrange(1, r), c.generator)), dtype=np.uint64)
+    jobs = [(fe([rng.randrange(r) for _ in range(n)], r), fe([rng.randrange(r)], r), fe([rng.randrange(1, r)], r))
+            for _ in range(k)]
+    chal = [[fe([rng.randrange(1, r)], r)[0] for _ in range(13)] for _ in range(k)]
+    inv = [[fe([P.inv(P.from_mont(P.limbs_to_int(x), r), r)], r)[0] for x in row] for row in chal]
+
+    def run(idx):
+        sess = [pcdl.IpaSession.with_xi(jobs[i][0], jobs[i][1], Hw, jobs[i][2], "pallas") for i in idx]
+        arr = (ctypes.c_void_p * len(sess))(*[s_._s.value for s_ in sess])
+        out = [([], []) for _ in idx]
+        for rd in range(13):
+            Lb = np.zeros((len(idx), 8), dtype=np.uint64)
+            Rb = np.zeros((len(idx), 8), dtype=np.uint64)
+            hal.check(L.halo_ipa_round_lr_multi(arr, len(idx), hal.ptr(Lb), hal.ptr(Rb)))
+            xa = np.ascontiguousarray(np.stack([chal[i][rd] for i in idx]))
+            xia = np.ascontiguousarray(np.stack([inv[i][rd] for i in idx]))
+            hal.check(L.halo_ipa_fold_multi(arr, len(idx), hal.ptr(xa), hal.ptr(xia)))
+            for q in range(len(idx)):
+                out[q][0].append(Lb[q].copy())
+                out[q][1].append(Rb[q].copy())
+        ends = [s_.end() for s_ in sess]
+        return [(o[0], o[1], e[0], e[1]) for o, e in zip(out, ends)]
+
+    together = run(list(range(k)))
+    for i in range(k):
+        alone = run([i])[0]
+        for a, b in zip(together[i][0] + together[i][1], alone[0] + alone[1]):
+            assert np.array_equal(a, b), i
+        assert np.array_equal(together[i][2], alone[2]) and np.array_equal(together[i][3], alone[3]), i
+
+
 def test_ipa_fold_large_vs_c_oracle(hal, corc):
     """One fold at m = 2^14 (per-element scalar multiplication + affine normalisation)."""
     c = P.PALLAS

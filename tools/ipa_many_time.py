@@ -13,15 +13,15 @@ H.check(L.halo_srs_precompute_windows(0))
 B = prover.DeviceBackend("pallas")
 rng = np.random.default_rng(2)
 ps = [B.random_vec(n, rng) for _ in range(3)]
-for rep in range(2):
+for rep in range(3):
     for k in (1, 2, 3):
-        jobs = [(ps[i], n, 1234 + i, B.h_mul(77 + i)) for i in range(k)]
+        jobs = [(ps[i], n, 1234 + i, 77 + i) for i in range(k)]  # (p, n, z, xi_0): the prover's xi mode
         chals = [prover.Challenges(B.m, seed=i) for i in range(k)]
         B.sync()
         t = time.perf_counter()
-        B.ipa_many(jobs, chals)
+        B.ipa_many_xi(jobs, chals)
         print(f"rep {rep} k={k}: {1e3 * (time.perf_counter() - t):.1f} ms", flush=True)
 t = time.perf_counter()
 for i in range(2):
-    B.ipa_many([(ps[i], n, 1234 + i, B.h_mul(77 + i))], [prover.Challenges(B.m, seed=i)])
+    B.ipa_many_xi([(ps[i], n, 1234 + i, 77 + i)], [prover.Challenges(B.m, seed=i)])
 print(f"2 sequential: {1e3 * (time.perf_counter() - t):.1f} ms")
