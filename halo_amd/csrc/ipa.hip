@@ -543,6 +543,7 @@ struct halo_ipa_session {
     int wcur = 0;
     hipStream_t aux = nullptr;        // builds the 2^i H' table beside round 1's accumulation
     hipEvent_t htab_ready = nullptr;  // recorded on aux after the table
+    bool fold_inflight = false;       // a fold's H2D copy of xi may still read `pinned`
     bool htab_waited = false;         // round 1 waited for it (later rounds follow a host sync of round 1)
     // xi mode (halo_ipa_begin_xi / _dev_xi): the hiding terms use the resident 2^i H table and the
     // dots scaled by xi_0 (dot H' = (dot xi_0) H), so there is neither H' nor a per-session table
@@ -1113,6 +1114,10 @@ static int ipa_fold_launch(halo_ipa_session* ses, const halo_fe_t* xi, const hal
     if (ses->m == 0) return set_error(HALO_EINVAL, "halo_ipa_fold: no rounds left");
     hipStream_t s = ses->s;
     char* sm = (char*)ses->small.ptr;
+    // the previous fold's H2D copy from the pinned staging must have completed (a round in between
+    // synchronises the stream; two folds in a row wait here)
+    if (ses->fold_inflight) HALO_HIP(hipStreamSynchronize(s));
+    ses->fold_inflight = true;
     memcpy(ses->pinned + 128, xi, 32);
     memcpy(ses->pinned + 160, xi_inv, 32);
     HALO_HIP(hipMemcpyAsync(sm + 384, ses->pinned + 128, 64, hipMemcpyHostToDevice, s));
@@ -1162,6 +1167,7 @@ extern "C" int halo_ipa_round_lr_multi(halo_ipa_session* const* ses, size_t k, h
     }
     for (size_t i = 0; i < k; i++) {
         HALO_HIP(hipStreamSynchronize(ses[i]->s));
+        ses[i]->fold_inflight = false;
         host_xyzz_to_wrapped(ses[i]->curve, ses[i]->pinned + 256, &L[i]);
         host_xyzz_to_wrapped(ses[i]->curve, ses[i]->pinned + 384, &R[i]);
     }
@@ -1185,7 +1191,8 @@ extern "C" int halo_ipa_fold_multi(halo_ipa_session* const* ses, size_t k, const
         if (!ses[i]) return set_error(HALO_EINVAL, "halo_ipa_fold_multi: null session %zu", i);
         HALO_CHECK(ipa_fold_launch(ses[i], &xi[i], &xi_inv[i]));
     }
-    for (size_t i = 0; i < k; i++) HALO_HIP(hipStreamSynchronize(ses[i]->s));
+    // no host wait: the fold is stream-ordered before the next round (which synchronises), so the host
+    // goes on to the transcript and the next round's launches while it runs
     return HALO_OK;
 }
 
