@@ -50,20 +50,34 @@ struct RsIn {
     uint32_t shift;  // digit = (key >> shift) & 255
 };
 
-// entry e of the pass input -> (key, val) or invalid
-HALO_DEV bool rs_fetch(const RsIn& in, size_t e, size_t limit, uint32_t& key, uint32_t& val) {
+// Entry e of the pass input, in two phases so that a thread's loads for all its rounds are issued
+// back to back: rs_load reads the raw words at a clamped index (no control flow depends on loaded
+// data; the arrays hold at least one word), rs_decode then forms (key, val) or rejects the entry.
+// PASS0: a = digit (val unused); later passes: a = key, b = val (b only when WANT_VAL).
+template <bool PASS0, bool WANT_VAL = true>
+HALO_DEV void rs_load(const RsIn& in, size_t e, size_t limit, uint32_t& a, uint32_t& b) {
+    const size_t ec = e < limit ? e : (limit ? limit - 1 : 0);
+    if constexpr (PASS0) {
+        a = in.digits[ec];
+        b = 0;
+    } else {
+        a = in.keys[ec];
+        b = WANT_VAL ? in.vals[ec] : 0u;
+    }
+}
+template <bool PASS0>
+HALO_DEV bool rs_decode(const RsIn& in, size_t e, size_t limit, uint32_t a, uint32_t b, uint32_t& key, uint32_t& val) {
     if (e >= limit) return false;
-    if (in.pass == 0) {
-        const uint32_t d = in.digits[e];
-        if (d == RS_NONE) return false;
+    if constexpr (PASS0) {
+        if (a == RS_NONE) return false;
         // entries < 2^32; one window (npw >= E) needs no division
         const uint32_t w = (in.npw >= in.E) ? 0u : (uint32_t)e / (uint32_t)in.npw;
-        key = w * in.B + (d & 0x7fffffffu);
-        val = ((uint32_t)e - w * (uint32_t)in.npw) | (d & 0x80000000u);
-        return true;
+        key = w * in.B + (a & 0x7fffffffu);
+        val = ((uint32_t)e - w * (uint32_t)in.npw) | (a & 0x80000000u);
+    } else {
+        key = a;
+        val = b;
     }
-    key = in.keys[e];
-    val = in.vals[e];
     return true;
 }
 
@@ -173,18 +187,24 @@ HALO_DEV void rs_publish_and_scan(const uint32_t* h, uint32_t tile, uint32_t nti
     if (d == 0) __hip_atomic_store(ctr + nchunks, 0u, RS_RLX_AGENT);
 }
 
-template <int ROUNDS>
+template <int ROUNDS, bool PASS0>
 __global__ __launch_bounds__(RS_THREADS) void k_rs_hist(RsIn in, uint32_t ntiles, uint32_t* hist, uint32_t* chunk,
                                                         uint32_t* ctr, uint32_t* count) {
     constexpr int RS_TILE = RS_THREADS * ROUNDS;
     __shared__ uint32_t h[RS_BINS];
     if (threadIdx.x < RS_BINS) h[threadIdx.x] = 0;
-    __syncthreads();
     const size_t limit = rs_limit(in);
     const size_t base = (size_t)blockIdx.x * RS_TILE;
+    // every round's load in flight before the first use (keys only: the histogram needs no values)
+    uint32_t A[ROUNDS], Bv[ROUNDS];
+#pragma unroll
+    for (int r = 0; r < ROUNDS; r++)
+        rs_load<PASS0, false>(in, base + (size_t)r * RS_THREADS + threadIdx.x, limit, A[r], Bv[r]);
+    __syncthreads();
+#pragma unroll
     for (int r = 0; r < ROUNDS; r++) {
         uint32_t k, v;
-        if (rs_fetch(in, base + (size_t)r * RS_THREADS + threadIdx.x, limit, k, v))
+        if (rs_decode<PASS0>(in, base + (size_t)r * RS_THREADS + threadIdx.x, limit, A[r], Bv[r], k, v))
             atomicAdd(&h[(k >> in.shift) & 255u], 1u);
     }
     __syncthreads();
@@ -215,7 +235,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_hist_sc(const uint4* sc, uint
 // wave-local (ballots + a wave-private LDS run counter per digit) and the workgroup needs only
 // three barriers: after the per-wave histograms, after the prefix, after staging.
 // SF: void, or the scalar field of a fused first pass (k_rs_hist_sc's entries, in.sc != null)
-template <int ROUNDS, class SF = void>
+template <int ROUNDS, class SF = void, bool PASS0 = false>
 __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(RsIn in, const uint32_t* tile_off, const uint32_t* chunk_off,
                                                            uint32_t* keys_out, uint32_t* vals_out) {
     constexpr int RS_TILE = RS_THREADS * ROUNDS;
@@ -250,11 +270,14 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(RsIn in, const uint32
             });
     } else {
         // all loads of the tile issued back to back (memory-level parallelism), kept in registers
+        uint32_t A[R], Bv[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) rs_load<PASS0>(in, wbase + (size_t)r * 64 + lane, limit, A[r], Bv[r]);
 #pragma unroll
         for (int r = 0; r < R; r++) {
             K[r] = 0;
             V[r] = 0;
-            if (rs_fetch(in, wbase + (size_t)r * 64 + lane, limit, K[r], V[r])) validmask |= 1u << r;
+            if (rs_decode<PASS0>(in, wbase + (size_t)r * 64 + lane, limit, A[r], Bv[r], K[r], V[r])) validmask |= 1u << r;
         }
     }
     if (tid < RS_BINS) {
@@ -495,9 +518,10 @@ int msm_radix_sort(const uint32_t* digits, size_t E, size_t npw, uint32_t B, uin
             });
         } else {
             // pass 0 also stores the number of valid (nonzero-digit) entries
-            hipLaunchKernelGGL(small_tiles ? k_rs_hist<8> : k_rs_hist<16>, dim3(nt), dim3(RS_THREADS), 0, s, in, nt,
-                               S.hist.as<uint32_t>(), S.offs.as<uint32_t>(), S.ctr.as<uint32_t>(),
-                               p == 0 ? S.count.as<uint32_t>() : nullptr);
+            auto kh = p == 0 ? (small_tiles ? k_rs_hist<8, true> : k_rs_hist<16, true>)
+                             : (small_tiles ? k_rs_hist<8, false> : k_rs_hist<16, false>);
+            hipLaunchKernelGGL(kh, dim3(nt), dim3(RS_THREADS), 0, s, in, nt, S.hist.as<uint32_t>(), S.offs.as<uint32_t>(),
+                               S.ctr.as<uint32_t>(), p == 0 ? S.count.as<uint32_t>() : nullptr);
         }
         if (fp) {
             DISPATCH_FIELD(fused->field, SF, {
@@ -506,9 +530,10 @@ int msm_radix_sort(const uint32_t* digits, size_t E, size_t npw, uint32_t B, uin
                                    S.vals[cur].as<uint32_t>());
             });
         } else {
-            hipLaunchKernelGGL(small_tiles ? k_rs_scatter<8> : k_rs_scatter<16>, dim3(nt), dim3(RS_THREADS), 0, s, in,
-                               S.hist.as<const uint32_t>(), S.offs.as<const uint32_t>(), S.keys[cur].as<uint32_t>(),
-                               S.vals[cur].as<uint32_t>());
+            auto ks = p == 0 ? (small_tiles ? k_rs_scatter<8, void, true> : k_rs_scatter<16, void, true>)
+                             : (small_tiles ? k_rs_scatter<8, void, false> : k_rs_scatter<16, void, false>);
+            hipLaunchKernelGGL(ks, dim3(nt), dim3(RS_THREADS), 0, s, in, S.hist.as<const uint32_t>(),
+                               S.offs.as<const uint32_t>(), S.keys[cur].as<uint32_t>(), S.vals[cur].as<uint32_t>());
         }
         HALO_HIP(hipGetLastError());
         cur ^= 1;
