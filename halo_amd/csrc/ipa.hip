@@ -327,15 +327,19 @@ static int dot_device(int field, const void* x, const void* y, size_t n, void* o
 // session keeps G0 = G at the switch round and the fold weights w (G_j[i] = sum_u w[u] G0[i + u len],
 // fold: w' = interleave(w, xi w)).  L and R are then direct sums over G0 with expanded scalars
 //   k = j + u len:  s[k] = c[m + j] w[u] (j < m, -> L),  c[j - m] w[u] (j >= m, -> R),
-// evaluated from a table 2^(8 win) G0[k] (win < 16, built once): each scalar is split by GLV,
-// s = k1 + lambda k2 with |k1|, |k2| < 2^128, so every (k, win, half) term is an 8-bit
-// double-and-add (~16 dependent curve operations) of the table entry or of phi of it (x -> beta x),
-// then block trees.  The table's doubling chain is 120 doublings instead of 248.
+// evaluated from a table d 2^(4 win) G0[k] (win < 32, 1 <= d <= 15, built once per session): each
+// scalar is split by GLV, s = k1 + lambda k2 with |k1|, |k2| < 2^128, so every (k, win, half) term
+// is one table entry (or phi of it, x -> beta x) selected by a 4-bit digit -- no per-term
+// double-and-add chain on the rounds' critical path -- and the terms go through block trees.  The
+// table's doubling chain is 124 doublings instead of 248; the 15 multiples of each 2^(4 win) G0[k]
+// cost 14 curve operations per (win, k) lane, once.
 // U = sum_u w[u] G0[u] at the end.  c and z keep their ordinary elementwise folds (pcdl.rs:430-435).
 constexpr size_t IPA_TAIL_N = 2048;
 constexpr int IPA_HTAB = 128;  // entries 2^i H' of the session's hiding table (GLV split of the scalar)
-constexpr int TAIL_TBL = 16;                          // table windows (8 bits each: 128-bit GLV halves)
-constexpr int TAIL_WIN = 2 * TAIL_TBL, TAIL_THREADS = 256;  // terms per point: 16 windows x (k1, k2)
+constexpr int TAIL_DB = 4;                            // digit bits
+constexpr int TAIL_TBL = 128 / TAIL_DB;               // table windows per 128-bit GLV half
+constexpr int TAIL_MUL = (1 << TAIL_DB) - 1;          // multiples d = 1..15 per window
+constexpr int TAIL_WIN = 2 * TAIL_TBL, TAIL_THREADS = 256;  // terms per point: 32 windows x (k1, k2)
 
 // the doubling chain in Jacobian coordinates (dbl-2009-l: 7 multiplications against XYZZ's 9)
 template <class Cv>
@@ -347,8 +351,40 @@ __global__ __launch_bounds__(64) void k_tail_table(const uint4* gs, int gs_xyzz,
     xyzz_store(table + 8 * k, p0);
     Jac<F> j = jac_from_xyzz(p0);
     for (int w = 1; w < TAIL_TBL; w++) {
-        for (int b = 0; b < 8; b++) j = jac_dbl(j);
-        xyzz_store(table + 8 * ((size_t)w * n0 + k), jac_to_xyzz(j));
+        for (int b = 0; b < TAIL_DB; b++) j = jac_dbl(j);
+        xyzz_store(table + 8 * ((size_t)w * TAIL_MUL * n0 + k), jac_to_xyzz(j));
+    }
+}
+
+// entry (w, d, k) of the tail table: d 2^(4 w) G0[k], 1 <= d <= 15 (XYZZ)
+HALO_DEV size_t tail_entry(size_t w, uint32_t d, size_t n0, size_t k) {
+    return 8 * ((w * TAIL_MUL + (d - 1)) * n0 + k);
+}
+
+// The multiples 2..15 of each window base P = 2^(4 w) G0[k] written by k_tail_table.  Lane
+// (j, w, k), j < 4, owns d = 4j + 1 .. 4j + 4: it forms (4j + 1) P by double-and-add, then a running
+// sum (two live points) -- at most 7 dependent curve operations per lane instead of 14.
+constexpr int TAIL_MLANES = 4;
+template <class Cv>
+__global__ __launch_bounds__(64) void k_tail_mults(size_t n0, uint4* table) {
+    using F = typename Cv::Base;
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (size_t)TAIL_MLANES * TAIL_TBL * n0) return;
+    const uint32_t j = (uint32_t)(t / ((size_t)TAIL_TBL * n0));
+    const size_t r = t % ((size_t)TAIL_TBL * n0), w = r / n0, k = r % n0;
+    const XYZZ<F> p = xyzz_load<F>(table + tail_entry(w, 1, n0, k));
+    const uint32_t s = 4 * j + 1;
+    XYZZ<F> cur = p;
+#pragma unroll 1
+    for (int b = 31 - __clz(s) - 1; b >= 0; b--) {  // s P, s = 4 j + 1 (bit 0 set: the last step adds)
+        cur = xyzz_dbl(cur);
+        if ((s >> b) & 1u) cur = xyzz_add(cur, p);
+    }
+    if (j) xyzz_store(table + tail_entry(w, s, n0, k), cur);
+#pragma unroll 1
+    for (uint32_t d = s + 1; d <= min(s + 3, (uint32_t)TAIL_MUL); d++) {
+        cur = (d == 2) ? xyzz_dbl(p) : xyzz_add(cur, p);
+        xyzz_store(table + tail_entry(w, d, n0, k), cur);
     }
 }
 
@@ -411,19 +447,14 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail_msm(const uint4* table, c
         k = t % n0;
     }
     if (valid) {
+        constexpr uint32_t DPW = 32 / TAIL_DB;  // digits per scalar word
         const uint32_t half = (uint32_t)win / TAIL_TBL, bw = (uint32_t)win % TAIL_TBL;
-        const uint32_t d = (scal[8 * k + 4 * half + (bw >> 2)] >> (8 * (bw & 3))) & 255u;
+        const uint32_t d = (scal[8 * k + 4 * half + bw / DPW] >> (TAIL_DB * (bw % DPW))) & (uint32_t)TAIL_MUL;
         const uint32_t sk = side[k];
         if (d) {
-            XYZZ<F> q = xyzz_load<F>(table + 8 * ((size_t)bw * n0 + k));
-            if (half) q.X = fe_mul(q.X, fe_from_const<F>(Cv::K::BETA));  // phi
-            if ((sk >> (1 + half)) & 1u) q = xyzz_neg(q);
-            const int top = 31 - __clz(d);
-            acc = q;
-            for (int b = top - 1; b >= 0; b--) {
-                acc = xyzz_dbl(acc);
-                if ((d >> b) & 1u) acc = xyzz_add(acc, q);
-            }
+            acc = xyzz_load<F>(table + tail_entry(bw, d, n0, k));
+            if (half) acc.X = fe_mul(acc.X, fe_from_const<F>(Cv::K::BETA));  // phi
+            if ((sk >> (1 + half)) & 1u) acc = xyzz_neg(acc);
         }
     }
     acc = block_group_sum<F>(acc, TAIL_THREADS, red);
@@ -965,7 +996,7 @@ extern "C" int halo_ipa_begin_vectors(halo_curve_t curve, const halo_wrapped_poi
 static int ipa_enter_tail(halo_ipa_session* ses, hipStream_t s) {
     const size_t n0 = 2 * ses->m;
     const size_t nblk = (TAIL_WIN * n0 + TAIL_THREADS - 1) / TAIL_THREADS + 2;  // (+ mode 0's per-side rounding)
-    HALO_CHECK(ses->table.reserve((size_t)TAIL_TBL * n0 * 128));
+    HALO_CHECK(ses->table.reserve((size_t)TAIL_TBL * TAIL_MUL * n0 * 128));
     HALO_CHECK(ses->w[0].reserve(n0 * 32));
     HALO_CHECK(ses->w[1].reserve(n0 * 32));
     HALO_CHECK(ses->scal.reserve(n0 * 32));
@@ -974,6 +1005,8 @@ static int ipa_enter_tail(halo_ipa_session* ses, hipStream_t s) {
     DISPATCH_CURVE(ses->curve, Cv, {
         hipLaunchKernelGGL(k_tail_table<Cv>, dim3(gridn(n0, 64)), dim3(64), 0, s, ses->gs.as<const uint4>(),
                            (int)ses->gs_xyzz, n0,
+                           ses->table.as<uint4>());
+        hipLaunchKernelGGL(k_tail_mults<Cv>, dim3(gridn((size_t)TAIL_MLANES * TAIL_TBL * n0, 64)), dim3(64), 0, s, n0,
                            ses->table.as<uint4>());
         hipLaunchKernelGGL(k_set_one_ark<typename Cv::Scalar>, dim3(1), dim3(64), 0, s, ses->w[0].as<uint4>());
     });
