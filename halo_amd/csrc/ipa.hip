@@ -1040,6 +1040,53 @@ static int ipa_tail_sums(halo_ipa_session* ses, int mode, hipStream_t s) {
     return HALO_OK;
 }
 
+// Small MSM over the resident SRS prefix (msm.hpp): the tail rounds' machinery with G0 = Gs[0..n0),
+// n0 = min(SRS_SMALL_N, srs.n): the multiples table (k_tail_table + k_tail_mults) is built on first
+// use per SRS, the scalars are zero-padded to n0 (a zero digit is an identity term), and mode 1 of
+// k_tail_scalars / k_tail_msm gives sum_k s[k] G0[k]; k_tail_final adds w S from the 2^i S table.
+int halo::msm_srs_small(DeviceState* st, int curve, const void* scalars_ark, size_t n, const void* hide_scalar,
+                  void* d_out_wrapped, hipStream_t s) {
+    SrsState& srs = st->srs[curve];
+    const size_t n0 = std::min(SRS_SMALL_N, srs.n);
+    if (n < 1 || n > n0) return set_error(HALO_EINVAL, "small SRS MSM: n (%zu) outside [1, %zu]", n, n0);
+    const size_t nblk = (TAIL_WIN * n0 + TAIL_THREADS - 1) / TAIL_THREADS;
+    // scratch: scalars (n0 x 32 B) | GLV words (n0 x 32 B) | sides (n0 B, 256-B aligned) | partials
+    const size_t o_scal = n0 * 32, o_side = 2 * n0 * 32, o_part = o_side + ((n0 + 255) & ~(size_t)255);
+    HALO_CHECK(srs.small_scr.reserve(o_part + nblk * 256));
+    if (!srs.small_ev)
+        HALO_HIP(hipEventCreateWithFlags(&srs.small_ev, hipEventDisableTiming));
+    else  // the previous small MSM (perhaps on another stream) is done with small_scr
+        HALO_HIP(hipStreamWaitEvent(s, srs.small_ev, 0));
+    if (srs.small_n0 != n0) {
+        HALO_CHECK(srs.small_tab.reserve((size_t)TAIL_TBL * TAIL_MUL * n0 * 128));
+        DISPATCH_CURVE(curve, Cv, {
+            hipLaunchKernelGGL(k_tail_table<Cv>, dim3(gridn(n0, 64)), dim3(64), 0, s, srs.gs.as<const uint4>(), 0, n0,
+                               srs.small_tab.as<uint4>());
+            hipLaunchKernelGGL(k_tail_mults<Cv>, dim3(gridn((size_t)TAIL_MLANES * TAIL_TBL * n0, 64)), dim3(64), 0, s,
+                               n0, srs.small_tab.as<uint4>());
+        });
+        HALO_HIP(hipGetLastError());
+        srs.small_n0 = n0;
+    }
+    char* scr = (char*)srs.small_scr.ptr;
+    if (n < n0) HALO_HIP(hipMemsetAsync(scr + n * 32, 0, (n0 - n) * 32, s));
+    HALO_HIP(hipMemcpyAsync(scr, scalars_ark, n * 32, hipMemcpyDeviceToDevice, s));
+    DISPATCH_CURVE(curve, Cv, {
+        hipLaunchKernelGGL(k_tail_scalars<Cv>, dim3(gridn(n0, 256)), dim3(256), 0, s, (const uint4*)nullptr,
+                           (const uint4*)scr, n0, (size_t)1, (size_t)0, 1, (uint32_t*)(scr + o_scal),
+                           (uint8_t*)(scr + o_side));
+        hipLaunchKernelGGL(k_tail_msm<Cv>, dim3((unsigned)nblk), dim3(TAIL_THREADS), 0, s,
+                           srs.small_tab.as<const uint4>(), (const uint32_t*)(scr + o_scal),
+                           (const uint8_t*)(scr + o_side), n0, (size_t)0, 1, 0u, (uint4*)(scr + o_part));
+        hipLaunchKernelGGL(k_tail_final<Cv>, dim3(1), dim3(TAIL_THREADS), 0, s, (const uint4*)(scr + o_part), (int)nblk,
+                           hide_scalar ? srs.s_table.as<const uint4>() : (const uint4*)nullptr,
+                           (const uint4*)hide_scalar, (uint4*)d_out_wrapped, 0);
+    });
+    HALO_HIP(hipGetLastError());
+    HALO_HIP(hipEventRecord(srs.small_ev, s));
+    return HALO_OK;
+}
+
 static int ipa_copy_out(halo_ipa_session* ses) {
     // L, R as packed XYZZ (128 B each): the affine conversion runs on the host (host_xyzz_to_wrapped)
     HALO_HIP(hipMemcpyAsync(ses->pinned + 256, (char*)ses->small.ptr + 512, 256, hipMemcpyDeviceToHost, ses->s));

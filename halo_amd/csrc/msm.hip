@@ -1022,6 +1022,12 @@ int msm_srs_device(DeviceState* st, int curve, const void* scalars_ark, size_t n
     if (n > srs.n) return set_error(HALO_ESRSRANGE, "n (%zu) exceeds the resident SRS length (%zu)", n, srs.n);
     const void* table = hide_scalar ? srs.s_table.ptr : nullptr;
     if (hide_scalar && !srs.has_sh) return set_error(HALO_ESRSRANGE, "hiding commitment needs S: upload (S, H)");
+    static const bool small_off = [] {  // HALO_SRS_SMALL=0: A/B knob, small MSMs through the bucket pipeline
+        const char* e = getenv("HALO_SRS_SMALL");
+        return e && e[0] == '0';
+    }();
+    if (!async && !small_off && n >= 1 && n <= SRS_SMALL_N)
+        return msm_srs_small(st, curve, scalars_ark, n, hide_scalar, d_out_wrapped, s);
     int rc;
     // the shifted copies hold W windows of srs.n points each; an MSM of n <= srs.n points uses the
     // prefix of every window (point index w * srs.n + i)
@@ -1618,6 +1624,7 @@ static int srs_install(DeviceState* st, int curve, const void* d_wrapped, size_t
     HALO_CHECK(convert_wrapped_to_internal(curve, d_wrapped, srs.gs.ptr, n, s));
     srs.n = n;
     srs.shifted_c = 0;
+    srs.small_n0 = 0;
     if (S && H) {
         HALO_CHECK(st->scratch[1].reserve(256));
         char* tmp = (char*)st->scratch[1].ptr;

@@ -61,6 +61,13 @@ int msm_srs_pairs_device(DeviceState* st, int curve, size_t np, const MsmPairIO*
 int msm_shared_batch(DeviceState* st, int curve, const void* bases_int, const void* w_ark, size_t T, size_t len,
                      void* out, bool xyzz_out, BatchScratch& S, hipStream_t s, size_t shift_stride = 0, int c_s = 0);
 int srs_precompute_windows(DeviceState* st, int curve, hipStream_t s);
+// Small MSM over the resident SRS prefix (1 <= n <= SRS_SMALL_N, ipa.hip): every (point, 4-bit GLV
+// window) term is one entry of a per-SRS multiples table, then block trees with the hiding term
+// hide_scalar * S from the 2^i S table -- no sort, buckets or bucket reduction.  Stream-ordered on s;
+// writes one ark WrappedPoint to d_out_wrapped.
+constexpr size_t SRS_SMALL_N = 1024;
+int msm_srs_small(DeviceState* st, int curve, const void* scalars_ark, size_t n, const void* hide_scalar,
+                  void* d_out_wrapped, hipStream_t s);
 // Host conversion of a 128-B packed XYZZ point (internal format, each coordinate < 2p) to an ark
 // WrappedPoint: one inversion in 4 x 64-bit Montgomery arithmetic on the CPU (identity -> (0, 0)).
 void host_xyzz_to_wrapped(int curve, const void* xyzz, void* wrapped);

@@ -56,6 +56,10 @@ struct SrsState {
     DevBuf h_table;     // 2^i H (i < 128), internal affine: the IPA's H' = xi_0 H terms (halo_ipa_begin_xi)
     uint64_t h_key[8] = {};  // the WrappedPoint H that h_table was built from
     bool h_built = false;
+    DevBuf small_tab;   // d 2^(4 w) G_k (k < small_n0, w < 32, d < 16), XYZZ: small SRS MSMs (ipa.hip)
+    size_t small_n0 = 0;             // 0 = not built for the current SRS
+    DevBuf small_scr;                // padded scalars, GLV digits, block partials of a small MSM
+    hipEvent_t small_ev = nullptr;   // last small MSM's completion (orders reuse of small_scr)
     DevBuf shifted;     // optional window-shifted copies
     int shifted_c = 0;  // window bits of `shifted`
     int shifted_windows = 0;

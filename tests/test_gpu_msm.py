@@ -107,6 +107,34 @@ def test_pedersen_length_assert(hal, corc):
 
 
 @pytest.mark.parametrize("cname,cid", CURVES)
+def test_small_srs_msm_table_path(hal, golden, corc, cname, cid):
+    """SRS MSMs of n <= 1024 points (the multiples-table path, msm_srs_small): n = 1, an SRS shorter
+    than the table (n0 = SRS length), all-zero scalars, the 1024 / 1025 boundary with the bucket
+    pipeline, hiding, and a re-uploaded SRS with a different prefix (the table must be rebuilt)."""
+    c = P.CURVES[cname]
+    r = c.scalar
+    S, Hh = golden[f"ref_sh_{cname}"]
+    base = corc.srs_generate(cname, 2048)
+    for g in (np.ascontiguousarray(base[:300]), np.ascontiguousarray(base[::-1]), base):
+        group.PublicParams.upload(cname, g, S, Hh, precompute_windows=len(g) == 2048)
+        N = len(g)
+        for d in (0, 3, 255, 1023, 2047):
+            if d > N - 1:
+                continue
+            coeffs = rand_sc(d + 1, d + 11)
+            if d >= 7:
+                coeffs[:6] = fe([(r - 1) // 2, (r + 1) // 2, 0, 1, r - 1, 1 << 254], r)
+            assert np.array_equal(pcdl.commit(coeffs, d, None, cname), corc.msm(cname, g[: d + 1], coeffs)), (N, d)
+        zero = np.zeros((16, 4), dtype=np.uint64)
+        assert np.array_equal(pcdl.commit(zero, 15, None, cname), corc.msm(cname, g[:16], zero))
+        w = rand_sc(1, 5)
+        coeffs = rand_sc(64, 6)
+        exp = P.add(c, P.wrapped_to_point(c, list(corc.msm(cname, g[:64], coeffs))),
+                    P.mul_fast(c, P.from_mont(limbs_canon(w[0]), r), P.wrapped_to_point(c, list(S))))
+        assert list(pcdl.commit(coeffs, 63, w, cname)) == P.point_to_wrapped(c, exp)
+
+
+@pytest.mark.parametrize("cname,cid", CURVES)
 def test_pcdl_commit_reference_srs(hal, golden, corc, cname, cid):
     """pcdl.rs:275-287 over the resident reference-recipe SRS (2^16 here), both MSM paths (windowed,
     and window-shifted precomputed bases), with and without hiding; and its assertion messages."""
