@@ -719,9 +719,21 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
     ta.hide_table = hide_table;
     ta.hide_scalar = hide_scalar;
     ta.out_wrapped = d_out_wrapped;
+    static const bool fuse_off = [] {  // HALO_FUSE_FINAL=0: A/B knob, separate k_final launch
+        const char* e = getenv("HALO_FUSE_FINAL");
+        return e && e[0] == '0';
+    }();
+    // one window set with a nonempty MSM (the tail reaches k_bitcombine): it also finishes the MSM
+    const bool fuse = SW == 1 && n > 0 && !fuse_off;
+    if (fuse) {
+        ta.final_mode = out_xyzz ? 2 : 1;
+        ta.final_hide = (const uint4*)hide_slot;
+        ta.final_out = (uint4*)d_out_wrapped;
+    }
     HALO_CHECK(msm_tail_launch(curve_id<Cv>(), ta, ts));
-    hipLaunchKernelGGL(k_final<Cv>, dim3(1), dim3(64), 0, ts, M.window_sums.as<const uint4>(), SW, c,
-                       (const uint4*)hide_slot, d_out_wrapped, (int)out_xyzz);
+    if (!fuse)
+        hipLaunchKernelGGL(k_final<Cv>, dim3(1), dim3(64), 0, ts, M.window_sums.as<const uint4>(), SW, c,
+                           (const uint4*)hide_slot, d_out_wrapped, (int)out_xyzz);
     HALO_HIP(hipGetLastError());
     HALO_HIP(hipEventRecord(M.tail_done, ts));
     M.tail_pending = true;

@@ -94,6 +94,11 @@ struct MsmTailArgs {
     const uint4* hide_scalar;
     uint4* out_wrapped;
     bool batch_windows = false;  // SW windows of 128 buckets: k_batch_window_sums instead of the grid reduction
+    // SW == 1 only: k_bitcombine also does k_final's work (+ final_hide, -> final_out as an ark
+    // WrappedPoint (1) or packed XYZZ (2)); 0: it writes window_sums and k_final follows
+    int final_mode = 0;
+    const uint4* final_hide = nullptr;
+    uint4* final_out = nullptr;
 };
 int msm_tail_launch(int curve, const MsmTailArgs& a, hipStream_t ts);
 

@@ -156,10 +156,12 @@ __global__ __launch_bounds__(256) void k_bitterms(const uint4* rows, const uint4
     if (tid == 0) xyzz_store(out + 8 * ((size_t)w * NT + k), acc);
 }
 
-// grid SW, 64 threads: S_w = T_0 + sum_j 2^(j + logL) U_j + sum_j 2^j V_j
+// grid SW, 64 threads: S_w = T_0 + sum_j 2^(j + logL) U_j + sum_j 2^j V_j.  fin (SW == 1): lane 0 then
+// finishes the MSM as k_final would (+ hide, -> ark WrappedPoint (1) or packed XYZZ (2)), one
+// lone-wave launch fewer on the tail's critical path.
 template <class Cv>
 __global__ __launch_bounds__(64) void k_bitcombine(const uint4* terms, uint32_t NT, uint32_t logH, uint32_t logL,
-                                                   uint4* window_sums) {
+                                                   uint4* window_sums, int fin, const uint4* hide, uint4* out) {
     using F = typename Cv::Base;
     const uint32_t w = blockIdx.x, k = threadIdx.x;
     XYZZ<F> v = xyzz_id<F>();
@@ -172,7 +174,16 @@ __global__ __launch_bounds__(64) void k_bitcombine(const uint4* terms, uint32_t 
     uint32_t G = 1;
     while (G < NT) G <<= 1;
     v = wave_group_sum<F>(v, G);
-    if (k == 0) xyzz_store(window_sums + 8 * w, v);
+    if (k != 0) return;
+    if (fin == 0) {
+        xyzz_store(window_sums + 8 * w, v);
+        return;
+    }
+    if (hide) v = xyzz_add(v, xyzz_load<F>(hide));
+    if (fin == 2)
+        xyzz_store(out, v);
+    else
+        aff_to_wrapped(out, xyzz_to_aff(v));
 }
 
 // Many small windows (msm_shared_batch: SW = len * W windows of B = 16..128 buckets): 8 lanes per
@@ -240,8 +251,9 @@ static int tail_launch_t(const MsmTailArgs& a, hipStream_t ts) {
                            a.H, a.rows, a.cols);
         hipLaunchKernelGGL(k_bitterms<Cv>, dim3(a.NT, a.SW), dim3(256), 0, ts, (const uint4*)a.rows,
                            (const uint4*)a.cols, a.H, a.L, a.logH, a.terms);
+        const int fin = a.SW == 1 ? a.final_mode : 0;
         hipLaunchKernelGGL(k_bitcombine<Cv>, dim3(a.SW), dim3(64), 0, ts, (const uint4*)a.terms, a.NT, a.logH, a.logL,
-                           a.window_sums);
+                           a.window_sums, fin, a.final_hide, a.final_out);
     }
     HALO_HIP(hipGetLastError());
     return HALO_OK;
