@@ -213,6 +213,32 @@ __global__ __launch_bounds__(64) void k_hiding_point(const uint4* C, const uint4
 
 }  // namespace halo
 
+int halo::pcdl_pbar_device(int curve, const void* q, size_t d, const void* z, void* p_bar, hipStream_t s) {
+    const size_t n = d + 1;
+    DISPATCH_FIELD(curve == HALO_PALLAS ? HALO_FP : HALO_FQ, Fs, {
+        hipLaunchKernelGGL(k_pbar<Fs>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (const uint4*)q, d,
+                           (const uint4*)z, (uint4*)p_bar);
+    });
+    HALO_HIP(hipGetLastError());
+    return HALO_OK;
+}
+
+int halo::pcdl_combine_device(int curve, const void* p, size_t len, const void* p_bar, size_t n, const void* alpha,
+                              const void* w, const void* w_bar, const void* C, const void* C_bar, const void* S_int,
+                              void* p_prime, void* C_prime, void* w_prime, hipStream_t s) {
+    DISPATCH_FIELD(curve == HALO_PALLAS ? HALO_FP : HALO_FQ, Fs, {
+        hipLaunchKernelGGL(k_axpy_pad<Fs>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (const uint4*)p, len,
+                           (const uint4*)p_bar, n, (const uint4*)alpha, (uint4*)p_prime);
+    });
+    DISPATCH_CURVE(curve, Cv, {
+        hipLaunchKernelGGL(k_hiding_point<Cv>, dim3(1), dim3(64), 0, s, (const uint4*)C, (const uint4*)C_bar,
+                           (const uint4*)S_int, (const uint4*)alpha, (const uint4*)w, (const uint4*)w_bar, (uint4*)C_prime,
+                           (uint4*)w_prime);
+    });
+    HALO_HIP(hipGetLastError());
+    return HALO_OK;
+}
+
 static int hiding_checks(DeviceState* st, halo_curve_t curve, size_t d) {
     SrsState& srs = st->srs[curve];
     if (!srs.n) return set_error(HALO_ESRSRANGE, "no resident SRS: call halo_srs_upload first");
@@ -243,12 +269,7 @@ extern "C" int halo_pcdl_hiding_blind(halo_curve_t curve, const halo_fe_t* q, si
     HALO_CHECK(copy_h2d(st->scratch[0].ptr, q, d * 32, s));
     HALO_CHECK(copy_h2d(small, z, 32, s));
     HALO_CHECK(copy_h2d(small + 32, w_bar, 32, s));
-    const int field = curve == HALO_PALLAS ? HALO_FP : HALO_FQ;
-    DISPATCH_FIELD(field, Fs, {
-        hipLaunchKernelGGL(k_pbar<Fs>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, st->scratch[0].as<const uint4>(),
-                           d, (const uint4*)small, st->scratch[1].as<uint4>());
-    });
-    HALO_HIP(hipGetLastError());
+    HALO_CHECK(pcdl_pbar_device(curve, st->scratch[0].ptr, d, small, st->scratch[1].ptr, s));
     HALO_CHECK(msm_srs_device(st, curve, st->scratch[1].ptr, n, small + 32, small + 64, s));
     if (p_bar_out) HALO_CHECK(copy_d2h(p_bar_out, st->scratch[1].ptr, n * 32, s));
     return copy_d2h(C_bar_out, small + 64, 64, s);
@@ -284,18 +305,8 @@ extern "C" int halo_pcdl_hiding_combine(halo_curve_t curve, const halo_fe_t* p, 
     HALO_CHECK(copy_h2d(sm + 128, C, 64, s));
     HALO_CHECK(copy_h2d(sm + 192, C_bar, 64, s));
     HALO_CHECK(copy_h2d(sm + 256, st->srs[curve].S, 64, s));
-    const int field = curve == HALO_PALLAS ? HALO_FP : HALO_FQ;
-    DISPATCH_FIELD(field, Fs, {
-        hipLaunchKernelGGL(k_axpy_pad<Fs>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
-                           st->scratch[0].as<const uint4>(), len, st->scratch[1].as<const uint4>(), n, (const uint4*)sm,
-                           st->scratch[3].as<uint4>());
-    });
-    DISPATCH_CURVE(curve, Cv, {
-        hipLaunchKernelGGL(k_hiding_point<Cv>, dim3(1), dim3(64), 0, s, (const uint4*)(sm + 128), (const uint4*)(sm + 192),
-                           (const uint4*)(sm + 256), (const uint4*)sm, (const uint4*)(sm + 32), (const uint4*)(sm + 64),
-                           (uint4*)(sm + 320), (uint4*)(sm + 384));
-    });
-    HALO_HIP(hipGetLastError());
+    HALO_CHECK(pcdl_combine_device(curve, st->scratch[0].ptr, len, st->scratch[1].ptr, n, sm, sm + 32, sm + 64, sm + 128,
+                                   sm + 192, sm + 256, st->scratch[3].ptr, sm + 320, sm + 384, s));
     HALO_CHECK(copy_d2h(p_prime_out, st->scratch[3].ptr, n * 32, s));
     HALO_CHECK(copy_d2h(w_prime_out, sm + 384, 32, s));
     return copy_d2h(C_prime_out, sm + 320, 64, s);

@@ -356,9 +356,10 @@ __global__ __launch_bounds__(64) void k_tail_table(const uint4* gs, int gs_xyzz,
     }
 }
 
-// entry (w, d, k) of the tail table: d 2^(4 w) G0[k], 1 <= d <= 15 (XYZZ)
-HALO_DEV size_t tail_entry(size_t w, uint32_t d, size_t n0, size_t k) {
-    return 8 * ((w * TAIL_MUL + (d - 1)) * n0 + k);
+// entry (w, d, k) of the tail table: d 2^(4 w) G0[k], 1 <= d <= 15 (XYZZ); ld = the number of
+// points the table was built for (a session may use a prefix of the SRS's table)
+HALO_DEV size_t tail_entry(size_t w, uint32_t d, size_t ld, size_t k) {
+    return 8 * ((w * TAIL_MUL + (d - 1)) * ld + k);
 }
 
 // The multiples 2..15 of each window base P = 2^(4 w) G0[k] written by k_tail_table.  Lane
@@ -424,8 +425,9 @@ __global__ __launch_bounds__(256) void k_tail_scalars(const uint4* cs, const uin
 // side is (win, u, j) = window, fold weight, j < m, at point k = j + u 2m + side m.  mode 1 (U): terms
 // t = win n0 + k, all on side 0.
 template <class Cv>
-__global__ __launch_bounds__(TAIL_THREADS) void k_tail_msm(const uint4* table, const uint32_t* scal, const uint8_t* side,
-                                                            size_t n0, size_t m, int mode, uint32_t nbs, uint4* part) {
+__global__ __launch_bounds__(TAIL_THREADS) void k_tail_msm(const uint4* table, size_t ld, const uint32_t* scal,
+                                                            const uint8_t* side, size_t n0, size_t m, int mode, uint32_t nbs,
+                                                            uint4* part) {
     using F = typename Cv::Base;
     __shared__ uint4 red[TAIL_THREADS / 2 * 8];
     const int tid = threadIdx.x;
@@ -452,7 +454,7 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail_msm(const uint4* table, c
         const uint32_t d = (scal[8 * k + 4 * half + bw / DPW] >> (TAIL_DB * (bw % DPW))) & (uint32_t)TAIL_MUL;
         const uint32_t sk = side[k];
         if (d) {
-            acc = xyzz_load<F>(table + tail_entry(bw, d, n0, k));
+            acc = xyzz_load<F>(table + tail_entry(bw, d, ld, k));
             if (half) acc.X = fe_mul(acc.X, fe_from_const<F>(Cv::K::BETA));  // phi
             if ((sk >> (1 + half)) & 1u) acc = xyzz_neg(acc);
         }
@@ -558,30 +560,59 @@ __global__ __launch_bounds__(256) void k_weighted_scalars(const uint4* cs, const
 
 using namespace halo;
 
+// One opening.  Sessions are pooled per device (ipa_acquire / ipa_release): the streams, events,
+// pinned staging and every device buffer survive halo_ipa_end and are reused by the next opening,
+// so an opening allocates nothing once the pool is warm (~11 hipMallocs, two stream
+// creations and a pinned allocation per opening; ADVICE r02: the buffers leaked at end).
 struct halo_ipa_session {
-    int curve;
-    size_t n, m;
-    DevBuf gs, cs, zs, htab, small, tmp;
-    hipStream_t s;
+    // ---- resources (kept across pooled uses)
+    int device = -1;
+    hipStream_t s = nullptr;
+    hipStream_t aux = nullptr;        // builds the 2^i H' table beside round 1's accumulation
+    hipEvent_t htab_ready = nullptr;  // recorded on aux after the table
+    uint8_t* pinned = nullptr;  // [128, 192) xi|xi_inv (H2D), [256, 512) L|R XYZZ (D2H): async, several sessions in flight
+    DevBuf gs, cs, zs, htab, small, tmp, pbar;
+    DevBuf own_table, w[2], scal, side, part;
+    BatchScratch mat;  // weighted -> tail switch (msm_shared_batch)
+    // ---- per-opening state (reset by ipa_acquire)
+    int curve = 0;
+    size_t n = 0, m = 0;
     // tail rounds (length <= IPA_TAIL_N, sessions over the SRS only): see k_tail_table
     bool allow_tail = false, tail = false;
     bool srs_round0 = false;  // G is still the SRS prefix (no fold yet): L/R on the resident shifted SRS
+    bool gs_srs_prefix = false;  // G (length 2m) = Gs[0..2m): the tail can use the SRS's multiples table
     bool gs_xyzz = false;     // gs holds XYZZ points (materialised for the tail table only)
+    bool gs_valid = false;    // gs holds the current G (halo_ipa_state may read it)
     bool weighted = false;    // G is never folded: L/R over the resident shifted SRS (k_weighted_scalars)
     size_t n0 = 0, wlen = 0;
-    DevBuf table, w[2], scal, side, part;
-    BatchScratch mat;  // weighted -> tail switch (msm_shared_batch)
     int wcur = 0;
-    hipStream_t aux = nullptr;        // builds the 2^i H' table beside round 1's accumulation
-    hipEvent_t htab_ready = nullptr;  // recorded on aux after the table
+    const uint4* table = nullptr;  // tail multiples table: own_table, or the SRS's small table
+    size_t table_ld = 0;
     bool fold_inflight = false;       // a fold's H2D copy of xi may still read `pinned`
     bool htab_waited = false;         // round 1 waited for it (later rounds follow a host sync of round 1)
-    // xi mode (halo_ipa_begin_xi / _dev_xi): the hiding terms use the resident 2^i H table and the
-    // dots scaled by xi_0 (dot H' = (dot xi_0) H), so there is neither H' nor a per-session table
+    // xi mode (halo_ipa_begin_xi / _dev_xi / halo_pcdl_open_start): the hiding terms use the resident
+    // 2^i H table and the dots scaled by xi_0 (dot H' = (dot xi_0) H), so there is neither H' nor a
+    // per-session table
     bool xi_mode = false;
-    const void* htab_ptr = nullptr;  // 2^i H' (own table) or 2^i H (SrsState::h_table)
-    uint8_t* pinned = nullptr;  // [128, 192) xi|xi_inv (H2D), [256, 512) L|R XYZZ (D2H): async, several sessions in flight
-    ~halo_ipa_session() {
+    const void* htab_ptr = nullptr;  // 2^i H' (own table) or 2^i H (SrsState::h_tables)
+    bool started = false;            // rounds may run (a pcdl open session starts at halo_pcdl_open_start)
+    bool blinded = false;            // halo_pcdl_open_blind ran (pbar holds p_bar)
+    bool combined = false;           // halo_pcdl_open_combine ran
+
+    void reset_state() {
+        curve = 0;
+        n = m = 0;
+        allow_tail = tail = srs_round0 = gs_srs_prefix = gs_xyzz = gs_valid = weighted = false;
+        n0 = wlen = 0;
+        wcur = 0;
+        table = nullptr;
+        table_ld = 0;
+        fold_inflight = htab_waited = xi_mode = false;
+        htab_ptr = nullptr;
+        started = blinded = combined = false;
+    }
+    void destroy() {
+        if (s) (void)hipStreamSynchronize(s);
         if (aux) {
             (void)hipStreamSynchronize(aux);
             (void)hipStreamDestroy(aux);
@@ -589,8 +620,86 @@ struct halo_ipa_session {
         if (htab_ready) (void)hipEventDestroy(htab_ready);
         if (s) (void)hipStreamDestroy(s);
         if (pinned) (void)hipHostFree(pinned);
+        s = aux = nullptr;
+        htab_ready = nullptr;
+        pinned = nullptr;
+        for (DevBuf* b : {&gs, &cs, &zs, &htab, &small, &tmp, &pbar, &own_table, &w[0], &w[1], &scal, &side, &part})
+            b->release();
+        for (DevBuf* b : {&mat.digits, &mat.lists, &mat.keys, &mat.vals, &mat.bstart, &mat.partials, &mat.bucket_sums,
+                          &mat.window_sums})
+            b->release();
     }
 };
+
+namespace {
+constexpr size_t IPA_POOL_MAX = 8;  // idle sessions kept per device
+std::mutex g_pool_mu;
+std::vector<halo_ipa_session*> g_pool;
+
+// A session for the current device: from the pool, or new with its streams and pinned staging.
+halo_ipa_session* ipa_acquire(DeviceState* st) {
+    {
+        std::lock_guard<std::mutex> g(g_pool_mu);
+        for (size_t i = g_pool.size(); i-- > 0;)
+            if (g_pool[i]->device == st->device) {
+                halo_ipa_session* ses = g_pool[i];
+                g_pool.erase(g_pool.begin() + i);
+                ses->reset_state();
+                return ses;
+            }
+    }
+    auto* ses = new halo_ipa_session();
+    ses->device = st->device;
+    // the side stream for the H' table only when the runtime has hardware queues to spare
+    // (GPU_MAX_HW_QUEUES >= 8, as bench.py sets): with HIP's default 4 the extra stream shares a queue
+    // with the session's and the MSM tail streams, which cost ~0.3 ms per 2^16 round
+    const char* hwq = getenv("GPU_MAX_HW_QUEUES");
+    const bool use_aux = hwq && atoi(hwq) >= 8;
+    if (hipStreamCreateWithFlags(&ses->s, hipStreamNonBlocking) != hipSuccess ||
+        (use_aux && hipStreamCreateWithFlags(&ses->aux, hipStreamNonBlocking) != hipSuccess) ||
+        hipEventCreateWithFlags(&ses->htab_ready, hipEventDisableTiming) != hipSuccess ||
+        hipHostMalloc((void**)&ses->pinned, 512, hipHostMallocDefault) != hipSuccess) {
+        ses->destroy();
+        delete ses;
+        set_error(HALO_EDEVICE, "halo_ipa_begin: stream / pinned buffer allocation failed");
+        return nullptr;
+    }
+    return ses;
+}
+
+// Back to the pool once its stream is idle (the pinned staging is then free); beyond IPA_POOL_MAX
+// idle sessions on the device the resources are released.
+void ipa_release(halo_ipa_session* ses) {
+    if (!ses) return;
+    if (ses->s) (void)hipStreamSynchronize(ses->s);
+    if (ses->aux) (void)hipStreamSynchronize(ses->aux);
+    {
+        std::lock_guard<std::mutex> g(g_pool_mu);
+        size_t same = 0;
+        for (halo_ipa_session* p : g_pool) same += p->device == ses->device;
+        if (same < IPA_POOL_MAX) {
+            g_pool.push_back(ses);
+            return;
+        }
+    }
+    ses->destroy();
+    delete ses;
+}
+}  // namespace
+
+// halo_shutdown: releases the pooled sessions while the HIP runtime is alive.
+void halo::ipa_shutdown() {
+    std::lock_guard<std::mutex> g(g_pool_mu);
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    for (halo_ipa_session* ses : g_pool) {
+        (void)hipSetDevice(ses->device);
+        ses->destroy();
+        delete ses;
+    }
+    g_pool.clear();
+    (void)hipSetDevice(cur);
+}
 
 static int check_field_i(halo_field_t f) {
     if (f != HALO_FP && f != HALO_FQ) return set_error(HALO_EINVAL, "unknown field id %d", (int)f);
@@ -797,26 +906,173 @@ static size_t ipa_mat_n() {
     return e ? (size_t)atoll(e) : IPA_MAT_N;
 }
 
-// The 2^i H table (i < IPA_HTAB, internal affine) of xi-mode sessions, kept per device and curve and
-// rebuilt only when H changes (one ~1 ms doubling chain, then shared by every later opening).
-static int ipa_h_table(DeviceState* st, int curve, const halo_wrapped_point_t* Hpt) {
+// The 2^i H tables (i < IPA_HTAB, internal affine) of xi-mode sessions, kept per device and curve,
+// one per distinct H and never rewritten (open sessions hold pointers into them; ADVICE r02: a new H
+// used to rebuild the one shared table under live sessions).  One ~1 ms doubling chain per H, then
+// shared by every later opening.  Past IPA_HTABLES_MAX distinct H, *out = nullptr: the session builds
+// its own table.
+constexpr size_t IPA_HTABLES_MAX = 8;
+static int ipa_h_table(DeviceState* st, int curve, const halo_wrapped_point_t* Hpt, const void** out) {
     SrsState& srs = st->srs[curve];
-    if (srs.h_built && !memcmp(srs.h_key, Hpt, 64)) return HALO_OK;
-    HALO_CHECK(srs.h_table.reserve(IPA_HTAB * 64));
+    *out = nullptr;
+    for (auto& t : srs.h_tables)
+        if (!memcmp(t->key, Hpt, 64)) {
+            *out = t->t.ptr;
+            return HALO_OK;
+        }
+    if (srs.h_tables.size() >= IPA_HTABLES_MAX) return HALO_OK;
+    auto ht = std::make_unique<SrsState::HTable>();
+    HALO_CHECK(ht->t.reserve(IPA_HTAB * 64));
+    const hipStream_t s = nullptr;
+    ScratchUse su(st, s);
     HALO_CHECK(st->scratch[7].reserve(IPA_HTAB * 128 + 64));
     char* tmp = (char*)st->scratch[7].ptr;
-    const hipStream_t s = nullptr;
     HALO_CHECK(copy_h2d(tmp + IPA_HTAB * 128, Hpt, 64, s));
     DISPATCH_CURVE(curve, Cv, {
         hipLaunchKernelGGL(k_pow2_xyzz_from_wrapped<Cv>, dim3(1), dim3(64), 0, s, (const uint4*)(tmp + IPA_HTAB * 128),
                            (uint4*)tmp, IPA_HTAB);
         hipLaunchKernelGGL(k_xyzz_to_aff_ipa<Cv>, dim3(IPA_HTAB / 64), dim3(64), 0, s, (const uint4*)tmp,
-                           srs.h_table.as<uint4>(), IPA_HTAB);
+                           ht->t.as<uint4>(), IPA_HTAB);
     });
     HALO_HIP(hipGetLastError());
     HALO_HIP(hipStreamSynchronize(s));  // sessions on other streams read it
-    memcpy(srs.h_key, Hpt, 64);
-    srs.h_built = true;
+    memcpy(ht->key, Hpt, 64);
+    *out = ht->t.ptr;
+    srs.h_tables.push_back(std::move(ht));
+    return HALO_OK;
+}
+
+// small-buffer layout of a session (ses->small, device):
+//   [0, 32) z | [64, 128) H' (or H) | [128, 192) dots | [192, 224) xi_0 | [256, 384) U | c
+//   [384, 448) xi | xi^-1 | [512, 768) L | R XYZZ
+//   hiding open: [1024) w_bar, [1056) alpha, [1088) w, [1120) w' out, [1152) C, [1216) C_bar out,
+//   [1280) S (internal), [1344) C' out
+constexpr size_t SM_BYTES = 2048;
+constexpr size_t SM_WBAR = 1024, SM_ALPHA = 1056, SM_W = 1088, SM_WP = 1120, SM_C = 1152, SM_CBAR = 1216, SM_S = 1280,
+                 SM_CP = 1344;
+
+// Phase 1 of a session: G (resident SRS prefix, or explicit gs_host), c (cs_len coefficients, host or
+// device (ordered on the null stream), zero-padded to n), z = powers of z (or explicit zs_host) on the
+// device.  st->mu held; ses freshly acquired.
+static int ipa_setup(DeviceState* st, halo_ipa_session* ses, int curve, size_t n, const halo_wrapped_point_t* gs_host,
+                     const halo_fe_t* cs, size_t cs_len, bool cs_on_device, const halo_fe_t* zs_host, const halo_fe_t* z) {
+    SrsState& srs = st->srs[curve];
+    ses->curve = curve;
+    {
+        const char* e = getenv("HALO_IPA_TAIL");
+        const char* ew = getenv("HALO_IPA_WEIGHTED");  // A/B knob: 0 = fold G every round
+        ses->allow_tail = !gs_host && !(e && e[0] == '0');
+        ses->weighted = !gs_host && srs.shifted_c != 0 && n > ipa_tail_n() && !(ew && ew[0] == '0');
+        if (ses->weighted) ses->allow_tail = false;
+        ses->srs_round0 = !gs_host && srs.shifted_c != 0 && !ses->weighted;
+        ses->gs_srs_prefix = !gs_host && !ses->weighted;
+    }
+    ses->n = n;
+    ses->m = n / 2;
+    hipStream_t s = ses->s;
+    // an SRS session that starts in the tail rounds never reads G itself (the SRS's table does)
+    const bool need_gs = !ses->weighted && !(ses->gs_srs_prefix && ses->allow_tail && n <= ipa_tail_n());
+    if (need_gs || gs_host) HALO_CHECK(ses->gs.reserve(n * 64));
+    ses->gs_valid = need_gs || gs_host;
+    if (ses->weighted) {  // w = [1]; scal holds the two n/2-term scalar vectors of a round
+        HALO_CHECK(ses->w[0].reserve(n * 32));
+        HALO_CHECK(ses->w[1].reserve(n * 32));
+        HALO_CHECK(ses->scal.reserve(n * 32));
+        DISPATCH_CURVE(curve, Cv, {
+            hipLaunchKernelGGL(k_set_one_ark<typename Cv::Scalar>, dim3(1), dim3(64), 0, s, ses->w[0].as<uint4>());
+        });
+        ses->n0 = n;
+        ses->wlen = 1;
+        ses->wcur = 0;
+    }
+    HALO_CHECK(ses->cs.reserve(n * 32));
+    HALO_CHECK(ses->zs.reserve(n * 32));
+    HALO_CHECK(ses->small.reserve(SM_BYTES));
+    HALO_CHECK(ses->tmp.reserve(std::max<size_t>(4096 * 32, gs_host ? n * 64 : 0)));
+    if (gs_host) {
+        HALO_CHECK(copy_h2d(ses->tmp.ptr, gs_host, n * 64, s));
+        HALO_CHECK(convert_wrapped_to_internal(curve, ses->tmp.ptr, ses->gs.ptr, n, s));
+    } else if (need_gs) {
+        HALO_HIP(hipMemcpyAsync(ses->gs.ptr, srs.gs.ptr, n * 64, hipMemcpyDeviceToDevice, s));
+    }
+    if (cs_len < n) HALO_HIP(hipMemsetAsync(ses->cs.as<char>() + cs_len * 32, 0, (n - cs_len) * 32, s));
+    if (cs_on_device) {  // the producer ran on the null stream: order the session's stream after it
+        hipEvent_t ev;
+        if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess || hipEventRecord(ev, 0) != hipSuccess ||
+            hipStreamWaitEvent(s, ev, 0) != hipSuccess || hipEventDestroy(ev) != hipSuccess)
+            return set_error(HALO_EDEVICE, "halo_ipa_begin_dev: stream ordering failed");
+        if (cs_len) HALO_HIP(hipMemcpyAsync(ses->cs.ptr, cs, cs_len * 32, hipMemcpyDeviceToDevice, s));
+    } else {
+        HALO_CHECK(copy_h2d(ses->cs.ptr, cs, cs_len * 32, s));
+    }
+    char* sm = (char*)ses->small.ptr;
+    if (zs_host) {
+        HALO_CHECK(copy_h2d(ses->zs.ptr, zs_host, n * 32, s));
+    } else {
+        HALO_CHECK(copy_h2d(sm, z, 32, s));
+        const size_t run = 16;
+        DISPATCH_CURVE(curve, Cv, {
+            hipLaunchKernelGGL(k_powers<typename Cv::Scalar>, dim3(gridn((n + run - 1) / run, 128)), dim3(128), 0, s,
+                               (const uint4*)sm, n, run, ses->zs.as<uint4>());
+        });
+        HALO_HIP(hipGetLastError());
+    }
+    if (gs_host) HALO_HIP(hipStreamSynchronize(s));  // tmp held the staged bases
+    return HALO_OK;
+}
+
+// G of a session that skipped its copy of the SRS prefix (ipa_setup: it was to start in the tail
+// rounds) but folds G before any round ran (pcdl.rs:627-687 test_u_check drives folds only).
+static int ipa_ensure_gs(DeviceState* st, halo_ipa_session* ses) {
+    if (ses->gs_valid) return HALO_OK;
+    if (!ses->gs_srs_prefix) return set_error(HALO_EINVAL, "ipa: G is not resident");
+    const size_t len = 2 * ses->m;
+    HALO_CHECK(ses->gs.reserve(ses->n * 64));
+    HALO_HIP(hipMemcpyAsync(ses->gs.ptr, st->srs[ses->curve].gs.ptr, len * 64, hipMemcpyDeviceToDevice, ses->s));
+    ses->gs_valid = true;
+    return HALO_OK;
+}
+
+// Phase 2: the hiding terms' table.  xi mode (xi0 and H): the shared 2^i H table and dots scaled by
+// xi_0; otherwise (H_prime) a per-session 2^i H' table.  The rounds may run afterwards.
+static int ipa_start(DeviceState* st, halo_ipa_session* ses, const halo_wrapped_point_t* H_prime, const halo_fe_t* xi0,
+                     const halo_wrapped_point_t* Hpt) {
+    hipStream_t s = ses->s;
+    char* sm = (char*)ses->small.ptr;
+    ses->xi_mode = xi0 != nullptr;
+    const halo_wrapped_point_t* own = H_prime;  // the point of a per-session table, if one is needed
+    if (ses->xi_mode) {  // xi_0 at [192, 224)
+        HALO_CHECK(ipa_h_table(st, ses->curve, Hpt, &ses->htab_ptr));
+        HALO_CHECK(copy_h2d(sm + 192, xi0, 32, s));
+        own = ses->htab_ptr ? nullptr : Hpt;
+    }
+    ses->started = true;
+    if (!own) {
+        ses->htab_waited = true;
+        return HALO_OK;
+    }
+    HALO_CHECK(ses->htab.reserve(IPA_HTAB * (64 + 128)));  // affine table + XYZZ chain scratch
+    ses->htab_ptr = ses->htab.ptr;
+    HALO_CHECK(copy_h2d(sm + 64, own, 64, s));
+    // 2^i H' for i < 128 (the hiding terms use the GLV split of their scalar, k_hide_term): a ~1 ms
+    // one-lane doubling chain, built on the side stream while round 1's digits, sort and accumulation
+    // run; the hiding-term kernels wait for htab_ready
+    const hipStream_t hs = ses->aux ? ses->aux : s;
+    if (ses->aux) {
+        hipEvent_t h_in;
+        if (hipEventCreateWithFlags(&h_in, hipEventDisableTiming) != hipSuccess || hipEventRecord(h_in, s) != hipSuccess ||
+            hipStreamWaitEvent(ses->aux, h_in, 0) != hipSuccess || hipEventDestroy(h_in) != hipSuccess)
+            return set_error(HALO_EDEVICE, "halo_ipa_begin: stream ordering failed");
+    }
+    uint4* chain = ses->htab.as<uint4>() + 4 * IPA_HTAB;  // XYZZ scratch after the affine table
+    DISPATCH_CURVE(ses->curve, Cv, {
+        hipLaunchKernelGGL(k_pow2_xyzz_from_wrapped<Cv>, dim3(1), dim3(64), 0, hs, (const uint4*)(sm + 64), chain, IPA_HTAB);
+        hipLaunchKernelGGL(k_xyzz_to_aff_ipa<Cv>, dim3(IPA_HTAB / 64), dim3(64), 0, hs, (const uint4*)chain,
+                           ses->htab.as<uint4>(), IPA_HTAB);
+    });
+    HALO_HIP(hipGetLastError());
+    HALO_HIP(hipEventRecord(ses->htab_ready, hs));
+    ses->htab_waited = false;
     return HALO_OK;
 }
 
@@ -834,121 +1090,12 @@ static int ipa_begin(halo_curve_t curve, size_t n, const halo_wrapped_point_t* g
     std::lock_guard<std::mutex> g(st->mu);
     SrsState& srs = st->srs[curve];
     if (!gs_host && n > srs.n) return set_error(HALO_ESRSRANGE, "d (%zu) <= D (%zu)", n - 1, srs.n ? srs.n - 1 : 0);
-    int rc0;
-    if (xi0 && (rc0 = ipa_h_table(st, curve, Hpt))) return rc0;
-    auto* ses = new halo_ipa_session();
-    ses->curve = curve;
-    ses->xi_mode = xi0 != nullptr;
-    {
-        const char* e = getenv("HALO_IPA_TAIL");
-        const char* ew = getenv("HALO_IPA_WEIGHTED");  // A/B knob: 0 = fold G every round
-        ses->allow_tail = !gs_host && !(e && e[0] == '0');
-        ses->weighted = !gs_host && srs.shifted_c != 0 && n > ipa_tail_n() && !(ew && ew[0] == '0');
-        if (ses->weighted) ses->allow_tail = false;
-        ses->srs_round0 = !gs_host && srs.shifted_c != 0 && !ses->weighted;
-    }
-    ses->n = n;
-    ses->m = n / 2;
-    ses->s = nullptr;
-    // the side stream for the H' table only when the runtime has hardware queues to spare
-    // (GPU_MAX_HW_QUEUES >= 8, as bench.py sets): with HIP's default 4 the extra stream shares a queue
-    // with the session's and the MSM tail streams, which cost ~0.3 ms per 2^16 round
-    const char* hwq = getenv("GPU_MAX_HW_QUEUES");
-    const bool use_aux = hwq && atoi(hwq) >= 8;
-    if (hipStreamCreateWithFlags(&ses->s, hipStreamNonBlocking) != hipSuccess ||
-        (use_aux && hipStreamCreateWithFlags(&ses->aux, hipStreamNonBlocking) != hipSuccess) ||
-        hipEventCreateWithFlags(&ses->htab_ready, hipEventDisableTiming) != hipSuccess ||
-        hipHostMalloc((void**)&ses->pinned, 512, hipHostMallocDefault) != hipSuccess) {
-        delete ses;
-        return set_error(HALO_EDEVICE, "halo_ipa_begin: stream / pinned buffer allocation failed");
-    }
-    hipStream_t s = ses->s;
-    int rc = HALO_OK;
-    do {
-        if (!ses->weighted && (rc = ses->gs.reserve(n * 64))) break;
-        if (ses->weighted) {  // w = [1]; scal holds the two n/2-term scalar vectors of a round
-            if ((rc = ses->w[0].reserve(n * 32)) || (rc = ses->w[1].reserve(n * 32)) || (rc = ses->scal.reserve(n * 32)))
-                break;
-            DISPATCH_CURVE(curve, Cv, {
-                hipLaunchKernelGGL(k_set_one_ark<typename Cv::Scalar>, dim3(1), dim3(64), 0, s, ses->w[0].as<uint4>());
-            });
-            ses->n0 = n;
-            ses->wlen = 1;
-            ses->wcur = 0;
-        }
-        if ((rc = ses->cs.reserve(n * 32))) break;
-        if ((rc = ses->zs.reserve(n * 32))) break;
-        if (!ses->xi_mode && (rc = ses->htab.reserve(IPA_HTAB * (64 + 128)))) break;  // affine table + XYZZ chain scratch
-        ses->htab_ptr = ses->xi_mode ? srs.h_table.ptr : ses->htab.ptr;
-        if ((rc = ses->small.reserve(1024))) break;
-        if ((rc = ses->tmp.reserve(std::max<size_t>(4096 * 32, gs_host ? n * 64 : 0)))) break;
-        if (gs_host) {
-            if ((rc = copy_h2d(ses->tmp.ptr, gs_host, n * 64, s))) break;
-            if ((rc = convert_wrapped_to_internal(curve, ses->tmp.ptr, ses->gs.ptr, n, s))) break;
-        } else if (!ses->weighted &&
-                   hipMemcpyAsync(ses->gs.ptr, srs.gs.ptr, n * 64, hipMemcpyDeviceToDevice, s) != hipSuccess) {
-            rc = set_error(HALO_EDEVICE, "copy of the SRS prefix failed");
-            break;
-        }
-        if (cs_on_device) {  // the producer ran on the null stream: order the session's stream after it
-            hipEvent_t ev;
-            if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess || hipEventRecord(ev, 0) != hipSuccess ||
-                hipStreamWaitEvent(s, ev, 0) != hipSuccess || hipEventDestroy(ev) != hipSuccess) {
-                rc = set_error(HALO_EDEVICE, "halo_ipa_begin_dev: stream ordering failed");
-                break;
-            }
-            if (hipMemcpyAsync(ses->cs.ptr, cs, n * 32, hipMemcpyDeviceToDevice, s) != hipSuccess) {
-                rc = set_error(HALO_EDEVICE, "copy of the coefficients failed");
-                break;
-            }
-        } else if ((rc = copy_h2d(ses->cs.ptr, cs, n * 32, s))) {
-            break;
-        }
-        char* sm = (char*)ses->small.ptr;
-        if (zs_host) {
-            if ((rc = copy_h2d(ses->zs.ptr, zs_host, n * 32, s))) break;
-        } else {
-            if ((rc = copy_h2d(sm, z, 32, s))) break;
-        }
-        if (ses->xi_mode) {  // xi_0 at [192, 224); the 2^i H table is the SRS's
-            if ((rc = copy_h2d(sm + 192, xi0, 32, s))) break;
-            ses->htab_waited = true;
-        } else if ((rc = copy_h2d(sm + 64, H_prime, 64, s))) {
-            break;
-        }
-        const size_t run = 16;
-        DISPATCH_CURVE(curve, Cv, {
-            if (!zs_host)
-                hipLaunchKernelGGL(k_powers<typename Cv::Scalar>, dim3(gridn((n + run - 1) / run, 128)), dim3(128), 0,
-                                   s, (const uint4*)sm, n, run, ses->zs.as<uint4>());
-        });
-        if (ses->xi_mode) break;  // (rc == HALO_OK: nothing more to build)
-        // 2^i H' for i < 128 (the hiding terms use the GLV split of their scalar, k_hide_term): a
-        // ~1 ms one-lane doubling chain, built on the side stream while round 1's digits, sort and
-        // accumulation run; the hiding-term kernels wait for htab_ready
-        const hipStream_t hs = ses->aux ? ses->aux : s;
-        if (ses->aux) {
-            hipEvent_t h_in;
-            if (hipEventCreateWithFlags(&h_in, hipEventDisableTiming) != hipSuccess || hipEventRecord(h_in, s) != hipSuccess ||
-                hipStreamWaitEvent(ses->aux, h_in, 0) != hipSuccess || hipEventDestroy(h_in) != hipSuccess) {
-                rc = set_error(HALO_EDEVICE, "halo_ipa_begin: stream ordering failed");
-                break;
-            }
-        }
-        uint4* chain = ses->htab.as<uint4>() + 4 * IPA_HTAB;  // XYZZ scratch after the affine table
-        DISPATCH_CURVE(curve, Cv, {
-            hipLaunchKernelGGL(k_pow2_xyzz_from_wrapped<Cv>, dim3(1), dim3(64), 0, hs, (const uint4*)(sm + 64), chain,
-                               IPA_HTAB);
-            hipLaunchKernelGGL(k_xyzz_to_aff_ipa<Cv>, dim3(IPA_HTAB / 64), dim3(64), 0, hs, (const uint4*)chain,
-                               ses->htab.as<uint4>(), IPA_HTAB);
-        });
-        if (hipGetLastError() != hipSuccess || hipEventRecord(ses->htab_ready, hs) != hipSuccess)
-            rc = set_error(HALO_EDEVICE, "ipa begin launch failed");
-        if (!rc && gs_host && hipStreamSynchronize(s) != hipSuccess)  // tmp held the staged bases
-            rc = set_error(HALO_EDEVICE, "ipa begin: synchronisation failed");
-    } while (0);
+    halo_ipa_session* ses = ipa_acquire(st);
+    if (!ses) return HALO_EDEVICE;
+    int rc = ipa_setup(st, ses, curve, n, gs_host, cs, n, cs_on_device, zs_host, z);
+    if (!rc) rc = ipa_start(st, ses, H_prime, xi0, Hpt);
     if (rc) {
-        delete ses;
+        ipa_release(ses);
         return rc;
     }
     *out = ses;
@@ -992,22 +1139,147 @@ extern "C" int halo_ipa_begin_vectors(halo_curve_t curve, const halo_wrapped_poi
     return ipa_begin(curve, n, gs, cs, zs, nullptr, H_prime, out);
 }
 
-// Switch to the tail rounds: G0 = current G (length 2m), table 2^(8 win) G0, w = [1].
-static int ipa_enter_tail(halo_ipa_session* ses, hipStream_t s) {
+// ---------------------------------------------------------------------------------------------
+// pcdl::open_without_eval (pcdl.rs:326-392) with p, p_bar and p' kept in the session's buffers
+// (the hiding open used to download p_bar / p' and upload p, p_bar, p' between three
+// host calls).  The caller owns the transcript, as in the reference:
+//   halo_pcdl_open_begin(p, d, z)          asserts of pcdl.rs:338-341; c = p padded to n on the device
+//   [hiding] halo_pcdl_open_blind(q, w_bar) -> C_bar      p_bar = (X - z) q, C_bar = commit(p_bar, w_bar)
+//            (transcript: absorb C, C_bar, z, v; alpha = challenge)
+//            halo_pcdl_open_combine(alpha, C, w) -> C', w'   c = p + alpha p_bar (in place), pcdl.rs:366-371
+//   (transcript: absorb C', z, v; xi_0 = challenge)
+//   halo_pcdl_open_start(H, xi_0)           H' = xi_0 H; then halo_ipa_round_lr / fold / end
+// ---------------------------------------------------------------------------------------------
+extern "C" int halo_pcdl_open_begin(halo_curve_t curve, const halo_fe_t* p, size_t len, size_t d, const halo_fe_t* z,
+                                    halo_ipa_session** out) {
+    clear_error();
+    if (curve != HALO_PALLAS && curve != HALO_VESTA) return set_error(HALO_EINVAL, "unknown curve");
+    if ((len && !p) || !z || !out) return set_error(HALO_EINVAL, "halo_pcdl_open_begin: null argument");
+    const size_t n = d + 1;
+    if (n <= 1) return set_error(HALO_EINVAL, "assertion failed: n > 1");
+    if (!is_pow2(n)) return set_error(HALO_ENOTPOW2, "n (%zu) is not a power of two", n);
+    // p.degree() <= d: trailing zero coefficients do not count towards the degree
+    size_t deg_len = len;
+    while (deg_len > 0 && !(p[deg_len - 1].l[0] | p[deg_len - 1].l[1] | p[deg_len - 1].l[2] | p[deg_len - 1].l[3]))
+        deg_len--;
+    if (deg_len > n) return set_error(HALO_EDEGREE, "assertion failed: p.degree() <= d");
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    SrsState& srs = st->srs[curve];
+    if (!srs.n || d > srs.n - 1) return set_error(HALO_ESRSRANGE, "assertion failed: d <= pp.D");
+    halo_ipa_session* ses = ipa_acquire(st);
+    if (!ses) return HALO_EDEVICE;
+    const int rc = ipa_setup(st, ses, curve, n, nullptr, p, deg_len, false, nullptr, z);
+    if (rc) {
+        ipa_release(ses);
+        return rc;
+    }
+    *out = ses;
+    return HALO_OK;
+}
+
+extern "C" int halo_pcdl_open_blind(halo_ipa_session* ses, const halo_fe_t* q, const halo_fe_t* w_bar,
+                                    halo_wrapped_point_t* C_bar) {
+    clear_error();
+    if (!ses || !q || !w_bar || !C_bar) return set_error(HALO_EINVAL, "halo_pcdl_open_blind: null argument");
+    if (ses->started || ses->blinded) return set_error(HALO_EINVAL, "halo_pcdl_open_blind: session already blinded or started");
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    SrsState& srs = st->srs[ses->curve];
+    if (!srs.has_sh) return set_error(HALO_ESRSRANGE, "hiding commitment needs S: upload the SRS (S, H) first");
+    hipStream_t s = ses->s;
+    const size_t n = ses->n, d = n - 1;
+    char* sm = ses->small.as<char>();
+    HALO_CHECK(ses->pbar.reserve(n * 32));
+    HALO_CHECK(ses->tmp.reserve(std::max<size_t>(4096 * 32, d * 32)));
+    HALO_CHECK(copy_h2d(ses->tmp.ptr, q, d * 32, s));
+    HALO_CHECK(copy_h2d(sm + SM_WBAR, w_bar, 32, s));
+    HALO_CHECK(pcdl_pbar_device(ses->curve, ses->tmp.ptr, d, sm, ses->pbar.ptr, s));  // z at sm[0, 32)
+    HALO_CHECK(msm_srs_device(st, ses->curve, ses->pbar.ptr, n, sm + SM_WBAR, sm + SM_CBAR, s));
+    HALO_CHECK(copy_d2h(C_bar, sm + SM_CBAR, 64, s));
+    ses->blinded = true;
+    return HALO_OK;
+}
+
+extern "C" int halo_pcdl_open_combine(halo_ipa_session* ses, const halo_fe_t* alpha, const halo_wrapped_point_t* C,
+                                      const halo_fe_t* w, halo_fe_t* w_prime, halo_wrapped_point_t* C_prime) {
+    clear_error();
+    if (!ses || !alpha || !C || !w || !w_prime || !C_prime)
+        return set_error(HALO_EINVAL, "halo_pcdl_open_combine: null argument");
+    if (!ses->blinded || ses->combined || ses->started)
+        return set_error(HALO_EINVAL, "halo_pcdl_open_combine: needs exactly one halo_pcdl_open_blind before it");
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    hipStream_t s = ses->s;
+    char* sm = ses->small.as<char>();
+    HALO_CHECK(copy_h2d(sm + SM_ALPHA, alpha, 32, s));
+    HALO_CHECK(copy_h2d(sm + SM_W, w, 32, s));
+    HALO_CHECK(copy_h2d(sm + SM_C, C, 64, s));
+    HALO_CHECK(copy_h2d(sm + SM_S, st->srs[ses->curve].S, 64, s));
+    // c (= p padded) += alpha p_bar in place: p' (pcdl.rs:366); C' = C + alpha C_bar - w' S, w' = w + alpha w_bar
+    HALO_CHECK(pcdl_combine_device(ses->curve, ses->cs.ptr, ses->n, ses->pbar.ptr, ses->n, sm + SM_ALPHA, sm + SM_W,
+                                   sm + SM_WBAR, sm + SM_C, sm + SM_CBAR, sm + SM_S, ses->cs.ptr, sm + SM_CP, sm + SM_WP,
+                                   s));
+    HALO_HIP(hipMemcpyAsync(ses->pinned, sm + SM_WP, 32, hipMemcpyDeviceToHost, s));
+    HALO_HIP(hipMemcpyAsync(ses->pinned + 32, sm + SM_CP, 64, hipMemcpyDeviceToHost, s));
+    HALO_HIP(hipStreamSynchronize(s));
+    memcpy(w_prime, ses->pinned, 32);
+    memcpy(C_prime, ses->pinned + 32, 64);
+    ses->combined = true;
+    return HALO_OK;
+}
+
+extern "C" int halo_pcdl_open_start(halo_ipa_session* ses, const halo_wrapped_point_t* H, const halo_fe_t* xi0) {
+    clear_error();
+    if (!ses || !xi0) return set_error(HALO_EINVAL, "halo_pcdl_open_start: null argument");
+    if (ses->started) return set_error(HALO_EINVAL, "halo_pcdl_open_start: session already started");
+    if (ses->blinded && !ses->combined)
+        return set_error(HALO_EINVAL, "halo_pcdl_open_start: a blinded opening needs halo_pcdl_open_combine first");
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    if (!H) {  // the resident SRS's H (pp.H, pcdl.rs:390)
+        const SrsState& srs = st->srs[ses->curve];
+        if (!srs.has_sh) return set_error(HALO_ESRSRANGE, "no (S, H) uploaded");
+        H = &srs.H_wrapped;
+    }
+    return ipa_start(st, ses, nullptr, xi0, H);
+}
+
+// Switch to the tail rounds: G0 = current G (length 2m), w = [1], and the multiples table of G0:
+// the SRS's own table when G0 is still the SRS prefix (a session of n <= IPA_TAIL_N over the SRS:
+// the reference's small pcdl_open shapes, benches/pcdl.rs:35-57), else built for the session.
+static int ipa_enter_tail(DeviceState* st, halo_ipa_session* ses, hipStream_t s) {
     const size_t n0 = 2 * ses->m;
     const size_t nblk = (TAIL_WIN * n0 + TAIL_THREADS - 1) / TAIL_THREADS + 2;  // (+ mode 0's per-side rounding)
-    HALO_CHECK(ses->table.reserve((size_t)TAIL_TBL * TAIL_MUL * n0 * 128));
     HALO_CHECK(ses->w[0].reserve(n0 * 32));
     HALO_CHECK(ses->w[1].reserve(n0 * 32));
     HALO_CHECK(ses->scal.reserve(n0 * 32));
     HALO_CHECK(ses->side.reserve(n0));
     HALO_CHECK(ses->part.reserve(nblk * 2 * 128));
+    SrsState& srs = st->srs[ses->curve];
+    static const bool srs_tab = !(getenv("HALO_IPA_SRS_TABLE") && getenv("HALO_IPA_SRS_TABLE")[0] == '0');  // A/B knob
+    if (srs_tab && ses->gs_srs_prefix && n0 <= std::min(SRS_SMALL_N, srs.n)) {
+        HALO_CHECK(srs_small_table(st, ses->curve, s));
+        ses->table = srs.small_tab.as<const uint4>();
+        ses->table_ld = srs.small_n0;
+    } else {
+        if (!ses->gs_valid) return set_error(HALO_EINVAL, "ipa tail: G not resident");
+        HALO_CHECK(ses->own_table.reserve((size_t)TAIL_TBL * TAIL_MUL * n0 * 128));
+        DISPATCH_CURVE(ses->curve, Cv, {
+            hipLaunchKernelGGL(k_tail_table<Cv>, dim3(gridn(n0, 64)), dim3(64), 0, s, ses->gs.as<const uint4>(),
+                               (int)ses->gs_xyzz, n0, ses->own_table.as<uint4>());
+            hipLaunchKernelGGL(k_tail_mults<Cv>, dim3(gridn((size_t)TAIL_MLANES * TAIL_TBL * n0, 64)), dim3(64), 0, s, n0,
+                               ses->own_table.as<uint4>());
+        });
+        HALO_HIP(hipGetLastError());
+        ses->table = ses->own_table.as<const uint4>();
+        ses->table_ld = n0;
+    }
     DISPATCH_CURVE(ses->curve, Cv, {
-        hipLaunchKernelGGL(k_tail_table<Cv>, dim3(gridn(n0, 64)), dim3(64), 0, s, ses->gs.as<const uint4>(),
-                           (int)ses->gs_xyzz, n0,
-                           ses->table.as<uint4>());
-        hipLaunchKernelGGL(k_tail_mults<Cv>, dim3(gridn((size_t)TAIL_MLANES * TAIL_TBL * n0, 64)), dim3(64), 0, s, n0,
-                           ses->table.as<uint4>());
         hipLaunchKernelGGL(k_set_one_ark<typename Cv::Scalar>, dim3(1), dim3(64), 0, s, ses->w[0].as<uint4>());
     });
     HALO_HIP(hipGetLastError());
@@ -1029,7 +1301,7 @@ static int ipa_tail_sums(halo_ipa_session* ses, int mode, hipStream_t s) {
         hipLaunchKernelGGL(k_tail_scalars<Cv>, dim3(gridn(n0, 256)), dim3(256), 0, s, ses->cs.as<const uint4>(),
                            ses->w[ses->wcur].as<const uint4>(), n0, 2 * m, m, mode, ses->scal.as<uint32_t>(),
                            ses->side.as<uint8_t>());
-        hipLaunchKernelGGL(k_tail_msm<Cv>, dim3((unsigned)nblk), dim3(TAIL_THREADS), 0, s, ses->table.as<const uint4>(),
+        hipLaunchKernelGGL(k_tail_msm<Cv>, dim3((unsigned)nblk), dim3(TAIL_THREADS), 0, s, ses->table, ses->table_ld,
                            ses->scal.as<const uint32_t>(), ses->side.as<const uint8_t>(), n0, m, mode, (uint32_t)nbs,
                            ses->part.as<uint4>());
         hipLaunchKernelGGL(k_tail_final<Cv>, dim3(mode == 0 ? 2 : 1), dim3(TAIL_THREADS), 0, s,
@@ -1040,44 +1312,54 @@ static int ipa_tail_sums(halo_ipa_session* ses, int mode, hipStream_t s) {
     return HALO_OK;
 }
 
-// Small MSM over the resident SRS prefix (msm.hpp): the tail rounds' machinery with G0 = Gs[0..n0),
-// n0 = min(SRS_SMALL_N, srs.n): the multiples table (k_tail_table + k_tail_mults) is built on first
-// use per SRS, the scalars are zero-padded to n0 (a zero digit is an identity term), and mode 1 of
-// k_tail_scalars / k_tail_msm gives sum_k s[k] G0[k]; k_tail_final adds w S from the 2^i S table.
+// The SRS prefix's multiples table d 2^(4 w) G_k (k < n0 = min(SRS_SMALL_N, srs.n)), built on first
+// use per SRS (k_tail_table + k_tail_mults on stream s; small_tab_ev marks its completion for other
+// streams).  SrsState::invalidate_derived() (every writer of the SRS points) forces a rebuild.
+int halo::srs_small_table(DeviceState* st, int curve, hipStream_t s) {
+    SrsState& srs = st->srs[curve];
+    const size_t n0 = std::min(SRS_SMALL_N, srs.n);
+    if (!n0) return set_error(HALO_ESRSRANGE, "no resident SRS: call halo_srs_upload first");
+    if (!srs.small_tab_ev) HALO_HIP(hipEventCreateWithFlags(&srs.small_tab_ev, hipEventDisableTiming));
+    if (srs.small_n0 == n0) {
+        HALO_HIP(hipStreamWaitEvent(s, srs.small_tab_ev, 0));
+        return HALO_OK;
+    }
+    if (srs.small_ev) HALO_HIP(hipStreamWaitEvent(s, srs.small_ev, 0));  // the old table's last reader
+    HALO_CHECK(srs.small_tab.reserve((size_t)TAIL_TBL * TAIL_MUL * n0 * 128));
+    DISPATCH_CURVE(curve, Cv, {
+        hipLaunchKernelGGL(k_tail_table<Cv>, dim3(gridn(n0, 64)), dim3(64), 0, s, srs.gs.as<const uint4>(), 0, n0,
+                           srs.small_tab.as<uint4>());
+        hipLaunchKernelGGL(k_tail_mults<Cv>, dim3(gridn((size_t)TAIL_MLANES * TAIL_TBL * n0, 64)), dim3(64), 0, s, n0,
+                           srs.small_tab.as<uint4>());
+    });
+    HALO_HIP(hipGetLastError());
+    HALO_HIP(hipEventRecord(srs.small_tab_ev, s));
+    srs.small_n0 = n0;
+    return HALO_OK;
+}
+
+// Small MSM over the resident SRS prefix (msm.hpp): the tail rounds' machinery over G0 = Gs[0..n)
+// with the SRS's multiples table (leading dimension small_n0 >= n); mode 1 of k_tail_scalars /
+// k_tail_msm gives sum_k s[k] G0[k] (64 n table terms), k_tail_final adds w S from the 2^i S table.
 int halo::msm_srs_small(DeviceState* st, int curve, const void* scalars_ark, size_t n, const void* hide_scalar,
                   void* d_out_wrapped, hipStream_t s) {
     SrsState& srs = st->srs[curve];
-    const size_t n0 = std::min(SRS_SMALL_N, srs.n);
-    if (n < 1 || n > n0) return set_error(HALO_EINVAL, "small SRS MSM: n (%zu) outside [1, %zu]", n, n0);
-    const size_t nblk = (TAIL_WIN * n0 + TAIL_THREADS - 1) / TAIL_THREADS;
-    // scratch: scalars (n0 x 32 B) | GLV words (n0 x 32 B) | sides (n0 B, 256-B aligned) | partials
-    const size_t o_scal = n0 * 32, o_side = 2 * n0 * 32, o_part = o_side + ((n0 + 255) & ~(size_t)255);
+    const size_t nmax = std::min(SRS_SMALL_N, srs.n);
+    if (n < 1 || n > nmax) return set_error(HALO_EINVAL, "small SRS MSM: n (%zu) outside [1, %zu]", n, nmax);
+    const size_t nblk = (TAIL_WIN * n + TAIL_THREADS - 1) / TAIL_THREADS;
+    // scratch: GLV words (n x 32 B) | sides (n B, 256-B aligned) | partials
+    const size_t o_side = n * 32, o_part = o_side + ((n + 255) & ~(size_t)255);
+    if (srs.small_ev) HALO_HIP(hipStreamWaitEvent(s, srs.small_ev, 0));  // the previous small MSM is done with small_scr
+    else HALO_HIP(hipEventCreateWithFlags(&srs.small_ev, hipEventDisableTiming));
     HALO_CHECK(srs.small_scr.reserve(o_part + nblk * 256));
-    if (!srs.small_ev)
-        HALO_HIP(hipEventCreateWithFlags(&srs.small_ev, hipEventDisableTiming));
-    else  // the previous small MSM (perhaps on another stream) is done with small_scr
-        HALO_HIP(hipStreamWaitEvent(s, srs.small_ev, 0));
-    if (srs.small_n0 != n0) {
-        HALO_CHECK(srs.small_tab.reserve((size_t)TAIL_TBL * TAIL_MUL * n0 * 128));
-        DISPATCH_CURVE(curve, Cv, {
-            hipLaunchKernelGGL(k_tail_table<Cv>, dim3(gridn(n0, 64)), dim3(64), 0, s, srs.gs.as<const uint4>(), 0, n0,
-                               srs.small_tab.as<uint4>());
-            hipLaunchKernelGGL(k_tail_mults<Cv>, dim3(gridn((size_t)TAIL_MLANES * TAIL_TBL * n0, 64)), dim3(64), 0, s,
-                               n0, srs.small_tab.as<uint4>());
-        });
-        HALO_HIP(hipGetLastError());
-        srs.small_n0 = n0;
-    }
+    HALO_CHECK(srs_small_table(st, curve, s));
     char* scr = (char*)srs.small_scr.ptr;
-    if (n < n0) HALO_HIP(hipMemsetAsync(scr + n * 32, 0, (n0 - n) * 32, s));
-    HALO_HIP(hipMemcpyAsync(scr, scalars_ark, n * 32, hipMemcpyDeviceToDevice, s));
     DISPATCH_CURVE(curve, Cv, {
-        hipLaunchKernelGGL(k_tail_scalars<Cv>, dim3(gridn(n0, 256)), dim3(256), 0, s, (const uint4*)nullptr,
-                           (const uint4*)scr, n0, (size_t)1, (size_t)0, 1, (uint32_t*)(scr + o_scal),
-                           (uint8_t*)(scr + o_side));
+        hipLaunchKernelGGL(k_tail_scalars<Cv>, dim3(gridn(n, 256)), dim3(256), 0, s, (const uint4*)nullptr,
+                           (const uint4*)scalars_ark, n, (size_t)1, (size_t)0, 1, (uint32_t*)scr, (uint8_t*)(scr + o_side));
         hipLaunchKernelGGL(k_tail_msm<Cv>, dim3((unsigned)nblk), dim3(TAIL_THREADS), 0, s,
-                           srs.small_tab.as<const uint4>(), (const uint32_t*)(scr + o_scal),
-                           (const uint8_t*)(scr + o_side), n0, (size_t)0, 1, 0u, (uint4*)(scr + o_part));
+                           srs.small_tab.as<const uint4>(), srs.small_n0, (const uint32_t*)scr,
+                           (const uint8_t*)(scr + o_side), n, (size_t)0, 1, 0u, (uint4*)(scr + o_part));
         hipLaunchKernelGGL(k_tail_final<Cv>, dim3(1), dim3(TAIL_THREADS), 0, s, (const uint4*)(scr + o_part), (int)nblk,
                            hide_scalar ? srs.s_table.as<const uint4>() : (const uint4*)nullptr,
                            (const uint4*)hide_scalar, (uint4*)d_out_wrapped, 0);
@@ -1096,6 +1378,7 @@ static int ipa_copy_out(halo_ipa_session* ses) {
 // Enqueues one round's L and R (with their H' terms) and their D2H copy into ses->pinned.
 static int ipa_round_launch(DeviceState* st, halo_ipa_session* ses) {
     if (ses->m == 0) return set_error(HALO_EINVAL, "halo_ipa_round_lr: no rounds left");
+    if (!ses->started) return set_error(HALO_EINVAL, "halo_ipa_round_lr: session not started (halo_pcdl_open_start)");
     hipStream_t s = ses->s;
     const size_t m = ses->m;
     const int sf = ses->curve == HALO_PALLAS ? HALO_FP : HALO_FQ;
@@ -1116,9 +1399,11 @@ static int ipa_round_launch(DeviceState* st, halo_ipa_session* ses) {
                                     ses->wlen, 2 * m, ses->gs.ptr, to_tail, ses->mat, s, sh ? srs.n : 0,
                                     sh ? srs.shifted_c : 0));
         ses->gs_xyzz = to_tail;
+        ses->gs_valid = true;
+        ses->gs_srs_prefix = false;
         ses->weighted = false;
     }
-    if (!ses->tail && ses->allow_tail && 2 * m <= ipa_tail_n()) HALO_CHECK(ipa_enter_tail(ses, s));
+    if (!ses->tail && ses->allow_tail && 2 * m <= ipa_tail_n()) HALO_CHECK(ipa_enter_tail(st, ses, s));
     const char* gs = ses->gs.as<const char>();  // (materialised above in a weighted session)
     // only round 1 orders its hiding terms after the side-stream table: every later round starts after
     // the host has synchronised on round 1's results, which needed the table (a cross-stream wait in
@@ -1190,8 +1475,9 @@ static int ipa_round_launch(DeviceState* st, halo_ipa_session* ses) {
 }
 
 // Enqueues one fold with challenge xi (pcdl.rs:427-435); the session advances to the next round.
-static int ipa_fold_launch(halo_ipa_session* ses, const halo_fe_t* xi, const halo_fe_t* xi_inv) {
+static int ipa_fold_launch(DeviceState* st, halo_ipa_session* ses, const halo_fe_t* xi, const halo_fe_t* xi_inv) {
     if (ses->m == 0) return set_error(HALO_EINVAL, "halo_ipa_fold: no rounds left");
+    if (!ses->started) return set_error(HALO_EINVAL, "halo_ipa_fold: session not started (halo_pcdl_open_start)");
     hipStream_t s = ses->s;
     char* sm = (char*)ses->small.ptr;
     // the previous fold's H2D copy from the pinned staging must have completed (a round in between
@@ -1203,6 +1489,10 @@ static int ipa_fold_launch(halo_ipa_session* ses, const halo_fe_t* xi, const hal
     HALO_HIP(hipMemcpyAsync(sm + 384, ses->pinned + 128, 64, hipMemcpyHostToDevice, s));
     const size_t m = ses->m;
     ses->srs_round0 = false;
+    if (!ses->tail && !ses->weighted) {  // G itself is folded below
+        HALO_CHECK(ipa_ensure_gs(st, ses));
+        ses->gs_srs_prefix = false;
+    }
     if (ses->tail || ses->weighted) {
         DISPATCH_CURVE(ses->curve, Cv, {
             hipLaunchKernelGGL(k_tail_fold<Cv>, dim3(gridn(std::max(m, ses->wlen), 256)), dim3(256), 0, s,
@@ -1269,7 +1559,7 @@ extern "C" int halo_ipa_fold_multi(halo_ipa_session* const* ses, size_t k, const
     std::lock_guard<std::mutex> g(st->mu);
     for (size_t i = 0; i < k; i++) {
         if (!ses[i]) return set_error(HALO_EINVAL, "halo_ipa_fold_multi: null session %zu", i);
-        HALO_CHECK(ipa_fold_launch(ses[i], &xi[i], &xi_inv[i]));
+        HALO_CHECK(ipa_fold_launch(st, ses[i], &xi[i], &xi_inv[i]));
     }
     // no host wait: the fold is stream-ordered before the next round (which synchronises), so the host
     // goes on to the transcript and the next round's launches while it runs
@@ -1285,7 +1575,7 @@ extern "C" int halo_ipa_state(halo_ipa_session* ses, size_t* m, halo_wrapped_poi
     hipStream_t s = ses->s;
     const size_t len = std::max<size_t>(2 * ses->m, 1);
     if (m) *m = ses->m;
-    if (gs && (ses->tail || ses->weighted))
+    if (gs && (ses->tail || ses->weighted || !ses->gs_valid))
         return set_error(HALO_EINVAL,
                          "halo_ipa_state: G is not materialised in the weighted / tail rounds (HALO_IPA_WEIGHTED=0, "
                          "HALO_IPA_TAIL=0)");
@@ -1306,13 +1596,15 @@ extern "C" int halo_ipa_end(halo_ipa_session* ses, halo_wrapped_point_t* U, halo
     if (U || c) {
         DeviceState* st = current_state();
         if (!st) {
-            delete ses;
+            ipa_release(ses);
             return HALO_EDEVICE;
         }
         std::lock_guard<std::mutex> g(st->mu);
         hipStream_t s = ses->s;
         char* sm = (char*)ses->small.ptr;
-        if (ses->tail || ses->weighted) {
+        if (!ses->started) {
+            rc = set_error(HALO_EINVAL, "halo_ipa_end: session not started");
+        } else if (ses->tail || ses->weighted) {
             // U = G_0 = sum_u w[u] G0[u] (len = 1 once every round ran)
             if (ses->m != 0)
                 rc = set_error(HALO_EINVAL, "halo_ipa_end: U needs every round in the weighted / tail rounds (m = %zu)",
@@ -1324,6 +1616,7 @@ extern "C" int halo_ipa_end(halo_ipa_session* ses, halo_wrapped_point_t* U, halo
                                           s, false);
             if (!rc && hipMemcpyAsync(sm + 320, ses->cs.ptr, 32, hipMemcpyDeviceToDevice, s) != hipSuccess)
                 rc = set_error(HALO_EDEVICE, "ipa end copy failed");
+        } else if ((rc = ipa_ensure_gs(st, ses))) {
         } else {
             DISPATCH_CURVE(ses->curve, Cv, {
                 hipLaunchKernelGGL(k_copy_first_wrapped<Cv>, dim3(1), dim3(64), 0, s, ses->gs.as<const uint4>(),
@@ -1331,10 +1624,14 @@ extern "C" int halo_ipa_end(halo_ipa_session* ses, halo_wrapped_point_t* U, halo
             });
             if (hipGetLastError() != hipSuccess) rc = set_error(HALO_EDEVICE, "ipa end launch failed");
         }
-        if (!rc && U) rc = copy_d2h(U, sm + 256, 64, s);
-        if (!rc && c) rc = copy_d2h(c, sm + 320, 32, s);
+        // U | c are contiguous: one copy through the pinned staging
+        if (!rc && hipMemcpyAsync(ses->pinned + 256, sm + 256, 96, hipMemcpyDeviceToHost, s) != hipSuccess)
+            rc = set_error(HALO_EDEVICE, "ipa end copy failed");
+        if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = set_error(HALO_EDEVICE, "ipa end synchronisation failed");
+        if (!rc && U) memcpy(U, ses->pinned + 256, 64);
+        if (!rc && c) memcpy(c, ses->pinned + 320, 32);
     }
-    delete ses;
+    ipa_release(ses);
     return rc;
 }
 

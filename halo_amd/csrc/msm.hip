@@ -1635,8 +1635,7 @@ static int srs_install(DeviceState* st, int curve, const void* d_wrapped, size_t
     HALO_CHECK(srs.gs.reserve(std::max<size_t>(n, 1) * 64));
     HALO_CHECK(convert_wrapped_to_internal(curve, d_wrapped, srs.gs.ptr, n, s));
     srs.n = n;
-    srs.shifted_c = 0;
-    srs.small_n0 = 0;
+    srs.invalidate_derived();
     if (S && H) {
         HALO_CHECK(st->scratch[1].reserve(256));
         char* tmp = (char*)st->scratch[1].ptr;
@@ -1645,6 +1644,7 @@ static int srs_install(DeviceState* st, int curve, const void* d_wrapped, size_t
         HALO_CHECK(convert_wrapped_to_internal(curve, tmp, tmp + 128, 2, s));
         HALO_CHECK(copy_d2h(srs.S, tmp + 128, 64, s));
         HALO_CHECK(copy_d2h(srs.H, tmp + 192, 64, s));
+        srs.H_wrapped = *H;
         srs.has_sh = true;
         HALO_CHECK(build_s_table(st, curve, s));
     }
@@ -1843,7 +1843,7 @@ extern "C" int halo_srs_synthesize(halo_curve_t curve, size_t n, uint64_t seed) 
     }
     HALO_HIP(hipStreamSynchronize(s));
     srs.n = n;
-    srs.shifted_c = 0;
+    srs.invalidate_derived();
     return HALO_OK;
 }
 

@@ -24,6 +24,8 @@ int msm_batch_device(DeviceState* st, int curve, const void* const* d_scalars, c
                      hipStream_t s);
 // Destroys the MSM pipeline's streams and events (halo_shutdown).
 void msm_shutdown();
+// Releases the pooled IPA sessions (halo_shutdown, ipa.hip).
+void ipa_shutdown();
 // Makes stream s wait for the reduction tails of the async MSMs enqueued on s.
 int msm_join(DeviceState* st, hipStream_t s);
 // MSM over the resident SRS prefix (window-shifted copies when precomputed); optional hiding
@@ -65,9 +67,21 @@ int srs_precompute_windows(DeviceState* st, int curve, hipStream_t s);
 // window) term is one entry of a per-SRS multiples table, then block trees with the hiding term
 // hide_scalar * S from the 2^i S table -- no sort, buckets or bucket reduction.  Stream-ordered on s;
 // writes one ark WrappedPoint to d_out_wrapped.
-constexpr size_t SRS_SMALL_N = 1024;
+constexpr size_t SRS_SMALL_N = 2048;
+// The multiples table of the SRS prefix (SrsState::small_tab, built on first use over
+// min(SRS_SMALL_N, srs.n) points); stream s waits for its completion.  Shared by the small MSMs and
+// by IPA sessions whose tail rounds start on the unfolded SRS prefix.
+int srs_small_table(DeviceState* st, int curve, hipStream_t s);
 int msm_srs_small(DeviceState* st, int curve, const void* scalars_ark, size_t n, const void* hide_scalar,
                   void* d_out_wrapped, hipStream_t s);
+// The hiding branch of pcdl::open_without_eval on device buffers (field_ops.hip), stream-ordered on s:
+// p_bar = (X - z) q (q: d ark coefficients, z: ark scalar) -> d + 1 ark coefficients;
+// p' = p (len coefficients, zero-padded to n) + alpha p_bar (p' may alias p), w' = w + alpha w_bar,
+// C' = C + alpha C_bar - w' S (C, C_bar, C' WrappedPoints; S internal affine).
+int pcdl_pbar_device(int curve, const void* q, size_t d, const void* z, void* p_bar, hipStream_t s);
+int pcdl_combine_device(int curve, const void* p, size_t len, const void* p_bar, size_t n, const void* alpha,
+                        const void* w, const void* w_bar, const void* C, const void* C_bar, const void* S_int,
+                        void* p_prime, void* C_prime, void* w_prime, hipStream_t s);
 // Host conversion of a 128-B packed XYZZ point (internal format, each coordinate < 2p) to an ark
 // WrappedPoint: one inversion in 4 x 64-bit Montgomery arithmetic on the CPU (identity -> (0, 0)).
 void host_xyzz_to_wrapped(int curve, const void* xyzz, void* wrapped);

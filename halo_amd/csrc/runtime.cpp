@@ -51,6 +51,12 @@ ScratchUse::~ScratchUse() {
     }
 }
 
+void DevBuf::release() {
+    if (ptr) (void)hipFree(ptr);
+    ptr = nullptr;
+    bytes = 0;
+}
+
 DevBuf::~DevBuf() {
     // Device state lives for the process; freeing at exit can race the HIP runtime teardown.
 }
@@ -209,12 +215,18 @@ int halo_shutdown(void) {
         g_prof_on = false;
     }
     msm_shutdown();
+    ipa_shutdown();
     std::lock_guard<std::mutex> g(g_states_mu);
     for (DeviceState* st : g_states) {
         if (!st) continue;
         std::lock_guard<std::mutex> g2(st->mu);
         if (st->scratch_ev) (void)hipEventDestroy(st->scratch_ev);
         st->scratch_ev = nullptr;
+        for (SrsState& srs : st->srs) {
+            if (srs.small_ev) (void)hipEventDestroy(srs.small_ev);
+            if (srs.small_tab_ev) (void)hipEventDestroy(srs.small_tab_ev);
+            srs.small_ev = srs.small_tab_ev = nullptr;
+        }
         st->scratch_used = false;
         st->scratch_last = nullptr;
     }

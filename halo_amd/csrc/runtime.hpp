@@ -40,6 +40,7 @@ struct DevBuf {
     void* ptr = nullptr;
     size_t bytes = 0;
     int reserve(size_t n);  // ensures capacity >= n bytes
+    void release();         // hipFree now (the caller has ordered every user of the buffer before it)
     template <class T>
     T* as() const { return static_cast<T*>(ptr); }
     ~DevBuf();
@@ -52,17 +53,31 @@ struct SrsState {
     bool has_sh = false;
     uint32_t S[16];     // internal packed (x, y)
     uint32_t H[16];
+    halo_wrapped_point_t H_wrapped;  // H as uploaded (the key of its 2^i H table)
     DevBuf s_table;     // 2^i S (i < 256), internal affine: hiding term of pedersen::commit
-    DevBuf h_table;     // 2^i H (i < 128), internal affine: the IPA's H' = xi_0 H terms (halo_ipa_begin_xi)
-    uint64_t h_key[8] = {};  // the WrappedPoint H that h_table was built from
-    bool h_built = false;
-    DevBuf small_tab;   // d 2^(4 w) G_k (k < small_n0, w < 32, d < 16), XYZZ: small SRS MSMs (ipa.hip)
+    // 2^i H (i < 128), internal affine: the IPA's H' = xi_0 H terms (halo_ipa_begin_xi), one table per
+    // distinct H, never rewritten while the library lives (open sessions keep pointers into them)
+    struct HTable {
+        uint64_t key[8];  // the WrappedPoint H the table was built from
+        DevBuf t;
+    };
+    std::vector<std::unique_ptr<HTable>> h_tables;
+    DevBuf small_tab;   // d 2^(4 w) G_k (k < small_n0, w < 32, d < 16), XYZZ: small SRS MSMs, IPA tails (ipa.hip)
     size_t small_n0 = 0;             // 0 = not built for the current SRS
-    DevBuf small_scr;                // padded scalars, GLV digits, block partials of a small MSM
+    hipEvent_t small_tab_ev = nullptr;  // small_tab's build completed
+    DevBuf small_scr;                // GLV digits, block partials of a small MSM
     hipEvent_t small_ev = nullptr;   // last small MSM's completion (orders reuse of small_scr)
     DevBuf shifted;     // optional window-shifted copies
     int shifted_c = 0;  // window bits of `shifted`
     int shifted_windows = 0;
+    // Every writer of `gs` calls this: the tables derived from the old points (window-shifted copies,
+    // the small-MSM / tail multiples table) are rebuilt on next use.  (a synthesize after
+    // a small commit used to keep the old SRS's table.)
+    void invalidate_derived() {
+        shifted_c = 0;
+        shifted_windows = 0;
+        small_n0 = 0;
+    }
 };
 
 struct DeviceState {

@@ -139,58 +139,60 @@ def _ark_inverse(x: np.ndarray, cid: int) -> np.ndarray:
 def open_without_eval(p, C, d: int, z, v, w=None, transcript=None, q=None, w_bar=None, curve="pallas") -> dict:
     """pcdl::open_without_eval (pcdl.rs:326-453) on the device, hiding branch included.
 
-    p: coefficients (ark scalars, <= d + 1 of them); C its commitment; z, v ark scalars; w the
-    commitment randomness (None: non-hiding).  ``transcript`` is the caller's Fiat-Shamir sponge with
-    the reference's interface (outer_sponge.rs: absorb_g(points), absorb_fr(scalars), challenge()),
-    over WrappedPoints / ark scalars; a fresh PCDL sponge, as pcdl.rs:336 creates.  q (d coefficients)
-    and w_bar are the random draws the reference takes from its rng (pcdl.rs:347,352).
+    p: coefficients (ark scalars, degree <= d); C its commitment; z, v ark scalars; w the commitment
+    randomness (None: non-hiding).  ``transcript`` is the caller's Fiat-Shamir sponge with the
+    reference's interface (outer_sponge.rs: absorb_g(points), absorb_fr(scalars), challenge()) over
+    WrappedPoints / ark scalars -- a fresh PCDL sponge, as pcdl.rs:336 creates; it is required (the
+    sponge is host logic outside this backend).  q (d coefficients) and w_bar are the random draws the
+    reference takes from its rng (pcdl.rs:347,352).  p, p_bar and p' stay in the session's device
+    buffers from the blind to the rounds (halo_pcdl_open_begin / _blind / _combine / _start).
     Returns the EvalProof: dict(Ls, Rs, U, c, C_bar, w_prime)."""
+    if transcript is None:
+        raise ValueError("open_without_eval needs the caller's PCDL transcript (pcdl.rs:336 Sponge::new(PCDL))")
     H.ensure_device()
     L = H.load()
     cid = _curve(curve)
     n = d + 1
-    assert n > 1
-    assert n & (n - 1) == 0, f"n ({n}) is not a power of two"
     p = H.fe_array(p) if len(p) else np.zeros((0, 4), dtype=np.uint64)
     zz, vv = H.fe_array(z, 1)[0], H.fe_array(v, 1)[0]
     C = H.point_array(C).reshape(8)
-    C_bar = w_prime = None
-    if w is not None:
-        qq = H.fe_array(q)
-        wb = H.fe_array(w_bar, 1)
-        p_bar = np.zeros((n, 4), dtype=np.uint64)
-        C_bar = np.zeros(8, dtype=np.uint64)
-        H.check(L.halo_pcdl_hiding_blind(cid, H.ptr(qq), d, H.ptr(zz), H.ptr(wb), H.ptr(p_bar), H.ptr(C_bar)))
-        transcript.absorb_g([C, C_bar])
+    s = ctypes.c_void_p()
+    # asserts n > 1, n a power of two, p.degree() <= d, d <= D (pcdl.rs:338-341)
+    H.check(L.halo_pcdl_open_begin(cid, H.ptr(p) if len(p) else None, len(p), d, H.ptr(zz), ctypes.byref(s)))
+    ses = IpaSession.__new__(IpaSession)
+    ses.curve, ses.n, ses._s = cid, n, s
+    try:
+        C_bar = w_prime = None
+        if w is not None:
+            C_bar = np.zeros(8, dtype=np.uint64)
+            H.check(L.halo_pcdl_open_blind(s, H.ptr(H.fe_array(q, d)), H.ptr(H.fe_array(w_bar, 1)), H.ptr(C_bar)))
+            transcript.absorb_g([C, C_bar])
+            transcript.absorb_fr([zz, vv])
+            alpha = np.ascontiguousarray(transcript.challenge(), dtype=np.uint64)
+            w_prime = np.zeros(4, dtype=np.uint64)
+            C_prime = np.zeros(8, dtype=np.uint64)
+            H.check(L.halo_pcdl_open_combine(s, H.ptr(alpha), H.ptr(C), H.ptr(H.fe_array(w, 1)), H.ptr(w_prime),
+                                             H.ptr(C_prime)))
+        else:
+            C_prime = C
+        transcript.absorb_g([C_prime])
         transcript.absorb_fr([zz, vv])
-        alpha = np.ascontiguousarray(transcript.challenge(), dtype=np.uint64)
-        p_prime = np.zeros((n, 4), dtype=np.uint64)
-        w_prime = np.zeros(4, dtype=np.uint64)
-        C_prime = np.zeros(8, dtype=np.uint64)
-        H.check(L.halo_pcdl_hiding_combine(cid, H.ptr(p) if len(p) else None, len(p), H.ptr(p_bar), d, H.ptr(alpha),
-                                           H.ptr(C), H.ptr(C_bar), H.ptr(H.fe_array(w, 1)), H.ptr(wb),
-                                           H.ptr(p_prime), H.ptr(w_prime), H.ptr(C_prime)))
-        p = p_prime
-    else:
-        C_prime = C
-    transcript.absorb_g([C_prime])
-    transcript.absorb_fr([zz, vv])
-    xi = np.ascontiguousarray(transcript.challenge(), dtype=np.uint64)
-    from .group import PublicParams
-    _, Hpt = PublicParams.sh(curve)
-    cs = np.zeros((n, 4), dtype=np.uint64)
-    cs[: len(p)] = p[:n]
-    ses = IpaSession.with_xi(cs, zz, Hpt, xi, curve)  # H' = xi_0 H (pcdl.rs:390-391) on the device
-    Ls, Rs = [], []
-    for _ in range(n.bit_length() - 1):
-        Lp, Rp = ses.round_lr()
-        Ls.append(Lp)
-        Rs.append(Rp)
-        transcript.absorb_fr([xi])
-        transcript.absorb_g([Lp, Rp])
         xi = np.ascontiguousarray(transcript.challenge(), dtype=np.uint64)
-        ses.fold(xi, _ark_inverse(xi, cid))
-    U, c = ses.end()
+        H.check(L.halo_pcdl_open_start(s, None, H.ptr(xi)))  # H' = xi_0 pp.H (pcdl.rs:390)
+        Ls, Rs = [], []
+        for _ in range(n.bit_length() - 1):
+            Lp, Rp = ses.round_lr()
+            Ls.append(Lp)
+            Rs.append(Rp)
+            transcript.absorb_fr([xi])
+            transcript.absorb_g([Lp, Rp])
+            xi = np.ascontiguousarray(transcript.challenge(), dtype=np.uint64)
+            ses.fold(xi, _ark_inverse(xi, cid))
+        U, c = ses.end()
+    finally:
+        if ses._s is not None:  # an assertion or error above: return the session to the pool
+            L.halo_ipa_end(ses._s, None, None)
+            ses._s = None
     return {"Ls": Ls, "Rs": Rs, "U": U, "c": c, "C_bar": C_bar, "w_prime": w_prime}
 
 

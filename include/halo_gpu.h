@@ -303,6 +303,28 @@ int halo_ipa_begin_dev_xi(halo_curve_t curve, const void* d_cs, size_t n, const 
 int halo_ipa_begin_vectors(halo_curve_t curve, const halo_wrapped_point_t* gs, const halo_fe_t* cs,
                            const halo_fe_t* zs, size_t n, const halo_wrapped_point_t* H_prime,
                            halo_ipa_session** out);
+/* pcdl::open_without_eval (crates/accumulation/src/pcdl.rs:326-392) as one session whose p, p_bar
+ * and p' never leave the device; the caller keeps the transcript between the steps, as the
+ * reference does:
+ *   halo_pcdl_open_begin(p: len coefficients, d, z)    n = d + 1 > 1 a power of two, p.degree() <= d,
+ *                                                      d <= D (pcdl.rs:338-341); c = p padded to n
+ *   hiding (w = Some):
+ *     halo_pcdl_open_blind(q: d coefficients, w_bar) -> C_bar       p_bar = (X - z) q,
+ *                                                      C_bar = pcdl::commit(p_bar, d, w_bar) (pcdl.rs:344-355)
+ *     (transcript: absorb_g(C, C_bar), absorb_fr(z, v), alpha = challenge)
+ *     halo_pcdl_open_combine(alpha, C, w) -> w', C'  c = p + alpha p_bar, w' = w + alpha w_bar,
+ *                                                      C' = C + alpha C_bar - w' S (pcdl.rs:366-371)
+ *   (transcript: absorb_g(C'), absorb_fr(z, v), xi_0 = challenge)
+ *   halo_pcdl_open_start(H, xi_0)                     H' = xi_0 H (pcdl.rs:390; H = NULL: the resident
+ *                                                      SRS's pp.H), then the rounds
+ * followed by halo_ipa_round_lr / halo_ipa_fold / halo_ipa_end as for the other sessions.  The
+ * rounds refuse a session that was not started. */
+int halo_pcdl_open_begin(halo_curve_t curve, const halo_fe_t* p, size_t len, size_t d, const halo_fe_t* z,
+                         halo_ipa_session** out);
+int halo_pcdl_open_blind(halo_ipa_session* s, const halo_fe_t* q, const halo_fe_t* w_bar, halo_wrapped_point_t* C_bar);
+int halo_pcdl_open_combine(halo_ipa_session* s, const halo_fe_t* alpha, const halo_wrapped_point_t* C,
+                           const halo_fe_t* w, halo_fe_t* w_prime, halo_wrapped_point_t* C_prime);
+int halo_pcdl_open_start(halo_ipa_session* s, const halo_wrapped_point_t* H, const halo_fe_t* xi0);
 /* L = <c_r, G_l> + H' <c_r, z_l>,  R = <c_l, G_r> + H' <c_l, z_r>  (pcdl.rs:412-418) */
 int halo_ipa_round_lr(halo_ipa_session* s, halo_wrapped_point_t* L, halo_wrapped_point_t* R);
 /* G_l[j] = G_l[j] + xi G_r[j] (affine), c_l[j] += xi^-1 c_r[j], z_l[j] += xi z_r[j]; m /= 2
@@ -320,7 +342,9 @@ int halo_ipa_fold_multi(halo_ipa_session* const* ses, size_t k, const halo_fe_t*
  * round): asking for gs there is HALO_EINVAL. */
 int halo_ipa_state(halo_ipa_session* s, size_t* m, halo_wrapped_point_t* gs, halo_fe_t* cs,
                    halo_fe_t* zs);
-/* U = G_0 and c_0 after the last round (in weighted / tail rounds U is only defined then). */
+/* U = G_0 and c_0 after the last round (in weighted / tail rounds U is only defined then).  The
+ * session's streams and device buffers go back to a per-device pool (reused by the next opening;
+ * released by halo_shutdown), so a warm opening allocates nothing. */
 int halo_ipa_end(halo_ipa_session* s, halo_wrapped_point_t* U, halo_fe_t* c);
 /* One stateless fold over host vectors of length 2m (the loop body of pcdl.rs:427-435), in place
  * on the left halves. */

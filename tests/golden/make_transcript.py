@@ -105,7 +105,55 @@ def main():
             out[key + "_Cbar"] = pw([pi["C_bar"]])
             out[key + "_wprime_alpha"] = fe([pi["w_prime"], pi["alpha"]])
         print(key, "done", flush=True)
+    # round 3: openings long enough for the device's weighted -> materialised ->
+    # tail rounds (n > 2048) under the reference's transcript order (pcdl.rs:387-425).  Their inputs
+    # p, q, z, w, w_bar are not stored: det_scalars(seed, k) (shared with tests/test_gpu_transcript.py)
+    # regenerates them from the stored seed, so only the outputs take space.
+    for seed, (cname, n, hiding) in enumerate((("pallas", 4096, True), ("pallas", 16384, False),
+                                                ("vesta", 4096, False), ("vesta", 16384, True),
+                                                ("pallas", 4096, False), ("vesta", 4096, True)), start=100):
+        c = P.CURVES[cname]
+        r = c.scalar
+        d = n - 1
+        gs = corc.srs_generate(cname, n)
+        S, H = [P.wrapped_to_point(c, [int(x) for x in row]) for row in
+                P.decode_sh(open(f"{REF}/group/.precompute/{cname}/sh.bin", "rb").read())]
+        ins = det_scalars(seed, 2 * n + 4)  # p (n - 1: degree d - 1), q (d), z, w, w_bar
+        val = [P.from_mont(limbs_int(x), r) for x in ins]
+        p = val[: n - 1]
+        q = val[n: n + d] if hiding else None
+        z = val[2 * n]
+        w = val[2 * n + 1] if hiding else None
+        w_bar = val[2 * n + 2] if hiding else None
+        v = P.horner(p, z, r)
+        C = pcdl_ref.commit(cname, gs, p, w, S)
+        pi = pcdl_ref.open_without_eval(cname, p, C, d, z, v, gs, S, H, w=w, q=q, w_bar=w_bar)
+        key = f"big_{cname}_n{n}_{'hiding' if hiding else 'plain'}"
+        fe = lambda xs: np.array([P.int_to_limbs(P.to_mont(x % r, r)) for x in xs], dtype=np.uint64).reshape(-1, 4)  # noqa: E731
+        pw = lambda pts: np.array([P.point_to_wrapped(c, x) for x in pts], dtype=np.uint64).reshape(-1, 8)  # noqa: E731
+        out[key + "_seed"] = np.array([seed], dtype=np.uint64)
+        out[key + "_zv"] = fe([z, v])
+        out[key + "_C"] = pw([C])
+        out[key + "_Ls"] = pw(pi["Ls"])
+        out[key + "_Rs"] = pw(pi["Rs"])
+        out[key + "_U"] = pw([pi["U"]])
+        out[key + "_c"] = fe([pi["c"]])
+        if hiding:
+            out[key + "_Cbar"] = pw([pi["C_bar"]])
+            out[key + "_wprime_alpha"] = fe([pi["w_prime"], pi["alpha"]])
+        print(key, "done", flush=True)
     np.savez_compressed(os.path.join(HERE, "transcript.npz"), **out)
+
+
+def det_scalars(seed: int, k: int) -> np.ndarray:
+    """k Montgomery-form scalars (valid in Fp and Fq: every value is < 2^254 < r) from seed."""
+    a = np.random.default_rng(seed).integers(0, 2**64 - 1, size=(k, 4), dtype=np.uint64, endpoint=True)
+    a[:, 3] &= np.uint64(0x3FFFFFFFFFFFFFFF)
+    return np.ascontiguousarray(a)
+
+
+def limbs_int(x) -> int:
+    return int(x[0]) | int(x[1]) << 64 | int(x[2]) << 128 | int(x[3]) << 192
 
 
 if __name__ == "__main__":

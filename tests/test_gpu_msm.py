@@ -267,6 +267,32 @@ def test_msm_small_chunks_shifted_skew(hal):
             assert list(got) == P.point_to_wrapped(c, P.mul_fast(c, acc, c.generator)), (lg, name)
 
 
+def test_small_table_follows_synthesize(hal, golden, corc):
+    """the small-MSM multiples table must be rebuilt when halo_srs_synthesize
+    replaces the points (same length, so the same table size): upload A, a small commit over A,
+    synthesize B, a small commit over B checked by B's known logs; then an IPA opening's tail over B."""
+    c = P.PALLAS
+    r = c.scalar
+    n = 4096
+    S, Hh = golden["ref_sh_pallas"]
+    group.PublicParams.upload("pallas", corc.srs_generate("pallas", n), S, Hh, precompute_windows=True)
+    sc = rand_sc(300, 77)
+    assert np.array_equal(pcdl.commit(sc, 511, None, "pallas"),
+                          corc.msm("pallas", corc.srs_generate("pallas", 300), sc))
+    seed = 1234
+    group.PublicParams.synthesize("pallas", n, seed, precompute_windows=True)
+    ks = [limbs_canon(k) for k in synth_scalars_np(seed, 300)]
+    sb = sc.tobytes()
+    acc = sum(int.from_bytes(sb[32 * j:32 * j + 32], "little") * ks[j] for j in range(300)) * pow(1 << 256, -1, r) % r
+    assert list(pcdl.commit(sc, 511, None, "pallas")) == P.point_to_wrapped(c, P.mul_fast(c, acc, c.generator))
+    for d in (0, 1023, 2047):  # the table's full range, and both sides of the old 1024 threshold
+        sc2 = rand_sc(d + 1, d)
+        sb2 = sc2.tobytes()
+        ks2 = [limbs_canon(k) for k in synth_scalars_np(seed, d + 1)]
+        acc = sum(int.from_bytes(sb2[32 * j:32 * j + 32], "little") * ks2[j] for j in range(d + 1)) * pow(1 << 256, -1, r) % r
+        assert list(pcdl.commit(sc2, d, None, "pallas")) == P.point_to_wrapped(c, P.mul_fast(c, acc, c.generator)), d
+
+
 def synth_scalars_np(seed: int, n: int) -> np.ndarray:
     """numpy restatement of halo_synth_scalar (splitmix64 stream per index; top word masked)."""
     M = np.uint64(0xFFFFFFFFFFFFFFFF)

@@ -46,6 +46,45 @@ def test_msm_2p24_synthetic_srs_known_logs(hal, corc):
     assert np.array_equal(got, corc.known_log_msm("pallas", sc[:m], k[:m]))
 
 
+def test_msm_2p24_window_partitioned_virtual_ranks_known_logs(hal, corc):
+    """BASELINE configs[4] at its size on one GPU: the 2^24-point MSM split by windows over 8 virtual
+    ranks (halo_amd.dist.window_range, the ranges bench.py --gpus 8 gives its ranks), each rank's
+    partial from halo_msm_srs_windows_dev, the partials summed on the device (halo_point_sum_dev, the
+    RCCL leg's combine) -- checked against the known-log identity (an independent oracle, not the
+    device's own one-GPU MSM); and the 3-rank partition of the same MSM."""
+    import ctypes
+
+    import torch
+    from halo_amd.dist import window_range
+
+    L = hal.load()
+    n = 1 << 24
+    seed = 0x57494E44
+    group.PublicParams.synthesize("pallas", n, seed, precompute_windows=True)
+    k = corc.synth_scalars(seed, n)
+    sc = rand_words(n, 4242)
+    sc[0] = P.int_to_limbs(P.to_mont(P.FP_MODULUS - 1, P.FP_MODULUS))
+    sc[1:2049] = sc[7]  # one bucket per window takes 2^11 extra points
+    exp = corc.known_log_msm("pallas", sc, k)
+    W = L.halo_srs_windows(0)
+    d_sc = torch.from_numpy(sc.view(np.int64)).cuda()
+    sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for world in (8, 3):
+        outs = torch.zeros((world, 8), dtype=torch.int64, device="cuda")
+        for r in range(world):
+            lo, hi = window_range(W, r, world)
+            assert hi > lo
+            hal.check(L.halo_msm_srs_windows_dev(0, ctypes.c_void_p(d_sc.data_ptr()), n, lo, hi,
+                                                 ctypes.c_void_p(outs[r].data_ptr()), sp))
+        hal.check(L.halo_msm_join(sp))
+        total = torch.zeros(8, dtype=torch.int64, device="cuda")
+        hal.check(L.halo_point_sum_dev(0, ctypes.c_void_p(outs.data_ptr()), world, 64, ctypes.c_void_p(total.data_ptr()),
+                                       sp))
+        torch.cuda.synchronize()
+        assert np.array_equal(total.cpu().numpy().view(np.uint64), exp), world
+    del d_sc
+
+
 @pytest.mark.parametrize("tag,fid,inverse", [("fp", 0, True), ("fq", 1, False)])
 def test_ntt_2p24_vs_c_oracle(hal, corc, tag, fid, inverse):
     L = hal.load()

@@ -1,12 +1,14 @@
 """GPU parity: pcdl::open_without_eval driven by the reference's own transcript.
 
-The device round loop (halo_amd.pcdl.open_without_eval: halo_pcdl_hiding_blind / _combine, the IPA
-session) is driven by the CPU restatement of the Poseidon PCDL sponge (oracle/poseidon.py, pinned
+The device round loop (halo_amd.pcdl.open_without_eval: halo_pcdl_open_begin / _blind / _combine /
+_start, the IPA session) is driven by the CPU restatement of the Poseidon PCDL sponge (oracle/poseidon.py, pinned
 to the reference's Kimchi / Mina vectors in tests/test_oracle.py), so every challenge -- alpha,
 xi_0 and the per-round xi -- is derived from the device's own C_bar, L and R exactly as
 pcdl.rs:326-453 derives them.  The resulting EvalProof (Ls, Rs, U, c, C_bar, w') must equal the
 committed fixture of tests/golden/make_transcript.py bit for bit (plain and hiding openings, n =
-16..1024, Pallas and Vesta, reference-recipe SRS and the reference's (S, H))."""
+16..1024, Pallas and Vesta, reference-recipe SRS and the reference's (S, H)).  The n = 4096 / 2^14
+cases ("big_*") run the device's weighted -> materialised -> tail rounds under the reference's
+transcript order (pcdl.rs:387-425); their inputs are regenerated from the stored seed."""
 import os
 
 import numpy as np
@@ -19,6 +21,7 @@ from halo_amd import group, pcdl
 pytestmark = pytest.mark.gpu
 G = np.load(os.path.join(os.path.dirname(__file__), "golden", "transcript.npz"))
 CASES = sorted({k[:-2] for k in G.files if k.startswith("open_") and k.endswith("_p")})
+BIG = sorted({k[:-5] for k in G.files if k.startswith("big_") and k.endswith("_seed")})
 
 
 class SpongeAdapter:
@@ -62,6 +65,37 @@ def test_open_without_eval_matches_transcript_fixture(hal, golden, corc, key):
         assert np.array_equal(pi["w_prime"], G[key + "_wprime_alpha"][0]), key
 
 
+def det_scalars(seed: int, k: int) -> np.ndarray:
+    """tests/golden/make_transcript.py det_scalars: k Montgomery-form scalars < 2^254 from seed."""
+    a = np.random.default_rng(seed).integers(0, 2**64 - 1, size=(k, 4), dtype=np.uint64, endpoint=True)
+    a[:, 3] &= np.uint64(0x3FFFFFFFFFFFFFFF)
+    return np.ascontiguousarray(a)
+
+
+@pytest.mark.parametrize("key", BIG)
+def test_open_without_eval_weighted_rounds_transcript(hal, golden, corc, key):
+    cname = key.split("_")[1]
+    n = int(key.split("_")[2][1:])
+    hiding = key.endswith("hiding")
+    S, Hh = golden[f"ref_sh_{cname}"]
+    group.PublicParams.upload(cname, corc.srs_generate(cname, n), S, Hh, precompute_windows=True)
+    ins = det_scalars(int(G[key + "_seed"][0]), 2 * n + 4)
+    p = ins[: n - 1]
+    z, v = G[key + "_zv"]
+    assert np.array_equal(z, ins[2 * n])
+    w = q = w_bar = None
+    if hiding:
+        q, w, w_bar = ins[n: 2 * n - 1], ins[2 * n + 1], ins[2 * n + 2]
+    pi = pcdl.open_without_eval(p, G[key + "_C"][0], n - 1, z, v, w=w, transcript=SpongeAdapter(cname), q=q,
+                                w_bar=w_bar, curve=cname)
+    assert np.array_equal(np.stack(pi["Ls"]), G[key + "_Ls"]), key
+    assert np.array_equal(np.stack(pi["Rs"]), G[key + "_Rs"]), key
+    assert np.array_equal(pi["U"], G[key + "_U"][0]) and np.array_equal(pi["c"], G[key + "_c"][0]), key
+    if hiding:
+        assert np.array_equal(pi["C_bar"], G[key + "_Cbar"][0]), key
+        assert np.array_equal(pi["w_prime"], G[key + "_wprime_alpha"][0]), key
+
+
 def test_hiding_assertions(hal, golden, corc):
     S, Hh = golden["ref_sh_pallas"]
     group.PublicParams.upload("pallas", corc.srs_generate("pallas", 64), S, Hh, precompute_windows=False)
@@ -70,3 +104,38 @@ def test_hiding_assertions(hal, golden, corc):
     with pytest.raises(AssertionError, match=r"n \(11\) is not a power of two"):
         pcdl.open_without_eval(q, np.zeros(8, dtype=np.uint64), 10, one, one, w=one, transcript=SpongeAdapter("pallas"),
                                q=q, w_bar=one)
+    # p.degree() <= d and d <= pp.D (pcdl.rs:340-341); trailing zero coefficients do not count
+    p = np.ones((9, 4), dtype=np.uint64)
+    with pytest.raises(AssertionError, match=r"p.degree\(\) <= d"):
+        pcdl.open_without_eval(p, np.zeros(8, dtype=np.uint64), 7, one, one, transcript=SpongeAdapter("pallas"))
+    with pytest.raises(AssertionError, match=r"d <= pp.D"):
+        pcdl.open_without_eval(p[:4], np.zeros(8, dtype=np.uint64), 127, one, one, transcript=SpongeAdapter("pallas"))
+    with pytest.raises(ValueError, match="transcript"):
+        pcdl.open_without_eval(p[:4], np.zeros(8, dtype=np.uint64), 7, one, one)
+
+
+def test_open_session_pool_and_srs_change(hal, golden, corc):
+    """Openings reuse pooled sessions (halo_ipa_end returns them): many openings in a row stay
+    bit-exact, device memory stays flat, and a re-uploaded SRS (new points, same length) is seen by
+    the next opening's tail table (no stale SRS-derived tables)."""
+    import torch
+    key = "open_pallas_n256_plain"
+    S, Hh = golden["ref_sh_pallas"]
+    n = 256
+    z, v = G[key + "_zv"]
+    g = corc.srs_generate("pallas", n)
+    group.PublicParams.upload("pallas", g, S, Hh, precompute_windows=True)
+    free0 = None
+    for i in range(40):
+        pi = pcdl.open_without_eval(G[key + "_p"], G[key + "_C"][0], n - 1, z, v, transcript=SpongeAdapter("pallas"))
+        assert np.array_equal(np.stack(pi["Ls"]), G[key + "_Ls"]) and np.array_equal(pi["U"], G[key + "_U"][0]), i
+        if i == 5:
+            free0 = torch.cuda.mem_get_info()[0]
+    assert torch.cuda.mem_get_info()[0] >= free0 - (64 << 20)
+    # a different SRS of the same length: the opening must follow it (U = <h, G> changes)
+    group.PublicParams.upload("pallas", np.ascontiguousarray(g[::-1]), S, Hh, precompute_windows=True)
+    pi = pcdl.open_without_eval(G[key + "_p"], G[key + "_C"][0], n - 1, z, v, transcript=SpongeAdapter("pallas"))
+    assert not np.array_equal(pi["U"], G[key + "_U"][0])
+    group.PublicParams.upload("pallas", g, S, Hh, precompute_windows=True)
+    pi = pcdl.open_without_eval(G[key + "_p"], G[key + "_C"][0], n - 1, z, v, transcript=SpongeAdapter("pallas"))
+    assert np.array_equal(pi["U"], G[key + "_U"][0])

@@ -1,0 +1,23 @@
+# Kernel timeline of the last hiding pcdl open at 2^${1:-2} (tools/pcdl_open_time.py): every kernel
+# from the last k_pbar (the blind) on, with the idle gaps between them; run through gpurun from the
+# repo root.  Output: gpurun_out/tl_open/timeline.txt
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+O=gpurun_out/tl_open_${1:-2}
+rm -rf $O && mkdir -p $O
+timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $O/t -o run -- python3 tools/pcdl_open_time.py ${1:-2} > $O/log 2>&1 || { tail -20 $O/log; exit 1; }
+f=$(find $O/t -name "*kernel_trace.csv" | head -1)
+python3 - "$f" > $O/timeline.txt <<'PY'
+import csv, sys
+rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r['Start_Timestamp']))
+ws = [r for r in rows if 'k_pbar' in r['Kernel_Name']]
+t0 = int(ws[-1]['Start_Timestamp'])
+prev_end = None
+for r in rows:
+    s = int(r['Start_Timestamp']); e = int(r['End_Timestamp'])
+    if s >= t0 - 1000000:
+        gap = (s - prev_end) / 1e3 if prev_end else 0.0
+        print(f"{(s - t0)/1e3:9.1f} {(e - t0)/1e3:9.1f} {(e - s)/1e3:8.1f} us gap {gap:7.1f} q{r.get('Queue_Id','?'):>3} {r['Kernel_Name'][:70]}")
+        prev_end = max(prev_end or 0, e)
+PY
+rm -rf $O/t
+cat $O/log
