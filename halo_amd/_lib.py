@@ -109,7 +109,7 @@ SIGNATURES = {
     "halo_ipa_round_lr_multi": [_vp, _sz, _vp, _vp],
     "halo_ipa_fold_multi": [_vp, _sz, _vp, _vp],
     "halo_ipa_begin_vectors": [ctypes.c_int, _vp, _vp, _vp, _sz, _vp, ctypes.POINTER(_vp)],
-    "halo_pcdl_open_begin": [ctypes.c_int, _vp, _sz, _sz, _vp, ctypes.POINTER(_vp)],
+    "halo_pcdl_open_begin": [ctypes.c_int, _vp, _sz, _sz, _vp, _vp, ctypes.POINTER(_vp)],
     "halo_pcdl_open_blind": [_vp, _vp, _vp, _vp],
     "halo_pcdl_open_combine": [_vp, _vp, _vp, _vp, _vp, _vp],
     "halo_pcdl_open_start": [_vp, _vp, _vp],

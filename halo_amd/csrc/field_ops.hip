@@ -211,7 +211,53 @@ __global__ __launch_bounds__(64) void k_hiding_point(const uint4* C, const uint4
     }
 }
 
+template <class Sc>
+__global__ void k_combine_scalars(uint4* p, uint4* pb, size_t n, const uint4* alpha, const uint4* w, const uint4* w_bar,
+                                  uint4* w_prime, uint4* negw) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const Fe<Sc> a = fe_from_ark<Sc>(alpha);
+    if (i < n) {
+        const Fe<Sc> t = fe_mul(a, fe_from_ark<Sc>(pb + 2 * i));
+        fe_to_ark(p + 2 * i, fe_add(fe_from_ark<Sc>(p + 2 * i), t));
+        fe_to_ark(pb + 2 * i, t);
+    }
+    if (i == 0) {
+        const Fe<Sc> wv = fe_from_ark<Sc>(w);
+        fe_to_ark(w_prime, fe_add(wv, fe_mul(a, fe_from_ark<Sc>(w_bar))));
+        fe_to_ark(negw, fe_neg(wv));
+    }
+}
+
+template <class Cv>
+__global__ void k_xyzz_add_wrapped(uint4* xyzz, const uint4* wrapped, const uint4* first_wrapped) {
+    using F = typename Cv::Base;
+    if (threadIdx.x != 0) return;
+    const XYZZ<F> a = first_wrapped ? xyzz_from_aff(aff_from_wrapped<F>(first_wrapped)) : xyzz_load<F>(xyzz);
+    xyzz_store(xyzz, xyzz_madd(a, aff_from_wrapped<F>(wrapped)));
+}
+
 }  // namespace halo
+
+int halo::pcdl_combine_scalars_device(int curve, void* p, void* p_bar, size_t n, const void* alpha, const void* w,
+                                      const void* w_bar, void* w_prime, void* negw, hipStream_t s) {
+    DISPATCH_FIELD(curve == HALO_PALLAS ? HALO_FP : HALO_FQ, Fs, {
+        hipLaunchKernelGGL(k_combine_scalars<Fs>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (uint4*)p,
+                           (uint4*)p_bar, n, (const uint4*)alpha, (const uint4*)w, (const uint4*)w_bar, (uint4*)w_prime,
+                           (uint4*)negw);
+    });
+    HALO_HIP(hipGetLastError());
+    return HALO_OK;
+}
+
+int halo::xyzz_add_wrapped_device(int curve, void* xyzz, const void* wrapped, hipStream_t s, bool from_wrapped,
+                                  const void* first_wrapped) {
+    DISPATCH_CURVE(curve, Cv, {
+        hipLaunchKernelGGL(k_xyzz_add_wrapped<Cv>, dim3(1), dim3(64), 0, s, (uint4*)xyzz, (const uint4*)wrapped,
+                           from_wrapped ? (const uint4*)first_wrapped : (const uint4*)nullptr);
+    });
+    HALO_HIP(hipGetLastError());
+    return HALO_OK;
+}
 
 int halo::pcdl_pbar_device(int curve, const void* q, size_t d, const void* z, void* p_bar, hipStream_t s) {
     const size_t n = d + 1;

@@ -391,11 +391,9 @@ __global__ __launch_bounds__(64) void k_tail_mults(size_t n0, uint4* table) {
 
 // mode 0: L/R scalars of the current round (len = 2m); mode 1: U's scalars s[k] = w[k]
 template <class Cv>
-__global__ __launch_bounds__(256) void k_tail_scalars(const uint4* cs, const uint4* w, size_t n0, size_t len, size_t m,
-                                                      int mode, uint32_t* scal, uint8_t* side) {
+HALO_DEV void tail_scalar_one(const uint4* cs, const uint4* w, size_t k, size_t len, size_t m, int mode, uint32_t* scal,
+                              uint8_t* side) {
     using S = typename Cv::Scalar;
-    const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n0) return;
     Fe<S> v;
     uint8_t sd = 0;
     if (mode == 0) {
@@ -420,18 +418,115 @@ __global__ __launch_bounds__(256) void k_tail_scalars(const uint4* cs, const uin
     side[k] = sd | (n1 ? 2 : 0) | (n2 ? 4 : 0);
 }
 
+template <class Cv>
+__global__ __launch_bounds__(256) void k_tail_scalars(const uint4* cs, const uint4* w, size_t n0, size_t len, size_t m,
+                                                      int mode, uint32_t* scal, uint8_t* side) {
+    const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < n0) tail_scalar_one<Cv>(cs, w, k, len, m, mode, scal, side);
+}
+
+// One tail round's preparation in one launch: blocks [0, nsb) form the GLV digits of the n0 L/R
+// scalars (as k_tail_scalars, mode 0); block nsb reduces the round's two dot products <c_r, z_l>,
+// <c_l, z_r> (m <= IPA_TAIL_N / 2 elements), scaled by xi_0 in xi mode, to dots_ark -- instead of
+// two dot_device reductions and k_scale_ark (five launches).
+// Lanes 0, 1 also write the GLV split of their dot (k1, k2 words and signs, 10 words per side) to hkw
+// for the hiding terms of k_tail_msm.
+template <class Cv>
+HALO_DEV void glv_split_words(const uint4* x_ark, uint32_t* out10) {
+    using S = typename Cv::Scalar;
+    uint32_t w8[8], k1[5], k2[5];
+    bool n1, n2;
+    fe_ark_to_canonical_words<S>(x_ark, w8);
+    glv::decompose<typename Cv::K>(w8, n1, k1, n2, k2);
+    for (int q = 0; q < 4; q++) {
+        out10[q] = k1[q];
+        out10[4 + q] = k2[q];
+    }
+    out10[8] = n1;
+    out10[9] = n2;
+}
+
+template <class Cv>
+__global__ __launch_bounds__(256) void k_tail_prep(const uint4* cs, const uint4* zs, const uint4* w, size_t n0, size_t len,
+                                                   size_t m, uint32_t* scal, uint8_t* side, uint32_t nsb,
+                                                   const uint4* xi0_ark, uint4* dots_ark, uint32_t* hkw) {
+    using S = typename Cv::Scalar;
+    const int tid = threadIdx.x;
+    if (blockIdx.x < nsb) {
+        const size_t k = (size_t)blockIdx.x * 256 + tid;
+        if (k < n0) tail_scalar_one<Cv>(cs, w, k, len, m, 0, scal, side);
+        return;
+    }
+    __shared__ uint4 red[2][256 * 2];
+    Fe<S> a = fe_zero<S>(), b = fe_zero<S>();
+    for (size_t i = tid; i < m; i += 256) {
+        a = fe_add(a, fe_mul(fe_from_ark<S>(cs + 2 * (m + i)), fe_from_ark<S>(zs + 2 * i)));
+        b = fe_add(b, fe_mul(fe_from_ark<S>(cs + 2 * i), fe_from_ark<S>(zs + 2 * (m + i))));
+    }
+    fe_store(red[0] + 2 * tid, a);
+    fe_store(red[1] + 2 * tid, b);
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+        if (tid < off) {
+            fe_store(red[0] + 2 * tid, fe_add(fe_load<S>(red[0] + 2 * tid), fe_load<S>(red[0] + 2 * (tid + off))));
+            fe_store(red[1] + 2 * tid, fe_add(fe_load<S>(red[1] + 2 * tid), fe_load<S>(red[1] + 2 * (tid + off))));
+        }
+        __syncthreads();
+    }
+    if (tid < 2) {
+        Fe<S> d = fe_load<S>(red[tid]);
+        if (xi0_ark) d = fe_mul(d, fe_from_ark<S>(xi0_ark));
+        fe_to_ark(dots_ark + 2 * tid, d);
+        glv_split_words<Cv>(dots_ark + 2 * tid, hkw + 10 * tid);
+    }
+}
+
+// The hiding term dot * P' of one side as lane terms: lane t < 256 returns the table entry for bit t
+// of the GLV split dot = k1 + lambda k2 (lanes 0-127: k1 with 2^t P', 128-255: k2 with phi(2^(t-128) P'))
+// or the identity.  Block-uniform call (it synchronises).
+// pre: the split already formed (glv_split_words, 10 words), else lane 0 forms it.
+template <class Cv>
+HALO_DEV XYZZ<typename Cv::Base> hiding_lane_term(const uint4* htab, const uint4* dot_ark, const uint32_t* pre,
+                                                  uint32_t (&kw)[10]) {
+    using F = typename Cv::Base;
+    const int tid = threadIdx.x;
+    if (pre) {
+        if (tid < 10) kw[tid] = pre[tid];
+    } else if (tid == 0) {
+        glv_split_words<Cv>(dot_ark, kw);
+    }
+    __syncthreads();
+    XYZZ<F> acc = xyzz_id<F>();
+    if ((kw[tid >> 5] >> (tid & 31)) & 1u) {
+        Affine<F> p = aff_load<F>(htab + 4 * (tid & 127));
+        if (tid >= 128) p.x = fe_mul(p.x, fe_from_const<F>(Cv::K::BETA));
+        if (kw[8 + (tid >> 7)]) p.y = fe_neg(p.y);
+        acc = xyzz_from_aff(p);
+    }
+    return acc;
+}
+
 // Block partial sums part[block][side].  mode 0 (L and R of a round, 2m = len): the first nbs blocks
 // take side 0's terms, the rest side 1's (each block one side: one tree, not two); the term q of a
 // side is (win, u, j) = window, fold weight, j < m, at point k = j + u 2m + side m.  mode 1 (U): terms
 // t = win n0 + k, all on side 0.
 template <class Cv>
+// With htab: side sd's first block also adds the hiding term dots[sd] * P (GLV table htab of 2^i P;
+// hkw: the dots' GLV splits when already formed) into its tree; with out_xyzz and nbs == 1 (the side
+// is one block) it writes the side's sum straight to out_xyzz + 8 sd (no k_tail_final).  Mode 1 is
+// one side of nbs blocks.
 __global__ __launch_bounds__(TAIL_THREADS) void k_tail_msm(const uint4* table, size_t ld, const uint32_t* scal,
                                                             const uint8_t* side, size_t n0, size_t m, int mode, uint32_t nbs,
-                                                            uint4* part) {
+                                                            uint4* part, const uint4* htab, const uint4* dots_ark,
+                                                            const uint32_t* hkw, uint4* out_xyzz) {
     using F = typename Cv::Base;
     __shared__ uint4 red[TAIL_THREADS / 2 * 8];
+    __shared__ uint32_t kw[10];
     const int tid = threadIdx.x;
     XYZZ<F> acc = xyzz_id<F>();
+    const uint32_t bsd = mode == 0 ? (uint32_t)(blockIdx.x >= nbs) : 0u;
+    const bool first = htab && blockIdx.x == bsd * nbs;
+    if (first) acc = hiding_lane_term<Cv>(htab, dots_ark + 2 * bsd, hkw ? hkw + 10 * bsd : nullptr, kw);
     uint32_t sd = 0;
     size_t win = 0, k = 0;
     bool valid;
@@ -454,13 +549,16 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail_msm(const uint4* table, s
         const uint32_t d = (scal[8 * k + 4 * half + bw / DPW] >> (TAIL_DB * (bw % DPW))) & (uint32_t)TAIL_MUL;
         const uint32_t sk = side[k];
         if (d) {
-            acc = xyzz_load<F>(table + tail_entry(bw, d, ld, k));
-            if (half) acc.X = fe_mul(acc.X, fe_from_const<F>(Cv::K::BETA));  // phi
-            if ((sk >> (1 + half)) & 1u) acc = xyzz_neg(acc);
+            XYZZ<F> t = xyzz_load<F>(table + tail_entry(bw, d, ld, k));
+            if (half) t.X = fe_mul(t.X, fe_from_const<F>(Cv::K::BETA));  // phi
+            if ((sk >> (1 + half)) & 1u) t = xyzz_neg(t);
+            acc = first ? xyzz_add(acc, t) : t;
         }
     }
     acc = block_group_sum<F>(acc, TAIL_THREADS, red);
-    if (tid == 0) {
+    if (out_xyzz && nbs == 1) {
+        if (tid == 0) xyzz_store(out_xyzz + 8 * bsd, acc);
+    } else if (tid == 0) {
         xyzz_store(part + 8 * (2 * (size_t)blockIdx.x + sd), acc);
         xyzz_store(part + 8 * (2 * (size_t)blockIdx.x + (sd ^ 1)), xyzz_id<F>());
     }
@@ -581,6 +679,7 @@ struct halo_ipa_session {
     bool allow_tail = false, tail = false;
     bool srs_round0 = false;  // G is still the SRS prefix (no fold yet): L/R on the resident shifted SRS
     bool gs_srs_prefix = false;  // G (length 2m) = Gs[0..2m): the tail can use the SRS's multiples table
+    bool tail_from_srs = false;  // n <= ipa_srs_tail_max(): tail rounds from round 1 over the SRS's table
     bool gs_xyzz = false;     // gs holds XYZZ points (materialised for the tail table only)
     bool gs_valid = false;    // gs holds the current G (halo_ipa_state may read it)
     bool weighted = false;    // G is never folded: L/R over the resident shifted SRS (k_weighted_scalars)
@@ -602,7 +701,7 @@ struct halo_ipa_session {
     void reset_state() {
         curve = 0;
         n = m = 0;
-        allow_tail = tail = srs_round0 = gs_srs_prefix = gs_xyzz = gs_valid = weighted = false;
+        allow_tail = tail = srs_round0 = gs_srs_prefix = tail_from_srs = gs_xyzz = gs_valid = weighted = false;
         n0 = wlen = 0;
         wcur = 0;
         table = nullptr;
@@ -894,6 +993,28 @@ static size_t ipa_tail_n() {
     return tail_n;
 }
 
+static size_t env_size(const char* name, size_t dflt) {
+    const char* e = getenv(name);
+    return e ? (size_t)atoll(e) : dflt;
+}
+// 8192 points (0.5 GB of XYZZ multiples per curve): the small MSMs up to 2^13 and the openings up to
+// 2^13 run entirely on the table (tail rounds from round 1, no weighted rounds, no materialisation)
+size_t halo::srs_tab_n() {
+    static const size_t v = env_size("HALO_SRS_TAB_N", 8192);  // A/B knob
+    return v;
+}
+size_t halo::srs_small_max() {
+    static const size_t v = std::min(env_size("HALO_SRS_SMALL_N", srs_tab_n()), srs_tab_n());  // A/B knob
+    return v;
+}
+// SRS sessions of n <= this start in the tail rounds over the SRS's table.  A tail round costs ~64 n0
+// table terms: measured per round (hiding open, tools/pcdl_open_time.py) 0.23 ms at n0 = 4096 against
+// 0.29 ms for the weighted path's average (opening 2^12: 5.95 -> 3.86 ms), but 0.33 ms at n0 = 8192,
+// where the weighted rounds are cheaper.
+static size_t ipa_srs_tail_max() {  // (read per session: the tests pin the other paths with it)
+    return std::min(env_size("HALO_IPA_SRS_TAIL_N", 4096), srs_tab_n());  // A/B knob
+}
+
 // Length at which weighted rounds materialise G = sum_u w[u] SRS[i + u len] (one batched MSM with
 // the fold weights as shared scalars, msm_shared_batch) and continue as tail rounds: a weighted
 // round costs two n/2-term MSMs whatever the length (~0.75 ms at 2^16), a tail round ~0.25 ms.
@@ -949,7 +1070,8 @@ static int ipa_h_table(DeviceState* st, int curve, const halo_wrapped_point_t* H
 //   [1280) S (internal), [1344) C' out
 constexpr size_t SM_BYTES = 2048;
 constexpr size_t SM_WBAR = 1024, SM_ALPHA = 1056, SM_W = 1088, SM_WP = 1120, SM_C = 1152, SM_CBAR = 1216, SM_S = 1280,
-                 SM_CP = 1344;
+                 SM_CP = 1344, SM_NEGW = 1408, SM_T = 1536, SM_EVAL = 1664, SM_V = 1696,  // SM_T: 128 B XYZZ
+                 SM_HKW = 1728;  // 2 x 10 words: the round's dots split by GLV (k_tail_prep)
 
 // Phase 1 of a session: G (resident SRS prefix, or explicit gs_host), c (cs_len coefficients, host or
 // device (ordered on the null stream), zero-padded to n), z = powers of z (or explicit zs_host) on the
@@ -962,7 +1084,9 @@ static int ipa_setup(DeviceState* st, halo_ipa_session* ses, int curve, size_t n
         const char* e = getenv("HALO_IPA_TAIL");
         const char* ew = getenv("HALO_IPA_WEIGHTED");  // A/B knob: 0 = fold G every round
         ses->allow_tail = !gs_host && !(e && e[0] == '0');
-        ses->weighted = !gs_host && srs.shifted_c != 0 && n > ipa_tail_n() && !(ew && ew[0] == '0');
+        ses->tail_from_srs = ses->allow_tail && n <= std::min(ipa_srs_tail_max(), srs.n);
+        ses->weighted = !gs_host && srs.shifted_c != 0 && n > ipa_tail_n() && !ses->tail_from_srs &&
+                        !(ew && ew[0] == '0');
         if (ses->weighted) ses->allow_tail = false;
         ses->srs_round0 = !gs_host && srs.shifted_c != 0 && !ses->weighted;
         ses->gs_srs_prefix = !gs_host && !ses->weighted;
@@ -971,7 +1095,7 @@ static int ipa_setup(DeviceState* st, halo_ipa_session* ses, int curve, size_t n
     ses->m = n / 2;
     hipStream_t s = ses->s;
     // an SRS session that starts in the tail rounds never reads G itself (the SRS's table does)
-    const bool need_gs = !ses->weighted && !(ses->gs_srs_prefix && ses->allow_tail && n <= ipa_tail_n());
+    const bool need_gs = !ses->weighted && !(ses->gs_srs_prefix && ses->allow_tail && (n <= ipa_tail_n() || ses->tail_from_srs));
     if (need_gs || gs_host) HALO_CHECK(ses->gs.reserve(n * 64));
     ses->gs_valid = need_gs || gs_host;
     if (ses->weighted) {  // w = [1]; scal holds the two n/2-term scalar vectors of a round
@@ -1139,6 +1263,33 @@ extern "C" int halo_ipa_begin_vectors(halo_curve_t curve, const halo_wrapped_poi
     return ipa_begin(curve, n, gs, cs, zs, nullptr, H_prime, out);
 }
 
+// v = c(z) over the session's first len coefficients (z at small[0, 32)), to the host (stream sync).
+static int ipa_eval_cs(halo_ipa_session* ses, size_t len, halo_fe_t* v_out) {
+    hipStream_t s = ses->s;
+    char* sm = ses->small.as<char>();
+    if (!len) {
+        memset(v_out, 0, 32);
+        return HALO_OK;
+    }
+    const size_t chunk = 32;
+    const int nchunks = (int)((len + chunk * RED_THREADS - 1) / (chunk * RED_THREADS));
+    HALO_CHECK(ses->tmp.reserve(std::max<size_t>(4096 * 32, (size_t)nchunks * 32)));
+    const void* tab[2] = {ses->cs.ptr, (const void*)len};  // the pointer table and length of k_eval_chunks
+    HALO_CHECK(copy_h2d(sm + SM_EVAL, tab, 16, s));
+    DISPATCH_CURVE(ses->curve, Cv, {
+        using Sc = typename Cv::Scalar;
+        hipLaunchKernelGGL(k_eval_chunks<Sc>, dim3(nchunks, 1), dim3(RED_THREADS), 0, s, (const uint4* const*)(sm + SM_EVAL),
+                           (const size_t*)(sm + SM_EVAL + 8), (const uint4*)sm, chunk, nchunks, ses->tmp.as<uint4>());
+        hipLaunchKernelGGL(k_sum_internal_to_ark<Sc>, dim3(1), dim3(RED_THREADS), 0, s, ses->tmp.as<const uint4>(),
+                           nchunks, (uint4*)(sm + SM_V));
+    });
+    HALO_HIP(hipGetLastError());
+    HALO_HIP(hipMemcpyAsync(ses->pinned, sm + SM_V, 32, hipMemcpyDeviceToHost, s));
+    HALO_HIP(hipStreamSynchronize(s));
+    memcpy(v_out, ses->pinned, 32);
+    return HALO_OK;
+}
+
 // ---------------------------------------------------------------------------------------------
 // pcdl::open_without_eval (pcdl.rs:326-392) with p, p_bar and p' kept in the session's buffers
 // (the hiding open used to download p_bar / p' and upload p, p_bar, p' between three
@@ -1151,7 +1302,7 @@ extern "C" int halo_ipa_begin_vectors(halo_curve_t curve, const halo_wrapped_poi
 //   halo_pcdl_open_start(H, xi_0)           H' = xi_0 H; then halo_ipa_round_lr / fold / end
 // ---------------------------------------------------------------------------------------------
 extern "C" int halo_pcdl_open_begin(halo_curve_t curve, const halo_fe_t* p, size_t len, size_t d, const halo_fe_t* z,
-                                    halo_ipa_session** out) {
+                                    halo_fe_t* v_out, halo_ipa_session** out) {
     clear_error();
     if (curve != HALO_PALLAS && curve != HALO_VESTA) return set_error(HALO_EINVAL, "unknown curve");
     if ((len && !p) || !z || !out) return set_error(HALO_EINVAL, "halo_pcdl_open_begin: null argument");
@@ -1170,7 +1321,8 @@ extern "C" int halo_pcdl_open_begin(halo_curve_t curve, const halo_fe_t* p, size
     if (!srs.n || d > srs.n - 1) return set_error(HALO_ESRSRANGE, "assertion failed: d <= pp.D");
     halo_ipa_session* ses = ipa_acquire(st);
     if (!ses) return HALO_EDEVICE;
-    const int rc = ipa_setup(st, ses, curve, n, nullptr, p, deg_len, false, nullptr, z);
+    int rc = ipa_setup(st, ses, curve, n, nullptr, p, deg_len, false, nullptr, z);
+    if (!rc && v_out) rc = ipa_eval_cs(ses, deg_len, v_out);  // v = p(z) (pcdl::open, pcdl.rs:471)
     if (rc) {
         ipa_release(ses);
         return rc;
@@ -1197,8 +1349,15 @@ extern "C" int halo_pcdl_open_blind(halo_ipa_session* ses, const halo_fe_t* q, c
     HALO_CHECK(copy_h2d(ses->tmp.ptr, q, d * 32, s));
     HALO_CHECK(copy_h2d(sm + SM_WBAR, w_bar, 32, s));
     HALO_CHECK(pcdl_pbar_device(ses->curve, ses->tmp.ptr, d, sm, ses->pbar.ptr, s));  // z at sm[0, 32)
-    HALO_CHECK(msm_srs_device(st, ses->curve, ses->pbar.ptr, n, sm + SM_WBAR, sm + SM_CBAR, s));
-    HALO_CHECK(copy_d2h(C_bar, sm + SM_CBAR, 64, s));
+    if (n <= std::min(srs_small_max(), srs.n)) {  // (the combine's MSM route needs no device copy of C_bar)
+        HALO_CHECK(msm_srs_small(st, ses->curve, ses->pbar.ptr, n, sm + SM_WBAR, sm + SM_T, s, true));
+        HALO_HIP(hipMemcpyAsync(ses->pinned + 128, sm + SM_T, 128, hipMemcpyDeviceToHost, s));
+        HALO_HIP(hipStreamSynchronize(s));
+        host_xyzz_to_wrapped(ses->curve, ses->pinned + 128, C_bar);
+    } else {
+        HALO_CHECK(msm_srs_device(st, ses->curve, ses->pbar.ptr, n, sm + SM_WBAR, sm + SM_CBAR, s));
+        HALO_CHECK(copy_d2h(C_bar, sm + SM_CBAR, 64, s));
+    }
     ses->blinded = true;
     return HALO_OK;
 }
@@ -1219,15 +1378,37 @@ extern "C" int halo_pcdl_open_combine(halo_ipa_session* ses, const halo_fe_t* al
     HALO_CHECK(copy_h2d(sm + SM_W, w, 32, s));
     HALO_CHECK(copy_h2d(sm + SM_C, C, 64, s));
     HALO_CHECK(copy_h2d(sm + SM_S, st->srs[ses->curve].S, 64, s));
-    // c (= p padded) += alpha p_bar in place: p' (pcdl.rs:366); C' = C + alpha C_bar - w' S, w' = w + alpha w_bar
-    HALO_CHECK(pcdl_combine_device(ses->curve, ses->cs.ptr, ses->n, ses->pbar.ptr, ses->n, sm + SM_ALPHA, sm + SM_W,
-                                   sm + SM_WBAR, sm + SM_C, sm + SM_CBAR, sm + SM_S, ses->cs.ptr, sm + SM_CP, sm + SM_WP,
-                                   s));
-    HALO_HIP(hipMemcpyAsync(ses->pinned, sm + SM_WP, 32, hipMemcpyDeviceToHost, s));
-    HALO_HIP(hipMemcpyAsync(ses->pinned + 32, sm + SM_CP, 64, hipMemcpyDeviceToHost, s));
-    HALO_HIP(hipStreamSynchronize(s));
-    memcpy(w_prime, ses->pinned, 32);
-    memcpy(C_prime, ses->pinned + 32, 64);
+    // c (= p padded) += alpha p_bar in place: p' (pcdl.rs:366); C' = C + alpha C_bar - w' S, w' = w + alpha w_bar.
+    // Up to COMBINE_MSM_MAX coefficients C' is formed as C + MSM(G, alpha p_bar) - w S (= C + alpha C_bar - w' S,
+    // since C_bar = MSM(G, p_bar) + w_bar S): an MSM (the table path, or the bucket pipeline) instead of
+    // the lone-lane scalar multiplications of k_hiding_point (~1.3 ms of dependent curve operations).
+    const SrsState& srs = st->srs[ses->curve];
+    constexpr size_t COMBINE_MSM_MAX = (size_t)1 << 16;
+    if (ses->n <= COMBINE_MSM_MAX) {
+        HALO_CHECK(pcdl_combine_scalars_device(ses->curve, ses->cs.ptr, ses->pbar.ptr, ses->n, sm + SM_ALPHA, sm + SM_W,
+                                               sm + SM_WBAR, sm + SM_WP, sm + SM_NEGW, s));
+        if (ses->n <= std::min(srs_small_max(), srs.n)) {
+            HALO_CHECK(msm_srs_small(st, ses->curve, ses->pbar.ptr, ses->n, sm + SM_NEGW, sm + SM_T, s, true));
+            HALO_CHECK(xyzz_add_wrapped_device(ses->curve, sm + SM_T, sm + SM_C, s, false));
+        } else {
+            HALO_CHECK(msm_srs_device(st, ses->curve, ses->pbar.ptr, ses->n, sm + SM_NEGW, sm + SM_CP, s));
+            HALO_CHECK(xyzz_add_wrapped_device(ses->curve, sm + SM_T, sm + SM_C, s, true, sm + SM_CP));
+        }
+        HALO_HIP(hipMemcpyAsync(ses->pinned, sm + SM_WP, 32, hipMemcpyDeviceToHost, s));
+        HALO_HIP(hipMemcpyAsync(ses->pinned + 128, sm + SM_T, 128, hipMemcpyDeviceToHost, s));
+        HALO_HIP(hipStreamSynchronize(s));
+        memcpy(w_prime, ses->pinned, 32);
+        host_xyzz_to_wrapped(ses->curve, ses->pinned + 128, C_prime);
+    } else {
+        HALO_CHECK(pcdl_combine_device(ses->curve, ses->cs.ptr, ses->n, ses->pbar.ptr, ses->n, sm + SM_ALPHA, sm + SM_W,
+                                       sm + SM_WBAR, sm + SM_C, sm + SM_CBAR, sm + SM_S, ses->cs.ptr, sm + SM_CP,
+                                       sm + SM_WP, s));
+        HALO_HIP(hipMemcpyAsync(ses->pinned, sm + SM_WP, 32, hipMemcpyDeviceToHost, s));
+        HALO_HIP(hipMemcpyAsync(ses->pinned + 32, sm + SM_CP, 64, hipMemcpyDeviceToHost, s));
+        HALO_HIP(hipStreamSynchronize(s));
+        memcpy(w_prime, ses->pinned, 32);
+        memcpy(C_prime, ses->pinned + 32, 64);
+    }
     ses->combined = true;
     return HALO_OK;
 }
@@ -1262,7 +1443,7 @@ static int ipa_enter_tail(DeviceState* st, halo_ipa_session* ses, hipStream_t s)
     HALO_CHECK(ses->part.reserve(nblk * 2 * 128));
     SrsState& srs = st->srs[ses->curve];
     static const bool srs_tab = !(getenv("HALO_IPA_SRS_TABLE") && getenv("HALO_IPA_SRS_TABLE")[0] == '0');  // A/B knob
-    if (srs_tab && ses->gs_srs_prefix && n0 <= std::min(SRS_SMALL_N, srs.n)) {
+    if (srs_tab && ses->gs_srs_prefix && n0 <= std::min(srs_tab_n(), srs.n)) {
         HALO_CHECK(srs_small_table(st, ses->curve, s));
         ses->table = srs.small_tab.as<const uint4>();
         ses->table_ld = srs.small_n0;
@@ -1290,34 +1471,49 @@ static int ipa_enter_tail(DeviceState* st, halo_ipa_session* ses, hipStream_t s)
     return HALO_OK;
 }
 
-// mode 0: L, R of the current round -> small[256..384) (with the dot * H' terms from small[128..192));
-// mode 1: U = sum_u w[u] G0[u] -> small[256..320)
+// mode 0: L, R of the current round (with their dot * H' terms) -> small[512..768) as XYZZ; the round's
+// scalars and dots come from k_tail_prep (one launch), the hiding terms ride in each side's first
+// k_tail_msm block, and k_tail_final runs only when a side spans several blocks.
+// mode 1: U = sum_u w[u] G0[u] -> small[256..384) as XYZZ (converted on the host).
 static int ipa_tail_sums(halo_ipa_session* ses, int mode, hipStream_t s) {
     const size_t n0 = ses->n0, m = ses->m;
     const size_t nbs = (TAIL_WIN * (n0 / 2) + TAIL_THREADS - 1) / TAIL_THREADS;  // mode 0: blocks per side
     const size_t nblk = mode == 0 ? 2 * nbs : (TAIL_WIN * n0 + TAIL_THREADS - 1) / TAIL_THREADS;
     char* sm = (char*)ses->small.ptr;
     DISPATCH_CURVE(ses->curve, Cv, {
-        hipLaunchKernelGGL(k_tail_scalars<Cv>, dim3(gridn(n0, 256)), dim3(256), 0, s, ses->cs.as<const uint4>(),
-                           ses->w[ses->wcur].as<const uint4>(), n0, 2 * m, m, mode, ses->scal.as<uint32_t>(),
-                           ses->side.as<uint8_t>());
+        if (mode == 0) {
+            const uint32_t nsb = gridn(n0, 256);
+            hipLaunchKernelGGL(k_tail_prep<Cv>, dim3(nsb + 1), dim3(256), 0, s, ses->cs.as<const uint4>(),
+                               ses->zs.as<const uint4>(), ses->w[ses->wcur].as<const uint4>(), n0, 2 * m, m,
+                               ses->scal.as<uint32_t>(), ses->side.as<uint8_t>(), nsb,
+                               ses->xi_mode ? (const uint4*)(sm + 192) : (const uint4*)nullptr, (uint4*)(sm + 128),
+                               (uint32_t*)(sm + SM_HKW));
+        } else {
+            hipLaunchKernelGGL(k_tail_scalars<Cv>, dim3(gridn(n0, 256)), dim3(256), 0, s, ses->cs.as<const uint4>(),
+                               ses->w[ses->wcur].as<const uint4>(), n0, 2 * m, m, mode, ses->scal.as<uint32_t>(),
+                               ses->side.as<uint8_t>());
+        }
+        const uint32_t side_blocks = (uint32_t)(mode == 0 ? nbs : nblk);
+        uint4* out = (uint4*)(sm + (mode == 0 ? 512 : 256));
         hipLaunchKernelGGL(k_tail_msm<Cv>, dim3((unsigned)nblk), dim3(TAIL_THREADS), 0, s, ses->table, ses->table_ld,
-                           ses->scal.as<const uint32_t>(), ses->side.as<const uint8_t>(), n0, m, mode, (uint32_t)nbs,
-                           ses->part.as<uint4>());
-        hipLaunchKernelGGL(k_tail_final<Cv>, dim3(mode == 0 ? 2 : 1), dim3(TAIL_THREADS), 0, s,
-                           ses->part.as<const uint4>(), (int)nblk, mode == 0 ? (const uint4*)ses->htab_ptr : nullptr,
-                           (const uint4*)(sm + 128), (uint4*)(sm + (mode == 0 ? 512 : 256)), (int)(mode == 0));
+                           ses->scal.as<const uint32_t>(), ses->side.as<const uint8_t>(), n0, m, mode, side_blocks,
+                           ses->part.as<uint4>(), mode == 0 ? (const uint4*)ses->htab_ptr : (const uint4*)nullptr,
+                           (const uint4*)(sm + 128), (const uint32_t*)(sm + SM_HKW), out);
+        if (side_blocks > 1)
+            hipLaunchKernelGGL(k_tail_final<Cv>, dim3(mode == 0 ? 2 : 1), dim3(TAIL_THREADS), 0, s,
+                               ses->part.as<const uint4>(), (int)nblk, (const uint4*)nullptr, (const uint4*)nullptr,
+                               out, 1);
     });
     HALO_HIP(hipGetLastError());
     return HALO_OK;
 }
 
-// The SRS prefix's multiples table d 2^(4 w) G_k (k < n0 = min(SRS_SMALL_N, srs.n)), built on first
+// The SRS prefix's multiples table d 2^(4 w) G_k (k < n0 = min(srs_tab_n(), srs.n)), built on first
 // use per SRS (k_tail_table + k_tail_mults on stream s; small_tab_ev marks its completion for other
 // streams).  SrsState::invalidate_derived() (every writer of the SRS points) forces a rebuild.
 int halo::srs_small_table(DeviceState* st, int curve, hipStream_t s) {
     SrsState& srs = st->srs[curve];
-    const size_t n0 = std::min(SRS_SMALL_N, srs.n);
+    const size_t n0 = std::min(srs_tab_n(), srs.n);
     if (!n0) return set_error(HALO_ESRSRANGE, "no resident SRS: call halo_srs_upload first");
     if (!srs.small_tab_ev) HALO_HIP(hipEventCreateWithFlags(&srs.small_tab_ev, hipEventDisableTiming));
     if (srs.small_n0 == n0) {
@@ -1342,9 +1538,9 @@ int halo::srs_small_table(DeviceState* st, int curve, hipStream_t s) {
 // with the SRS's multiples table (leading dimension small_n0 >= n); mode 1 of k_tail_scalars /
 // k_tail_msm gives sum_k s[k] G0[k] (64 n table terms), k_tail_final adds w S from the 2^i S table.
 int halo::msm_srs_small(DeviceState* st, int curve, const void* scalars_ark, size_t n, const void* hide_scalar,
-                  void* d_out_wrapped, hipStream_t s) {
+                  void* d_out_wrapped, hipStream_t s, bool out_xyzz) {
     SrsState& srs = st->srs[curve];
-    const size_t nmax = std::min(SRS_SMALL_N, srs.n);
+    const size_t nmax = std::min(srs_small_max(), srs.n);
     if (n < 1 || n > nmax) return set_error(HALO_EINVAL, "small SRS MSM: n (%zu) outside [1, %zu]", n, nmax);
     const size_t nblk = (TAIL_WIN * n + TAIL_THREADS - 1) / TAIL_THREADS;
     // scratch: GLV words (n x 32 B) | sides (n B, 256-B aligned) | partials
@@ -1357,12 +1553,17 @@ int halo::msm_srs_small(DeviceState* st, int curve, const void* scalars_ark, siz
     DISPATCH_CURVE(curve, Cv, {
         hipLaunchKernelGGL(k_tail_scalars<Cv>, dim3(gridn(n, 256)), dim3(256), 0, s, (const uint4*)nullptr,
                            (const uint4*)scalars_ark, n, (size_t)1, (size_t)0, 1, (uint32_t*)scr, (uint8_t*)(scr + o_side));
+        // the hiding term w S rides in block 0 (2^i S table); one block and an XYZZ result: no k_tail_final
+        const bool direct = out_xyzz && nblk == 1;
         hipLaunchKernelGGL(k_tail_msm<Cv>, dim3((unsigned)nblk), dim3(TAIL_THREADS), 0, s,
                            srs.small_tab.as<const uint4>(), srs.small_n0, (const uint32_t*)scr,
-                           (const uint8_t*)(scr + o_side), n, (size_t)0, 1, 0u, (uint4*)(scr + o_part));
-        hipLaunchKernelGGL(k_tail_final<Cv>, dim3(1), dim3(TAIL_THREADS), 0, s, (const uint4*)(scr + o_part), (int)nblk,
-                           hide_scalar ? srs.s_table.as<const uint4>() : (const uint4*)nullptr,
-                           (const uint4*)hide_scalar, (uint4*)d_out_wrapped, 0);
+                           (const uint8_t*)(scr + o_side), n, (size_t)0, 1, (uint32_t)nblk, (uint4*)(scr + o_part),
+                           hide_scalar ? srs.s_table.as<const uint4>() : (const uint4*)nullptr, (const uint4*)hide_scalar,
+                           (const uint32_t*)nullptr, direct ? (uint4*)d_out_wrapped : (uint4*)nullptr);
+        if (!direct)
+            hipLaunchKernelGGL(k_tail_final<Cv>, dim3(1), dim3(TAIL_THREADS), 0, s, (const uint4*)(scr + o_part),
+                               (int)nblk, (const uint4*)nullptr, (const uint4*)nullptr, (uint4*)d_out_wrapped,
+                               (int)out_xyzz);
     });
     HALO_HIP(hipGetLastError());
     HALO_HIP(hipEventRecord(srs.small_ev, s));
@@ -1403,13 +1604,18 @@ static int ipa_round_launch(DeviceState* st, halo_ipa_session* ses) {
         ses->gs_srs_prefix = false;
         ses->weighted = false;
     }
-    if (!ses->tail && ses->allow_tail && 2 * m <= ipa_tail_n()) HALO_CHECK(ipa_enter_tail(st, ses, s));
+    if (!ses->tail && ses->allow_tail && (2 * m <= ipa_tail_n() || ses->tail_from_srs)) HALO_CHECK(ipa_enter_tail(st, ses, s));
     const char* gs = ses->gs.as<const char>();  // (materialised above in a weighted session)
     // only round 1 orders its hiding terms after the side-stream table: every later round starts after
     // the host has synchronised on round 1's results, which needed the table (a cross-stream wait in
     // every round cost ~0.3 ms per 2^16 round)
     hipEvent_t hr = ses->htab_waited ? nullptr : ses->htab_ready;
     ses->htab_waited = true;
+    if (ses->tail) {  // k_tail_prep forms the dots (scaled by xi_0) with the round's scalars
+        if (hr) HALO_HIP(hipStreamWaitEvent(s, hr, 0));
+        HALO_CHECK(ipa_tail_sums(ses, 0, s));
+        return ipa_copy_out(ses);
+    }
     HALO_CHECK(dot_device(sf, cs + m * 32, zs, m, sm + 128, ses->tmp.ptr, s));        // <c_r, z_l>
     HALO_CHECK(dot_device(sf, cs, zs + m * 32, m, sm + 160, ses->tmp.ptr, s));        // <c_l, z_r>
     if (ses->xi_mode) {  // dot H' = (dot xi_0) H
@@ -1419,10 +1625,7 @@ static int ipa_round_launch(DeviceState* st, halo_ipa_session* ses) {
         });
         HALO_HIP(hipGetLastError());
     }
-    if (ses->tail) {
-        if (hr) HALO_HIP(hipStreamWaitEvent(s, hr, 0));
-        HALO_CHECK(ipa_tail_sums(ses, 0, s));
-    } else if (ses->weighted) {
+    if (ses->weighted) {
         const size_t half = ses->n0 / 2;  // = wlen * m terms per side
         const uint32_t lgm = ilog2(m);
         const char* sl = cs + m * 32;     // round 0 (w = [1]): the scalars are c_r, c_l themselves
@@ -1538,8 +1741,9 @@ extern "C" int halo_ipa_round_lr_multi(halo_ipa_session* const* ses, size_t k, h
     for (size_t i = 0; i < k; i++) {
         HALO_HIP(hipStreamSynchronize(ses[i]->s));
         ses[i]->fold_inflight = false;
-        host_xyzz_to_wrapped(ses[i]->curve, ses[i]->pinned + 256, &L[i]);
-        host_xyzz_to_wrapped(ses[i]->curve, ses[i]->pinned + 384, &R[i]);
+        const void* src[2] = {ses[i]->pinned + 256, ses[i]->pinned + 384};
+        void* dst[2] = {&L[i], &R[i]};
+        host_xyzz_to_wrapped2(ses[i]->curve, src, dst, 2);
     }
     return HALO_OK;
 }
@@ -1610,11 +1814,11 @@ extern "C" int halo_ipa_end(halo_ipa_session* ses, halo_wrapped_point_t* U, halo
                 rc = set_error(HALO_EINVAL, "halo_ipa_end: U needs every round in the weighted / tail rounds (m = %zu)",
                                ses->m);
             else if (ses->tail)
-                rc = ipa_tail_sums(ses, 1, s);
+                rc = ipa_tail_sums(ses, 1, s);  // XYZZ at [256, 384), converted below
             else
                 rc = msm_srs_range_device(st, ses->curve, 0, ses->w[ses->wcur].ptr, ses->n0, nullptr, nullptr, sm + 256,
                                           s, false);
-            if (!rc && hipMemcpyAsync(sm + 320, ses->cs.ptr, 32, hipMemcpyDeviceToDevice, s) != hipSuccess)
+            if (!rc && !ses->tail && hipMemcpyAsync(sm + 320, ses->cs.ptr, 32, hipMemcpyDeviceToDevice, s) != hipSuccess)
                 rc = set_error(HALO_EDEVICE, "ipa end copy failed");
         } else if ((rc = ipa_ensure_gs(st, ses))) {
         } else {
@@ -1624,12 +1828,20 @@ extern "C" int halo_ipa_end(halo_ipa_session* ses, halo_wrapped_point_t* U, halo
             });
             if (hipGetLastError() != hipSuccess) rc = set_error(HALO_EDEVICE, "ipa end launch failed");
         }
-        // U | c are contiguous: one copy through the pinned staging
-        if (!rc && hipMemcpyAsync(ses->pinned + 256, sm + 256, 96, hipMemcpyDeviceToHost, s) != hipSuccess)
+        // one copy through the pinned staging: U (wrapped, or XYZZ [256, 384) after tail rounds), c
+        const bool u_xyzz = ses->tail;
+        if (!rc && u_xyzz && hipMemcpyAsync(sm + 384, ses->cs.ptr, 32, hipMemcpyDeviceToDevice, s) != hipSuccess)
+            rc = set_error(HALO_EDEVICE, "ipa end copy failed");
+        if (!rc && hipMemcpyAsync(ses->pinned + 256, sm + 256, u_xyzz ? 160 : 96, hipMemcpyDeviceToHost, s) != hipSuccess)
             rc = set_error(HALO_EDEVICE, "ipa end copy failed");
         if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = set_error(HALO_EDEVICE, "ipa end synchronisation failed");
-        if (!rc && U) memcpy(U, ses->pinned + 256, 64);
-        if (!rc && c) memcpy(c, ses->pinned + 320, 32);
+        if (!rc && U) {
+            if (u_xyzz)
+                host_xyzz_to_wrapped(ses->curve, ses->pinned + 256, U);
+            else
+                memcpy(U, ses->pinned + 256, 64);
+        }
+        if (!rc && c) memcpy(c, ses->pinned + (u_xyzz ? 384 : 320), 32);
     }
     ipa_release(ses);
     return rc;

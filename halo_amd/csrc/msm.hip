@@ -1038,7 +1038,7 @@ int msm_srs_device(DeviceState* st, int curve, const void* scalars_ark, size_t n
         const char* e = getenv("HALO_SRS_SMALL");
         return e && e[0] == '0';
     }();
-    if (!async && !small_off && n >= 1 && n <= SRS_SMALL_N)
+    if (!async && !small_off && n >= 1 && n <= srs_small_max())
         return msm_srs_small(st, curve, scalars_ark, n, hide_scalar, d_out_wrapped, s);
     int rc;
     // the shifted copies hold W windows of srs.n points each; an MSM of n <= srs.n points uses the
@@ -1394,7 +1394,57 @@ void host_xyzz_to_wrapped_t(const void* xyzz, void* wrapped) {
         out[4 + i] = y[i];
     }
 }
+// k points with one inversion (Montgomery's trick over the ZZ ZZZ products; k <= 16)
+template <class F>
+void host_xyzz_to_wrapped2_t(const void* const* xyzz, void* const* wrapped, int k) {
+    static const HostMont M(F::MODULUS64);
+    uint64_t m[16][4][4], t[16][4], pre[17][4];
+    bool id[16];
+    for (int j = 0; j < 4; j++) pre[0][j] = M.one[j];
+    for (int i = 0; i < k; i++) {
+        const uint64_t* q = (const uint64_t*)xyzz[i];
+        uint64_t c[4][4];
+        for (int a = 0; a < 4; a++) {
+            for (int j = 0; j < 4; j++) c[a][j] = q[4 * a + j];
+            if (M.geq_p(c[a])) M.sub_p(c[a]);
+        }
+        id[i] = !(c[2][0] | c[2][1] | c[2][2] | c[2][3]);
+        for (int a = 0; a < 4; a++) M.mul(c[a], M.r2, m[i][a]);
+        if (id[i])
+            for (int j = 0; j < 4; j++) t[i][j] = M.one[j];
+        else
+            M.mul(m[i][2], m[i][3], t[i]);
+        M.mul(pre[i], t[i], pre[i + 1]);
+    }
+    uint64_t inv[4];
+    M.inv(pre[k], inv);  // (prod_i ZZ_i ZZZ_i)^-1
+    for (int i = k - 1; i >= 0; i--) {
+        uint64_t iv[4], u[4], x[4], y[4];
+        M.mul(inv, pre[i], iv);  // (ZZ_i ZZZ_i)^-1
+        M.mul(inv, t[i], inv);
+        uint64_t* out = (uint64_t*)wrapped[i];
+        if (id[i]) {
+            for (int j = 0; j < 8; j++) out[j] = 0;
+            continue;
+        }
+        M.mul(m[i][0], m[i][3], u);
+        M.mul(u, iv, x);
+        M.mul(m[i][1], m[i][2], u);
+        M.mul(u, iv, y);
+        for (int j = 0; j < 4; j++) {
+            out[j] = x[j];
+            out[4 + j] = y[j];
+        }
+    }
+}
 }  // namespace
+
+void host_xyzz_to_wrapped2(int curve, const void* const* xyzz, void* const* wrapped, int k) {
+    if (curve == HALO_PALLAS)
+        host_xyzz_to_wrapped2_t<PallasCurve::Base>(xyzz, wrapped, k);
+    else
+        host_xyzz_to_wrapped2_t<VestaCurve::Base>(xyzz, wrapped, k);
+}
 
 void host_xyzz_to_wrapped(int curve, const void* xyzz, void* wrapped) {
     if (curve == HALO_PALLAS)

@@ -63,17 +63,19 @@ int msm_srs_pairs_device(DeviceState* st, int curve, size_t np, const MsmPairIO*
 int msm_shared_batch(DeviceState* st, int curve, const void* bases_int, const void* w_ark, size_t T, size_t len,
                      void* out, bool xyzz_out, BatchScratch& S, hipStream_t s, size_t shift_stride = 0, int c_s = 0);
 int srs_precompute_windows(DeviceState* st, int curve, hipStream_t s);
-// Small MSM over the resident SRS prefix (1 <= n <= SRS_SMALL_N, ipa.hip): every (point, 4-bit GLV
+// Small MSM over the resident SRS prefix (1 <= n <= srs_small_max(), ipa.hip): every (point, 4-bit GLV
 // window) term is one entry of a per-SRS multiples table, then block trees with the hiding term
 // hide_scalar * S from the 2^i S table -- no sort, buckets or bucket reduction.  Stream-ordered on s;
 // writes one ark WrappedPoint to d_out_wrapped.
-constexpr size_t SRS_SMALL_N = 2048;
+size_t srs_tab_n();      // points covered by the SRS multiples table (HALO_SRS_TAB_N, default 8192)
+size_t srs_small_max();  // largest MSM on the table path (HALO_SRS_SMALL_N, default srs_tab_n())
 // The multiples table of the SRS prefix (SrsState::small_tab, built on first use over
-// min(SRS_SMALL_N, srs.n) points); stream s waits for its completion.  Shared by the small MSMs and
+// min(srs_tab_n(), srs.n) points); stream s waits for its completion.  Shared by the small MSMs and
 // by IPA sessions whose tail rounds start on the unfolded SRS prefix.
 int srs_small_table(DeviceState* st, int curve, hipStream_t s);
+// out_xyzz: the result as 128 B packed XYZZ (host_xyzz_to_wrapped) instead of a WrappedPoint.
 int msm_srs_small(DeviceState* st, int curve, const void* scalars_ark, size_t n, const void* hide_scalar,
-                  void* d_out_wrapped, hipStream_t s);
+                  void* d_out_wrapped, hipStream_t s, bool out_xyzz = false);
 // The hiding branch of pcdl::open_without_eval on device buffers (field_ops.hip), stream-ordered on s:
 // p_bar = (X - z) q (q: d ark coefficients, z: ark scalar) -> d + 1 ark coefficients;
 // p' = p (len coefficients, zero-padded to n) + alpha p_bar (p' may alias p), w' = w + alpha w_bar,
@@ -82,9 +84,18 @@ int pcdl_pbar_device(int curve, const void* q, size_t d, const void* z, void* p_
 int pcdl_combine_device(int curve, const void* p, size_t len, const void* p_bar, size_t n, const void* alpha,
                         const void* w, const void* w_bar, const void* C, const void* C_bar, const void* S_int,
                         void* p_prime, void* C_prime, void* w_prime, hipStream_t s);
+// p[i] += alpha p_bar[i] and p_bar[i] = alpha p_bar[i] in place (i < n); w' = w + alpha w_bar, negw = -w.
+int pcdl_combine_scalars_device(int curve, void* p, void* p_bar, size_t n, const void* alpha, const void* w,
+                                const void* w_bar, void* w_prime, void* negw, hipStream_t s);
+// xyzz (128 B packed XYZZ) = xyzz (or, from_wrapped, the WrappedPoint first_wrapped) + the WrappedPoint
+// at wrapped (one lane).
+int xyzz_add_wrapped_device(int curve, void* xyzz, const void* wrapped, hipStream_t s, bool from_wrapped = false,
+                            const void* first_wrapped = nullptr);
 // Host conversion of a 128-B packed XYZZ point (internal format, each coordinate < 2p) to an ark
 // WrappedPoint: one inversion in 4 x 64-bit Montgomery arithmetic on the CPU (identity -> (0, 0)).
 void host_xyzz_to_wrapped(int curve, const void* xyzz, void* wrapped);
+// k <= 16 points at once with one inversion (Montgomery's trick)
+void host_xyzz_to_wrapped2(int curve, const void* const* xyzz, void* const* wrapped, int k);
 int convert_wrapped_to_internal(int curve, const void* in, void* out, size_t n, hipStream_t s);
 int convert_internal_to_wrapped(int curve, const void* in, void* out, size_t n, hipStream_t s);
 int ntt_device_dispatch(DeviceState* st, int field, const void* d_in, void* d_out, void* d_tmp, unsigned logn,

@@ -154,11 +154,16 @@ def open_without_eval(p, C, d: int, z, v, w=None, transcript=None, q=None, w_bar
     cid = _curve(curve)
     n = d + 1
     p = H.fe_array(p) if len(p) else np.zeros((0, 4), dtype=np.uint64)
-    zz, vv = H.fe_array(z, 1)[0], H.fe_array(v, 1)[0]
+    zz = H.fe_array(z, 1)[0]
+    vv = H.fe_array(v, 1)[0] if v is not None else None
     C = H.point_array(C).reshape(8)
     s = ctypes.c_void_p()
     # asserts n > 1, n a power of two, p.degree() <= d, d <= D (pcdl.rs:338-341)
-    H.check(L.halo_pcdl_open_begin(cid, H.ptr(p) if len(p) else None, len(p), d, H.ptr(zz), ctypes.byref(s)))
+    v_out = np.zeros(4, dtype=np.uint64) if v is None else None  # pcdl::open: v = p(z) on the device
+    H.check(L.halo_pcdl_open_begin(cid, H.ptr(p) if len(p) else None, len(p), d, H.ptr(zz), H.ptr(v_out),
+                                   ctypes.byref(s)))
+    if v is None:
+        vv = v_out
     ses = IpaSession.__new__(IpaSession)
     ses.curve, ses.n, ses._s = cid, n, s
     try:
@@ -193,7 +198,7 @@ def open_without_eval(p, C, d: int, z, v, w=None, transcript=None, q=None, w_bar
         if ses._s is not None:  # an assertion or error above: return the session to the pool
             L.halo_ipa_end(ses._s, None, None)
             ses._s = None
-    return {"Ls": Ls, "Rs": Rs, "U": U, "c": c, "C_bar": C_bar, "w_prime": w_prime}
+    return {"Ls": Ls, "Rs": Rs, "U": U, "c": c, "C_bar": C_bar, "w_prime": w_prime, "v": vv}
 
 
 class StandInTranscript:
@@ -237,11 +242,9 @@ def evaluate(p, z, curve="pallas") -> np.ndarray:
 
 
 def open(p, C, d: int, z, w=None, transcript=None, q=None, w_bar=None, curve="pallas") -> dict:  # noqa: A001
-    """pcdl::open (pcdl.rs:463-473): v = p(z), then open_without_eval."""
-    v = evaluate(p, z, curve)
-    pi = open_without_eval(p, C, d, z, v, w=w, transcript=transcript, q=q, w_bar=w_bar, curve=curve)
-    pi["v"] = v
-    return pi
+    """pcdl::open (pcdl.rs:463-473): v = p(z) (evaluated on the device inside the session start,
+    halo_pcdl_open_begin), then open_without_eval.  The EvalProof dict carries v."""
+    return open_without_eval(p, C, d, z, None, w=w, transcript=transcript, q=q, w_bar=w_bar, curve=curve)
 
 
 class HPoly:

@@ -307,7 +307,8 @@ int halo_ipa_begin_vectors(halo_curve_t curve, const halo_wrapped_point_t* gs, c
  * and p' never leave the device; the caller keeps the transcript between the steps, as the
  * reference does:
  *   halo_pcdl_open_begin(p: len coefficients, d, z)    n = d + 1 > 1 a power of two, p.degree() <= d,
- *                                                      d <= D (pcdl.rs:338-341); c = p padded to n
+ *                                                      d <= D (pcdl.rs:338-341); c = p padded to n;
+ *                                                      v_out (optional) = p(z), pcdl::open's evaluation (pcdl.rs:471)
  *   hiding (w = Some):
  *     halo_pcdl_open_blind(q: d coefficients, w_bar) -> C_bar       p_bar = (X - z) q,
  *                                                      C_bar = pcdl::commit(p_bar, d, w_bar) (pcdl.rs:344-355)
@@ -320,7 +321,7 @@ int halo_ipa_begin_vectors(halo_curve_t curve, const halo_wrapped_point_t* gs, c
  * followed by halo_ipa_round_lr / halo_ipa_fold / halo_ipa_end as for the other sessions.  The
  * rounds refuse a session that was not started. */
 int halo_pcdl_open_begin(halo_curve_t curve, const halo_fe_t* p, size_t len, size_t d, const halo_fe_t* z,
-                         halo_ipa_session** out);
+                         halo_fe_t* v_out, halo_ipa_session** out);
 int halo_pcdl_open_blind(halo_ipa_session* s, const halo_fe_t* q, const halo_fe_t* w_bar, halo_wrapped_point_t* C_bar);
 int halo_pcdl_open_combine(halo_ipa_session* s, const halo_fe_t* alpha, const halo_wrapped_point_t* C,
                            const halo_fe_t* w, halo_fe_t* w_prime, halo_wrapped_point_t* C_prime);

@@ -121,6 +121,7 @@ def test_permutation_accumulator_scan_large(hal):
     ("pallas", 12, "fold"), ("pallas", 13, "fold"), ("pallas", 13, "fold_srs_round0"),
     ("pallas", 12, "weighted"), ("pallas", 14, "weighted"), ("vesta", 13, "weighted"),
     ("pallas", 13, "weighted_to_end"), ("pallas", 15, "weighted"), ("pallas", 12, "weighted_fold_after"),
+    ("pallas", 13, "srs_tail"), ("vesta", 12, "srs_tail"),
 ])
 def test_ipa_open_tail_switch_vs_c_restatement(hal, monkeypatch, curve, logn, mode):
     """An SRS-based opening longer than the tail threshold (2048), against the C restatement of
@@ -130,7 +131,8 @@ def test_ipa_open_tail_switch_vs_c_restatement(hal, monkeypatch, curve, logn, mo
     with the shifted SRS): G is never folded, every round's L / R are block-mapped MSMs over the
     shifted SRS with scalars c * w until the length reaches 1024, where G is materialised by one
     batched shared-scalar MSM and the tail rounds finish; weighted_to_end: no switch, U = sum w[u] G[u]
-    at the end; weighted_fold_after: the materialised G continues with ordinary rounds."""
+    at the end; weighted_fold_after: the materialised G continues with ordinary rounds; srs_tail:
+    every round a tail round over the SRS's own multiples table (no weighted rounds, no materialised G)."""
     from prover_ref import CRefBackend
 
     n = 1 << logn
@@ -140,6 +142,9 @@ def test_ipa_open_tail_switch_vs_c_restatement(hal, monkeypatch, curve, logn, mo
     if mode != "fold":
         hal.check(L.halo_srs_precompute_windows(cid))
     monkeypatch.setenv("HALO_IPA_WEIGHTED", "1" if mode.startswith("weighted") else "0")
+    # srs_tail (the default up to 2^13): tail rounds from round 1 over the SRS's multiples table; the
+    # other modes pin the weighted / fold paths at these sizes
+    monkeypatch.setenv("HALO_IPA_SRS_TAIL_N", str(n) if mode == "srs_tail" else "0")
     if mode == "weighted_to_end":  # no switch to the tail rounds: U = sum w[u] G[u] over the SRS
         monkeypatch.setenv("HALO_IPA_MAT_N", "0")
     if mode == "weighted_fold_after":  # materialised G (affine) continues with L/R MSMs + GLV folds

@@ -55,8 +55,13 @@ def test_open_without_eval_matches_transcript_fixture(hal, golden, corc, key):
     if hiding:
         w, w_bar = G[key + "_w"]
         q = G[key + "_q"]
-    pi = pcdl.open_without_eval(G[key + "_p"], G[key + "_C"][0], n - 1, z, v, w=w, transcript=SpongeAdapter(cname),
-                                q=q, w_bar=w_bar, curve=cname)
+    if hiding:  # pcdl::open (pcdl.rs:463-473): v = p(z) formed on the device at the session start
+        pi = pcdl.open(G[key + "_p"], G[key + "_C"][0], n - 1, z, w=w, transcript=SpongeAdapter(cname), q=q,
+                       w_bar=w_bar, curve=cname)
+        assert np.array_equal(pi["v"], v), key
+    else:
+        pi = pcdl.open_without_eval(G[key + "_p"], G[key + "_C"][0], n - 1, z, v, w=w,
+                                    transcript=SpongeAdapter(cname), q=q, w_bar=w_bar, curve=cname)
     assert np.array_equal(np.stack(pi["Ls"]), G[key + "_Ls"]), key
     assert np.array_equal(np.stack(pi["Rs"]), G[key + "_Rs"]), key
     assert np.array_equal(pi["U"], G[key + "_U"][0]) and np.array_equal(pi["c"], G[key + "_c"][0]), key
