@@ -87,6 +87,7 @@ SIGNATURES = {
     "halo_ntt_dev_zero_tail": [ctypes.c_int, _vp, ctypes.c_uint, _sz, _sz, _vp],
     "halo_hpoly_coeffs": [ctypes.c_int, _vp, _sz, _vp],
     "halo_hpoly_combine": [ctypes.c_int, _vp, _sz, _sz, _vp, _vp, ctypes.POINTER(_sz)],
+    "halo_hpoly_combine_dev": [ctypes.c_int, _vp, _sz, _sz, _vp, _vp, _vp],
     "halo_pcdl_decider_commit": [ctypes.c_int, _vp, _sz, _sz, _vp],
     "halo_trace_commit_batch": [ctypes.c_int, _vp, _sz, ctypes.c_uint, _sz, _vp, _vp, _vp],
     "halo_srs_load_bincode": [ctypes.c_int, _vp, _vp, _sz, _vp, _sz, _sz],
@@ -95,6 +96,7 @@ SIGNATURES = {
     "halo_divide_by_vanishing": [ctypes.c_int, _vp, _sz, _sz, _vp, ctypes.POINTER(_sz), _vp, ctypes.POINTER(_sz)],
     "halo_divide_by_vanishing_dev": [ctypes.c_int, _vp, _sz, _sz, _vp, _vp, _vp],
     "halo_evals_scan_dev": [ctypes.c_int, ctypes.c_int, _vp, _vp, _sz, _vp],
+    "halo_poly_lincomb_dev": [ctypes.c_int, _vp, _vp, _sz, _vp, _vp, _sz, _vp],
     "halo_gate_constraints_dev": [ctypes.c_int, _vp, _vp, _vp, _vp, _vp, _sz, ctypes.c_uint, _vp, _vp],
     "halo_ntt_twiddle_dev": [ctypes.c_int, _vp, ctypes.c_uint, _sz, _sz, _sz, _sz, ctypes.c_int, _vp],
     "halo_transpose_dev": [_vp, _vp, _sz, _sz, _sz, _sz, _vp],

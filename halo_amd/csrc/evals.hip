@@ -365,9 +365,63 @@ static int check_evals_args(halo_field_t field, int op, const void* a, const voi
     return HALO_OK;
 }
 
+// sum_i zeta^i p_i over k <= LINCOMB_MAX coefficient vectors of lengths len_i (missing coefficients
+// are zero): per element a Horner pass over the k inputs in the raw ark domain -- fe_mul by an
+// internal-form constant is value-preserving on ark words -- so each input is read once and the
+// result written once (protocol.rs:542-548's geometric combinations: one launch instead of 2k
+// elementwise scale / add launches and k temporaries).
+constexpr int LINCOMB_MAX = 64;
+struct LincombArgs {
+    const uint4* p[LINCOMB_MAX];
+    uint32_t len[LINCOMB_MAX];
+};
+template <class F>
+__global__ __launch_bounds__(256) void k_lincomb(const LincombArgs a, uint32_t k, uint4 z0, uint4 z1, size_t n_out,
+                                                 uint4* out) {
+    const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n_out) return;
+    const uint4 zw[2] = {z0, z1};
+    const Fe<F> z = fe_from_ark<F>(zw);
+    Fe<F> acc = fe_zero<F>();
+    for (int j = (int)k - 1; j >= 0; j--) {
+        acc = fe_mul(acc, z);
+        if (e < a.len[j]) acc = fe_add(acc, fe_load<F>(a.p[j] + 2 * e));  // raw ark words (< p)
+    }
+    fe_store(out + 2 * e, fe_canon(acc));
+}
+
 }  // namespace halo
 
 using namespace halo;
+
+extern "C" int halo_poly_lincomb_dev(halo_field_t field, const void* const* d_polys, const size_t* lens, size_t k,
+                                     const halo_fe_t* zeta, void* d_out, size_t n_out, void* stream) {
+    clear_error();
+    if (field != HALO_FP && field != HALO_FQ) return set_error(HALO_EINVAL, "unknown field id %d", (int)field);
+    if (k > LINCOMB_MAX) return set_error(HALO_EINVAL, "halo_poly_lincomb_dev: k = %zu > %d", k, LINCOMB_MAX);
+    if (!zeta || (n_out && !d_out) || (k && (!d_polys || !lens)))
+        return set_error(HALO_EINVAL, "halo_poly_lincomb_dev: null argument");
+    if (!n_out) return HALO_OK;
+    LincombArgs a;
+    for (size_t j = 0; j < k; j++) {
+        if (lens[j] > 0xffffffffu || (lens[j] && !d_polys[j]))
+            return set_error(HALO_EINVAL, "halo_poly_lincomb_dev: bad polynomial %zu", j);
+        a.p[j] = (const uint4*)d_polys[j];
+        a.len[j] = (uint32_t)lens[j];
+    }
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    const uint4 z0 = make_uint4((uint32_t)zeta->l[0], (uint32_t)(zeta->l[0] >> 32), (uint32_t)zeta->l[1],
+                                (uint32_t)(zeta->l[1] >> 32));
+    const uint4 z1 = make_uint4((uint32_t)zeta->l[2], (uint32_t)(zeta->l[2] >> 32), (uint32_t)zeta->l[3],
+                                (uint32_t)(zeta->l[3] >> 32));
+    DISPATCH_FIELD(field, F, {
+        hipLaunchKernelGGL(k_lincomb<F>, dim3((unsigned)((n_out + 255) / 256)), dim3(256), 0, (hipStream_t)stream, a,
+                           (uint32_t)k, z0, z1, n_out, (uint4*)d_out);
+    });
+    HALO_HIP(hipGetLastError());
+    return HALO_OK;
+}
 
 extern "C" int halo_evals_op_dev(halo_field_t field, int op, const void* d_a, const void* d_b, const halo_fe_t* scalar,
                                  uint32_t exponent, void* d_out, size_t n, void* stream) {

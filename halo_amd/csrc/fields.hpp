@@ -25,6 +25,14 @@
 
 #include "consts.hpp"
 
+// Default build: every column of a product is ONE inline-asm v_mad_u64_u32 chain (mad_chain.hpp,
+// HALO_MAD_COL).  HALO_MAD_ILP (latency-bound tail kernels) and HALO_MAD_C: the plain C expression,
+// which the compiler splits into parallel partial sums.
+#if !defined(HALO_MAD_ILP) && !defined(HALO_MAD_C) && !defined(HALO_MAD_PER_PRODUCT)
+#define HALO_MAD_COL 1
+#include "mad_chain.hpp"
+#endif
+
 // Arithmetic namespace: translation units compiled with HALO_MAD_ILP (latency-bound kernels, see
 // msm_tail.hip) get the same code in the inline namespace halo::ilp with split column sums.
 #ifdef HALO_MAD_ILP
@@ -45,7 +53,7 @@ HALO_ARITH_BEGIN
 // chain form issues ~12% fewer VALU instructions per multiplication and is ~10% faster
 // (tools/micro/fe_mul_bench.hip); latency-bound single-wave code loses a little.
 HALO_DEV uint64_t mad_acc(uint32_t a, uint32_t b, uint64_t c) {
-#ifdef HALO_MAD_ILP
+#if defined(HALO_MAD_ILP) || defined(HALO_MAD_C)
     return (uint64_t)a * b + c;
 #else
     uint64_t d, cc;
@@ -56,7 +64,7 @@ HALO_DEV uint64_t mad_acc(uint32_t a, uint32_t b, uint64_t c) {
 // acc + a * K for a compile-time constant K (SGPR operand)
 template <uint32_t K>
 HALO_DEV uint64_t mad_acc_k(uint32_t a, uint64_t c) {
-#ifdef HALO_MAD_ILP
+#if defined(HALO_MAD_ILP) || defined(HALO_MAD_C)
     return (uint64_t)a * K + c;
 #else
     uint64_t d, cc;
@@ -159,6 +167,162 @@ HALO_DEV uint64_t fe_reduce_col(const uint32_t (&m)[NLIMB], int k, uint64_t acc)
     return fe_red_term<C, 1>(m, k, acc);
 }
 
+#ifdef HALO_MAD_COL
+// ---- column form (HALO_MAD_COL): per column one asm chain of the products, one of the reduction terms
+namespace colmul {
+// products a_i b_j, i + j = K (or, SQR, the doubled cross products a2_i a_j, i < j, and a_(K/2)^2)
+template <int K, bool SQR>
+constexpr int n_prod() {
+    int c = 0;
+    for (int i = 0; i < NLIMB; i++) {
+        const int j = K - i;
+        if (j < 0 || j >= NLIMB) continue;
+        if (!SQR || i < j || i == j) c++;
+    }
+    return c;
+}
+template <class C, int K>
+constexpr int n_red() {
+    int c = 0;
+    for (int j = 1; j < NLIMB; j++)
+        if (C::P[j] != 0 && K - j >= 0 && K - j < NLIMB) c++;
+    return c;
+}
+// acc (+)= the column-K products of a and b (SQR: a2 = 2a limb-wise, b unused)
+template <int K, bool SQR, bool ZERO>
+HALO_DEV void prod(uint64_t& acc, const uint32_t (&a)[NLIMB], const uint32_t (&a2)[NLIMB], const uint32_t (&b)[NLIMB]) {
+    constexpr int N = n_prod<K, SQR>();
+    uint32_t x[N > 0 ? N : 1], y[N > 0 ? N : 1];
+    int t = 0;
+#pragma unroll
+    for (int i = 0; i < NLIMB; i++) {
+        const int j = K - i;
+        if (j < 0 || j >= NLIMB) continue;
+        if (!SQR) {
+            x[t] = a[i];
+            y[t] = b[j];
+            t++;
+        } else if (i < j) {
+            x[t] = a2[i];
+            y[t] = a[j];
+            t++;
+        } else if (i == j) {
+            x[t] = a[i];
+            y[t] = a[i];
+            t++;
+        }
+    }
+    if constexpr (ZERO)
+        MadCol<N>::vv_z(acc, x, y);
+    else
+        MadCol<N>::vv(acc, x, y);
+}
+template <class C, int K>
+HALO_DEV void red(uint64_t& acc, const uint32_t (&m)[NLIMB]) {
+    constexpr int R = n_red<C, K>();
+    uint32_t x[R > 0 ? R : 1], y[R > 0 ? R : 1];
+    int t = 0;
+#pragma unroll
+    for (int j = 1; j < NLIMB; j++)
+        if (C::P[j] != 0 && K - j >= 0 && K - j < NLIMB) {
+            x[t] = m[K - j];
+            y[t] = C::P[j];
+            t++;
+        }
+    MadCol<R>::vs(acc, x, y);
+}
+template <class C, int K>
+HALO_DEV void finish(uint64_t& acc, uint32_t (&m)[NLIMB], uint32_t (&r)[NLIMB]) {
+    if constexpr (K < NLIMB) {
+        const uint32_t mk = (0u - (uint32_t)acc) & LIMB_MASK;
+        m[K] = mk;
+        acc += mk;  // p[0] == 1: clears the low 29 bits
+        acc >>= LIMB_BITS;
+    } else {
+        r[K - NLIMB] = (uint32_t)acc & LIMB_MASK;
+        acc >>= LIMB_BITS;
+    }
+}
+// one product (SQR: a^2), columns K..2 NLIMB - 2
+template <class C, int K, bool SQR>
+HALO_DEV void mul_cols(uint64_t& acc, const uint32_t (&a)[NLIMB], const uint32_t (&a2)[NLIMB], const uint32_t (&b)[NLIMB],
+                       uint32_t (&m)[NLIMB], uint32_t (&r)[NLIMB]) {
+    if constexpr (K < 2 * NLIMB - 1) {
+        prod<K, SQR, K == 0>(acc, a, a2, b);
+        red<C, K>(acc, m);
+        finish<C, K>(acc, m, r);
+        mul_cols<C, K + 1, SQR>(acc, a, a2, b, m, r);
+    }
+}
+// a b + c d with one reduction: the two products as two chains per column, joined once per column
+template <class C, int K>
+HALO_DEV void mul2_cols(uint64_t& acc, const uint32_t (&a)[NLIMB], const uint32_t (&b)[NLIMB], const uint32_t (&c)[NLIMB],
+                        const uint32_t (&d)[NLIMB], uint32_t (&m)[NLIMB], uint32_t (&r)[NLIMB]) {
+    if constexpr (K < 2 * NLIMB - 1) {
+        uint64_t acc2;
+        prod<K, false, K == 0>(acc, a, a, b);
+        prod<K, false, true>(acc2, c, c, d);
+        acc += acc2;
+        red<C, K>(acc, m);
+        finish<C, K>(acc, m, r);
+        mul2_cols<C, K + 1>(acc, a, b, c, d, m, r);
+    }
+}
+// two independent products, their column chains side by side
+template <class C, int K>
+HALO_DEV void mulx2_cols(uint64_t& acc1, uint64_t& acc2, const uint32_t (&a1)[NLIMB], const uint32_t (&b1)[NLIMB],
+                         const uint32_t (&a2)[NLIMB], const uint32_t (&b2)[NLIMB], uint32_t (&m1)[NLIMB],
+                         uint32_t (&m2)[NLIMB], uint32_t (&r1)[NLIMB], uint32_t (&r2)[NLIMB]) {
+    if constexpr (K < 2 * NLIMB - 1) {
+        prod<K, false, K == 0>(acc1, a1, a1, b1);
+        prod<K, false, K == 0>(acc2, a2, a2, b2);
+        red<C, K>(acc1, m1);
+        red<C, K>(acc2, m2);
+        finish<C, K>(acc1, m1, r1);
+        finish<C, K>(acc2, m2, r2);
+        mulx2_cols<C, K + 1>(acc1, acc2, a1, b1, a2, b2, m1, m2, r1, r2);
+    }
+}
+}  // namespace colmul
+
+template <class C>
+HALO_DEV Fe<C> fe_mul(const Fe<C>& a, const Fe<C>& b) {
+    uint32_t m[NLIMB];
+    Fe<C> r;
+    uint64_t acc;
+    colmul::mul_cols<C, 0, false>(acc, a.v, a.v, b.v, m, r.v);
+    r.v[NLIMB - 1] = (uint32_t)acc;
+    return r;
+}
+template <class C>
+HALO_DEV Fe<C> fe_mul2(const Fe<C>& a, const Fe<C>& b, const Fe<C>& c, const Fe<C>& d) {
+    uint32_t m[NLIMB];
+    Fe<C> r;
+    uint64_t acc;
+    colmul::mul2_cols<C, 0>(acc, a.v, b.v, c.v, d.v, m, r.v);
+    r.v[NLIMB - 1] = (uint32_t)acc;
+    return r;
+}
+template <class C>
+HALO_DEV void fe_mul_x2(const Fe<C>& a1, const Fe<C>& b1, const Fe<C>& a2, const Fe<C>& b2, Fe<C>& r1, Fe<C>& r2) {
+    uint32_t m1[NLIMB], m2[NLIMB];
+    uint64_t acc1, acc2;
+    colmul::mulx2_cols<C, 0>(acc1, acc2, a1.v, b1.v, a2.v, b2.v, m1, m2, r1.v, r2.v);
+    r1.v[NLIMB - 1] = (uint32_t)acc1;
+    r2.v[NLIMB - 1] = (uint32_t)acc2;
+}
+template <class C>
+HALO_DEV Fe<C> fe_sqr(const Fe<C>& a) {
+    uint32_t m[NLIMB], a2[NLIMB];
+#pragma unroll
+    for (int i = 0; i < NLIMB; i++) a2[i] = a.v[i] << 1;
+    Fe<C> r;
+    uint64_t acc;
+    colmul::mul_cols<C, 0, true>(acc, a.v, a2, a.v, m, r.v);
+    r.v[NLIMB - 1] = (uint32_t)acc;
+    return r;
+}
+#else
 template <class C>
 HALO_DEV Fe<C> fe_mul(const Fe<C>& a, const Fe<C>& b) {
     uint32_t m[NLIMB];
@@ -291,6 +455,8 @@ HALO_DEV Fe<C> fe_sqr(const Fe<C>& a) {
     r.v[NLIMB - 1] = (uint32_t)acc;
     return r;
 }
+
+#endif  // HALO_MAD_COL
 
 // ----------------------------------------------------------------------------------------------
 // Additive operations (results normalized, < 2p)

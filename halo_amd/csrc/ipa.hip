@@ -1976,6 +1976,22 @@ extern "C" int halo_hpoly_combine(halo_field_t field, const halo_fe_t* xis, size
     return HALO_OK;
 }
 
+// Device-resident variant (acc::prover's h(X), acc.rs:89 / pcdl.rs:198-219): the 2^(n_xis - 1)
+// coefficients (ark, untrimmed) go to d_out on `stream`; h never crosses PCIe.
+extern "C" int halo_hpoly_combine_dev(halo_field_t field, const halo_fe_t* xis, size_t k, size_t n_xis,
+                                      const halo_fe_t* alphas, void* d_out, void* stream) {
+    clear_error();
+    HALO_CHECK(check_field_i(field));
+    if (n_xis < 1 || n_xis > 29) return set_error(HALO_EINVAL, "halo_hpoly: n_xis %zu out of range [1, 29]", n_xis);
+    if (!k || !xis || !d_out) return set_error(HALO_EINVAL, "halo_hpoly: null buffer or k = 0");
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    hipStream_t s = (hipStream_t)stream;
+    ScratchUse su(st, s);
+    return hpoly_device(st, field, xis, k, n_xis, alphas, d_out, s);
+}
+
 extern "C" int halo_hpoly_coeffs(halo_field_t field, const halo_fe_t* xis, size_t n_xis, halo_fe_t* out) {
     return halo_hpoly_combine(field, xis, 1, n_xis, nullptr, out, nullptr);
 }

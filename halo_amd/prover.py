@@ -181,7 +181,9 @@ def synthetic_witness(B, n: int, seed: int = 1):
 
 
 def geometric_polys(B, zeta: int, polys):
-    """protocol.rs:542-548: sum_i zeta^i p_i."""
+    """protocol.rs:542-548: sum_i zeta^i p_i (the device backend: one fused launch, halo_poly_lincomb_dev)."""
+    if hasattr(B, "lincomb"):
+        return B.lincomb(polys, zeta)
     result = None
     zi = 1
     for p in polys:
@@ -499,6 +501,17 @@ class DeviceBackend:
     def poly_sub(self, a, b):
         return self.poly_add(a, b, sub=True)
 
+    def lincomb(self, polys, zeta: int):
+        """sum_i zeta^i polys[i] in one device pass (halo_poly_lincomb_dev); length = the longest."""
+        k = len(polys)
+        n_out = max(p.shape[0] for p in polys)
+        out = self._empty(n_out)
+        ptrs = (ctypes.c_void_p * k)(*[p.data_ptr() for p in polys])
+        lens = (ctypes.c_size_t * k)(*[p.shape[0] for p in polys])
+        self.H.check(self.L.halo_poly_lincomb_dev(self.field, ptrs, lens, k, self.H.ptr(self.fe(zeta)), self._p(out),
+                                                  n_out, self.sp))
+        return out
+
     def poly_scale(self, a, s):
         return self._op(3, a, None, s, 0, self._empty(a.shape[0]))
 
@@ -625,25 +638,24 @@ class DeviceBackend:
         return list(out)
 
     def point_combine(self, points, scalars):
+        """sum_i scalars[i] points[i] (acc.rs:166 point_dot over the U_i): one small MSM over the
+        caller's points (halo_msm) instead of per-point scalar multiplications and a point sum."""
         pts = np.ascontiguousarray(np.stack(points))
         ks = np.ascontiguousarray(np.stack([self.fe(s) for s in scalars]))
-        prod = np.zeros_like(pts)
-        self.H.check(self.L.halo_curve_op(self.curve, 2, self.H.ptr(pts), None, self.H.ptr(ks), len(pts),
-                                          self.H.ptr(prod)))
         out = np.zeros(8, dtype=np.uint64)
-        self.H.check(self.L.halo_point_sum(self.curve, self.H.ptr(prod), len(prod), self.H.ptr(out)))
+        self.H.check(self.L.halo_msm(self.curve, self.H.ptr(pts), len(pts), self.H.ptr(ks), len(ks), self.H.ptr(out)))
         return out
 
     def hpoly(self, xis_rows, alphas):
+        """sum_i alphas[i] h_i(X) (acc.rs:89) generated on the device (halo_hpoly_combine_dev): h never
+        crosses PCIe before its commitment and opening."""
         k, nx = len(xis_rows), len(xis_rows[0])
         xs = np.ascontiguousarray(np.stack([self.fe(x) for row in xis_rows for x in row]))
         al = np.ascontiguousarray(np.stack([self.fe(a) for a in alphas]))
-        n = 1 << (nx - 1)
-        out = np.zeros((n, 4), dtype=np.uint64)
-        ln = ctypes.c_size_t(0)
-        self.H.check(self.L.halo_hpoly_combine(self.field, self.H.ptr(xs), k, nx, self.H.ptr(al), self.H.ptr(out),
-                                               ctypes.byref(ln)))
-        return self.torch.from_numpy(out.view(np.int64)).cuda()
+        out = self._empty(1 << (nx - 1))
+        self.H.check(self.L.halo_hpoly_combine_dev(self.field, self.H.ptr(xs), k, nx, self.H.ptr(al), self._p(out),
+                                                   self.sp))
+        return out
 
     def ipa_many(self, jobs, chals, xi_mode=False):
         """jobs = [(p, n, z, H')] with one challenge stream each; all sessions advance in lockstep

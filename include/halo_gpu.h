@@ -223,6 +223,10 @@ int halo_hpoly_coeffs(halo_field_t field, const halo_fe_t* xis, size_t n_xis, ha
  * *out_len (if not NULL) = trimmed length. */
 int halo_hpoly_combine(halo_field_t field, const halo_fe_t* xis, size_t k, size_t n_xis, const halo_fe_t* alphas,
                        halo_fe_t* out, size_t* out_len);
+/* The same combination into a device buffer d_out (2^(n_xis - 1) ark coefficients, untrimmed), stream-
+ * ordered on `stream` (acc::prover's h(X) stays on the device for its commitment and opening). */
+int halo_hpoly_combine_dev(halo_field_t field, const halo_fe_t* xis, size_t k, size_t n_xis,
+                           const halo_fe_t* alphas, void* d_out, void* stream);
 /* pcdl::check step 5 (pcdl.rs:579): pedersen::commit(None, &pp.Gs[0..d+1], &h.get_poly().coeffs)
  * against the resident SRS, the coefficients never leaving the device. */
 int halo_pcdl_decider_commit(halo_curve_t curve, const halo_fe_t* xis, size_t n_xis, size_t d,
@@ -262,6 +266,11 @@ int halo_gate_constraints_dev(halo_field_t field, const void* const* d_w, const 
 /* Running product of the permutation argument (protocol.rs:143-154): inclusive prefix product
  * out[i] = prod_{j<=i} in[j] over n device elements (reverse != 0: suffix product prod_{j>=i}). */
 int halo_evals_scan_dev(halo_field_t field, int reverse, const void* d_in, void* d_out, size_t n, void* stream);
+/* sum_i zeta^i p_i (protocol.rs:542-548, the geometric combinations of round 5) over k <= 64 device
+ * coefficient vectors d_polys[i] of lens[i] ark elements (shorter ones zero-extended) into d_out
+ * (n_out elements, n_out >= max lens[i]), one launch on `stream`. */
+int halo_poly_lincomb_dev(halo_field_t field, const void* const* d_polys, const size_t* lens, size_t k,
+                          const halo_fe_t* zeta, void* d_out, size_t n_out, void* stream);
 
 /* ------------------------------------------------------------------ a8: evaluation / dots */
 /* DensePolynomial::evaluate (Horner; pcdl.rs:49,471), k polynomials at one point z. */

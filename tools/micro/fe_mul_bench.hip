@@ -1,5 +1,6 @@
-// Microbenchmark: throughput of halo::fe_mul (compiler-scheduled column sums) versus a variant whose
-// column accumulations are single v_mad_u64_u32 chains (inline asm), on gfx950.
+// Microbenchmark: throughput of halo::fe_mul (round 3: one inline-asm v_mad_u64_u32 chain per column,
+// mad_chain.hpp) against one asm statement per product (round 2), two interleaved chains, and the
+// compiler-scheduled C expression (split column sums), on gfx950; plus single-wave latency.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <vector>
@@ -88,17 +89,6 @@ __device__ __forceinline__ Fe<C> fe_mul_asm2(const Fe<C>& a, const Fe<C>& b) {
     return r;
 }
 
-template <int V>
-__global__ void bench(uint4* d, int iters) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    Fe<FqCfg> a = fe_load<FqCfg>(d + 4 * i), b = fe_load<FqCfg>(d + 4 * i + 2);
-    for (int k = 0; k < iters; k++) {
-        Fe<FqCfg> c = V == 0 ? fe_mul(a, b) : (V == 1 ? fe_mul_asm(a, b) : fe_mul_asm2(a, b));
-        b = a;
-        a = c;
-    }
-    fe_store(d + 4 * i, a);
-}
 
 template <typename K>
 double timeit(K kern, uint4* d, int blocks, int threads, int iters) {
@@ -146,10 +136,22 @@ __device__ __forceinline__ Fe<C> fe_mul_c(const Fe<C>& a, const Fe<C>& b) {
     return r;
 }
 template <int V>
+__global__ void bench(uint4* d, int iters) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    Fe<FqCfg> a = fe_load<FqCfg>(d + 4 * i), b = fe_load<FqCfg>(d + 4 * i + 2);
+    for (int k = 0; k < iters; k++) {
+        Fe<FqCfg> c = V == 0 ? fe_mul(a, b) : (V == 1 ? fe_mul_asm(a, b) : (V == 2 ? fe_mul_asm2(a, b) : fe_mul_c(a, b)));
+        b = a;
+        a = c;
+    }
+    fe_store(d + 4 * i, a);
+}
+
+template <int V>
 __global__ void lat(uint4* d, int iters) {
     const int i = threadIdx.x;
     Fe<FqCfg> a = fe_load<FqCfg>(d + 4 * i), b = fe_load<FqCfg>(d + 4 * i + 2);
-    for (int k = 0; k < iters; k++) a = V == 0 ? fe_mul_c(a, b) : fe_mul_asm(a, b);
+    for (int k = 0; k < iters; k++) a = V == 0 ? fe_mul_c(a, b) : (V == 1 ? fe_mul_asm(a, b) : fe_mul(a, b));
     fe_store(d + 4 * i, a);
 }
 
@@ -157,9 +159,10 @@ int main() {
     {
         uint4* d; CHECK(hipMalloc(&d, 64 * 4 * sizeof(uint4)));
         CHECK(hipMemset(d, 1, 64 * 4 * sizeof(uint4)));
-        for (int v = 0; v < 2; v++) {
-            double t = timeit(v == 0 ? lat<0> : lat<1>, d, 1, 64, 4096);
-            printf("single-wave dependent chain: %s %.1f ns per modmul\n", v == 0 ? "compiler-split" : "asm-chain", t * 1e6 / 4096);
+        for (int v = 0; v < 3; v++) {
+            double t = timeit(v == 0 ? lat<0> : (v == 1 ? lat<1> : lat<2>), d, 1, 64, 4096);
+            printf("single-wave dependent chain: %s %.1f ns per modmul\n",
+                   v == 0 ? "compiler-split" : (v == 1 ? "asm per product" : "asm per column (fields.hpp)"), t * 1e6 / 4096);
         }
         CHECK(hipFree(d));
     }
@@ -177,6 +180,8 @@ int main() {
         double t1 = timeit(bench<1>, d, blocks, threads, iters);
         CHECK(hipMemcpy(d, h.data(), h.size() * 4, hipMemcpyHostToDevice));
         double t2 = timeit(bench<2>, d, blocks, threads, iters);
+        CHECK(hipMemcpy(d, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+        double t3 = timeit(bench<3>, d, blocks, threads, iters);
         std::vector<uint32_t> o0(n * 16), o1(n * 16);
         CHECK(hipMemcpy(d, h.data(), h.size() * 4, hipMemcpyHostToDevice));
         hipLaunchKernelGGL(bench<0>, dim3(blocks), dim3(threads), 0, 0, d, 7);
@@ -188,9 +193,13 @@ int main() {
         CHECK(hipMemcpy(d, h.data(), h.size() * 4, hipMemcpyHostToDevice));
         hipLaunchKernelGGL(bench<2>, dim3(blocks), dim3(threads), 0, 0, d, 7);
         CHECK(hipMemcpy(o2.data(), d, h.size() * 4, hipMemcpyDeviceToHost));
-        printf("waves/SIMD %d: fe_mul %.3e, asm-chain %.3e, asm-2chain %.3e modmul/s, same=%d%d\n", wps,
+        std::vector<uint32_t> o3(n * 16);
+        CHECK(hipMemcpy(d, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+        hipLaunchKernelGGL(bench<3>, dim3(blocks), dim3(threads), 0, 0, d, 7);
+        CHECK(hipMemcpy(o3.data(), d, h.size() * 4, hipMemcpyDeviceToHost));
+        printf("waves/SIMD %d: fe_mul (asm per column) %.3e, asm per product %.3e, asm-2chain %.3e, compiler-split %.3e modmul/s, same=%d%d%d\n", wps,
                n * (double)iters / (t0 * 1e-3), n * (double)iters / (t1 * 1e-3), n * (double)iters / (t2 * 1e-3),
-               (int)(o0 == o1), (int)(o0 == o2));
+               n * (double)iters / (t3 * 1e-3), (int)(o0 == o1), (int)(o0 == o2), (int)(o0 == o3));
         CHECK(hipFree(d));
     }
     return 0;
