@@ -2,12 +2,11 @@
 // sum_i (i + 1) B_i per window (k_final, the single-wave Horner, stays in msm.hip: measured faster
 // with the single-chain multiplication).
 //
-// Every kernel here is latency-bound (a few waves doing dependent chains of curve additions), so this
-// translation unit is compiled with HALO_MAD_ILP: the field multiplication keeps the compiler's
-// split column sums (shorter dependency chains: 418 vs 523 ns per dependent modmul on one wave,
-// tools/micro/fe_mul_bench.hip) instead of the single-chain form that wins in the throughput
-// kernels.  The arithmetic lives in the inline namespace halo::ilp here (fields.hpp), so the two
-// variants never collide.
+// Every kernel here is latency-bound (a few waves doing dependent chains of curve additions).  Round 2
+// compiled this translation unit with HALO_MAD_ILP (the compiler's split column sums: 418 vs 523 ns
+// per dependent modmul on one wave against one asm statement per product); since round 3 the default
+// build uses the per-column asm chains here as well (HALO_TAIL_COL: 382 ns, tools/micro/fe_mul_bench.hip),
+// and HALO_MAD_ILP remains an A/B build option (arithmetic in the inline namespace halo::ilp then).
 #include <algorithm>
 
 #include "dispatch.hpp"
@@ -16,8 +15,8 @@
 #include "sort.hpp"
 #include "tree.hpp"
 
-#ifndef HALO_MAD_ILP
-#error "msm_tail.hip must be compiled with -DHALO_MAD_ILP (see Makefile)"
+#if !defined(HALO_MAD_ILP) && !defined(HALO_TAIL_COL)
+#error "msm_tail.hip must be compiled with -DHALO_MAD_ILP or -DHALO_TAIL_COL (see Makefile)"
 #endif
 
 
