@@ -390,20 +390,10 @@ __global__ __launch_bounds__(64) void k_tail_mults(size_t n0, uint4* table) {
 }
 
 // mode 0: L/R scalars of the current round (len = 2m); mode 1: U's scalars s[k] = w[k]
+// the GLV digits of term k's scalar v (internal form) and its side
 template <class Cv>
-HALO_DEV void tail_scalar_one(const uint4* cs, const uint4* w, size_t k, size_t len, size_t m, int mode, uint32_t* scal,
-                              uint8_t* side) {
+HALO_DEV void tail_scalar_val(const Fe<typename Cv::Scalar>& v, uint8_t sd, size_t k, uint32_t* scal, uint8_t* side) {
     using S = typename Cv::Scalar;
-    Fe<S> v;
-    uint8_t sd = 0;
-    if (mode == 0) {
-        const size_t j = k % len, u = k / len;
-        const size_t ci = (j < m) ? m + j : j - m;
-        sd = (j < m) ? 0 : 1;
-        v = fe_mul(fe_from_ark<S>(cs + 2 * ci), fe_from_ark<S>(w + 2 * u));
-    } else {
-        v = fe_from_ark<S>(w + 2 * k);
-    }
     Fe<S> one_raw = fe_zero<S>();  // internal (x 2^261) -> canonical: Montgomery product with 1
     one_raw.v[0] = 1;
     uint32_t w8[8], k1[5], k2[5];
@@ -416,6 +406,20 @@ HALO_DEV void tail_scalar_one(const uint4* cs, const uint4* w, size_t k, size_t 
         scal[8 * k + 4 + q] = k2[q];
     }
     side[k] = sd | (n1 ? 2 : 0) | (n2 ? 4 : 0);
+}
+
+template <class Cv>
+HALO_DEV void tail_scalar_one(const uint4* cs, const uint4* w, size_t k, size_t len, size_t m, int mode, uint32_t* scal,
+                              uint8_t* side) {
+    using S = typename Cv::Scalar;
+    if (mode == 0) {
+        const size_t j = k % len, u = k / len;
+        const size_t ci = (j < m) ? m + j : j - m;
+        tail_scalar_val<Cv>(fe_mul(fe_from_ark<S>(cs + 2 * ci), fe_from_ark<S>(w + 2 * u)), (j < m) ? 0 : 1, k, scal,
+                            side);
+    } else {
+        tail_scalar_val<Cv>(fe_from_ark<S>(w + 2 * k), 0, k, scal, side);
+    }
 }
 
 template <class Cv>
@@ -446,22 +450,66 @@ HALO_DEV void glv_split_words(const uint4* x_ark, uint32_t* out10) {
     out10[9] = n2;
 }
 
+// The previous round's fold (pcdl.rs:430-435, w' = interleave(w, xi w)) deferred into this launch:
+// halo_ipa_fold only records xi (passed here by value -- no H2D copy, no k_tail_fold launch); the
+// scalar blocks read the unfolded c, w and fold the entries they need on the fly, the dots block
+// writes the folded c, z, w to the other buffers of their ping-pong pairs.
+struct TailFoldArgs {
+    uint4 xi[2], xinv[2];  // ark
+    uint4 *cs_out, *zs_out, *w_out;
+    size_t wlen_in;  // fold weights before the fold
+    int active;
+};
+
 template <class Cv>
 __global__ __launch_bounds__(256) void k_tail_prep(const uint4* cs, const uint4* zs, const uint4* w, size_t n0, size_t len,
                                                    size_t m, uint32_t* scal, uint8_t* side, uint32_t nsb,
-                                                   const uint4* xi0_ark, uint4* dots_ark, uint32_t* hkw) {
+                                                   const uint4* xi0_ark, uint4* dots_ark, uint32_t* hkw,
+                                                   const TailFoldArgs f) {
     using S = typename Cv::Scalar;
     const int tid = threadIdx.x;
     if (blockIdx.x < nsb) {
         const size_t k = (size_t)blockIdx.x * 256 + tid;
-        if (k < n0) tail_scalar_one<Cv>(cs, w, k, len, m, 0, scal, side);
+        if (k >= n0) return;
+        if (!f.active) {
+            tail_scalar_one<Cv>(cs, w, k, len, m, 0, scal, side);
+            return;
+        }
+        // c' = c_l + xi^-1 c_r over the unfolded c (length 2 len), w'[u] = w[u / 2] (u odd: xi w[u / 2])
+        const size_t j = k % len, u = k / len;
+        const size_t ci = (j < m) ? m + j : j - m;
+        const Fe<S> c1 = fe_add(fe_from_ark<S>(cs + 2 * ci), fe_mul(fe_from_ark<S>(cs + 2 * (ci + len)), fe_from_ark<S>(f.xinv)));
+        Fe<S> wu = fe_from_ark<S>(w + 2 * (u >> 1));
+        if (u & 1) wu = fe_mul(wu, fe_from_ark<S>(f.xi));
+        tail_scalar_val<Cv>(fe_mul(c1, wu), (j < m) ? 0 : 1, k, scal, side);
         return;
     }
     __shared__ uint4 red[2][256 * 2];
     Fe<S> a = fe_zero<S>(), b = fe_zero<S>();
-    for (size_t i = tid; i < m; i += 256) {
-        a = fe_add(a, fe_mul(fe_from_ark<S>(cs + 2 * (m + i)), fe_from_ark<S>(zs + 2 * i)));
-        b = fe_add(b, fe_mul(fe_from_ark<S>(cs + 2 * i), fe_from_ark<S>(zs + 2 * (m + i))));
+    if (f.active) {
+        const Fe<S> xi = fe_from_ark<S>(f.xi), xinv = fe_from_ark<S>(f.xinv);
+        for (size_t i = tid; i < m; i += 256) {
+            const Fe<S> cl = fe_add(fe_from_ark<S>(cs + 2 * i), fe_mul(fe_from_ark<S>(cs + 2 * (i + len)), xinv));
+            const Fe<S> cr = fe_add(fe_from_ark<S>(cs + 2 * (m + i)), fe_mul(fe_from_ark<S>(cs + 2 * (m + i + len)), xinv));
+            const Fe<S> zl = fe_add(fe_from_ark<S>(zs + 2 * i), fe_mul(fe_from_ark<S>(zs + 2 * (i + len)), xi));
+            const Fe<S> zr = fe_add(fe_from_ark<S>(zs + 2 * (m + i)), fe_mul(fe_from_ark<S>(zs + 2 * (m + i + len)), xi));
+            fe_to_ark(f.cs_out + 2 * i, cl);
+            fe_to_ark(f.cs_out + 2 * (m + i), cr);
+            fe_to_ark(f.zs_out + 2 * i, zl);
+            fe_to_ark(f.zs_out + 2 * (m + i), zr);
+            a = fe_add(a, fe_mul(cr, zl));
+            b = fe_add(b, fe_mul(cl, zr));
+        }
+        for (size_t u = tid; u < f.wlen_in; u += 256) {
+            const Fe<S> wv = fe_from_ark<S>(w + 2 * u);
+            fe_to_ark(f.w_out + 2 * (2 * u), wv);
+            fe_to_ark(f.w_out + 2 * (2 * u + 1), fe_mul(wv, xi));
+        }
+    } else {
+        for (size_t i = tid; i < m; i += 256) {
+            a = fe_add(a, fe_mul(fe_from_ark<S>(cs + 2 * (m + i)), fe_from_ark<S>(zs + 2 * i)));
+            b = fe_add(b, fe_mul(fe_from_ark<S>(cs + 2 * i), fe_from_ark<S>(zs + 2 * (m + i))));
+        }
     }
     fe_store(red[0] + 2 * tid, a);
     fe_store(red[1] + 2 * tid, b);
@@ -670,6 +718,7 @@ struct halo_ipa_session {
     hipEvent_t htab_ready = nullptr;  // recorded on aux after the table
     uint8_t* pinned = nullptr;  // [128, 192) xi|xi_inv (H2D), [256, 512) L|R XYZZ (D2H): async, several sessions in flight
     DevBuf gs, cs, zs, htab, small, tmp, pbar;
+    DevBuf cs2, zs2;  // ping-pong partners of cs / zs (tail rounds with a deferred fold)
     DevBuf own_table, w[2], scal, side, part;
     BatchScratch mat;  // weighted -> tail switch (msm_shared_batch)
     // ---- per-opening state (reset by ipa_acquire)
@@ -688,6 +737,9 @@ struct halo_ipa_session {
     const uint4* table = nullptr;  // tail multiples table: own_table, or the SRS's small table
     size_t table_ld = 0;
     bool fold_inflight = false;       // a fold's H2D copy of xi may still read `pinned`
+    bool fold_pending = false;        // tail rounds: the last fold is applied by the next launch (k_tail_prep)
+    halo_fe_t pend_xi{}, pend_xinv{};
+    size_t pend_m = 0;                // the half-length m the pending fold folds (before its m /= 2)
     bool htab_waited = false;         // round 1 waited for it (later rounds follow a host sync of round 1)
     // xi mode (halo_ipa_begin_xi / _dev_xi / halo_pcdl_open_start): the hiding terms use the resident
     // 2^i H table and the dots scaled by xi_0 (dot H' = (dot xi_0) H), so there is neither H' nor a
@@ -706,7 +758,7 @@ struct halo_ipa_session {
         wcur = 0;
         table = nullptr;
         table_ld = 0;
-        fold_inflight = htab_waited = xi_mode = false;
+        fold_inflight = htab_waited = xi_mode = fold_pending = false;
         htab_ptr = nullptr;
         started = blinded = combined = false;
     }
@@ -722,7 +774,8 @@ struct halo_ipa_session {
         s = aux = nullptr;
         htab_ready = nullptr;
         pinned = nullptr;
-        for (DevBuf* b : {&gs, &cs, &zs, &htab, &small, &tmp, &pbar, &own_table, &w[0], &w[1], &scal, &side, &part})
+        for (DevBuf* b : {&gs, &cs, &zs, &cs2, &zs2, &htab, &small, &tmp, &pbar, &own_table, &w[0], &w[1], &scal, &side,
+                          &part})
             b->release();
         for (DevBuf* b : {&mat.digits, &mat.lists, &mat.keys, &mat.vals, &mat.bstart, &mat.partials, &mat.bucket_sums,
                           &mat.window_sums})
@@ -1438,6 +1491,8 @@ static int ipa_enter_tail(DeviceState* st, halo_ipa_session* ses, hipStream_t s)
     const size_t nblk = (TAIL_WIN * n0 + TAIL_THREADS - 1) / TAIL_THREADS + 2;  // (+ mode 0's per-side rounding)
     HALO_CHECK(ses->w[0].reserve(n0 * 32));
     HALO_CHECK(ses->w[1].reserve(n0 * 32));
+    HALO_CHECK(ses->cs2.reserve(n0 * 32));
+    HALO_CHECK(ses->zs2.reserve(n0 * 32));
     HALO_CHECK(ses->scal.reserve(n0 * 32));
     HALO_CHECK(ses->side.reserve(n0));
     HALO_CHECK(ses->part.reserve(nblk * 2 * 128));
@@ -1483,11 +1538,30 @@ static int ipa_tail_sums(halo_ipa_session* ses, int mode, hipStream_t s) {
     DISPATCH_CURVE(ses->curve, Cv, {
         if (mode == 0) {
             const uint32_t nsb = gridn(n0, 256);
+            TailFoldArgs f{};
+            f.active = ses->fold_pending;
+            if (f.active) {  // the previous round's fold, applied here (halo_ipa_fold deferred it)
+                memcpy(&f.xi, &ses->pend_xi, 32);
+                memcpy(&f.xinv, &ses->pend_xinv, 32);
+                f.cs_out = ses->cs2.as<uint4>();
+                f.zs_out = ses->zs2.as<uint4>();
+                f.w_out = ses->w[ses->wcur ^ 1].as<uint4>();
+                f.wlen_in = ses->wlen;
+            }
             hipLaunchKernelGGL(k_tail_prep<Cv>, dim3(nsb + 1), dim3(256), 0, s, ses->cs.as<const uint4>(),
                                ses->zs.as<const uint4>(), ses->w[ses->wcur].as<const uint4>(), n0, 2 * m, m,
                                ses->scal.as<uint32_t>(), ses->side.as<uint8_t>(), nsb,
                                ses->xi_mode ? (const uint4*)(sm + 192) : (const uint4*)nullptr, (uint4*)(sm + 128),
-                               (uint32_t*)(sm + SM_HKW));
+                               (uint32_t*)(sm + SM_HKW), f);
+            if (f.active) {
+                std::swap(ses->cs.ptr, ses->cs2.ptr);
+                std::swap(ses->cs.bytes, ses->cs2.bytes);
+                std::swap(ses->zs.ptr, ses->zs2.ptr);
+                std::swap(ses->zs.bytes, ses->zs2.bytes);
+                ses->wcur ^= 1;
+                ses->wlen *= 2;
+                ses->fold_pending = false;
+            }
         } else {
             hipLaunchKernelGGL(k_tail_scalars<Cv>, dim3(gridn(n0, 256)), dim3(256), 0, s, ses->cs.as<const uint4>(),
                                ses->w[ses->wcur].as<const uint4>(), n0, 2 * m, m, mode, ses->scal.as<uint32_t>(),
@@ -1678,9 +1752,34 @@ static int ipa_round_launch(DeviceState* st, halo_ipa_session* ses) {
 }
 
 // Enqueues one fold with challenge xi (pcdl.rs:427-435); the session advances to the next round.
+static int ipa_fold_now(DeviceState* st, halo_ipa_session* ses, const halo_fe_t* xi, const halo_fe_t* xi_inv);
+
+// A deferred tail-round fold applied on its own (before U at the end, a state read, or a second fold).
+static int ipa_apply_pending_fold(DeviceState* st, halo_ipa_session* ses) {
+    if (!ses->fold_pending) return HALO_OK;
+    ses->fold_pending = false;
+    ses->m = ses->pend_m;  // ipa_fold_now halves it again
+    return ipa_fold_now(st, ses, &ses->pend_xi, &ses->pend_xinv);
+}
+
 static int ipa_fold_launch(DeviceState* st, halo_ipa_session* ses, const halo_fe_t* xi, const halo_fe_t* xi_inv) {
     if (ses->m == 0) return set_error(HALO_EINVAL, "halo_ipa_fold: no rounds left");
     if (!ses->started) return set_error(HALO_EINVAL, "halo_ipa_fold: session not started (halo_pcdl_open_start)");
+    static const bool defer = !(getenv("HALO_IPA_DEFER_FOLD") && getenv("HALO_IPA_DEFER_FOLD")[0] == '0');  // A/B knob
+    if (ses->tail && defer) {  // applied by the next round's k_tail_prep (no launch, no copy now)
+        HALO_CHECK(ipa_apply_pending_fold(st, ses));
+        ses->pend_xi = *xi;
+        ses->pend_xinv = *xi_inv;
+        ses->pend_m = ses->m;
+        ses->fold_pending = true;
+        ses->srs_round0 = false;
+        ses->m /= 2;
+        return HALO_OK;
+    }
+    return ipa_fold_now(st, ses, xi, xi_inv);
+}
+
+static int ipa_fold_now(DeviceState* st, halo_ipa_session* ses, const halo_fe_t* xi, const halo_fe_t* xi_inv) {
     hipStream_t s = ses->s;
     char* sm = (char*)ses->small.ptr;
     // the previous fold's H2D copy from the pinned staging must have completed (a round in between
@@ -1777,6 +1876,7 @@ extern "C" int halo_ipa_state(halo_ipa_session* ses, size_t* m, halo_wrapped_poi
     if (!st) return HALO_EDEVICE;
     std::lock_guard<std::mutex> g(st->mu);
     hipStream_t s = ses->s;
+    HALO_CHECK(ipa_apply_pending_fold(st, ses));
     const size_t len = std::max<size_t>(2 * ses->m, 1);
     if (m) *m = ses->m;
     if (gs && (ses->tail || ses->weighted || !ses->gs_valid))
@@ -1808,6 +1908,7 @@ extern "C" int halo_ipa_end(halo_ipa_session* ses, halo_wrapped_point_t* U, halo
         char* sm = (char*)ses->small.ptr;
         if (!ses->started) {
             rc = set_error(HALO_EINVAL, "halo_ipa_end: session not started");
+        } else if ((rc = ipa_apply_pending_fold(st, ses))) {
         } else if (ses->tail || ses->weighted) {
             // U = G_0 = sum_u w[u] G0[u] (len = 1 once every round ran)
             if (ses->m != 0)
