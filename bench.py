@@ -504,6 +504,19 @@ def main():
             tt = torch.tensor([time.perf_counter() - a0], dtype=torch.float64, device="cuda")
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             out["ms_per_msm_with_broadcast" if bcast else "ms_per_msm_resident_scalars"] = float(tt.item()) * 1e3 / reps
+        # the collective alone: the scalar broadcast (n x 32 B from rank 0) with no MSM behind it
+        dist.broadcast(sc, 0)
+        torch.cuda.synchronize()
+        dist.barrier()
+        a0 = time.perf_counter()
+        for _ in range(reps):
+            dist.broadcast(sc, 0)
+        torch.cuda.synchronize()
+        dist.barrier()
+        tt = torch.tensor([time.perf_counter() - a0], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        out["ms_broadcast_only"] = float(tt.item()) * 1e3 / reps
+        out["broadcast_GB_per_s"] = n_ * 32 / (out["ms_broadcast_only"] * 1e-3) / 1e9
         # the partitioned result must equal rank 0's whole MSM of the same scalars
         ok = None
         if rank == 0:
