@@ -23,6 +23,167 @@ HALO_DEV XYZZ<F> xyzz_shfl_xor(const XYZZ<F>& p, int m) {
     }
     return r;
 }
+#ifndef HALO_TREE_COOP
+#define HALO_TREE_COOP 1  // 0: one addition per lane per level (A/B knob)
+#endif
+
+#if HALO_TREE_COOP
+// ---------------------------------------------------------------------------------------------
+// Quad-cooperative additions.  A tree level inside one wave is issue-bound, not latency-bound: the
+// wave's SIMD spends the same cycles on an addition whether 32 lanes or 1 lane need it, and a level
+// with one addition per lane costs the full 12M + 2S of xyzz_add.  Here four lanes (a quad) share
+// one addition: its multiplications form four dependent rounds (U1 U2 S1 S2 | PP RR ZZ1ZZ2 ZZZ1ZZZ2 |
+// ZZ3 PPP Q | Y3a Y3b ZZZ3), each lane computes one product per round (operands picked by its role)
+// and the quad exchanges the products with DPP quad broadcasts, so a level costs four multiplication
+// issues per 16 additions instead of fourteen.  Same formula and operations as xyzz_add (curve.hpp),
+// so the results are bit-identical; the exceptional case (P == +-Q) falls back to xyzz_dbl / the
+// identity, wave-uniformly skipped when no lane hits it.
+// ---------------------------------------------------------------------------------------------
+// v_mov_b32 with a DPP quad permutation: lane i of each quad reads lane (CTRL >> 2 i) & 3
+#ifndef HALO_QPERM_DPP
+#define HALO_QPERM_DPP 1
+#endif
+template <int CTRL, class F>
+HALO_DEV Fe<F> qperm(const Fe<F>& a) {
+    Fe<F> r;
+#if HALO_QPERM_DPP
+#pragma unroll
+    for (int l = 0; l < NLIMB; l++) r.v[l] = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.v[l], CTRL, 0xF, 0xF, false);
+#else
+    const uint32_t q = threadIdx.x & 3u;
+    const int src = (int)((threadIdx.x & 60u) | ((uint32_t)(CTRL >> (2 * q)) & 3u));
+#pragma unroll
+    for (int l = 0; l < NLIMB; l++) r.v[l] = __shfl(a.v[l], src);
+#endif
+    return r;
+}
+constexpr int qp(int l0, int l1, int l2, int l3) { return l0 | (l1 << 2) | (l2 << 4) | (l3 << 6); }
+// branch-free per-lane pick: m all ones -> a, zero -> b (v_bfi_b32)
+template <class F>
+HALO_DEV Fe<F> pick(uint32_t m, const Fe<F>& a, const Fe<F>& b) {
+    Fe<F> r;
+#pragma unroll
+    for (int l = 0; l < NLIMB; l++) r.v[l] = (a.v[l] & m) | (b.v[l] & ~m);
+    return r;
+}
+template <class F>
+HALO_DEV XYZZ<F> xyzz_shfl(const XYZZ<F>& p, int src) {
+    XYZZ<F> r;
+#pragma unroll
+    for (int l = 0; l < NLIMB; l++) {
+        r.X.v[l] = __shfl(p.X.v[l], src);
+        r.Y.v[l] = __shfl(p.Y.v[l], src);
+        r.ZZ.v[l] = __shfl(p.ZZ.v[l], src);
+        r.ZZZ.v[l] = __shfl(p.ZZZ.v[l], src);
+    }
+    return r;
+}
+// p + q (the points of lanes s1 and s2 of v) by the quad: role = lane & 3 computes one product per
+// round and the quad trades products by DPP quad permutations:
+//   round 1  U1 = X1 ZZ2 | U2 = X2 ZZ1 | S1 = Y1 ZZZ2 | S2 = Y2 ZZZ1    (operands fetched by lane)
+//            pairs swap: lanes 0, 1 form P = U2 - U1, lanes 2, 3 R = S2 - S1
+//   round 2  PP = P P | A = ZZ1 ZZ2 | RR = R R | B = ZZZ1 ZZZ2          (ZZ / ZZZ from the pair swap)
+//   round 3  Q = U1 PP | PPP = P PP | ZZ3 = A PP | -
+//   round 4  - | ZZZ3 = B PPP | Y3a = R (Q - X3) | Y3b = S1 PPP         (X3 = RR - PPP - 2 Q)
+// The sum is assembled in the quad's lane 2.  Trivial additions (an identity operand, idp / idq) are
+// left to the caller, which takes the other operand instead.
+template <class F>
+HALO_DEV XYZZ<F> xyzz_add_quad(const XYZZ<F>& v, uint32_t s1, uint32_t s2, bool idp, bool idq) {
+    const uint32_t role = threadIdx.x & 3u;
+    const uint32_t odd = (role & 1u) ? ~0u : 0u, lo = role < 2 ? ~0u : 0u, r2 = role == 2 ? ~0u : 0u;
+    const uint32_t sa = (role & 1u) ? s2 : s1, sb = (role & 1u) ? s1 : s2;
+    Fe<F> a, b;
+#pragma unroll
+    for (int l = 0; l < NLIMB; l++) {  // role 0: p.X q.ZZ, 1: q.X p.ZZ, 2: p.Y q.ZZZ, 3: q.Y p.ZZZ
+        const uint32_t x = __shfl(v.X.v[l], (int)sa), y = __shfl(v.Y.v[l], (int)sa);
+        const uint32_t zz = __shfl(v.ZZ.v[l], (int)sb), zzz = __shfl(v.ZZZ.v[l], (int)sb);
+        a.v[l] = (x & lo) | (y & ~lo);
+        b.v[l] = (zz & lo) | (zzz & ~lo);
+    }
+    const Fe<F> t1 = fe_mul(a, b);
+    constexpr int SWAP = qp(1, 0, 3, 2);
+    const Fe<F> t1s = qperm<SWAP>(t1), bs = qperm<SWAP>(b);
+    const Fe<F> d = fe_sub_k<2>(pick(odd, t1, t1s), pick(odd, t1s, t1));  // P (lanes 0, 1), R (2, 3)
+    const Fe<F> t2 = fe_mul(pick(odd, b, d), pick(odd, bs, d));
+    const Fe<F> PPb = qperm<qp(0, 0, 0, 0)>(t2), Ab = qperm<qp(0, 1, 1, 3)>(t2);
+    const Fe<F> t3 = fe_mul(pick(lo, pick(odd, d, t1), Ab), PPb);
+    const Fe<F> Bb = qperm<qp(0, 3, 2, 3)>(t2), Qb = qperm<qp(0, 1, 0, 3)>(t3), PPPb = qperm<qp(1, 1, 1, 1)>(t3);
+    XYZZ<F> r;
+    r.X = fe_reduce_8p(fe_sub_k<6>(t2, fe_add_nc(PPPb, fe_add_nc(Qb, Qb))));  // (lane 2: t2 = RR)
+    const Fe<F> t4 = fe_mul(pick(lo, Bb, pick(odd, t1s, d)), pick(r2, fe_sub_k<2>(Qb, r.X), PPPb));
+    r.Y = fe_sub(t4, qperm<qp(0, 1, 3, 3)>(t4));
+    r.ZZ = t3;
+    r.ZZZ = qperm<qp(0, 1, 1, 3)>(t4);
+    const bool exc = role == 2 && !idp && !idq && fe_is_zero(t3);
+    if (__any(exc)) {  // P == +-Q: doubling or the identity (rare)
+        const XYZZ<F> p = xyzz_shfl(v, (int)s1);
+        if (exc) r = fe_is_zero_4p(d) ? xyzz_dbl(p) : xyzz_id<F>();
+    }
+    return r;
+}
+// sum over aligned groups of G lanes (G a power of two <= 64), valid in the group's first lane.  The
+// points live as a flat list (group g's at lanes [g G, g G + G)); a level turns the list of groups of
+// size gs into one of size gs / 2 by 64 / G * gs / 2 quad additions (16 per batch), each addition's
+// sum moved to its lane in the new list.
+template <class F>
+HALO_DEV XYZZ<F> wave_group_sum(XYZZ<F> v, uint32_t G) {
+    const uint32_t lane = threadIdx.x & 63u;
+    for (uint32_t gs = G; gs > 1; gs >>= 1) {
+        const uint32_t m = gs >> 1, nadd = (64u / G) * m;  // 64 / G groups x m additions
+        const uint32_t idv = xyzz_is_id(v) ? 1u : 0u;
+        XYZZ<F> nxt = xyzz_id<F>();
+        for (uint32_t b = 0; b * 16 < nadd; b++) {
+            // the quad's addition a = 16 b + lane / 4: lanes s1 = g gs + i and s2 = s1 + m
+            const uint32_t a = b * 16 + (lane >> 2);
+            const uint32_t s1 = ((a / m) * gs + a % m) & 63u, s2 = (s1 + m) & 63u;
+            const uint32_t fp = __shfl(idv, (int)s1), fq = __shfl(idv, (int)s2);
+            const bool idp = a >= nadd || fp != 0u, idq = a >= nadd || fq != 0u;
+            XYZZ<F> r = xyzz_id<F>();
+            if (!__all(idp || idq)) r = xyzz_add_quad(v, s1, s2, idp, idq);
+            // lane c = 16 b + j of the new list takes addition c's sum (quad j, lane 2), or, for an identity
+            // operand, the other operand itself
+            const uint32_t c = lane, j = (c - b * 16) & 15u;
+            const bool mine = c >= b * 16 && c < b * 16 + 16 && c < nadd;
+            const uint32_t c1 = ((c / m) * gs + c % m) & 63u, c2 = (c1 + m) & 63u;
+            const bool cp = __shfl(idv, (int)c1) != 0u, cq = __shfl(idv, (int)c2) != 0u;
+            const bool triv = mine && (cp || cq);
+            XYZZ<F> t = xyzz_shfl(r, (int)(4 * j + 2));
+            if (__any(triv)) {
+                const XYZZ<F> o = xyzz_shfl(v, (int)(cp ? c2 : c1));
+                if (triv) t = o;
+            }
+            if (mine) nxt = t;
+        }
+        v = nxt;
+    }
+    // group g's sum is at lane g now; its first lane is g G
+    return G > 1 && G < 64 ? xyzz_shfl(v, (int)(lane / G)) : v;
+}
+// sum over aligned groups of G threads (G a power of two <= blockDim): valid in the group's first
+// thread.  Every wave sums its lanes (G <= 64: its groups) cooperatively; for G > 64 the first wave
+// of the block sums the waves' sums of every group and hands each group's sum back to its first
+// thread through LDS.  red: LDS scratch for blockDim / 64 points (>= 1).  Every thread of the block must
+// call it.
+template <class F>
+HALO_DEV XYZZ<F> block_group_sum(XYZZ<F> v, uint32_t G, uint4* red) {
+    if (G <= 64) return wave_group_sum<F>(v, G);
+    v = wave_group_sum<F>(v, 64u);
+    const uint32_t wv = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = threadIdx.x & 63u;
+    if (lane == 0) xyzz_store(red + 8 * wv, v);
+    __syncthreads();
+    XYZZ<F> w = xyzz_id<F>();
+    if (wv == 0 && lane < nw) w = xyzz_load<F>(red + 8 * lane);
+    __syncthreads();
+    if (wv == 0) {  // (wave-uniform)
+        w = wave_group_sum<F>(w, G >> 6);
+        if (lane < nw && (lane & ((G >> 6) - 1)) == 0) xyzz_store(red + 8 * (lane / (G >> 6)), w);
+    }
+    __syncthreads();
+    const uint32_t gpos = threadIdx.x & (G - 1);
+    if (gpos == 0) v = xyzz_load<F>(red + 8 * (threadIdx.x / G));
+    return v;
+}
+#else
 // every lane gets the sum over its aligned group of G lanes (G a power of two <= 64)
 template <class F>
 HALO_DEV XYZZ<F> wave_group_sum(XYZZ<F> v, uint32_t G) {
@@ -47,5 +208,7 @@ HALO_DEV XYZZ<F> block_group_sum(XYZZ<F> v, uint32_t G, uint4* red) {
     if (gpos < 64) v = wave_group_sum<F>(v, G < 64 ? G : 64u);
     return v;
 }
+
+#endif
 
 HALO_ARITH_END
