@@ -339,7 +339,10 @@ constexpr int IPA_HTAB = 128;  // entries 2^i H' of the session's hiding table (
 constexpr int TAIL_DB = 4;                            // digit bits
 constexpr int TAIL_TBL = 128 / TAIL_DB;               // table windows per 128-bit GLV half
 constexpr int TAIL_MUL = (1 << TAIL_DB) - 1;          // multiples d = 1..15 per window
-constexpr int TAIL_WIN = 2 * TAIL_TBL, TAIL_THREADS = 256;  // terms per point: 32 windows x (k1, k2)
+constexpr int TAIL_WIN = 2 * TAIL_TBL;  // terms per point: 32 windows x (k1, k2)
+// threads per tail block: 256, one wave per SIMD (512 measured slower, opening 2^10 1.93 -> 2.13 ms: two
+// waves' quad trees then share a SIMD's issue slots)
+constexpr int TAIL_THREADS = 256;
 
 // the doubling chain in Jacobian coordinates (dbl-2009-l: 7 multiplications against XYZZ's 9)
 template <class Cv>
@@ -644,7 +647,11 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail_final(const uint4* part, 
         if (neg[tid >> 7]) p.y = fe_neg(p.y);
         acc = xyzz_from_aff(p);
     }
-    for (int i = tid; i < nblk; i += TAIL_THREADS) acc = xyzz_add(acc, xyzz_load<F>(part + 8 * (2 * (size_t)i + b)));
+    // this side's partials (blocks [b per_side, (b + 1) per_side)), dealt round-robin over the waves so
+    // that every SIMD's wave sums a quarter of them
+    const int per_side = nblk / (int)gridDim.x, j0 = (tid & 63) * (TAIL_THREADS / 64) + (tid >> 6);
+    for (int j = j0; j < per_side; j += TAIL_THREADS)
+        acc = xyzz_add(acc, xyzz_load<F>(part + 8 * (2 * (size_t)(b * per_side + j) + b)));
     acc = block_group_sum<F>(acc, TAIL_THREADS, red);
     if (tid == 0) {
         if (xyzz_out)  // 128 B per side, converted on the host (host_xyzz_to_wrapped)

@@ -37,9 +37,10 @@ __global__ void k_points(uint4* out, uint32_t n) {
 }
 
 // G: group size; block = 64 (wave) or 256 threads
-__global__ __launch_bounds__(256) void k_tree(const uint4* pts, uint32_t G, uint4* out) {
+// live: lanes (of each wave) holding points, the others the identity
+__global__ __launch_bounds__(256) void k_tree(const uint4* pts, uint32_t G, uint4* out, uint32_t live) {
     __shared__ uint4 red[256 / 2 * 8];
-    XYZZ<F> v = xyzz_load<F>(pts + 8 * threadIdx.x);
+    XYZZ<F> v = (threadIdx.x & 63u) < live ? xyzz_load<F>(pts + 8 * threadIdx.x) : xyzz_id<F>();
     for (int it = 0; it < ITER; it++) {
         const XYZZ<F> s = G <= 64 ? wave_group_sum<F>(v, G) : block_group_sum<F>(v, G, red);
         if (threadIdx.x == 0) v = s;  // the next tree depends on this one
@@ -54,15 +55,16 @@ int main() {
     CHECK(hipMalloc(&out, 128));
     hipLaunchKernelGGL(k_points<PallasCurve>, dim3(1), dim3(256), 0, 0, pts, 256);
     CHECK(hipDeviceSynchronize());
-    const struct { int block; uint32_t G; } cfg[] = {{64, 64}, {64, 8}, {256, 256}, {256, 64}};
+    const struct { int block; uint32_t G, live; } cfg[] = {{64, 64, 64}, {64, 8, 64}, {256, 256, 64}, {256, 64, 64},
+                                                           {256, 256, 16}, {64, 64, 16}, {64, 64, 1}};
     for (auto c : cfg) {
         hipEvent_t a, b;
         CHECK(hipEventCreate(&a));
         CHECK(hipEventCreate(&b));
-        hipLaunchKernelGGL(k_tree, dim3(1), dim3(c.block), 0, 0, pts, c.G, out);
+        hipLaunchKernelGGL(k_tree, dim3(1), dim3(c.block), 0, 0, pts, c.G, out, c.live);
         CHECK(hipDeviceSynchronize());
         CHECK(hipEventRecord(a));
-        hipLaunchKernelGGL(k_tree, dim3(1), dim3(c.block), 0, 0, pts, c.G, out);
+        hipLaunchKernelGGL(k_tree, dim3(1), dim3(c.block), 0, 0, pts, c.G, out, c.live);
         CHECK(hipEventRecord(b));
         CHECK(hipEventSynchronize(b));
         float ms;
@@ -71,8 +73,8 @@ int main() {
         CHECK(hipMemcpy(h, out, 128, hipMemcpyDeviceToHost));
         uint32_t x = 0;
         for (int i = 0; i < 32; i++) x = x * 31 + h[i];
-        printf("block %3d G %3u: %.2f us per tree (COOP=%d, check %08x)\n", c.block, c.G, ms * 1e3 / ITER,
-               HALO_TREE_COOP, x);
+        printf("block %3d G %3u live %2u: %.2f us per tree (COOP=%d, check %08x)\n", c.block, c.G, c.live,
+               ms * 1e3 / ITER, HALO_TREE_COOP, x);
     }
     return 0;
 }
