@@ -26,7 +26,16 @@ namespace halo {
 
 constexpr int NTT_E = 1024;        // elements per workgroup for passes with R <= 256
 constexpr int NTT_E_BIG = 2048;    // ... and for the two-pass split of 2^17..2^22 (R up to 2048)
-constexpr int NTT_EPT = 4;         // elements per thread (radix-4 register groups)
+constexpr int NTT_EPT = 4;         // elements per thread (radix-4 register groups) on 1024-element blocks
+// ... and on the 2048-element blocks of the 2^17..2^22 passes.  HALO_NTT_EPT_BIG=8 selects radix-8
+// register groups there (three stages per LDS round trip: an 11-bit pass makes 4 LDS round trips and
+// 4 barriers instead of 6), measured slower: 2^22 pair 1.05 -> 1.09 ms (192 VGPRs and 256-thread
+// blocks: 2 waves per SIMD instead of 4, so the barrier waits are hidden worse than they are saved)
+#ifndef HALO_NTT_EPT_BIG
+#define HALO_NTT_EPT_BIG 4
+#endif
+constexpr int NTT_EPT_BIG = HALO_NTT_EPT_BIG;
+constexpr int ntt_lg(int ept) { return ept == 8 ? 3 : 2; }
 constexpr int NTT_MAX_LOG_R_MULTI = 8;
 constexpr int NTT_TW_MAX = 2048;  // stage-twiddle table entries (stages 0..10), read through L1/L2
 constexpr unsigned NTT_FULL_TABLE_MAX_LOG = 24;  // per-pass twiddle tables up to 2^24
@@ -145,19 +154,23 @@ HALO_DEV void ntt_group(Fe<F> (&v)[EPT], uint32_t s, uint32_t G, uint32_t k0, co
 // stage s uses omega_{2^(s+1)}^k0 for both of its butterflies, stage s + 1 omega_{2^(s+2)}^(k0) and
 // ^(k0 + 2^s).  Loaded packed (3 x 32 B) BEFORE the barrier that precedes the group's LDS reads, so
 // the L2 round trip of the table overlaps the barrier wait instead of following it.
+// (LG = 3: stage s + 2 omega_{2^(s+3)}^(k0 + j 2^s), j < 4, as well: 7 twiddles)
+template <int LG>
 struct NttGroupTw {
-    uint4 w[3][2];
+    uint4 w[(1 << LG) - 1][2];
 };
-HALO_DEV void ntt_group_tw_load(NttGroupTw& t, uint32_t s, uint32_t G, uint32_t k0, const uint4* twg) {
-    const uint32_t i0 = (1u << s) - 1u + k0;
-    t.w[0][0] = twg[2 * i0];
-    t.w[0][1] = twg[2 * i0 + 1];
-    if (G > 1) {
-        const uint32_t i1 = (2u << s) - 1u + k0, i2 = i1 + (1u << s);
-        t.w[1][0] = twg[2 * i1];
-        t.w[1][1] = twg[2 * i1 + 1];
-        t.w[2][0] = twg[2 * i2];
-        t.w[2][1] = twg[2 * i2 + 1];
+template <int LG>
+HALO_DEV void ntt_group_tw_load(NttGroupTw<LG>& t, uint32_t s, uint32_t G, uint32_t k0, const uint4* twg) {
+    // stage s + g: omega_{2^(s+g+1)}^(k0 + j 2^s), j < 2^g, at entry 2^(s+g) - 1 + k0 + j 2^s
+#pragma unroll
+    for (int g = 0; g < LG; g++) {
+        if ((uint32_t)g >= G) break;
+#pragma unroll
+        for (int j = 0; j < (1 << g); j++) {
+            const uint32_t i = ((1u << (s + g)) - 1u) + k0 + ((uint32_t)j << s);
+            t.w[(1 << g) - 1 + j][0] = twg[2 * i];
+            t.w[(1 << g) - 1 + j][1] = twg[2 * i + 1];
+        }
     }
 }
 template <class F>
@@ -171,7 +184,7 @@ HALO_DEV Fe<F> ntt_tw_unpack(const uint4 (&w)[2]) {
 // minuend of fe_sub_k (int32 limb chain, |x| < 2^31), and only the values leaving the group are
 // carry-normalized -- two fe_norm per group instead of four.
 template <class F>
-HALO_DEV void ntt_group4_pre(Fe<F> (&v)[4], uint32_t G, const NttGroupTw& t) {
+HALO_DEV void ntt_group4_pre(Fe<F> (&v)[4], uint32_t G, const NttGroupTw<2>& t) {
     {
         const Fe<F> w = ntt_tw_unpack<F>(t.w[0]);
 #pragma unroll
@@ -194,6 +207,40 @@ HALO_DEV void ntt_group4_pre(Fe<F> (&v)[4], uint32_t G, const NttGroupTw& t) {
     }
 }
 
+// The radix-8 group (EPT = 8, three stages s, s + 1, s + 2; always full on the 2048-element blocks:
+// the host splits every such pass so that r - G0 and r - prune are multiples of 3).  Same arithmetic
+// and value bounds as ntt_group: stage s's sums stay limb-unnormalized (limbs < 2^30; they enter stage
+// s + 1 only as multiplication inputs or fe_sub_k minuends), stage s + 1's and s + 2's sums are
+// carry-normalized.
+template <class F>
+HALO_DEV void ntt_group8_pre(Fe<F> (&v)[8], const NttGroupTw<3>& t) {
+    {
+        const Fe<F> w = ntt_tw_unpack<F>(t.w[0]);
+#pragma unroll
+        for (int m = 0; m < 8; m += 2) {
+            const Fe<F> x = fe_mul(v[m + 1], w);
+            v[m + 1] = fe_sub_k<2>(v[m], x);
+            v[m] = fe_add_nc(v[m], x);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        const Fe<F> w = ntt_tw_unpack<F>(t.w[1 + j]);
+#pragma unroll
+        for (int m = j; m < 8; m += 4) {
+            const Fe<F> x = fe_mul(v[m + 2], w);
+            v[m + 2] = fe_sub_k<2>(v[m], x);
+            v[m] = fe_norm(fe_add_nc(v[m], x));
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+        const Fe<F> x = fe_mul(v[m + 4], ntt_tw_unpack<F>(t.w[3 + m]));
+        v[m + 4] = fe_sub_k<2>(v[m], x);
+        v[m] = fe_norm(fe_add_nc(v[m], x));
+    }
+}
+
 // raw workgroup barrier: LDS writes complete, global loads left in flight (a __syncthreads() would
 // also drain them)
 HALO_DEV void ntt_lds_barrier() {
@@ -206,10 +253,9 @@ HALO_DEV void ntt_lds_barrier() {
 // owns T = NTT_E / R consecutive columns.  Each thread holds EPT elements in registers; the first
 // LG stages are done straight from the global loads, the rest in groups of LG stages through LDS,
 // and a final coalesced store phase writes y[(j / Ns) Ns R + (j mod Ns) + k Ns].
-template <class F, int NE>
-__global__ __launch_bounds__(NE / NTT_EPT) void k_ntt_pass(NttPassArgs a) {
-    constexpr int EPT = NTT_EPT;
-    constexpr int LG = 2;
+template <class F, int NE, int EPT>
+__global__ __launch_bounds__(NE / EPT) void k_ntt_pass(NttPassArgs a) {
+    constexpr int LG = ntt_lg(EPT);
     constexpr uint32_t TH = NE / EPT;
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t* data = smem;
@@ -268,8 +314,8 @@ __global__ __launch_bounds__(NE / NTT_EPT) void k_ntt_pass(NttPassArgs a) {
             v[m] = fe_zero<F>();
         }
     }
-    // odd r on the wide blocks: the single-stage group goes first, so later groups stay in range
-    const uint32_t G0 = (NE >= NTT_E_BIG && (r & 1)) ? 1u : (r < (uint32_t)LG ? r : (uint32_t)LG);
+    // on the wide blocks the short group goes first (r mod LG stages), so later groups stay in range
+    const uint32_t G0 = (NE >= NTT_E_BIG && (r % LG)) ? r % LG : (r < (uint32_t)LG ? r : (uint32_t)LG);
     if (!a.prune) ntt_group<F, EPT, LG>(v, 0, G0, 0, a.stage_tw);  // (pruned: host guarantees prune >= G0)
     {
         const uint32_t pb = ntt_swz<NE>(base);
@@ -280,7 +326,7 @@ __global__ __launch_bounds__(NE / NTT_EPT) void k_ntt_pass(NttPassArgs a) {
     // ---- remaining stages in groups of LG through LDS; each group's twiddles are loaded before the
     // barrier that precedes its LDS reads
     uint32_t s = a.prune ? a.prune : G0;
-    NttGroupTw tw;
+    NttGroupTw<LG> tw;
     if (s < r) ntt_group_tw_load(tw, s, (r - s) < (uint32_t)LG ? (r - s) : (uint32_t)LG, tau & ((1u << s) - 1),
                                  a.stage_tw);
     ntt_lds_barrier();
@@ -295,7 +341,10 @@ __global__ __launch_bounds__(NE / NTT_EPT) void k_ntt_pass(NttPassArgs a) {
             const uint32_t ph = (pos ^ shb) ^ ntt_swz_hi<NE>(((uint32_t)m * h) >> 5);
             if (pos < EB) v[m] = lds_get_soa<F>(data, ph, NE);
         }
-        ntt_group4_pre<F>(v, G, tw);
+        if constexpr (LG == 3)
+            ntt_group8_pre<F>(v, tw);  // (G == 3 on every group, see G0)
+        else
+            ntt_group4_pre<F>(v, G, tw);
         // (no barrier here: a thread writes back exactly the positions it read)
 #pragma unroll
         for (int m = 0; m < EPT; m++) {
@@ -485,9 +534,10 @@ static std::vector<unsigned> ntt_radices(unsigned logn) {
 static unsigned ntt_pass0_prune(unsigned lr, unsigned prune) {
     if (!prune) return 0;
     const bool big = lr > NTT_MAX_LOG_R_MULTI;
-    const unsigned g0 = (big && (lr & 1)) ? 1u : std::min(lr, 2u);
+    const unsigned lg = big ? (unsigned)ntt_lg(NTT_EPT_BIG) : 2u;
+    const unsigned g0 = (big && (lr % lg)) ? lr % lg : std::min(lr, lg);
     unsigned pr = std::min(prune, lr);
-    if (big && ((lr - pr) & 1)) pr--;
+    while (big && pr > 0 && ((lr - pr) % lg)) pr--;
     return (pr >= g0 && pr < lr) ? pr : 0u;
 }
 
@@ -590,9 +640,9 @@ static int ntt_device(DeviceState* st, int field, const void* d_in, void* d_out,
         dim3 grid((unsigned)(NJ / T), (unsigned)batch);
         ProfScope prof("ntt_pass", s);
         if (NE == NTT_E_BIG)
-            HALO_LAUNCH(prof, (k_ntt_pass<F, NTT_E_BIG>), grid, dim3(NTT_E_BIG / NTT_EPT), lds, s, a);
+            HALO_LAUNCH(prof, (k_ntt_pass<F, NTT_E_BIG, NTT_EPT_BIG>), grid, dim3(NTT_E_BIG / NTT_EPT_BIG), lds, s, a);
         else
-            HALO_LAUNCH(prof, (k_ntt_pass<F, NTT_E>), grid, dim3(NTT_E / NTT_EPT), lds, s, a);
+            HALO_LAUNCH(prof, (k_ntt_pass<F, NTT_E, NTT_EPT>), grid, dim3(NTT_E / NTT_EPT), lds, s, a);
         HALO_HIP(hipGetLastError());
         log_ns += lr;
     }
