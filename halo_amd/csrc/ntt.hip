@@ -36,6 +36,10 @@ constexpr int NTT_EPT = 4;         // elements per thread (radix-4 register grou
 #endif
 constexpr int NTT_EPT_BIG = HALO_NTT_EPT_BIG;
 constexpr int ntt_lg(int ept) { return ept == 8 ? 3 : 2; }
+#ifndef HALO_NTT_WAVE_SYNC
+#define HALO_NTT_WAVE_SYNC 1
+#endif
+constexpr bool NTT_WAVE_SYNC = HALO_NTT_WAVE_SYNC;
 constexpr int NTT_MAX_LOG_R_MULTI = 8;
 constexpr int NTT_TW_MAX = 2048;  // stage-twiddle table entries (stages 0..10), read through L1/L2
 constexpr unsigned NTT_FULL_TABLE_MAX_LOG = 24;  // per-pass twiddle tables up to 2^24
@@ -242,10 +246,11 @@ HALO_DEV void ntt_group8_pre(Fe<F> (&v)[8], const NttGroupTw<3>& t) {
 }
 
 // raw workgroup barrier: LDS writes complete, global loads left in flight (a __syncthreads() would
-// also drain them)
-HALO_DEV void ntt_lds_barrier() {
+// also drain them).  wave_only: the LDS positions the wave reads next are exactly the ones it just
+// wrote (its own EPT * 64-position chunk), so its own writes completing is enough -- no s_barrier.
+HALO_DEV void ntt_lds_barrier(bool wave_only = false) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    if (!wave_only) __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
 }
 
@@ -329,7 +334,13 @@ __global__ __launch_bounds__(NE / EPT) void k_ntt_pass(NttPassArgs a) {
     NttGroupTw<LG> tw;
     if (s < r) ntt_group_tw_load(tw, s, (r - s) < (uint32_t)LG ? (r - s) : (uint32_t)LG, tau & ((1u << s) - 1),
                                  a.stage_tw);
-    ntt_lds_barrier();
+    // Wave-local exchanges: a group at stage s <= 6 (2^s <= 64) reads and writes exactly its wave's
+    // chunk of EPT * 64 consecutive positions [EPT 64 w, EPT 64 (w + 1)), and so does the load phase
+    // of a one-column block (base = EPT tau); between two such phases the wave only waits for its own
+    // LDS writes (HALO_NTT_WAVE_SYNC=0 A/B: s_barrier everywhere).
+    const bool wave_sync = NTT_WAVE_SYNC && (T == 1u || R < (uint32_t)EPT);
+    bool chunk = wave_sync;
+    ntt_lds_barrier(chunk && s < r && s <= 6);
     for (; s < r; s += LG) {
         const uint32_t G = (r - s) < (uint32_t)LG ? (r - s) : (uint32_t)LG;
         const uint32_t h = 1u << s;
@@ -356,7 +367,8 @@ __global__ __launch_bounds__(NE / EPT) void k_ntt_pass(NttPassArgs a) {
         if (sn < r)
             ntt_group_tw_load(tw, sn, (r - sn) < (uint32_t)LG ? (r - sn) : (uint32_t)LG, tau & ((1u << sn) - 1),
                               a.stage_tw);
-        ntt_lds_barrier();
+        chunk = NTT_WAVE_SYNC && s <= 6;
+        ntt_lds_barrier(chunk && sn < r && sn <= 6);
     }
 
     // ---- store y[(j / Ns) Ns R + (j mod Ns) + k Ns]
