@@ -185,6 +185,55 @@ HALO_DEV XYZZ<F> xyzz_madd_acc(const XYZZ<F>& p, const Affine<F>& q, uint32_t ne
     return r;
 }
 
+// xyzz_madd_acc for k_acc's running bucket sums, with fewer identity tests per addition: the caller
+// tracks whether the accumulator is the identity (`fresh`) instead of testing ZZ, the base point's
+// identity test runs only when the bases may hold one (check_q), and the exceptional case q = +-acc
+// (P = U2 - X1 = 0 mod p) is screened by P's low limb: P < 10p with normalized limbs is a multiple of
+// p only if that limb is < 10 (p = 1 mod 2^29), so the full ZZ3 test runs (almost) never.  Same
+// formula and results as xyzz_madd_acc.
+template <class F>
+HALO_DEV XYZZ<F> xyzz_madd_run(const XYZZ<F>& p, bool& fresh, const Affine<F>& q, uint32_t negmask, bool check_q) {
+    if (check_q && aff_is_id(q)) return p;
+    if (fresh) {
+        fresh = false;
+        XYZZ<F> r;
+        r.X = q.x;
+        r.Y = negmask ? fe_neg(q.y) : q.y;
+        r.ZZ = fe_one<F>();
+        r.ZZZ = fe_one<F>();
+        return r;
+    }
+    const Fe<F> U2 = fe_mul(q.x, p.ZZ);
+    const Fe<F> S2 = fe_mul(q.y, p.ZZZ);
+    const Fe<F> P = fe_sub_k<8>(U2, p.X);              // < 10p
+    const Fe<F> R = fe_sub_k_sgn<4>(S2, p.Y, negmask);  // < 6p
+    const Fe<F> PP = fe_sqr(P);
+    const Fe<F> R2 = fe_sqr(R);
+    const Fe<F> ZZ3 = fe_mul(p.ZZ, PP);
+    const Fe<F> PPP = fe_mul(P, PP);
+    const Fe<F> Q = fe_mul(p.X, PP);
+    XYZZ<F> r;
+    r.X = fe_sub_k<6>(R2, fe_add_nc(PPP, fe_add_nc(Q, Q)));  // < 8p
+    const Fe<F> T = fe_sub_k<8>(Q, r.X);                       // < 10p
+#ifndef HALO_Y3_TWO_MULS
+    r.Y = fe_mul2(R, T, PPP, fe_sub_k<2>(fe_zero<F>(), p.Y));
+#else
+    r.Y = fe_sub(fe_mul(R, T), fe_mul(p.Y, PPP));
+#endif
+    r.ZZ = ZZ3;
+    r.ZZZ = fe_mul(p.ZZZ, PPP);
+    if (P.v[0] < 10u && fe_is_zero(ZZ3)) {  // U2 == X1: q = +-p, off the common path
+        if (fe_is_zero(fe_reduce_8p(R))) {
+            Affine<F> qs = q;
+            if (negmask) qs.y = fe_neg(q.y);
+            return xyzz_mdbl(qs);
+        }
+        fresh = true;
+        return xyzz_id<F>();
+    }
+    return r;
+}
+
 // X of an xyzz_madd_acc accumulator back below 2p (storage needs < 2^256; the general formulas < 2p)
 template <class F>
 HALO_DEV XYZZ<F> xyzz_settle(const XYZZ<F>& p) {

@@ -169,7 +169,7 @@ __device__ __forceinline__ void acc_chunk(size_t t, uint32_t cnt, const uint32_t
                                           const uint4* bases, uint32_t n_per_window, uint32_t npw_lg, size_t stride,
                                           uint32_t blk_lg, uint32_t glv_n, uint4* first, uint4* last,
                                           uint4* bucket_sums, uint32_t* bstart, uint32_t NB, uint32_t key_lg,
-                                          uint32_t poly_off) {
+                                          uint32_t poly_off, bool check_q) {
     using F = typename Cv::Base;
     const size_t beg = t * K;
     if (beg >= cnt) {
@@ -188,6 +188,7 @@ __device__ __forceinline__ void acc_chunk(size_t t, uint32_t cnt, const uint32_t
     }
     bool first_done = false;
     XYZZ<F> acc = xyzz_id<F>();
+    bool fresh = true;  // acc is the identity (xyzz_madd_run)
     for (uint32_t e = (uint32_t)beg; e < end; e++) {
         const uint32_t k = keys[e];
         if (k != cur) {  // bucket boundary inside the chunk
@@ -199,6 +200,7 @@ __device__ __forceinline__ void acc_chunk(size_t t, uint32_t cnt, const uint32_t
                 xyzz_store(bucket_sums + 8 * (size_t)cur, xyzz_settle(acc));
             }
             acc = xyzz_id<F>();
+            fresh = true;
             cur = k;
         }
         const uint32_t v = vals[e];
@@ -214,7 +216,7 @@ __device__ __forceinline__ void acc_chunk(size_t t, uint32_t cnt, const uint32_t
         if (phi) idx -= glv_n;
         Affine<F> p = aff_load<F>(bases + 4 * idx);
         if (phi) p.x = fe_mul(p.x, fe_from_const<F>(Cv::K::BETA));
-        acc = xyzz_madd_acc(acc, p, (v & 0x80000000u) ? ~0u : 0u);
+        acc = xyzz_madd_run(acc, fresh, p, (v & 0x80000000u) ? ~0u : 0u, check_q);
     }
     xyzz_store((first_done ? last : first) + 8 * t, xyzz_settle(acc));
     if (end == cnt)
@@ -229,11 +231,13 @@ __global__ __launch_bounds__(256, HALO_ACC_MINB) void k_acc(const uint32_t* keys
                                              uint32_t K, const uint4* bases, uint32_t n_per_window, uint32_t npw_lg,
                                              size_t stride, uint32_t blk_lg, uint32_t glv_n, uint4* first, uint4* last,
                                              uint4* bucket_sums, uint32_t* work_ctr, uint32_t nblocks, uint32_t* bstart,
-                                             uint32_t NB, uint32_t key_lg = 31, uint32_t poly_off = 0) {
+                                             uint32_t NB, uint32_t key_lg = 31, uint32_t poly_off = 0,
+                                             uint32_t check_q = 1) {
     const uint32_t cnt = *count;
     if constexpr (!PERSIST) {
         acc_chunk<Cv>((size_t)blockIdx.x * blockDim.x + threadIdx.x, cnt, keys, vals, K, bases, n_per_window,
-                                npw_lg, stride, blk_lg, glv_n, first, last, bucket_sums, bstart, NB, key_lg, poly_off);
+                                npw_lg, stride, blk_lg, glv_n, first, last, bucket_sums, bstart, NB, key_lg, poly_off,
+                                check_q != 0);
     } else {
         __shared__ uint32_t sblk;
         for (;;) {
@@ -243,7 +247,8 @@ __global__ __launch_bounds__(256, HALO_ACC_MINB) void k_acc(const uint32_t* keys
             __syncthreads();
             if (blk >= nblocks) break;  // uniform per workgroup: every wave leaves
             acc_chunk<Cv>((size_t)blk * blockDim.x + threadIdx.x, cnt, keys, vals, K, bases, n_per_window,
-                                    npw_lg, stride, blk_lg, glv_n, first, last, bucket_sums, bstart, NB, key_lg, poly_off);
+                                    npw_lg, stride, blk_lg, glv_n, first, last, bucket_sums, bstart, NB, key_lg, poly_off,
+                                check_q != 0);
         }
     }
 }
@@ -352,11 +357,14 @@ __global__ __launch_bounds__(64) void k_final(const uint4* window_sums, int W, i
 // SRS precomputation: window-shifted bases 2^(c w) G_i (w < W) and the hiding table 2^i S
 // ---------------------------------------------------------------------------------------------
 template <class Cv>
-__global__ __launch_bounds__(64) void k_shift_windows(const uint4* gs, size_t n, int c, int W, uint4* out) {
+__global__ __launch_bounds__(64) void k_shift_windows(const uint4* gs, size_t n, int c, int W, uint4* out,
+                                                      uint32_t* has_id) {
     using F = typename Cv::Base;
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const Affine<F> g = aff_load<F>(gs + 4 * i);
+    if (aff_is_id(g)) has_id[0] = 1u;  // (every copy of an identity is the identity; a prime-order
+                                       // group has no other point with 2^(c w) g = 0)
     aff_store(out + 4 * i, g);
     XYZZ<F> p = xyzz_from_aff(g);
     for (int w = 1; w < W; w++) {
@@ -673,13 +681,20 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
             HALO_HIP(hipMemsetAsync(work_ctr, 0, 4, s));
             grid = std::min<unsigned>(nblocks, (unsigned)st->num_cu * msm_acc_wgs_per_cu());
         }
+        // the resident window-shifted SRS without identity points: k_acc skips the bases' identity test
+        const SrsState& srs_c = st->srs[curve_id<Cv>()];
+        const bool srs_bases = shifted && srs_c.shifted_c != 0 && srs_c.shifted.ptr &&
+                               (const char*)bases_int >= srs_c.shifted.as<const char>() &&
+                               (const char*)bases_int < srs_c.shifted.as<const char>() + srs_c.shifted.bytes;
+        const uint32_t check_q = (srs_bases && !srs_c.shifted_has_id) ? 0u : 1u;
         ProfScope prof("msm_acc", s);
         auto kacc = work_ctr ? k_acc<Cv, true> : k_acc<Cv, false>;
         HALO_LAUNCH(prof, kacc, dim3(grid), dim3(256), 0, s, (const uint32_t*)skeys,
                     (const uint32_t*)svals, scount, K, bases_int, (uint32_t)nn, is_pow2(nn) ? ilog2(nn) : 0xffu,
                     (shifted && (shift_stride != nn || blk_lg < 32)) ? shift_stride : (size_t)0, blk_lg,
                     glv ? (uint32_t)nn : 0u, P_first,
-                    P_last, M.bucket_sums.as<uint4>(), work_ctr, nblocks, M.bstart.as<uint32_t>(), (uint32_t)NB, 31u, 0u);
+                    P_last, M.bucket_sums.as<uint4>(), work_ctr, nblocks, M.bstart.as<uint32_t>(), (uint32_t)NB, 31u, 0u,
+                    check_q);
         M.skeys = skeys;
         M.scount = scount;
         HALO_HIP(hipGetLastError());
@@ -813,7 +828,7 @@ static int msm_multi_device_t(DeviceState* st, const void* const* scalars, const
         HALO_LAUNCH(prof, kacc, dim3(nblocks), dim3(256), 0, s, (const uint32_t*)skeys, (const uint32_t*)svals, scount,
                     K, srs.shifted.as<const uint4>(), (uint32_t)ld, is_pow2(ld) ? ilog2(ld) : 0xffu, srs.n, 32u, 0u,
                     P_first, P_last, M.bucket_sums.as<uint4>(), (uint32_t*)nullptr, nblocks, M.bstart.as<uint32_t>(),
-                    (uint32_t)NB, 31u, 0u);
+                    (uint32_t)NB, 31u, 0u, srs.shifted_has_id ? 1u : 0u);
         HALO_HIP(hipGetLastError());
     }
     MsmTailArgs ta;
@@ -933,7 +948,7 @@ static int msm_srs_pairs_t(DeviceState* st, size_t np, const MsmPairIO* io, size
         HALO_LAUNCH(prof, kacc, dim3(nblocks), dim3(256), 0, s, (const uint32_t*)skeys, (const uint32_t*)svals, scount,
                     K, srs.shifted.as<const uint4>(), (uint32_t)half, ilog2(half), srs.n, lgm, 0u, P_first, P_last,
                     M.bucket_sums.as<uint4>(), (uint32_t*)nullptr, nblocks, M.bstart.as<uint32_t>(), (uint32_t)NB,
-                    (uint32_t)(c - 1), (uint32_t)m);
+                    (uint32_t)(c - 1), (uint32_t)m, srs.shifted_has_id ? 1u : 0u);
         HALO_HIP(hipGetLastError());
     }
     MsmTailArgs ta;
@@ -1237,7 +1252,7 @@ static int msm_shared_batch_t(DeviceState* st, const uint4* bases, const uint4* 
     hipLaunchKernelGGL((k_acc<Cv, false>), dim3(grid_for(nchunks, 256)), dim3(256), 0, s, S.keys.as<const uint32_t>(),
                        S.vals.as<const uint32_t>(), (const uint32_t*)(tot + 1), K, bases, 1u, 0u, (size_t)0, 32u, 0u,
                        P_first, P_last, S.bucket_sums.as<uint4>(), (uint32_t*)nullptr, (uint32_t)grid_for(nchunks, 256),
-                       S.bstart.as<uint32_t>(), (uint32_t)NB, 31u, 0u);
+                       S.bstart.as<uint32_t>(), (uint32_t)NB, 31u, 0u, 1u);
     HALO_HIP(hipGetLastError());
     MsmTailArgs ta;
     ta.n = T;
@@ -1495,12 +1510,19 @@ int srs_precompute_windows(DeviceState* st, int curve, hipStream_t s) {
     const int c = msm_shifted_window_bits(srs.n);
     const int W = msm_windows(c);
     HALO_CHECK(srs.shifted.reserve((size_t)W * srs.n * 64));
+    ScratchUse su(st, s);
+    HALO_CHECK(st->scratch[7].reserve(4));
+    uint32_t* flag = st->scratch[7].as<uint32_t>();
+    HALO_HIP(hipMemsetAsync(flag, 0, 4, s));
     DISPATCH_CURVE(curve, Cv, {
         hipLaunchKernelGGL(k_shift_windows<Cv>, dim3(grid_for(srs.n, 64)), dim3(64), 0, s, srs.gs.as<const uint4>(),
-                           srs.n, c, W, srs.shifted.as<uint4>());
+                           srs.n, c, W, srs.shifted.as<uint4>(), flag);
     });
     HALO_HIP(hipGetLastError());
+    uint32_t has_id = 1;
+    HALO_HIP(hipMemcpyAsync(&has_id, flag, 4, hipMemcpyDeviceToHost, s));
     HALO_HIP(hipStreamSynchronize(s));
+    srs.shifted_has_id = has_id != 0;
     srs.shifted_c = c;
     return HALO_OK;
 }

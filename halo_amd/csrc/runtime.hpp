@@ -69,6 +69,7 @@ struct SrsState {
     hipEvent_t small_ev = nullptr;   // last small MSM's completion (orders reuse of small_scr)
     DevBuf shifted;     // optional window-shifted copies
     int shifted_c = 0;  // window bits of `shifted`
+    bool shifted_has_id = true;  // some SRS point is the identity (k_acc then tests every base)
     int shifted_windows = 0;
     // Every writer of `gs` calls this: the tables derived from the old points (window-shifted copies,
     // the small-MSM / tail multiples table) are rebuilt on next use.  (a synthesize after
@@ -76,6 +77,7 @@ struct SrsState {
     void invalidate_derived() {
         shifted_c = 0;
         shifted_windows = 0;
+        shifted_has_id = true;
         small_n0 = 0;
     }
 };
