@@ -524,3 +524,21 @@ def test_window_partitioned_msm_virtual_ranks(hal, corc):
         if world == 3:
             lo, hi = window_range(W, 1, 3)
             assert np.array_equal(parts[1], corc.msm("pallas", g, corc.window_scalars("pallas", sc, c, lo, hi)))
+
+
+@pytest.mark.parametrize("cname,cid", CURVES)
+def test_shifted_srs_with_identity_points(hal, corc, cname, cid):
+    """k_acc skips the bases' identity test only when the window precompute found no identity point in
+    the SRS; an SRS holding identities (WrappedPoint (0, 0)) must keep the test: the window-shifted
+    MSM against the C oracle, with identity points among the bases (and an identity-free SRS after)."""
+    n = 1 << 14  # above the small-table path (n <= 8192): the bucket MSM over the shifted SRS
+    g = corc.srs_generate(cname, n).copy()
+    g[[0, 5, 1000, n - 1]] = 0
+    group.PublicParams.upload(cname, g, precompute_windows=True)
+    for seed in (31, 32):
+        sc = rand_sc(n, seed)
+        assert np.array_equal(pcdl.commit(sc, n - 1, None, cname), corc.msm(cname, g, sc)), seed
+    g2 = corc.srs_generate(cname, n)
+    group.PublicParams.upload(cname, g2, precompute_windows=True)
+    sc = rand_sc(n, 33)
+    assert np.array_equal(pcdl.commit(sc, n - 1, None, cname), corc.msm(cname, g2, sc))
