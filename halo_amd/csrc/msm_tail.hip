@@ -8,6 +8,7 @@
 // build uses the per-column asm chains here as well (HALO_TAIL_COL: 382 ns, tools/micro/fe_mul_bench.hip),
 // and HALO_MAD_ILP remains an A/B build option (arithmetic in the inline namespace halo::ilp then).
 #include <algorithm>
+#include <cstdlib>
 
 #include "dispatch.hpp"
 #include "msm.hpp"
@@ -45,52 +46,70 @@ __global__ __launch_bounds__(MSM_GROUP) void k_group_sums(const uint32_t* keys, 
 // come from the group sums.  A bucket strictly inside one chunk was written by k_acc.  The loop is
 // software-pipelined: the next source's 128 B are loaded before the current addition, so each
 // step's memory latency hides under the previous addition (the lane's chain is latency-bound).
-template <class Cv>
+template <class Cv, int LN>
 __global__ __launch_bounds__(256) void k_merge(const uint32_t* bstart, const uint32_t* count, uint32_t K, size_t nb,
                                                const uint4* first, const uint4* last, const uint4* g1, const uint4* g2,
                                                uint4* bucket_sums) {
     using F = typename Cv::Base;
-    const size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= nb) return;
-    const uint32_t s = bstart[b], e = bstart[b + 1];
-    if (s == e) {
-        xyzz_store(bucket_sums + 8 * b, xyzz_id<F>());
-        return;
-    }
-    const uint32_t cnt = *count;
-    const uint32_t t0 = s / K, t1 = (e - 1) / K;
-    const bool starts = s == t0 * K;  // the bucket is chunk t0's first segment
-    if (t0 == t1 && !starts && e < min(cnt, (t0 + 1) * K)) return;  // interior: done by k_acc
-    constexpr uint32_t G2 = MSM_GROUP * MSM_GROUP;
-    uint32_t t = t0 + 1;
-    auto next_src = [&]() -> const uint4* {
-        const uint4* src;
-        if (t % G2 == 0 && t + G2 <= t1) {
-            src = g2 + 8 * (size_t)(t / G2);
-            t += G2;
-        } else if (t % MSM_GROUP == 0 && t + MSM_GROUP <= t1) {
-            src = g1 + 8 * (size_t)(t / MSM_GROUP);
-            t += MSM_GROUP;
+    // LN lanes per bucket (aligned groups of consecutive lanes): lane j sums the j-th contiguous part of
+    // the bucket's sources, then the parts meet in a shuffle tree -- the chain per lane is 1 / LN as
+    // long and the grid holds LN times the waves (one lane per bucket leaves one wave per SIMD, each
+    // stalled on its dependent additions)
+    const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t b = gid / LN;
+    const uint32_t j = (uint32_t)(gid % LN);
+    bool active = false, starts = false;
+    uint32_t t0 = 0, t1 = 0;
+    if (b < nb) {
+        const uint32_t s = bstart[b], e = bstart[b + 1];
+        if (s == e) {
+            if (j == 0) xyzz_store(bucket_sums + 8 * b, xyzz_id<F>());
         } else {
-            src = first + 8 * (size_t)t;
-            t++;
-        }
-        return src;
-    };
-    // chunk t0's partial starts the sum (no addition to the identity); one addition per step, so
-    // lanes that take different sources do not execute several inlined copies of it
-    XYZZ<F> acc = xyzz_load<F>((starts ? first : last) + 8 * (size_t)t0);
-    if (t <= t1) {
-        XYZZ<F> nxt = xyzz_load<F>(next_src());
-        for (;;) {
-            const XYZZ<F> cur = nxt;
-            const bool more = t <= t1;
-            if (more) nxt = xyzz_load<F>(next_src());
-            acc = xyzz_add(acc, cur);
-            if (!more) break;
+            const uint32_t cnt = *count;
+            t0 = s / K;
+            t1 = (e - 1) / K;
+            starts = s == t0 * K;  // the bucket is chunk t0's first segment
+            active = !(t0 == t1 && !starts && e < min(cnt, (t0 + 1) * K));  // interior: done by k_acc
         }
     }
-    xyzz_store(bucket_sums + 8 * b, acc);
+    XYZZ<F> acc = xyzz_id<F>();
+    if (active) {
+        // this lane's sources: chunks (t0, t1] split in LN contiguous parts [t, tb]
+        const uint32_t total = t1 - t0, per = (total + LN - 1) / LN;
+        uint32_t t = t0 + 1 + j * per;
+        const uint32_t tb = min(t1, t0 + (j + 1) * per);
+        constexpr uint32_t G2 = MSM_GROUP * MSM_GROUP;
+        auto next_src = [&]() -> const uint4* {
+            const uint4* src;
+            if (t % G2 == 0 && t + G2 <= tb) {
+                src = g2 + 8 * (size_t)(t / G2);
+                t += G2;
+            } else if (t % MSM_GROUP == 0 && t + MSM_GROUP <= tb) {
+                src = g1 + 8 * (size_t)(t / MSM_GROUP);
+                t += MSM_GROUP;
+            } else {
+                src = first + 8 * (size_t)t;
+                t++;
+            }
+            return src;
+        };
+        // chunk t0's partial starts lane 0's sum (no addition to the identity); one addition per step,
+        // so lanes that take different sources do not execute several inlined copies of it
+        if (j == 0) acc = xyzz_load<F>((starts ? first : last) + 8 * (size_t)t0);
+        else if (t <= tb) acc = xyzz_load<F>(next_src());
+        if (t <= tb) {
+            XYZZ<F> nxt = xyzz_load<F>(next_src());
+            for (;;) {
+                const XYZZ<F> cur = nxt;
+                const bool more = t <= tb;
+                if (more) nxt = xyzz_load<F>(next_src());
+                acc = xyzz_add(acc, cur);
+                if (!more) break;
+            }
+        }
+    }
+    for (int m = 1; m < LN; m <<= 1) acc = xyzz_add(acc, xyzz_shfl_xor(acc, m));
+    if (active && j == 0) xyzz_store(bucket_sums + 8 * b, acc);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -233,7 +252,13 @@ static int tail_launch_t(const MsmTailArgs& a, hipStream_t ts) {
         if (a.ng2)
             hipLaunchKernelGGL(k_group_sums<Cv>, dim3((unsigned)a.ng2), dim3(MSM_GROUP), 0, ts, a.skeys, a.scount, a.K,
                                MSM_GROUP, (const uint4*)a.g1, a.g2);
-        hipLaunchKernelGGL(k_merge<Cv>, dim3(grid_for_t(a.NB, 256)), dim3(256), 0, ts, (const uint32_t*)a.bstart,
+        static const int lanes = [] {  // HALO_MERGE_LANES: lanes per bucket (1, 2, 4)
+            const char* e = getenv("HALO_MERGE_LANES");
+            const int v = e ? atoi(e) : 2;
+            return v == 1 || v == 4 ? v : 2;
+        }();
+        auto km = lanes == 1 ? k_merge<Cv, 1> : lanes == 4 ? k_merge<Cv, 4> : k_merge<Cv, 2>;
+        hipLaunchKernelGGL(km, dim3(grid_for_t(a.NB * lanes, 256)), dim3(256), 0, ts, (const uint32_t*)a.bstart,
                            a.scount, a.K, a.NB, (const uint4*)a.first, (const uint4*)a.last,
                            (const uint4*)a.g1, (const uint4*)a.g2, a.bucket_sums);
         if (a.batch_windows) {
