@@ -131,7 +131,7 @@ def main():
         if world > 1:
             dist.barrier()
         L.halo_profile_reset()
-        L.halo_profile_enable(1)
+        L.halo_profile_enable(0 if os.environ.get("HALO_BENCH_NOPROF") == "1" else 1)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
