@@ -183,15 +183,40 @@ __global__ __launch_bounds__(64) void k_bitcombine(const uint4* terms, uint32_t 
     using F = typename Cv::Base;
     const uint32_t w = blockIdx.x, k = threadIdx.x;
     XYZZ<F> v = xyzz_id<F>();
-    if (k < NT) {
-        v = xyzz_load<F>(terms + 8 * ((size_t)w * NT + k));
-        const uint32_t d = (k == 0) ? 0 : (k <= logH ? (k - 1 + logL) : (k - 1 - logH));
-        for (uint32_t i = 0; i < d; i++) v = xyzz_dbl(v);
+    const uint32_t D = logH + logL;  // doubling classes d = 0 .. D - 1, one U or V term each (+ T_0 at d = 0)
+#if HALO_TREE_COOP
+    if (D <= 16) {
+        // quad j (lanes 4j .. 4j + 3) doubles the term of class j j times with quad-cooperative doublings
+        // (three product rounds per doubling instead of nine on one lane); then lanes 0 .. D - 1 take the
+        // quads' results, lane D takes T_0, and a tree sums them
+        const uint32_t j = k >> 2;
+        if (j < D) {
+            const uint32_t kt = j < logL ? 1 + logH + j : 1 + (j - logL);  // V_j or U_(j - logL)
+            v = xyzz_load<F>(terms + 8 * ((size_t)w * NT + kt));
+        }
+        for (uint32_t i = 0; i + 1 < D; i++) {
+            const XYZZ<F> d2 = xyzz_dbl_quad(v);
+            if (i < j) v = d2;
+        }
+        v = xyzz_shfl(v, (int)((4 * k) & 63u));
+        if (k == D) v = xyzz_load<F>(terms + 8 * (size_t)w * NT);
+        if (k > D) v = xyzz_id<F>();
+        uint32_t G = 1;
+        while (G < D + 1) G <<= 1;
+        v = wave_group_sum<F>(v, G);
+    } else
+#endif
+    {
+        if (k < NT) {
+            v = xyzz_load<F>(terms + 8 * ((size_t)w * NT + k));
+            const uint32_t d = (k == 0) ? 0 : (k <= logH ? (k - 1 + logL) : (k - 1 - logH));
+            for (uint32_t i = 0; i < d; i++) v = xyzz_dbl(v);
+        }
+        // NT <= 64 terms: a tree over the wave's lanes
+        uint32_t G = 1;
+        while (G < NT) G <<= 1;
+        v = wave_group_sum<F>(v, G);
     }
-    // NT <= 64 terms: a tree over the wave's lanes
-    uint32_t G = 1;
-    while (G < NT) G <<= 1;
-    v = wave_group_sum<F>(v, G);
     if (k != 0) return;
     if (fin == 0) {
         xyzz_store(window_sums + 8 * w, v);

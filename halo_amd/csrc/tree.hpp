@@ -121,6 +121,30 @@ HALO_DEV XYZZ<F> xyzz_add_quad(const XYZZ<F>& v, uint32_t s1, uint32_t s2, bool 
     }
     return r;
 }
+// 2p by the quad (every lane of an aligned quad holds p; every lane gets 2p): xyzz_dbl's nine products
+// in three dependent rounds (V = U^2, X^2 | W = U V, S = X V, M^2, ZZ V | M (S - X3), W Y, W ZZZ),
+// one product per lane per round, exchanged by DPP quad broadcasts.  The identity doubles to a point
+// with ZZ = 0, i.e. the identity again.
+template <class F>
+HALO_DEV XYZZ<F> xyzz_dbl_quad(const XYZZ<F>& p) {
+    const uint32_t role = threadIdx.x & 3u;
+    const uint32_t odd = (role & 1u) ? ~0u : 0u, lo = role < 2 ? ~0u : 0u, r0 = role == 0 ? ~0u : 0u;
+    const Fe<F> U = fe_add_nc(p.Y, p.Y);
+    const Fe<F> t1 = fe_sqr(pick(odd, p.X, U));  // lanes 0, 2: V = U^2; 1, 3: X^2
+    const Fe<F> V = qperm<qp(0, 0, 0, 0)>(t1), X2 = qperm<qp(1, 1, 1, 1)>(t1);
+    const Fe<F> M = fe_norm(fe_add_nc(X2, fe_add_nc(X2, X2)));  // < 6p
+    // lane 0: W = U V; 1: S = X V; 2: M^2; 3: ZZ3 = V ZZ
+    const Fe<F> t2 = fe_mul(pick(lo, pick(odd, p.X, U), pick(odd, V, M)), pick(lo, V, pick(odd, p.ZZ, M)));
+    const Fe<F> W = qperm<qp(0, 0, 0, 0)>(t2), S = qperm<qp(1, 1, 1, 1)>(t2), MM = qperm<qp(2, 2, 2, 2)>(t2);
+    XYZZ<F> r;
+    r.ZZ = qperm<qp(3, 3, 3, 3)>(t2);
+    r.X = fe_reduce_8p(fe_sub_k<4>(MM, fe_add_nc(S, S)));
+    // lane 0: M (S - X3); 1: W Y; 2 (and 3): ZZZ3 = W ZZZ
+    const Fe<F> t3 = fe_mul(pick(r0, M, W), pick(r0, fe_sub_k<2>(S, r.X), pick(odd, p.Y, p.ZZZ)));
+    r.Y = fe_sub(qperm<qp(0, 0, 0, 0)>(t3), qperm<qp(1, 1, 1, 1)>(t3));
+    r.ZZZ = qperm<qp(2, 2, 2, 2)>(t3);
+    return r;
+}
 // sum over aligned groups of G lanes (G a power of two <= 64), valid in the group's first lane.  The
 // points live as a flat list (group g's at lanes [g G, g G + G)); a level turns the list of groups of
 // size gs into one of size gs / 2 by 64 / G * gs / 2 quad additions (16 per batch), each addition's
