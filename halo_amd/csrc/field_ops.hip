@@ -5,6 +5,7 @@
 #include "glv.hpp"
 #include "runtime.hpp"
 #include "msm.hpp"
+#include "tree.hpp"
 
 namespace halo {
 
@@ -70,11 +71,82 @@ HALO_DEV XYZZ<typename Cv::Base> scalar_mul_glv(const Affine<typename Cv::Base>&
     return acc;
 }
 
+#if HALO_TREE_COOP
+// The same scalar multiplication by an aligned quad of lanes (every lane holds P, k and the running
+// sum): the doublings are xyzz_dbl_quad (three product rounds instead of nine) and the additions
+// xyzz_add_quad (four instead of fourteen).  tab: 32 XYZZ of this quad in LDS, d P for d < 16 and
+// phi(d P) at 16 + d.  Quads of one wave that take different digits stay in lockstep: an addition
+// is skipped only when it is trivial for every quad.
+template <class Cv>
+HALO_DEV XYZZ<typename Cv::Base> scalar_mul_glv_quad(const Affine<typename Cv::Base>& P, const uint32_t (&k)[8],
+                                                    uint4* tab) {
+    using F = typename Cv::Base;
+    const uint32_t lane = threadIdx.x & 63u, role = lane & 3u, s1 = lane & ~3u;
+    bool n1, n2;
+    uint32_t k1[5], k2[5];
+    glv::decompose<typename Cv::K>(k, n1, k1, n2, k2);
+    const XYZZ<F> p1 = xyzz_from_aff(P);
+    // acc + t (t the same in every lane of the quad; trivial when either is the identity)
+    auto add = [&](const XYZZ<F>& acc, const XYZZ<F>& t, bool tid) -> XYZZ<F> {
+        const bool idp = xyzz_is_id(acc), idq = tid || xyzz_is_id(t);
+        XYZZ<F> r = xyzz_id<F>();
+        if (!__all(idp || idq)) r = xyzz_add_quad(role == 1 ? t : acc, s1, s1 + 1, idp, idq);
+        const XYZZ<F> sum = xyzz_shfl(r, (int)(s1 + 2));
+        return idq ? acc : (idp ? t : sum);
+    };
+    if (role == 0) {
+        xyzz_store(tab, xyzz_id<F>());
+        xyzz_store(tab + 8, p1);
+    }
+    XYZZ<F> prev = p1;  // d P for the previous d
+    for (int d = 2; d < 16; d++) {
+        const XYZZ<F> v = (d & 1) ? add(prev, p1, false) : xyzz_dbl_quad(xyzz_load<F>(tab + 8 * (d / 2)));
+        if (role == 0) xyzz_store(tab + 8 * d, v);
+        __syncthreads();  // (one wave per block: the quad's other lanes read entry d / 2 next)
+        prev = v;
+    }
+    // phi(d P) = (beta X, Y, ZZ, ZZZ): lane r of the quad forms d = r, r + 4, r + 8, r + 12
+    const Fe<F> beta = fe_from_const<F>(Cv::K::BETA);
+    for (int j = 0; j < 4; j++) {
+        const int d = (int)role + 4 * j;
+        XYZZ<F> t = xyzz_load<F>(tab + 8 * d);
+        t.X = fe_mul(t.X, beta);
+        xyzz_store(tab + 8 * (16 + d), t);
+    }
+    __syncthreads();
+    XYZZ<F> acc = xyzz_id<F>();
+    for (int w = 32; w >= 0; w--) {  // 33 windows cover 132 bits
+        if (w != 32)
+            for (int b = 0; b < 4; b++) acc = xyzz_dbl_quad(acc);
+        const int q = (4 * w) >> 5, sh = (4 * w) & 31;
+        const uint32_t d1 = (k1[q] >> sh) & 15u, d2 = (k2[q] >> sh) & 15u;
+        XYZZ<F> t = xyzz_load<F>(tab + 8 * d1);
+        if (n1) t.Y = fe_neg(t.Y);
+        acc = add(acc, t, d1 == 0);
+        t = xyzz_load<F>(tab + 8 * (16 + d2));
+        if (n2) t.Y = fe_neg(t.Y);
+        acc = add(acc, t, d2 == 0);
+    }
+    return acc;
+}
+#endif
+
 template <class Cv>
 __global__ __launch_bounds__(64) void k_curve_op(int op, const uint4* a, const uint4* b, const uint4* k, uint4* out, size_t n) {
     using F = typename Cv::Base;
     using S = typename Cv::Scalar;
     extern __shared__ uint4 smul_tab[];  // op 2: 16 XYZZ (128 B) per lane
+#if HALO_TREE_COOP
+    if (op == 2) {  // one quad per scalar multiplication (the quad's lanes share i: it leaves whole)
+        const size_t i = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2;
+        if (i >= n) return;
+        uint32_t w[8];
+        fe_ark_to_canonical_words<S>(k + 2 * i, w);
+        const XYZZ<F> r = scalar_mul_glv_quad<Cv>(aff_from_wrapped<F>(a + 4 * i), w, smul_tab + 32 * 8 * (threadIdx.x >> 2));
+        if ((threadIdx.x & 3u) == 0) aff_to_wrapped(out + 4 * i, xyzz_to_aff(r));
+        return;
+    }
+#endif
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     Affine<F> p = aff_from_wrapped<F>(a + 4 * i);
@@ -141,8 +213,15 @@ extern "C" int halo_curve_op(halo_curve_t curve, int op, const halo_wrapped_poin
     HALO_CHECK(copy_h2d(st->scratch[0].ptr, a, pb, s));
     if (b) HALO_CHECK(copy_h2d(st->scratch[1].ptr, b, pb, s));
     if (k) HALO_CHECK(copy_h2d(st->scratch[2].ptr, k, kb, s));
+#if HALO_TREE_COOP
+    // op 2: a quad per scalar multiplication, 32 table entries of 128 B per quad
+    const size_t lanes = op == 2 ? 4 * n : n;
+    const unsigned threads = op == 2 ? 4 * CURVE_OP_SMUL_THREADS : 64, blocks = (unsigned)((lanes + threads - 1) / threads);
+    const size_t smem = op == 2 ? (size_t)(threads / 4) * 32 * 128 : 0;
+#else
     const unsigned threads = op == 2 ? CURVE_OP_SMUL_THREADS : 64, blocks = (unsigned)((n + threads - 1) / threads);
     const size_t smem = op == 2 ? (size_t)threads * 16 * 128 : 0;
+#endif
     DISPATCH_CURVE(curve, Cv, {
         hipLaunchKernelGGL(k_curve_op<Cv>, dim3(blocks), dim3(threads), smem, s, op, st->scratch[0].as<const uint4>(),
                            st->scratch[1].as<const uint4>(), st->scratch[2].as<const uint4>(),

@@ -330,29 +330,6 @@ __global__ __launch_bounds__(64) void k_pairs_out(const uint4* window_sums, cons
     xyzz_store(outs.o[p], xyzz_add(xyzz_load<F>(window_sums + 8 * p), xyzz_load<F>(hide + 8 * p)));
 }
 
-// Horner over the window sums (one lane; the c doublings per window run in Jacobian coordinates),
-// plus the precomputed hiding term (or null), -> affine -> ark WrappedPoint.
-template <class Cv>
-__global__ __launch_bounds__(64) void k_final(const uint4* window_sums, int W, int c, const uint4* hide_xyzz,
-                                              uint4* out_wrapped, int xyzz_out) {
-    using F = typename Cv::Base;
-    if (threadIdx.x != 0) return;
-    XYZZ<F> horner = xyzz_id<F>();
-    for (int w = W - 1; w >= 0; w--) {
-        if (w != W - 1 && !xyzz_is_id(horner)) {
-            Jac<F> j = jac_from_xyzz(horner);
-            for (int k = 0; k < c; k++) j = jac_dbl(j);
-            horner = jac_to_xyzz(j);
-        }
-        horner = xyzz_add(horner, xyzz_load<F>(window_sums + 8 * w));
-    }
-    if (hide_xyzz) horner = xyzz_add(horner, xyzz_load<F>(hide_xyzz));
-    if (xyzz_out)  // 128 B packed XYZZ: the host converts (halo_ipa_round_lr, no inversion on the lane)
-        xyzz_store(out_wrapped, horner);
-    else
-        aff_to_wrapped(out_wrapped, xyzz_to_aff(horner));
-}
-
 // ---------------------------------------------------------------------------------------------
 // SRS precomputation: window-shifted bases 2^(c w) G_i (w < W) and the hiding table 2^i S
 // ---------------------------------------------------------------------------------------------
@@ -747,8 +724,8 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
     }
     HALO_CHECK(msm_tail_launch(curve_id<Cv>(), ta, ts));
     if (!fuse)
-        hipLaunchKernelGGL(k_final<Cv>, dim3(1), dim3(64), 0, ts, M.window_sums.as<const uint4>(), SW, c,
-                           (const uint4*)hide_slot, d_out_wrapped, (int)out_xyzz);
+        HALO_CHECK(msm_final_launch(curve_id<Cv>(), M.window_sums.as<const uint4>(), SW, c, (const uint4*)hide_slot,
+                                    d_out_wrapped, (int)out_xyzz, ts));
     HALO_HIP(hipGetLastError());
     HALO_HIP(hipEventRecord(M.tail_done, ts));
     M.tail_pending = true;

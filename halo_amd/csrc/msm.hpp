@@ -126,5 +126,8 @@ struct MsmTailArgs {
     uint4* final_out = nullptr;
 };
 int msm_tail_launch(int curve, const MsmTailArgs& a, hipStream_t ts);
+// Horner over W window sums (+ the hiding term) -> ark WrappedPoint, or packed XYZZ (xyzz_out)
+int msm_final_launch(int curve, const uint4* window_sums, int W, int c, const uint4* hide, uint4* out, int xyzz_out,
+                     hipStream_t s);
 
 }  // namespace halo

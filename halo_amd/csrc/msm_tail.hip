@@ -1,6 +1,6 @@
-// MSM reduction tail: chunk-partial merge and the bucket reduction
-// sum_i (i + 1) B_i per window (k_final, the single-wave Horner, stays in msm.hip: measured faster
-// with the single-chain multiplication).
+// MSM reduction tail: chunk-partial merge, the bucket reduction
+// sum_i (i + 1) B_i per window and the Horner over the windows (k_final; since the quad-cooperative
+// doublings it is latency-bound like the rest, so it takes this unit's per-column multiplication).
 //
 // Every kernel here is latency-bound (a few waves doing dependent chains of curve additions).  Round 2
 // compiled this translation unit with HALO_MAD_ILP (the compiler's split column sums: 418 vs 523 ns
@@ -266,6 +266,51 @@ __global__ __launch_bounds__(256) void k_batch_window_sums(const uint4* bucket_s
     if (k == 0 && w < SW) xyzz_store(window_sums + 8 * w, v);
 }
 
+// Horner over the window sums (the c doublings per window run in Jacobian coordinates),
+// plus the precomputed hiding term (or null), -> affine -> ark WrappedPoint.
+template <class Cv>
+__global__ __launch_bounds__(64) void k_final(const uint4* window_sums, int W, int c, const uint4* hide_xyzz,
+                                              uint4* out_wrapped, int xyzz_out) {
+    using F = typename Cv::Base;
+    XYZZ<F> horner = xyzz_id<F>();
+#if HALO_TREE_COOP
+    // every quad of the wave runs the same Horner chain (identical data, so every branch is uniform):
+    // quad-cooperative doublings (3 product rounds instead of 7) and additions (4 instead of 14)
+    const uint32_t s1 = threadIdx.x & 60u;
+    for (int w = W - 1; w >= 0; w--) {
+        if (w != W - 1 && !xyzz_is_id(horner)) {
+            Jac<F> j = jac_from_xyzz(horner);
+            for (int k = 0; k < c; k++) j = jac_dbl_quad(j);
+            horner = jac_to_xyzz(j);
+        }
+        const XYZZ<F> ws = xyzz_load<F>(window_sums + 8 * w);
+        const bool idp = xyzz_is_id(horner), idq = xyzz_is_id(ws);
+        if (idp || idq) {
+            if (idp) horner = ws;
+        } else {
+            const XYZZ<F> r = xyzz_add_quad((threadIdx.x & 3u) == 1 ? ws : horner, s1, s1 + 1, false, false);
+            horner = xyzz_shfl(r, (int)(s1 + 2));
+        }
+    }
+    if (threadIdx.x != 0) return;
+#else
+    if (threadIdx.x != 0) return;
+    for (int w = W - 1; w >= 0; w--) {
+        if (w != W - 1 && !xyzz_is_id(horner)) {
+            Jac<F> j = jac_from_xyzz(horner);
+            for (int k = 0; k < c; k++) j = jac_dbl(j);
+            horner = jac_to_xyzz(j);
+        }
+        horner = xyzz_add(horner, xyzz_load<F>(window_sums + 8 * w));
+    }
+#endif
+    if (hide_xyzz) horner = xyzz_add(horner, xyzz_load<F>(hide_xyzz));
+    if (xyzz_out)  // 128 B packed XYZZ: the host converts (halo_ipa_round_lr, no inversion on the lane)
+        xyzz_store(out_wrapped, horner);
+    else
+        aff_to_wrapped(out_wrapped, xyzz_to_aff(horner));
+}
+
 static unsigned grid_for_t(size_t n, unsigned thr) { return (unsigned)std::max<size_t>(1, (n + thr - 1) / thr); }
 
 template <class Cv>
@@ -304,6 +349,15 @@ static int tail_launch_t(const MsmTailArgs& a, hipStream_t ts) {
         hipLaunchKernelGGL(k_bitcombine<Cv>, dim3(a.SW), dim3(64), 0, ts, (const uint4*)a.terms, a.NT, a.logH, a.logL,
                            a.window_sums, fin, a.final_hide, a.final_out);
     }
+    HALO_HIP(hipGetLastError());
+    return HALO_OK;
+}
+
+int msm_final_launch(int curve, const uint4* window_sums, int W, int c, const uint4* hide, uint4* out, int xyzz_out,
+                     hipStream_t s) {
+    DISPATCH_CURVE(curve, Cv, {
+        hipLaunchKernelGGL(k_final<Cv>, dim3(1), dim3(64), 0, s, window_sums, W, c, hide, out, xyzz_out);
+    });
     HALO_HIP(hipGetLastError());
     return HALO_OK;
 }

@@ -542,3 +542,23 @@ def test_shifted_srs_with_identity_points(hal, corc, cname, cid):
     group.PublicParams.upload(cname, g2, precompute_windows=True)
     sc = rand_sc(n, 33)
     assert np.array_equal(pcdl.commit(sc, n - 1, None, cname), corc.msm(cname, g2, sc))
+
+
+@pytest.mark.parametrize("cname,cid", CURVES)
+def test_msm_caller_bases_sparse_windows(hal, corc, cname, cid):
+    """k_final's Horner over the window sums (caller bases, GLV windows): window sums that are the
+    identity at the top, in the middle and at the bottom of the chain (scalars built from a few set
+    bits), and a single term, against the C oracle."""
+    c = P.CURVES[cname]
+    g = corc.srs_generate(cname, 64)
+    cases = [
+        [1] * 64,                                           # only window 0
+        [1 << 200] * 64,                                     # only a high window (GLV: both halves)
+        [(1 << 250) + 1] * 32 + [1 << 100] * 32,             # top and bottom, empty middle
+        [(c.scalar - 1)] + [0] * 63,                         # one term, r - 1
+        list(range(64)),                                     # small scalars: empty upper windows
+    ]
+    for k, vals in enumerate(cases):
+        sc = fe(vals, c.scalar)
+        exp = corc.msm(cname, g, sc)
+        assert np.array_equal(group.point_dot_affine(sc, g, cname), exp), k
