@@ -275,13 +275,22 @@ __global__ __launch_bounds__(FOLD_THREADS, 4) void k_ipa_fold(uint4* gs, uint4* 
 template <class Cv>
 __global__ __launch_bounds__(64) void k_pow2_xyzz_from_wrapped(const uint4* P_wrapped, uint4* out_xyzz, int count) {
     using F = typename Cv::Base;
-    if (threadIdx.x != 0) return;
     // the doubling chain runs in Jacobian coordinates (dbl-2009-l: 1M + 5S, vs 6M + 3S in XYZZ); the
-    // per-entry XYZZ conversion (Z^2, Z^3) is off the chain's dependency path
+    // per-entry XYZZ conversion (Z^2, Z^3) is off the chain's dependency path.  Quad-cooperative
+    // doublings (lanes 0-3, jac_dbl_quad) when the tree code is cooperative.
+#if HALO_TREE_COOP
+    if (threadIdx.x >= 4) return;
+#else
+    if (threadIdx.x != 0) return;
+#endif
     Jac<F> j = jac_from_xyzz(xyzz_from_aff(aff_from_wrapped<F>(P_wrapped)));
     for (int i = 0; i < count; i++) {
-        xyzz_store(out_xyzz + 8 * i, jac_to_xyzz(j));
+        if (threadIdx.x == 0) xyzz_store(out_xyzz + 8 * i, jac_to_xyzz(j));
+#if HALO_TREE_COOP
+        j = jac_dbl_quad(j);
+#else
         j = jac_dbl(j);
+#endif
     }
 }
 
@@ -344,18 +353,30 @@ constexpr int TAIL_WIN = 2 * TAIL_TBL;  // terms per point: 32 windows x (k1, k2
 // waves' quad trees then share a SIMD's issue slots)
 constexpr int TAIL_THREADS = 256;
 
-// the doubling chain in Jacobian coordinates (dbl-2009-l: 7 multiplications against XYZZ's 9)
+// the doubling chain in Jacobian coordinates (dbl-2009-l: 7 multiplications against XYZZ's 9), by a
+// quad of lanes per point (jac_dbl_quad: three product rounds per doubling; TAIL_TABLE_LANES = 4) --
+// the chain is latency-bound and the grid is small (n0 <= 8192 points)
+#if HALO_TREE_COOP
+constexpr int TAIL_TABLE_LANES = 4;
+#else
+constexpr int TAIL_TABLE_LANES = 1;
+#endif
 template <class Cv>
 __global__ __launch_bounds__(64) void k_tail_table(const uint4* gs, int gs_xyzz, size_t n0, uint4* table) {
     using F = typename Cv::Base;
-    const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n0) return;
+    const size_t k = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / TAIL_TABLE_LANES;
+    if (k >= n0) return;  // (whole quads leave)
+    const bool lead = threadIdx.x % TAIL_TABLE_LANES == 0;
     const XYZZ<F> p0 = gs_xyzz ? xyzz_load<F>(gs + 8 * k) : xyzz_from_aff(aff_load<F>(gs + 4 * k));
-    xyzz_store(table + 8 * k, p0);
+    if (lead) xyzz_store(table + 8 * k, p0);
     Jac<F> j = jac_from_xyzz(p0);
     for (int w = 1; w < TAIL_TBL; w++) {
+#if HALO_TREE_COOP
+        for (int b = 0; b < TAIL_DB; b++) j = jac_dbl_quad(j);
+#else
         for (int b = 0; b < TAIL_DB; b++) j = jac_dbl(j);
-        xyzz_store(table + 8 * ((size_t)w * TAIL_MUL * n0 + k), jac_to_xyzz(j));
+#endif
+        if (lead) xyzz_store(table + 8 * ((size_t)w * TAIL_MUL * n0 + k), jac_to_xyzz(j));
     }
 }
 
@@ -1513,7 +1534,7 @@ static int ipa_enter_tail(DeviceState* st, halo_ipa_session* ses, hipStream_t s)
         if (!ses->gs_valid) return set_error(HALO_EINVAL, "ipa tail: G not resident");
         HALO_CHECK(ses->own_table.reserve((size_t)TAIL_TBL * TAIL_MUL * n0 * 128));
         DISPATCH_CURVE(ses->curve, Cv, {
-            hipLaunchKernelGGL(k_tail_table<Cv>, dim3(gridn(n0, 64)), dim3(64), 0, s, ses->gs.as<const uint4>(),
+            hipLaunchKernelGGL(k_tail_table<Cv>, dim3(gridn((size_t)TAIL_TABLE_LANES * n0, 64)), dim3(64), 0, s, ses->gs.as<const uint4>(),
                                (int)ses->gs_xyzz, n0, ses->own_table.as<uint4>());
             hipLaunchKernelGGL(k_tail_mults<Cv>, dim3(gridn((size_t)TAIL_MLANES * TAIL_TBL * n0, 64)), dim3(64), 0, s, n0,
                                ses->own_table.as<uint4>());
@@ -1604,7 +1625,7 @@ int halo::srs_small_table(DeviceState* st, int curve, hipStream_t s) {
     if (srs.small_ev) HALO_HIP(hipStreamWaitEvent(s, srs.small_ev, 0));  // the old table's last reader
     HALO_CHECK(srs.small_tab.reserve((size_t)TAIL_TBL * TAIL_MUL * n0 * 128));
     DISPATCH_CURVE(curve, Cv, {
-        hipLaunchKernelGGL(k_tail_table<Cv>, dim3(gridn(n0, 64)), dim3(64), 0, s, srs.gs.as<const uint4>(), 0, n0,
+        hipLaunchKernelGGL(k_tail_table<Cv>, dim3(gridn((size_t)TAIL_TABLE_LANES * n0, 64)), dim3(64), 0, s, srs.gs.as<const uint4>(), 0, n0,
                            srs.small_tab.as<uint4>());
         hipLaunchKernelGGL(k_tail_mults<Cv>, dim3(gridn((size_t)TAIL_MLANES * TAIL_TBL * n0, 64)), dim3(64), 0, s, n0,
                            srs.small_tab.as<uint4>());
