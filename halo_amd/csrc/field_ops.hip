@@ -135,15 +135,16 @@ template <class Cv>
 __global__ __launch_bounds__(64) void k_curve_op(int op, const uint4* a, const uint4* b, const uint4* k, uint4* out, size_t n) {
     using F = typename Cv::Base;
     using S = typename Cv::Scalar;
-    extern __shared__ uint4 smul_tab[];  // op 2: 16 XYZZ (128 B) per lane
+    extern __shared__ uint4 smul_tab[];  // op 2: 32 XYZZ (128 B) per quad (16 per lane without HALO_TREE_COOP)
 #if HALO_TREE_COOP
-    if (op == 2) {  // one quad per scalar multiplication (the quad's lanes share i: it leaves whole)
+    if (op == 2) {  // one quad per scalar multiplication; quads past n repeat the last one (no store), so
+                    // every lane reaches the table build's barriers
         const size_t i = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2;
-        if (i >= n) return;
+        const size_t ic = i < n ? i : n - 1;
         uint32_t w[8];
-        fe_ark_to_canonical_words<S>(k + 2 * i, w);
-        const XYZZ<F> r = scalar_mul_glv_quad<Cv>(aff_from_wrapped<F>(a + 4 * i), w, smul_tab + 32 * 8 * (threadIdx.x >> 2));
-        if ((threadIdx.x & 3u) == 0) aff_to_wrapped(out + 4 * i, xyzz_to_aff(r));
+        fe_ark_to_canonical_words<S>(k + 2 * ic, w);
+        const XYZZ<F> r = scalar_mul_glv_quad<Cv>(aff_from_wrapped<F>(a + 4 * ic), w, smul_tab + 32 * 8 * (threadIdx.x >> 2));
+        if (i < n && (threadIdx.x & 3u) == 0) aff_to_wrapped(out + 4 * i, xyzz_to_aff(r));
         return;
     }
 #endif
