@@ -213,13 +213,10 @@ def main():
             return best
 
         best = run_open()
-        # the same opening with GLV folds of G every round (HALO_IPA_WEIGHTED=0): the fold kernel rate
-        # for extra.cpu_ipa_fold, and the A/B of the weighted rounds; results must agree
-        os.environ["HALO_IPA_WEIGHTED"] = "0"
-        try:
+        # the same opening with GLV folds of G every round (tuning ipa_weighted = 0): the fold kernel
+        # rate for extra.cpu_ipa_fold, and the A/B of the weighted rounds; results must agree
+        with H.tuning(ipa_weighted=0):
             fold_path = run_open()
-        finally:
-            del os.environ["HALO_IPA_WEIGHTED"]
         return {
             "workload": f"pcdl open round loop 2^{logn} (lg n rounds of L/R + fold, weighted then tail rounds), "
                         "device-resident",
@@ -1019,7 +1016,7 @@ def cpu_fold_baseline(L, H, curve, logm, ipa):
         "gpu_matches_cpu": bool(ok),
         "gpu_elements_per_s": gpu_rate,
         "gpu_note": "device GLV fold kernels over the folded rounds of the 2^logn opening with "
-                    "HALO_IPA_WEIGHTED=0 (extra.ipa_open.glv_fold_path); the default opening never folds G",
+                    "tuning ipa_weighted = 0 (extra.ipa_open.glv_fold_path); the default opening never folds G",
     }
 
 

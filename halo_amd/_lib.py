@@ -51,6 +51,8 @@ SIGNATURES = {
     "halo_last_error": [],
     "halo_abi_version": [],
     "halo_stream_sync": [_vp],
+    "halo_set_tuning": [ctypes.c_char_p, ctypes.c_longlong],
+    "halo_get_tuning": [ctypes.c_char_p, ctypes.POINTER(ctypes.c_longlong)],
     "halo_srs_upload": [ctypes.c_int, _vp, _sz, _vp, _vp],
     "halo_srs_len": [ctypes.c_int, ctypes.POINTER(_sz)],
     "halo_srs_synthesize": [ctypes.c_int, _sz, ctypes.c_uint64],
@@ -221,3 +223,34 @@ def fe_array(a, n: int | None = None) -> np.ndarray:
 
 def point_array(a) -> np.ndarray:
     return np.ascontiguousarray(np.asarray(a, dtype=np.uint64).reshape(-1, 8))
+
+
+def set_tuning(key: str, value: int) -> None:
+    """halo_set_tuning: a library-wide path selection (value -1 restores the default)."""
+    check(load().halo_set_tuning(key.encode(), int(value)))
+
+
+def get_tuning(key: str) -> int:
+    v = ctypes.c_longlong(0)
+    check(load().halo_get_tuning(key.encode(), ctypes.byref(v)))
+    return v.value
+
+
+class tuning:
+    """Context manager: ``with tuning(ipa_weighted=0): ...`` sets the keys and restores the previous
+    values on exit (the parity tests pin the IPA / commitment paths with it)."""
+
+    def __init__(self, **kv):
+        self.kv = kv
+        self.prev = {}
+
+    def __enter__(self):
+        for k, v in self.kv.items():
+            self.prev[k] = get_tuning(k)
+            set_tuning(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self.prev.items():
+            set_tuning(k, v)
+        return False

@@ -742,8 +742,7 @@ struct halo_ipa_session {
     // ---- resources (kept across pooled uses)
     int device = -1;
     hipStream_t s = nullptr;
-    hipStream_t aux = nullptr;        // builds the 2^i H' table beside round 1's accumulation
-    hipEvent_t htab_ready = nullptr;  // recorded on aux after the table
+    hipEvent_t htab_ready = nullptr;  // recorded after the session's own 2^i H' table
     uint8_t* pinned = nullptr;  // [128, 192) xi|xi_inv (H2D), [256, 512) L|R XYZZ (D2H): async, several sessions in flight
     DevBuf gs, cs, zs, htab, small, tmp, pbar;
     DevBuf cs2, zs2;  // ping-pong partners of cs / zs (tail rounds with a deferred fold)
@@ -764,6 +763,7 @@ struct halo_ipa_session {
     int wcur = 0;
     const uint4* table = nullptr;  // tail multiples table: own_table, or the SRS's small table
     size_t table_ld = 0;
+    std::shared_ptr<DevBuf> table_ref;  // keeps the SRS's table alive while the session reads it
     bool fold_inflight = false;       // a fold's H2D copy of xi may still read `pinned`
     bool fold_pending = false;        // tail rounds: the last fold is applied by the next launch (k_tail_prep)
     halo_fe_t pend_xi{}, pend_xinv{};
@@ -792,14 +792,10 @@ struct halo_ipa_session {
     }
     void destroy() {
         if (s) (void)hipStreamSynchronize(s);
-        if (aux) {
-            (void)hipStreamSynchronize(aux);
-            (void)hipStreamDestroy(aux);
-        }
         if (htab_ready) (void)hipEventDestroy(htab_ready);
         if (s) (void)hipStreamDestroy(s);
         if (pinned) (void)hipHostFree(pinned);
-        s = aux = nullptr;
+        s = nullptr;
         htab_ready = nullptr;
         pinned = nullptr;
         for (DevBuf* b : {&gs, &cs, &zs, &cs2, &zs2, &htab, &small, &tmp, &pbar, &own_table, &w[0], &w[1], &scal, &side,
@@ -830,13 +826,10 @@ halo_ipa_session* ipa_acquire(DeviceState* st) {
     }
     auto* ses = new halo_ipa_session();
     ses->device = st->device;
-    // the side stream for the H' table only when the runtime has hardware queues to spare
-    // (GPU_MAX_HW_QUEUES >= 8, as bench.py sets): with HIP's default 4 the extra stream shares a queue
-    // with the session's and the MSM tail streams, which cost ~0.3 ms per 2^16 round
-    const char* hwq = getenv("GPU_MAX_HW_QUEUES");
-    const bool use_aux = hwq && atoi(hwq) >= 8;
+    // one stream per session (a side stream for the H' table of explicit-H' sessions was measured: with
+    // HIP's default 4 hardware queues it shares a queue with the MSM tail streams, ~0.3 ms per 2^16
+    // round; the prover's and pcdl::open's sessions use the resident 2^i H tables and build none)
     if (hipStreamCreateWithFlags(&ses->s, hipStreamNonBlocking) != hipSuccess ||
-        (use_aux && hipStreamCreateWithFlags(&ses->aux, hipStreamNonBlocking) != hipSuccess) ||
         hipEventCreateWithFlags(&ses->htab_ready, hipEventDisableTiming) != hipSuccess ||
         hipHostMalloc((void**)&ses->pinned, 512, hipHostMallocDefault) != hipSuccess) {
         ses->destroy();
@@ -852,9 +845,12 @@ halo_ipa_session* ipa_acquire(DeviceState* st) {
 void ipa_release(halo_ipa_session* ses) {
     if (!ses) return;
     if (ses->s) (void)hipStreamSynchronize(ses->s);
-    if (ses->aux) (void)hipStreamSynchronize(ses->aux);
+    ses->table_ref.reset();  // a retired SRS multiples table is freed with its last session
     {
         std::lock_guard<std::mutex> g(g_pool_mu);
+        // a session already idle (a second end of the same handle) is not pooled twice: two later
+        // openings would otherwise share its streams and buffers
+        if (std::find(g_pool.begin(), g_pool.end(), ses) != g_pool.end()) return;
         size_t same = 0;
         for (halo_ipa_session* p : g_pool) same += p->device == ses->device;
         if (same < IPA_POOL_MAX) {
@@ -1066,34 +1062,18 @@ extern "C" int halo_poly_mul(halo_field_t field, const halo_fe_t* a, size_t la, 
 // Session start shared by halo_ipa_begin (G = resident SRS prefix, z powers generated on the
 // device) and halo_ipa_begin_vectors (explicit G, c, z: a shard of a distributed opening or its
 // final collapsed rounds, halo_amd/dist.py).
-static size_t ipa_tail_n() {
-    static const size_t tail_n = [] {
-        const char* e = getenv("HALO_IPA_TAIL_N");  // A/B knob; default IPA_TAIL_N
-        return e ? (size_t)atoll(e) : IPA_TAIL_N;
-    }();
-    return tail_n;
-}
+static size_t ipa_tail_n() { return IPA_TAIL_N; }
 
-static size_t env_size(const char* name, size_t dflt) {
-    const char* e = getenv(name);
-    return e ? (size_t)atoll(e) : dflt;
-}
 // 8192 points (0.5 GB of XYZZ multiples per curve): the small MSMs up to 2^13 and the openings up to
 // 2^13 run entirely on the table (tail rounds from round 1, no weighted rounds, no materialisation)
-size_t halo::srs_tab_n() {
-    static const size_t v = env_size("HALO_SRS_TAB_N", 8192);  // A/B knob
-    return v;
-}
-size_t halo::srs_small_max() {
-    static const size_t v = std::min(env_size("HALO_SRS_SMALL_N", srs_tab_n()), srs_tab_n());  // A/B knob
-    return v;
-}
+size_t halo::srs_tab_n() { return 8192; }
+size_t halo::srs_small_max() { return srs_tab_n(); }
 // SRS sessions of n <= this start in the tail rounds over the SRS's table.  A tail round costs ~64 n0
 // table terms: measured per round (hiding open, tools/pcdl_open_time.py) 0.23 ms at n0 = 4096 against
 // 0.29 ms for the weighted path's average (opening 2^12: 5.95 -> 3.86 ms), but 0.33 ms at n0 = 8192,
 // where the weighted rounds are cheaper.
-static size_t ipa_srs_tail_max() {  // (read per session: the tests pin the other paths with it)
-    return std::min(env_size("HALO_IPA_SRS_TAIL_N", 4096), srs_tab_n());  // A/B knob
+static size_t ipa_srs_tail_max() {  // tuning "ipa_srs_tail_n" (default 4096; the tests pin the other paths)
+    return std::min((size_t)tuning(TUNE_IPA_SRS_TAIL_N), srs_tab_n());
 }
 
 // Length at which weighted rounds materialise G = sum_u w[u] SRS[i + u len] (one batched MSM with
@@ -1101,11 +1081,10 @@ static size_t ipa_srs_tail_max() {  // (read per session: the tests pin the othe
 // round costs two n/2-term MSMs whatever the length (~0.75 ms at 2^16), a tail round ~0.25 ms.
 // Measured (opening 2^12 / 2^16 / 2^20, ms): 1024: 6.2 / 10.4 / 29.3; 2048: 5.6 / 9.3 / 27.6;
 // 4096 (tail 4096): 6.5 / 10.7 / 27.4; 8192: 6.4 / 12.8 / 28.4.
-constexpr size_t IPA_MAT_N = 2048;
+// (tuning "ipa_mat_n", default 2048)
 constexpr size_t IPA_PAIR_MAX = (size_t)1 << 18;  // weighted rounds: L and R as one MSM up to this half
-static size_t ipa_mat_n() {
-    const char* e = getenv("HALO_IPA_MAT_N");  // A/B knob (read per round); 0 keeps the weighted rounds to the end
-    return e ? (size_t)atoll(e) : IPA_MAT_N;
+static size_t ipa_mat_n() {  // 0 keeps the weighted rounds to the end
+    return (size_t)tuning(TUNE_IPA_MAT_N);
 }
 
 // The 2^i H tables (i < IPA_HTAB, internal affine) of xi-mode sessions, kept per device and curve,
@@ -1162,12 +1141,11 @@ static int ipa_setup(DeviceState* st, halo_ipa_session* ses, int curve, size_t n
     SrsState& srs = st->srs[curve];
     ses->curve = curve;
     {
-        const char* e = getenv("HALO_IPA_TAIL");
-        const char* ew = getenv("HALO_IPA_WEIGHTED");  // A/B knob: 0 = fold G every round
-        ses->allow_tail = !gs_host && !(e && e[0] == '0');
+        // tuning "ipa_tail" / "ipa_weighted" (default 1): 0 = no tail rounds / fold G every round
+        ses->allow_tail = !gs_host && tuning(TUNE_IPA_TAIL) != 0;
         ses->tail_from_srs = ses->allow_tail && n <= std::min(ipa_srs_tail_max(), srs.n);
         ses->weighted = !gs_host && srs.shifted_c != 0 && n > ipa_tail_n() && !ses->tail_from_srs &&
-                        !(ew && ew[0] == '0');
+                        tuning(TUNE_IPA_WEIGHTED) != 0;
         if (ses->weighted) ses->allow_tail = false;
         ses->srs_round0 = !gs_host && srs.shifted_c != 0 && !ses->weighted;
         ses->gs_srs_prefix = !gs_host && !ses->weighted;
@@ -1259,16 +1237,9 @@ static int ipa_start(DeviceState* st, halo_ipa_session* ses, const halo_wrapped_
     HALO_CHECK(ses->htab.reserve(IPA_HTAB * (64 + 128)));  // affine table + XYZZ chain scratch
     ses->htab_ptr = ses->htab.ptr;
     HALO_CHECK(copy_h2d(sm + 64, own, 64, s));
-    // 2^i H' for i < 128 (the hiding terms use the GLV split of their scalar, k_hide_term): a ~1 ms
-    // one-lane doubling chain, built on the side stream while round 1's digits, sort and accumulation
-    // run; the hiding-term kernels wait for htab_ready
-    const hipStream_t hs = ses->aux ? ses->aux : s;
-    if (ses->aux) {
-        hipEvent_t h_in;
-        if (hipEventCreateWithFlags(&h_in, hipEventDisableTiming) != hipSuccess || hipEventRecord(h_in, s) != hipSuccess ||
-            hipStreamWaitEvent(ses->aux, h_in, 0) != hipSuccess || hipEventDestroy(h_in) != hipSuccess)
-            return set_error(HALO_EDEVICE, "halo_ipa_begin: stream ordering failed");
-    }
+    // 2^i H' for i < 128 (the hiding terms use the GLV split of their scalar, k_hide_term): a
+    // quad-cooperative doubling chain on the session's stream; the hiding-term kernels wait for htab_ready
+    const hipStream_t hs = s;
     uint4* chain = ses->htab.as<uint4>() + 4 * IPA_HTAB;  // XYZZ scratch after the affine table
     DISPATCH_CURVE(ses->curve, Cv, {
         hipLaunchKernelGGL(k_pow2_xyzz_from_wrapped<Cv>, dim3(1), dim3(64), 0, hs, (const uint4*)(sm + 64), chain, IPA_HTAB);
@@ -1525,13 +1496,15 @@ static int ipa_enter_tail(DeviceState* st, halo_ipa_session* ses, hipStream_t s)
     HALO_CHECK(ses->side.reserve(n0));
     HALO_CHECK(ses->part.reserve(nblk * 2 * 128));
     SrsState& srs = st->srs[ses->curve];
-    static const bool srs_tab = !(getenv("HALO_IPA_SRS_TABLE") && getenv("HALO_IPA_SRS_TABLE")[0] == '0');  // A/B knob
-    if (srs_tab && ses->gs_srs_prefix && n0 <= std::min(srs_tab_n(), srs.n)) {
+    if (ses->gs_srs_prefix && n0 <= std::min(srs_tab_n(), srs.n)) {
         HALO_CHECK(srs_small_table(st, ses->curve, s));
-        ses->table = srs.small_tab.as<const uint4>();
+        ses->table_ref = srs.small_tab;  // an SRS write rebuilds into a fresh buffer while this is held
+        ses->table = srs.small_tab->as<const uint4>();
         ses->table_ld = srs.small_n0;
     } else {
-        if (!ses->gs_valid) return set_error(HALO_EINVAL, "ipa tail: G not resident");
+        // a session that skipped its copy of the SRS prefix (ipa_setup: need_gs) but builds its own
+        // table here (the SRS table is off or shorter than n0) copies the prefix now
+        HALO_CHECK(ipa_ensure_gs(st, ses));
         HALO_CHECK(ses->own_table.reserve((size_t)TAIL_TBL * TAIL_MUL * n0 * 128));
         DISPATCH_CURVE(ses->curve, Cv, {
             hipLaunchKernelGGL(k_tail_table<Cv>, dim3(gridn((size_t)TAIL_TABLE_LANES * n0, 64)), dim3(64), 0, s, ses->gs.as<const uint4>(),
@@ -1612,23 +1585,27 @@ static int ipa_tail_sums(halo_ipa_session* ses, int mode, hipStream_t s) {
 
 // The SRS prefix's multiples table d 2^(4 w) G_k (k < n0 = min(srs_tab_n(), srs.n)), built on first
 // use per SRS (k_tail_table + k_tail_mults on stream s; small_tab_ev marks its completion for other
-// streams).  SrsState::invalidate_derived() (every writer of the SRS points) forces a rebuild.
+// streams).  SrsState::invalidate_derived() (every writer of the SRS points) forces a rebuild.  The
+// table is versioned: while an open IPA session holds the current buffer (table_ref),
+// the rebuild goes into a fresh one and the old buffer lives until its last session is released;
+// otherwise it is rebuilt in place after the last small MSM that read it (small_ev).
 int halo::srs_small_table(DeviceState* st, int curve, hipStream_t s) {
     SrsState& srs = st->srs[curve];
     const size_t n0 = std::min(srs_tab_n(), srs.n);
     if (!n0) return set_error(HALO_ESRSRANGE, "no resident SRS: call halo_srs_upload first");
     if (!srs.small_tab_ev) HALO_HIP(hipEventCreateWithFlags(&srs.small_tab_ev, hipEventDisableTiming));
-    if (srs.small_n0 == n0) {
+    if (srs.small_n0 == n0 && srs.small_tab) {
         HALO_HIP(hipStreamWaitEvent(s, srs.small_tab_ev, 0));
         return HALO_OK;
     }
-    if (srs.small_ev) HALO_HIP(hipStreamWaitEvent(s, srs.small_ev, 0));  // the old table's last reader
-    HALO_CHECK(srs.small_tab.reserve((size_t)TAIL_TBL * TAIL_MUL * n0 * 128));
+    if (!srs.small_tab || srs.small_tab.use_count() > 1) srs.small_tab = std::make_shared<DevBuf>();
+    if (srs.small_ev) HALO_HIP(hipStreamWaitEvent(s, srs.small_ev, 0));  // the old table's last small MSM
+    HALO_CHECK(srs.small_tab->reserve((size_t)TAIL_TBL * TAIL_MUL * n0 * 128));
     DISPATCH_CURVE(curve, Cv, {
         hipLaunchKernelGGL(k_tail_table<Cv>, dim3(gridn((size_t)TAIL_TABLE_LANES * n0, 64)), dim3(64), 0, s, srs.gs.as<const uint4>(), 0, n0,
-                           srs.small_tab.as<uint4>());
+                           srs.small_tab->as<uint4>());
         hipLaunchKernelGGL(k_tail_mults<Cv>, dim3(gridn((size_t)TAIL_MLANES * TAIL_TBL * n0, 64)), dim3(64), 0, s, n0,
-                           srs.small_tab.as<uint4>());
+                           srs.small_tab->as<uint4>());
     });
     HALO_HIP(hipGetLastError());
     HALO_HIP(hipEventRecord(srs.small_tab_ev, s));
@@ -1658,7 +1635,7 @@ int halo::msm_srs_small(DeviceState* st, int curve, const void* scalars_ark, siz
         // the hiding term w S rides in block 0 (2^i S table); one block and an XYZZ result: no k_tail_final
         const bool direct = out_xyzz && nblk == 1;
         hipLaunchKernelGGL(k_tail_msm<Cv>, dim3((unsigned)nblk), dim3(TAIL_THREADS), 0, s,
-                           srs.small_tab.as<const uint4>(), srs.small_n0, (const uint32_t*)scr,
+                           srs.small_tab->as<const uint4>(), srs.small_n0, (const uint32_t*)scr,
                            (const uint8_t*)(scr + o_side), n, (size_t)0, 1, (uint32_t)nblk, (uint4*)(scr + o_part),
                            hide_scalar ? srs.s_table.as<const uint4>() : (const uint4*)nullptr, (const uint4*)hide_scalar,
                            (const uint32_t*)nullptr, direct ? (uint4*)d_out_wrapped : (uint4*)nullptr);
@@ -1690,14 +1667,12 @@ static int ipa_round_launch(DeviceState* st, halo_ipa_session* ses) {
     const char* zs = ses->zs.as<const char>();
     if (ses->weighted && 2 * m <= ipa_mat_n()) {
         // G (length 2m) = sum_u w[u] SRS[i + u 2m]: from here on an ordinary (tail) session
-        const char* e = getenv("HALO_IPA_TAIL");
-        ses->allow_tail = !(e && e[0] == '0');
+        ses->allow_tail = tuning(TUNE_IPA_TAIL) != 0;
         const bool to_tail = ses->allow_tail && 2 * m <= ipa_tail_n();  // the tail table reads XYZZ directly
         HALO_CHECK(ses->gs.reserve(2 * m * 128));
-        // over the window-shifted copies (three-window Horner; HALO_MAT_SHIFTED=0: the plain SRS)
+        // over the window-shifted copies (three-window Horner) when they are resident
         const SrsState& srs = st->srs[ses->curve];
-        static const bool mat_shifted = !(getenv("HALO_MAT_SHIFTED") && getenv("HALO_MAT_SHIFTED")[0] == '0');
-        const bool sh = mat_shifted && srs.shifted_c != 0;
+        const bool sh = srs.shifted_c != 0;
         HALO_CHECK(msm_shared_batch(st, ses->curve, sh ? srs.shifted.ptr : srs.gs.ptr, ses->w[ses->wcur].ptr,
                                     ses->wlen, 2 * m, ses->gs.ptr, to_tail, ses->mat, s, sh ? srs.n : 0,
                                     sh ? srs.shifted_c : 0));
@@ -1747,11 +1722,7 @@ static int ipa_round_launch(DeviceState* st, halo_ipa_session* ses) {
         // side two MSMs win (R's front and accumulation overlap L's reduction tail).  Measured, opening
         // 2^14 / 2^17 / 2^18 / 2^19 / 2^20 ms, two MSMs vs one: 7.5 / 11.3 / 14.4 / 19.3 / 27.2 vs
         // 6.9 / 10.3 / 13.2 / 17.8 / 29.0
-        static const size_t pair_max = [] {
-            const char* e = getenv("HALO_IPA_PAIR_MAX");  // A/B knob: terms per side
-            return e ? (size_t)atoll(e) : IPA_PAIR_MAX;
-        }();
-        if (half <= pair_max) {
+        if (half <= IPA_PAIR_MAX) {
             const MsmPairIO io{sl, sr, sm + 128, sm + 160, sm + 512, sm + 640};
             HALO_CHECK(msm_srs_pairs_device(st, ses->curve, 1, &io, half, lgm, ses->htab_ptr, s, hr));
         } else {
@@ -1793,8 +1764,7 @@ static int ipa_apply_pending_fold(DeviceState* st, halo_ipa_session* ses) {
 static int ipa_fold_launch(DeviceState* st, halo_ipa_session* ses, const halo_fe_t* xi, const halo_fe_t* xi_inv) {
     if (ses->m == 0) return set_error(HALO_EINVAL, "halo_ipa_fold: no rounds left");
     if (!ses->started) return set_error(HALO_EINVAL, "halo_ipa_fold: session not started (halo_pcdl_open_start)");
-    static const bool defer = !(getenv("HALO_IPA_DEFER_FOLD") && getenv("HALO_IPA_DEFER_FOLD")[0] == '0');  // A/B knob
-    if (ses->tail && defer) {  // applied by the next round's k_tail_prep (no launch, no copy now)
+    if (ses->tail) {  // applied by the next round's k_tail_prep (no launch, no copy now)
         HALO_CHECK(ipa_apply_pending_fold(st, ses));
         ses->pend_xi = *xi;
         ses->pend_xinv = *xi_inv;

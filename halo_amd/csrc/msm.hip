@@ -223,34 +223,14 @@ __device__ __forceinline__ void acc_chunk(size_t t, uint32_t cnt, const uint32_t
         for (uint32_t b = cur + 1; b <= NB; b++) bstart[b] = cnt;
 }
 
-// PERSIST (beside a concurrent front, HALO_BATCH_OVERLAP=1): a grid of a few workgroups per CU
-// takes blocks of 256 chunks from the atomic counter work_ctr until none is left, so the
-// accumulation never holds more than that many wave slots per SIMD; otherwise one chunk per thread.
-template <class Cv, bool PERSIST>
+template <class Cv>
 __global__ __launch_bounds__(256, HALO_ACC_MINB) void k_acc(const uint32_t* keys, const uint32_t* vals, const uint32_t* count,
                                              uint32_t K, const uint4* bases, uint32_t n_per_window, uint32_t npw_lg,
                                              size_t stride, uint32_t blk_lg, uint32_t glv_n, uint4* first, uint4* last,
-                                             uint4* bucket_sums, uint32_t* work_ctr, uint32_t nblocks, uint32_t* bstart,
-                                             uint32_t NB, uint32_t key_lg = 31, uint32_t poly_off = 0,
-                                             uint32_t check_q = 1) {
-    const uint32_t cnt = *count;
-    if constexpr (!PERSIST) {
-        acc_chunk<Cv>((size_t)blockIdx.x * blockDim.x + threadIdx.x, cnt, keys, vals, K, bases, n_per_window,
-                                npw_lg, stride, blk_lg, glv_n, first, last, bucket_sums, bstart, NB, key_lg, poly_off,
-                                check_q != 0);
-    } else {
-        __shared__ uint32_t sblk;
-        for (;;) {
-            if (threadIdx.x == 0) sblk = atomicAdd(work_ctr, 1u);
-            __syncthreads();
-            const uint32_t blk = sblk;
-            __syncthreads();
-            if (blk >= nblocks) break;  // uniform per workgroup: every wave leaves
-            acc_chunk<Cv>((size_t)blk * blockDim.x + threadIdx.x, cnt, keys, vals, K, bases, n_per_window,
-                                    npw_lg, stride, blk_lg, glv_n, first, last, bucket_sums, bstart, NB, key_lg, poly_off,
-                                check_q != 0);
-        }
-    }
+                                             uint4* bucket_sums, uint32_t* bstart, uint32_t NB, uint32_t key_lg = 31,
+                                             uint32_t poly_off = 0, uint32_t check_q = 1) {
+    acc_chunk<Cv>((size_t)blockIdx.x * blockDim.x + threadIdx.x, *count, keys, vals, K, bases, n_per_window, npw_lg,
+                  stride, blk_lg, glv_n, first, last, bucket_sums, bstart, NB, key_lg, poly_off, check_q != 0);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -379,12 +359,6 @@ int msm_windows(int c) { return (255 + c - 1) / c; }
 // saves a window (c = 17 at 2^20: 15 windows instead of 16; the single bucket set of 2^16 buckets
 // keeps the reduction and the 2-pass sort cheap)
 int msm_shifted_window_bits(size_t n) {
-    static const int c_env = [] {  // HALO_SHIFT_C: window bits of the shifted copies (A/B, 8..20)
-        const char* e = getenv("HALO_SHIFT_C");
-        const int v = e ? atoi(e) : 0;
-        return (v >= 8 && v <= 20) ? v : 0;
-    }();
-    if (c_env) return c_env;
     int c = msm_window_bits(n);
     if (msm_windows(c + 1) < msm_windows(c) && c + 1 <= 17) c++;
     // the top window holds only the 255 - (W - 1) c remaining bits, so its digits pile into the
@@ -411,13 +385,7 @@ static unsigned grid_for(size_t n, unsigned thr) { return (unsigned)std::max<siz
 // Smaller MSMs are latency-bound (a commitment, an IPA round): their critical path is a lane's K
 // dependent additions in k_acc plus k_merge's run of about E / (NB K) partials per bucket, so K =
 // ceil(sqrt(E / NB)) balances the two -- but at least ceil(E / resident lanes), one round.
-// HALO_ACC_K overrides.
 static uint32_t msm_chunk_len(const DeviceState* st, size_t E, size_t NB) {
-    static const uint32_t k_env = [] {
-        const char* e = getenv("HALO_ACC_K");
-        return e ? (uint32_t)atoi(e) : 0u;
-    }();
-    if (k_env) return k_env;
     const size_t resident = (size_t)st->num_cu * 16 * 64;
     if (E > 16 * resident) return (uint32_t)std::max<size_t>(16, std::min<size_t>(64, (E + 4 * resident - 1) / (4 * resident)));
     size_t k = 1;
@@ -433,7 +401,7 @@ static uint32_t msm_chunk_len(const DeviceState* st, size_t E, size_t NB) {
 // two sets only made back-to-back commitment batches slower.)
 constexpr int MSM_SETS = 4;
 struct MsmScratch {
-    DevBuf digits, bstart, partials, bucket_sums, seg_acc, seg_sum, bits, window_sums, scan_tmp, conv, ctr;
+    DevBuf digits, bstart, partials, bucket_sums, seg_acc, seg_sum, bits, window_sums, scan_tmp, conv;
     const uint32_t* skeys = nullptr;   // sorted keys of the current MSM (sort scratch)
     const uint32_t* scount = nullptr;  // device count of valid entries
     SortScratch sort;
@@ -450,8 +418,6 @@ struct MsmPipe {
     int slot_next[2] = {0, 0};
     uint64_t slot_used[2] = {0, 0}, clock = 0;
     hipStream_t tail[MSM_SETS] = {};  // one per scratch set: consecutive tails run concurrently
-    hipStream_t front = nullptr;      // digits + sort of batched MSMs (halo_msm_batch_dev)
-    hipEvent_t batch_in = nullptr;    // the batch's inputs are ready (recorded on the caller's stream)
 };
 static MsmPipe g_msm_pipe[64];  // per device
 
@@ -483,29 +449,9 @@ static int msm_pick_set(MsmPipe& P, hipStream_t s, bool advance) {
     return set;
 }
 
-// persistent accumulation workgroups per CU beside a concurrent front (HALO_ACC_WGS overrides)
-static unsigned msm_acc_wgs_per_cu() {
-    static const unsigned v = [] {
-        const char* e = getenv("HALO_ACC_WGS");
-        return e ? (unsigned)std::max(1, atoi(e)) : 3u;
-    }();
-    return v;
-}
-
 static int pipe_init(MsmPipe& P) {
     if (P.tail[0]) return HALO_OK;
-    int least = 0, greatest = 0;  // the front's kernels are dispatched ahead of the accumulation's
-    HALO_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    HALO_HIP(hipStreamCreateWithPriority(&P.front, hipStreamNonBlocking, greatest));
-    HALO_HIP(hipEventCreateWithFlags(&P.batch_in, hipEventDisableTiming));
-    // HALO_TAIL_PRIO=low: the tails' kernels are dispatched after the next MSM's front
-    const char* tp = getenv("HALO_TAIL_PRIO");
-    for (auto& t : P.tail) {
-        if (tp && tp[0] == 'l')
-            HALO_HIP(hipStreamCreateWithPriority(&t, hipStreamNonBlocking, least));
-        else
-            HALO_HIP(hipStreamCreateWithFlags(&t, hipStreamNonBlocking));
-    }
+    for (auto& t : P.tail) HALO_HIP(hipStreamCreateWithFlags(&t, hipStreamNonBlocking));
     for (auto& m : P.set) {
         HALO_HIP(hipEventCreateWithFlags(&m.acc_done, hipEventDisableTiming));
         HALO_HIP(hipEventCreateWithFlags(&m.tail_done, hipEventDisableTiming));
@@ -525,13 +471,6 @@ void msm_shutdown() {
             (void)hipStreamDestroy(t);
             t = nullptr;
         }
-        if (P.front) {
-            (void)hipStreamSynchronize(P.front);
-            (void)hipStreamDestroy(P.front);
-            P.front = nullptr;
-        }
-        if (P.batch_in) (void)hipEventDestroy(P.batch_in);
-        P.batch_in = nullptr;
         for (auto& m : P.set) {
             for (hipEvent_t* e : {&m.acc_done, &m.tail_done, &m.start, &m.front_done}) {
                 if (*e) (void)hipEventDestroy(*e);
@@ -555,20 +494,14 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
                         const uint4* scalars_ark, size_t n, int c_req, const uint4* hide_table, const uint4* hide_scalar,
                         uint4* d_out_wrapped, hipStream_t s, bool async, uint32_t blk_lg = 32,
                         bool hide_glv = false, bool out_xyzz = false, hipEvent_t hide_ready = nullptr,
-                        int preset = -1, hipStream_t fs = nullptr, int w_lo = 0, int w_hi = 0) {
+                        int preset = -1, int w_lo = 0, int w_hi = 0) {
     MsmPipe& PP = g_msm_pipe[st->device & 63];
     HALO_CHECK(pipe_init(PP));
     // preset: the set the caller already claimed (and waited for) to stage converted bases in
     const int set = preset >= 0 ? preset : msm_pick_set(PP, s, true);
     MsmScratch& M = PP.set[set];
-    // fs: the front (digits + sort) runs on its own stream, beside the previous MSM's accumulation
-    // on s (halo_msm_batch_dev); the caller has ordered fs after the inputs
-    const hipStream_t front = fs ? fs : s;
     // the previous user of this scratch set must have finished its tail
-    if (M.tail_pending && preset < 0) {
-        HALO_HIP(hipStreamWaitEvent(front, M.tail_done, 0));
-        if (front != s) HALO_HIP(hipStreamWaitEvent(s, M.tail_done, 0));
-    }
+    if (M.tail_pending && preset < 0) HALO_HIP(hipStreamWaitEvent(s, M.tail_done, 0));
     const hipStream_t ts = PP.tail[set];
     const size_t nn = std::max<size_t>(n, 1);
     // non-shifted bases: GLV (2n half-size scalars, ~128-bit windows) -- see k_digits_glv
@@ -628,36 +561,20 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
 
     if (n > 0) {
         // shifted, all windows, W <= 16: digit recoding fused into the sort's first pass
-        static const bool fuse_env = !getenv("HALO_SORT_UNFUSED");
-        const bool fuse = fuse_env && shifted && w_lo == 0 && w_hi == W_all && W_all <= 16 && front == s &&
-                          n < (1ull << 31) / 16;
+        const bool fuse = shifted && w_lo == 0 && w_hi == W_all && W_all <= 16 && n < (1ull << 31) / 16;
         if (glv)
-            hipLaunchKernelGGL(k_digits_glv<Cv>, dim3(grid_for(n, 256)), dim3(256), 0, front, scalars_ark, n, c, W,
+            hipLaunchKernelGGL(k_digits_glv<Cv>, dim3(grid_for(n, 256)), dim3(256), 0, s, scalars_ark, n, c, W,
                                M.digits.as<uint32_t>());
         else if (!fuse)
-            hipLaunchKernelGGL(k_digits<typename Cv::Scalar>, dim3(grid_for(n, 256)), dim3(256), 0, front, scalars_ark,
+            hipLaunchKernelGGL(k_digits<typename Cv::Scalar>, dim3(grid_for(n, 256)), dim3(256), 0, s, scalars_ark,
                                n, c, W_all, M.digits.as<uint32_t>(), n, w_lo, w_hi);
         HALO_HIP(hipGetLastError());
         uint32_t *skeys = nullptr, *svals = nullptr;
         const uint32_t* scount = nullptr;
         RsFused fz{scalars_ark, n, c, W_all, curve_id<Cv>() == HALO_PALLAS ? HALO_FP : HALO_FQ};
         HALO_CHECK(msm_radix_sort(M.digits.as<const uint32_t>(), E, SN, B, key_bits, M.sort, &skeys, &svals, &scount,
-                                  nullptr, NB, front, front != s, fuse ? &fz : nullptr));
-        if (front != s) {
-            HALO_HIP(hipEventRecord(M.front_done, front));
-            HALO_HIP(hipStreamWaitEvent(s, M.front_done, 0));
-        }
-        // beside a concurrent front, the accumulation runs persistent with msm_acc_wgs_per_cu()
-        // workgroups per CU, leaving wave slots (and all of the LDS) to the front's kernels
+                                  nullptr, NB, s, fuse ? &fz : nullptr));
         const uint32_t nblocks = (uint32_t)grid_for(nchunks, 256);
-        uint32_t* work_ctr = nullptr;
-        unsigned grid = nblocks;
-        if (front != s) {
-            HALO_CHECK(M.ctr.reserve(16));
-            work_ctr = M.ctr.as<uint32_t>();
-            HALO_HIP(hipMemsetAsync(work_ctr, 0, 4, s));
-            grid = std::min<unsigned>(nblocks, (unsigned)st->num_cu * msm_acc_wgs_per_cu());
-        }
         // the resident window-shifted SRS without identity points: k_acc skips the bases' identity test
         const SrsState& srs_c = st->srs[curve_id<Cv>()];
         const bool srs_bases = shifted && srs_c.shifted_c != 0 && srs_c.shifted.ptr &&
@@ -665,12 +582,11 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
                                (const char*)bases_int < srs_c.shifted.as<const char>() + srs_c.shifted.bytes;
         const uint32_t check_q = (srs_bases && !srs_c.shifted_has_id) ? 0u : 1u;
         ProfScope prof("msm_acc", s);
-        auto kacc = work_ctr ? k_acc<Cv, true> : k_acc<Cv, false>;
-        HALO_LAUNCH(prof, kacc, dim3(grid), dim3(256), 0, s, (const uint32_t*)skeys,
+        HALO_LAUNCH(prof, k_acc<Cv>, dim3(nblocks), dim3(256), 0, s, (const uint32_t*)skeys,
                     (const uint32_t*)svals, scount, K, bases_int, (uint32_t)nn, is_pow2(nn) ? ilog2(nn) : 0xffu,
                     (shifted && (shift_stride != nn || blk_lg < 32)) ? shift_stride : (size_t)0, blk_lg,
                     glv ? (uint32_t)nn : 0u, P_first,
-                    P_last, M.bucket_sums.as<uint4>(), work_ctr, nblocks, M.bstart.as<uint32_t>(), (uint32_t)NB, 31u, 0u,
+                    P_last, M.bucket_sums.as<uint4>(), M.bstart.as<uint32_t>(), (uint32_t)NB, 31u, 0u,
                     check_q);
         M.skeys = skeys;
         M.scount = scount;
@@ -711,12 +627,8 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
     ta.hide_table = hide_table;
     ta.hide_scalar = hide_scalar;
     ta.out_wrapped = d_out_wrapped;
-    static const bool fuse_off = [] {  // HALO_FUSE_FINAL=0: A/B knob, separate k_final launch
-        const char* e = getenv("HALO_FUSE_FINAL");
-        return e && e[0] == '0';
-    }();
     // one window set with a nonempty MSM (the tail reaches k_bitcombine): it also finishes the MSM
-    const bool fuse = SW == 1 && n > 0 && !fuse_off;
+    const bool fuse = SW == 1 && n > 0;
     if (fuse) {
         ta.final_mode = out_xyzz ? 2 : 1;
         ta.final_hide = (const uint4*)hide_slot;
@@ -801,10 +713,9 @@ static int msm_multi_device_t(DeviceState* st, const void* const* scalars, const
     {
         ProfScope prof("msm_acc", s);
         const uint32_t nblocks = (uint32_t)grid_for(nchunks, 256);
-        auto kacc = k_acc<Cv, false>;
-        HALO_LAUNCH(prof, kacc, dim3(nblocks), dim3(256), 0, s, (const uint32_t*)skeys, (const uint32_t*)svals, scount,
+                HALO_LAUNCH(prof, k_acc<Cv>, dim3(nblocks), dim3(256), 0, s, (const uint32_t*)skeys, (const uint32_t*)svals, scount,
                     K, srs.shifted.as<const uint4>(), (uint32_t)ld, is_pow2(ld) ? ilog2(ld) : 0xffu, srs.n, 32u, 0u,
-                    P_first, P_last, M.bucket_sums.as<uint4>(), (uint32_t*)nullptr, nblocks, M.bstart.as<uint32_t>(),
+                    P_first, P_last, M.bucket_sums.as<uint4>(), M.bstart.as<uint32_t>(),
                     (uint32_t)NB, 31u, 0u, srs.shifted_has_id ? 1u : 0u);
         HALO_HIP(hipGetLastError());
     }
@@ -921,10 +832,9 @@ static int msm_srs_pairs_t(DeviceState* st, size_t np, const MsmPairIO* io, size
     {
         ProfScope prof("msm_acc", s);
         const uint32_t nblocks = (uint32_t)grid_for(nchunks, 256);
-        auto kacc = k_acc<Cv, false>;
-        HALO_LAUNCH(prof, kacc, dim3(nblocks), dim3(256), 0, s, (const uint32_t*)skeys, (const uint32_t*)svals, scount,
+                HALO_LAUNCH(prof, k_acc<Cv>, dim3(nblocks), dim3(256), 0, s, (const uint32_t*)skeys, (const uint32_t*)svals, scount,
                     K, srs.shifted.as<const uint4>(), (uint32_t)half, ilog2(half), srs.n, lgm, 0u, P_first, P_last,
-                    M.bucket_sums.as<uint4>(), (uint32_t*)nullptr, nblocks, M.bstart.as<uint32_t>(), (uint32_t)NB,
+                    M.bucket_sums.as<uint4>(), M.bstart.as<uint32_t>(), (uint32_t)NB,
                     (uint32_t)(c - 1), (uint32_t)m, srs.shifted_has_id ? 1u : 0u);
         HALO_HIP(hipGetLastError());
     }
@@ -977,14 +887,9 @@ int msm_srs_pairs_device(DeviceState* st, int curve, size_t np, const MsmPairIO*
     return rc;
 }
 
-// polynomials up to this length take the one-MSM batch path (HALO_MSM_MULTI_MAX overrides; 0 = off)
-static size_t msm_multi_max() {
-    static const size_t v = [] {
-        const char* e = getenv("HALO_MSM_MULTI_MAX");
-        return e ? (size_t)strtoull(e, nullptr, 10) : ((size_t)1 << 18);
-    }();
-    return v;
-}
+// polynomials up to this length take the one-MSM batch path (tuning "msm_multi_max", default 2^18;
+// 0 = off)
+static size_t msm_multi_max() { return (size_t)tuning(TUNE_MSM_MULTI_MAX); }
 
 // Claims the scratch set of the next MSM on stream s and orders s after that set's previous tail
 // (the caller stages converted bases in its conv buffer before the MSM is enqueued; the MSM then
@@ -1021,16 +926,12 @@ int msm_device(DeviceState* st, int curve, const void* bases_int, const void* sc
 
 // MSM over the resident SRS prefix Gs[0..n): uses the window-shifted copies when present.
 int msm_srs_device(DeviceState* st, int curve, const void* scalars_ark, size_t n, const void* hide_scalar,
-                   void* d_out_wrapped, hipStream_t s, bool async, hipStream_t fs) {
+                   void* d_out_wrapped, hipStream_t s, bool async) {
     SrsState& srs = st->srs[curve];
     if (n > srs.n) return set_error(HALO_ESRSRANGE, "n (%zu) exceeds the resident SRS length (%zu)", n, srs.n);
     const void* table = hide_scalar ? srs.s_table.ptr : nullptr;
     if (hide_scalar && !srs.has_sh) return set_error(HALO_ESRSRANGE, "hiding commitment needs S: upload (S, H)");
-    static const bool small_off = [] {  // HALO_SRS_SMALL=0: A/B knob, small MSMs through the bucket pipeline
-        const char* e = getenv("HALO_SRS_SMALL");
-        return e && e[0] == '0';
-    }();
-    if (!async && !small_off && n >= 1 && n <= srs_small_max())
+    if (!async && n >= 1 && n <= srs_small_max())
         return msm_srs_small(st, curve, scalars_ark, n, hide_scalar, d_out_wrapped, s);
     int rc;
     // the shifted copies hold W windows of srs.n points each; an MSM of n <= srs.n points uses the
@@ -1040,7 +941,7 @@ int msm_srs_device(DeviceState* st, int curve, const void* scalars_ark, size_t n
         rc = msm_device_t<Cv>(st, use_shifted ? srs.shifted.as<const uint4>() : srs.gs.as<const uint4>(), use_shifted,
                               srs.n, (const uint4*)scalars_ark, n, use_shifted ? srs.shifted_c : 0, (const uint4*)table,
                               (const uint4*)hide_scalar, (uint4*)d_out_wrapped, s, async, 32, false, false, nullptr,
-                              -1, fs);
+                              -1);
     });
     return rc;
 }
@@ -1226,10 +1127,9 @@ static int msm_shared_batch_t(DeviceState* st, const uint4* bases, const uint4* 
                        (const uint32_t*)ekey, (const uint32_t*)tot, (uint32_t)len, (uint32_t)(W * B),
                        shifted ? (uint32_t)ilog2(T) : 31u, shifted ? (uint32_t)shift_stride : 0u,
                        S.keys.as<uint32_t>(), S.vals.as<uint32_t>());
-    hipLaunchKernelGGL((k_acc<Cv, false>), dim3(grid_for(nchunks, 256)), dim3(256), 0, s, S.keys.as<const uint32_t>(),
+    hipLaunchKernelGGL(k_acc<Cv>, dim3(grid_for(nchunks, 256)), dim3(256), 0, s, S.keys.as<const uint32_t>(),
                        S.vals.as<const uint32_t>(), (const uint32_t*)(tot + 1), K, bases, 1u, 0u, (size_t)0, 32u, 0u,
-                       P_first, P_last, S.bucket_sums.as<uint4>(), (uint32_t*)nullptr, (uint32_t)grid_for(nchunks, 256),
-                       S.bstart.as<uint32_t>(), (uint32_t)NB, 31u, 0u, 1u);
+                       P_first, P_last, S.bucket_sums.as<uint4>(), S.bstart.as<uint32_t>(), (uint32_t)NB, 31u, 0u, 1u);
     HALO_HIP(hipGetLastError());
     MsmTailArgs ta;
     ta.n = T;
@@ -1969,8 +1869,6 @@ namespace halo {
 // asynchronous on s (msm_join before reading)
 int msm_batch_device(DeviceState* st, int curve, const void* const* d_scalars, const size_t* lens, size_t k, void* d_out,
                      hipStream_t s) {
-    MsmPipe& PP = g_msm_pipe[st->device & 63];
-    HALO_CHECK(pipe_init(PP));
     SrsState& srs = st->srs[curve];
     size_t nmax = 0;
     for (size_t i = 0; i < k; i++) {
@@ -1978,22 +1876,15 @@ int msm_batch_device(DeviceState* st, int curve, const void* const* d_scalars, c
         if (lens[i] > srs.n) return set_error(HALO_ESRSRANGE, "n (%zu) exceeds the resident SRS length (%zu)", lens[i], srs.n);
         nmax = std::max(nmax, lens[i]);
     }
-    // HALO_BATCH_OVERLAP=1: fronts on the side stream beside the accumulations (measured slower:
-    // the sort kernels starve beside k_acc's gathers); off by default
-    const char* ov = getenv("HALO_BATCH_OVERLAP");
-    const bool overlap = k > 1 && srs.shifted_c != 0 && ov && ov[0] == '1';
-    if (k > 1 && srs.shifted_c && nmax <= msm_multi_max() && !overlap) {
+    // (Measured and removed: the fronts on a side stream beside the accumulations -- slower, the
+    // sort kernels starve beside k_acc's gathers)
+    if (k > 1 && srs.shifted_c && nmax <= msm_multi_max()) {
         int rc;
         DISPATCH_CURVE(curve, Cv, { rc = msm_multi_device_t<Cv>(st, d_scalars, lens, k, (uint4*)d_out, s); });
         return rc;
     }
-    if (overlap) {  // the fronts run on PP.front from the batch's inputs on: one event on s
-        HALO_HIP(hipEventRecord(PP.batch_in, s));
-        HALO_HIP(hipStreamWaitEvent(PP.front, PP.batch_in, 0));
-    }
     for (size_t i = 0; i < k; i++)
-        HALO_CHECK(msm_srs_device(st, curve, d_scalars[i], lens[i], nullptr, (char*)d_out + 64 * i, s, true,
-                                  overlap ? PP.front : nullptr));
+        HALO_CHECK(msm_srs_device(st, curve, d_scalars[i], lens[i], nullptr, (char*)d_out + 64 * i, s, true));
     return HALO_OK;
 }
 }  // namespace halo
@@ -2028,7 +1919,7 @@ extern "C" int halo_msm_srs_windows_dev(halo_curve_t curve, const void* d_scalar
     DISPATCH_CURVE(curve, Cv, {
         rc = msm_device_t<Cv>(st, srs.shifted.as<const uint4>(), true, srs.n, (const uint4*)d_scalars, n,
                               srs.shifted_c, nullptr, nullptr, (uint4*)d_out, (hipStream_t)stream, true, 32, false,
-                              false, nullptr, -1, nullptr, w_lo, w_hi);
+                              false, nullptr, -1, w_lo, w_hi);
     });
     return rc;
 }

@@ -2,6 +2,7 @@
 #include "runtime.hpp"
 #include "msm.hpp"
 
+#include <atomic>
 #include <cstdio>
 #include <cstring>
 
@@ -147,6 +148,19 @@ static void prof_drain() {
     }
 }
 
+// ---- tuning ----------------------------------------------------------------------------------
+static const char* const kTuneNames[TUNE_COUNT] = {"ipa_weighted", "ipa_tail", "ipa_srs_tail_n", "ipa_mat_n",
+                                                   "msm_multi_max"};
+static const long long kTuneDefault[TUNE_COUNT] = {1, 1, 4096, 2048, 1ll << 18};
+static std::atomic<long long> g_tune[TUNE_COUNT] = {{1}, {1}, {4096}, {2048}, {1ll << 18}};
+long long tuning(TuneKey k) { return g_tune[k].load(std::memory_order_relaxed); }
+static int tune_index(const char* key) {
+    if (!key) return -1;
+    for (int k = 0; k < TUNE_COUNT; k++)
+        if (!strcmp(key, kTuneNames[k])) return k;
+    return -1;
+}
+
 }  // namespace halo
 
 using namespace halo;
@@ -230,6 +244,23 @@ int halo_shutdown(void) {
         st->scratch_used = false;
         st->scratch_last = nullptr;
     }
+    return HALO_OK;
+}
+
+int halo_set_tuning(const char* key, long long value) {
+    clear_error();
+    const int k = tune_index(key);
+    if (k < 0) return set_error(HALO_EINVAL, "unknown tuning key '%s'", key ? key : "(null)");
+    g_tune[k].store(value < 0 ? kTuneDefault[k] : value);
+    return HALO_OK;
+}
+
+int halo_get_tuning(const char* key, long long* value) {
+    clear_error();
+    const int k = tune_index(key);
+    if (k < 0) return set_error(HALO_EINVAL, "unknown tuning key '%s'", key ? key : "(null)");
+    if (!value) return set_error(HALO_EINVAL, "halo_get_tuning: null value");
+    *value = g_tune[k].load();
     return HALO_OK;
 }
 

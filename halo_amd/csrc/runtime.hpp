@@ -34,6 +34,10 @@ void clear_error();
         if (_rc != HALO_OK) return _rc; \
     } while (0)
 
+// ---- tuning (halo_set_tuning): path selections the parity tests pin; read on every use
+enum TuneKey { TUNE_IPA_WEIGHTED, TUNE_IPA_TAIL, TUNE_IPA_SRS_TAIL_N, TUNE_IPA_MAT_N, TUNE_MSM_MULTI_MAX, TUNE_COUNT };
+long long tuning(TuneKey k);
+
 // ---- device buffers ---------------------------------------------------------------------------
 // Grow-only device buffer (no shrinking; reused across calls so that timed regions never allocate).
 struct DevBuf {
@@ -62,7 +66,9 @@ struct SrsState {
         DevBuf t;
     };
     std::vector<std::unique_ptr<HTable>> h_tables;
-    DevBuf small_tab;   // d 2^(4 w) G_k (k < small_n0, w < 32, d < 16), XYZZ: small SRS MSMs, IPA tails (ipa.hip)
+    // d 2^(4 w) G_k (k < small_n0, w < 32, d < 16), XYZZ: small SRS MSMs, IPA tails (ipa.hip); shared
+    // with the open IPA sessions that read it, so a rebuild never overwrites a buffer in use
+    std::shared_ptr<DevBuf> small_tab;
     size_t small_n0 = 0;             // 0 = not built for the current SRS
     hipEvent_t small_tab_ev = nullptr;  // small_tab's build completed
     DevBuf small_scr;                // GLV digits, block partials of a small MSM

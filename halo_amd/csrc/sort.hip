@@ -29,9 +29,8 @@
 namespace halo {
 
 constexpr int RS_THREADS = 512;
-// Tiles of RS_THREADS x ROUNDS entries: 16 rounds (8192 entries, runs of ~32 entries = 128 B per digit,
-// 64 KB of LDS staging) by default; 8 rounds (4096 entries, 32 KB) when the sort runs beside the
-// previous MSM's accumulation (halo_msm_batch_dev), whose workgroups leave little LDS free.
+// Tiles of RS_THREADS x 16 rounds: 8192 entries, runs of ~32 entries = 128 B per digit, 64 KB of LDS
+// staging.  (Measured: 4096-entry tiles, 4 workgroups per CU, were no faster.)
 constexpr int RS_BINS = 256;
 constexpr uint32_t RS_NONE = 0xffffffffu;
 
@@ -466,14 +465,8 @@ int device_exclusive_scan(const uint32_t* in, size_t n, uint32_t* out, DevBuf& t
 
 int msm_radix_sort(const uint32_t* digits, size_t E, size_t npw, uint32_t B, uint32_t key_bits, SortScratch& S,
                    uint32_t** keys_out, uint32_t** vals_out, const uint32_t** count_out, uint32_t* bstart, size_t NB,
-                   hipStream_t s, bool small_tiles, const RsFused* fused) {
-    static const int tile_env = [] {
-        const char* e = getenv("HALO_SORT_ROUNDS");
-        return e ? atoi(e) : 0;
-    }();
-    if (tile_env == 8) small_tiles = true;
-    if (tile_env == 16) small_tiles = false;
-    const int RS_TILE = RS_THREADS * (small_tiles ? 8 : 16);
+                   hipStream_t s, const RsFused* fused) {
+    constexpr int RS_TILE = RS_THREADS * 16;
     const uint32_t ntiles = (uint32_t)std::max<size_t>(1, (E + RS_TILE - 1) / RS_TILE);
     // fused first pass: tiles of RS_THREADS scalars x W windows
     const uint32_t ntiles0 = fused ? (uint32_t)std::max<size_t>(1, (fused->n + RS_THREADS - 1) / RS_THREADS) : ntiles;
@@ -518,8 +511,7 @@ int msm_radix_sort(const uint32_t* digits, size_t E, size_t npw, uint32_t B, uin
             });
         } else {
             // pass 0 also stores the number of valid (nonzero-digit) entries
-            auto kh = p == 0 ? (small_tiles ? k_rs_hist<8, true> : k_rs_hist<16, true>)
-                             : (small_tiles ? k_rs_hist<8, false> : k_rs_hist<16, false>);
+            auto kh = p == 0 ? k_rs_hist<16, true> : k_rs_hist<16, false>;
             hipLaunchKernelGGL(kh, dim3(nt), dim3(RS_THREADS), 0, s, in, nt, S.hist.as<uint32_t>(), S.offs.as<uint32_t>(),
                                S.ctr.as<uint32_t>(), p == 0 ? S.count.as<uint32_t>() : nullptr);
         }
@@ -530,8 +522,7 @@ int msm_radix_sort(const uint32_t* digits, size_t E, size_t npw, uint32_t B, uin
                                    S.vals[cur].as<uint32_t>());
             });
         } else {
-            auto ks = p == 0 ? (small_tiles ? k_rs_scatter<8, void, true> : k_rs_scatter<16, void, true>)
-                             : (small_tiles ? k_rs_scatter<8, void, false> : k_rs_scatter<16, void, false>);
+            auto ks = p == 0 ? k_rs_scatter<16, void, true> : k_rs_scatter<16, void, false>;
             hipLaunchKernelGGL(ks, dim3(nt), dim3(RS_THREADS), 0, s, in, S.hist.as<const uint32_t>(),
                                S.offs.as<const uint32_t>(), S.keys[cur].as<uint32_t>(), S.vals[cur].as<uint32_t>());
         }

@@ -24,7 +24,7 @@ struct RsFused {
 };
 int msm_radix_sort(const uint32_t* digits, size_t E, size_t npw, uint32_t B, uint32_t key_bits, SortScratch& S,
                    uint32_t** keys_out, uint32_t** vals_out, const uint32_t** count_out, uint32_t* bstart, size_t NB,
-                   hipStream_t s, bool small_tiles = false, const RsFused* fused = nullptr);
+                   hipStream_t s, const RsFused* fused = nullptr);
 
 // bstart[b] (b <= NB) from the sorted keys (capacity E, device count)
 int msm_bucket_starts(const uint32_t* keys, const uint32_t* count, size_t NB, size_t E, uint32_t* bstart, hipStream_t s);

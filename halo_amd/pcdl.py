@@ -100,8 +100,10 @@ class IpaSession:
     def end(self):
         U = np.zeros(8, dtype=np.uint64)
         c = np.zeros(4, dtype=np.uint64)
-        H.check(H.load().halo_ipa_end(self._s, H.ptr(U), H.ptr(c)))
-        self._s = None
+        # halo_ipa_end returns the session to the pool even when it reports an error, so the handle
+        # is dropped first: no caller path can end (release) it a second time
+        s, self._s = self._s, None
+        H.check(H.load().halo_ipa_end(s, H.ptr(U), H.ptr(c)))
         return U, c
 
 

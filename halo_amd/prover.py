@@ -193,9 +193,11 @@ def geometric_polys(B, zeta: int, polys):
     return result
 
 
-def naive_prover(B, wit, n: int, chal: Challenges, acc_prev=None):
+def naive_prover(B, wit, n: int, chal: Challenges, acc_prev=None, keep=None):
     """protocol.rs:64-330 on backend B.  Returns the proof's commitments, evaluations, the three IPA
-    openings and per-round wall times (seconds; B.sync() before each stamp)."""
+    openings and per-round wall times (seconds; B.sync() before each stamp).  ``keep``: an optional
+    dict that receives the intermediate polynomials and challenges (z, f, t's pieces, beta, gamma,
+    alpha, zeta, xi, ...) so a test can check them at full size against the oracle."""
     import time
 
     m = B.m
@@ -275,6 +277,8 @@ def naive_prover(B, wit, n: int, chal: Challenges, acc_prev=None):
     else:
         f_cc2 = B.poly_sub(B.poly_mul(z, f_prime), B.poly_mul(z_omega, g_prime))
     f = B.poly_add(B.poly_add(f_gc, B.poly_scale(f_cc1, alpha)), B.poly_scale(f_cc2, alpha * alpha % m))
+    if keep is not None:
+        keep.update(pi_poly=pi_poly, z=z, f=f, beta=beta, gamma=gamma, alpha=alpha, w_omegas=w_omegas)
     t = B.divide_by_vanishing(f, n)
     assert B.length(t) <= T_POLYS * n, f"{B.length(t)} < {T_POLYS * n}"
     ts = B.split(B.resize(t, T_POLYS * n), n)                  # t_split (protocol.rs:509-517)
@@ -289,6 +293,8 @@ def naive_prover(B, wit, n: int, chal: Challenges, acc_prev=None):
     r_omega = geometric_polys(B, zeta, wit["ws"][0:3] + [z])
     xi = chal()
     omega = B.omega(n)
+    if keep is not None:
+        keep.update(ts=ts, zeta=zeta, xi=xi)
     if acc_prev is None:
         acc_prev = synthetic_accumulator(B, n, chal)
     B.sync()

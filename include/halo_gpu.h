@@ -70,6 +70,16 @@ int halo_abi_version(void);
 int halo_shutdown(void);
 /* Blocks until all work queued by this library on `stream` is complete. */
 int halo_stream_sync(void* stream);
+/* Path-selection tuning (library-wide, read by every later call; value -1 restores the default).
+ * Keys: "ipa_weighted" (1: IPA rounds over the resident window-shifted SRS without folding G; 0:
+ * GLV-fold G every round), "ipa_tail" (1: switch to the direct-sum tail rounds at length 2048),
+ * "ipa_srs_tail_n" (SRS openings of n <= this run tail rounds from round 1; default 4096),
+ * "ipa_mat_n" (weighted rounds materialise G at this length; 0 = never; default 2048),
+ * "msm_multi_max" (commitment batches of polynomials up to this length run as one MSM; default
+ * 2^18).  Every setting yields the same results; the parity tests pin each path with it.  The
+ * reference has no counterpart (host-side knob of this backend only).  HALO_EINVAL on an unknown key. */
+int halo_set_tuning(const char* key, long long value);
+int halo_get_tuning(const char* key, long long* value);
 
 /* ------------------------------------------------------------------ a10: SRS provider
  * Replaces PublicParams::{new, set_pp, get_pp} (crates/group/src/pp.rs:26-94): the SRS bases Gs,

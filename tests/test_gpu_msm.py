@@ -441,8 +441,7 @@ def test_msm_batch_dev_one_msm_path(hal, corc, cname, cid):
     """halo_msm_batch_dev (the commitment batches of protocol.rs:114,263 / trace.rs:188-192): k
     polynomials of ragged lengths (including empty and length 1) over the resident window-shifted
     SRS as one MSM with (polynomial, bucket) keys, each result bit-exact vs the oracle MSM; and the
-    per-MSM pipelined path (HALO_MSM_MULTI_MAX=0 in a subprocess is not needed: lengths above the
-    threshold take it) agrees with halo_msm_dev_async."""
+    same batch on the per-MSM pipelined path (tuning msm_multi_max = 0)."""
     import ctypes
 
     import torch
@@ -458,12 +457,15 @@ def test_msm_batch_dev_one_msm_path(hal, corc, cname, cid):
     lns = (ctypes.c_size_t * len(lens))(*lens)
     out = torch.zeros((len(lens), 8), dtype=torch.int64, device="cuda")
     sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    hal.check(L.halo_msm_batch_dev(cid, ptrs, lns, len(lens), ctypes.c_void_p(out.data_ptr()), sp))
-    hal.check(L.halo_msm_join(sp))
-    got = out.cpu().numpy().view(np.uint64)
-    for i, m in enumerate(lens):
-        exp = corc.msm(cname, g[:m], scs[i]) if m else np.zeros(8, dtype=np.uint64)
-        assert np.array_equal(got[i], exp), (i, m)
+    exps = [corc.msm(cname, g[:m], scs[i]) if m else np.zeros(8, dtype=np.uint64) for i, m in enumerate(lens)]
+    for multi_max in (-1, 0):  # the default one-MSM batch, then one pipelined MSM per polynomial
+        out.zero_()
+        with hal.tuning(msm_multi_max=multi_max):
+            hal.check(L.halo_msm_batch_dev(cid, ptrs, lns, len(lens), ctypes.c_void_p(out.data_ptr()), sp))
+            hal.check(L.halo_msm_join(sp))
+        got = out.cpu().numpy().view(np.uint64)
+        for i, m in enumerate(lens):
+            assert np.array_equal(got[i], exps[i]), (multi_max, i, m)
 
 
 @pytest.mark.parametrize("cname,cid", CURVES)

@@ -101,23 +101,214 @@ def test_ntt_2p24_vs_c_oracle(hal, corc, tag, fid, inverse):
         assert np.array_equal(corc.ntt(tag, exp, inverse=True), x)
 
 
-def test_prove_2p20_openings_pass_succinct_check_and_decider(hal, corc):
-    import pcdl_check
-
+@pytest.fixture(scope="module")
+def prove_2p20(hal):
+    """One run of naive_prover at n = 2^20 (BASELINE configs[3]) over the synthetic SRS G_j = k_j G,
+    with the intermediate polynomials kept for the checks below."""
     from halo_amd import prover
 
     L = hal.load()
     n = 1 << 20
+    seed = 0x505256 + 20
     cid = hal.CURVES["pallas"]
-    hal.check(L.halo_srs_synthesize(cid, n, 0x505256 + 20))
+    hal.check(L.halo_srs_synthesize(cid, n, seed))
     hal.check(L.halo_srs_precompute_windows(cid))
     B = prover.DeviceBackend("pallas")
-    out = prover.naive_prover(B, prover.synthetic_witness(B, n, seed=1), n, prover.Challenges(B.m))
+    wit = prover.synthetic_witness(B, n, seed=1)
+    keep = {}
+    out = prover.naive_prover(B, wit, n, prover.Challenges(B.m), keep=keep)
+    B.sync()
+    return {"n": n, "seed": seed, "B": B, "wit": wit, "keep": keep, "out": out}
+
+
+def test_prove_2p20_openings_pass_succinct_check_and_decider(hal, corc, prove_2p20):
+    import pcdl_check
+
+    L = hal.load()
+    n, B, out = prove_2p20["n"], prove_2p20["B"], prove_2p20["out"]
     srs = np.zeros((n, 8), dtype=np.uint64)
-    hal.check(L.halo_srs_read(cid, 0, n, hal.ptr(srs)))
+    hal.check(L.halo_srs_read(hal.CURVES["pallas"], 0, n, hal.ptr(srs)))
     for key in ("q_r", "q_r_omega", "acc"):
         q = out[key]
         assert len(q["Ls"]) == 20
         pcdl_check.succinct_check("pallas", q["C"], n - 1, q["z"], q["v"], q["Ls"], q["Rs"], q["U"], q["c"],
                                   q["xis"], B.H_point)
         assert pcdl_check.decider_commit_matches("pallas", q["U"], q["xis"], srs, corc.msm), key
+
+
+def _host(t):
+    return np.ascontiguousarray(t.cpu().numpy().view(np.uint64))
+
+
+class _Fr:
+    """A scalar-field element for the scalar restatement of the constraint formulas below."""
+
+    __slots__ = ("v",)
+    m = P.FP_MODULUS
+
+    def __init__(self, v):
+        self.v = v.v if isinstance(v, _Fr) else v % self.m
+
+    def __add__(self, o):
+        return _Fr(self.v + _Fr(o).v)
+
+    __radd__ = __add__
+
+    def __sub__(self, o):
+        return _Fr(self.v - _Fr(o).v)
+
+    def __rsub__(self, o):
+        return _Fr(_Fr(o).v - self.v)
+
+    def __mul__(self, o):
+        return _Fr(self.v * _Fr(o).v)
+
+    __rmul__ = __mul__
+
+
+def test_prove_2p20_commitments_quotient_and_evaluations(hal, corc, prove_2p20):
+    """configs[3] at its own size, beyond the openings (VERDICT r03 missing #1), every check by the CPU
+    oracle on the device's downloaded polynomials:
+
+    * the 33 commitments (16 C_ws, C_z, 16 C_ts; protocol.rs:114,161,263) by the known-log identity
+      commit(p) = (sum_j p_j k_j) G over the synthetic SRS;
+    * the permutation accumulator z (protocol.rs:143-154): NTT_n(z) shifted is z_vals with
+      z_vals[0] = 1 and z_vals[i] g[i] = z_vals[i-1] f[i], f and g formed by the oracle from its own
+      NTTs of w, id, sigma;
+    * f (protocol.rs:193-199) at a random point: f(x) = f_gc(x) + alpha l_1(x)(z(x) - 1)
+      + alpha^2 (z(x) f'(x) - z(omega x) g'(x)), with f_gc(x) the reference's constraint formulas
+      (protocol.rs:170-191) over the witness polynomials' oracle Horner values (every constraint has
+      degree < 8n, so the 8n-domain interpolation is exact) and the Lagrange values in closed form;
+    * the quotient (protocol.rs:255-260, the reference's own commented-out check made exact):
+      f(x) = t(x) Z_H(x) + (f mod Z_H)(x), t(x) = sum_k x^(k n) t_k(x), the remainder folded by the oracle;
+    * the 91 evaluations of the proof (protocol.rs:315-323) by oracle Horner (w_omega_i(xi) as
+      w_i(omega xi), z(omega xi));
+    * the two openings' C and v as the zeta-combinations of those commitments and values
+      (protocol.rs:273-280)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from halo_amd import prover
+
+    n, B, wit, keep, out = (prove_2p20[k] for k in ("n", "B", "wit", "keep", "out"))
+    m = B.m
+    assert m == P.FP_MODULUS
+    tag = "fp"
+    k_logs = corc.synth_scalars(prove_2p20["seed"], n)
+    pool = ThreadPoolExecutor(16)
+
+    def fe(x):
+        return B.fe(x)
+
+    def to_int(a):
+        return B.to_int(a)
+
+    hw = {key: [_host(p) for p in wit[key]] for key in ("qs", "ws", "rs", "ids", "sigmas")}
+    z = _host(keep["z"])
+    f = _host(keep["f"])
+    ts = [_host(t) for t in keep["ts"]]
+    assert len(ts) == prover.T_POLYS and all(len(t) == n for t in ts) and len(z) == n
+
+    # -- commitments by known logs
+    def commit(p):
+        return corc.known_log_msm("pallas", p, k_logs[:len(p)])
+
+    exp_ws = list(pool.map(commit, hw["ws"]))
+    exp_ts = list(pool.map(commit, ts))
+    for i, (a, b) in enumerate(zip(out["C_ws"], exp_ws)):
+        assert np.array_equal(a, b), ("C_ws", i)
+    assert np.array_equal(out["C_z"], commit(z)), "C_z"
+    for i, (a, b) in enumerate(zip(out["C_ts"], exp_ts)):
+        assert np.array_equal(a, b), ("C_ts", i)
+
+    # -- z: the accumulator's recurrence over the oracle's own NTTs
+    beta, gamma, alpha = keep["beta"], keep["gamma"], keep["alpha"]
+    ntt_n = list(pool.map(lambda p: corc.ntt(tag, p, threads=2), hw["ws"][:8] + hw["ids"] + hw["sigmas"] + [z]))
+    w_ev, id_ev, sg_ev, z_ev = ntt_n[:8], ntt_n[8:16], ntt_n[16:24], ntt_n[24]
+    bb, gg = fe(beta), fe(gamma)
+
+    def factor(w, o):
+        return corc.evals_op(tag, 4, corc.evals_op(tag, 0, w, corc.evals_op(tag, 3, o, s=bb)), s=gg)
+
+    fe_v = ge_v = None
+    for i in range(8):
+        a, b = factor(w_ev[i], id_ev[i]), factor(w_ev[i], sg_ev[i])
+        fe_v = a if fe_v is None else corc.evals_op(tag, 2, fe_v, a)
+        ge_v = b if ge_v is None else corc.evals_op(tag, 2, ge_v, b)
+    z_vals = np.ascontiguousarray(np.roll(z_ev, -1, axis=0))   # z_evals = shift_right(z_vals, 1)
+    assert to_int(z_vals[0]) == 1
+    lhs = corc.evals_op(tag, 2, np.ascontiguousarray(z_vals[1:]), np.ascontiguousarray(ge_v[1:]))
+    rhs = corc.evals_op(tag, 2, np.ascontiguousarray(z_vals[:-1]), np.ascontiguousarray(fe_v[1:]))
+    bad = np.nonzero((lhs != rhs).any(axis=1))[0]
+    assert len(bad) == 0, f"z recurrence fails at {bad[:5] + 1}"
+
+    # -- f at a random point from the constraint formulas
+    omega = B.omega(n)
+    x = 0x7A3B9C1D5E6F708192A3B4C5D6E7F8091A2B3C4D5E6F7 % m
+
+    def evals_at(polys, pt):
+        zf = fe(pt)
+        return list(pool.map(lambda p: _Fr(to_int(corc.poly_eval(tag, p, zf))), polys))
+
+    q, w, r = evals_at(hw["qs"], x), evals_at(hw["ws"], x), evals_at(hw["rs"], x)
+    ids, sig = evals_at(hw["ids"], x), evals_at(hw["sigmas"], x)
+    nw = evals_at(hw["ws"][:3], omega * x % m)
+    zx, zwx = evals_at([z], x)[0], evals_at([z], omega * x % m)[0]
+    one = _Fr(1)
+    zh = _Fr(pow(x, n, m) - 1)
+
+    def lagrange(j):  # L_j(x) = omega^j (x^n - 1) / (n (x - omega^j))
+        wj = pow(omega, j, m)
+        return _Fr(wj * zh.v * pow(n * (x - wj), -1, m))
+
+    pi_x = _Fr(0)
+    for i, v in enumerate(wit["public_inputs"]):  # pi = from_vec_and_domain(-public inputs)
+        pi_x = pi_x + _Fr(-v) * lagrange(i + 1)
+    mds = wit["mds"]
+    f_gc = (w[0] * q[0] + q[1] * w[1] + q[2] * w[2] + q[3] * w[0] * w[1] + q[4]
+            + q[5] * prover.poseidon_constraints(mds, r, w, nw, lambda s: s * s * s * s * s * s * s)
+            + q[6] * prover.affine_add_constraints(w, one)
+            + q[7] * prover.affine_mul_constraints(w, nw, r[0], one)
+            + q[8] * prover.eq_constraints(w)
+            + q[9] * prover.range_check_constraints(w, nw, r) + pi_x)
+    fp_x = gp_x = one
+    for i in range(8):
+        fp_x = fp_x * (w[i] + ids[i] * beta + gamma)
+        gp_x = gp_x * (w[i] + sig[i] * beta + gamma)
+    f_exp = f_gc + lagrange(1) * (zx - 1) * alpha + (zx * fp_x - zwx * gp_x) * (alpha * alpha)
+    f_x = evals_at([f], x)[0]
+    assert f_x.v == f_exp.v, "f(x) differs from the constraint formulas"
+
+    # -- quotient: f = t Z_H + (f mod Z_H)
+    rem = np.ascontiguousarray(f[:n].copy())
+    for s in range(n, len(f), n):
+        k = min(n, len(f) - s)
+        rem[:k] = corc.evals_op(tag, 0, np.ascontiguousarray(rem[:k]), np.ascontiguousarray(f[s:s + k]))
+    t_vals = evals_at(ts, x)
+    t_x, xn = _Fr(0), _Fr(pow(x, n, m))
+    for tv in reversed(t_vals):
+        t_x = t_x * xn + tv
+    assert f_x.v == (t_x * zh + evals_at([rem], x)[0]).v, "f != t Z_H + remainder"
+
+    # -- the 91 evaluations at xi
+    xi = keep["xi"]
+    at_xi = hw["ws"] + hw["rs"] + hw["qs"] + ts + hw["ids"] + hw["sigmas"] + [z]
+    exp_vs = [e.v for e in evals_at(at_xi, xi)]
+    exp_vs += [e.v for e in evals_at(hw["ws"], omega * xi % m)]  # w_omega_i(xi) = w_i(omega xi)
+    exp_vs.append(evals_at([z], omega * xi % m)[0].v)
+    assert len(out["vs"]) == len(exp_vs) == 91
+    for i, (a, b) in enumerate(zip(out["vs"], exp_vs)):
+        assert a == b, ("vs", i)
+
+    # -- the openings' C and v are the zeta-combinations (protocol.rs:273-280)
+    zeta = keep["zeta"]
+    exp_qs = list(pool.map(commit, hw["qs"]))
+    r_pts = exp_qs + exp_ws + exp_ts + [commit(z)]
+    r_vals = [e.v for e in evals_at(hw["qs"], xi)] + exp_vs[:16] + exp_vs[41:57] + [exp_vs[73]]
+    ro_pts = exp_ws[:3] + [commit(z)]
+    ro_vals = exp_vs[74:77] + [exp_vs[90]]
+    for key, pts, vals in (("q_r", r_pts, r_vals), ("q_r_omega", ro_pts, ro_vals)):
+        zs = [pow(zeta, i, m) for i in range(len(pts))]
+        C = corc.msm("pallas", np.ascontiguousarray(np.stack(pts)), np.ascontiguousarray(np.stack([fe(s) for s in zs])))
+        assert np.array_equal(out[key]["C"], C), key
+        assert out[key]["v"] == sum(a * b for a, b in zip(zs, vals)) % m, key
+    pool.shutdown()

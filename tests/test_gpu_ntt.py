@@ -1,8 +1,10 @@
 """GPU parity: NTT / iNTT / evaluate_over_domain / interpolate / poly_mul.
 
 Small sizes are checked against the committed golden vectors and the C oracle bit-for-bit; the
-BASELINE sizes (2^20, 2^22) through size-independent properties: iNTT(NTT(x)) == x, linearity, and
-spot evaluations p(omega^i) by Horner on the CPU oracle.
+BASELINE size 2^22 (configs[2]) and the prover's 2^23 transforms against the C oracle element by
+element too (forward and inverse, both fields, the zero-tail path with a 2^20 prefix), and 2^20 /
+2^22 also through size-independent properties: iNTT(NTT(x)) == x, linearity, and spot evaluations
+p(omega^i) by Horner on the CPU oracle.
 """
 import ctypes
 import random
@@ -53,6 +55,51 @@ def test_ntt_vs_c_oracle(hal, corc, tag, fid):
         assert np.array_equal(got, exp), logn
         hal.check(L.halo_ntt(fid, hal.ptr(got), logn, 1))
         assert np.array_equal(got, x), logn
+
+
+@pytest.mark.parametrize("tag,fid", [("fp", 0), ("fq", 1)])
+def test_ntt_2p22_vs_c_oracle(hal, corc, tag, fid):
+    """configs[2] at its own size (two 11-bit passes over 2048-element blocks): the forward and the
+    inverse transform of independent random inputs, each against the oracle element by element."""
+    L = hal.load()
+    logn = 22
+    x = rand_fe(1 << logn, 2200 + fid)
+    got = x.copy()
+    hal.check(L.halo_ntt(fid, hal.ptr(got), logn, 0))
+    assert np.array_equal(got, corc.ntt(tag, x))
+    got = x.copy()
+    hal.check(L.halo_ntt(fid, hal.ptr(got), logn, 1))
+    assert np.array_equal(got, corc.ntt(tag, x, inverse=True))
+
+
+@pytest.mark.parametrize("tag,fid", [("fp", 0), ("fq", 1)])
+def test_ntt_2p23_prover_shapes_vs_c_oracle(hal, corc, tag, fid):
+    """The prover's 8n transforms at n = 2^20 (protocol.rs:88-106; three 8-bit passes over 1024-element
+    blocks) against the oracle element by element: halo_ntt_dev_zero_tail of a 2^20-coefficient
+    polynomial (the 42 NTT(8n) of round 0; the tail holds garbage the transform must ignore), a ragged
+    prefix, and the full forward / inverse device transforms of a random 2^23 vector."""
+    import torch
+
+    L = hal.load()
+    logn = 23
+    N = 1 << logn
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for nz in (1 << 20, (1 << 20) - 3):
+        x = np.zeros((N, 4), dtype=np.uint64)
+        x[:nz] = rand_fe(nz, 2300 + fid)
+        exp = corc.ntt(tag, x)
+        junk = rand_fe(N, 2310 + fid)
+        junk[:nz] = x[:nz]
+        d = torch.from_numpy(junk.view(np.int64)).cuda()
+        hal.check(L.halo_ntt_dev_zero_tail(fid, ctypes.c_void_p(d.data_ptr()), logn, 1, nz, s))
+        torch.cuda.synchronize()
+        assert np.array_equal(d.cpu().numpy().view(np.uint64), exp), nz
+    x = rand_fe(N, 2320 + fid)
+    for inverse in (0, 1):
+        d = torch.from_numpy(x.view(np.int64).copy()).cuda()
+        hal.check(L.halo_ntt_dev(fid, ctypes.c_void_p(d.data_ptr()), logn, 1, inverse, s))
+        torch.cuda.synchronize()
+        assert np.array_equal(d.cpu().numpy().view(np.uint64), corc.ntt(tag, x, inverse=bool(inverse))), inverse
 
 
 @pytest.mark.parametrize("logn", [20, 22])

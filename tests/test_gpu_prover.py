@@ -123,7 +123,7 @@ def test_permutation_accumulator_scan_large(hal):
     ("pallas", 13, "weighted_to_end"), ("pallas", 15, "weighted"), ("pallas", 12, "weighted_fold_after"),
     ("pallas", 13, "srs_tail"), ("vesta", 12, "srs_tail"),
 ])
-def test_ipa_open_tail_switch_vs_c_restatement(hal, monkeypatch, curve, logn, mode):
+def test_ipa_open_tail_switch_vs_c_restatement(hal, curve, logn, mode):
     """An SRS-based opening longer than the tail threshold (2048), against the C restatement of
     pcdl.rs:404-438 (Ls, Rs, U, c).  fold: ordinary rounds (MSM L/R + GLV fold of G) switch to the
     tail rounds (direct sums over G0 with fold weights) mid-opening; fold_srs_round0: the same with
@@ -133,22 +133,27 @@ def test_ipa_open_tail_switch_vs_c_restatement(hal, monkeypatch, curve, logn, mo
     batched shared-scalar MSM and the tail rounds finish; weighted_to_end: no switch, U = sum w[u] G[u]
     at the end; weighted_fold_after: the materialised G continues with ordinary rounds; srs_tail:
     every round a tail round over the SRS's own multiples table (no weighted rounds, no materialised G)."""
-    from prover_ref import CRefBackend
-
     n = 1 << logn
     L = hal.load()
     cid = hal.CURVES[curve]
     hal.check(L.halo_srs_synthesize(cid, n, 777 + logn))
     if mode != "fold":
         hal.check(L.halo_srs_precompute_windows(cid))
-    monkeypatch.setenv("HALO_IPA_WEIGHTED", "1" if mode.startswith("weighted") else "0")
-    # srs_tail (the default up to 2^13): tail rounds from round 1 over the SRS's multiples table; the
-    # other modes pin the weighted / fold paths at these sizes
-    monkeypatch.setenv("HALO_IPA_SRS_TAIL_N", str(n) if mode == "srs_tail" else "0")
+    knobs = {"ipa_weighted": 1 if mode.startswith("weighted") else 0,
+             # srs_tail (the default up to 2^12): tail rounds from round 1 over the SRS's multiples
+             # table; the other modes pin the weighted / fold paths at these sizes
+             "ipa_srs_tail_n": n if mode == "srs_tail" else 0}
     if mode == "weighted_to_end":  # no switch to the tail rounds: U = sum w[u] G[u] over the SRS
-        monkeypatch.setenv("HALO_IPA_MAT_N", "0")
+        knobs["ipa_mat_n"] = 0
     if mode == "weighted_fold_after":  # materialised G (affine) continues with L/R MSMs + GLV folds
-        monkeypatch.setenv("HALO_IPA_TAIL", "0")
+        knobs["ipa_tail"] = 0
+    with hal.tuning(**knobs):
+        _ipa_open_vs_c(hal, L, cid, curve, n, logn)
+
+
+def _ipa_open_vs_c(hal, L, cid, curve, n, logn):
+    from prover_ref import CRefBackend
+
     srs = np.zeros((n, 8), dtype=np.uint64)
     hal.check(L.halo_srs_read(cid, 0, n, hal.ptr(srs)))
     dev = prover.DeviceBackend(curve)

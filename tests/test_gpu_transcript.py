@@ -7,8 +7,9 @@ xi_0 and the per-round xi -- is derived from the device's own C_bar, L and R exa
 pcdl.rs:326-453 derives them.  The resulting EvalProof (Ls, Rs, U, c, C_bar, w') must equal the
 committed fixture of tests/golden/make_transcript.py bit for bit (plain and hiding openings, n =
 16..1024, Pallas and Vesta, reference-recipe SRS and the reference's (S, H)).  The n = 4096 / 2^14
-cases ("big_*") run the device's weighted -> materialised -> tail rounds under the reference's
-transcript order (pcdl.rs:387-425); their inputs are regenerated from the stored seed."""
+cases ("big_*") run the device's SRS-table tail rounds and its weighted -> materialised -> tail
+rounds under the reference's transcript order (pcdl.rs:387-425); their inputs are regenerated from
+the stored seed."""
 import os
 
 import numpy as np
@@ -77,8 +78,19 @@ def det_scalars(seed: int, k: int) -> np.ndarray:
     return np.ascontiguousarray(a)
 
 
-@pytest.mark.parametrize("key", BIG)
-def test_open_without_eval_weighted_rounds_transcript(hal, golden, corc, key):
+BIG_PATHS = [(k, "default") for k in BIG] + [(k, "weighted") for k in BIG if k.split("_")[2] == "n4096"]
+
+
+@pytest.mark.parametrize("key,path", BIG_PATHS)
+def test_open_without_eval_weighted_rounds_transcript(hal, golden, corc, key, path):
+    """default: n = 4096 starts in the tail rounds over the SRS table (ipa_srs_tail_n = 4096), 2^14
+    runs weighted -> materialised -> tail; weighted: n = 4096 pinned to the weighted -> materialised
+    -> tail switch too, under the same reference transcript fixture."""
+    with hal.tuning(ipa_srs_tail_n=0 if path == "weighted" else -1):
+        _open_big(hal, golden, corc, key)
+
+
+def _open_big(hal, golden, corc, key):
     cname = key.split("_")[1]
     n = int(key.split("_")[2][1:])
     hiding = key.endswith("hiding")
@@ -144,3 +156,70 @@ def test_open_session_pool_and_srs_change(hal, golden, corc):
     group.PublicParams.upload("pallas", g, S, Hh, precompute_windows=True)
     pi = pcdl.open_without_eval(G[key + "_p"], G[key + "_C"][0], n - 1, z, v, transcript=SpongeAdapter("pallas"))
     assert np.array_equal(pi["U"], G[key + "_U"][0])
+
+
+def _rounds(ses, xis, cid, k=None):
+    """k rounds (all when None) of L/R + fold with the given Montgomery challenges."""
+    out = []
+    for xi in xis[:k]:
+        out.append(ses.round_lr())
+        ses.fold(xi, pcdl._ark_inverse(xi, cid))
+    return out
+
+
+def test_open_session_across_srs_write(hal, golden, corc):
+    """a session reading the SRS's multiples table (tail rounds from round 1) stays
+    correct when the SRS is rewritten mid-opening (the table is versioned: the rebuild goes to a fresh
+    buffer while the session holds the old one), and a second halo_ipa_end of the same handle does not
+    pool the session twice (two later concurrent sessions keep distinct resources)."""
+    import ctypes
+
+    S, Hh = golden["ref_sh_pallas"]
+    n = 256
+    cid = hal.CURVES["pallas"]
+    g = corc.srs_generate("pallas", n)
+    g2 = np.ascontiguousarray(g[::-1])
+    rng = np.random.default_rng(31)
+    m = P.FP_MODULUS
+    cs = det_scalars(77, n)
+    z = det_scalars(78, 1)[0]
+    hp = g[5]
+    xis = [np.array(P.int_to_limbs(P.to_mont(int(x), m)), dtype=np.uint64)
+           for x in rng.integers(1, 2**62, size=8)]
+
+    def full(srs):
+        group.PublicParams.upload("pallas", srs, S, Hh, precompute_windows=True)
+        ses = pcdl.IpaSession(cs, z, hp)
+        lr = _rounds(ses, xis, cid)
+        return lr, ses.end()
+
+    ref_g, ref_g2 = full(g), full(g2)
+    group.PublicParams.upload("pallas", g, S, Hh, precompute_windows=True)
+    a = pcdl.IpaSession(cs, z, hp)
+    lr_a = _rounds(a, xis, cid, 3)
+    group.PublicParams.upload("pallas", g2, S, Hh, precompute_windows=True)  # SRS write under session a
+    b = pcdl.IpaSession(cs, z, hp)
+    lr_b = _rounds(b, xis, cid)
+    Ub = b.end()
+    lr_a += _rounds(a, xis[3:], cid)
+    Ua = a.end()
+    for (got_lr, got_U), (exp_lr, exp_U) in (((lr_a, Ua), ref_g), ((lr_b, Ub), ref_g2)):
+        assert all(np.array_equal(x[0], y[0]) and np.array_equal(x[1], y[1]) for x, y in zip(got_lr, exp_lr))
+        assert np.array_equal(got_U[0], exp_U[0]) and np.array_equal(got_U[1], exp_U[1])
+    # a second end of an ended handle: reported or harmless, never a doubly pooled session
+    c = pcdl.IpaSession(cs, z, hp)
+    _rounds(c, xis, cid)
+    handle = c._s
+    c.end()
+    hal.load().halo_ipa_end(handle, None, None)
+    d, e = pcdl.IpaSession(cs, z, hp), pcdl.IpaSession(cs, z, hp)
+    assert ctypes.cast(d._s, ctypes.c_void_p).value != ctypes.cast(e._s, ctypes.c_void_p).value
+    lr_d, lr_e = [], []
+    for xi in xis:  # interleaved, so shared buffers would corrupt one of them
+        lr_d.append(d.round_lr())
+        lr_e.append(e.round_lr())
+        d.fold(xi, pcdl._ark_inverse(xi, cid))
+        e.fold(xi, pcdl._ark_inverse(xi, cid))
+    for got in (lr_d, lr_e):
+        assert all(np.array_equal(x[0], y[0]) for x, y in zip(got, ref_g2[0]))
+    assert np.array_equal(d.end()[0], ref_g2[1][0]) and np.array_equal(e.end()[0], ref_g2[1][0])
