@@ -463,12 +463,15 @@ def main():
     # (halo_amd.dist.window_range): every rank the same SRS and scalars (broadcast from rank 0 over
     # RCCL), rank r the windows of its range, partials all-gathered + summed on the device
     def measure_window_partition(lg, reps=4):
-        from halo_amd.dist import window_range
+        from halo_amd.dist import partition_window_bits, window_range
         n_ = 1 << lg
         H.check(L.halo_srs_synthesize(curve, n_, 0x57494E44))  # same seed on every rank
-        H.check(L.halo_srs_precompute_windows(curve))
-        W = L.halo_srs_windows(curve)
+        # a window width whose W divides the world (16 windows of 16 bits over 8 ranks), and on each
+        # rank only the copies of its own windows (2 x 2^24 x 64 B instead of all 15 or 16)
+        c = partition_window_bits(world)
+        W = -(-255 // c)
         lo, hi = window_range(W, rank, world)
+        H.check(L.halo_srs_precompute_window_range(curve, c, lo, hi))
         sc = torch.empty((n_, 4), dtype=torch.int64, device="cuda")
         if rank == 0:
             sc.copy_(torch.randint(-(2**63), 2**63 - 1, (n_, 4), dtype=torch.int64, device="cuda", generator=gen))
@@ -524,8 +527,9 @@ def main():
             torch.cuda.synchronize()
             ok = bool(torch.equal(whole, res))
         del sc
-        return {"workload": f"one 2^{lg}-point MSM, {W} windows split over {world} ranks (window_range), scalars "
-                            f"broadcast from rank 0, partials all-gathered", "windows_of_rank0": [lo, hi],
+        return {"workload": f"one 2^{lg}-point MSM, {W} windows of {c} bits split over {world} ranks (window_range; "
+                            f"each rank holds only its own windows' shifted copies), scalars broadcast from rank 0, "
+                            f"partials all-gathered", "windows_of_rank0": [lo, hi],
                 "points_per_s_with_broadcast": n_ / (out["ms_per_msm_with_broadcast"] * 1e-3),
                 "points_per_s_resident_scalars": n_ / (out["ms_per_msm_resident_scalars"] * 1e-3),
                 "matches_single_gpu": ok, "scaling": "strong", **out}
@@ -601,7 +605,7 @@ def main():
     # every rank holds the same synthetic 2^logn SRS; rank r opens with the shard G[i P + r]
     dist_ipa = None
     if world > 1 and args.ipa and args.dist_ipa:
-        from halo_amd.dist import GpuIpaOps, ipa_shard, sharded_ipa_rounds, torch_gather_objects
+        from halo_amd.dist import GpuIpaOps, ipa_shard, sharded_ipa_rounds, torch_gather_arrays
         n_ = 1 << args.logn
         H.check(L.halo_srs_synthesize(curve, n_, 777))
         G = np.zeros((n_, 8), dtype=np.uint64)
@@ -629,7 +633,7 @@ def main():
             return fe1(pow(v, -1, Rm))
 
         shard = (ipa_shard(G, rank, world), ipa_shard(cs, rank, world), ipa_shard(zs, rank, world))
-        gather = torch_gather_objects(dist)
+        gather = torch_gather_arrays(dist, "cuda")
         best = None
         for _ in range(2):
             ks["k"] = 0

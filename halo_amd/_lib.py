@@ -58,6 +58,7 @@ SIGNATURES = {
     "halo_srs_synthesize": [ctypes.c_int, _sz, ctypes.c_uint64],
     "halo_synth_scalar": [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, _vp],
     "halo_srs_precompute_windows": [ctypes.c_int],
+    "halo_srs_precompute_window_range": [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int],
     "halo_msm": [ctypes.c_int, _vp, _sz, _vp, _sz, _vp],
     "halo_msm_srs": [ctypes.c_int, _vp, _sz, _vp],
     "halo_pedersen_commit": [ctypes.c_int, _vp, _vp, _sz, _vp, _sz, _vp],

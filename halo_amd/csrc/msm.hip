@@ -313,8 +313,9 @@ __global__ __launch_bounds__(64) void k_pairs_out(const uint4* window_sums, cons
 // ---------------------------------------------------------------------------------------------
 // SRS precomputation: window-shifted bases 2^(c w) G_i (w < W) and the hiding table 2^i S
 // ---------------------------------------------------------------------------------------------
+// copies w in [w_lo, w_hi) -> out[(w - w_lo) n + i] (a rank of a window partition holds only its own)
 template <class Cv>
-__global__ __launch_bounds__(64) void k_shift_windows(const uint4* gs, size_t n, int c, int W, uint4* out,
+__global__ __launch_bounds__(64) void k_shift_windows(const uint4* gs, size_t n, int c, int w_lo, int w_hi, uint4* out,
                                                       uint32_t* has_id) {
     using F = typename Cv::Base;
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -322,11 +323,11 @@ __global__ __launch_bounds__(64) void k_shift_windows(const uint4* gs, size_t n,
     const Affine<F> g = aff_load<F>(gs + 4 * i);
     if (aff_is_id(g)) has_id[0] = 1u;  // (every copy of an identity is the identity; a prime-order
                                        // group has no other point with 2^(c w) g = 0)
-    aff_store(out + 4 * i, g);
+    if (w_lo == 0) aff_store(out + 4 * i, g);
     XYZZ<F> p = xyzz_from_aff(g);
-    for (int w = 1; w < W; w++) {
+    for (int w = 1; w < w_hi; w++) {
         for (int k = 0; k < c; k++) p = xyzz_dbl(p);
-        aff_store(out + 4 * ((size_t)w * n + i), xyzz_to_aff(p));
+        if (w >= w_lo) aff_store(out + 4 * ((size_t)(w - w_lo) * n + i), xyzz_to_aff(p));
     }
 }
 
@@ -494,7 +495,7 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
                         const uint4* scalars_ark, size_t n, int c_req, const uint4* hide_table, const uint4* hide_scalar,
                         uint4* d_out_wrapped, hipStream_t s, bool async, uint32_t blk_lg = 32,
                         bool hide_glv = false, bool out_xyzz = false, hipEvent_t hide_ready = nullptr,
-                        int preset = -1, int w_lo = 0, int w_hi = 0) {
+                        int preset = -1, int w_lo = 0, int w_hi = 0, int base_w0 = 0) {
     MsmPipe& PP = g_msm_pipe[st->device & 63];
     HALO_CHECK(pipe_init(PP));
     // preset: the set the caller already claimed (and waited for) to stage converted bases in
@@ -518,7 +519,8 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
     if (w_lo < 0 || w_hi > W_all || w_lo >= w_hi)
         return set_error(HALO_EINVAL, "window range [%d, %d) outside [0, %d)", w_lo, w_hi, W_all);
     const int W = w_hi - w_lo;
-    if (shifted && w_lo) bases_int += 4 * (size_t)w_lo * shift_stride;
+    // (the copies start at window base_w0: a partially precomputed range)
+    if (shifted && w_lo != base_w0) bases_int += 4 * (size_t)(w_lo - base_w0) * shift_stride;
     const uint32_t B = 1u << (c - 1);
     // sort geometry: SW windows of SN entries each (shifted: one window over all W * n digits)
     const int SW = shifted ? 1 : W;
@@ -1381,26 +1383,40 @@ static int build_s_table(DeviceState* st, int curve, hipStream_t s) {
     return HALO_OK;
 }
 
-int srs_precompute_windows(DeviceState* st, int curve, hipStream_t s) {
+// The window-shifted copies 2^(c w) G_i for w in [w_lo, w_hi) (c = 0: the default width for the SRS
+// length; w_hi = 0: every window).  The full set serves every SRS MSM; a partial range (one rank of a
+// window-partitioned MSM, BASELINE configs[4]) serves halo_msm_srs_windows_dev over that range only.
+int srs_precompute_windows(DeviceState* st, int curve, hipStream_t s, int c, int w_lo, int w_hi) {
     SrsState& srs = st->srs[curve];
     if (!srs.n) return set_error(HALO_ESRSRANGE, "no resident SRS to precompute");
-    const int c = msm_shifted_window_bits(srs.n);
+    if (c == 0) c = msm_shifted_window_bits(srs.n);
+    if (c < 8 || c > 20) return set_error(HALO_EINVAL, "window bits %d outside [8, 20]", c);
     const int W = msm_windows(c);
-    HALO_CHECK(srs.shifted.reserve((size_t)W * srs.n * 64));
+    if (w_hi == 0) w_hi = W;
+    if (w_lo < 0 || w_hi > W || w_lo >= w_hi)
+        return set_error(HALO_EINVAL, "window range [%d, %d) outside [0, %d)", w_lo, w_hi, W);
+    srs.shifted_c = srs.part_c = 0;  // nothing valid while the copies are rewritten
+    HALO_CHECK(srs.shifted.reserve((size_t)(w_hi - w_lo) * srs.n * 64));
     ScratchUse su(st, s);
     HALO_CHECK(st->scratch[7].reserve(4));
     uint32_t* flag = st->scratch[7].as<uint32_t>();
     HALO_HIP(hipMemsetAsync(flag, 0, 4, s));
     DISPATCH_CURVE(curve, Cv, {
         hipLaunchKernelGGL(k_shift_windows<Cv>, dim3(grid_for(srs.n, 64)), dim3(64), 0, s, srs.gs.as<const uint4>(),
-                           srs.n, c, W, srs.shifted.as<uint4>(), flag);
+                           srs.n, c, w_lo, w_hi, srs.shifted.as<uint4>(), flag);
     });
     HALO_HIP(hipGetLastError());
     uint32_t has_id = 1;
     HALO_HIP(hipMemcpyAsync(&has_id, flag, 4, hipMemcpyDeviceToHost, s));
     HALO_HIP(hipStreamSynchronize(s));
     srs.shifted_has_id = has_id != 0;
-    srs.shifted_c = c;
+    if (w_lo == 0 && w_hi == W) {
+        srs.shifted_c = c;
+    } else {
+        srs.part_c = c;
+        srs.part_w0 = w_lo;
+        srs.part_w1 = w_hi;
+    }
     return HALO_OK;
 }
 
@@ -1441,7 +1457,8 @@ extern "C" int halo_srs_window_bits(halo_curve_t curve) {
     DeviceState* st = current_state();
     if (!st) return HALO_EDEVICE;
     std::lock_guard<std::mutex> g(st->mu);
-    return st->srs[curve].shifted_c;
+    const SrsState& srs = st->srs[curve];
+    return srs.shifted_c ? srs.shifted_c : srs.part_c;
 }
 
 extern "C" int halo_point_sum(halo_curve_t curve, const halo_wrapped_point_t* pts, size_t k, halo_wrapped_point_t* out) {
@@ -1797,13 +1814,17 @@ extern "C" int halo_srs_synthesize(halo_curve_t curve, size_t n, uint64_t seed) 
 }
 
 extern "C" int halo_srs_precompute_windows(halo_curve_t curve) {
+    return halo_srs_precompute_window_range(curve, 0, 0, 0);
+}
+
+extern "C" int halo_srs_precompute_window_range(halo_curve_t curve, int c, int w_lo, int w_hi) {
     clear_error();
     HALO_CHECK(check_curve(curve));
     DeviceState* st = current_state();
     if (!st) return HALO_EDEVICE;
     std::lock_guard<std::mutex> g(st->mu);
     ScratchUse su(st, 0);
-    return srs_precompute_windows(st, curve, 0);
+    return srs_precompute_windows(st, curve, 0, c, w_lo, w_hi);
 }
 
 extern "C" int halo_msm_srs(halo_curve_t curve, const halo_fe_t* scalars, size_t n, halo_wrapped_point_t* out) {
@@ -1912,14 +1933,19 @@ extern "C" int halo_msm_srs_windows_dev(halo_curve_t curve, const void* d_scalar
     if (!st) return HALO_EDEVICE;
     std::lock_guard<std::mutex> g(st->mu);
     SrsState& srs = st->srs[curve];
-    if (!srs.shifted_c) return set_error(HALO_EINVAL, "halo_msm_srs_windows_dev: no window-shifted SRS");
+    // the full set of copies, or this rank's range of them (halo_srs_precompute_window_range)
+    const int c = srs.shifted_c ? srs.shifted_c : srs.part_c;
+    const int w0 = srs.shifted_c ? 0 : srs.part_w0, w1 = srs.shifted_c ? msm_windows(c) : srs.part_w1;
+    if (!c) return set_error(HALO_EINVAL, "halo_msm_srs_windows_dev: no window-shifted SRS");
     if (n > srs.n) return set_error(HALO_ESRSRANGE, "n (%zu) exceeds the resident SRS length (%zu)", n, srs.n);
     if (w_hi <= w_lo) return set_error(HALO_EINVAL, "empty window range [%d, %d)", w_lo, w_hi);
+    if (w_lo < w0 || w_hi > w1)
+        return set_error(HALO_EINVAL, "window range [%d, %d) not resident (copies of [%d, %d))", w_lo, w_hi, w0, w1);
     int rc;
     DISPATCH_CURVE(curve, Cv, {
-        rc = msm_device_t<Cv>(st, srs.shifted.as<const uint4>(), true, srs.n, (const uint4*)d_scalars, n,
-                              srs.shifted_c, nullptr, nullptr, (uint4*)d_out, (hipStream_t)stream, true, 32, false,
-                              false, nullptr, -1, w_lo, w_hi);
+        rc = msm_device_t<Cv>(st, srs.shifted.as<const uint4>(), true, srs.n, (const uint4*)d_scalars, n, c, nullptr,
+                              nullptr, (uint4*)d_out, (hipStream_t)stream, true, 32, false, false, nullptr, -1, w_lo,
+                              w_hi, w0);
     });
     return rc;
 }
@@ -1930,7 +1956,9 @@ extern "C" int halo_srs_windows(halo_curve_t curve) {
     DeviceState* st = current_state();
     if (!st) return HALO_EDEVICE;
     std::lock_guard<std::mutex> g(st->mu);
-    return st->srs[curve].shifted_c ? msm_windows(st->srs[curve].shifted_c) : 0;
+    const SrsState& srs = st->srs[curve];
+    const int c = srs.shifted_c ? srs.shifted_c : srs.part_c;
+    return c ? msm_windows(c) : 0;
 }
 
 extern "C" int halo_msm_join(void* stream) {

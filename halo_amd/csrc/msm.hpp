@@ -62,7 +62,7 @@ int msm_srs_pairs_device(DeviceState* st, int curve, size_t np, const MsmPairIO*
 // over three windows (~2 c_s / 3 doublings) instead of ~255 / c windows (~255 doublings).
 int msm_shared_batch(DeviceState* st, int curve, const void* bases_int, const void* w_ark, size_t T, size_t len,
                      void* out, bool xyzz_out, BatchScratch& S, hipStream_t s, size_t shift_stride = 0, int c_s = 0);
-int srs_precompute_windows(DeviceState* st, int curve, hipStream_t s);
+int srs_precompute_windows(DeviceState* st, int curve, hipStream_t s, int c = 0, int w_lo = 0, int w_hi = 0);
 // Small MSM over the resident SRS prefix (1 <= n <= srs_small_max(), ipa.hip): every (point, 4-bit GLV
 // window) term is one entry of a per-SRS multiples table, then block trees with the hiding term
 // hide_scalar * S from the 2^i S table -- no sort, buckets or bucket reduction.  Stream-ordered on s;

@@ -74,14 +74,15 @@ struct SrsState {
     DevBuf small_scr;                // GLV digits, block partials of a small MSM
     hipEvent_t small_ev = nullptr;   // last small MSM's completion (orders reuse of small_scr)
     DevBuf shifted;     // optional window-shifted copies
-    int shifted_c = 0;  // window bits of `shifted`
+    int shifted_c = 0;  // window bits of `shifted` when it holds every window (0: not built)
+    int part_c = 0, part_w0 = 0, part_w1 = 0;  // ... or only the windows [part_w0, part_w1) of width part_c
     bool shifted_has_id = true;  // some SRS point is the identity (k_acc then tests every base)
     int shifted_windows = 0;
     // Every writer of `gs` calls this: the tables derived from the old points (window-shifted copies,
     // the small-MSM / tail multiples table) are rebuilt on next use.  (a synthesize after
     // a small commit used to keep the old SRS's table.)
     void invalidate_derived() {
-        shifted_c = 0;
+        shifted_c = part_c = 0;
         shifted_windows = 0;
         shifted_has_id = true;
         small_n0 = 0;

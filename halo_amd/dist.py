@@ -19,17 +19,24 @@ def shard_range(n_total: int, rank: int, world: int) -> tuple[int, int]:
     return lo, min(n_total, lo + per)
 
 
-def allgather_points(partial: np.ndarray, dist, device=None) -> np.ndarray:
-    """All-gather one WrappedPoint (8 x u64) per rank -> (world, 8) uint64 array."""
+def allgather_words(words: np.ndarray, dist, device=None) -> np.ndarray:
+    """All-gather a fixed-shape uint64 array from every rank as one tensor collective (RCCL over xGMI
+    when `device` is a GPU, gloo on the CPU; no object pickling) -> (world, *shape) uint64 array."""
     import torch
 
     world = dist.get_world_size()
-    t = torch.from_numpy(np.ascontiguousarray(partial, dtype=np.uint64).view(np.int64).copy())
+    a = np.ascontiguousarray(words, dtype=np.uint64)
+    t = torch.from_numpy(a.reshape(-1).view(np.int64).copy())
     if device is not None:
         t = t.to(device)
     parts = [torch.empty_like(t) for _ in range(world)]
     dist.all_gather(parts, t)
-    return np.stack([p.cpu().numpy().view(np.uint64) for p in parts])
+    return torch.stack(parts).cpu().numpy().view(np.uint64).reshape((world,) + a.shape)
+
+
+def allgather_points(partial: np.ndarray, dist, device=None) -> np.ndarray:
+    """All-gather one WrappedPoint (8 x u64) per rank -> (world, 8) uint64 array."""
+    return allgather_words(np.asarray(partial, dtype=np.uint64).reshape(8), dist, device)
 
 
 def sharded_msm(partial_msm: Callable[[int, int], np.ndarray], point_sum: Callable[[np.ndarray], np.ndarray],
@@ -49,10 +56,22 @@ def sharded_msm(partial_msm: Callable[[int, int], np.ndarray], point_sum: Callab
 # and the same window-shifted SRS copies; rank r takes the windows window_range(W, r, P) of every
 # scalar (halo_msm_srs_windows_dev).  With the shifted copies 2^(c w) G the per-window sums are
 # already weighted, so the partials simply add: the same all-gather + point sum as point-partition.
-# It costs a scalar broadcast (32 B x n over xGMI) that point-partition does not need, and W rarely
-# divides evenly (15 windows over 8 ranks: 2 + ... + 1), so point-partition is the default
-# (DESIGN.md §6); this path is measured beside it in bench.py (extra.msm_window_partition).
+# It costs a scalar broadcast (32 B x n over xGMI) that point-partition does not need; the window
+# width is chosen so that W divides the world size (partition_window_bits: 16 windows of 16 bits over
+# 8 ranks) and each rank precomputes only its own windows' copies (halo_srs_precompute_window_range).
+# Point-partition stays the default; this path is measured beside it in bench.py.
 # ---------------------------------------------------------------------------------------------
+def partition_window_bits(world: int) -> int:
+    """Window width for a window partition over `world` ranks: the default 17 bits (15 windows) when
+    15 splits evenly, else the nearest width whose window count W = ceil(255 / c) does (16 bits: 16
+    windows for 2, 4, 8, 16 ranks), so no rank carries an extra window (15 over 8 ranks would cap the
+    split at 7.5x)."""
+    for c in (17, 16, 15, 18, 14):
+        if (-(-255 // c)) % world == 0:
+            return c
+    return 17
+
+
 def window_range(W: int, rank: int, world: int) -> tuple[int, int]:
     """Contiguous windows [lo, hi) of rank r: the first W % P ranks take one more."""
     base, extra = divmod(W, world)
@@ -260,17 +279,17 @@ def poly_eval_combine(parts, n_total: int, z, ops: PolyOps) -> np.ndarray:
     return np.asarray(ops.eval_batch([np.stack(parts)], ops.pow(z, per))[0], dtype=np.uint64)
 
 
-def sharded_poly_eval(coeffs_local, n_total: int, z, dist, ops: PolyOps | None = None) -> np.ndarray:
+def sharded_poly_eval(coeffs_local, n_total: int, z, dist, ops: PolyOps | None = None, device=None) -> np.ndarray:
     """DensePolynomial::evaluate (pcdl.rs:49,471) of a polynomial whose coefficients are split into
-    contiguous blocks over the ranks (rank r holds coeffs[shard_range(n_total, r, P)])."""
+    contiguous blocks over the ranks (rank r holds coeffs[shard_range(n_total, r, P)]).  The 32-B
+    partial values travel as one tensor all-gather (RCCL when `device` is the rank's GPU)."""
     ops = ops or PolyOps()
     rank, world = dist.get_rank(), dist.get_world_size()
     lo, hi = shard_range(n_total, rank, world)
     if len(coeffs_local) != hi - lo:
         raise ValueError("coefficient block does not match shard_range")
-    parts = [None] * world
-    dist.all_gather_object(parts, poly_eval_partial(coeffs_local, z, ops))
-    return poly_eval_combine(parts, n_total, z, ops)
+    parts = allgather_words(poly_eval_partial(coeffs_local, z, ops), dist, device)
+    return poly_eval_combine(list(parts), n_total, z, ops)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -352,7 +371,7 @@ def sharded_ipa_rounds(local_shards, H_prime, challenge: Callable, inverse: Call
                        gather: Callable):
     """Distributed pcdl round loop.  ``local_shards``: the (gs, cs, zs) strided shards (ipa_shard)
     this process holds -- one with a real communicator, all P with virtual ranks; ``gather(objs)``
-    returns the list of every rank's objs in rank order (torch_gather_objects(dist), or identity for
+    returns the list of every rank's objs in rank order (torch_gather_arrays(dist), or identity for
     virtual ranks).  Returns (Ls, Rs, U, c) exactly as the single-session ipa_rounds does."""
     if world < 1 or world & (world - 1):
         raise ValueError("world size must be a power of two")
@@ -378,12 +397,28 @@ def sharded_ipa_rounds(local_shards, H_prime, challenge: Callable, inverse: Call
     return Ls, Rs, np.asarray(G[0], dtype=np.uint64), np.asarray(C[0], dtype=np.uint64)
 
 
-def torch_gather_objects(dist):
-    """gather() for sharded_ipa_rounds over a torch.distributed group (gloo or RCCL)."""
+def torch_gather_arrays(dist, device=None):
+    """gather() for sharded_ipa_rounds over a torch.distributed group: each rank's objs (tuples of
+    uint64 arrays whose shapes are the same on every rank: (L, R) points, or the final (g, c, z)) are
+    flattened into one word vector and exchanged by one tensor all-gather (RCCL when `device` is the
+    rank's GPU, gloo on the CPU) -- no object pickling on the data path."""
 
     def f(objs):
-        out = [None] * dist.get_world_size()
-        dist.all_gather_object(out, list(objs))
-        return [o for part in out for o in part]
+        objs = [tuple(np.ascontiguousarray(a, dtype=np.uint64) for a in o) for o in objs]
+        shapes = [[a.shape for a in o] for o in objs]
+        flat = np.concatenate([a.reshape(-1) for o in objs for a in o]) if objs else np.zeros(0, np.uint64)
+        got = allgather_words(flat, dist, device)
+        out = []
+        for r in range(got.shape[0]):
+            pos = 0
+            for shp in shapes:
+                parts = []
+                for sh in shp:
+                    k = int(np.prod(sh))
+                    parts.append(got[r, pos:pos + k].reshape(sh))
+                    pos += k
+                out.append(tuple(parts))
+        return out
 
     return f
+

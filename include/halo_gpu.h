@@ -108,6 +108,11 @@ void halo_synth_scalar(halo_curve_t curve, uint64_t seed, uint64_t j, uint64_t o
 /* Precomputes the window-shifted copies 2^(c*w) * G_i of the resident SRS used by the
  * single-bucket-set MSM (trades HBM capacity for the per-window combination); optional. */
 int halo_srs_precompute_windows(halo_curve_t curve);
+/* The copies of windows [w_lo, w_hi) only, of width c bits (c = 0: the default width for the SRS
+ * length; w_hi = 0: every window): one rank of a window-partitioned MSM holds just its own windows
+ * (BASELINE configs[4]); such a partial set serves halo_msm_srs_windows_dev over that range only (the
+ * other SRS MSMs then run without shifted copies). */
+int halo_srs_precompute_window_range(halo_curve_t curve, int c, int w_lo, int w_hi);
 
 /* Copies resident SRS points Gs[offset .. offset + n) back to the host as WrappedPoints. */
 int halo_srs_read(halo_curve_t curve, size_t offset, size_t n, halo_wrapped_point_t* out);
@@ -174,7 +179,8 @@ int halo_msm_batch_dev(halo_curve_t curve, const void* const* d_scalars, const s
 /* Window-partitioned MSM (BASELINE configs[4]): one rank's share -- the signed digits of windows
  * [w_lo, w_hi) of the n scalars against the resident window-shifted copies 2^(c w) G_i -- as a 64-B
  * partial sum at d_out (asynchronous, halo_msm_join).  Partials of a partition of [0, W) add up to
- * the full MSM (pedersen.rs:21).  halo_srs_windows gives W (0 without the shifted copies). */
+ * the full MSM (pedersen.rs:21).  halo_srs_windows gives W (0 without the shifted copies); the range
+ * must lie inside the resident copies (all of them, or halo_srs_precompute_window_range's range). */
 int halo_msm_srs_windows_dev(halo_curve_t curve, const void* d_scalars, size_t n, int w_lo, int w_hi, void* d_out,
                              void* stream);
 int halo_srs_windows(halo_curve_t curve);

@@ -254,7 +254,7 @@ def _ipa_worker(rank, world, port, cname, n, q):
     sys.path.insert(0, ROOT)
     import torch.distributed as dist
 
-    from halo_amd.dist import ipa_shard, sharded_ipa_rounds, torch_gather_objects
+    from halo_amd.dist import ipa_shard, sharded_ipa_rounds, torch_gather_arrays
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -262,7 +262,7 @@ def _ipa_worker(rank, world, port, cname, n, q):
     g, cs, zs, Hp = ipa_instance(cname, n)
     shard = (ipa_shard(g, rank, world), ipa_shard(cs, rank, world), ipa_shard(zs, rank, world))
     ch, inv = ipa_transcript(cname)
-    Ls, Rs, U, c = sharded_ipa_rounds([shard], Hp, ch, inv, OracleIpaOps(cname), world, torch_gather_objects(dist))
+    Ls, Rs, U, c = sharded_ipa_rounds([shard], Hp, ch, inv, OracleIpaOps(cname), world, torch_gather_arrays(dist))
     q.put((rank, [x.tolist() for x in Ls], [x.tolist() for x in Rs], U.tolist(), c.tolist()))
     dist.barrier()
     dist.destroy_process_group()
@@ -434,3 +434,15 @@ def test_window_partitioned_msm_gloo(corc, world):
     sc[:, 3] &= np.uint64(0x3FFFFFFFFFFFFFFF)
     exp = corc.msm("pallas", g, sc).tolist()
     assert all(o[1] == exp for o in out)
+
+
+def test_partition_window_bits_balanced():
+    """configs[4]: the window width chosen for a window partition splits W evenly over the ranks
+    (16 windows of 16 bits over 2 / 4 / 8 / 16 ranks, the default 15 x 17 bits over 3 / 5)."""
+    from halo_amd.dist import partition_window_bits, window_range
+    for world, c in ((1, 17), (2, 16), (3, 17), (4, 16), (5, 17), (8, 16), (16, 16)):
+        assert partition_window_bits(world) == c
+        W = -(-255 // c)
+        spans = [window_range(W, r, world) for r in range(world)]
+        assert spans[0][0] == 0 and spans[-1][1] == W
+        assert len({hi - lo for lo, hi in spans}) == 1

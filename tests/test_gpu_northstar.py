@@ -48,40 +48,66 @@ def test_msm_2p24_synthetic_srs_known_logs(hal, corc):
 
 def test_msm_2p24_window_partitioned_virtual_ranks_known_logs(hal, corc):
     """BASELINE configs[4] at its size on one GPU: the 2^24-point MSM split by windows over 8 virtual
-    ranks (halo_amd.dist.window_range, the ranges bench.py --gpus 8 gives its ranks), each rank's
-    partial from halo_msm_srs_windows_dev, the partials summed on the device (halo_point_sum_dev, the
-    RCCL leg's combine) -- checked against the known-log identity (an independent oracle, not the
-    device's own one-GPU MSM); and the 3-rank partition of the same MSM."""
+    ranks as bench.py --gpus 8 splits it -- 16 windows of 16 bits (halo_amd.dist.partition_window_bits),
+    2 per rank, and each rank precomputing ONLY its own windows' shifted copies
+    (halo_srs_precompute_window_range) before its partial (halo_msm_srs_windows_dev); the partials
+    summed on the device (halo_point_sum_dev, the RCCL leg's combine) and checked against the
+    known-log identity (an independent oracle).  Then the 3-rank partition (15 windows of 17 bits,
+    5 each) over the full set of copies."""
     import ctypes
 
     import torch
-    from halo_amd.dist import window_range
+    from halo_amd.dist import partition_window_bits, window_range
 
     L = hal.load()
     n = 1 << 24
     seed = 0x57494E44
-    group.PublicParams.synthesize("pallas", n, seed, precompute_windows=True)
+    cid = hal.CURVES["pallas"]
+    hal.check(L.halo_srs_synthesize(cid, n, seed))
     k = corc.synth_scalars(seed, n)
     sc = rand_words(n, 4242)
     sc[0] = P.int_to_limbs(P.to_mont(P.FP_MODULUS - 1, P.FP_MODULUS))
     sc[1:2049] = sc[7]  # one bucket per window takes 2^11 extra points
     exp = corc.known_log_msm("pallas", sc, k)
-    W = L.halo_srs_windows(0)
     d_sc = torch.from_numpy(sc.view(np.int64)).cuda()
     sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    for world in (8, 3):
-        outs = torch.zeros((world, 8), dtype=torch.int64, device="cuda")
-        for r in range(world):
-            lo, hi = window_range(W, r, world)
-            assert hi > lo
-            hal.check(L.halo_msm_srs_windows_dev(0, ctypes.c_void_p(d_sc.data_ptr()), n, lo, hi,
-                                                 ctypes.c_void_p(outs[r].data_ptr()), sp))
-        hal.check(L.halo_msm_join(sp))
+
+    def combine(outs, world):
         total = torch.zeros(8, dtype=torch.int64, device="cuda")
-        hal.check(L.halo_point_sum_dev(0, ctypes.c_void_p(outs.data_ptr()), world, 64, ctypes.c_void_p(total.data_ptr()),
-                                       sp))
+        hal.check(L.halo_point_sum_dev(cid, ctypes.c_void_p(outs.data_ptr()), world, 64,
+                                       ctypes.c_void_p(total.data_ptr()), sp))
         torch.cuda.synchronize()
-        assert np.array_equal(total.cpu().numpy().view(np.uint64), exp), world
+        return total.cpu().numpy().view(np.uint64)
+
+    world = 8
+    c = partition_window_bits(world)
+    W = -(-255 // c)
+    assert (c, W) == (16, 16)
+    outs = torch.zeros((world, 8), dtype=torch.int64, device="cuda")
+    for r in range(world):
+        lo, hi = window_range(W, r, world)
+        assert hi - lo == W // world  # balanced: no rank carries an extra window
+        hal.check(L.halo_srs_precompute_window_range(cid, c, lo, hi))  # this rank's copies only
+        assert L.halo_srs_windows(cid) == W and L.halo_srs_window_bits(cid) == c
+        if r:  # a window outside the resident range is refused
+            assert L.halo_msm_srs_windows_dev(cid, ctypes.c_void_p(d_sc.data_ptr()), n, 0, hi,
+                                              ctypes.c_void_p(outs[r].data_ptr()), sp) != 0
+        hal.check(L.halo_msm_srs_windows_dev(cid, ctypes.c_void_p(d_sc.data_ptr()), n, lo, hi,
+                                             ctypes.c_void_p(outs[r].data_ptr()), sp))
+        hal.check(L.halo_msm_join(sp))
+    assert np.array_equal(combine(outs, world), exp)
+
+    group.PublicParams.synthesize("pallas", n, seed, precompute_windows=True)
+    W = L.halo_srs_windows(cid)
+    world = 3
+    outs = torch.zeros((world, 8), dtype=torch.int64, device="cuda")
+    for r in range(world):
+        lo, hi = window_range(W, r, world)
+        assert hi - lo == 5
+        hal.check(L.halo_msm_srs_windows_dev(cid, ctypes.c_void_p(d_sc.data_ptr()), n, lo, hi,
+                                             ctypes.c_void_p(outs[r].data_ptr()), sp))
+    hal.check(L.halo_msm_join(sp))
+    assert np.array_equal(combine(outs, world), exp)
     del d_sc
 
 
