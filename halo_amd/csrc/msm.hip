@@ -1390,7 +1390,7 @@ int srs_precompute_windows(DeviceState* st, int curve, hipStream_t s, int c, int
     SrsState& srs = st->srs[curve];
     if (!srs.n) return set_error(HALO_ESRSRANGE, "no resident SRS to precompute");
     if (c == 0) c = msm_shifted_window_bits(srs.n);
-    if (c < 8 || c > 20) return set_error(HALO_EINVAL, "window bits %d outside [8, 20]", c);
+    if (c < 2 || c > 20) return set_error(HALO_EINVAL, "window bits %d outside [2, 20]", c);
     const int W = msm_windows(c);
     if (w_hi == 0) w_hi = W;
     if (w_lo < 0 || w_hi > W || w_lo >= w_hi)
