@@ -79,7 +79,7 @@ HALO_DEV Affine<F> aff_neg(const Affine<F>& a) {
 template <class F>
 HALO_DEV XYZZ<F> xyzz_dbl(const XYZZ<F>& p) {
     if (xyzz_is_id(p)) return p;
-    const Fe<F> U = fe_add_nc(p.Y, p.Y);
+    const Fe<F> U = fe_norm(fe_add_nc(p.Y, p.Y));  // normalized: squared below (fields.hpp bounds)
     const Fe<F> V = fe_sqr(U);
     const Fe<F> W = fe_mul(U, V);
     const Fe<F> S = fe_mul(p.X, V);
@@ -96,7 +96,7 @@ HALO_DEV XYZZ<F> xyzz_dbl(const XYZZ<F>& p) {
 // Doubling of an affine point into XYZZ (mdbl-2008-s-1)
 template <class F>
 HALO_DEV XYZZ<F> xyzz_mdbl(const Affine<F>& a) {
-    const Fe<F> U = fe_add_nc(a.y, a.y);
+    const Fe<F> U = fe_norm(fe_add_nc(a.y, a.y));  // normalized: squared below
     const Fe<F> V = fe_sqr(U);
     const Fe<F> W = fe_mul(U, V);
     const Fe<F> S = fe_mul(a.x, V);
@@ -167,11 +167,7 @@ HALO_DEV XYZZ<F> xyzz_madd_acc(const XYZZ<F>& p, const Affine<F>& q, uint32_t ne
     XYZZ<F> r;
     r.X = fe_sub_k<6>(R2, fe_add_nc(PPP, fe_add_nc(Q, Q)));  // < 8p
     const Fe<F> T = fe_sub_k<8>(Q, r.X);                       // < 10p
-#ifndef HALO_Y3_TWO_MULS
     r.Y = fe_mul2(R, T, PPP, fe_sub_k<2>(fe_zero<F>(), p.Y));
-#else
-    r.Y = fe_sub(fe_mul(R, T), fe_mul(p.Y, PPP));
-#endif
     r.ZZ = ZZ3;
     r.ZZZ = fe_mul(p.ZZZ, PPP);
     if (fe_is_zero(ZZ3)) {  // U2 == X1: q = +-p (ZZ1 != 0), off the common path
@@ -215,11 +211,7 @@ HALO_DEV XYZZ<F> xyzz_madd_run(const XYZZ<F>& p, bool& fresh, const Affine<F>& q
     XYZZ<F> r;
     r.X = fe_sub_k<6>(R2, fe_add_nc(PPP, fe_add_nc(Q, Q)));  // < 8p
     const Fe<F> T = fe_sub_k<8>(Q, r.X);                       // < 10p
-#ifndef HALO_Y3_TWO_MULS
     r.Y = fe_mul2(R, T, PPP, fe_sub_k<2>(fe_zero<F>(), p.Y));
-#else
-    r.Y = fe_sub(fe_mul(R, T), fe_mul(p.Y, PPP));
-#endif
     r.ZZ = ZZ3;
     r.ZZZ = fe_mul(p.ZZZ, PPP);
     if (P.v[0] < 10u && fe_is_zero(ZZ3)) {  // U2 == X1: q = +-p, off the common path

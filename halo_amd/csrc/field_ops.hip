@@ -71,7 +71,6 @@ HALO_DEV XYZZ<typename Cv::Base> scalar_mul_glv(const Affine<typename Cv::Base>&
     return acc;
 }
 
-#if HALO_TREE_COOP
 // The same scalar multiplication by an aligned quad of lanes (every lane holds P, k and the running
 // sum): the doublings are xyzz_dbl_quad (three product rounds instead of nine) and the additions
 // xyzz_add_quad (four instead of fourteen).  tab: 32 XYZZ of this quad in LDS, d P for d < 16 and
@@ -129,14 +128,12 @@ HALO_DEV XYZZ<typename Cv::Base> scalar_mul_glv_quad(const Affine<typename Cv::B
     }
     return acc;
 }
-#endif
 
 template <class Cv>
 __global__ __launch_bounds__(64) void k_curve_op(int op, const uint4* a, const uint4* b, const uint4* k, uint4* out, size_t n) {
     using F = typename Cv::Base;
     using S = typename Cv::Scalar;
-    extern __shared__ uint4 smul_tab[];  // op 2: 32 XYZZ (128 B) per quad (16 per lane without HALO_TREE_COOP)
-#if HALO_TREE_COOP
+    extern __shared__ uint4 smul_tab[];  // op 2: 32 XYZZ (128 B) per quad
     if (op == 2) {  // one quad per scalar multiplication; quads past n repeat the last one (no store), so
                     // every lane reaches the table build's barriers
         const size_t i = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2;
@@ -147,7 +144,6 @@ __global__ __launch_bounds__(64) void k_curve_op(int op, const uint4* a, const u
         if (i < n && (threadIdx.x & 3u) == 0) aff_to_wrapped(out + 4 * i, xyzz_to_aff(r));
         return;
     }
-#endif
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     Affine<F> p = aff_from_wrapped<F>(a + 4 * i);
@@ -214,15 +210,10 @@ extern "C" int halo_curve_op(halo_curve_t curve, int op, const halo_wrapped_poin
     HALO_CHECK(copy_h2d(st->scratch[0].ptr, a, pb, s));
     if (b) HALO_CHECK(copy_h2d(st->scratch[1].ptr, b, pb, s));
     if (k) HALO_CHECK(copy_h2d(st->scratch[2].ptr, k, kb, s));
-#if HALO_TREE_COOP
     // op 2: a quad per scalar multiplication, 32 table entries of 128 B per quad
     const size_t lanes = op == 2 ? 4 * n : n;
     const unsigned threads = op == 2 ? 4 * CURVE_OP_SMUL_THREADS : 64, blocks = (unsigned)((lanes + threads - 1) / threads);
     const size_t smem = op == 2 ? (size_t)(threads / 4) * 32 * 128 : 0;
-#else
-    const unsigned threads = op == 2 ? CURVE_OP_SMUL_THREADS : 64, blocks = (unsigned)((n + threads - 1) / threads);
-    const size_t smem = op == 2 ? (size_t)threads * 16 * 128 : 0;
-#endif
     DISPATCH_CURVE(curve, Cv, {
         hipLaunchKernelGGL(k_curve_op<Cv>, dim3(blocks), dim3(threads), smem, s, op, st->scratch[0].as<const uint4>(),
                            st->scratch[1].as<const uint4>(), st->scratch[2].as<const uint4>(),

@@ -278,19 +278,11 @@ __global__ __launch_bounds__(64) void k_pow2_xyzz_from_wrapped(const uint4* P_wr
     // the doubling chain runs in Jacobian coordinates (dbl-2009-l: 1M + 5S, vs 6M + 3S in XYZZ); the
     // per-entry XYZZ conversion (Z^2, Z^3) is off the chain's dependency path.  Quad-cooperative
     // doublings (lanes 0-3, jac_dbl_quad) when the tree code is cooperative.
-#if HALO_TREE_COOP
     if (threadIdx.x >= 4) return;
-#else
-    if (threadIdx.x != 0) return;
-#endif
     Jac<F> j = jac_from_xyzz(xyzz_from_aff(aff_from_wrapped<F>(P_wrapped)));
     for (int i = 0; i < count; i++) {
         if (threadIdx.x == 0) xyzz_store(out_xyzz + 8 * i, jac_to_xyzz(j));
-#if HALO_TREE_COOP
         j = jac_dbl_quad(j);
-#else
-        j = jac_dbl(j);
-#endif
     }
 }
 
@@ -356,11 +348,7 @@ constexpr int TAIL_THREADS = 256;
 // the doubling chain in Jacobian coordinates (dbl-2009-l: 7 multiplications against XYZZ's 9), by a
 // quad of lanes per point (jac_dbl_quad: three product rounds per doubling; TAIL_TABLE_LANES = 4) --
 // the chain is latency-bound and the grid is small (n0 <= 8192 points)
-#if HALO_TREE_COOP
 constexpr int TAIL_TABLE_LANES = 4;
-#else
-constexpr int TAIL_TABLE_LANES = 1;
-#endif
 template <class Cv>
 __global__ __launch_bounds__(64) void k_tail_table(const uint4* gs, int gs_xyzz, size_t n0, uint4* table) {
     using F = typename Cv::Base;
@@ -371,11 +359,7 @@ __global__ __launch_bounds__(64) void k_tail_table(const uint4* gs, int gs_xyzz,
     if (lead) xyzz_store(table + 8 * k, p0);
     Jac<F> j = jac_from_xyzz(p0);
     for (int w = 1; w < TAIL_TBL; w++) {
-#if HALO_TREE_COOP
         for (int b = 0; b < TAIL_DB; b++) j = jac_dbl_quad(j);
-#else
-        for (int b = 0; b < TAIL_DB; b++) j = jac_dbl(j);
-#endif
         if (lead) xyzz_store(table + 8 * ((size_t)w * TAIL_MUL * n0 + k), jac_to_xyzz(j));
     }
 }
@@ -453,12 +437,6 @@ __global__ __launch_bounds__(256) void k_tail_scalars(const uint4* cs, const uin
     if (k < n0) tail_scalar_one<Cv>(cs, w, k, len, m, mode, scal, side);
 }
 
-// One tail round's preparation in one launch: blocks [0, nsb) form the GLV digits of the n0 L/R
-// scalars (as k_tail_scalars, mode 0); block nsb reduces the round's two dot products <c_r, z_l>,
-// <c_l, z_r> (m <= IPA_TAIL_N / 2 elements), scaled by xi_0 in xi mode, to dots_ark -- instead of
-// two dot_device reductions and k_scale_ark (five launches).
-// Lanes 0, 1 also write the GLV split of their dot (k1, k2 words and signs, 10 words per side) to hkw
-// for the hiding terms of k_tail_msm.
 template <class Cv>
 HALO_DEV void glv_split_words(const uint4* x_ark, uint32_t* out10) {
     using S = typename Cv::Scalar;
@@ -484,74 +462,6 @@ struct TailFoldArgs {
     size_t wlen_in;  // fold weights before the fold
     int active;
 };
-
-template <class Cv>
-__global__ __launch_bounds__(256) void k_tail_prep(const uint4* cs, const uint4* zs, const uint4* w, size_t n0, size_t len,
-                                                   size_t m, uint32_t* scal, uint8_t* side, uint32_t nsb,
-                                                   const uint4* xi0_ark, uint4* dots_ark, uint32_t* hkw,
-                                                   const TailFoldArgs f) {
-    using S = typename Cv::Scalar;
-    const int tid = threadIdx.x;
-    if (blockIdx.x < nsb) {
-        const size_t k = (size_t)blockIdx.x * 256 + tid;
-        if (k >= n0) return;
-        if (!f.active) {
-            tail_scalar_one<Cv>(cs, w, k, len, m, 0, scal, side);
-            return;
-        }
-        // c' = c_l + xi^-1 c_r over the unfolded c (length 2 len), w'[u] = w[u / 2] (u odd: xi w[u / 2])
-        const size_t j = k % len, u = k / len;
-        const size_t ci = (j < m) ? m + j : j - m;
-        const Fe<S> c1 = fe_add(fe_from_ark<S>(cs + 2 * ci), fe_mul(fe_from_ark<S>(cs + 2 * (ci + len)), fe_from_ark<S>(f.xinv)));
-        Fe<S> wu = fe_from_ark<S>(w + 2 * (u >> 1));
-        if (u & 1) wu = fe_mul(wu, fe_from_ark<S>(f.xi));
-        tail_scalar_val<Cv>(fe_mul(c1, wu), (j < m) ? 0 : 1, k, scal, side);
-        return;
-    }
-    __shared__ uint4 red[2][256 * 2];
-    Fe<S> a = fe_zero<S>(), b = fe_zero<S>();
-    if (f.active) {
-        const Fe<S> xi = fe_from_ark<S>(f.xi), xinv = fe_from_ark<S>(f.xinv);
-        for (size_t i = tid; i < m; i += 256) {
-            const Fe<S> cl = fe_add(fe_from_ark<S>(cs + 2 * i), fe_mul(fe_from_ark<S>(cs + 2 * (i + len)), xinv));
-            const Fe<S> cr = fe_add(fe_from_ark<S>(cs + 2 * (m + i)), fe_mul(fe_from_ark<S>(cs + 2 * (m + i + len)), xinv));
-            const Fe<S> zl = fe_add(fe_from_ark<S>(zs + 2 * i), fe_mul(fe_from_ark<S>(zs + 2 * (i + len)), xi));
-            const Fe<S> zr = fe_add(fe_from_ark<S>(zs + 2 * (m + i)), fe_mul(fe_from_ark<S>(zs + 2 * (m + i + len)), xi));
-            fe_to_ark(f.cs_out + 2 * i, cl);
-            fe_to_ark(f.cs_out + 2 * (m + i), cr);
-            fe_to_ark(f.zs_out + 2 * i, zl);
-            fe_to_ark(f.zs_out + 2 * (m + i), zr);
-            a = fe_add(a, fe_mul(cr, zl));
-            b = fe_add(b, fe_mul(cl, zr));
-        }
-        for (size_t u = tid; u < f.wlen_in; u += 256) {
-            const Fe<S> wv = fe_from_ark<S>(w + 2 * u);
-            fe_to_ark(f.w_out + 2 * (2 * u), wv);
-            fe_to_ark(f.w_out + 2 * (2 * u + 1), fe_mul(wv, xi));
-        }
-    } else {
-        for (size_t i = tid; i < m; i += 256) {
-            a = fe_add(a, fe_mul(fe_from_ark<S>(cs + 2 * (m + i)), fe_from_ark<S>(zs + 2 * i)));
-            b = fe_add(b, fe_mul(fe_from_ark<S>(cs + 2 * i), fe_from_ark<S>(zs + 2 * (m + i))));
-        }
-    }
-    fe_store(red[0] + 2 * tid, a);
-    fe_store(red[1] + 2 * tid, b);
-    __syncthreads();
-    for (int off = 128; off > 0; off >>= 1) {
-        if (tid < off) {
-            fe_store(red[0] + 2 * tid, fe_add(fe_load<S>(red[0] + 2 * tid), fe_load<S>(red[0] + 2 * (tid + off))));
-            fe_store(red[1] + 2 * tid, fe_add(fe_load<S>(red[1] + 2 * tid), fe_load<S>(red[1] + 2 * (tid + off))));
-        }
-        __syncthreads();
-    }
-    if (tid < 2) {
-        Fe<S> d = fe_load<S>(red[tid]);
-        if (xi0_ark) d = fe_mul(d, fe_from_ark<S>(xi0_ark));
-        fe_to_ark(dots_ark + 2 * tid, d);
-        glv_split_words<Cv>(dots_ark + 2 * tid, hkw + 10 * tid);
-    }
-}
 
 // The hiding term dot * P' of one side as lane terms: lane t < 256 returns the table entry for bit t
 // of the GLV split dot = k1 + lambda k2 (lanes 0-127: k1 with 2^t P', 128-255: k2 with phi(2^(t-128) P'))
@@ -634,6 +544,204 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail_msm(const uint4* table, s
         xyzz_store(part + 8 * (2 * (size_t)blockIdx.x + sd), acc);
         xyzz_store(part + 8 * (2 * (size_t)blockIdx.x + (sd ^ 1)), xyzz_id<F>());
     }
+}
+
+// One tail round (L and R with their hiding terms) in ONE launch (round 4; was k_tail_prep + k_tail_msm +
+// k_tail_final).  Blocks [0, 2 nbs) own 4 points each (one per wave), all on one side: side sd's point
+// q = (block - sd nbs) 4 + wave (q < n0 / 2) is k = j + u 2m + sd m with u = q / m, j = q % m, and its
+// 64 lanes are its 64 window terms (32 4-bit GLV windows x (k1, k2)).  Every lane of the wave forms the
+// point's scalar c[ci] w[u] and its GLV split itself (wave-uniform work: the SIMD issues it once), so
+// no preparation launch is needed; with a deferred fold the unfolded c / w are folded on the fly as
+// k_tail_prep did.  Block 2 nbs forms the two dot products (and, with a deferred fold, writes the
+// folded c, z, w), scales them by xi_0 in xi mode, and adds each side's hiding term dot_sd * H' as one
+// more partial.  Each block publishes its partial (relaxed agent-scope stores drained, then an
+// agent-scope release add on its side's counter -- two counters, the dots block counts on both); the
+// last block to arrive on a side takes an agent acquire, sums the side's nbs + 1 partials and writes
+// the side's XYZZ sum to out_xyzz + 8 sd, then resets the counter.  No block waits for another.
+struct TailRoundArgs {
+    const uint4* table;
+    size_t ld, n0, m;
+    const uint4 *cs, *zs, *w;
+    uint32_t nbs;              // point blocks per side
+    const uint4* xi0_ark;      // xi mode: dots scaled by xi_0
+    const uint4* htab;         // 2^i H' (or 2^i H in xi mode), i < 128
+    uint4* dots_ark;           // [2] out
+    uint4* part;               // [2][nbs + 1] XYZZ partials
+    uint32_t* ctr;             // [2] arrival counters (zero between launches)
+    uint4* out_xyzz;           // [2] L, R
+};
+
+HALO_DEV uint32_t tail_word(const uint32_t (&k)[5], uint32_t i) {  // k[i], i < 4, without dynamic indexing
+    uint32_t r = k[0];
+    r = i == 1 ? k[1] : r;
+    r = i == 2 ? k[2] : r;
+    return i == 3 ? k[3] : r;
+}
+
+template <class F>
+HALO_DEV void tail_publish(uint4* dst, const XYZZ<F>& v) {  // relaxed agent-scope stores (sc1), one lane
+    uint32_t w[32];
+    uint32_t x[8];
+    fe_pack(v.X, x);
+#pragma unroll
+    for (int i = 0; i < 8; i++) w[i] = x[i];
+    fe_pack(v.Y, x);
+#pragma unroll
+    for (int i = 0; i < 8; i++) w[8 + i] = x[i];
+    fe_pack(v.ZZ, x);
+#pragma unroll
+    for (int i = 0; i < 8; i++) w[16 + i] = x[i];
+    fe_pack(v.ZZZ, x);
+#pragma unroll
+    for (int i = 0; i < 8; i++) w[24 + i] = x[i];
+    uint32_t* d = (uint32_t*)dst;
+#pragma unroll
+    for (int i = 0; i < 32; i++) __hip_atomic_store(d + i, w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// true in the block whose release add on *c returned total - 1 (then acquired); block-uniform
+HALO_DEV bool tail_arrive(uint32_t* c, uint32_t total, uint32_t* flag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t got = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        *flag = got == total - 1;
+        if (*flag) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    __syncthreads();
+    return *flag != 0;
+}
+
+template <class Cv>
+HALO_DEV void tail_side_final(const TailRoundArgs& a, uint32_t sd, uint4* red) {
+    using F = typename Cv::Base;
+    const uint32_t np = a.nbs + 1;
+    XYZZ<F> acc = xyzz_id<F>();
+    for (uint32_t j = threadIdx.x; j < np; j += TAIL_THREADS) acc = xyzz_add(acc, xyzz_load<F>(a.part + 8 * ((size_t)sd * np + j)));
+    acc = block_group_sum<F>(acc, TAIL_THREADS, red);
+    if (threadIdx.x == 0) {
+        xyzz_store(a.out_xyzz + 8 * sd, acc);
+        __hip_atomic_store(a.ctr + sd, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+template <class Cv>
+__global__ __launch_bounds__(TAIL_THREADS) void k_tail_round(const TailRoundArgs a, const TailFoldArgs f) {
+    using F = typename Cv::Base;
+    using S = typename Cv::Scalar;
+    __shared__ uint4 red[TAIL_THREADS / 2 * 8];
+    __shared__ uint32_t flag;
+    const int tid = threadIdx.x;
+    const size_t m = a.m, len = 2 * m, hn = a.n0 / 2;
+    if (blockIdx.x < 2 * a.nbs) {
+        const uint32_t sd = blockIdx.x >= a.nbs;
+        const size_t q = (size_t)(blockIdx.x - sd * a.nbs) * (TAIL_THREADS / 64) + (tid >> 6);
+        XYZZ<F> acc = xyzz_id<F>();
+        if (q < hn) {  // (wave-uniform)
+            const size_t u = q / m, j = q % m, k = j + u * len + sd * m;
+            const size_t ci = sd ? j : m + j;
+            Fe<S> c, wu;
+            if (f.active) {  // c' = c_l + xi^-1 c_r over the unfolded c; w'[u] = w[u / 2] (xi w[u / 2] for odd u)
+                c = fe_add(fe_from_ark<S>(a.cs + 2 * ci), fe_mul(fe_from_ark<S>(a.cs + 2 * (ci + len)), fe_from_ark<S>(f.xinv)));
+                wu = fe_from_ark<S>(a.w + 2 * (u >> 1));
+                if (u & 1) wu = fe_mul(wu, fe_from_ark<S>(f.xi));
+            } else {
+                c = fe_from_ark<S>(a.cs + 2 * ci);
+                wu = fe_from_ark<S>(a.w + 2 * u);
+            }
+            Fe<S> one_raw = fe_zero<S>();  // internal (x 2^261) -> canonical: Montgomery product with 1
+            one_raw.v[0] = 1;
+            uint32_t w8[8], k1[5], k2[5];
+            bool n1, n2;
+            fe_pack(fe_canon(fe_mul(fe_mul(c, wu), one_raw)), w8);
+            glv::decompose<typename Cv::K>(w8, n1, k1, n2, k2);
+            constexpr uint32_t DPW = 32 / TAIL_DB;  // digits per scalar word
+            const uint32_t win = tid & 63, half = win / TAIL_TBL, bw = win % TAIL_TBL;
+            const uint32_t word = half ? tail_word(k2, bw / DPW) : tail_word(k1, bw / DPW);
+            const uint32_t d = (word >> (TAIL_DB * (bw % DPW))) & (uint32_t)TAIL_MUL;
+            if (d) {
+                XYZZ<F> t = xyzz_load<F>(a.table + tail_entry(bw, d, a.ld, k));
+                if (half) t.X = fe_mul(t.X, fe_from_const<F>(Cv::K::BETA));  // phi
+                if (half ? n2 : n1) t = xyzz_neg(t);
+                acc = t;
+            }
+        }
+        acc = block_group_sum<F>(acc, TAIL_THREADS, red);
+        if (tid == 0) tail_publish(a.part + 8 * ((size_t)sd * (a.nbs + 1) + (blockIdx.x - sd * a.nbs)), acc);
+        if (tail_arrive(a.ctr + sd, a.nbs + 1, &flag)) tail_side_final<Cv>(a, sd, red);
+        return;
+    }
+    // ---- the dots block (k_tail_prep's last block) and the two hiding terms
+    __shared__ uint4 dred[2][256 * 2];
+    __shared__ uint32_t kw[2][10];
+    Fe<S> da = fe_zero<S>(), db = fe_zero<S>();
+    if (f.active) {
+        const Fe<S> xi = fe_from_ark<S>(f.xi), xinv = fe_from_ark<S>(f.xinv);
+        for (size_t i = tid; i < m; i += 256) {
+            const Fe<S> cl = fe_add(fe_from_ark<S>(a.cs + 2 * i), fe_mul(fe_from_ark<S>(a.cs + 2 * (i + len)), xinv));
+            const Fe<S> cr = fe_add(fe_from_ark<S>(a.cs + 2 * (m + i)), fe_mul(fe_from_ark<S>(a.cs + 2 * (m + i + len)), xinv));
+            const Fe<S> zl = fe_add(fe_from_ark<S>(a.zs + 2 * i), fe_mul(fe_from_ark<S>(a.zs + 2 * (i + len)), xi));
+            const Fe<S> zr = fe_add(fe_from_ark<S>(a.zs + 2 * (m + i)), fe_mul(fe_from_ark<S>(a.zs + 2 * (m + i + len)), xi));
+            fe_to_ark(f.cs_out + 2 * i, cl);
+            fe_to_ark(f.cs_out + 2 * (m + i), cr);
+            fe_to_ark(f.zs_out + 2 * i, zl);
+            fe_to_ark(f.zs_out + 2 * (m + i), zr);
+            da = fe_add(da, fe_mul(cr, zl));
+            db = fe_add(db, fe_mul(cl, zr));
+        }
+        for (size_t u = tid; u < f.wlen_in; u += 256) {
+            const Fe<S> wv = fe_from_ark<S>(a.w + 2 * u);
+            fe_to_ark(f.w_out + 2 * (2 * u), wv);
+            fe_to_ark(f.w_out + 2 * (2 * u + 1), fe_mul(wv, xi));
+        }
+    } else {
+        for (size_t i = tid; i < m; i += 256) {
+            da = fe_add(da, fe_mul(fe_from_ark<S>(a.cs + 2 * (m + i)), fe_from_ark<S>(a.zs + 2 * i)));
+            db = fe_add(db, fe_mul(fe_from_ark<S>(a.cs + 2 * i), fe_from_ark<S>(a.zs + 2 * (m + i))));
+        }
+    }
+    fe_store(dred[0] + 2 * tid, da);
+    fe_store(dred[1] + 2 * tid, db);
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+        if (tid < off) {
+            fe_store(dred[0] + 2 * tid, fe_add(fe_load<S>(dred[0] + 2 * tid), fe_load<S>(dred[0] + 2 * (tid + off))));
+            fe_store(dred[1] + 2 * tid, fe_add(fe_load<S>(dred[1] + 2 * tid), fe_load<S>(dred[1] + 2 * (tid + off))));
+        }
+        __syncthreads();
+    }
+    if (tid < 2) {
+        Fe<S> d = fe_load<S>(dred[tid]);
+        if (a.xi0_ark) d = fe_mul(d, fe_from_ark<S>(a.xi0_ark));
+        fe_to_ark(a.dots_ark + 2 * tid, d);
+        uint32_t w8[8], k1[5], k2[5];
+        bool n1, n2;
+        Fe<S> one_raw = fe_zero<S>();
+        one_raw.v[0] = 1;
+        fe_pack(fe_canon(fe_mul(d, one_raw)), w8);
+        glv::decompose<typename Cv::K>(w8, n1, k1, n2, k2);
+        for (int i = 0; i < 4; i++) {
+            kw[tid][i] = k1[i];
+            kw[tid][4 + i] = k2[i];
+        }
+        kw[tid][8] = n1;
+        kw[tid][9] = n2;
+    }
+    __syncthreads();
+    for (uint32_t sd = 0; sd < 2; sd++) {  // dot_sd H': lane t < 128 bit t of k1 with 2^t H', t >= 128 k2 with phi
+        XYZZ<F> acc = xyzz_id<F>();
+        if ((kw[sd][tid >> 5] >> (tid & 31)) & 1u) {
+            Affine<F> p = aff_load<F>(a.htab + 4 * (tid & 127));
+            if (tid >= 128) p.x = fe_mul(p.x, fe_from_const<F>(Cv::K::BETA));
+            if (kw[sd][8 + (tid >> 7)]) p.y = fe_neg(p.y);
+            acc = xyzz_from_aff(p);
+        }
+        acc = block_group_sum<F>(acc, TAIL_THREADS, red);
+        if (tid == 0) tail_publish(a.part + 8 * ((size_t)sd * (a.nbs + 1) + a.nbs), acc);
+        __syncthreads();
+    }
+    for (uint32_t sd = 0; sd < 2; sd++)
+        if (tail_arrive(a.ctr + sd, a.nbs + 1, &flag)) tail_side_final<Cv>(a, sd, red);
 }
 
 // block b (0: L, 1: R): sum of the partials + dot_b * H' (from the 2^i H' table), -> WrappedPoint
@@ -1131,7 +1239,7 @@ static int ipa_h_table(DeviceState* st, int curve, const halo_wrapped_point_t* H
 constexpr size_t SM_BYTES = 2048;
 constexpr size_t SM_WBAR = 1024, SM_ALPHA = 1056, SM_W = 1088, SM_WP = 1120, SM_C = 1152, SM_CBAR = 1216, SM_S = 1280,
                  SM_CP = 1344, SM_NEGW = 1408, SM_T = 1536, SM_EVAL = 1664, SM_V = 1696,  // SM_T: 128 B XYZZ
-                 SM_HKW = 1728;  // 2 x 10 words: the round's dots split by GLV (k_tail_prep)
+                 SM_CTR = 1856;  // 2 x u32 arrival counters of k_tail_round (zero between launches)
 
 // Phase 1 of a session: G (resident SRS prefix, or explicit gs_host), c (cs_len coefficients, host or
 // device (ordered on the null stream), zero-padded to n), z = powers of z (or explicit zs_host) on the
@@ -1171,6 +1279,7 @@ static int ipa_setup(DeviceState* st, halo_ipa_session* ses, int curve, size_t n
     HALO_CHECK(ses->cs.reserve(n * 32));
     HALO_CHECK(ses->zs.reserve(n * 32));
     HALO_CHECK(ses->small.reserve(SM_BYTES));
+    HALO_HIP(hipMemsetAsync(ses->small.as<char>() + SM_CTR, 0, 8, s));  // k_tail_round's counters
     HALO_CHECK(ses->tmp.reserve(std::max<size_t>(4096 * 32, gs_host ? n * 64 : 0)));
     if (gs_host) {
         HALO_CHECK(copy_h2d(ses->tmp.ptr, gs_host, n * 64, s));
@@ -1533,51 +1642,62 @@ static int ipa_enter_tail(DeviceState* st, halo_ipa_session* ses, hipStream_t s)
 // mode 1: U = sum_u w[u] G0[u] -> small[256..384) as XYZZ (converted on the host).
 static int ipa_tail_sums(halo_ipa_session* ses, int mode, hipStream_t s) {
     const size_t n0 = ses->n0, m = ses->m;
-    const size_t nbs = (TAIL_WIN * (n0 / 2) + TAIL_THREADS - 1) / TAIL_THREADS;  // mode 0: blocks per side
-    const size_t nblk = mode == 0 ? 2 * nbs : (TAIL_WIN * n0 + TAIL_THREADS - 1) / TAIL_THREADS;
     char* sm = (char*)ses->small.ptr;
-    DISPATCH_CURVE(ses->curve, Cv, {
-        if (mode == 0) {
-            const uint32_t nsb = gridn(n0, 256);
-            TailFoldArgs f{};
-            f.active = ses->fold_pending;
-            if (f.active) {  // the previous round's fold, applied here (halo_ipa_fold deferred it)
-                memcpy(&f.xi, &ses->pend_xi, 32);
-                memcpy(&f.xinv, &ses->pend_xinv, 32);
-                f.cs_out = ses->cs2.as<uint4>();
-                f.zs_out = ses->zs2.as<uint4>();
-                f.w_out = ses->w[ses->wcur ^ 1].as<uint4>();
-                f.wlen_in = ses->wlen;
-            }
-            hipLaunchKernelGGL(k_tail_prep<Cv>, dim3(nsb + 1), dim3(256), 0, s, ses->cs.as<const uint4>(),
-                               ses->zs.as<const uint4>(), ses->w[ses->wcur].as<const uint4>(), n0, 2 * m, m,
-                               ses->scal.as<uint32_t>(), ses->side.as<uint8_t>(), nsb,
-                               ses->xi_mode ? (const uint4*)(sm + 192) : (const uint4*)nullptr, (uint4*)(sm + 128),
-                               (uint32_t*)(sm + SM_HKW), f);
-            if (f.active) {
-                std::swap(ses->cs.ptr, ses->cs2.ptr);
-                std::swap(ses->cs.bytes, ses->cs2.bytes);
-                std::swap(ses->zs.ptr, ses->zs2.ptr);
-                std::swap(ses->zs.bytes, ses->zs2.bytes);
-                ses->wcur ^= 1;
-                ses->wlen *= 2;
-                ses->fold_pending = false;
-            }
-        } else {
-            hipLaunchKernelGGL(k_tail_scalars<Cv>, dim3(gridn(n0, 256)), dim3(256), 0, s, ses->cs.as<const uint4>(),
-                               ses->w[ses->wcur].as<const uint4>(), n0, 2 * m, m, mode, ses->scal.as<uint32_t>(),
-                               ses->side.as<uint8_t>());
+    if (mode == 0) {  // one fused launch (k_tail_round)
+        TailFoldArgs f{};
+        f.active = ses->fold_pending;
+        if (f.active) {  // the previous round's fold, applied here (halo_ipa_fold deferred it)
+            memcpy(&f.xi, &ses->pend_xi, 32);
+            memcpy(&f.xinv, &ses->pend_xinv, 32);
+            f.cs_out = ses->cs2.as<uint4>();
+            f.zs_out = ses->zs2.as<uint4>();
+            f.w_out = ses->w[ses->wcur ^ 1].as<uint4>();
+            f.wlen_in = ses->wlen;
         }
-        const uint32_t side_blocks = (uint32_t)(mode == 0 ? nbs : nblk);
-        uint4* out = (uint4*)(sm + (mode == 0 ? 512 : 256));
+        TailRoundArgs ra{};
+        ra.table = ses->table;
+        ra.ld = ses->table_ld;
+        ra.n0 = n0;
+        ra.m = m;
+        ra.cs = ses->cs.as<const uint4>();
+        ra.zs = ses->zs.as<const uint4>();
+        ra.w = ses->w[ses->wcur].as<const uint4>();
+        ra.nbs = (uint32_t)((n0 / 2 + TAIL_THREADS / 64 - 1) / (TAIL_THREADS / 64));
+        ra.xi0_ark = ses->xi_mode ? (const uint4*)(sm + 192) : nullptr;
+        ra.htab = (const uint4*)ses->htab_ptr;
+        ra.dots_ark = (uint4*)(sm + 128);
+        ra.part = ses->part.as<uint4>();
+        ra.ctr = (uint32_t*)(sm + SM_CTR);
+        ra.out_xyzz = (uint4*)(sm + 512);
+        DISPATCH_CURVE(ses->curve, Cv, {
+            hipLaunchKernelGGL(k_tail_round<Cv>, dim3(2 * ra.nbs + 1), dim3(TAIL_THREADS), 0, s, ra, f);
+        });
+        HALO_HIP(hipGetLastError());
+        if (f.active) {
+            std::swap(ses->cs.ptr, ses->cs2.ptr);
+            std::swap(ses->cs.bytes, ses->cs2.bytes);
+            std::swap(ses->zs.ptr, ses->zs2.ptr);
+            std::swap(ses->zs.bytes, ses->zs2.bytes);
+            ses->wcur ^= 1;
+            ses->wlen *= 2;
+            ses->fold_pending = false;
+        }
+        return HALO_OK;
+    }
+    // mode 1: U = sum_u w[u] G0[u]
+    const size_t nblk = (TAIL_WIN * n0 + TAIL_THREADS - 1) / TAIL_THREADS;
+    uint4* out = (uint4*)(sm + 256);
+    DISPATCH_CURVE(ses->curve, Cv, {
+        hipLaunchKernelGGL(k_tail_scalars<Cv>, dim3(gridn(n0, 256)), dim3(256), 0, s, ses->cs.as<const uint4>(),
+                           ses->w[ses->wcur].as<const uint4>(), n0, 2 * m, m, 1, ses->scal.as<uint32_t>(),
+                           ses->side.as<uint8_t>());
         hipLaunchKernelGGL(k_tail_msm<Cv>, dim3((unsigned)nblk), dim3(TAIL_THREADS), 0, s, ses->table, ses->table_ld,
-                           ses->scal.as<const uint32_t>(), ses->side.as<const uint8_t>(), n0, m, mode, side_blocks,
-                           ses->part.as<uint4>(), mode == 0 ? (const uint4*)ses->htab_ptr : (const uint4*)nullptr,
-                           (const uint4*)(sm + 128), (const uint32_t*)(sm + SM_HKW), out);
-        if (side_blocks > 1)
-            hipLaunchKernelGGL(k_tail_final<Cv>, dim3(mode == 0 ? 2 : 1), dim3(TAIL_THREADS), 0, s,
-                               ses->part.as<const uint4>(), (int)nblk, (const uint4*)nullptr, (const uint4*)nullptr,
-                               out, 1);
+                           ses->scal.as<const uint32_t>(), ses->side.as<const uint8_t>(), n0, m, 1, (uint32_t)nblk,
+                           ses->part.as<uint4>(), (const uint4*)nullptr, (const uint4*)nullptr, (const uint32_t*)nullptr,
+                           out);
+        if (nblk > 1)
+            hipLaunchKernelGGL(k_tail_final<Cv>, dim3(1), dim3(TAIL_THREADS), 0, s, ses->part.as<const uint4>(), (int)nblk,
+                               (const uint4*)nullptr, (const uint4*)nullptr, out, 1);
     });
     HALO_HIP(hipGetLastError());
     return HALO_OK;

@@ -2,11 +2,10 @@
 // sum_i (i + 1) B_i per window and the Horner over the windows (k_final; since the quad-cooperative
 // doublings it is latency-bound like the rest, so it takes this unit's per-column multiplication).
 //
-// Every kernel here is latency-bound (a few waves doing dependent chains of curve additions).  Round 2
-// compiled this translation unit with HALO_MAD_ILP (the compiler's split column sums: 418 vs 523 ns
-// per dependent modmul on one wave against one asm statement per product); since round 3 the default
-// build uses the per-column asm chains here as well (HALO_TAIL_COL: 382 ns, tools/micro/fe_mul_bench.hip),
-// and HALO_MAD_ILP remains an A/B build option (arithmetic in the inline namespace halo::ilp then).
+// Every kernel here is latency-bound (a few waves doing dependent chains of curve additions).  They use
+// the same per-column asm multiplication as the throughput kernels (round 3 measured it against the
+// compiler's split column sums: 382 vs 418 ns per dependent modmul on one wave,
+// tools/micro/fe_mul_bench.hip; the split form was removed in round 4).
 #include <algorithm>
 #include <cstdlib>
 
@@ -15,10 +14,6 @@
 #include "runtime.hpp"
 #include "sort.hpp"
 #include "tree.hpp"
-
-#if !defined(HALO_MAD_ILP) && !defined(HALO_TAIL_COL)
-#error "msm_tail.hip must be compiled with -DHALO_MAD_ILP or -DHALO_TAIL_COL (see Makefile)"
-#endif
 
 
 namespace halo {
@@ -184,7 +179,6 @@ __global__ __launch_bounds__(64) void k_bitcombine(const uint4* terms, uint32_t 
     const uint32_t w = blockIdx.x, k = threadIdx.x;
     XYZZ<F> v = xyzz_id<F>();
     const uint32_t D = logH + logL;  // doubling classes d = 0 .. D - 1, one U or V term each (+ T_0 at d = 0)
-#if HALO_TREE_COOP
     if (D <= 16) {
         // quad j (lanes 4j .. 4j + 3) doubles the term of class j j times with quad-cooperative doublings
         // (three product rounds per doubling instead of nine on one lane); then lanes 0 .. D - 1 take the
@@ -205,7 +199,6 @@ __global__ __launch_bounds__(64) void k_bitcombine(const uint4* terms, uint32_t 
         while (G < D + 1) G <<= 1;
         v = wave_group_sum<F>(v, G);
     } else
-#endif
     {
         if (k < NT) {
             v = xyzz_load<F>(terms + 8 * ((size_t)w * NT + k));
@@ -273,7 +266,6 @@ __global__ __launch_bounds__(64) void k_final(const uint4* window_sums, int W, i
                                               uint4* out_wrapped, int xyzz_out) {
     using F = typename Cv::Base;
     XYZZ<F> horner = xyzz_id<F>();
-#if HALO_TREE_COOP
     // every quad of the wave runs the same Horner chain (identical data, so every branch is uniform):
     // quad-cooperative doublings (3 product rounds instead of 7) and additions (4 instead of 14)
     const uint32_t s1 = threadIdx.x & 60u;
@@ -293,17 +285,6 @@ __global__ __launch_bounds__(64) void k_final(const uint4* window_sums, int W, i
         }
     }
     if (threadIdx.x != 0) return;
-#else
-    if (threadIdx.x != 0) return;
-    for (int w = W - 1; w >= 0; w--) {
-        if (w != W - 1 && !xyzz_is_id(horner)) {
-            Jac<F> j = jac_from_xyzz(horner);
-            for (int k = 0; k < c; k++) j = jac_dbl(j);
-            horner = jac_to_xyzz(j);
-        }
-        horner = xyzz_add(horner, xyzz_load<F>(window_sums + 8 * w));
-    }
-#endif
     if (hide_xyzz) horner = xyzz_add(horner, xyzz_load<F>(hide_xyzz));
     if (xyzz_out)  // 128 B packed XYZZ: the host converts (halo_ipa_round_lr, no inversion on the lane)
         xyzz_store(out_wrapped, horner);

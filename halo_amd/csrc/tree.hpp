@@ -23,11 +23,7 @@ HALO_DEV XYZZ<F> xyzz_shfl_xor(const XYZZ<F>& p, int m) {
     }
     return r;
 }
-#ifndef HALO_TREE_COOP
-#define HALO_TREE_COOP 1  // 0: one addition per lane per level (A/B knob)
-#endif
 
-#if HALO_TREE_COOP
 // ---------------------------------------------------------------------------------------------
 // Quad-cooperative additions.  A tree level inside one wave is issue-bound, not latency-bound: the
 // wave's SIMD spends the same cycles on an addition whether 32 lanes or 1 lane need it, and a level
@@ -40,21 +36,11 @@ HALO_DEV XYZZ<F> xyzz_shfl_xor(const XYZZ<F>& p, int m) {
 // identity, wave-uniformly skipped when no lane hits it.
 // ---------------------------------------------------------------------------------------------
 // v_mov_b32 with a DPP quad permutation: lane i of each quad reads lane (CTRL >> 2 i) & 3
-#ifndef HALO_QPERM_DPP
-#define HALO_QPERM_DPP 1
-#endif
 template <int CTRL, class F>
 HALO_DEV Fe<F> qperm(const Fe<F>& a) {
     Fe<F> r;
-#if HALO_QPERM_DPP
 #pragma unroll
     for (int l = 0; l < NLIMB; l++) r.v[l] = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.v[l], CTRL, 0xF, 0xF, false);
-#else
-    const uint32_t q = threadIdx.x & 3u;
-    const int src = (int)((threadIdx.x & 60u) | ((uint32_t)(CTRL >> (2 * q)) & 3u));
-#pragma unroll
-    for (int l = 0; l < NLIMB; l++) r.v[l] = __shfl(a.v[l], src);
-#endif
     return r;
 }
 constexpr int qp(int l0, int l1, int l2, int l3) { return l0 | (l1 << 2) | (l2 << 4) | (l3 << 6); }
@@ -129,7 +115,7 @@ template <class F>
 HALO_DEV XYZZ<F> xyzz_dbl_quad(const XYZZ<F>& p) {
     const uint32_t role = threadIdx.x & 3u;
     const uint32_t odd = (role & 1u) ? ~0u : 0u, lo = role < 2 ? ~0u : 0u, r0 = role == 0 ? ~0u : 0u;
-    const Fe<F> U = fe_add_nc(p.Y, p.Y);
+    const Fe<F> U = fe_norm(fe_add_nc(p.Y, p.Y));  // normalized: squared below (fields.hpp bounds)
     const Fe<F> t1 = fe_sqr(pick(odd, p.X, U));  // lanes 0, 2: V = U^2; 1, 3: X^2
     const Fe<F> V = qperm<qp(0, 0, 0, 0)>(t1), X2 = qperm<qp(1, 1, 1, 1)>(t1);
     const Fe<F> M = fe_norm(fe_add_nc(X2, fe_add_nc(X2, X2)));  // < 6p
@@ -230,32 +216,5 @@ HALO_DEV XYZZ<F> block_group_sum(XYZZ<F> v, uint32_t G, uint4* red) {
     if (gpos == 0) v = xyzz_load<F>(red + 8 * (threadIdx.x / G));
     return v;
 }
-#else
-// every lane gets the sum over its aligned group of G lanes (G a power of two <= 64)
-template <class F>
-HALO_DEV XYZZ<F> wave_group_sum(XYZZ<F> v, uint32_t G) {
-    for (uint32_t m = G >> 1; m > 0; m >>= 1) v = xyzz_add(v, xyzz_shfl_xor(v, (int)m));
-    return v;
-}
-// sum over aligned groups of G threads (G a power of two <= blockDim): valid in the group's first
-// thread.  While a group spans several waves its upper half hands its points to the lower half
-// through LDS (the number of waves that add halves each level, as in an LDS tree), then the last
-// wave of each group finishes with lane shuffles (no barriers).  red: LDS scratch for blockDim / 2
-// points.  Every thread of the block must call it.
-template <class F>
-HALO_DEV XYZZ<F> block_group_sum(XYZZ<F> v, uint32_t G, uint4* red) {
-    const uint32_t gpos = threadIdx.x & (G - 1), gbase = threadIdx.x - gpos;
-    for (uint32_t span = G; span > 64; span >>= 1) {  // active: gpos < span (wave-uniform tests)
-        const uint32_t half = span >> 1;
-        if (gpos >= half && gpos < span) xyzz_store(red + 8 * ((gbase >> 1) + gpos - half), v);
-        __syncthreads();
-        if (gpos < half) v = xyzz_add(v, xyzz_load<F>(red + 8 * ((gbase >> 1) + gpos)));
-        __syncthreads();
-    }
-    if (gpos < 64) v = wave_group_sum<F>(v, G < 64 ? G : 64u);
-    return v;
-}
-
-#endif
 
 HALO_ARITH_END

@@ -1,7 +1,7 @@
 """A/B of batched commitments (halo_msm_batch_dev, fronts beside the previous accumulation) against
 back-to-back halo_msm_dev_async calls, 2^logn points per MSM over the resident window-shifted
 synthetic SRS.  Prints ms per MSM for each and whether every result agrees.
-usage: python tools/msm_batch_time.py [logn] [k] [reps]   (env: HALO_BATCH_OVERLAP, HALO_ACC_LDS)"""
+usage: python tools/msm_batch_time.py [logn] [k] [reps]"""
 import ctypes
 import os
 import sys
@@ -59,4 +59,4 @@ ta = timeit(run_async)
 tb = timeit(run_batch)
 same = bool(torch.equal(out_a, out_b))
 print(f"logn {logn} k {k}: async {ta:.3f} ms/MSM, batch {tb:.3f} ms/MSM, same={same}, "
-      f"overlap={os.environ.get('HALO_BATCH_OVERLAP', '1')} acc_lds={os.environ.get('HALO_ACC_LDS', '41984')}")
+      "")
