@@ -59,6 +59,8 @@ def parse():
                     help="log2 n of the pcdl_commit / pcdl_open sweeps with w = Some (extra.pcdl; '' = off)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal only: every rank on cuda:0 over gloo (multi-rank runs on a one-GPU box)")
+    ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
+                    help="halo_set_tuning before the run (A/B of path selections; results are identical)")
     return ap.parse_args()
 
 
@@ -83,6 +85,9 @@ def main():
     H.ensure_device(local)
     torch.cuda.set_device(local)
     L = H.load()
+    for kv in args.tune:
+        k, v = kv.split("=")
+        H.set_tuning(k, int(v))
     if world > 1:
         if args.same_device:  # RCCL refuses two ranks on one GPU: rehearse the protocol over gloo
             dist.init_process_group("gloo")

@@ -552,12 +552,13 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail_msm(const uint4* table, s
 // 64 lanes are its 64 window terms (32 4-bit GLV windows x (k1, k2)).  Every lane of the wave forms the
 // point's scalar c[ci] w[u] and its GLV split itself (wave-uniform work: the SIMD issues it once), so
 // no preparation launch is needed; with a deferred fold the unfolded c / w are folded on the fly as
-// k_tail_prep did.  Block 2 nbs forms the two dot products (and, with a deferred fold, writes the
-// folded c, z, w), scales them by xi_0 in xi mode, and adds each side's hiding term dot_sd * H' as one
-// more partial.  Each block publishes its partial (relaxed agent-scope stores drained, then an
-// agent-scope release add on its side's counter -- two counters, the dots block counts on both); the
-// last block to arrive on a side takes an agent acquire, sums the side's nbs + 1 partials and writes
-// the side's XYZZ sum to out_xyzz + 8 sd, then resets the counter.  No block waits for another.
+// k_tail_prep did.  Blocks 2 nbs + sd form side sd's dot product (with a deferred fold they also write
+// their halves of the folded c, z, w), scale it by xi_0 in xi mode, and add the side's hiding term
+// dot_sd * H' as one more partial -- one block per side, in parallel with the point blocks.  Each block
+// publishes its partial (relaxed agent-scope stores drained, then an agent-scope release add on its
+// side's counter); the last block to arrive on a side takes an agent acquire, sums the side's nbs + 1
+// partials and writes the side's XYZZ sum to out_xyzz + 8 sd, then resets the counter.  No block waits
+// for another.
 struct TailRoundArgs {
     const uint4* table;
     size_t ld, n0, m;
@@ -571,6 +572,12 @@ struct TailRoundArgs {
     uint4* out_xyzz;           // [2] L, R
 };
 
+// n0 up to this: one launch per round (k_tail_round, scalars formed in the points' waves); above it the
+// three-launch round (k_tail_digits, k_tail_msm, k_tail_final) is faster (measured per 2^10 / 2^12 round:
+// 0.118 / 0.195 vs 0.125-0.131 / 0.206 ms fused; 2^4 / 2^6 / 2^8: 0.103 / 0.110 / 0.114 vs 0.092-0.094 /
+// 0.094-0.097 / 0.097-0.109 ms for the fused one)
+constexpr size_t TAIL_FUSE_N = 256;
+
 HALO_DEV uint32_t tail_word(const uint32_t (&k)[5], uint32_t i) {  // k[i], i < 4, without dynamic indexing
     uint32_t r = k[0];
     r = i == 1 ? k[1] : r;
@@ -579,24 +586,19 @@ HALO_DEV uint32_t tail_word(const uint32_t (&k)[5], uint32_t i) {  // k[i], i < 
 }
 
 template <class F>
-HALO_DEV void tail_publish(uint4* dst, const XYZZ<F>& v) {  // relaxed agent-scope stores (sc1), one lane
-    uint32_t w[32];
+HALO_DEV void tail_publish_fe(uint32_t* d, const Fe<F>& v) {
     uint32_t x[8];
-    fe_pack(v.X, x);
+    fe_pack(v, x);
 #pragma unroll
-    for (int i = 0; i < 8; i++) w[i] = x[i];
-    fe_pack(v.Y, x);
-#pragma unroll
-    for (int i = 0; i < 8; i++) w[8 + i] = x[i];
-    fe_pack(v.ZZ, x);
-#pragma unroll
-    for (int i = 0; i < 8; i++) w[16 + i] = x[i];
-    fe_pack(v.ZZZ, x);
-#pragma unroll
-    for (int i = 0; i < 8; i++) w[24 + i] = x[i];
+    for (int i = 0; i < 8; i++) __hip_atomic_store(d + i, x[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class F>
+HALO_DEV void tail_publish(uint4* dst, const XYZZ<F>& v) {  // relaxed agent-scope stores (sc1), one lane
     uint32_t* d = (uint32_t*)dst;
-#pragma unroll
-    for (int i = 0; i < 32; i++) __hip_atomic_store(d + i, w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    tail_publish_fe(d, v.X);
+    tail_publish_fe(d + 8, v.Y);
+    tail_publish_fe(d + 16, v.ZZ);
+    tail_publish_fe(d + 24, v.ZZZ);
 }
 
 // true in the block whose release add on *c returned total - 1 (then acquired); block-uniform
@@ -616,17 +618,114 @@ template <class Cv>
 HALO_DEV void tail_side_final(const TailRoundArgs& a, uint32_t sd, uint4* red) {
     using F = typename Cv::Base;
     const uint32_t np = a.nbs + 1;
+    // partial j to lane j / 4 of wave j % 4: every wave gets a quarter, and its tree skips the identity
+    // lanes above them (as k_tail_final deals them)
+    const uint32_t tid = threadIdx.x, j0 = (tid & 63) * (TAIL_THREADS / 64) + (tid >> 6);
     XYZZ<F> acc = xyzz_id<F>();
-    for (uint32_t j = threadIdx.x; j < np; j += TAIL_THREADS) acc = xyzz_add(acc, xyzz_load<F>(a.part + 8 * ((size_t)sd * np + j)));
+    for (uint32_t j = j0; j < np; j += TAIL_THREADS) acc = xyzz_add(acc, xyzz_load<F>(a.part + 8 * ((size_t)sd * np + j)));
     acc = block_group_sum<F>(acc, TAIL_THREADS, red);
-    if (threadIdx.x == 0) {
+    if (tid == 0) {
         xyzz_store(a.out_xyzz + 8 * sd, acc);
         __hip_atomic_store(a.ctr + sd, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
+// Side sd's dot (0: <c_r, z_l>, 1: <c_l, z_r>) by one block, scaled by xi_0 in xi mode, to dots_ark +
+// 2 sd and its GLV split to kw (10 words: k1, k2 words, signs; visible to the block on return).  With a
+// deferred fold the block folds the halves its dot reads and writes them to the ping-pong buffers (side
+// 0: c_r, z_l and the even w'; side 1: c_l, z_r and the odd w').
 template <class Cv>
-__global__ __launch_bounds__(TAIL_THREADS) void k_tail_round(const TailRoundArgs a, const TailFoldArgs f) {
+HALO_DEV void tail_side_dot(const uint4* cs, const uint4* zs, const uint4* w, size_t m, uint32_t sd, const TailFoldArgs& f,
+                            const uint4* xi0_ark, uint4* dots_ark, uint32_t* kw) {
+    using S = typename Cv::Scalar;
+    const int tid = threadIdx.x;
+    const size_t len = 2 * m;
+    const size_t oc = sd ? 0 : m, oz = sd ? m : 0;  // c_r z_l (side 0), c_l z_r (side 1)
+    Fe<S> acc_s = fe_zero<S>();
+    if (f.active) {
+        const Fe<S> xi = fe_from_ark<S>(f.xi), xinv = fe_from_ark<S>(f.xinv);
+        for (size_t i = tid; i < m; i += TAIL_THREADS) {
+            const Fe<S> c = fe_add(fe_from_ark<S>(cs + 2 * (oc + i)), fe_mul(fe_from_ark<S>(cs + 2 * (oc + i + len)), xinv));
+            const Fe<S> z = fe_add(fe_from_ark<S>(zs + 2 * (oz + i)), fe_mul(fe_from_ark<S>(zs + 2 * (oz + i + len)), xi));
+            fe_to_ark(f.cs_out + 2 * (oc + i), c);
+            fe_to_ark(f.zs_out + 2 * (oz + i), z);
+            acc_s = fe_add(acc_s, fe_mul(c, z));
+        }
+        for (size_t u = tid; u < f.wlen_in; u += TAIL_THREADS) {
+            const Fe<S> wv = fe_from_ark<S>(w + 2 * u);
+            fe_to_ark(f.w_out + 2 * (2 * u + sd), sd ? fe_mul(wv, xi) : wv);
+        }
+    } else {
+        for (size_t i = tid; i < m; i += TAIL_THREADS)
+            acc_s = fe_add(acc_s, fe_mul(fe_from_ark<S>(cs + 2 * (oc + i)), fe_from_ark<S>(zs + 2 * (oz + i))));
+    }
+    // block sum: lane shuffles inside each wave, then the four wave sums through LDS
+    for (int off = 32; off > 0; off >>= 1) {
+        Fe<S> o;
+#pragma unroll
+        for (int l = 0; l < NLIMB; l++) o.v[l] = __shfl_xor(acc_s.v[l], off);
+        acc_s = fe_add(acc_s, o);
+    }
+    __shared__ uint4 wsum[TAIL_THREADS / 64][2];
+    if ((tid & 63) == 0) fe_store(wsum[tid >> 6], acc_s);
+    __syncthreads();
+    if (tid == 0) {
+        Fe<S> d = fe_load<S>(wsum[0]);
+        for (int q = 1; q < TAIL_THREADS / 64; q++) d = fe_add(d, fe_load<S>(wsum[q]));
+        if (xi0_ark) d = fe_mul(d, fe_from_ark<S>(xi0_ark));
+        fe_to_ark(dots_ark + 2 * sd, d);
+        Fe<S> one_raw = fe_zero<S>();
+        one_raw.v[0] = 1;
+        uint32_t w8[8], k1[5], k2[5];
+        bool n1, n2;
+        fe_pack(fe_canon(fe_mul(d, one_raw)), w8);
+        glv::decompose<typename Cv::K>(w8, n1, k1, n2, k2);
+        for (int i = 0; i < 4; i++) {
+            kw[i] = k1[i];
+            kw[4 + i] = k2[i];
+        }
+        kw[8] = n1;
+        kw[9] = n2;
+    }
+    __syncthreads();
+}
+
+// The round's n0 point scalars c[ci] w[u] (with a deferred fold applied on the fly) as GLV words, one
+// lane per point, and (the last two blocks) the two sides' dots with their GLV splits (hkw, for
+// k_tail_msm's hiding terms) and the folded c, z, w: the first launch of a tail round over more than
+// TAIL_FUSE_N points, where forming the scalars once per point beats forming them in each point's
+// wave of k_tail_round (64 times the instructions).
+template <class Cv>
+__global__ __launch_bounds__(256) void k_tail_digits(const uint4* cs, const uint4* zs, const uint4* w, size_t n0, size_t m,
+                                                     const TailFoldArgs f, uint32_t* scal, uint8_t* side,
+                                                     const uint4* xi0_ark, uint4* dots_ark, uint32_t* hkw) {
+    using S = typename Cv::Scalar;
+    const uint32_t nsb = (uint32_t)((n0 + 255) / 256);
+    if (blockIdx.x >= nsb) {
+        __shared__ uint32_t kw[10];
+        const uint32_t sd = blockIdx.x - nsb;
+        tail_side_dot<Cv>(cs, zs, w, m, sd, f, xi0_ark, dots_ark, kw);
+        if (threadIdx.x < 10) hkw[10 * sd + threadIdx.x] = kw[threadIdx.x];
+        return;
+    }
+    const size_t k = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (k >= n0) return;
+    const size_t len = 2 * m, j = k % len, u = k / len;
+    const size_t ci = (j < m) ? m + j : j - m;
+    Fe<S> c, wu;
+    if (f.active) {
+        c = fe_add(fe_from_ark<S>(cs + 2 * ci), fe_mul(fe_from_ark<S>(cs + 2 * (ci + len)), fe_from_ark<S>(f.xinv)));
+        wu = fe_from_ark<S>(w + 2 * (u >> 1));
+        if (u & 1) wu = fe_mul(wu, fe_from_ark<S>(f.xi));
+    } else {
+        c = fe_from_ark<S>(cs + 2 * ci);
+        wu = fe_from_ark<S>(w + 2 * u);
+    }
+    tail_scalar_val<Cv>(fe_mul(c, wu), (j < m) ? 0 : 1, k, scal, side);
+}
+
+template <class Cv>
+__global__ __launch_bounds__(TAIL_THREADS, 1) void k_tail_round(const TailRoundArgs a, const TailFoldArgs f) {
     using F = typename Cv::Base;
     using S = typename Cv::Scalar;
     __shared__ uint4 red[TAIL_THREADS / 2 * 8];
@@ -671,77 +770,21 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail_round(const TailRoundArgs
         if (tail_arrive(a.ctr + sd, a.nbs + 1, &flag)) tail_side_final<Cv>(a, sd, red);
         return;
     }
-    // ---- the dots block (k_tail_prep's last block) and the two hiding terms
-    __shared__ uint4 dred[2][256 * 2];
-    __shared__ uint32_t kw[2][10];
-    Fe<S> da = fe_zero<S>(), db = fe_zero<S>();
-    if (f.active) {
-        const Fe<S> xi = fe_from_ark<S>(f.xi), xinv = fe_from_ark<S>(f.xinv);
-        for (size_t i = tid; i < m; i += 256) {
-            const Fe<S> cl = fe_add(fe_from_ark<S>(a.cs + 2 * i), fe_mul(fe_from_ark<S>(a.cs + 2 * (i + len)), xinv));
-            const Fe<S> cr = fe_add(fe_from_ark<S>(a.cs + 2 * (m + i)), fe_mul(fe_from_ark<S>(a.cs + 2 * (m + i + len)), xinv));
-            const Fe<S> zl = fe_add(fe_from_ark<S>(a.zs + 2 * i), fe_mul(fe_from_ark<S>(a.zs + 2 * (i + len)), xi));
-            const Fe<S> zr = fe_add(fe_from_ark<S>(a.zs + 2 * (m + i)), fe_mul(fe_from_ark<S>(a.zs + 2 * (m + i + len)), xi));
-            fe_to_ark(f.cs_out + 2 * i, cl);
-            fe_to_ark(f.cs_out + 2 * (m + i), cr);
-            fe_to_ark(f.zs_out + 2 * i, zl);
-            fe_to_ark(f.zs_out + 2 * (m + i), zr);
-            da = fe_add(da, fe_mul(cr, zl));
-            db = fe_add(db, fe_mul(cl, zr));
-        }
-        for (size_t u = tid; u < f.wlen_in; u += 256) {
-            const Fe<S> wv = fe_from_ark<S>(a.w + 2 * u);
-            fe_to_ark(f.w_out + 2 * (2 * u), wv);
-            fe_to_ark(f.w_out + 2 * (2 * u + 1), fe_mul(wv, xi));
-        }
-    } else {
-        for (size_t i = tid; i < m; i += 256) {
-            da = fe_add(da, fe_mul(fe_from_ark<S>(a.cs + 2 * (m + i)), fe_from_ark<S>(a.zs + 2 * i)));
-            db = fe_add(db, fe_mul(fe_from_ark<S>(a.cs + 2 * i), fe_from_ark<S>(a.zs + 2 * (m + i))));
-        }
+    // ---- hiding blocks 2 nbs + sd: side sd's dot, its GLV split and the term dot_sd H'
+    const uint32_t sd = blockIdx.x - 2 * a.nbs;
+    __shared__ uint32_t kw[10];
+    tail_side_dot<Cv>(a.cs, a.zs, a.w, m, sd, f, a.xi0_ark, a.dots_ark, kw);
+    // dot H': lane t < 128 bit t of k1 with 2^t H', t >= 128 bit t - 128 of k2 with phi(2^(t-128) H')
+    XYZZ<F> acc = xyzz_id<F>();
+    if ((kw[tid >> 5] >> (tid & 31)) & 1u) {
+        Affine<F> p = aff_load<F>(a.htab + 4 * (tid & 127));
+        if (tid >= 128) p.x = fe_mul(p.x, fe_from_const<F>(Cv::K::BETA));
+        if (kw[8 + (tid >> 7)]) p.y = fe_neg(p.y);
+        acc = xyzz_from_aff(p);
     }
-    fe_store(dred[0] + 2 * tid, da);
-    fe_store(dred[1] + 2 * tid, db);
-    __syncthreads();
-    for (int off = 128; off > 0; off >>= 1) {
-        if (tid < off) {
-            fe_store(dred[0] + 2 * tid, fe_add(fe_load<S>(dred[0] + 2 * tid), fe_load<S>(dred[0] + 2 * (tid + off))));
-            fe_store(dred[1] + 2 * tid, fe_add(fe_load<S>(dred[1] + 2 * tid), fe_load<S>(dred[1] + 2 * (tid + off))));
-        }
-        __syncthreads();
-    }
-    if (tid < 2) {
-        Fe<S> d = fe_load<S>(dred[tid]);
-        if (a.xi0_ark) d = fe_mul(d, fe_from_ark<S>(a.xi0_ark));
-        fe_to_ark(a.dots_ark + 2 * tid, d);
-        uint32_t w8[8], k1[5], k2[5];
-        bool n1, n2;
-        Fe<S> one_raw = fe_zero<S>();
-        one_raw.v[0] = 1;
-        fe_pack(fe_canon(fe_mul(d, one_raw)), w8);
-        glv::decompose<typename Cv::K>(w8, n1, k1, n2, k2);
-        for (int i = 0; i < 4; i++) {
-            kw[tid][i] = k1[i];
-            kw[tid][4 + i] = k2[i];
-        }
-        kw[tid][8] = n1;
-        kw[tid][9] = n2;
-    }
-    __syncthreads();
-    for (uint32_t sd = 0; sd < 2; sd++) {  // dot_sd H': lane t < 128 bit t of k1 with 2^t H', t >= 128 k2 with phi
-        XYZZ<F> acc = xyzz_id<F>();
-        if ((kw[sd][tid >> 5] >> (tid & 31)) & 1u) {
-            Affine<F> p = aff_load<F>(a.htab + 4 * (tid & 127));
-            if (tid >= 128) p.x = fe_mul(p.x, fe_from_const<F>(Cv::K::BETA));
-            if (kw[sd][8 + (tid >> 7)]) p.y = fe_neg(p.y);
-            acc = xyzz_from_aff(p);
-        }
-        acc = block_group_sum<F>(acc, TAIL_THREADS, red);
-        if (tid == 0) tail_publish(a.part + 8 * ((size_t)sd * (a.nbs + 1) + a.nbs), acc);
-        __syncthreads();
-    }
-    for (uint32_t sd = 0; sd < 2; sd++)
-        if (tail_arrive(a.ctr + sd, a.nbs + 1, &flag)) tail_side_final<Cv>(a, sd, red);
+    acc = block_group_sum<F>(acc, TAIL_THREADS, red);
+    if (tid == 0) tail_publish(a.part + 8 * ((size_t)sd * (a.nbs + 1) + a.nbs), acc);
+    if (tail_arrive(a.ctr + sd, a.nbs + 1, &flag)) tail_side_final<Cv>(a, sd, red);
 }
 
 // block b (0: L, 1: R): sum of the partials + dot_b * H' (from the 2^i H' table), -> WrappedPoint
@@ -898,6 +941,20 @@ struct halo_ipa_session {
         htab_ptr = nullptr;
         started = blinded = combined = false;
     }
+    size_t buffer_bytes() const {
+        size_t b = 0;
+        for (const DevBuf* d : {&gs, &cs, &zs, &cs2, &zs2, &htab, &small, &tmp, &pbar, &own_table, &w[0], &w[1], &scal,
+                                &side, &part, &mat.digits, &mat.lists, &mat.keys, &mat.vals, &mat.bstart, &mat.partials,
+                                &mat.bucket_sums, &mat.window_sums})
+            b += d->bytes;
+        return b;
+    }
+    void release_large() {  // everything sized by n (the small staging and the H' table stay)
+        for (DevBuf* d : {&gs, &cs, &zs, &cs2, &zs2, &tmp, &pbar, &own_table, &w[0], &w[1], &scal, &side, &part,
+                          &mat.digits, &mat.lists, &mat.keys, &mat.vals, &mat.bstart, &mat.partials, &mat.bucket_sums,
+                          &mat.window_sums})
+            d->release();
+    }
     void destroy() {
         if (s) (void)hipStreamSynchronize(s);
         if (htab_ready) (void)hipEventDestroy(htab_ready);
@@ -954,6 +1011,10 @@ void ipa_release(halo_ipa_session* ses) {
     if (!ses) return;
     if (ses->s) (void)hipStreamSynchronize(ses->s);
     ses->table_ref.reset();  // a retired SRS multiples table is freed with its last session
+    // an idle session keeps at most "ipa_pool_keep_bytes" of device buffers (tuning, default 1 GB: a
+    // 2^20 opening's ~0.6 GB stay pooled for the next one): above it the per-size buffers
+    // are released here
+    if ((long long)ses->buffer_bytes() > tuning(TUNE_IPA_POOL_KEEP)) ses->release_large();
     {
         std::lock_guard<std::mutex> g(g_pool_mu);
         // a session already idle (a second end of the same handle) is not pooled twice: two later
@@ -1239,6 +1300,7 @@ static int ipa_h_table(DeviceState* st, int curve, const halo_wrapped_point_t* H
 constexpr size_t SM_BYTES = 2048;
 constexpr size_t SM_WBAR = 1024, SM_ALPHA = 1056, SM_W = 1088, SM_WP = 1120, SM_C = 1152, SM_CBAR = 1216, SM_S = 1280,
                  SM_CP = 1344, SM_NEGW = 1408, SM_T = 1536, SM_EVAL = 1664, SM_V = 1696,  // SM_T: 128 B XYZZ
+                 SM_HKW = 1728,  // 2 x 10 words: the dots' GLV splits (k_tail_digits -> k_tail_round)
                  SM_CTR = 1856;  // 2 x u32 arrival counters of k_tail_round (zero between launches)
 
 // Phase 1 of a session: G (resident SRS prefix, or explicit gs_host), c (cs_len coefficients, host or
@@ -1643,7 +1705,7 @@ static int ipa_enter_tail(DeviceState* st, halo_ipa_session* ses, hipStream_t s)
 static int ipa_tail_sums(halo_ipa_session* ses, int mode, hipStream_t s) {
     const size_t n0 = ses->n0, m = ses->m;
     char* sm = (char*)ses->small.ptr;
-    if (mode == 0) {  // one fused launch (k_tail_round)
+    if (mode == 0) {  // one fused launch (k_tail_round) up to TAIL_FUSE_N points, three above
         TailFoldArgs f{};
         f.active = ses->fold_pending;
         if (f.active) {  // the previous round's fold, applied here (halo_ipa_fold deferred it)
@@ -1669,9 +1731,26 @@ static int ipa_tail_sums(halo_ipa_session* ses, int mode, hipStream_t s) {
         ra.part = ses->part.as<uint4>();
         ra.ctr = (uint32_t*)(sm + SM_CTR);
         ra.out_xyzz = (uint4*)(sm + 512);
-        DISPATCH_CURVE(ses->curve, Cv, {
-            hipLaunchKernelGGL(k_tail_round<Cv>, dim3(2 * ra.nbs + 1), dim3(TAIL_THREADS), 0, s, ra, f);
-        });
+        if (n0 <= TAIL_FUSE_N) {
+            DISPATCH_CURVE(ses->curve, Cv, {
+                hipLaunchKernelGGL(k_tail_round<Cv>, dim3(2 * ra.nbs + 2), dim3(TAIL_THREADS), 0, s, ra, f);
+            });
+        } else {  // k_tail_digits (the point scalars and the dots) + k_tail_msm + k_tail_final
+            const size_t nbs = (TAIL_WIN * (n0 / 2) + TAIL_THREADS - 1) / TAIL_THREADS, nblk = 2 * nbs;
+            DISPATCH_CURVE(ses->curve, Cv, {
+                hipLaunchKernelGGL(k_tail_digits<Cv>, dim3(gridn(n0, 256) + 2), dim3(256), 0, s, ses->cs.as<const uint4>(),
+                                   ses->zs.as<const uint4>(), ses->w[ses->wcur].as<const uint4>(), n0, m, f,
+                                   ses->scal.as<uint32_t>(), ses->side.as<uint8_t>(), ra.xi0_ark, ra.dots_ark,
+                                   (uint32_t*)(sm + SM_HKW));
+                hipLaunchKernelGGL(k_tail_msm<Cv>, dim3((unsigned)nblk), dim3(TAIL_THREADS), 0, s, ses->table, ses->table_ld,
+                                   ses->scal.as<const uint32_t>(), ses->side.as<const uint8_t>(), n0, m, 0, (uint32_t)nbs,
+                                   ses->part.as<uint4>(), (const uint4*)ses->htab_ptr, (const uint4*)(sm + 128),
+                                   (const uint32_t*)(sm + SM_HKW), (uint4*)(sm + 512));
+                if (nbs > 1)
+                    hipLaunchKernelGGL(k_tail_final<Cv>, dim3(2), dim3(TAIL_THREADS), 0, s, ses->part.as<const uint4>(),
+                                       (int)nblk, (const uint4*)nullptr, (const uint4*)nullptr, (uint4*)(sm + 512), 1);
+            });
+        }
         HALO_HIP(hipGetLastError());
         if (f.active) {
             std::swap(ses->cs.ptr, ses->cs2.ptr);

@@ -382,7 +382,10 @@ static unsigned grid_for(size_t n, unsigned thr) { return (unsigned)std::max<siz
 // Chunk length K of k_acc for E sorted entries.  Large MSMs (E > 16 x the resident lanes, 256 CUs x
 // 16 waves x 64): >= 4 rounds of resident lanes, 16 <= K <= 64 -- every lane does the same number
 // of mixed additions, and several rounds absorb the CU slots held by the previous MSM's tail kernels,
-// which one exact round would not (measured: K = 60 at 2^20 is 1 round and 15 % slower than K = 16).
+// which one exact round would not (measured: K = 60 at 2^20 is 1 round and 15 % slower than K = 16;
+// round 4, pipelined 2^20 step: 2 rounds (K = 30) 1.378, 3 rounds (K = 20) 1.365, 4 rounds 1.354 ms,
+// and 6 / 8 rounds (K = 10 / 8: k_acc 0.87 / 0.85 ms, but twice the chunk partials for k_merge)
+// 1.362 / 1.374 ms).
 // Smaller MSMs are latency-bound (a commitment, an IPA round): their critical path is a lane's K
 // dependent additions in k_acc plus k_merge's run of about E / (NB K) partials per bucket, so K =
 // ceil(sqrt(E / NB)) balances the two -- but at least ceil(E / resident lanes), one round.
@@ -450,6 +453,10 @@ static int msm_pick_set(MsmPipe& P, hipStream_t s, bool advance) {
     return set;
 }
 
+// (Measured and rejected, round 4: tail streams restricted to a CU mask (32 / 64 / 128 of the 256
+// CUs, hipExtStreamCreateWithCUMask) so that the tail would not share CUs with the next MSM's sort:
+// 2^20 step 1.34 -> 2.71 / 2.08 / 1.89 ms -- the tail chain is throughput-bound on fewer CUs and
+// becomes the critical path.)
 static int pipe_init(MsmPipe& P) {
     if (P.tail[0]) return HALO_OK;
     for (auto& t : P.tail) HALO_HIP(hipStreamCreateWithFlags(&t, hipStreamNonBlocking));

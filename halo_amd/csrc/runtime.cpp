@@ -150,9 +150,9 @@ static void prof_drain() {
 
 // ---- tuning ----------------------------------------------------------------------------------
 static const char* const kTuneNames[TUNE_COUNT] = {"ipa_weighted", "ipa_tail", "ipa_srs_tail_n", "ipa_mat_n",
-                                                   "msm_multi_max"};
-static const long long kTuneDefault[TUNE_COUNT] = {1, 1, 4096, 2048, 1ll << 18};
-static std::atomic<long long> g_tune[TUNE_COUNT] = {{1}, {1}, {4096}, {2048}, {1ll << 18}};
+                                                   "msm_multi_max", "ipa_pool_keep_bytes"};
+static const long long kTuneDefault[TUNE_COUNT] = {1, 1, 4096, 2048, 1ll << 18, 1ll << 30};
+static std::atomic<long long> g_tune[TUNE_COUNT] = {{1}, {1}, {4096}, {2048}, {1ll << 18}, {1ll << 30}};
 long long tuning(TuneKey k) { return g_tune[k].load(std::memory_order_relaxed); }
 static int tune_index(const char* key) {
     if (!key) return -1;

@@ -35,7 +35,7 @@ void clear_error();
     } while (0)
 
 // ---- tuning (halo_set_tuning): path selections the parity tests pin; read on every use
-enum TuneKey { TUNE_IPA_WEIGHTED, TUNE_IPA_TAIL, TUNE_IPA_SRS_TAIL_N, TUNE_IPA_MAT_N, TUNE_MSM_MULTI_MAX, TUNE_COUNT };
+enum TuneKey { TUNE_IPA_WEIGHTED, TUNE_IPA_TAIL, TUNE_IPA_SRS_TAIL_N, TUNE_IPA_MAT_N, TUNE_MSM_MULTI_MAX, TUNE_IPA_POOL_KEEP, TUNE_COUNT };
 long long tuning(TuneKey k);
 
 // ---- device buffers ---------------------------------------------------------------------------

@@ -32,6 +32,7 @@ constexpr int RS_THREADS = 512;
 // Tiles of RS_THREADS x 16 rounds: 8192 entries, runs of ~32 entries = 128 B per digit, 64 KB of LDS
 // staging.  (Measured: 4096-entry tiles, 4 workgroups per CU, were no faster.)
 constexpr int RS_BINS = 256;
+constexpr size_t RS_STAGE_BYTES = 2 * 4 * RS_THREADS * 16;  // k_rs_scatter's key / value staging
 constexpr uint32_t RS_NONE = 0xffffffffu;
 
 struct RsIn {
@@ -243,7 +244,15 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(RsIn in, const uint32
     __shared__ uint32_t goff[RS_BINS];           // global start of this tile's run per digit
     __shared__ uint32_t lstart[RS_BINS];         // tile-local start per digit
     __shared__ uint32_t wpos[WAVES][RS_BINS];    // per-wave histogram, then per-wave next position
-    __shared__ uint32_t skey[RS_TILE], sval[RS_TILE];
+    // the staging arrays (64 KB) are dynamic LDS (RS_STAGE_BYTES at launch): with a static size the
+    // compiler derives the LDS-limited occupancy (4 waves per SIMD) and pads the VGPR allocation to
+    // match it (76 used -> 97 allocated), which would keep the workgroup from being resident beside
+    // the previous MSM's tail kernels (k_merge: 2 waves per SIMD of 161 VGPRs).  (Measured: 2^20
+    // headline unchanged, 1.337 vs 1.336 ms -- the front and the tail contend for VALU issue, not slots.)
+    static_assert(2 * 4 * RS_TILE == RS_STAGE_BYTES, "staging size");
+    extern __shared__ uint32_t rs_stage[];
+    uint32_t* skey = rs_stage;
+    uint32_t* sval = rs_stage + RS_TILE;
     __shared__ uint32_t total;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const size_t limit = rs_limit(in);
@@ -517,13 +526,13 @@ int msm_radix_sort(const uint32_t* digits, size_t E, size_t npw, uint32_t B, uin
         }
         if (fp) {
             DISPATCH_FIELD(fused->field, SF, {
-                hipLaunchKernelGGL((k_rs_scatter<16, SF>), dim3(nt), dim3(RS_THREADS), 0, s, in,
+                hipLaunchKernelGGL((k_rs_scatter<16, SF>), dim3(nt), dim3(RS_THREADS), RS_STAGE_BYTES, s, in,
                                    S.hist.as<const uint32_t>(), S.offs.as<const uint32_t>(), S.keys[cur].as<uint32_t>(),
                                    S.vals[cur].as<uint32_t>());
             });
         } else {
             auto ks = p == 0 ? k_rs_scatter<16, void, true> : k_rs_scatter<16, void, false>;
-            hipLaunchKernelGGL(ks, dim3(nt), dim3(RS_THREADS), 0, s, in, S.hist.as<const uint32_t>(),
+            hipLaunchKernelGGL(ks, dim3(nt), dim3(RS_THREADS), RS_STAGE_BYTES, s, in, S.hist.as<const uint32_t>(),
                                S.offs.as<const uint32_t>(), S.keys[cur].as<uint32_t>(), S.vals[cur].as<uint32_t>());
         }
         HALO_HIP(hipGetLastError());

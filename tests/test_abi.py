@@ -77,7 +77,8 @@ def test_fails_loudly_without_gpu(lib_path):
 def test_tuning_keys_roundtrip_and_reject_unknown(lib_path):
     """halo_set_tuning / halo_get_tuning are host-only: every key round-trips, -1 restores the
     default, an unknown key is HALO_EINVAL (no GPU needed)."""
-    defaults = {"ipa_weighted": 1, "ipa_tail": 1, "ipa_srs_tail_n": 4096, "ipa_mat_n": 2048, "msm_multi_max": 1 << 18}
+    defaults = {"ipa_weighted": 1, "ipa_tail": 1, "ipa_srs_tail_n": 4096, "ipa_mat_n": 2048, "msm_multi_max": 1 << 18,
+                "ipa_pool_keep_bytes": 1 << 30}
     for k, v in defaults.items():
         assert H.get_tuning(k) == v
         with H.tuning(**{k: 7}):

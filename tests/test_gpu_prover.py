@@ -167,3 +167,37 @@ def _ipa_open_vs_c(hal, L, cid, curve, n, logn):
     assert all(np.array_equal(x, y) for x, y in zip(a[0], b[0]))
     assert all(np.array_equal(x, y) for x, y in zip(a[1], b[1]))
     assert np.array_equal(a[2], b[2]) and a[3] == b[3]
+
+
+def test_pooled_session_releases_large_buffers(hal):
+    """an idle pooled IPA session keeps at most "ipa_pool_keep_bytes" of device buffers.
+    A 2^18 opening (weighted rounds, materialised G, the session's own 126 MB tail table) is run on a
+    drained pool (halo_shutdown) and the device memory it leaves allocated is compared between the
+    default cap (1 GB: the session keeps its buffers for the next opening) and a 64 MB cap (released
+    at halo_ipa_end): the difference is the session's large buffers, the tail table at least."""
+    import torch
+
+    n = 1 << 18
+    L = hal.load()
+    cid = hal.CURVES["pallas"]
+    hal.check(L.halo_srs_synthesize(cid, n, 4218))
+    hal.check(L.halo_srs_precompute_windows(cid))
+    dev = prover.DeviceBackend("pallas")
+    rng = np.random.default_rng(18)
+    p = dev.random_vec(n, rng)
+
+    def opening():
+        return dev.ipa(p, n, 0x1234567, dev.h_mul(0xABCDEF), prover.Challenges(dev.m, seed=5))
+
+    ref = opening()  # warms the shared scratch (MSM sets, SRS-derived tables)
+    kept = {}
+    for cap in (-1, 64 << 20):
+        with hal.tuning(ipa_pool_keep_bytes=cap):
+            hal.check(L.halo_shutdown())  # drains the session pool (the library stays usable)
+            torch.cuda.synchronize()
+            free0 = torch.cuda.mem_get_info()[0]
+            got = opening()
+            torch.cuda.synchronize()
+            kept[cap] = free0 - torch.cuda.mem_get_info()[0]
+        assert np.array_equal(got[2], ref[2]) and got[3] == ref[3]
+    assert kept[-1] - kept[64 << 20] > (100 << 20), {k: v / 2**20 for k, v in kept.items()}

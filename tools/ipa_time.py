@@ -1,5 +1,6 @@
 """Times a full device-resident IPA opening (pcdl.rs:392-438 round loop): lg n rounds of L/R MSMs +
-fold, with a stand-in transcript (fixed pseudo-random challenges)."""
+fold, with a stand-in transcript (fixed pseudo-random challenges).  MAT_N=<len>[,<len>...]: repeat
+with the weighted rounds materialising G at each length (tuning ipa_mat_n)."""
 import ctypes, os, random, sys, time
 os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")  # as bench.py
 sys.path.insert(0, '/root/repo')
@@ -15,7 +16,9 @@ def fe1(v):
     return np.array([(m >> (64 * i)) & (2**64 - 1) for i in range(4)], dtype=np.uint64)
 
 
-for lg in [int(x) for x in (sys.argv[1:] or ['16', '20'])]:
+MATS = [int(x) for x in os.environ.get("MAT_N", "-1").split(",")]
+for lg, mat in [(int(x), m) for x in (sys.argv[1:] or ['16', '20']) for m in MATS]:
+    H.set_tuning("ipa_mat_n", mat)
     n = 1 << lg
     H.check(L.halo_srs_synthesize(0, n, 77))
     H.check(L.halo_srs_precompute_windows(0))  # as bench.py: round 1 L/R on the shifted SRS
@@ -50,6 +53,6 @@ for lg in [int(x) for x in (sys.argv[1:] or ['16', '20'])]:
         nl = ctypes.c_size_t(0); ms = ctypes.c_double(0)
         H.check(L.halo_profile_read(b"ipa_fold", ctypes.byref(nl), ctypes.byref(ms)))
         H.check(L.halo_profile_enable(0))
-        print(f"open 2^{lg}: total {1e3*(t1-t0):.2f} ms (L/R rounds {1e3*t_lr:.2f} ms, folds {1e3*t_fold:.2f} ms; "
+        print(f"open 2^{lg} (ipa_mat_n {H.get_tuning('ipa_mat_n')}): total {1e3*(t1-t0):.2f} ms (L/R rounds {1e3*t_lr:.2f} ms, folds {1e3*t_fold:.2f} ms; "
               f"fold kernels {ms.value:.2f} ms over {nl.value})", flush=True)
         print("  per round (lr ms, fold ms):", per, flush=True)

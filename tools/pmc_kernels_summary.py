@@ -1,6 +1,8 @@
 """Summarises tools/pmc_kernels.sh: per kernel (name prefix up to the template arguments), mean
 serialised duration, counters per launch, HBM bytes (FETCH_SIZE x 2 for streaming reads on gfx950 is
-NOT applied here: raw values, MI355X_MICROARCH.md HBM section) and VALU issue per CU-cycle.
+NOT applied here: raw values, MI355X_MICROARCH.md HBM section), VALU issue per CU-cycle, VALU
+instructions per wave (k_acc: a wave's 64 lanes each run K = 16 additions, so / 16 = per addition)
+and the GUI-active clock in MHz.
 usage: python tools/pmc_kernels_summary.py <dir> [substring ...]"""
 import collections
 import csv
@@ -47,7 +49,7 @@ for p in "abcde":
     for k, d in counters(p).items():
         c.setdefault(k, {}).update(d)
 print(f"{'kernel':70s} {'us':>8s} {'n':>4s} {'VALU/CU/clk':>11s} {'LDSi/CU/clk':>11s} {'wait%':>6s} "
-      f"{'issue%':>6s} {'fetchMB':>8s} {'writeMB':>8s} {'ldsconf%':>8s} {'waves':>7s}")
+      f"{'issue%':>6s} {'fetchMB':>8s} {'writeMB':>8s} {'ldsconf%':>8s} {'waves':>7s} {'VALU/wave':>10s} {'MHz':>6s}")
 for k in sorted(c, key=lambda k: -dur.get(k, (0, 0))[0]):
     d = c[k]
     us, n = dur.get(k, (0.0, 0))
@@ -58,4 +60,5 @@ for k in sorted(c, key=lambda k: -dur.get(k, (0, 0))[0]):
     conf = d.get("SQ_LDS_BANK_CONFLICT", 0) / (d.get("SQ_LDS_IDX_ACTIVE", 0) or 1) * 100
     print(f"{k:70s} {us:8.1f} {n:4d} {valu:11.3f} {ldsi:11.3f} {100 * d.get('SQ_WAIT_ANY', 0) / wc:6.1f} "
           f"{100 * d.get('SQ_WAIT_INST_ANY', 0) / wc:6.1f} {d.get('FETCH_SIZE', 0) / 1024:8.1f} "
-          f"{d.get('WRITE_SIZE', 0) / 1024:8.1f} {conf:8.1f} {d.get('SQ_WAVES', 0):7.0f}")
+          f"{d.get('WRITE_SIZE', 0) / 1024:8.1f} {conf:8.1f} {d.get('SQ_WAVES', 0):7.0f} "
+          f"{d.get('SQ_INSTS_VALU', 0) / (d.get('SQ_WAVES', 0) or 1):10.0f} {cyc / us if us else 0:6.0f}")

@@ -19,3 +19,5 @@ for lib in "$@"; do
   echo "== pcdl open $(basename $lib)"
   HALO_LIB=$PWD/$lib timeout -k 10 200 python tools/pcdl_open_time.py 2 4 6 8 10 12 16 2>&1 | grep "^2^" | sed 's/begin+eval.*rounds=/rounds=/' || exit 1
 done
+echo "== ipa_mat_n sweep (in-tree library)"
+MAT_N=2048,8192,32768,131072 REPS=2 timeout -k 10 300 python tools/ipa_time.py 20 2>&1 | grep "^open" || exit 1
