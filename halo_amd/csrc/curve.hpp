@@ -315,6 +315,43 @@ HALO_DEV void xyzz_store(uint4* p, const XYZZ<F>& a) {
     fe_store(p + 6, a.ZZZ);
 }
 
+// Chunk partials (k_acc -> k_group_sums -> k_merge): XYZZ as 4 x 9 raw limbs, 36 dwords = 9 uint4
+// (144 B), with X as k_acc's running sum leaves it (normalized limbs, < 8p).  k_acc then stores
+// without settling X or packing limbs; its bucket-boundary stores are divergent (at 2^20 about a
+// quarter of its steps have a lane at a boundary), so they cost the whole wave.  The loader settles X.
+constexpr int PARTIAL_U4 = 9;
+template <class F>
+HALO_DEV void partial_store(uint4* p, const XYZZ<F>& a) {
+    const Fe<F>* c[4] = {&a.X, &a.Y, &a.ZZ, &a.ZZZ};
+    uint32_t w[4 * NLIMB];
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+#pragma unroll
+        for (int i = 0; i < NLIMB; i++) w[k * NLIMB + i] = c[k]->v[i];
+#pragma unroll
+    for (int q = 0; q < PARTIAL_U4; q++) p[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+}
+template <class F>
+HALO_DEV XYZZ<F> partial_load(const uint4* p) {
+    uint32_t w[4 * NLIMB];
+#pragma unroll
+    for (int q = 0; q < PARTIAL_U4; q++) {
+        const uint4 v = p[q];
+        w[4 * q] = v.x;
+        w[4 * q + 1] = v.y;
+        w[4 * q + 2] = v.z;
+        w[4 * q + 3] = v.w;
+    }
+    XYZZ<F> a;
+    Fe<F>* c[4] = {&a.X, &a.Y, &a.ZZ, &a.ZZZ};
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+#pragma unroll
+        for (int i = 0; i < NLIMB; i++) c[k]->v[i] = w[k * NLIMB + i];
+    a.X = fe_reduce_8p(a.X);
+    return a;
+}
+
 // WrappedPoint (ark Montgomery x, y; (0,0) = identity) -> internal affine
 template <class F>
 HALO_DEV Affine<F> aff_from_wrapped(const uint4* p) {

@@ -194,7 +194,7 @@ __device__ __forceinline__ void acc_chunk(size_t t, uint32_t cnt, const uint32_t
         if (k != cur) {  // bucket boundary inside the chunk
             for (uint32_t b = cur + 1; b <= k; b++) bstart[b] = e;
             if (!first_done) {
-                xyzz_store(first + 8 * t, xyzz_settle(acc));
+                partial_store(first + PARTIAL_U4 * t, acc);
                 first_done = true;
             } else {
                 xyzz_store(bucket_sums + 8 * (size_t)cur, xyzz_settle(acc));
@@ -218,7 +218,7 @@ __device__ __forceinline__ void acc_chunk(size_t t, uint32_t cnt, const uint32_t
         if (phi) p.x = fe_mul(p.x, fe_from_const<F>(Cv::K::BETA));
         acc = xyzz_madd_run(acc, fresh, p, (v & 0x80000000u) ? ~0u : 0u, check_q);
     }
-    xyzz_store((first_done ? last : first) + 8 * t, xyzz_settle(acc));
+    partial_store((first_done ? last : first) + PARTIAL_U4 * t, acc);
     if (end == cnt)
         for (uint32_t b = cur + 1; b <= NB; b++) bstart[b] = cnt;
 }
@@ -545,11 +545,11 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
     const uint32_t K = msm_chunk_len(st, E, NB);
     const size_t nchunks = (E + K - 1) / K;
     const size_t ng1 = nchunks / MSM_GROUP, ng2 = nchunks / (MSM_GROUP * MSM_GROUP);
-    HALO_CHECK(M.partials.reserve((std::max<size_t>(nchunks, 1) * 2 + ng1 + ng2 + 2) * 128));
+    HALO_CHECK(M.partials.reserve((std::max<size_t>(nchunks, 1) * 2 + ng1 + ng2 + 2) * 16 * PARTIAL_U4));
     uint4* P_first = M.partials.as<uint4>();
-    uint4* P_last = P_first + 8 * std::max<size_t>(nchunks, 1);
-    uint4* P_g1 = P_last + 8 * std::max<size_t>(nchunks, 1);
-    uint4* P_g2 = P_g1 + 8 * (ng1 + 1);
+    uint4* P_last = P_first + PARTIAL_U4 * std::max<size_t>(nchunks, 1);
+    uint4* P_g1 = P_last + PARTIAL_U4 * std::max<size_t>(nchunks, 1);
+    uint4* P_g2 = P_g1 + PARTIAL_U4 * (ng1 + 1);
     HALO_CHECK(M.bucket_sums.reserve(NB * 128));
     HALO_CHECK(M.seg_acc.reserve((size_t)SW * H * 128));  // row sums
     HALO_CHECK(M.seg_sum.reserve((size_t)SW * L * 128));  // column sums
@@ -699,16 +699,16 @@ static int msm_multi_device_t(DeviceState* st, const void* const* scalars, const
     const size_t ng1 = nchunks / MSM_GROUP, ng2 = nchunks / (MSM_GROUP * MSM_GROUP);
     HALO_CHECK(M.digits.reserve(E * 4));
     HALO_CHECK(M.bstart.reserve((NB + 1) * 4));
-    HALO_CHECK(M.partials.reserve((nchunks * 2 + ng1 + ng2 + 2) * 128));
+    HALO_CHECK(M.partials.reserve((nchunks * 2 + ng1 + ng2 + 2) * 16 * PARTIAL_U4));
     HALO_CHECK(M.bucket_sums.reserve(NB * 128));
     HALO_CHECK(M.seg_acc.reserve((size_t)SW * H * 128));
     HALO_CHECK(M.seg_sum.reserve((size_t)SW * L * 128));
     HALO_CHECK(M.bits.reserve((size_t)SW * NT * 128));
     HALO_CHECK(M.window_sums.reserve((size_t)SW * 128));
     uint4* P_first = M.partials.as<uint4>();
-    uint4* P_last = P_first + 8 * nchunks;
-    uint4* P_g1 = P_last + 8 * nchunks;
-    uint4* P_g2 = P_g1 + 8 * (ng1 + 1);
+    uint4* P_last = P_first + PARTIAL_U4 * nchunks;
+    uint4* P_g1 = P_last + PARTIAL_U4 * nchunks;
+    uint4* P_g2 = P_g1 + PARTIAL_U4 * (ng1 + 1);
     uint32_t* digits = M.digits.as<uint32_t>();
     if (ragged) HALO_HIP(hipMemsetAsync(digits, 0xff, E * 4, s));  // DIGIT_NONE past each length
     for (size_t p = 0; p < k; p++)
@@ -804,16 +804,16 @@ static int msm_srs_pairs_t(DeviceState* st, size_t np, const MsmPairIO* io, size
     const size_t ng1 = nchunks / MSM_GROUP, ng2 = nchunks / (MSM_GROUP * MSM_GROUP);
     HALO_CHECK(M.digits.reserve(E * 4));
     HALO_CHECK(M.bstart.reserve((NB + 1) * 4));
-    HALO_CHECK(M.partials.reserve((nchunks * 2 + ng1 + ng2 + 2) * 128));
+    HALO_CHECK(M.partials.reserve((nchunks * 2 + ng1 + ng2 + 2) * 16 * PARTIAL_U4));
     HALO_CHECK(M.bucket_sums.reserve(NB * 128));
     HALO_CHECK(M.seg_acc.reserve((size_t)SW * H * 128));
     HALO_CHECK(M.seg_sum.reserve((size_t)SW * L * 128));
     HALO_CHECK(M.bits.reserve((size_t)SW * NT * 128));
     HALO_CHECK(M.window_sums.reserve((size_t)(2 * SW) * 128));  // + the hiding terms
     uint4* P_first = M.partials.as<uint4>();
-    uint4* P_last = P_first + 8 * nchunks;
-    uint4* P_g1 = P_last + 8 * nchunks;
-    uint4* P_g2 = P_g1 + 8 * (ng1 + 1);
+    uint4* P_last = P_first + PARTIAL_U4 * nchunks;
+    uint4* P_g1 = P_last + PARTIAL_U4 * nchunks;
+    uint4* P_g2 = P_g1 + PARTIAL_U4 * (ng1 + 1);
     uint4* hide_slot = M.window_sums.as<uint4>() + 8 * SW;
     // the hiding terms on the tail stream, beside the front and the accumulation
     HALO_HIP(hipEventRecord(M.start, s));
@@ -1107,16 +1107,16 @@ static int msm_shared_batch_t(DeviceState* st, const uint4* bases, const uint4* 
     HALO_CHECK(S.keys.reserve(E * 4));
     HALO_CHECK(S.vals.reserve(E * 4));
     HALO_CHECK(S.bstart.reserve((NB + 1) * 4));
-    HALO_CHECK(S.partials.reserve((nchunks * 2 + ng1 + ng2 + 2) * 128));
+    HALO_CHECK(S.partials.reserve((nchunks * 2 + ng1 + ng2 + 2) * 16 * PARTIAL_U4));
     HALO_CHECK(S.bucket_sums.reserve(NB * 128));
     HALO_CHECK(S.window_sums.reserve(SW * 128));
     uint32_t* ent = S.lists.as<uint32_t>();
     uint32_t* ekey = ent + (size_t)W * TS;
     uint32_t* tot = ekey + (size_t)W * TS;
     uint4* P_first = S.partials.as<uint4>();
-    uint4* P_last = P_first + 8 * nchunks;
-    uint4* P_g1 = P_last + 8 * nchunks;
-    uint4* P_g2 = P_g1 + 8 * (ng1 + 1);
+    uint4* P_last = P_first + PARTIAL_U4 * nchunks;
+    uint4* P_g1 = P_last + PARTIAL_U4 * nchunks;
+    uint4* P_g2 = P_g1 + PARTIAL_U4 * (ng1 + 1);
 
     const uint32_t* lists_in = S.digits.as<const uint32_t>();
     if (shifted) {

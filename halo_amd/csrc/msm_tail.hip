@@ -30,8 +30,8 @@ __global__ __launch_bounds__(MSM_GROUP) void k_group_sums(const uint32_t* keys, 
     const uint32_t cnt = *count;
     const size_t e0 = (size_t)g * MSM_GROUP * span * K, e1 = e0 + (size_t)MSM_GROUP * span * K;
     if (e1 > cnt || keys[e0] != keys[e1 - 1]) return;  // not one bucket throughout: never used (uniform)
-    const XYZZ<F> v = wave_group_sum<F>(xyzz_load<F>(src + 8 * ((size_t)g * MSM_GROUP + i)), 64);
-    if (i == 0) xyzz_store(out + 8 * (size_t)g, v);
+    const XYZZ<F> v = wave_group_sum<F>(partial_load<F>(src + PARTIAL_U4 * ((size_t)g * MSM_GROUP + i)), 64);
+    if (i == 0) partial_store(out + PARTIAL_U4 * (size_t)g, v);
 }
 
 // Buckets that touch a chunk boundary (or are empty): bucket b's entries [s, e) lie in chunks
@@ -77,27 +77,27 @@ __global__ __launch_bounds__(256) void k_merge(const uint32_t* bstart, const uin
         auto next_src = [&]() -> const uint4* {
             const uint4* src;
             if (t % G2 == 0 && t + G2 <= tb) {
-                src = g2 + 8 * (size_t)(t / G2);
+                src = g2 + PARTIAL_U4 * (size_t)(t / G2);
                 t += G2;
             } else if (t % MSM_GROUP == 0 && t + MSM_GROUP <= tb) {
-                src = g1 + 8 * (size_t)(t / MSM_GROUP);
+                src = g1 + PARTIAL_U4 * (size_t)(t / MSM_GROUP);
                 t += MSM_GROUP;
             } else {
-                src = first + 8 * (size_t)t;
+                src = first + PARTIAL_U4 * (size_t)t;
                 t++;
             }
             return src;
         };
         // chunk t0's partial starts lane 0's sum (no addition to the identity); one addition per step,
         // so lanes that take different sources do not execute several inlined copies of it
-        if (j == 0) acc = xyzz_load<F>((starts ? first : last) + 8 * (size_t)t0);
-        else if (t <= tb) acc = xyzz_load<F>(next_src());
+        if (j == 0) acc = partial_load<F>((starts ? first : last) + PARTIAL_U4 * (size_t)t0);
+        else if (t <= tb) acc = partial_load<F>(next_src());
         if (t <= tb) {
-            XYZZ<F> nxt = xyzz_load<F>(next_src());
+            XYZZ<F> nxt = partial_load<F>(next_src());
             for (;;) {
                 const XYZZ<F> cur = nxt;
                 const bool more = t <= tb;
-                if (more) nxt = xyzz_load<F>(next_src());
+                if (more) nxt = partial_load<F>(next_src());
                 acc = xyzz_add(acc, cur);
                 if (!more) break;
             }

@@ -339,6 +339,19 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(RsIn in, const uint32
         }
     }
     __syncthreads();
+    // The first pass needs no stability (the second, by the high byte, must keep the first's order,
+    // but the order of equal full keys is free: k_acc's bucket sums do not depend on it), so it ranks
+    // with the wave-private run counter's returning LDS add -- one ds_add_rtn per entry instead of the
+    // eight-ballot match below (~40 VALU per round).
+    if constexpr (PASS0 || !std::is_void<SF>::value) {
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            if (!((validmask >> r) & 1u)) continue;
+            const uint32_t pos = atomicAdd(&wpos[wave][(K[r] >> in.shift) & 255u], 1u);
+            skey[pos] = K[r];
+            sval[pos] = V[r];
+        }
+    } else {
     // stable, wave-local ranking: 16 rounds of 64 consecutive entries
 #pragma unroll
     for (int r = 0; r < R; r++) {
@@ -360,6 +373,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(RsIn in, const uint32
         __builtin_amdgcn_wave_barrier();
         if (valid && below == 0) wpos[wave][dg] += (uint32_t)__popcll(same);
         __builtin_amdgcn_wave_barrier();
+    }
     }
     __syncthreads();
     // write runs: staging index i belongs to digit dg, global position goff[dg] + (i - lstart[dg])
