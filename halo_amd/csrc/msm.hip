@@ -985,11 +985,12 @@ int msm_srs_range_device(DeviceState* st, int curve, size_t offset, const void* 
 // sorted layout k_acc and the reduction tail take, with SW = len W windows of B buckets.  A batched
 // Horner (one lane per output) finishes.
 // ---------------------------------------------------------------------------------------------
-constexpr int BATCH_C_MAX = 8;  // window bits: at most 32 windows of 128 buckets
+constexpr int BATCH_C_MAX = 8;  // unshifted window bits: at most 32 windows of 128 buckets
+constexpr uint32_t BATCH_B_MAX = 256;  // buckets per window (shifted: two 8-bit sub-digit windows)
 
 __global__ __launch_bounds__(256) void k_batch_lists(const uint32_t* digits, uint32_t T, int W, uint32_t B,
                                                      uint32_t len, uint32_t* ent, uint32_t* ekey, uint32_t* tot) {
-    __shared__ uint32_t cnt[(1 << (BATCH_C_MAX - 1)) + 1];
+    __shared__ uint32_t cnt[BATCH_B_MAX + 1];
     __shared__ uint32_t base;
     const uint32_t tid = threadIdx.x;
     if (tid == 0) base = 0;
@@ -1042,18 +1043,25 @@ __global__ __launch_bounds__(256) void k_batch_expand(const uint32_t* ent, const
     vals[p] = (i + (ee & ((1u << tlog) - 1u)) * len + (ee >> tlog) * wstride) | (e & 0x80000000u);
 }
 
-// Shifted-SRS batches: the signed c_s-bit digit of (copy w, scalar u) -> three unsigned cb-bit
-// sub-digits of its magnitude, window q at sub[q][w T + u] (its sign carried along; DIGIT_NONE for 0)
+// Shifted-SRS batches: the signed c_s-bit digit of (copy w, scalar u) -> two unsigned sub-digits
+// lo + 2^cb hi of its magnitude (mag <= 2^(c_s - 1) <= 2^(2 cb)), window q at sub[q][w T + u] (its sign
+// carried along; DIGIT_NONE for 0).  Sub-digit values run 1 .. 2^cb (bucket v - 1 of B = 2^cb): the one
+// magnitude with hi = 2^cb, mag = 2^(2 cb), is written as hi = 2^cb - 1, lo = 2^cb.
+// (Round 4: two windows of 2^8 buckets instead of three of 2^6 -- a third fewer bucket additions, the
+// dominant cost of the IPA's switch to the tail rounds: 47M -> 31M at 2^20.)
 __global__ __launch_bounds__(256) void k_batch_subdigits(const uint32_t* digits, uint32_t TW, int cb, uint32_t* sub) {
     const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= TW) return;
     const uint32_t d = digits[e];
     const uint32_t mag = d == DIGIT_NONE ? 0u : (d & 0x7fffffffu) + 1u, sign = d & 0x80000000u;
-#pragma unroll
-    for (int q = 0; q < 3; q++) {
-        const uint32_t v = (mag >> (cb * q)) & ((1u << cb) - 1u);
-        sub[(size_t)q * TW + e] = v ? ((v - 1u) | sign) : DIGIT_NONE;
+    const uint32_t full = 1u << cb;
+    uint32_t lo = mag & (full - 1u), hi = mag >> cb;
+    if (hi == full) {
+        hi = full - 1u;
+        lo += full;
     }
+    sub[e] = lo ? ((lo - 1u) | sign) : DIGIT_NONE;
+    sub[(size_t)TW + e] = hi ? ((hi - 1u) | sign) : DIGIT_NONE;
 }
 
 template <class Cv>
@@ -1082,27 +1090,27 @@ template <class Cv>
 static int msm_shared_batch_t(DeviceState* st, const uint4* bases, const uint4* w_ark, size_t T, size_t len,
                               uint4* out, bool xyzz_out, BatchScratch& S, hipStream_t s, size_t shift_stride, int c_s) {
     if (!T || !len) return set_error(HALO_EINVAL, "msm_shared_batch: empty batch");
-    // shifted: the lists run over TS = W_s T (copy, scalar) entries with three sub-digit windows of
-    // cb bits and 2^cb buckets (magnitudes 1..2^(c_s-1) < 2^(3 cb))
+    // shifted: the lists run over TS = W_s T (copy, scalar) entries with two sub-digit windows of
+    // 2^cb buckets (magnitudes 1..2^(c_s-1) <= 2^(2 cb), k_batch_subdigits)
     const bool shifted = shift_stride && c_s && (T & (T - 1)) == 0 &&
                          (size_t)msm_windows(c_s) * shift_stride < (1ull << 31);
     const int W_s = shifted ? msm_windows(c_s) : 1;
-    const int cb = shifted ? (c_s + 2) / 3 : 0;
+    const int cb = shifted ? c_s / 2 : 0;
     // unshifted window bits: about T / 4 buckets per window, so that the per-window reduction
     // (2 B additions) stays below the accumulation (T mixed additions)
     const int c = shifted ? cb : std::max(5, std::min(BATCH_C_MAX, (int)ilog2(std::max<size_t>(T, 2)) - 1));
-    const int W = shifted ? 3 : msm_windows(c);
+    const int W = shifted ? 2 : msm_windows(c);
     const uint32_t B = shifted ? 1u << cb : 1u << (c - 1);
     const size_t TS = (size_t)W_s * T;
     const size_t SW = len * (size_t)W, NB = SW * B, E = SW * TS;
-    if (E >= (1ull << 32) || T * len >= (1ull << 31) || B > (1u << (BATCH_C_MAX - 1)))
+    if (E >= (1ull << 32) || T * len >= (1ull << 31) || B > BATCH_B_MAX)
         return set_error(HALO_EINVAL, "msm_shared_batch: batch too large (len %zu, T %zu)", len, T);
     const uint32_t L = std::min<uint32_t>(MSM_SEG_L, B), logL = ilog2(L), H = B / L, logH = ilog2(H);
     const uint32_t NT = 1 + logH + logL;
     const uint32_t K = msm_chunk_len(st, E, NB);
     const size_t nchunks = (E + K - 1) / K;
     const size_t ng1 = nchunks / MSM_GROUP, ng2 = nchunks / (MSM_GROUP * MSM_GROUP);
-    HALO_CHECK(S.digits.reserve((size_t)(shifted ? W_s + 3 : W) * TS * 4));
+    HALO_CHECK(S.digits.reserve((size_t)(shifted ? W_s + W : W) * TS * 4));
     HALO_CHECK(S.lists.reserve((size_t)W * TS * 8 + 16));
     HALO_CHECK(S.keys.reserve(E * 4));
     HALO_CHECK(S.vals.reserve(E * 4));

@@ -226,15 +226,17 @@ __global__ __launch_bounds__(64) void k_bitcombine(const uint4* terms, uint32_t 
 // window, lane k owns the G = B / 8 buckets [G k, G k + G): a running sum gives R = sum B_b and
 // S = sum (b - G k + 1) B_b over the segment (2 G additions), the lane adds G k R (lg G doublings
 // and a 3-bit multiple), and a 3-level tree over the 8 lanes gives sum_b (b + 1) B_b.
-constexpr uint32_t BATCH_SEGS = 8;
-template <class Cv>
+constexpr uint32_t BATCH_SEGS = 8;  // lanes per window up to 64 buckets; B / 8 above (8 buckets a lane)
+template <class Cv, uint32_t SEGS>
 __global__ __launch_bounds__(256) void k_batch_window_sums(const uint4* bucket_sums, uint32_t SW, uint32_t B,
                                                            uint4* window_sums) {
     using F = typename Cv::Base;
+    static_assert(SEGS >= 2 && SEGS <= 64 && (SEGS & (SEGS - 1)) == 0, "lanes per window");
+    constexpr int KBITS = __builtin_ctz(SEGS);
     const uint32_t tid = threadIdx.x;
     const size_t t = (size_t)blockIdx.x * blockDim.x + tid;
-    const uint32_t k = tid % BATCH_SEGS, G = B / BATCH_SEGS;
-    const size_t w = t / BATCH_SEGS;
+    const uint32_t k = tid % SEGS, G = B / SEGS;
+    const size_t w = t / SEGS;
     XYZZ<F> v = xyzz_id<F>();
     if (w < SW) {
         const uint4* bs = bucket_sums + 8 * (w * B + (size_t)k * G);
@@ -247,7 +249,7 @@ __global__ __launch_bounds__(256) void k_batch_window_sums(const uint4* bucket_s
             XYZZ<F> X = R;
             for (uint32_t g = G; g > 1; g >>= 1) X = xyzz_dbl(X);  // G R
             XYZZ<F> Y = xyzz_id<F>();
-            for (int bit = 2; bit >= 0; bit--) {
+            for (int bit = KBITS - 1; bit >= 0; bit--) {
                 Y = xyzz_dbl(Y);
                 if ((k >> bit) & 1u) Y = xyzz_add(Y, X);
             }
@@ -255,7 +257,7 @@ __global__ __launch_bounds__(256) void k_batch_window_sums(const uint4* bucket_s
         }
         v = S;
     }
-    v = wave_group_sum<F>(v, BATCH_SEGS);
+    v = wave_group_sum<F>(v, SEGS);
     if (k == 0 && w < SW) xyzz_store(window_sums + 8 * w, v);
 }
 
@@ -311,9 +313,13 @@ static int tail_launch_t(const MsmTailArgs& a, hipStream_t ts) {
                            (const uint4*)a.g1, (const uint4*)a.g2, a.bucket_sums);
         if (a.batch_windows) {
             const uint32_t B = a.L * a.H;
-            if (B < 2 * BATCH_SEGS || B > 1024 || (B & (B - 1)))
+            if (B < 2 * BATCH_SEGS || B > 512 || (B & (B - 1)))
                 return set_error(HALO_EINVAL, "batched window sums: %u buckets per window", B);
-            hipLaunchKernelGGL(k_batch_window_sums<Cv>, dim3(grid_for_t((size_t)a.SW * BATCH_SEGS, 256)), dim3(256), 0, ts,
+            // lanes per window: 8, or 8 buckets per lane above 64 buckets
+            const uint32_t segs = std::max(BATCH_SEGS, B / 8);
+            auto kws = segs == 8 ? k_batch_window_sums<Cv, 8> : segs == 16 ? k_batch_window_sums<Cv, 16>
+                     : segs == 32 ? k_batch_window_sums<Cv, 32> : k_batch_window_sums<Cv, 64>;
+            hipLaunchKernelGGL(kws, dim3(grid_for_t((size_t)a.SW * segs, 256)), dim3(256), 0, ts,
                                (const uint4*)a.bucket_sums, (uint32_t)a.SW, B, a.window_sums);
             HALO_HIP(hipGetLastError());
             return HALO_OK;
