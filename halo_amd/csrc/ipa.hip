@@ -881,6 +881,75 @@ __global__ __launch_bounds__(256) void k_weighted_scalars(const uint4* cs, const
     fe_to_ark(sr + 2 * j, fe_mul(fe_from_ark<S>(cs + 2 * i), wu));
 }
 
+// A weighted round's preparation in one launch (was five: two dot products of two kernels each, the
+// xi_0 scaling and k_weighted_scalars): the weighted scalars of both sides (when sl is non-null: w has
+// more than one entry), and the two dots <c_r, z_l>, <c_l, z_r> as block partials whose last arriving
+// block (release / acquire on *ctr, reset by it) sums them, canonicalises, scales by xi_0 (xi0_ark
+// non-null) and writes dots_ark[0..2).  Same products and sums as k_dot_partial /
+// k_sum_partials_to_ark / k_scale_ark, so the results are identical.  part: 2 x gridDim.x elements.
+template <class S>
+__global__ __launch_bounds__(256) void k_weighted_prep(const uint4* cs, const uint4* zs, const uint4* w, size_t m,
+                                                       int lgm, size_t total, uint4* sl, uint4* sr, uint4* part,
+                                                       uint32_t* ctr, const uint4* xi0_ark, uint4* dots_ark) {
+    __shared__ uint4 red[256 * 4];
+    __shared__ uint32_t flag;
+    const uint32_t tid = threadIdx.x;
+    const size_t j0 = (size_t)blockIdx.x * 256 + tid, stride = (size_t)gridDim.x * 256;
+    // (grid-stride: the host caps the grid -- every block's arrival is one add on the same counter)
+    if (sl)
+        for (size_t j = j0; j < total; j += stride) {
+            const size_t u = j >> lgm, i = j & (m - 1);
+            const Fe<S> wu = fe_from_ark<S>(w + 2 * u);
+            fe_to_ark(sl + 2 * j, fe_mul(fe_from_ark<S>(cs + 2 * (m + i)), wu));
+            fe_to_ark(sr + 2 * j, fe_mul(fe_from_ark<S>(cs + 2 * i), wu));
+        }
+    Fe<S> a = fe_zero<S>(), b = fe_zero<S>();
+    for (size_t i = j0; i < m; i += stride) {
+        a = fe_add(a, fe_mul(fe_load<S>(cs + 2 * (m + i)), fe_from_ark<S>(zs + 2 * i)));
+        b = fe_add(b, fe_mul(fe_load<S>(cs + 2 * i), fe_from_ark<S>(zs + 2 * (m + i))));
+    }
+    auto block_sum2 = [&](Fe<S>& x, Fe<S>& y) {
+        fe_store(red + 4 * tid, x);
+        fe_store(red + 4 * tid + 2, y);
+        __syncthreads();
+        for (uint32_t off = 128; off > 0; off >>= 1) {
+            if (tid < off) {
+                fe_store(red + 4 * tid, fe_add(fe_load<S>(red + 4 * tid), fe_load<S>(red + 4 * (tid + off))));
+                fe_store(red + 4 * tid + 2, fe_add(fe_load<S>(red + 4 * tid + 2), fe_load<S>(red + 4 * (tid + off) + 2)));
+            }
+            __syncthreads();
+        }
+        x = fe_load<S>(red);
+        y = fe_load<S>(red + 2);
+    };
+    block_sum2(a, b);
+    if (tid == 0) {
+        tail_publish_fe((uint32_t*)(part + 4 * (size_t)blockIdx.x), a);
+        tail_publish_fe((uint32_t*)(part + 4 * (size_t)blockIdx.x + 2), b);
+    }
+    if (!tail_arrive(ctr, gridDim.x, &flag)) return;
+    a = fe_zero<S>();
+    b = fe_zero<S>();
+    for (uint32_t q = tid; q < gridDim.x; q += 256) {
+        a = fe_add(a, fe_load<S>(part + 4 * (size_t)q));
+        b = fe_add(b, fe_load<S>(part + 4 * (size_t)q + 2));
+    }
+    __syncthreads();  // (red is reused)
+    block_sum2(a, b);
+    if (tid != 0) return;
+    *ctr = 0u;
+    Fe<S> d[2] = {fe_canon(fe_reduce_2p(a)), fe_canon(fe_reduce_2p(b))};
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        if (xi0_ark) {
+            fe_store(dots_ark + 2 * k, d[k]);  // (ark words, as k_sum_partials_to_ark leaves them)
+            fe_to_ark(dots_ark + 2 * k, fe_mul(fe_from_ark<S>(dots_ark + 2 * k), fe_from_ark<S>(xi0_ark)));
+        } else {
+            fe_store(dots_ark + 2 * k, d[k]);
+        }
+    }
+}
+
 }  // namespace halo
 
 using namespace halo;
@@ -1301,7 +1370,7 @@ constexpr size_t SM_BYTES = 2048;
 constexpr size_t SM_WBAR = 1024, SM_ALPHA = 1056, SM_W = 1088, SM_WP = 1120, SM_C = 1152, SM_CBAR = 1216, SM_S = 1280,
                  SM_CP = 1344, SM_NEGW = 1408, SM_T = 1536, SM_EVAL = 1664, SM_V = 1696,  // SM_T: 128 B XYZZ
                  SM_HKW = 1728,  // 2 x 10 words: the dots' GLV splits (k_tail_digits -> k_tail_round)
-                 SM_CTR = 1856;  // 2 x u32 arrival counters of k_tail_round (zero between launches)
+                 SM_CTR = 1856;  // 2 x u32 arrival counters of k_tail_round, 1 of k_weighted_prep (zero between launches)
 
 // Phase 1 of a session: G (resident SRS prefix, or explicit gs_host), c (cs_len coefficients, host or
 // device (ordered on the null stream), zero-padded to n), z = powers of z (or explicit zs_host) on the
@@ -1341,8 +1410,9 @@ static int ipa_setup(DeviceState* st, halo_ipa_session* ses, int curve, size_t n
     HALO_CHECK(ses->cs.reserve(n * 32));
     HALO_CHECK(ses->zs.reserve(n * 32));
     HALO_CHECK(ses->small.reserve(SM_BYTES));
-    HALO_HIP(hipMemsetAsync(ses->small.as<char>() + SM_CTR, 0, 8, s));  // k_tail_round's counters
-    HALO_CHECK(ses->tmp.reserve(std::max<size_t>(4096 * 32, gs_host ? n * 64 : 0)));
+    HALO_HIP(hipMemsetAsync(ses->small.as<char>() + SM_CTR, 0, 12, s));  // k_tail_round's / k_weighted_prep's counters
+    // (n / 4: k_weighted_prep's block partials, 64 B per 256 terms of a side)
+    HALO_CHECK(ses->tmp.reserve(std::max<size_t>({4096 * 32, gs_host ? n * 64 : 0, n / 4})));
     if (gs_host) {
         HALO_CHECK(copy_h2d(ses->tmp.ptr, gs_host, n * 64, s));
         HALO_CHECK(convert_wrapped_to_internal(curve, ses->tmp.ptr, ses->gs.ptr, n, s));
@@ -1892,35 +1962,32 @@ static int ipa_round_launch(DeviceState* st, halo_ipa_session* ses) {
         HALO_CHECK(ipa_tail_sums(ses, 0, s));
         return ipa_copy_out(ses);
     }
-    HALO_CHECK(dot_device(sf, cs + m * 32, zs, m, sm + 128, ses->tmp.ptr, s));        // <c_r, z_l>
-    HALO_CHECK(dot_device(sf, cs, zs + m * 32, m, sm + 160, ses->tmp.ptr, s));        // <c_l, z_r>
-    if (ses->xi_mode) {  // dot H' = (dot xi_0) H
-        DISPATCH_CURVE(ses->curve, Cv, {
-            hipLaunchKernelGGL(k_scale_ark<typename Cv::Scalar>, dim3(1), dim3(64), 0, s, (uint4*)(sm + 128), 2,
-                               (const uint4*)(sm + 192));
-        });
-        HALO_HIP(hipGetLastError());
-    }
     if (ses->weighted) {
+        // the round's weighted scalars and its two dots (scaled by xi_0) in one launch
         const size_t half = ses->n0 / 2;  // = wlen * m terms per side
         const uint32_t lgm = ilog2(m);
         const char* sl = cs + m * 32;     // round 0 (w = [1]): the scalars are c_r, c_l themselves
         const char* sr = cs;
+        char* sb = (char*)ses->scal.ptr;
+        const unsigned nbk = std::min(gridn(half, 256), 256u);
+        HALO_CHECK(ses->tmp.reserve((size_t)nbk * 64));
+        DISPATCH_CURVE(ses->curve, Cv, {
+            hipLaunchKernelGGL(k_weighted_prep<typename Cv::Scalar>, dim3(nbk), dim3(256), 0, s, (const uint4*)cs,
+                               (const uint4*)zs, ses->w[ses->wcur].as<const uint4>(), m, (int)lgm, half,
+                               ses->wlen > 1 ? (uint4*)sb : nullptr, (uint4*)(sb + half * 32), ses->tmp.as<uint4>(),
+                               (uint32_t*)(sm + SM_CTR + 8), ses->xi_mode ? (const uint4*)(sm + 192) : nullptr,
+                               (uint4*)(sm + 128));
+        });
+        HALO_HIP(hipGetLastError());
         if (ses->wlen > 1) {
-            char* sb = (char*)ses->scal.ptr;
-            DISPATCH_CURVE(ses->curve, Cv, {
-                hipLaunchKernelGGL(k_weighted_scalars<typename Cv::Scalar>, dim3(gridn(half, 256)), dim3(256), 0, s,
-                                   (const uint4*)cs, ses->w[ses->wcur].as<const uint4>(), m, (int)lgm, half, (uint4*)sb,
-                                   (uint4*)(sb + half * 32));
-            });
-            HALO_HIP(hipGetLastError());
             sl = sb;
             sr = sb + half * 32;
         }
         // L and R as one MSM (key = (side, bucket)) while the round is latency-bound; at 2^19 terms per
         // side two MSMs win (R's front and accumulation overlap L's reduction tail).  Measured, opening
         // 2^14 / 2^17 / 2^18 / 2^19 / 2^20 ms, two MSMs vs one: 7.5 / 11.3 / 14.4 / 19.3 / 27.2 vs
-        // 6.9 / 10.3 / 13.2 / 17.8 / 29.0
+        // 6.9 / 10.3 / 13.2 / 17.8 / 29.0 (round 4, after the sort and accumulation changes: 2^20
+        // 21.7 vs 22.7 ms)
         if (half <= IPA_PAIR_MAX) {
             const MsmPairIO io{sl, sr, sm + 128, sm + 160, sm + 512, sm + 640};
             HALO_CHECK(msm_srs_pairs_device(st, ses->curve, 1, &io, half, lgm, ses->htab_ptr, s, hr));
@@ -1931,7 +1998,18 @@ static int ipa_round_launch(DeviceState* st, halo_ipa_session* ses) {
                                             lgm, true, true, hr));
         }
         HALO_CHECK(msm_join(st, s));
-    } else {
+        return ipa_copy_out(ses);
+    }
+    HALO_CHECK(dot_device(sf, cs + m * 32, zs, m, sm + 128, ses->tmp.ptr, s));        // <c_r, z_l>
+    HALO_CHECK(dot_device(sf, cs, zs + m * 32, m, sm + 160, ses->tmp.ptr, s));        // <c_l, z_r>
+    if (ses->xi_mode) {  // dot H' = (dot xi_0) H
+        DISPATCH_CURVE(ses->curve, Cv, {
+            hipLaunchKernelGGL(k_scale_ark<typename Cv::Scalar>, dim3(1), dim3(64), 0, s, (uint4*)(sm + 128), 2,
+                               (const uint4*)(sm + 192));
+        });
+        HALO_HIP(hipGetLastError());
+    }
+    {
         // L and R are independent: the second MSM's accumulation overlaps the first one's tail
         if (ses->srs_round0) {  // G_l = SRS[0, m), G_r = SRS[m, 2m): resident window-shifted copies, no Horner
             HALO_CHECK(msm_srs_range_device(st, ses->curve, 0, cs + m * 32, m, ses->htab_ptr, sm + 128, sm + 512, s, true,

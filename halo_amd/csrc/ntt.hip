@@ -132,7 +132,9 @@ HALO_DEV Fe<C> fe_reduce_q(const Fe<C>& x) {
 // (< 2p except raw ark words), stage 0 doubles that bound, every later stage adds at most 2p
 // (u + t and u - t + 2p with t = v w < 2p), so after 8 stages they are < 22p: still valid
 // Montgomery inputs (< 64p), reduced once at the end of the pass (fe_reduce_q, < 32p).
-template <class F, int EPT, int LG>
+// K0ZERO: k0 == 0 (the pass's first group, from the global loads): the butterflies with k = 0 have
+// twiddle omega^0 = 1 and skip their multiplication (stage 1: one of the thread's two)
+template <class F, int EPT, int LG, bool K0ZERO = false>
 HALO_DEV void ntt_group(Fe<F> (&v)[EPT], uint32_t s, uint32_t G, uint32_t k0, const uint4* twg) {
 #pragma unroll
     for (int g = 0; g < LG; g++) {
@@ -143,12 +145,15 @@ HALO_DEV void ntt_group(Fe<F> (&v)[EPT], uint32_t s, uint32_t G, uint32_t k0, co
             if (m & (1 << g)) continue;
             const int m2 = m + (1 << g);
             Fe<F> t = v[m2];
-            if (sp != 0) {
+            const bool unit = K0ZERO && sp != 0 && (m & ((1 << g) - 1)) == 0;
+            if (sp != 0 && !unit) {
                 const uint32_t k = k0 + ((uint32_t)(m & ((1 << g) - 1)) << s);
                 t = fe_mul(t, fe_load<F>(twg + 2 * ((1u << sp) - 1u + k)));
             }
-            // stage 0 (no multiplication): t is a pass input, < 4p even for non-canonical ark words
-            v[m2] = (sp == 0) ? fe_sub_k<4>(v[m], t) : fe_sub_k<2>(v[m], t);
+            // stage 0 (no multiplication): t is a pass input, < 4p even for non-canonical ark words;
+            // a unit-twiddle butterfly at stage 1 takes t < 8p unmultiplied (its sums < 16p, so after
+            // 8 stages the bound is 28p instead of 22p: still < 32p for fe_reduce_q)
+            v[m2] = (sp == 0) ? fe_sub_k<4>(v[m], t) : unit ? fe_sub_k<8>(v[m], t) : fe_sub_k<2>(v[m], t);
             v[m] = fe_norm(fe_add_nc(v[m], t));
         }
     }
@@ -321,7 +326,7 @@ __global__ __launch_bounds__(NE / EPT) void k_ntt_pass(NttPassArgs a) {
     }
     // on the wide blocks the short group goes first (r mod LG stages), so later groups stay in range
     const uint32_t G0 = (NE >= NTT_E_BIG && (r % LG)) ? r % LG : (r < (uint32_t)LG ? r : (uint32_t)LG);
-    if (!a.prune) ntt_group<F, EPT, LG>(v, 0, G0, 0, a.stage_tw);  // (pruned: host guarantees prune >= G0)
+    if (!a.prune) ntt_group<F, EPT, LG, true>(v, 0, G0, 0, a.stage_tw);  // (pruned: host guarantees prune >= G0)
     {
         const uint32_t pb = ntt_swz<NE>(base);
 #pragma unroll
