@@ -18,6 +18,8 @@
 #include <cstring>
 #include <vector>
 
+#include <chrono>
+
 #include "dispatch.hpp"
 #include "glv.hpp"
 #include "msm.hpp"
@@ -488,6 +490,25 @@ HALO_DEV XYZZ<typename Cv::Base> hiding_lane_term(const uint4* htab, const uint4
     return acc;
 }
 
+// A tail round's side sum straight into the session's pinned staging (coherent host memory): 32
+// words with system-scope stores, then the side's flag = seq with a system-scope release.  The host
+// polls the two flags instead of a D2H copy plus a stream synchronisation (round 3 measurement,
+// tools/micro/sync_bench.hip: 5.8 vs 11 us per host round trip).  host: L at [0, 32), R at [32, 64)
+// words; flags[0..2).
+template <class F>
+HALO_DEV void tail_emit_host(uint32_t* host, uint32_t* flags, uint32_t sd, const XYZZ<F>& v, uint32_t seq) {
+    const Fe<F>* c[4] = {&v.X, &v.Y, &v.ZZ, &v.ZZZ};
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        uint32_t w[8];
+        fe_pack(*c[k], w);
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+            __hip_atomic_store(host + 32 * sd + 8 * k + i, w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    __hip_atomic_store(flags + sd, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // Block partial sums part[block][side].  mode 0 (L and R of a round, 2m = len): the first nbs blocks
 // take side 0's terms, the rest side 1's (each block one side: one tree, not two); the term q of a
 // side is (win, u, j) = window, fold weight, j < m, at point k = j + u 2m + side m.  mode 1 (U): terms
@@ -500,7 +521,8 @@ template <class Cv>
 __global__ __launch_bounds__(TAIL_THREADS) void k_tail_msm(const uint4* table, size_t ld, const uint32_t* scal,
                                                             const uint8_t* side, size_t n0, size_t m, int mode, uint32_t nbs,
                                                             uint4* part, const uint4* htab, const uint4* dots_ark,
-                                                            const uint32_t* hkw, uint4* out_xyzz) {
+                                                            const uint32_t* hkw, uint4* out_xyzz,
+                                                            uint32_t* host = nullptr, uint32_t seq = 0) {
     using F = typename Cv::Base;
     __shared__ uint4 red[TAIL_THREADS / 2 * 8];
     __shared__ uint32_t kw[10];
@@ -539,7 +561,10 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail_msm(const uint4* table, s
     }
     acc = block_group_sum<F>(acc, TAIL_THREADS, red);
     if (out_xyzz && nbs == 1) {
-        if (tid == 0) xyzz_store(out_xyzz + 8 * bsd, acc);
+        if (tid == 0) {
+            xyzz_store(out_xyzz + 8 * bsd, acc);
+            if (host) tail_emit_host(host, host + 64, bsd, acc, seq);
+        }
     } else if (tid == 0) {
         xyzz_store(part + 8 * (2 * (size_t)blockIdx.x + sd), acc);
         xyzz_store(part + 8 * (2 * (size_t)blockIdx.x + (sd ^ 1)), xyzz_id<F>());
@@ -570,6 +595,8 @@ struct TailRoundArgs {
     uint4* part;               // [2][nbs + 1] XYZZ partials
     uint32_t* ctr;             // [2] arrival counters (zero between launches)
     uint4* out_xyzz;           // [2] L, R
+    uint32_t* host;            // the session's pinned L | R staging (tail_emit_host) or null
+    uint32_t seq;              // this round's flag value
 };
 
 // n0 up to this: one launch per round (k_tail_round, scalars formed in the points' waves); above it the
@@ -626,6 +653,7 @@ HALO_DEV void tail_side_final(const TailRoundArgs& a, uint32_t sd, uint4* red) {
     acc = block_group_sum<F>(acc, TAIL_THREADS, red);
     if (tid == 0) {
         xyzz_store(a.out_xyzz + 8 * sd, acc);
+        if (a.host) tail_emit_host(a.host, a.host + 64, sd, acc, a.seq);
         __hip_atomic_store(a.ctr + sd, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
@@ -791,7 +819,8 @@ __global__ __launch_bounds__(TAIL_THREADS, 1) void k_tail_round(const TailRoundA
 template <class Cv>
 __global__ __launch_bounds__(TAIL_THREADS) void k_tail_final(const uint4* part, int nblk, const uint4* htab,
                                                               const uint4* dots_ark, uint4* out_wrapped,
-                                                              int xyzz_out) {
+                                                              int xyzz_out, uint32_t* host = nullptr,
+                                                              uint32_t seq = 0) {
     using F = typename Cv::Base;
     using S = typename Cv::Scalar;
     __shared__ uint4 red[TAIL_THREADS / 2 * 8];
@@ -826,10 +855,12 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail_final(const uint4* part, 
         acc = xyzz_add(acc, xyzz_load<F>(part + 8 * (2 * (size_t)(b * per_side + j) + b)));
     acc = block_group_sum<F>(acc, TAIL_THREADS, red);
     if (tid == 0) {
-        if (xyzz_out)  // 128 B per side, converted on the host (host_xyzz_to_wrapped)
+        if (xyzz_out) {  // 128 B per side, converted on the host (host_xyzz_to_wrapped)
             xyzz_store(out_wrapped + 8 * b, acc);
-        else
+            if (host) tail_emit_host(host, host + 64, b, acc, seq);
+        } else {
             aff_to_wrapped(out_wrapped + 4 * b, xyzz_to_aff(acc));
+        }
     }
 }
 
@@ -886,25 +917,29 @@ __global__ __launch_bounds__(256) void k_weighted_scalars(const uint4* cs, const
 // more than one entry), and the two dots <c_r, z_l>, <c_l, z_r> as block partials whose last arriving
 // block (release / acquire on *ctr, reset by it) sums them, canonicalises, scales by xi_0 (xi0_ark
 // non-null) and writes dots_ark[0..2).  Same products and sums as k_dot_partial /
-// k_sum_partials_to_ark / k_scale_ark, so the results are identical.  part: 2 x gridDim.x elements.
+// k_sum_partials_to_ark / k_scale_ark, so the results are identical.  part: 2 x ndot elements
+// (ndot <= gridDim.x blocks carry the dots).
 template <class S>
 __global__ __launch_bounds__(256) void k_weighted_prep(const uint4* cs, const uint4* zs, const uint4* w, size_t m,
                                                        int lgm, size_t total, uint4* sl, uint4* sr, uint4* part,
-                                                       uint32_t* ctr, const uint4* xi0_ark, uint4* dots_ark) {
+                                                       uint32_t* ctr, const uint4* xi0_ark, uint4* dots_ark,
+                                                       uint32_t ndot) {
     __shared__ uint4 red[256 * 4];
     __shared__ uint32_t flag;
     const uint32_t tid = threadIdx.x;
-    const size_t j0 = (size_t)blockIdx.x * 256 + tid, stride = (size_t)gridDim.x * 256;
-    // (grid-stride: the host caps the grid -- every block's arrival is one add on the same counter)
-    if (sl)
-        for (size_t j = j0; j < total; j += stride) {
-            const size_t u = j >> lgm, i = j & (m - 1);
-            const Fe<S> wu = fe_from_ark<S>(w + 2 * u);
-            fe_to_ark(sl + 2 * j, fe_mul(fe_from_ark<S>(cs + 2 * (m + i)), wu));
-            fe_to_ark(sr + 2 * j, fe_mul(fe_from_ark<S>(cs + 2 * i), wu));
-        }
+    const size_t j = (size_t)blockIdx.x * 256 + tid;
+    if (sl && j < total) {
+        const size_t u = j >> lgm, i = j & (m - 1);
+        const Fe<S> wu = fe_from_ark<S>(w + 2 * u);
+        fe_to_ark(sl + 2 * j, fe_mul(fe_from_ark<S>(cs + 2 * (m + i)), wu));
+        fe_to_ark(sr + 2 * j, fe_mul(fe_from_ark<S>(cs + 2 * i), wu));
+    }
+    // the dots: the first ndot blocks only (grid-stride over m), so that at most ndot arrivals meet on
+    // the one counter (2048 same-address adds cost more than the launches they replace)
+    if (blockIdx.x >= ndot) return;
+    const size_t stride = (size_t)ndot * 256;
     Fe<S> a = fe_zero<S>(), b = fe_zero<S>();
-    for (size_t i = j0; i < m; i += stride) {
+    for (size_t i = j; i < m; i += stride) {
         a = fe_add(a, fe_mul(fe_load<S>(cs + 2 * (m + i)), fe_from_ark<S>(zs + 2 * i)));
         b = fe_add(b, fe_mul(fe_load<S>(cs + 2 * i), fe_from_ark<S>(zs + 2 * (m + i))));
     }
@@ -927,10 +962,10 @@ __global__ __launch_bounds__(256) void k_weighted_prep(const uint4* cs, const ui
         tail_publish_fe((uint32_t*)(part + 4 * (size_t)blockIdx.x), a);
         tail_publish_fe((uint32_t*)(part + 4 * (size_t)blockIdx.x + 2), b);
     }
-    if (!tail_arrive(ctr, gridDim.x, &flag)) return;
+    if (!tail_arrive(ctr, ndot, &flag)) return;
     a = fe_zero<S>();
     b = fe_zero<S>();
-    for (uint32_t q = tid; q < gridDim.x; q += 256) {
+    for (uint32_t q = tid; q < ndot; q += 256) {
         a = fe_add(a, fe_load<S>(part + 4 * (size_t)q));
         b = fe_add(b, fe_load<S>(part + 4 * (size_t)q + 2));
     }
@@ -963,7 +998,10 @@ struct halo_ipa_session {
     int device = -1;
     hipStream_t s = nullptr;
     hipEvent_t htab_ready = nullptr;  // recorded after the session's own 2^i H' table
-    uint8_t* pinned = nullptr;  // [128, 192) xi|xi_inv (H2D), [256, 512) L|R XYZZ (D2H): async, several sessions in flight
+    uint8_t* pinned = nullptr;  // [128, 192) xi|xi_inv (H2D), [256, 512) L|R XYZZ (D2H or tail_emit_host),
+                                // [512, 520) the L / R flags of tail_emit_host: coherent, several sessions in flight
+    uint32_t poll_seq = 0;      // the last tail round's flag value (monotonic over the session object's life)
+    bool poll_pending = false;  // the last round emits L / R to `pinned` itself: poll instead of synchronising
     DevBuf gs, cs, zs, htab, small, tmp, pbar;
     DevBuf cs2, zs2;  // ping-pong partners of cs / zs (tail rounds with a deferred fold)
     DevBuf own_table, w[2], scal, side, part;
@@ -1065,7 +1103,7 @@ halo_ipa_session* ipa_acquire(DeviceState* st) {
     // round; the prover's and pcdl::open's sessions use the resident 2^i H tables and build none)
     if (hipStreamCreateWithFlags(&ses->s, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&ses->htab_ready, hipEventDisableTiming) != hipSuccess ||
-        hipHostMalloc((void**)&ses->pinned, 512, hipHostMallocDefault) != hipSuccess) {
+        hipHostMalloc((void**)&ses->pinned, 1024, hipHostMallocCoherent) != hipSuccess) {
         ses->destroy();
         delete ses;
         set_error(HALO_EDEVICE, "halo_ipa_begin: stream / pinned buffer allocation failed");
@@ -1801,6 +1839,10 @@ static int ipa_tail_sums(halo_ipa_session* ses, int mode, hipStream_t s) {
         ra.part = ses->part.as<uint4>();
         ra.ctr = (uint32_t*)(sm + SM_CTR);
         ra.out_xyzz = (uint4*)(sm + 512);
+        ra.host = (uint32_t*)(ses->pinned + 256);
+        ra.seq = ++ses->poll_seq;
+        if (ra.seq == 0) ra.seq = ++ses->poll_seq;  // (0 is the flags' initial value)
+        ses->poll_pending = true;
         if (n0 <= TAIL_FUSE_N) {
             DISPATCH_CURVE(ses->curve, Cv, {
                 hipLaunchKernelGGL(k_tail_round<Cv>, dim3(2 * ra.nbs + 2), dim3(TAIL_THREADS), 0, s, ra, f);
@@ -1815,10 +1857,11 @@ static int ipa_tail_sums(halo_ipa_session* ses, int mode, hipStream_t s) {
                 hipLaunchKernelGGL(k_tail_msm<Cv>, dim3((unsigned)nblk), dim3(TAIL_THREADS), 0, s, ses->table, ses->table_ld,
                                    ses->scal.as<const uint32_t>(), ses->side.as<const uint8_t>(), n0, m, 0, (uint32_t)nbs,
                                    ses->part.as<uint4>(), (const uint4*)ses->htab_ptr, (const uint4*)(sm + 128),
-                                   (const uint32_t*)(sm + SM_HKW), (uint4*)(sm + 512));
+                                   (const uint32_t*)(sm + SM_HKW), (uint4*)(sm + 512), ra.host, ra.seq);
                 if (nbs > 1)
                     hipLaunchKernelGGL(k_tail_final<Cv>, dim3(2), dim3(TAIL_THREADS), 0, s, ses->part.as<const uint4>(),
-                                       (int)nblk, (const uint4*)nullptr, (const uint4*)nullptr, (uint4*)(sm + 512), 1);
+                                       (int)nblk, (const uint4*)nullptr, (const uint4*)nullptr, (uint4*)(sm + 512), 1,
+                                       ra.host, ra.seq);
             });
         }
         HALO_HIP(hipGetLastError());
@@ -1959,8 +2002,8 @@ static int ipa_round_launch(DeviceState* st, halo_ipa_session* ses) {
     ses->htab_waited = true;
     if (ses->tail) {  // k_tail_prep forms the dots (scaled by xi_0) with the round's scalars
         if (hr) HALO_HIP(hipStreamWaitEvent(s, hr, 0));
-        HALO_CHECK(ipa_tail_sums(ses, 0, s));
-        return ipa_copy_out(ses);
+        HALO_CHECK(ipa_tail_sums(ses, 0, s));  // (L and R reach `pinned` from the kernels: no copy)
+        return HALO_OK;
     }
     if (ses->weighted) {
         // the round's weighted scalars and its two dots (scaled by xi_0) in one launch
@@ -1969,14 +2012,14 @@ static int ipa_round_launch(DeviceState* st, halo_ipa_session* ses) {
         const char* sl = cs + m * 32;     // round 0 (w = [1]): the scalars are c_r, c_l themselves
         const char* sr = cs;
         char* sb = (char*)ses->scal.ptr;
-        const unsigned nbk = std::min(gridn(half, 256), 256u);
-        HALO_CHECK(ses->tmp.reserve((size_t)nbk * 64));
+        const unsigned nbk = gridn(half, 256), ndot = std::min(nbk, 256u);
+        HALO_CHECK(ses->tmp.reserve((size_t)ndot * 64));
         DISPATCH_CURVE(ses->curve, Cv, {
             hipLaunchKernelGGL(k_weighted_prep<typename Cv::Scalar>, dim3(nbk), dim3(256), 0, s, (const uint4*)cs,
                                (const uint4*)zs, ses->w[ses->wcur].as<const uint4>(), m, (int)lgm, half,
                                ses->wlen > 1 ? (uint4*)sb : nullptr, (uint4*)(sb + half * 32), ses->tmp.as<uint4>(),
                                (uint32_t*)(sm + SM_CTR + 8), ses->xi_mode ? (const uint4*)(sm + 192) : nullptr,
-                               (uint4*)(sm + 128));
+                               (uint4*)(sm + 128), ndot);
         });
         HALO_HIP(hipGetLastError());
         if (ses->wlen > 1) {
@@ -2093,6 +2136,24 @@ static int ipa_fold_now(DeviceState* st, halo_ipa_session* ses, const halo_fe_t*
     return HALO_OK;
 }
 
+// Waits for a tail round's L and R in `pinned` (tail_emit_host): spins on the two flags; after 2 s
+// (a failed or very late launch) it synchronises the stream, which reports a launch error, and takes
+// L, R from the device copy instead.
+static int ipa_poll_lr(halo_ipa_session* ses) {
+    ses->poll_pending = false;
+    const volatile uint32_t* fl = (const volatile uint32_t*)(ses->pinned + 512);
+    const uint32_t seq = ses->poll_seq;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 0;; spin++) {
+        if (__atomic_load_n(&fl[0], __ATOMIC_ACQUIRE) == seq && __atomic_load_n(&fl[1], __ATOMIC_ACQUIRE) == seq)
+            return HALO_OK;
+        if ((spin & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) break;
+    }
+    HALO_HIP(hipStreamSynchronize(ses->s));
+    HALO_HIP(hipMemcpy(ses->pinned + 256, (char*)ses->small.ptr + 512, 256, hipMemcpyDeviceToHost));
+    return HALO_OK;
+}
+
 extern "C" int halo_ipa_round_lr(halo_ipa_session* ses, halo_wrapped_point_t* L, halo_wrapped_point_t* R) {
     clear_error();
     if (!ses || !L || !R) return set_error(HALO_EINVAL, "halo_ipa_round_lr: null argument");
@@ -2113,8 +2174,12 @@ extern "C" int halo_ipa_round_lr_multi(halo_ipa_session* const* ses, size_t k, h
         HALO_CHECK(ipa_round_launch(st, ses[i]));
     }
     for (size_t i = 0; i < k; i++) {
-        HALO_HIP(hipStreamSynchronize(ses[i]->s));
-        ses[i]->fold_inflight = false;
+        if (ses[i]->poll_pending) {
+            HALO_CHECK(ipa_poll_lr(ses[i]));
+        } else {
+            HALO_HIP(hipStreamSynchronize(ses[i]->s));
+            ses[i]->fold_inflight = false;
+        }
         const void* src[2] = {ses[i]->pinned + 256, ses[i]->pinned + 384};
         void* dst[2] = {&L[i], &R[i]};
         host_xyzz_to_wrapped2(ses[i]->curve, src, dst, 2);
