@@ -89,3 +89,18 @@ def test_tuning_keys_roundtrip_and_reject_unknown(lib_path):
         assert H.get_tuning(k) == v
     with pytest.raises(H.HaloError):
         H.set_tuning("no_such_key", 1)
+
+
+def test_library_reads_no_environment():
+    """The product library's path selections are the tuning ABI, not environment variables (VERDICT
+    r03 item 7): no getenv / secure_getenv in the sources of libhalo_gpu.so (the Python mirror's
+    HALO_LIB, used by A/B tools to pick a build, is outside the library)."""
+    import glob
+    here = os.path.dirname(os.path.abspath(__file__))
+    srcs = glob.glob(os.path.join(here, "..", "halo_amd", "csrc", "*.hip")) + \
+        glob.glob(os.path.join(here, "..", "halo_amd", "csrc", "*.cpp")) + \
+        glob.glob(os.path.join(here, "..", "halo_amd", "csrc", "*.hpp"))
+    assert srcs
+    for f in srcs:
+        text = open(f).read()
+        assert not re.search(r"\b(secure_)?getenv\s*\(", text), f
