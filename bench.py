@@ -70,10 +70,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    # 8 hardware queues (HIP's default is 4): the MSM tail streams and the concurrent IPA sessions'
-    # streams then map onto distinct queues instead of serialising behind each other (measured: two
-    # concurrent 2^16 openings 56 ms on 4 queues, 38 ms on 8; the MSM pipeline is unchanged)
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+    # HIP's default 4 hardware queues (round 4, interleaved on one box: headline 1.322 vs 1.332 ms/step,
+    # opening 2^20 20.66 vs 20.73 ms, prover 2^20 199.2 vs 201.9 ms with 4 vs 8 queues)
     import torch
     import torch.distributed as dist
 

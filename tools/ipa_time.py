@@ -2,7 +2,6 @@
 fold, with a stand-in transcript (fixed pseudo-random challenges).  MAT_N=<len>[,<len>...]: repeat
 with the weighted rounds materialising G at each length (tuning ipa_mat_n)."""
 import ctypes, os, random, sys, time
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")  # as bench.py
 sys.path.insert(0, '/root/repo')
 import numpy as np
 from halo_amd import _lib as H

@@ -1,6 +1,5 @@
 """Times the device-resident naive_prover pipeline (halo_amd.prover) at n = 2^logn on one GPU."""
 import json, os, sys, time
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")  # as bench.py
 sys.path.insert(0, '/root/repo')
 from halo_amd import _lib as H
 from halo_amd import prover
