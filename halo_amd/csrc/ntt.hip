@@ -62,6 +62,10 @@ struct NttPassArgs {
     // pass multiplies by 2^261 (forward) or 2^261 / N (inverse) and emits ark words again: the
     // input conversion costs no multiplication.
     uint32_t out_const[NLIMB];
+    // out_scaled: the pass's pre-twiddle table already holds M(w, out_const) (the last pass of a
+    // table-driven transform): the rho = 0 inputs take M(x, out_const), the outputs no multiplication
+    // (the transform is linear and M(M(a, t), c) = M(M(a, c), t)), one multiplication per element fewer
+    uint32_t out_scaled;
     size_t stride;              // elements between consecutive transforms of a batch
 };
 
@@ -305,6 +309,12 @@ __global__ __launch_bounds__(NE / EPT) void k_ntt_pass(NttPassArgs a) {
             const size_t j = j0 + t;
             const uint4* src = in + 2 * (j + (size_t)rho * NJ);
             Fe<F> x = fe_load<F>(src);  // ark words are used as internal values (see out_const)
+            if (a.out_scaled && rho == 0) {
+                Fe<F> oc;
+#pragma unroll
+                for (int l = 0; l < NLIMB; l++) oc.v[l] = a.out_const[l];
+                x = fe_mul(x, oc);
+            }
             if (!a.in_ark && a.log_ns != 0 && rho != 0) {
                 const size_t jj = j & (Ns - 1);
                 Fe<F> w;
@@ -396,7 +406,7 @@ __global__ __launch_bounds__(NE / EPT) void k_ntt_pass(NttPassArgs a) {
         const size_t dst = ((j >> a.log_ns) << (a.log_ns + r)) + (j & (Ns - 1)) + (size_t)k * Ns;
         Fe<F> x = lds_get_soa<F>(data, ntt_swz<NE>(t * R + k), NE);
         if (a.out_ark) {
-            fe_store(out + 2 * dst, fe_canon(fe_mul(x, oc)));
+            fe_store(out + 2 * dst, fe_canon(a.out_scaled ? fe_reduce_q(x) : fe_mul(x, oc)));
         } else {
             fe_store(out + 2 * dst, fe_reduce_q(x));
         }
@@ -406,7 +416,7 @@ __global__ __launch_bounds__(NE / EPT) void k_ntt_pass(NttPassArgs a) {
 // Per-pass pre-twiddle table: tab[rho * Ns + jj] = omega_N^(rho jj N / (Ns R)) (internal packed).
 template <class F>
 __global__ void k_pass_twiddles(uint4* tab, uint32_t log_r, uint32_t log_ns, uint32_t logn, const uint4* lo,
-                                const uint4* hi, uint32_t lo_bits) {
+                                const uint4* hi, uint32_t lo_bits, Fe<F> scale, int scaled) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const size_t cnt = (size_t)1 << (log_r + log_ns);
     if (i >= cnt) return;
@@ -415,6 +425,7 @@ __global__ void k_pass_twiddles(uint4* tab, uint32_t log_r, uint32_t log_ns, uin
     Fe<F> w = fe_load<F>(lo + 2 * (e & (((size_t)1 << lo_bits) - 1)));
     const size_t eh = e >> lo_bits;
     if (eh) w = fe_mul(w, fe_load<F>(hi + 2 * eh));
+    if (scaled) w = fe_mul(w, scale);  // the last pass's table: M(w, out_const), NttPassArgs::out_scaled
     fe_store(tab + 2 * i, w);
 }
 
@@ -592,9 +603,12 @@ static int get_twiddles(DeviceState* st, int field, unsigned logn, int inverse, 
                 const size_t cnt = (size_t)1 << (rad[p] + log_ns);
                 HALO_CHECK(t->pass[p].reserve(cnt * 32));
                 const unsigned thr = 256, blocks = (unsigned)((cnt + thr - 1) / thr);
+                // the last pass's table is pre-scaled by the output constant (NttPassArgs::out_scaled)
+                Fe<F> oc;
+                for (int l = 0; l < NLIMB; l++) oc.v[l] = inverse ? F::NINV_ARK[logn][l] : F::ONE[l];
                 hipLaunchKernelGGL(k_pass_twiddles<F>, dim3(blocks), dim3(thr), 0, s, t->pass[p].as<uint4>(), rad[p],
                                    log_ns, logn, t->lo.as<const uint4>(), t->hi.as<const uint4>(),
-                                   (uint32_t)t->lo_bits);
+                                   (uint32_t)t->lo_bits, oc, (int)(p + 1 == rad.size()));
                 HALO_HIP(hipGetLastError());
             }
             log_ns += rad[p];
@@ -649,6 +663,7 @@ static int ntt_device(DeviceState* st, int field, const void* d_in, void* d_out,
         a.out_ark = (p == P - 1);
         a.prune = (p == 0 && !inverse) ? ntt_pass0_prune(lr, prune) : 0u;
         for (int l = 0; l < NLIMB; l++) a.out_const[l] = inverse ? F::NINV_ARK[logn][l] : F::ONE[l];
+        a.out_scaled = (a.out_ark && a.tw) ? 1u : 0u;  // (get_twiddles pre-scales the last pass's table)
         a.stride = N;
         const size_t NJ = N >> lr;
         const size_t NE = lr > NTT_MAX_LOG_R_MULTI ? NTT_E_BIG : NTT_E;

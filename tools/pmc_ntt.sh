@@ -1,19 +1,30 @@
-# SQ counters of the NTT pass kernel (run through gpurun from the repo root)
+# SQ counters of the NTT pass kernels at 2^22 (tools/ntt_time.py 22: 2 x 11-bit passes per transform),
+# run through gpurun from the repo root; per kernel: lane-instructions per element per pass, the VALU
+# issue rate, the LDS-instruction share and the share of wave cycles waiting on LDS / anything.
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 O=gpurun_out/pmc_ntt; rm -rf $O; mkdir -p $O
-timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAVES SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_INSTS_SALU SQ_WAIT_INST_LDS --output-format csv -d $O/a -o run -- python3 tools/ntt_time.py 22 > $O/a.log 2>&1 || exit 1
+timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAVES SQ_LDS_IDX_ACTIVE SQ_WAVE_CYCLES SQ_INSTS_SALU SQ_WAIT_INST_LDS --output-format csv -d $O/a -o run -- python3 tools/ntt_time.py 22 > $O/a.log 2>&1 || exit 1
 timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_INSTS_VMEM --output-format csv -d $O/b -o run -- python3 tools/ntt_time.py 22 > $O/b.log 2>&1 || exit 1
 python3 - $O <<'PY'
 import csv, glob, sys, collections
 O = sys.argv[1]
+agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for sub in ('a', 'b'):
     f = glob.glob(f'{O}/{sub}/**/*counter_collection.csv', recursive=True)[0]
-    agg = collections.defaultdict(lambda: collections.defaultdict(list))
     for r in csv.DictReader(open(f)):
-        k = r['Kernel_Name'][:40]
+        k = r['Kernel_Name'].split('(')[0]
+        if 'ntt_pass' not in k: continue
         agg[k][r['Counter_Name']].append(float(r['Counter_Value']))
-    for k, d in agg.items():
-        if 'ntt_pass' not in k and 'k_acc' not in k: continue
-        print(sub, k, {c: round(sum(v) / len(v)) for c, v in d.items()})
+for k, d in agg.items():
+    c = {n: sum(v) / len(v) for n, v in d.items()}
+    elems = 1 << 22  # per pass (one transform)
+    cyc = c['GRBM_GUI_ACTIVE'] / 8
+    print(k)
+    print(f"  VALU lane-instructions per element per pass: {c['SQ_INSTS_VALU'] * 64 / elems:.0f}")
+    print(f"  VALU wave-instructions per element: {c['SQ_INSTS_VALU'] / elems:.2f}; per wave: {c['SQ_INSTS_VALU'] / c['SQ_WAVES']:.0f}")
+    print(f"  VALU issue per CU per clock: {c['SQ_INSTS_VALU'] / (256 * cyc):.3f}; LDS instr per CU per clock: {c['SQ_INSTS_LDS'] / (256 * cyc):.3f}")
+    print(f"  LDS bank conflict share: {100 * c['SQ_LDS_BANK_CONFLICT'] / max(1, c['SQ_LDS_IDX_ACTIVE']):.1f} %")
+    print(f"  wave cycles waiting on LDS: {100 * c['SQ_WAIT_INST_LDS'] / c['SQ_WAVE_CYCLES']:.1f} %, waiting on anything: {100 * c['SQ_WAIT_ANY'] / c['SQ_WAVE_CYCLES']:.1f} %")
+    print(f"  raw: " + ", ".join(f"{n}={v:.0f}" for n, v in sorted(c.items())))
 PY
 rm -rf $O/a $O/b
