@@ -34,7 +34,15 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 MSM_BYTES_PER_POINT = 96
 NTT_BYTES_PER_ELEM = 64  # read + write 32 B per transform
-MODMUL_PEAK = 1.77e11  # 255-bit Montgomery multiplications/s, 1 MI355X, 8 waves/SIMD (fe_mul_bench)
+# 255-bit Montgomery multiplications/s of one MI355X at k_acc's occupancy (4 waves/SIMD), round-4
+# field code (tools/micro/fe_mul_bench.hip, profiles/r04_micro.txt: 1.80e11; round 3's code: 1.77e11)
+MODMUL_PEAK = 1.80e11
+# raw VALU issue ceiling: v_mad_u64_u32 back to back, 3.09e13 lane-instructions/s on one MI355X
+# (tools/micro/modmul_bench.hip, profiles/r04_micro.txt); every VOP3 integer op issues at that rate
+RAW_VOP3_PEAK = 3.09e13
+# k_acc's VALU instructions per wave (16 additions per lane, K = 16) from the committed counters
+# (profiles/r04_pmc_kernels.txt) -- a per-build constant, valid for the 2^20 headline configuration
+KACC_VALU_PER_WAVE = 27659
 
 
 def parse():
@@ -730,6 +738,11 @@ def main():
 
     madds = n * (-(-255 // window_bits)) if window_bits else 0  # one mixed addition per nonzero digit
     valu_achieved = madds * 10 / (acc_avg_ms * 1e-3) if acc_avg_ms > 0 else 0.0
+    # issue: k_acc's lane-instructions per launch (waves x the counted VALU per wave x 64 lanes) over the
+    # live launch time, against the raw v_mad_u64_u32 issue rate (only at the 2^20 headline shape, where
+    # the committed per-wave count applies: 15 windows, K = 16)
+    kacc_waves = (madds // 16 + 63) // 64 if args.logn == 20 and window_bits == 17 else 0
+    issue_achieved = kacc_waves * KACC_VALU_PER_WAVE * 64 / (acc_avg_ms * 1e-3) if acc_avg_ms > 0 and kacc_waves else None
 
     line = {
         "metric": "MSM points/sec (Pippenger, Pallas, 2^20 points, resident SRS)",
@@ -775,7 +788,16 @@ def main():
             "peak": MODMUL_PEAK,
             "frac": valu_achieved / MODMUL_PEAK,
             "note": "XYZZ mixed additions (8M + 2S, counted as 10 modmul) per launch / mean launch time, against the "
-                    "measured single-chain Montgomery multiplication rate of one MI355X (tools/micro/fe_mul_bench.hip)",
+                    "measured Montgomery multiplication rate of one MI355X at 4 waves/SIMD (tools/micro/fe_mul_bench.hip)",
+            "issue": {
+                "unit": "VALU lane-instructions/s",
+                "achieved": issue_achieved,
+                "peak": RAW_VOP3_PEAK,
+                "frac": issue_achieved / RAW_VOP3_PEAK if issue_achieved else None,
+                "note": "k_acc's counted VALU instructions (KACC_VALU_PER_WAVE per wave, profiles/r04_pmc_kernels.txt) "
+                        "over the live launch time, against back-to-back v_mad_u64_u32 issue (tools/micro/modmul_bench.hip); "
+                        "VOP2 ops (v_and, v_add_u32) issue twice as fast, so a mix can slightly exceed it",
+            },
         },
         "extra": {
             "msm_single_latency_ms": min(lat) if lat else None,

@@ -162,7 +162,7 @@ int main() {
         for (int v = 0; v < 3; v++) {
             double t = timeit(v == 0 ? lat<0> : (v == 1 ? lat<1> : lat<2>), d, 1, 64, 4096);
             printf("single-wave dependent chain: %s %.1f ns per modmul\n",
-                   v == 0 ? "compiler-split" : (v == 1 ? "asm per product" : "asm per column (fields.hpp)"), t * 1e6 / 4096);
+                   v == 0 ? "compiler-split" : (v == 1 ? "asm per product" : "fields.hpp fe_mul"), t * 1e6 / 4096);
         }
         CHECK(hipFree(d));
     }
@@ -197,7 +197,7 @@ int main() {
         CHECK(hipMemcpy(d, h.data(), h.size() * 4, hipMemcpyHostToDevice));
         hipLaunchKernelGGL(bench<3>, dim3(blocks), dim3(threads), 0, 0, d, 7);
         CHECK(hipMemcpy(o3.data(), d, h.size() * 4, hipMemcpyDeviceToHost));
-        printf("waves/SIMD %d: fe_mul (asm per column) %.3e, asm per product %.3e, asm-2chain %.3e, compiler-split %.3e modmul/s, same=%d%d%d\n", wps,
+        printf("waves/SIMD %d: fe_mul (fields.hpp, one asm statement per multiplication) %.3e, asm per product %.3e, asm-2chain %.3e, compiler-split %.3e modmul/s, same=%d%d%d\n", wps,
                n * (double)iters / (t0 * 1e-3), n * (double)iters / (t1 * 1e-3), n * (double)iters / (t2 * 1e-3),
                n * (double)iters / (t3 * 1e-3), (int)(o0 == o1), (int)(o0 == o2), (int)(o0 == o3));
         CHECK(hipFree(d));
