@@ -134,7 +134,7 @@ def _ark_inverse(x: np.ndarray, cid: int) -> np.ndarray:
     """x^-1 for an ark Montgomery scalar (x R -> x^-1 R), host big integers."""
     r = _SCALAR[cid]
     v = int(x[0]) | int(x[1]) << 64 | int(x[2]) << 128 | int(x[3]) << 192
-    inv = pow(v * pow(1 << 256, -1, r) % r, -1, r) * (1 << 256) % r
+    inv = pow(v, -1, r) * pow(2, 512, r) % r  # (x R)^-1 R^2 = x^-1 R: one modular inverse
     return np.array([(inv >> (64 * i)) & (2**64 - 1) for i in range(4)], dtype=np.uint64)
 
 
