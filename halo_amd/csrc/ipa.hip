@@ -2457,12 +2457,15 @@ extern "C" int halo_pcdl_decider_commit(halo_curve_t curve, const halo_fe_t* xis
         return set_error(HALO_ELENGTH, "ms must be larger than Gs: (Gs: %zu), (ms: %zu)", d + 1, n);
     hipStream_t s = 0;
     ScratchUse su(st, s);
-    HALO_CHECK(st->scratch[7].reserve(n * 32 + 64));
+    HALO_CHECK(st->scratch[7].reserve(n * 32 + 128));
     const int field = (curve == HALO_PALLAS) ? HALO_FP : HALO_FQ;
     HALO_CHECK(hpoly_device(st, field, xis, 1, n_xis, nullptr, st->scratch[7].ptr, s));
     char* d_out = (char*)st->scratch[7].ptr + n * 32;
-    HALO_CHECK(msm_srs_device(st, curve, st->scratch[7].ptr, n, nullptr, d_out, s));
-    return copy_d2h(out, d_out, 64, s);
+    HALO_CHECK(msm_srs_device(st, curve, st->scratch[7].ptr, n, nullptr, d_out, s, false, true));
+    alignas(16) uint64_t xyzz[16];  // converted on the host (msm.hip d2h_point)
+    HALO_CHECK(copy_d2h(xyzz, d_out, 128, s));
+    host_xyzz_to_wrapped(curve, xyzz, out);
+    return HALO_OK;
 }
 
 // ---------------------------------------------------------------------------------------------

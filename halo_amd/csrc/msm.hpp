@@ -31,7 +31,7 @@ int msm_join(DeviceState* st, hipStream_t s);
 // MSM over the resident SRS prefix (window-shifted copies when precomputed); optional hiding
 // scalar (ark, device pointer) times S.
 int msm_srs_device(DeviceState* st, int curve, const void* scalars_ark, size_t n, const void* hide_scalar,
-                   void* d_out_wrapped, hipStream_t s, bool async = false);
+                   void* d_out_wrapped, hipStream_t s, bool async = false, bool out_xyzz = false);
 // MSM over the resident SRS range [offset, offset + n) with a caller hiding table (2^i P, i < 256,
 // internal affine) and scalar; uses the window-shifted copies (returns HALO_EINVAL without them).
 // blk_lg < 32: scalar i goes with point offset + i + ((i >> blk_lg) << blk_lg), i.e. the blocks
