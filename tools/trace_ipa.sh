@@ -13,7 +13,7 @@ if len(sys.argv) > 2 and sys.argv[2]:
     ws = [r for r in rows if sys.argv[2] in r['Kernel_Name']]
     t0 = int(ws[-1]['Start_Timestamp']); t1 = t0 + 6000000
 else:
-    ws = [r for r in rows if 'k_weighted_scalars' in r['Kernel_Name']]
+    ws = [r for r in rows if 'k_weighted_prep' in r['Kernel_Name']]
     k = len(ws) - 6
     t0 = int(ws[k]['Start_Timestamp']); t1 = int(ws[k + 2]['Start_Timestamp'])
 prev_end = None
