@@ -869,6 +869,22 @@ __global__ void k_set_one_ark(uint4* out) {
     if (threadIdx.x == 0) fe_to_ark(out, fe_one<S>());
 }
 
+// Small host values passed by value and stored by one launch (instead of one H2D copy per value, each
+// a blit kernel of ~4 us on the stream): segment i is cnt[i] uint4 at dst[i], taken in order from v.
+struct PutArgs {
+    uint4* dst[4];
+    int cnt[4];
+    uint4 v[16];
+};
+__global__ void k_put_args(PutArgs a) {
+    int base = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        if ((int)threadIdx.x < a.cnt[i]) a.dst[i][threadIdx.x] = a.v[base + threadIdx.x];
+        base += a.cnt[i];
+    }
+}
+
 // x[i] *= k (ark scalars, i < count): the IPA's dots scaled by xi_0 in xi mode
 template <class S>
 __global__ void k_scale_ark(uint4* x, int count, const uint4* k) {
@@ -1481,7 +1497,9 @@ static int ipa_setup(DeviceState* st, halo_ipa_session* ses, int curve, size_t n
         HALO_CHECK(copy_h2d(ses->zs.ptr, zs_host, n * 32, s));
     } else {
         HALO_CHECK(copy_h2d(sm, z, 32, s));
-        const size_t run = 16;
+        // consecutive powers per thread: a thread's chain is its exponentiation (~log2 n + popcount
+        // products) plus `run`; small n is latency-bound (short runs), large n throughput-bound
+        const size_t run = n <= 4096 ? 2 : 16;
         DISPATCH_CURVE(curve, Cv, {
             hipLaunchKernelGGL(k_powers<typename Cv::Scalar>, dim3(gridn((n + run - 1) / run, 128)), dim3(128), 0, s,
                                (const uint4*)sm, n, run, ses->zs.as<uint4>());
@@ -1603,7 +1621,9 @@ extern "C" int halo_ipa_begin_vectors(halo_curve_t curve, const halo_wrapped_poi
     return ipa_begin(curve, n, gs, cs, zs, nullptr, H_prime, out);
 }
 
-// v = c(z) over the session's first len coefficients (z at small[0, 32)), to the host (stream sync).
+// v = c(z) over the session's first len coefficients, to the host (stream sync): the dot product of c
+// with the session's z^i vector (ipa_setup wrote it), one parallel multiplication per coefficient
+// instead of chunked Horner chains (2^10: 44 + 5 us of dependent chains -> one short dot launch pair)
 static int ipa_eval_cs(halo_ipa_session* ses, size_t len, halo_fe_t* v_out) {
     hipStream_t s = ses->s;
     char* sm = ses->small.as<char>();
@@ -1611,19 +1631,9 @@ static int ipa_eval_cs(halo_ipa_session* ses, size_t len, halo_fe_t* v_out) {
         memset(v_out, 0, 32);
         return HALO_OK;
     }
-    const size_t chunk = 32;
-    const int nchunks = (int)((len + chunk * RED_THREADS - 1) / (chunk * RED_THREADS));
-    HALO_CHECK(ses->tmp.reserve(std::max<size_t>(4096 * 32, (size_t)nchunks * 32)));
-    const void* tab[2] = {ses->cs.ptr, (const void*)len};  // the pointer table and length of k_eval_chunks
-    HALO_CHECK(copy_h2d(sm + SM_EVAL, tab, 16, s));
-    DISPATCH_CURVE(ses->curve, Cv, {
-        using Sc = typename Cv::Scalar;
-        hipLaunchKernelGGL(k_eval_chunks<Sc>, dim3(nchunks, 1), dim3(RED_THREADS), 0, s, (const uint4* const*)(sm + SM_EVAL),
-                           (const size_t*)(sm + SM_EVAL + 8), (const uint4*)sm, chunk, nchunks, ses->tmp.as<uint4>());
-        hipLaunchKernelGGL(k_sum_internal_to_ark<Sc>, dim3(1), dim3(RED_THREADS), 0, s, ses->tmp.as<const uint4>(),
-                           nchunks, (uint4*)(sm + SM_V));
-    });
-    HALO_HIP(hipGetLastError());
+    HALO_CHECK(ses->tmp.reserve(4096 * 32));  // dot_device: at most 1024 block partials
+    const int sf = ses->curve == HALO_PALLAS ? HALO_FP : HALO_FQ;
+    HALO_CHECK(dot_device(sf, ses->cs.ptr, ses->zs.ptr, len, sm + SM_V, ses->tmp.ptr, s));
     HALO_HIP(hipMemcpyAsync(ses->pinned, sm + SM_V, 32, hipMemcpyDeviceToHost, s));
     HALO_HIP(hipStreamSynchronize(s));
     memcpy(v_out, ses->pinned, 32);
@@ -1714,10 +1724,21 @@ extern "C" int halo_pcdl_open_combine(halo_ipa_session* ses, const halo_fe_t* al
     std::lock_guard<std::mutex> g(st->mu);
     hipStream_t s = ses->s;
     char* sm = ses->small.as<char>();
-    HALO_CHECK(copy_h2d(sm + SM_ALPHA, alpha, 32, s));
-    HALO_CHECK(copy_h2d(sm + SM_W, w, 32, s));
-    HALO_CHECK(copy_h2d(sm + SM_C, C, 64, s));
-    HALO_CHECK(copy_h2d(sm + SM_S, st->srs[ses->curve].S, 64, s));
+    {  // alpha, w, C and S (internal) in one launch
+        PutArgs a{};
+        const void* src[4] = {alpha, w, C, st->srs[ses->curve].S};
+        const size_t off[4] = {SM_ALPHA, SM_W, SM_C, SM_S};
+        const int cnt[4] = {2, 2, 4, 4};
+        int k = 0;
+        for (int i = 0; i < 4; i++) {
+            a.dst[i] = (uint4*)(sm + off[i]);
+            a.cnt[i] = cnt[i];
+            memcpy(&a.v[k], src[i], 16 * cnt[i]);
+            k += cnt[i];
+        }
+        hipLaunchKernelGGL(k_put_args, dim3(1), dim3(64), 0, s, a);
+        HALO_HIP(hipGetLastError());
+    }
     // c (= p padded) += alpha p_bar in place: p' (pcdl.rs:366); C' = C + alpha C_bar - w' S, w' = w + alpha w_bar.
     // Up to COMBINE_MSM_MAX coefficients C' is formed as C + MSM(G, alpha p_bar) - w S (= C + alpha C_bar - w' S,
     // since C_bar = MSM(G, p_bar) + w_bar S): an MSM (the table path, or the bucket pipeline) instead of
