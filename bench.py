@@ -67,6 +67,9 @@ def parse():
                     help="log2 n of the pcdl_commit / pcdl_open sweeps with w = Some (extra.pcdl; '' = off)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal only: every rank on cuda:0 over gloo (multi-rank runs on a one-GPU box)")
+    ap.add_argument("--msm-streams", type=int, default=2,
+                    help="streams the pipelined headline MSMs alternate over (independent MSMs; round 4, one box: "
+                         "1 / 2 / 3 streams 1.26 / 1.233 / 1.296 ms/step)")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
                     help="halo_set_tuning before the run (A/B of path selections; results are identical)")
     return ap.parse_args()
@@ -105,6 +108,24 @@ def main():
     gen.manual_seed(1234 + rank)
     stream = torch.cuda.current_stream().cuda_stream
     sp = ctypes.c_void_p(stream)
+    HIP = ctypes.CDLL("libamdhip64.so")
+    for fn in ("hipStreamCreateWithFlags", "hipStreamDestroy", "hipEventCreateWithFlags", "hipEventRecord",
+               "hipStreamWaitEvent", "hipEventDestroy"):
+        getattr(HIP, fn).restype = ctypes.c_int
+    HIP.hipStreamWaitEvent.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint]
+    HIP.hipEventRecord.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    HIP.hipStreamDestroy.argtypes = [ctypes.c_void_p]
+    HIP.hipEventDestroy.argtypes = [ctypes.c_void_p]
+    # the headline's extra streams (--msm-streams): plain HIP streams created before the library creates
+    # any of its own, so every later stream (the MSM tail streams, the IPA sessions') keeps its relative
+    # placement on the 4 hardware queues (an extra stream created after them made the opening leg
+    # 19.9 -> 21.2-22.1 ms)
+    extra_streams = []
+    for _ in range(max(1, args.msm_streams) - 1):
+        hs = ctypes.c_void_p()
+        if HIP.hipStreamCreateWithFlags(ctypes.byref(hs), 1) != 0:  # hipStreamNonBlocking
+            raise RuntimeError("hipStreamCreateWithFlags failed")
+        extra_streams.append(hs)
 
     def measure_msm(logn, steps, warmup, check_sync=True):
         """Pipelined MSM throughput at 2^logn points per rank against a resident synthetic SRS."""
@@ -122,13 +143,26 @@ def main():
         d_final = torch.zeros((total_steps, 8), dtype=torch.int64, device="cuda")
         out = np.zeros(8, dtype=np.uint64)
 
+        torch.cuda.synchronize()  # the scalars are written before the extra streams read them
+        sps = [sp] + extra_streams
+        extra = extra_streams
+
         def run_steps(first, k):
             """k MSM steps enqueued back to back (pipelined: each step's reduction tail overlaps the
-            next step's accumulation), then the multi-rank combine; no host synchronisation inside."""
+            next step's accumulation; with --msm-streams S the independent MSMs alternate over S
+            streams, so a step's front can also overlap the previous step's accumulation), then the
+            multi-rank combine; no host synchronisation inside."""
             for i in range(first, first + k):
                 H.check(L.halo_msm_dev_async(curve, None, ctypes.c_void_p(scalars[i % nbatch].data_ptr()), n,
-                                             ctypes.c_void_p(d_out[i].data_ptr()), sp))
-            H.check(L.halo_msm_join(sp))
+                                             ctypes.c_void_p(d_out[i].data_ptr()), sps[i % len(sps)]))
+            for q in sps:
+                H.check(L.halo_msm_join(q))
+            for es in extra:  # the current stream waits for the extra streams' MSMs
+                ev = ctypes.c_void_p()
+                HIP.hipEventCreateWithFlags(ctypes.byref(ev), 2)  # hipEventDisableTiming
+                HIP.hipEventRecord(ev, es)
+                HIP.hipStreamWaitEvent(sp, ev, 0)
+                HIP.hipEventDestroy(ev)
             if world > 1:
                 parts = [torch.empty((k, 8), dtype=torch.int64, device="cuda") for _ in range(world)]
                 dist.all_gather(parts, d_out[first:first + k].contiguous())
@@ -162,9 +196,13 @@ def main():
         acc_ms = ctypes.c_double(0)
         H.check(L.halo_profile_read(b"msm_acc", ctypes.byref(launches), ctypes.byref(acc_ms)))
         acc_avg_ms = acc_ms.value / max(1, launches.value)
-        # every step's result must equal the synchronous (non-pipelined) MSM of the same scalars
+        # every step's result must equal the synchronous (non-pipelined) MSM of the same scalars; these
+        # standalone MSMs also give k_acc's isolated launch time (the timed region's launches share the
+        # GPU with the other stream's front and the previous step's tail)
         sync_ok = True
         lat = []
+        L.halo_profile_reset()
+        L.halo_profile_enable(0 if os.environ.get("HALO_BENCH_NOPROF") == "1" else 1)
         for i in range(min(nbatch, 4) if check_sync else 1):
             torch.cuda.synchronize()
             a0 = time.perf_counter()
@@ -173,10 +211,14 @@ def main():
             for j in range(warmup, total_steps):
                 if j % nbatch == i:
                     sync_ok &= bool(np.array_equal(d_out[j].cpu().numpy().view(np.uint64), out))
+        L.halo_profile_enable(0)
+        H.check(L.halo_profile_read(b"msm_acc", ctypes.byref(launches), ctypes.byref(acc_ms)))
+        acc_iso_ms = acc_ms.value / max(1, launches.value)
         first = d_out[0].cpu().numpy().view(np.uint64).copy() if warmup > 0 else None
-        return elapsed, acc_avg_ms, sync_ok, lat, scalars[0], (seed, first)
+        torch.cuda.synchronize()
+        return elapsed, acc_avg_ms, acc_iso_ms, sync_ok, lat, scalars[0], (seed, first)
 
-    elapsed, acc_avg_ms, sync_ok, lat, scalars0, check0 = measure_msm(args.logn, args.steps, args.warmup)
+    elapsed, acc_avg_ms, acc_iso_ms, sync_ok, lat, scalars0, check0 = measure_msm(args.logn, args.steps, args.warmup)
     window_bits = L.halo_srs_window_bits(curve)
 
     # ---- IPA opening (pcdl::open_without_eval round loop, pcdl.rs:392-438) at 2^logn:
@@ -550,7 +592,7 @@ def main():
     sizes = {}
     size_checks = {}  # 2^lg MSM: (scalars[0] on the host, SRS seed, result), verified in the CPU leg
     for lg in [int(v) for v in args.sizes.split(",") if v.strip()]:
-        e, a_ms, ok, lt, sc0, chk = measure_msm(lg, 4, 2, check_sync=False)
+        e, a_ms, _, ok, lt, sc0, chk = measure_msm(lg, 4, 2, check_sync=False)
         if world == 1 and not args.no_cpu:
             size_checks[lg] = (sc0.cpu().numpy().view(np.uint64).copy(), chk)
         del sc0
@@ -566,7 +608,7 @@ def main():
         if world > 1 and (world & (world - 1)) == 0:
             # BASELINE configs[4]: one 2^lg-point MSM partitioned across the ranks (strong scaling)
             lr = lg - (world.bit_length() - 1)
-            e, a_ms, ok, lt, _, _ = measure_msm(lr, 4, 2, check_sync=False)
+            e, a_ms, _, ok, lt, _, _ = measure_msm(lr, 4, 2, check_sync=False)
             sizes[f"msm_2^{lg}_partitioned"] = {
                 "points_per_s": (1 << lg) * 4 / e,
                 "ms_per_msm": e * 1e3 / 4,
@@ -743,6 +785,9 @@ def main():
     # the committed per-wave count applies: 15 windows, K = 16)
     kacc_waves = (madds // 16 + 63) // 64 if args.logn == 20 and window_bits == 17 else 0
     issue_achieved = kacc_waves * KACC_VALU_PER_WAVE * 64 / (acc_avg_ms * 1e-3) if acc_avg_ms > 0 and kacc_waves else None
+    # the same rates over k_acc's isolated launch time (the standalone MSMs after the timed region)
+    valu_iso = madds * 10 / (acc_iso_ms * 1e-3) if acc_iso_ms > 0 else 0.0
+    issue_iso = kacc_waves * KACC_VALU_PER_WAVE * 64 / (acc_iso_ms * 1e-3) if acc_iso_ms > 0 and kacc_waves else None
 
     line = {
         "metric": "MSM points/sec (Pippenger, Pallas, 2^20 points, resident SRS)",
@@ -764,7 +809,9 @@ def main():
             "parallelism": f"point-partition x{world}, RCCL all-gather of partial sums",
             "world_size_reported": dist.get_world_size() if world > 1 else 1,
             "backend": dist.get_backend() if world > 1 else None,
-            "pipelining": "steps enqueued back to back: step k's reduction tail overlaps step k+1's accumulation",
+            "pipelining": f"steps enqueued back to back over {max(1, args.msm_streams)} stream(s): step k's reduction "
+                          "tail overlaps step k+1's accumulation, and with two streams step k+1's front also "
+                          "overlaps step k's accumulation",
         },
         "roofline": {
             "bound": "hbm",
@@ -777,7 +824,10 @@ def main():
             "traffic_note": traffic_note,
             "algorithmic_bytes_per_launch": acc_bytes,
             "avg_launch_ms": acc_avg_ms,
-            "note": "the MSM is bound by 255-bit modular multiplication on the VALU, not HBM (SURVEY §7 hard part 1)",
+            "isolated_launch_ms": acc_iso_ms,
+            "note": "the MSM is bound by 255-bit modular multiplication on the VALU, not HBM (SURVEY §7 hard part 1); "
+                    "avg_launch_ms is over the timed region's launches, which share the GPU with the other stream's "
+                    "front and the previous step's tail, isolated_launch_ms over the standalone MSMs after it",
         },
         "cpu_baseline": cpu,
         "compute_roofline": {
@@ -789,6 +839,13 @@ def main():
             "frac": valu_achieved / MODMUL_PEAK,
             "note": "XYZZ mixed additions (8M + 2S, counted as 10 modmul) per launch / mean launch time, against the "
                     "measured Montgomery multiplication rate of one MI355X at 4 waves/SIMD (tools/micro/fe_mul_bench.hip)",
+            "isolated": {
+                "achieved": valu_iso,
+                "frac": valu_iso / MODMUL_PEAK,
+                "issue_achieved": issue_iso,
+                "issue_frac": issue_iso / RAW_VOP3_PEAK if issue_iso else None,
+                "note": "over k_acc's isolated launch time (roofline.isolated_launch_ms)",
+            },
             "issue": {
                 "unit": "VALU lane-instructions/s",
                 "achieved": issue_achieved,
