@@ -1,0 +1,69 @@
+"""The 2^20 opening's time after a pipelined 2^20 MSM burst over S streams (the bench's headline then
+its opening leg), optionally with halo_shutdown in between.  Usage (GPU box):
+    python tools/ipa_after_msm.py S [reset]"""
+import ctypes
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from halo_amd import _lib as H  # noqa: E402
+
+S = int(sys.argv[1]) if len(sys.argv) > 1 else 1
+reset = len(sys.argv) > 2 and sys.argv[2] == "reset"
+H.ensure_device(0)
+L = H.load()
+HIP = ctypes.CDLL("libamdhip64.so")
+HIP.hipStreamCreateWithFlags.restype = ctypes.c_int
+n = 1 << 20
+H.check(L.halo_srs_synthesize(0, n, 0x48414C4F))
+H.check(L.halo_srs_precompute_windows(0))
+sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+streams = [sp]
+for _ in range(S - 1):
+    hs = ctypes.c_void_p()
+    HIP.hipStreamCreateWithFlags(ctypes.byref(hs), 1)
+    streams.append(hs)
+sc = torch.randint(0, 2**62, (4, n, 4), dtype=torch.int64, device="cuda")
+out = torch.zeros((32, 8), dtype=torch.int64, device="cuda")
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+for i in range(32):
+    H.check(L.halo_msm_dev_async(0, None, ctypes.c_void_p(sc[i % 4].data_ptr()), n,
+                                 ctypes.c_void_p(out[i].data_ptr()), streams[i % S]))
+for q in streams:
+    H.check(L.halo_msm_join(q))
+torch.cuda.synchronize()
+print(f"S={S}: {(time.perf_counter() - t0) * 1e3 / 32:.3f} ms per MSM", flush=True)
+if reset:
+    L.halo_shutdown()
+R = 0x40000000000000000000000000000000224698FC0994A8DD8C46EB2100000001
+
+
+def fe1(v):
+    m = v * (1 << 256) % R
+    return np.array([(m >> (64 * i)) & (2**64 - 1) for i in range(4)], dtype=np.uint64)
+
+
+cs = np.random.default_rng(99).integers(0, 2**62, size=(n, 4), dtype=np.uint64)
+hp = np.zeros(8, dtype=np.uint64)
+H.check(L.halo_srs_read(0, 1, 1, H.ptr(hp)))
+z = fe1(12345)
+for rep in range(3):
+    ses = ctypes.c_void_p()
+    H.check(L.halo_ipa_begin(0, H.ptr(cs), n, H.ptr(z), H.ptr(hp), ctypes.byref(ses)))
+    Lp = np.zeros(8, dtype=np.uint64)
+    Rp = np.zeros(8, dtype=np.uint64)
+    a0 = time.perf_counter()
+    for r in range(20):
+        H.check(L.halo_ipa_round_lr(ses, H.ptr(Lp), H.ptr(Rp)))
+        xi = (int.from_bytes(Lp.tobytes()[:16], "little") ^ (r + 1)) % R or 1
+        H.check(L.halo_ipa_fold(ses, H.ptr(fe1(xi)), H.ptr(fe1(pow(xi, -1, R)))))
+    U = np.zeros(8, dtype=np.uint64)
+    c0 = np.zeros(4, dtype=np.uint64)
+    H.check(L.halo_ipa_end(ses, H.ptr(U), H.ptr(c0)))
+    print(f"  open 2^20 rep {rep}: {(time.perf_counter() - a0) * 1e3:.2f} ms", flush=True)
