@@ -239,9 +239,9 @@ def main():
         H.check(L.halo_srs_read(curve, 1, 1, H.ptr(hp)))
         z = fe1(12345)
 
-        def run_open():
+        def run_open(reps=4):
             best = None
-            for _ in range(2):
+            for _ in range(reps):
                 ses = ctypes.c_void_p()
                 H.check(L.halo_ipa_begin(curve, H.ptr(cs), n_, H.ptr(z), H.ptr(hp), ctypes.byref(ses)))
                 Lp = np.zeros(8, dtype=np.uint64)
@@ -269,7 +269,7 @@ def main():
         # the same opening with GLV folds of G every round (tuning ipa_weighted = 0): the fold kernel
         # rate for extra.cpu_ipa_fold, and the A/B of the weighted rounds; results must agree
         with H.tuning(ipa_weighted=0):
-            fold_path = run_open()
+            fold_path = run_open(2)
         return {
             "workload": f"pcdl open round loop 2^{logn} (lg n rounds of L/R + fold, weighted then tail rounds), "
                         "device-resident",
