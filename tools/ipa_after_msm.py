@@ -14,7 +14,7 @@ import torch  # noqa: E402
 from halo_amd import _lib as H  # noqa: E402
 
 S = int(sys.argv[1]) if len(sys.argv) > 1 else 1
-reset = len(sys.argv) > 2 and sys.argv[2] == "reset"
+reset = "reset" in sys.argv[2:]
 H.ensure_device(0)
 L = H.load()
 HIP = ctypes.CDLL("libamdhip64.so")
@@ -39,6 +39,10 @@ for q in streams:
     H.check(L.halo_msm_join(q))
 torch.cuda.synchronize()
 print(f"S={S}: {(time.perf_counter() - t0) * 1e3 / 32:.3f} ms per MSM", flush=True)
+if "sync" in sys.argv[2:]:  # the bench's standalone MSMs after its timed region
+    o = np.zeros(8, dtype=np.uint64)
+    for i in range(4):
+        H.check(L.halo_msm_dev(0, None, ctypes.c_void_p(sc[i].data_ptr()), n, H.ptr(o), sp))
 if reset:
     L.halo_shutdown()
 R = 0x40000000000000000000000000000000224698FC0994A8DD8C46EB2100000001
@@ -58,6 +62,9 @@ for rep in range(3):
     H.check(L.halo_ipa_begin(0, H.ptr(cs), n, H.ptr(z), H.ptr(hp), ctypes.byref(ses)))
     Lp = np.zeros(8, dtype=np.uint64)
     Rp = np.zeros(8, dtype=np.uint64)
+    if "prof" in sys.argv[2:]:  # the bench's opening leg runs with the library's launch profiling on
+        L.halo_profile_reset()
+        L.halo_profile_enable(1)
     a0 = time.perf_counter()
     for r in range(20):
         H.check(L.halo_ipa_round_lr(ses, H.ptr(Lp), H.ptr(Rp)))
