@@ -1015,6 +1015,7 @@ struct halo_ipa_session {
     hipStream_t s = nullptr;
     hipStream_t s2 = nullptr;           // weighted rounds above IPA_PAIR_MAX: R's MSM (created on first use)
     bool solo = true;                   // the round call advances this session alone (s2 is used then)
+    bool slots_reset = false;           // this opening restarted the MSM slot assignment (msm_slots_reset)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     hipEvent_t htab_ready = nullptr;  // recorded after the session's own 2^i H' table
     uint8_t* pinned = nullptr;  // [128, 192) xi|xi_inv (H2D), [256, 512) L|R XYZZ (D2H or tail_emit_host),
@@ -1063,7 +1064,7 @@ struct halo_ipa_session {
         wcur = 0;
         table = nullptr;
         table_ld = 0;
-        fold_inflight = htab_waited = xi_mode = fold_pending = false;
+        fold_inflight = htab_waited = xi_mode = fold_pending = slots_reset = false;
         htab_ptr = nullptr;
         started = blinded = combined = false;
     }
@@ -2074,6 +2075,10 @@ static int ipa_round_launch(DeviceState* st, halo_ipa_session* ses) {
                 HALO_HIP(hipStreamCreateWithFlags(&ses->s2, hipStreamNonBlocking));
                 HALO_HIP(hipEventCreateWithFlags(&ses->ev_fork, hipEventDisableTiming));
                 HALO_HIP(hipEventCreateWithFlags(&ses->ev_join, hipEventDisableTiming));
+            }
+            if (!ses->slots_reset) {
+                msm_slots_reset(st);
+                ses->slots_reset = true;
             }
             HALO_HIP(hipEventRecord(ses->ev_fork, s));
             HALO_HIP(hipStreamWaitEvent(ses->s2, ses->ev_fork, 0));

@@ -914,6 +914,23 @@ int msm_claim_set(DeviceState* st, hipStream_t s, int* set, DevBuf** conv) {
 }
 
 // Makes `s` wait (device-side) for the tails of the MSMs enqueued on `s` that are still in flight.
+// Forgets which issuing streams own the two scratch-set slots and restarts each slot at its first set
+// (only when no set's tail is still running; every set still waits for its own previous tail when
+// reused).  An IPA opening calls it before its first two-stream round, so its two streams claim the
+// same sets in the same order however many MSMs earlier callers issued on which streams (measured: after
+// 23 two-stream MSMs the 2^20 opening took 21.7-22.6 ms, after 32 -- or after a reset -- 19.6-20.0).
+void msm_slots_reset(DeviceState* st) {
+    MsmPipe& P = g_msm_pipe[st->device & 63];
+    for (const auto& m : P.set)
+        if (set_busy(m)) return;
+    for (int k = 0; k < 2; k++) {
+        P.slot_owner[k] = nullptr;
+        P.slot_next[k] = 0;
+        P.slot_used[k] = 0;
+    }
+    P.clock = 0;
+}
+
 int msm_join(DeviceState* st, hipStream_t s) {
     MsmPipe& PP = g_msm_pipe[st->device & 63];
     for (auto& m : PP.set)

@@ -28,6 +28,8 @@ void msm_shutdown();
 void ipa_shutdown();
 // Makes stream s wait for the reduction tails of the async MSMs enqueued on s.
 int msm_join(DeviceState* st, hipStream_t s);
+// Restarts the scratch-set slot assignment (no owners, first sets) when no MSM tail is running.
+void msm_slots_reset(DeviceState* st);
 // MSM over the resident SRS prefix (window-shifted copies when precomputed); optional hiding
 // scalar (ark, device pointer) times S.
 int msm_srs_device(DeviceState* st, int curve, const void* scalars_ark, size_t n, const void* hide_scalar,

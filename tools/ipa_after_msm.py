@@ -28,17 +28,26 @@ for _ in range(S - 1):
     hs = ctypes.c_void_p()
     HIP.hipStreamCreateWithFlags(ctypes.byref(hs), 1)
     streams.append(hs)
-sc = torch.randint(0, 2**62, (4, n, 4), dtype=torch.int64, device="cuda")
-out = torch.zeros((32, 8), dtype=torch.int64, device="cuda")
+nb, nmsm = (8, 23) if "bench" in sys.argv[2:] else (4, 32)  # "bench": the headline's batch and step counts
+nb = int(os.environ.get("NB", nb))
+nmsm = int(os.environ.get("NMSM", nmsm))
+if os.environ.get("SMALL") == "1":
+    sc = torch.randint(0, 2**62, (nb, n, 4), dtype=torch.int64, device="cuda")
+else:
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(1234)
+    sc = torch.randint(-(2**63), 2**63 - 1, (nb, n, 4), dtype=torch.int64, device="cuda", generator=gen)
+    sc[..., 3] &= 0x0FFFFFFFFFFFFFFF
+out = torch.zeros((nmsm, 8), dtype=torch.int64, device="cuda")
 torch.cuda.synchronize()
 t0 = time.perf_counter()
-for i in range(32):
-    H.check(L.halo_msm_dev_async(0, None, ctypes.c_void_p(sc[i % 4].data_ptr()), n,
+for i in range(nmsm):
+    H.check(L.halo_msm_dev_async(0, None, ctypes.c_void_p(sc[i % nb].data_ptr()), n,
                                  ctypes.c_void_p(out[i].data_ptr()), streams[i % S]))
 for q in streams:
     H.check(L.halo_msm_join(q))
 torch.cuda.synchronize()
-print(f"S={S}: {(time.perf_counter() - t0) * 1e3 / 32:.3f} ms per MSM", flush=True)
+print(f"S={S}: {(time.perf_counter() - t0) * 1e3 / nmsm:.3f} ms per MSM", flush=True)
 if "sync" in sys.argv[2:]:  # the bench's standalone MSMs after its timed region
     o = np.zeros(8, dtype=np.uint64)
     for i in range(4):
