@@ -655,10 +655,14 @@ def main():
         del xl, y, z
 
     # ---- distributed IPA opening (strided shards, halo_amd.dist.sharded_ipa_rounds), N > 1 only:
-    # every rank holds the same synthetic 2^logn SRS; rank r opens with the shard G[i P + r]
+    # every rank synthesizes the same 2^logn SRS and then keeps only its shard G[i P + r] resident (with
+    # its window-shifted copies), so each shard runs the weighted rounds (GpuWeightedIpaOps); the
+    # per-round L_r, R_r are all-gathered on the device and summed there (torch_reduce_lr)
     dist_ipa = None
     if world > 1 and args.ipa and args.dist_ipa:
-        from halo_amd.dist import GpuIpaOps, ipa_shard, sharded_ipa_rounds, torch_gather_arrays
+        from halo_amd import pcdl as PC
+        from halo_amd.dist import GpuWeightedIpaOps, sharded_ipa_rounds, torch_gather_arrays, torch_reduce_lr
+        from halo_amd.group import PublicParams
         n_ = 1 << args.logn
         H.check(L.halo_srs_synthesize(curve, n_, 777))
         G = np.zeros((n_, 8), dtype=np.uint64)
@@ -671,9 +675,7 @@ def main():
 
         rng = np.random.default_rng(99)
         cs = rng.integers(0, 2**62, size=(n_, 4), dtype=np.uint64)
-        z = 12345
-        zs = np.zeros((n_, 4), dtype=np.uint64)
-        H.check(L.halo_construct_powers(H.FP, H.ptr(fe1(z)), n_, H.ptr(zs)))
+        z_ark = fe1(12345)
         hp = G[1].copy()
         ks = {"k": 0}
 
@@ -685,32 +687,38 @@ def main():
             v = int.from_bytes(x.tobytes(), "little") * pow(1 << 256, -1, Rm) % Rm
             return fe1(pow(v, -1, Rm))
 
-        shard = (ipa_shard(G, rank, world), ipa_shard(cs, rank, world), ipa_shard(zs, rank, world))
+        ref = None
+        if rank == 0:  # the unsharded opening of the same instance on one GPU (weighted rounds)
+            H.check(L.halo_srs_precompute_windows(curve))
+            ref = PC.ipa_rounds(cs, z_ark, hp, challenge, inverse, args.curve)
+        PublicParams.upload(args.curve, np.ascontiguousarray(G[rank::world]), precompute_windows=True)
+        shard = (np.ascontiguousarray(cs[rank::world]), z_ark)
+        ops = GpuWeightedIpaOps(args.curve, rank, world)
         gather = torch_gather_arrays(dist, "cuda")
+        reduce_lr = torch_reduce_lr(dist, args.curve, "cuda")
         best = None
-        for _ in range(2):
+        for _ in range(3):
             ks["k"] = 0
             dist.barrier()
             torch.cuda.synchronize()
             a0 = time.perf_counter()
-            Ls, Rs, U, c0 = sharded_ipa_rounds([shard], hp, challenge, inverse, GpuIpaOps(args.curve), world, gather)
+            Ls, Rs, U, c0 = sharded_ipa_rounds([shard], hp, challenge, inverse, ops, world, gather, reduce_lr)
             torch.cuda.synchronize()
             tt = torch.tensor([time.perf_counter() - a0], dtype=torch.float64, device="cuda")
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             best = float(tt.item()) if best is None else min(best, float(tt.item()))
         same = None
-        if rank == 0:  # the unsharded opening of the same instance on one GPU must give the same proof
-            ks["k"] = 0
-            Ls1, Rs1, U1, c1 = sharded_ipa_rounds([(G, cs, zs)], hp, challenge, inverse, GpuIpaOps(args.curve), 1,
-                                                  lambda o: o)
+        if rank == 0:
+            Ls1, Rs1, U1, c1 = ref
             same = all(np.array_equal(a_, b_) for a_, b_ in zip(Ls + Rs + [U, c0], Ls1 + Rs1 + [U1, c1]))
         dist_ipa = {
-            "workload": f"pcdl open 2^{args.logn} sharded over {world} ranks (strided G/c/z shards, "
-                        f"per-round all-gather of L_r, R_r, last lg P rounds collapsed)",
+            "workload": f"pcdl open 2^{args.logn} sharded over {world} ranks (rank r: resident SRS shard G[r::P] "
+                        f"with window-shifted copies, weighted rounds; per-round RCCL all-gather of L_r, R_r "
+                        f"summed on the device; last lg P rounds collapsed)",
             "open_ms": best * 1e3,
             "matches_single_gpu": same,
         }
-        del G, cs, zs
+        del G, cs
 
     if rank != 0:
         if world > 1:

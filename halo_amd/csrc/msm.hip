@@ -34,10 +34,7 @@ namespace halo {
 // Columns of the bucket reduction grid (k_rowcol): 256 x 256 at 2^16 buckets keeps the row, column
 // and bit-sliced tree depths at ~9 additions each (measured against 32 columns: single-MSM latency
 // 2.15 -> 2.02 ms at 2^20, IPA opening 36.8 -> 35.2 ms; the pipelined step unchanged).
-#ifndef HALO_SEG_L
-#define HALO_SEG_L 256
-#endif
-constexpr int MSM_SEG_L = HALO_SEG_L;
+constexpr int MSM_SEG_L = 256;
 
 // ---------------------------------------------------------------------------------------------
 // synthetic bases / scalars (shared host/device definition)
@@ -156,9 +153,9 @@ __global__ void k_digits_glv(const uint4* scalars, size_t n, int c, int W, uint3
 // first segment's sum goes to first[t], its last segment's (when there are >= 2) to last[t], and the
 // buckets strictly inside the chunk are complete, so they go straight to bucket_sums.  k_merge then
 // completes the buckets that straddle chunk boundaries.
-#ifndef HALO_ACC_MINB
-#define HALO_ACC_MINB 4  // workgroups per CU the register budget is sized for (A/B builds override)
-#endif
+// k_acc's register budget is sized for 4 workgroups per CU (the compiler's own allocation, 116 VGPRs;
+// 5 / 6 per CU measured slower).
+constexpr int ACC_MIN_BLOCKS = 4;
 // npw_lg: log2 n_per_window when it is a power of two (the window of a shifted entry is a shift,
 // not a division), else 0xff.
 // (Measured and rejected: an LDS-DMA double buffer gathering entry e + 1's point while entry e's
@@ -224,7 +221,7 @@ __device__ __forceinline__ void acc_chunk(size_t t, uint32_t cnt, const uint32_t
 }
 
 template <class Cv>
-__global__ __launch_bounds__(256, HALO_ACC_MINB) void k_acc(const uint32_t* keys, const uint32_t* vals, const uint32_t* count,
+__global__ __launch_bounds__(256, ACC_MIN_BLOCKS) void k_acc(const uint32_t* keys, const uint32_t* vals, const uint32_t* count,
                                              uint32_t K, const uint4* bases, uint32_t n_per_window, uint32_t npw_lg,
                                              size_t stride, uint32_t blk_lg, uint32_t glv_n, uint4* first, uint4* last,
                                              uint4* bucket_sums, uint32_t* bstart, uint32_t NB, uint32_t key_lg = 31,
@@ -1060,25 +1057,30 @@ __global__ __launch_bounds__(256) void k_batch_expand(const uint32_t* ent, const
     vals[p] = (i + (ee & ((1u << tlog) - 1u)) * len + (ee >> tlog) * wstride) | (e & 0x80000000u);
 }
 
-// Shifted-SRS batches: the signed c_s-bit digit of (copy w, scalar u) -> two unsigned sub-digits
-// lo + 2^cb hi of its magnitude (mag <= 2^(c_s - 1) <= 2^(2 cb)), window q at sub[q][w T + u] (its sign
-// carried along; DIGIT_NONE for 0).  Sub-digit values run 1 .. 2^cb (bucket v - 1 of B = 2^cb): the one
-// magnitude with hi = 2^cb, mag = 2^(2 cb), is written as hi = 2^cb - 1, lo = 2^cb.
-// (Round 4: two windows of 2^8 buckets instead of three of 2^6 -- a third fewer bucket additions, the
-// dominant cost of the IPA's switch to the tail rounds: 47M -> 31M at 2^20.)
-__global__ __launch_bounds__(256) void k_batch_subdigits(const uint32_t* digits, uint32_t TW, int cb, uint32_t* sub) {
+// Shifted-SRS batches: the signed c_s-bit digit of (copy w, scalar u) -> nsub unsigned sub-digits
+// d_0 + 2^cb d_1 (+ 2^(2 cb) d_2) of its magnitude (mag <= 2^(c_s - 1) <= 2^(nsub cb)), window q at
+// sub[q][w T + u] (its sign carried along; DIGIT_NONE for 0).  Sub-digit values run 1 .. 2^cb (bucket
+// v - 1 of B = 2^cb): the one magnitude whose top sub-digit would be 2^cb, mag = 2^(nsub cb), is written
+// as top = 2^cb - 1 and 2^cb in the sub-digit below.  Two sub-digits while 2^(c_s / 2) <= BATCH_B_MAX
+// (c_s <= 17), three above (window widths 18-20 would otherwise need 512-1024 buckets).
+// (Round 4: two windows of 2^8 buckets instead of three of 2^6 at c_s = 17 -- a third fewer bucket
+// additions, the dominant cost of the IPA's switch to the tail rounds: 47M -> 31M at 2^20.)
+__global__ __launch_bounds__(256) void k_batch_subdigits(const uint32_t* digits, uint32_t TW, int cb, int nsub,
+                                                         uint32_t* sub) {
     const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= TW) return;
     const uint32_t d = digits[e];
     const uint32_t mag = d == DIGIT_NONE ? 0u : (d & 0x7fffffffu) + 1u, sign = d & 0x80000000u;
     const uint32_t full = 1u << cb;
-    uint32_t lo = mag & (full - 1u), hi = mag >> cb;
-    if (hi == full) {
-        hi = full - 1u;
-        lo += full;
+    uint32_t q[3];
+    q[0] = mag & (full - 1u);
+    q[1] = nsub == 2 ? mag >> cb : (mag >> cb) & (full - 1u);
+    q[2] = nsub == 2 ? 0u : mag >> (2 * cb);
+    if (q[nsub - 1] == full) {
+        q[nsub - 1] = full - 1u;
+        q[nsub - 2] += full;
     }
-    sub[e] = lo ? ((lo - 1u) | sign) : DIGIT_NONE;
-    sub[(size_t)TW + e] = hi ? ((hi - 1u) | sign) : DIGIT_NONE;
+    for (int k = 0; k < nsub; k++) sub[(size_t)k * TW + e] = q[k] ? ((q[k] - 1u) | sign) : DIGIT_NONE;
 }
 
 template <class Cv>
@@ -1107,16 +1109,17 @@ template <class Cv>
 static int msm_shared_batch_t(DeviceState* st, const uint4* bases, const uint4* w_ark, size_t T, size_t len,
                               uint4* out, bool xyzz_out, BatchScratch& S, hipStream_t s, size_t shift_stride, int c_s) {
     if (!T || !len) return set_error(HALO_EINVAL, "msm_shared_batch: empty batch");
-    // shifted: the lists run over TS = W_s T (copy, scalar) entries with two sub-digit windows of
-    // 2^cb buckets (magnitudes 1..2^(c_s-1) <= 2^(2 cb), k_batch_subdigits)
+    // shifted: the lists run over TS = W_s T (copy, scalar) entries with nsub sub-digit windows of
+    // 2^cb buckets (magnitudes 1..2^(c_s-1) <= 2^(nsub cb), k_batch_subdigits)
     const bool shifted = shift_stride && c_s && (T & (T - 1)) == 0 &&
                          (size_t)msm_windows(c_s) * shift_stride < (1ull << 31);
     const int W_s = shifted ? msm_windows(c_s) : 1;
-    const int cb = shifted ? c_s / 2 : 0;
+    const int nsub = (shifted && (1u << (c_s / 2)) > BATCH_B_MAX) ? 3 : 2;
+    const int cb = shifted ? (nsub == 2 ? c_s / 2 : (c_s + 1) / 3) : 0;
     // unshifted window bits: about T / 4 buckets per window, so that the per-window reduction
     // (2 B additions) stays below the accumulation (T mixed additions)
     const int c = shifted ? cb : std::max(5, std::min(BATCH_C_MAX, (int)ilog2(std::max<size_t>(T, 2)) - 1));
-    const int W = shifted ? 2 : msm_windows(c);
+    const int W = shifted ? nsub : msm_windows(c);
     const uint32_t B = shifted ? 1u << cb : 1u << (c - 1);
     const size_t TS = (size_t)W_s * T;
     const size_t SW = len * (size_t)W, NB = SW * B, E = SW * TS;
@@ -1149,7 +1152,7 @@ static int msm_shared_batch_t(DeviceState* st, const uint4* bases, const uint4* 
                            S.digits.as<uint32_t>(), T, 0, W_s);
         uint32_t* sub = S.digits.as<uint32_t>() + TS;
         hipLaunchKernelGGL(k_batch_subdigits, dim3(grid_for(TS, 256)), dim3(256), 0, s, S.digits.as<const uint32_t>(),
-                           (uint32_t)TS, cb, sub);
+                           (uint32_t)TS, cb, nsub, sub);
         lists_in = sub;
     } else {
         hipLaunchKernelGGL(k_digits<typename Cv::Scalar>, dim3(grid_for(T, 256)), dim3(256), 0, s, w_ark, T, c, W,
@@ -1551,6 +1554,10 @@ int srs_precompute_windows(DeviceState* st, int curve, hipStream_t s, int c, int
     if (w_lo < 0 || w_hi > W || w_lo >= w_hi)
         return set_error(HALO_EINVAL, "window range [%d, %d) outside [0, %d)", w_lo, w_hi, W);
     srs.shifted_c = srs.part_c = 0;  // nothing valid while the copies are rewritten
+    // asynchronous MSMs (halo_msm_srs_windows_dev, the pipelined MSM sets) and weighted IPA rounds on
+    // other streams may still be reading the copies: drain the device before they are rewritten or
+    // reallocated (a precompute is a setup step, never on a timed path)
+    HALO_HIP(hipDeviceSynchronize());
     HALO_CHECK(srs.shifted.reserve((size_t)(w_hi - w_lo) * srs.n * 64));
     ScratchUse su(st, s);
     HALO_CHECK(st->scratch[7].reserve(4));

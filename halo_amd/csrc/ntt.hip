@@ -26,22 +26,13 @@ namespace halo {
 
 constexpr int NTT_E = 1024;        // elements per workgroup for passes with R <= 256
 constexpr int NTT_E_BIG = 2048;    // ... and for the two-pass split of 2^17..2^22 (R up to 2048)
-constexpr int NTT_EPT = 4;         // elements per thread (radix-4 register groups) on 1024-element blocks
-// ... and on the 2048-element blocks of the 2^17..2^22 passes.  HALO_NTT_EPT_BIG=8 selects radix-8
-// register groups there (three stages per LDS round trip: an 11-bit pass makes 4 LDS round trips and
-// 4 barriers instead of 6), measured slower: 2^22 pair 1.05 -> 1.09 ms (192 VGPRs and 256-thread
-// blocks: 2 waves per SIMD instead of 4, so the barrier waits are hidden worse than they are saved)
-#ifndef HALO_NTT_EPT_BIG
-#define HALO_NTT_EPT_BIG 4
-#endif
-constexpr int NTT_EPT_BIG = HALO_NTT_EPT_BIG;
-constexpr int ntt_lg(int ept) { return ept == 8 ? 3 : 2; }
-#ifndef HALO_NTT_WAVE_SYNC
-#define HALO_NTT_WAVE_SYNC 1
-#endif
-constexpr bool NTT_WAVE_SYNC = HALO_NTT_WAVE_SYNC;
+// Elements per thread: radix-4 register groups, two stages per LDS round trip.  (Round 3 measured radix-8
+// groups on the 2048-element blocks -- 4 LDS round trips per 11-bit pass instead of 6 -- slower: 192 VGPRs
+// leave 2 waves per SIMD and the barrier waits were hidden worse than they were saved.)
+constexpr int NTT_EPT = 4;
 constexpr int NTT_MAX_LOG_R_MULTI = 8;
 constexpr int NTT_TW_MAX = 2048;  // stage-twiddle table entries (stages 0..10), read through L1/L2
+constexpr int NTT_TW_U4 = 3;      // one stage twiddle: its 9 limbs in a 48-B entry (no unpacking in the groups)
 constexpr unsigned NTT_FULL_TABLE_MAX_LOG = 24;  // per-pass twiddle tables up to 2^24
 
 struct NttPassArgs {
@@ -50,7 +41,7 @@ struct NttPassArgs {
     const uint4* tw;        // per-pass pre-twiddle table tw[rho * Ns + jj] (internal packed), or null
     const uint4* tw_hi;     // 2-level fallback (logn > NTT_FULL_TABLE_MAX_LOG)
     const uint4* tw_lo;
-    const uint4* stage_tw;  // entry 2^s - 1 + k = omega_{2^(s+1)}^k (s < 8, k < 2^s)
+    const uint4* stage_tw;  // entry 2^s - 1 + k = omega_{2^(s+1)}^k (s < 11, k < 2^s), NTT_TW_U4 uint4 each
     uint32_t logn, log_r, log_ns, lo_bits;
     uint32_t in_ark, out_ark;
     // pass 0 of a forward transform whose inputs beyond N / 2^prune are zero: the first `prune`
@@ -70,11 +61,12 @@ struct NttPassArgs {
 };
 
 // LDS layout: limb-major (SoA), limb l of position p at smem[l * NE + swz(p)].  swz XORs the bank
-// bits with a linear function of p >> 5, chosen (by exhaustive check over every access pattern of
-// the load, group and store phases, tools: see DESIGN.md) so that every ds_read_b32 / ds_write_b32
-// is conflict-free: for NE = 1024 over r = 1..8, for NE = 2048 over r = 9..11.  (A 4096-element
-// variant for 2 x 12-bit passes at 2^24 was measured 47 % slower than 3 x 8 bits: one 1024-thread
-// block per CU and 32-byte strided column loads; not kept.)
+// bits with a linear function of p >> 5, chosen so that every ds_read_b32 / ds_write_b32 of the load,
+// group and store phases is conflict-free (each half-wave's 32 positions on 32 banks): for NE = 1024
+// over r = 1..8, for NE = 2048 over r = 9..11 including the unit-twiddle thread order of ntt_unit_tau.
+// tools/ntt_swizzle.py enumerates the access patterns and checks / searches the constants.  (A
+// 4096-element variant for 2 x 12-bit passes at 2^24 was measured 47 % slower than 3 x 8 bits: one
+// 1024-thread block per CU and 32-byte strided column loads; not kept.)
 template <int NE>
 struct NttSwz;
 template <>
@@ -85,7 +77,7 @@ struct NttSwz<1024> {
 template <>
 struct NttSwz<2048> {
     static constexpr int NB = 6;
-    static constexpr uint32_t C[6] = {10, 29, 31, 20, 30, 17};
+    static constexpr uint32_t C[6] = {29, 22, 20, 23, 9, 19};
 };
 
 template <int NE>
@@ -113,145 +105,183 @@ HALO_DEV void lds_put_soa(uint32_t* s, uint32_t idx, uint32_t stride, const Fe<F
     for (int l = 0; l < NLIMB; l++) s[l * stride + idx] = a.v[l];
 }
 
-// x < 2^259 with normalized limbs -> x mod p in [0, 2p): subtract (q - 1) p with q = floor(x / 2^254)
-// (p = 2^254 + delta, delta < 2^126, for both Pasta fields).
-template <class C>
-HALO_DEV Fe<C> fe_reduce_q(const Fe<C>& x) {
-    const int32_t qm = 1 - (int32_t)(x.v[NLIMB - 1] >> 22);
-    Fe<C> r;
+// ---- signed lazy butterflies (round 5) ----------------------------------------------------------
+// Inside a pass a value is 9 signed int32 limbs (value = sum l_i 2^(29 i), congruent mod p to the
+// element; its magnitude stays below ~20 p).  A butterfly is one limb-wise add and one limb-wise
+// subtract (18 instructions: no carries, no multiple of p added), and the twiddle product fs_mul takes
+// the signed operand through v_mad_i64_i32 (gen_field_asm.py fe_muls_asm) and returns low limbs in
+// [0, 2^29) with a signed top limb.  Limb bounds, in units of 2^29 (low limbs; the top limb is bounded
+// by the value): a product or a normalized value lies in (-eps, 1 + eps), and u +- t widens the
+// interval by one, so three butterflies from normalized values leave (-3, 4) -- still int32 -- and a
+// product operand in (-2, 3) keeps every column below 9 x 3 x 2^58 (products) + 5 x 2^58 (reduction
+// terms) < 2^63.  So fs_norm (parallel carries, 3 instructions per limb) runs once per radix-4 group,
+// and the stage from the loads (G0 = 1) needs none.  Round 4's unsigned form spent a signed carry chain
+// with a 2p / 4p offset per subtraction and a carry chain per addition pair.
+template <class F>
+HALO_DEV Fe<F> fs_add(const Fe<F>& a, const Fe<F>& b) {
+    Fe<F> r;
+#pragma unroll
+    for (int i = 0; i < NLIMB; i++) r.v[i] = a.v[i] + b.v[i];
+    return r;
+}
+template <class F>
+HALO_DEV Fe<F> fs_sub(const Fe<F>& a, const Fe<F>& b) {
+    Fe<F> r;
+#pragma unroll
+    for (int i = 0; i < NLIMB; i++) r.v[i] = a.v[i] - b.v[i];
+    return r;
+}
+// a w with a signed-limb a (limbs in (-2, 3) x 2^29) and a normalized twiddle w (< 2p)
+template <class F>
+HALO_DEV Fe<F> fs_mul(const Fe<F>& a, const Fe<F>& w) {
+    Fe<F> r;
+    fe_muls_asm(a.v, w.v, NegP<F>::v, r.v);
+    return r;
+}
+// limbs (-3, 4) x 2^29 -> [-3, 2^29 + 3): each limb keeps its low 29 bits plus the carry of the limb
+// below (independent per limb, no chain); the top limb absorbs limb 7's carry
+template <class F>
+HALO_DEV Fe<F> fs_norm(const Fe<F>& a) {
+    Fe<F> r;
+    r.v[0] = a.v[0] & LIMB_MASK;
+#pragma unroll
+    for (int i = 1; i < NLIMB; i++) {
+        const uint32_t c = (uint32_t)((int32_t)a.v[i - 1] >> LIMB_BITS);
+        r.v[i] = ((i == NLIMB - 1) ? a.v[i] : (a.v[i] & LIMB_MASK)) + c;
+    }
+    return r;
+}
+// limbs (-4, 4) x 2^29 -> exactly normalized low limbs [0, 2^29) (one signed carry chain; the top limb
+// takes the final carry)
+template <class F>
+HALO_DEV Fe<F> fs_carry(const Fe<F>& a) {
+    Fe<F> r;
+    int32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < NLIMB - 1; i++) {
+        const int32_t x = (int32_t)a.v[i] + c;
+        r.v[i] = (uint32_t)x & LIMB_MASK;
+        c = x >> LIMB_BITS;
+    }
+    r.v[NLIMB - 1] = a.v[NLIMB - 1] + (uint32_t)c;
+    return r;
+}
+// signed lazy value (limbs in (-3, 4) x 2^29) -> the same residue, non-negative with normalized limbs
+// and below 2^255 + 2^235 (< 4p, so it packs into 32 B): subtract (q - 1) p with q = floor(top limb /
+// 2^22), within one of floor(value / 2^254) (p = 2^254 + delta, delta < 2^126), in one signed carry chain
+template <class F>
+HALO_DEV Fe<F> fs_settle(const Fe<F>& x) {
+    const int32_t qm = 1 - ((int32_t)x.v[NLIMB - 1] >> 22);
+    Fe<F> r;
     int64_t c = 0;
 #pragma unroll
     for (int i = 0; i < NLIMB; i++) {
-        int64_t d = (int64_t)x.v[i] + c;
-        if (C::P[i] != 0) d += (int64_t)qm * (int64_t)C::P[i];
+        int64_t d = (int64_t)(int32_t)x.v[i] + c;
+        if (F::P[i] != 0) d += (int64_t)qm * (int64_t)F::P[i];
         r.v[i] = (i == NLIMB - 1) ? (uint32_t)d : ((uint32_t)d & LIMB_MASK);
         c = d >> LIMB_BITS;
     }
     return r;
 }
 
-// G radix-2 DIT stages s .. s+G-1 over the EPT register-resident elements at positions base + m 2^s
-// (m < EPT).  Stage s' pairs m and m + 2^(s'-s) and multiplies the upper element by
-// omega_{2^(s'+1)}^k, k = (base + m 2^s) mod 2^s'.  Lazy reduction: values entering a pass are < 4p
-// (< 2p except raw ark words), stage 0 doubles that bound, every later stage adds at most 2p
-// (u + t and u - t + 2p with t = v w < 2p), so after 8 stages they are < 22p: still valid
-// Montgomery inputs (< 64p), reduced once at the end of the pass (fe_reduce_q, < 32p).
-// K0ZERO: k0 == 0 (the pass's first group, from the global loads): the butterflies with k = 0 have
-// twiddle omega^0 = 1 and skip their multiplication (stage 1: one of the thread's two)
-template <class F, int EPT, int LG, bool K0ZERO = false>
-HALO_DEV void ntt_group(Fe<F> (&v)[EPT], uint32_t s, uint32_t G, uint32_t k0, const uint4* twg) {
+// The pass's first G0 <= 2 stages on the thread's EPT consecutive positions, straight from the loads:
+// stage 0's twiddles are 1; stage 1 pairs (0, 2) with twiddle 1 and (1, 3) with omega_4 (w4).  With
+// G0 = 2 the results are normalized (two more stages follow before the next fs_norm); with G0 = 1 not.
+template <class F>
+HALO_DEV void ntt_first(Fe<F> (&v)[NTT_EPT], uint32_t G0, const uint4* twg) {
 #pragma unroll
-    for (int g = 0; g < LG; g++) {
-        if ((uint32_t)g >= G) break;
-        const uint32_t sp = s + (uint32_t)g;
+    for (int m = 0; m < NTT_EPT; m += 2) {
+        const Fe<F> t = v[m + 1];
+        v[m + 1] = fs_sub(v[m], t);
+        v[m] = fs_add(v[m], t);
+    }
+    if (G0 > 1) {
+        Fe<F> w4;
+        const uint32_t* e = (const uint32_t*)(twg + NTT_TW_U4 * 2);
 #pragma unroll
-        for (int m = 0; m < EPT; m++) {
-            if (m & (1 << g)) continue;
-            const int m2 = m + (1 << g);
-            Fe<F> t = v[m2];
-            const bool unit = K0ZERO && sp != 0 && (m & ((1 << g) - 1)) == 0;
-            if (sp != 0 && !unit) {
-                const uint32_t k = k0 + ((uint32_t)(m & ((1 << g) - 1)) << s);
-                t = fe_mul(t, fe_load<F>(twg + 2 * ((1u << sp) - 1u + k)));
-            }
-            // stage 0 (no multiplication): t is a pass input, < 4p even for non-canonical ark words;
-            // a unit-twiddle butterfly at stage 1 takes t < 8p unmultiplied (its sums < 16p, so after
-            // 8 stages the bound is 28p instead of 22p: still < 32p for fe_reduce_q)
-            v[m2] = (sp == 0) ? fe_sub_k<4>(v[m], t) : unit ? fe_sub_k<8>(v[m], t) : fe_sub_k<2>(v[m], t);
-            v[m] = fe_norm(fe_add_nc(v[m], t));
-        }
+        for (int l = 0; l < NLIMB; l++) w4.v[l] = e[l];
+        Fe<F> t = v[2];
+        v[2] = fs_sub(v[0], t);
+        v[0] = fs_add(v[0], t);
+        t = fs_mul(v[3], w4);
+        v[3] = fs_sub(v[1], t);
+        v[1] = fs_add(v[1], t);
+#pragma unroll
+        for (int m = 0; m < NTT_EPT; m++) v[m] = fs_norm(v[m]);
     }
 }
 
-// The stage twiddles one thread needs for a radix-4 group at stages s, s + 1 (LG = 2, EPT = 4):
-// stage s uses omega_{2^(s+1)}^k0 for both of its butterflies, stage s + 1 omega_{2^(s+2)}^(k0) and
-// ^(k0 + 2^s).  Loaded packed (3 x 32 B) BEFORE the barrier that precedes the group's LDS reads, so
-// the L2 round trip of the table overlaps the barrier wait instead of following it.
-// (LG = 3: stage s + 2 omega_{2^(s+3)}^(k0 + j 2^s), j < 4, as well: 7 twiddles)
-template <int LG>
+// The stage twiddles one thread needs for a radix-4 group at stages s, s + 1: stage s uses
+// omega_{2^(s+1)}^k0 for both of its butterflies, stage s + 1 omega_{2^(s+2)}^(k0) and ^(k0 + 2^s).
+// Loaded (9 limbs each) BEFORE the barrier that precedes the group's LDS reads, so the L2 round trip of
+// the table overlaps the barrier wait instead of following it.
 struct NttGroupTw {
-    uint4 w[(1 << LG) - 1][2];
+    uint32_t w[3][NLIMB];
 };
-template <int LG>
-HALO_DEV void ntt_group_tw_load(NttGroupTw<LG>& t, uint32_t s, uint32_t G, uint32_t k0, const uint4* twg) {
-    // stage s + g: omega_{2^(s+g+1)}^(k0 + j 2^s), j < 2^g, at entry 2^(s+g) - 1 + k0 + j 2^s
+HALO_DEV void ntt_group_tw_load(NttGroupTw& t, uint32_t s, uint32_t G, uint32_t k0, const uint4* twg) {
 #pragma unroll
-    for (int g = 0; g < LG; g++) {
+    for (int g = 0; g < 2; g++) {
         if ((uint32_t)g >= G) break;
 #pragma unroll
         for (int j = 0; j < (1 << g); j++) {
             const uint32_t i = ((1u << (s + g)) - 1u) + k0 + ((uint32_t)j << s);
-            t.w[(1 << g) - 1 + j][0] = twg[2 * i];
-            t.w[(1 << g) - 1 + j][1] = twg[2 * i + 1];
+            const uint4* e = twg + NTT_TW_U4 * i;
+            const uint4 x = e[0], y = e[1];
+            uint32_t* w = t.w[(1 << g) - 1 + j];
+            w[0] = x.x, w[1] = x.y, w[2] = x.z, w[3] = x.w;
+            w[4] = y.x, w[5] = y.y, w[6] = y.z, w[7] = y.w;
+            w[8] = ((const uint32_t*)e)[8];
         }
     }
 }
 template <class F>
-HALO_DEV Fe<F> ntt_tw_unpack(const uint4 (&w)[2]) {
-    uint32_t x[8] = {w[0].x, w[0].y, w[0].z, w[0].w, w[1].x, w[1].y, w[1].z, w[1].w};
-    return fe_unpack<F>(x);
-}
-// ntt_group for EPT = 4, LG = 2, s >= 1 with the twiddles already loaded (same arithmetic and value
-// bounds).  The first stage's sums stay limb-unnormalized (limbs < 2^30): the second stage takes them
-// as a multiplication input (a column of 9 products < 2^59 plus the reduction stays < 2^63) or as the
-// minuend of fe_sub_k (int32 limb chain, |x| < 2^31), and only the values leaving the group are
-// carry-normalized -- two fe_norm per group instead of four.
-template <class F>
-HALO_DEV void ntt_group4_pre(Fe<F> (&v)[4], uint32_t G, const NttGroupTw<2>& t) {
-    {
-        const Fe<F> w = ntt_tw_unpack<F>(t.w[0]);
+HALO_DEV Fe<F> ntt_tw(const uint32_t (&w)[NLIMB]) {
+    Fe<F> r;
 #pragma unroll
-        for (int m = 0; m < 4; m += 2) {
-            const Fe<F> x = fe_mul(v[m + 1], w);
-            v[m + 1] = fe_sub_k<2>(v[m], x);
-            v[m] = fe_add_nc(v[m], x);
-        }
+    for (int l = 0; l < NLIMB; l++) r.v[l] = w[l];
+    return r;
+}
+
+// Radix-4 group at stages s, s + 1 (s >= 1) with the twiddles already loaded.  UNIT: k0 = 0, so the
+// twiddles of stage s and of stage s + 1's first pair are 1 (the wave-uniform unit group of
+// ntt_unit_tau: three of the four multiplications skipped).  An unmultiplied butterfly operand keeps
+// its own limb interval instead of a product's [0, 1), so the unit group first carries its inputs
+// exactly: v0 + v1 + v2 + v3 then stays below 4 (2^29 - 1) < 2^31.  norm: normalize the outputs (every
+// group except, when the output path multiplies nothing, the pass's last).
+template <class F, bool UNIT>
+HALO_DEV void ntt_group4(Fe<F> (&v)[NTT_EPT], uint32_t G, const NttGroupTw& t, bool norm) {
+    if (UNIT) {
+#pragma unroll
+        for (int m = 0; m < NTT_EPT; m++) v[m] = fs_carry(v[m]);
+    }
+#pragma unroll
+    for (int m = 0; m < NTT_EPT; m += 2) {
+        const Fe<F> x = UNIT ? v[m + 1] : fs_mul(v[m + 1], ntt_tw<F>(t.w[0]));
+        v[m + 1] = fs_sub(v[m], x);
+        v[m] = fs_add(v[m], x);
     }
     if (G > 1) {
+        Fe<F> x = UNIT ? v[2] : fs_mul(v[2], ntt_tw<F>(t.w[1]));
+        v[2] = fs_sub(v[0], x);
+        v[0] = fs_add(v[0], x);
+        x = fs_mul(v[3], ntt_tw<F>(t.w[2]));
+        v[3] = fs_sub(v[1], x);
+        v[1] = fs_add(v[1], x);
+    }
+    if (norm) {
 #pragma unroll
-        for (int m = 0; m < 2; m++) {
-            const Fe<F> x = fe_mul(v[m + 2], ntt_tw_unpack<F>(t.w[1 + m]));
-            v[m + 2] = fe_sub_k<2>(v[m], x);
-            v[m] = fe_norm(fe_add_nc(v[m], x));
-        }
-    } else {
-        v[0] = fe_norm(v[0]);
-        v[2] = fe_norm(v[2]);
+        for (int m = 0; m < NTT_EPT; m++) v[m] = fs_norm(v[m]);
     }
 }
 
-// The radix-8 group (EPT = 8, three stages s, s + 1, s + 2; always full on the 2048-element blocks:
-// the host splits every such pass so that r - G0 and r - prune are multiples of 3).  Same arithmetic
-// and value bounds as ntt_group: stage s's sums stay limb-unnormalized (limbs < 2^30; they enter stage
-// s + 1 only as multiplication inputs or fe_sub_k minuends), stage s + 1's and s + 2's sums are
-// carry-normalized.
-template <class F>
-HALO_DEV void ntt_group8_pre(Fe<F> (&v)[8], const NttGroupTw<3>& t) {
-    {
-        const Fe<F> w = ntt_tw_unpack<F>(t.w[0]);
-#pragma unroll
-        for (int m = 0; m < 8; m += 2) {
-            const Fe<F> x = fe_mul(v[m + 1], w);
-            v[m + 1] = fe_sub_k<2>(v[m], x);
-            v[m] = fe_add_nc(v[m], x);
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < 2; j++) {
-        const Fe<F> w = ntt_tw_unpack<F>(t.w[1 + j]);
-#pragma unroll
-        for (int m = j; m < 8; m += 4) {
-            const Fe<F> x = fe_mul(v[m + 2], w);
-            v[m + 2] = fe_sub_k<2>(v[m], x);
-            v[m] = fe_norm(fe_add_nc(v[m], x));
-        }
-    }
-#pragma unroll
-    for (int m = 0; m < 4; m++) {
-        const Fe<F> x = fe_mul(v[m + 4], ntt_tw_unpack<F>(t.w[3 + m]));
-        v[m + 4] = fe_sub_k<2>(v[m], x);
-        v[m] = fe_norm(fe_add_nc(v[m], x));
-    }
+// Thread order of the stage-1 group on one-column 2048-element blocks (the 11-bit passes of 2^21 and
+// 2^22): the group's position bit 0 -- its twiddle index k0 -- comes from thread bit 8, i.e. from the
+// wave (waves 0-3: k0 = 0, unit twiddles; waves 4-7: k0 = 1), so the skip is wave-uniform, and each SIMD
+// holds one unit and one full wave of the block (waves w and w + 4 share a SIMD,
+// MI355X_MICROARCH.md LDS).  Saves 3 of the group's 4 multiplications in half the waves: 0.375
+// multiplications per element per pass.
+HALO_DEV uint32_t ntt_unit_tau(uint32_t tau) {
+    return ((tau << 1) | (tau >> 8)) & 511u;
 }
 
 // raw workgroup barrier: LDS writes complete, global loads left in flight (a __syncthreads() would
@@ -264,12 +294,12 @@ HALO_DEV void ntt_lds_barrier(bool wave_only = false) {
 }
 
 // One Stockham pass: R = 2^log_r point DFTs over the columns j of the N/R x R view.  A workgroup
-// owns T = NTT_E / R consecutive columns.  Each thread holds EPT elements in registers; the first
-// LG stages are done straight from the global loads, the rest in groups of LG stages through LDS,
-// and a final coalesced store phase writes y[(j / Ns) Ns R + (j mod Ns) + k Ns].
-template <class F, int NE, int EPT>
-__global__ __launch_bounds__(NE / EPT) void k_ntt_pass(NttPassArgs a) {
-    constexpr int LG = ntt_lg(EPT);
+// owns T = NE / R consecutive columns.  Each thread holds EPT elements in registers; the first
+// G0 stages are done straight from the global loads, the rest in radix-4 groups through LDS, and a
+// final coalesced store phase writes y[(j / Ns) Ns R + (j mod Ns) + k Ns].
+template <class F, int NE>
+__global__ __launch_bounds__(NE / NTT_EPT) void k_ntt_pass(NttPassArgs a) {
+    constexpr int EPT = NTT_EPT;
     constexpr uint32_t TH = NE / EPT;
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t* data = smem;
@@ -289,7 +319,7 @@ __global__ __launch_bounds__(NE / EPT) void k_ntt_pass(NttPassArgs a) {
     uint4* out = a.out + (size_t)blockIdx.y * a.stride * 2;
     const uint32_t tau = threadIdx.x;
 
-    // ---- load + pre-twiddle + first LG stages (positions base + m)
+    // ---- load + pre-twiddle + first G0 stages (positions base + m)
     uint32_t base;
     if (R >= (uint32_t)EPT) {
         const uint32_t q = tau / T, t = tau % T;
@@ -313,7 +343,7 @@ __global__ __launch_bounds__(NE / EPT) void k_ntt_pass(NttPassArgs a) {
                 Fe<F> oc;
 #pragma unroll
                 for (int l = 0; l < NLIMB; l++) oc.v[l] = a.out_const[l];
-                x = fe_mul(x, oc);
+                x = fs_mul(x, oc);
             }
             if (!a.in_ark && a.log_ns != 0 && rho != 0) {
                 const size_t jj = j & (Ns - 1);
@@ -327,39 +357,47 @@ __global__ __launch_bounds__(NE / EPT) void k_ntt_pass(NttPassArgs a) {
                     const size_t eh = e >> a.lo_bits;
                     if (eh) w = fe_mul(w, fe_load<F>(a.tw_hi + 2 * eh));
                 }
-                x = fe_mul(x, w);
+                x = fs_mul(x, w);
             }
             v[m] = x;
         } else {
             v[m] = fe_zero<F>();
         }
     }
-    // on the wide blocks the short group goes first (r mod LG stages), so later groups stay in range
-    const uint32_t G0 = (NE >= NTT_E_BIG && (r % LG)) ? r % LG : (r < (uint32_t)LG ? r : (uint32_t)LG);
-    if (!a.prune) ntt_group<F, EPT, LG, true>(v, 0, G0, 0, a.stage_tw);  // (pruned: host guarantees prune >= G0)
+    // on the wide blocks the short group goes first (r mod 2 stages), so later groups stay in range
+    const uint32_t G0 = (NE >= NTT_E_BIG && (r & 1)) ? 1u : (r < 2u ? r : 2u);
+    if (!a.prune) ntt_first<F>(v, G0, a.stage_tw);  // (pruned: host guarantees prune >= G0)
     {
         const uint32_t pb = ntt_swz<NE>(base);
 #pragma unroll
         for (int m = 0; m < EPT; m++)
             if (base + m < EB) lds_put_soa(data, pb ^ (uint32_t)m, NE, v[m]);
     }
-    // ---- remaining stages in groups of LG through LDS; each group's twiddles are loaded before the
+    // ---- remaining stages in radix-4 groups through LDS; each group's twiddles are loaded before the
     // barrier that precedes its LDS reads
+    const bool unit_blocks = NE == NTT_E_BIG && T == 1u;
+    // wave-uniform: thread bit 8 (NE = 2048 blocks have 512 threads)
+    const bool unit_wave = unit_blocks && (__builtin_amdgcn_readfirstlane(tau) >> 8) == 0u;
+    // the output path multiplies unless the last pass's pre-twiddle table carries out_const
+    const bool out_mul = a.out_ark && !a.out_scaled;
     uint32_t s = a.prune ? a.prune : G0;
-    NttGroupTw<LG> tw;
-    if (s < r) ntt_group_tw_load(tw, s, (r - s) < (uint32_t)LG ? (r - s) : (uint32_t)LG, tau & ((1u << s) - 1),
-                                 a.stage_tw);
+    NttGroupTw tw;
+    {
+        const uint32_t tt = (unit_blocks && s == 1) ? ntt_unit_tau(tau) : tau;
+        if (s < r) ntt_group_tw_load(tw, s, (r - s) < 2u ? (r - s) : 2u, tt & ((1u << s) - 1), a.stage_tw);
+    }
     // Wave-local exchanges: a group at stage s <= 6 (2^s <= 64) reads and writes exactly its wave's
     // chunk of EPT * 64 consecutive positions [EPT 64 w, EPT 64 (w + 1)), and so does the load phase
     // of a one-column block (base = EPT tau); between two such phases the wave only waits for its own
-    // LDS writes (HALO_NTT_WAVE_SYNC=0 A/B: s_barrier everywhere).
-    const bool wave_sync = NTT_WAVE_SYNC && (T == 1u || R < (uint32_t)EPT);
-    bool chunk = wave_sync;
-    ntt_lds_barrier(chunk && s < r && s <= 6);
-    for (; s < r; s += LG) {
-        const uint32_t G = (r - s) < (uint32_t)LG ? (r - s) : (uint32_t)LG;
+    // LDS writes.  (The stage-1 unit order of ntt_unit_tau spans the block: full barriers around it.)
+    auto wave_local = [&](uint32_t sg) { return sg <= 6u && !(unit_blocks && sg == 1u); };
+    ntt_lds_barrier((T == 1u || R < (uint32_t)EPT) && s < r && wave_local(s));
+    for (; s < r; s += 2) {
+        const uint32_t G = (r - s) < 2u ? (r - s) : 2u;
         const uint32_t h = 1u << s;
-        const uint32_t gb = (tau & (h - 1)) | ((tau >> s) << (s + LG));
+        const bool unit_grp = unit_blocks && s == 1;
+        const uint32_t tt = unit_grp ? ntt_unit_tau(tau) : tau;
+        const uint32_t gb = (tt & (h - 1)) | ((tt >> s) << (s + 2));
         const uint32_t shb = ntt_swz_hi<NE>(gb >> 5);
 #pragma unroll
         for (int m = 0; m < EPT; m++) {
@@ -367,10 +405,11 @@ __global__ __launch_bounds__(NE / EPT) void k_ntt_pass(NttPassArgs a) {
             const uint32_t ph = (pos ^ shb) ^ ntt_swz_hi<NE>(((uint32_t)m * h) >> 5);
             if (pos < EB) v[m] = lds_get_soa<F>(data, ph, NE);
         }
-        if constexpr (LG == 3)
-            ntt_group8_pre<F>(v, tw);  // (G == 3 on every group, see G0)
+        const bool norm = s + 2 < r || out_mul;
+        if (unit_grp && unit_wave)
+            ntt_group4<F, true>(v, G, tw, norm);
         else
-            ntt_group4_pre<F>(v, G, tw);
+            ntt_group4<F, false>(v, G, tw, norm);
         // (no barrier here: a thread writes back exactly the positions it read)
 #pragma unroll
         for (int m = 0; m < EPT; m++) {
@@ -378,18 +417,15 @@ __global__ __launch_bounds__(NE / EPT) void k_ntt_pass(NttPassArgs a) {
             const uint32_t ph = (pos ^ shb) ^ ntt_swz_hi<NE>(((uint32_t)m * h) >> 5);
             if (pos < EB) lds_put_soa(data, ph, NE, v[m]);
         }
-        const uint32_t sn = s + LG;
-        if (sn < r)
-            ntt_group_tw_load(tw, sn, (r - sn) < (uint32_t)LG ? (r - sn) : (uint32_t)LG, tau & ((1u << sn) - 1),
-                              a.stage_tw);
-        chunk = NTT_WAVE_SYNC && s <= 6;
-        ntt_lds_barrier(chunk && sn < r && sn <= 6);
+        const uint32_t sn = s + 2;
+        if (sn < r) {
+            const uint32_t tn = (unit_blocks && sn == 1) ? ntt_unit_tau(tau) : tau;
+            ntt_group_tw_load(tw, sn, (r - sn) < 2u ? (r - sn) : 2u, tn & ((1u << sn) - 1), a.stage_tw);
+        }
+        ntt_lds_barrier(wave_local(s) && sn < r && wave_local(sn));
     }
 
     // ---- store y[(j / Ns) Ns R + (j mod Ns) + k Ns]
-    Fe<F> oc;
-#pragma unroll
-    for (int l = 0; l < NLIMB; l++) oc.v[l] = a.out_const[l];
 #pragma unroll
     for (int i = 0; i < EPT; i++) {
         const uint32_t idx = tau + TH * (uint32_t)i;
@@ -406,9 +442,15 @@ __global__ __launch_bounds__(NE / EPT) void k_ntt_pass(NttPassArgs a) {
         const size_t dst = ((j >> a.log_ns) << (a.log_ns + r)) + (j & (Ns - 1)) + (size_t)k * Ns;
         Fe<F> x = lds_get_soa<F>(data, ntt_swz<NE>(t * R + k), NE);
         if (a.out_ark) {
-            fe_store(out + 2 * dst, fe_canon(a.out_scaled ? fe_reduce_q(x) : fe_mul(x, oc)));
+            if (out_mul) {
+                Fe<F> oc;
+#pragma unroll
+                for (int l = 0; l < NLIMB; l++) oc.v[l] = a.out_const[l];
+                x = fs_mul(x, oc);
+            }
+            fe_store(out + 2 * dst, fe_canon(fe_reduce_2p(fs_settle(x))));
         } else {
-            fe_store(out + 2 * dst, fe_reduce_q(x));
+            fe_store(out + 2 * dst, fs_settle(x));
         }
     }
 }
@@ -443,6 +485,25 @@ __global__ void k_pow_table(uint4* out, size_t count, Fe<F> base, uint64_t step)
         e >>= 1;
     }
     fe_store(out + 2 * i, r);
+}
+
+// Stage twiddles omega^k, k < count, as 9 limbs in NTT_TW_U4 uint4 (limbs 0..8, then zero padding)
+template <class F>
+__global__ void k_stage_twiddles(uint4* out, size_t count, Fe<F> base) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    uint64_t e = i;
+    Fe<F> r = fe_one<F>();
+    Fe<F> b = base;
+    while (e) {
+        if (e & 1) r = fe_mul(r, b);
+        b = fe_sqr(b);
+        e >>= 1;
+    }
+    uint4* o = out + NTT_TW_U4 * i;
+    o[0] = make_uint4(r.v[0], r.v[1], r.v[2], r.v[3]);
+    o[1] = make_uint4(r.v[4], r.v[5], r.v[6], r.v[7]);
+    o[2] = make_uint4(r.v[8], 0u, 0u, 0u);
 }
 
 // Reduce coefficients mod X^N - 1: out[i] = sum_k in[i + kN] (ark format in and out).
@@ -562,7 +623,7 @@ static std::vector<unsigned> ntt_radices(unsigned logn) {
 static unsigned ntt_pass0_prune(unsigned lr, unsigned prune) {
     if (!prune) return 0;
     const bool big = lr > NTT_MAX_LOG_R_MULTI;
-    const unsigned lg = big ? (unsigned)ntt_lg(NTT_EPT_BIG) : 2u;
+    const unsigned lg = 2u;
     const unsigned g0 = (big && (lr % lg)) ? lr % lg : std::min(lr, lg);
     unsigned pr = std::min(prune, lr);
     while (big && pr > 0 && ((lr - pr) % lg)) pr--;
@@ -589,10 +650,13 @@ static int get_twiddles(DeviceState* st, int field, unsigned logn, int inverse, 
     HALO_CHECK(launch_pow_table<F>(t->lo.as<uint4>(), nlo, w, 1, s));
     HALO_CHECK(launch_pow_table<F>(t->hi.as<uint4>(), nhi, w, (uint64_t)nlo, s));
     // stage twiddles omega_{2^(s+1)}^k (the same for every N; kept per table for simplicity)
-    HALO_CHECK(t->stage.reserve(NTT_TW_MAX * 32));
+    HALO_CHECK(t->stage.reserve(NTT_TW_MAX * NTT_TW_U4 * 16));
     for (unsigned sg = 0; sg < NTT_MAX_LOG_R_BIG; sg++) {
         const Fe<F> ws = host_fe<F>(inverse ? F::OMEGA_INV[sg + 1] : F::OMEGA[sg + 1]);
-        HALO_CHECK(launch_pow_table<F>(t->stage.as<uint4>() + 2 * (((size_t)1 << sg) - 1), (size_t)1 << sg, ws, 1, s));
+        const size_t cnt = (size_t)1 << sg;
+        hipLaunchKernelGGL(k_stage_twiddles<F>, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s,
+                           t->stage.as<uint4>() + NTT_TW_U4 * (cnt - 1), cnt, ws);
+        HALO_HIP(hipGetLastError());
     }
     // per-pass pre-twiddle tables (one multiplication per element instead of two)
     if (logn <= NTT_FULL_TABLE_MAX_LOG) {
@@ -672,9 +736,9 @@ static int ntt_device(DeviceState* st, int field, const void* d_in, void* d_out,
         dim3 grid((unsigned)(NJ / T), (unsigned)batch);
         ProfScope prof("ntt_pass", s);
         if (NE == NTT_E_BIG)
-            HALO_LAUNCH(prof, (k_ntt_pass<F, NTT_E_BIG, NTT_EPT_BIG>), grid, dim3(NTT_E_BIG / NTT_EPT_BIG), lds, s, a);
+            HALO_LAUNCH(prof, (k_ntt_pass<F, NTT_E_BIG>), grid, dim3(NTT_E_BIG / NTT_EPT), lds, s, a);
         else
-            HALO_LAUNCH(prof, (k_ntt_pass<F, NTT_E, NTT_EPT>), grid, dim3(NTT_E / NTT_EPT), lds, s, a);
+            HALO_LAUNCH(prof, (k_ntt_pass<F, NTT_E>), grid, dim3(NTT_E / NTT_EPT), lds, s, a);
         HALO_HIP(hipGetLastError());
         log_ns += lr;
     }

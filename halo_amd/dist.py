@@ -302,6 +302,17 @@ def sharded_poly_eval(coeffs_local, n_total: int, z, dist, ops: PolyOps | None =
 # sums them on the device, and every rank runs the same transcript.  After lg(n / P) rounds each
 # rank holds one element; the P elements are all-gathered (global order j = r) and the last lg P
 # rounds run on one session, replicated on every rank (all ranks return the same proof).
+#
+# Two kinds of shard session (round 5):
+#  * weighted (GpuWeightedIpaOps, the default on GPUs): the rank's resident SRS IS its shard
+#    G[r::P] (uploaded with its window-shifted copies, as a rank of a sharded deployment holds it), so
+#    the shard runs the single-GPU weighted rounds (n/2-term MSMs over the resident copies, no fold of
+#    G).  Its z-vector z^(i P + r) = z^r (z^P)^i is the session's powers of z^P with the factor z^r
+#    moved onto the hiding point: H'_r = z^r H' (the dots <c, z> are linear in z), and the shard's final
+#    z is z^r times the session's folded one.
+#  * explicit vectors (GpuIpaOps): G, c, z of the shard handed over (halo_ipa_begin_vectors), G folded
+#    by GLV scalar multiplications every round -- the collapsed final rounds, and shards of an SRS that
+#    is not resident.
 # ---------------------------------------------------------------------------------------------
 def ipa_shard(vec, rank: int, world: int):
     """Rank r's strided shard vec[r::P] of an IPA vector."""
@@ -309,9 +320,11 @@ def ipa_shard(vec, rank: int, world: int):
 
 
 class IpaOps:
-    """Per-rank session primitives the distributed opening is written against."""
+    """Per-rank session primitives the distributed opening is written against.  ``shard`` is the
+    ops' own description of one rank's part (explicit (gs, cs, zs) vectors, or (cs, z) over a
+    resident SRS shard)."""
 
-    def begin(self, gs, cs, zs, H_prime):
+    def begin(self, shard, H_prime):
         raise NotImplementedError
 
     def round_lr(self, ses):  # -> (L, R) WrappedPoints of this shard (H' terms included)
@@ -326,14 +339,26 @@ class IpaOps:
     def point_sum(self, pts):  # (k, 8) WrappedPoints -> (8,)
         raise NotImplementedError
 
+    def begin_vectors(self, gs, cs, zs, H_prime):  # the collapsed final rounds' session
+        return self.begin((gs, cs, zs), H_prime)
+
+    def final_vectors(self, ses):  # ... and its folded element
+        return self.final(ses)
+
+    def shard_len(self, shard) -> int:
+        return len(shard[1])
+
 
 class GpuIpaOps(IpaOps):
+    """Shard sessions over explicit vectors: shard = (gs, cs, zs)."""
+
     def __init__(self, curve="pallas"):
         self.curve = curve
 
-    def begin(self, gs, cs, zs, H_prime):
+    def begin(self, shard, H_prime):
         from .pcdl import IpaSession
 
+        gs, cs, zs = shard
         return IpaSession.from_vectors(gs, cs, zs, H_prime, self.curve)
 
     def round_lr(self, ses):
@@ -353,37 +378,108 @@ class GpuIpaOps(IpaOps):
         return point_sum(pts, self.curve)
 
 
-def _ipa_loop(sessions, ops: IpaOps, gather, challenge, inverse, xi, Ls, Rs, rounds: int):
+class GpuWeightedIpaOps(GpuIpaOps):
+    """Shard sessions over the rank's resident SRS shard G[rank::world] (weighted rounds):
+    shard = (cs_shard, z) with z the opening point (ark scalar)."""
+
+    def __init__(self, curve, rank: int, world: int):
+        super().__init__(curve)
+        self.rank, self.world = rank, world
+
+    def _field(self):
+        return "fp" if self.curve in ("pallas", 0) else "fq"
+
+    def _pow(self, z, e: int):
+        from . import _lib as H
+        from .group import _field
+
+        zz = H.fe_array(z, 1)
+        out = np.zeros((1, 4), dtype=np.uint64)
+        H.check(H.load().halo_evals_op(_field(self._field()), 6, H.ptr(zz), None, None, e, H.ptr(out), 1))
+        return out[0]
+
+    def begin(self, shard, H_prime):
+        from .group import point_dot_affine
+        from .pcdl import IpaSession
+
+        cs, z = shard
+        z_r = self._pow(z, self.rank)
+        hp = np.asarray(H_prime, dtype=np.uint64).reshape(1, 8)
+        h_r = hp[0] if self.rank == 0 else point_dot_affine(z_r.reshape(1, 4), hp, self.curve)
+        ses = IpaSession(cs, self._pow(z, self.world), h_r, self.curve)
+        ses._z_r = z_r
+        return ses
+
+    def final(self, ses):
+        from .group import scalar_dot
+
+        _, _, cs, zs = ses.state(with_gs=False)
+        U, c = ses.end()
+        z = scalar_dot(ses._z_r.reshape(1, 4), zs[:1], self._field())
+        return U.reshape(1, 8), c.reshape(1, 4), np.asarray(z, dtype=np.uint64).reshape(1, 4)
+
+    def begin_vectors(self, gs, cs, zs, H_prime):
+        return GpuIpaOps.begin(self, (gs, cs, zs), H_prime)
+
+    def final_vectors(self, ses):
+        return GpuIpaOps.final(self, ses)
+
+    def shard_len(self, shard) -> int:
+        return len(shard[0])
+
+
+def ipa_shard_steps(ops: IpaOps, shard, H_prime, rounds: int):
+    """One rank's shard session as a generator: yields (L_r, R_r) each round, receives (xi, xi_inv),
+    returns the fully folded (g, c, z) element."""
+    ses = ops.begin(shard, H_prime)
     for _ in range(rounds):
-        parts = gather([ops.round_lr(s) for s in sessions])
-        L = ops.point_sum(np.stack([p[0] for p in parts]))
-        R = ops.point_sum(np.stack([p[1] for p in parts]))
+        xi, xi_inv = yield ops.round_lr(ses)
+        ops.fold(ses, xi, xi_inv)
+    return ops.final(ses)
+
+
+def _drive(gens, reduce_lr, challenge, inverse, xi, Ls, Rs, rounds: int):
+    lrs = [next(g) for g in gens]
+    finals = []
+    for k in range(rounds):
+        L, R = reduce_lr(lrs)
         Ls.append(L)
         Rs.append(R)
         xi = challenge(xi, L, R)
         xinv = inverse(xi)
-        for s in sessions:
-            ops.fold(s, xi, xinv)
-    return xi
+        lrs = []
+        for g in gens:
+            try:
+                lrs.append(g.send((xi, xinv)))
+            except StopIteration as e:
+                finals.append(e.value)
+    return xi, finals
 
 
 def sharded_ipa_rounds(local_shards, H_prime, challenge: Callable, inverse: Callable, ops: IpaOps, world: int,
-                       gather: Callable):
-    """Distributed pcdl round loop.  ``local_shards``: the (gs, cs, zs) strided shards (ipa_shard)
-    this process holds -- one with a real communicator, all P with virtual ranks; ``gather(objs)``
-    returns the list of every rank's objs in rank order (torch_gather_arrays(dist), or identity for
-    virtual ranks).  Returns (Ls, Rs, U, c) exactly as the single-session ipa_rounds does."""
+                       gather: Callable, reduce_lr: Callable | None = None):
+    """Distributed pcdl round loop.  ``local_shards``: the shards this process holds (ops.begin's
+    description; (gs, cs, zs) strided vectors for GpuIpaOps, (cs, z) for GpuWeightedIpaOps) -- one
+    with a real communicator, all P with virtual ranks; ``gather(objs)`` returns the list of every
+    rank's objs in rank order (torch_gather_arrays(dist), or identity for virtual ranks);
+    ``reduce_lr(local (L_r, R_r) list) -> (L, R)`` the round's sums over every rank (default: gather,
+    then ops.point_sum; torch_reduce_lr sums on the device).  Returns (Ls, Rs, U, c) exactly as the
+    single-session ipa_rounds does."""
     if world < 1 or world & (world - 1):
         raise ValueError("world size must be a power of two")
-    n_loc = len(local_shards[0][1])
+    n_loc = ops.shard_len(local_shards[0])
     if n_loc < 1 or n_loc & (n_loc - 1):
         raise ValueError("n / P must be a power of two")
+    if reduce_lr is None:
+        def reduce_lr(lrs):
+            parts = gather(lrs)
+            return (ops.point_sum(np.stack([p[0] for p in parts])), ops.point_sum(np.stack([p[1] for p in parts])))
     Ls, Rs = [], []
     xi = None
     if n_loc >= 2:
-        sessions = [ops.begin(g, c, z, H_prime) for g, c, z in local_shards]
-        xi = _ipa_loop(sessions, ops, gather, challenge, inverse, xi, Ls, Rs, n_loc.bit_length() - 1)
-        finals = gather([ops.final(s) for s in sessions])
+        gens = [ipa_shard_steps(ops, sh, H_prime, n_loc.bit_length() - 1) for sh in local_shards]
+        xi, finals = _drive(gens, reduce_lr, challenge, inverse, xi, Ls, Rs, n_loc.bit_length() - 1)
+        finals = gather(finals)
     else:
         finals = gather([(np.asarray(g).reshape(-1, 8)[:1], np.asarray(c).reshape(-1, 4)[:1],
                           np.asarray(z).reshape(-1, 4)[:1]) for g, c, z in local_shards])
@@ -391,9 +487,50 @@ def sharded_ipa_rounds(local_shards, H_prime, challenge: Callable, inverse: Call
     C = np.concatenate([f[1] for f in finals])
     Z = np.concatenate([f[2] for f in finals])
     if world > 1:
-        ses = ops.begin(G, C, Z, H_prime)
-        _ipa_loop([ses], ops, lambda objs: objs, challenge, inverse, xi, Ls, Rs, world.bit_length() - 1)
-        G, C, _ = ops.final(ses)
+        ses = ops.begin_vectors(G, C, Z, H_prime)
+        for _ in range(world.bit_length() - 1):
+            L, R = ops.round_lr(ses)
+            Ls.append(L)
+            Rs.append(R)
+            xi = challenge(xi, L, R)
+            ops.fold(ses, xi, inverse(xi))
+        G, C, _ = ops.final_vectors(ses)
+    return Ls, Rs, np.asarray(G[0], dtype=np.uint64), np.asarray(C[0], dtype=np.uint64)
+
+
+def sharded_ipa_fixed_challenges(ops_for_rank: Callable, shard_for_rank: Callable, H_prime, xis, xi_invs, world: int,
+                                 point_sum: Callable, ops_final: IpaOps):
+    """Virtual ranks run ONE AT A TIME (each may need its own resident SRS shard) against a challenge
+    sequence fixed in advance (xis[k] for round k, independent of L and R): rank r's generator is
+    driven to the end before rank r + 1 starts, then the per-round L_r, R_r are summed and the last
+    lg P rounds run on the gathered finals.  Used by the GPU test of the weighted shards on one
+    device; the live transcript needs real ranks (sharded_ipa_rounds).  Returns (Ls, Rs, U, c)."""
+    per_rank, finals = [], []
+    rounds = None
+    for r in range(world):
+        ops = ops_for_rank(r)
+        shard = shard_for_rank(r)
+        rounds = ops.shard_len(shard).bit_length() - 1
+        g = ipa_shard_steps(ops, shard, H_prime, rounds)
+        lr = [next(g)]
+        for k in range(rounds):
+            try:
+                lr.append(g.send((xis[k], xi_invs[k])))
+            except StopIteration as e:
+                finals.append(e.value)
+        per_rank.append(lr[:rounds])
+    Ls = [point_sum(np.stack([per_rank[r][k][0] for r in range(world)])) for k in range(rounds)]
+    Rs = [point_sum(np.stack([per_rank[r][k][1] for r in range(world)])) for k in range(rounds)]
+    G = np.concatenate([f[0] for f in finals])
+    C = np.concatenate([f[1] for f in finals])
+    Z = np.concatenate([f[2] for f in finals])
+    ses = ops_final.begin_vectors(G, C, Z, H_prime)
+    for k in range(rounds, rounds + world.bit_length() - 1):
+        L, R = ops_final.round_lr(ses)
+        Ls.append(L)
+        Rs.append(R)
+        ops_final.fold(ses, xis[k], xi_invs[k])
+    G, C, _ = ops_final.final_vectors(ses)
     return Ls, Rs, np.asarray(G[0], dtype=np.uint64), np.asarray(C[0], dtype=np.uint64)
 
 
@@ -422,3 +559,40 @@ def torch_gather_arrays(dist, device=None):
 
     return f
 
+
+def torch_reduce_lr(dist, curve, device):
+    """reduce_lr() for sharded_ipa_rounds with one shard per rank on a GPU: the rank's (L_r, R_r)
+    (2 x 64 B) go to the device once, one all_gather_into_tensor over RCCL collects every rank's,
+    and halo_point_sum_dev sums the L column and the R column on the device (strided 128-B rows);
+    only the two sums come back to the host, for the transcript."""
+    import ctypes
+
+    import torch
+
+    from . import _lib as H
+    from .group import _curve
+
+    world = dist.get_world_size()
+    L_ = H.load()
+    cid = _curve(curve)
+
+    # gloo (the one-GPU rehearsal) gathers host tensors; RCCL gathers on the device
+    gdev = device if dist.get_backend() == "nccl" else "cpu"
+
+    def f(lrs):
+        (Lr, Rr), = lrs
+        t = torch.from_numpy(np.concatenate([np.asarray(Lr, np.uint64).reshape(8),
+                                             np.asarray(Rr, np.uint64).reshape(8)]).view(np.int64)).to(gdev)
+        allv = torch.empty((world, 16), dtype=torch.int64, device=gdev)
+        dist.all_gather_into_tensor(allv, t)
+        allv = allv.to(device)
+        out = torch.empty(16, dtype=torch.int64, device=device)
+        sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        H.check(L_.halo_point_sum_dev(cid, ctypes.c_void_p(allv.data_ptr()), world, 128,
+                                      ctypes.c_void_p(out.data_ptr()), sp))
+        H.check(L_.halo_point_sum_dev(cid, ctypes.c_void_p(allv.data_ptr() + 64), world, 128,
+                                      ctypes.c_void_p(out.data_ptr() + 64), sp))
+        o = out.cpu().numpy().view(np.uint64)
+        return o[:8].copy(), o[8:].copy()
+
+    return f

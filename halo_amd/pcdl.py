@@ -87,14 +87,17 @@ class IpaSession:
     def fold(self, xi, xi_inv):
         H.check(H.load().halo_ipa_fold(self._s, H.ptr(H.fe_array(xi, 1)), H.ptr(H.fe_array(xi_inv, 1))))
 
-    def state(self):
+    def state(self, with_gs: bool = True):
+        """(m, gs, cs, zs): the folded vectors (length 2m).  Sessions over the resident SRS do not
+        materialise G in their weighted / tail rounds: with_gs=False there (gs is None)."""
         m = ctypes.c_size_t(0)
         H.check(H.load().halo_ipa_state(self._s, ctypes.byref(m), None, None, None))
         k = max(2 * m.value, 1)
-        gs = np.zeros((k, 8), dtype=np.uint64)
+        gs = np.zeros((k, 8), dtype=np.uint64) if with_gs else None
         cs = np.zeros((k, 4), dtype=np.uint64)
         zs = np.zeros((k, 4), dtype=np.uint64)
-        H.check(H.load().halo_ipa_state(self._s, ctypes.byref(m), H.ptr(gs), H.ptr(cs), H.ptr(zs)))
+        H.check(H.load().halo_ipa_state(self._s, ctypes.byref(m), H.ptr(gs) if with_gs else None, H.ptr(cs),
+                                        H.ptr(zs)))
         return m.value, gs, cs, zs
 
     def end(self):

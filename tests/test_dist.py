@@ -167,7 +167,10 @@ def _oracle_mods():
     return P
 
 
-class OracleIpaOps:
+from halo_amd.dist import IpaOps  # noqa: E402
+
+
+class OracleIpaOps(IpaOps):
     """halo_amd.dist.IpaOps on the CPU: pure-Python restatement of pcdl.rs:404-438."""
 
     def __init__(self, cname):
@@ -182,8 +185,9 @@ class OracleIpaOps:
         P, r = self.P, self.c.scalar
         return np.array([P.int_to_limbs(P.to_mont(x % r, r)) for x in xs], dtype=np.uint64).reshape(-1, 4)
 
-    def begin(self, gs, cs, zs, H_prime):
+    def begin(self, shard, H_prime):
         P, c = self.P, self.c
+        gs, cs, zs = shard
         G = [P.wrapped_to_point(c, list(g)) for g in np.asarray(gs, dtype=np.uint64).reshape(-1, 8)]
         return {"G": G, "C": self._ints(cs), "Z": self._ints(zs),
                 "H": P.wrapped_to_point(c, list(np.asarray(H_prime, dtype=np.uint64)))}

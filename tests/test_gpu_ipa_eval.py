@@ -139,6 +139,43 @@ def test_ipa_xi_mode_equals_h_prime(hal, corc, cname, cid, n):
         assert np.array_equal(Ua, Ub) and np.array_equal(ca, cb), trial
 
 
+@pytest.mark.parametrize("c_s", [18, 20])
+def test_ipa_wide_shifted_windows(hal, corc, c_s):
+    """A full window-shifted set of width 18 / 20 (halo_srs_precompute_window_range over every window)
+    drives the weighted rounds and the switch round's shared-scalar batch, whose sub-digits then need
+    three windows (2^(c_s / 2) > 256 buckets): the opening's L, R, U, c equal the same
+    opening over the SRS's default-width copies."""
+    c = P.PALLAS
+    r = c.scalar
+    n = 1 << 14
+    L = hal.load()
+    g = corc.srs_generate("pallas", n)
+    rng = random.Random(c_s)
+    cs = fe([rng.randrange(r) for _ in range(n)], r)
+    zz = fe([rng.randrange(r)], r)
+    Hw = np.array(P.point_to_wrapped(c, P.mul_fast(c, rng.randrange(1, r), c.generator)), dtype=np.uint64)
+    x0 = fe([rng.randrange(1, r)], r)
+    chal = [fe([rng.randrange(1, r)], r)[0] for _ in range(14)]
+    inv = [fe([P.inv(P.from_mont(P.limbs_to_int(x), r), r)], r)[0] for x in chal]
+
+    def opening():
+        s_ = pcdl.IpaSession.with_xi(cs, zz, Hw, x0, "pallas")
+        lr = []
+        for rd in range(14):
+            lr += [a.copy() for a in s_.round_lr()]
+            s_.fold(chal[rd], inv[rd])
+        return lr + list(s_.end())
+
+    group.PublicParams.upload("pallas", g, precompute_windows=True)
+    assert L.halo_srs_window_bits(0) < 18
+    ref = opening()
+    hal.check(L.halo_srs_precompute_window_range(0, c_s, 0, 0))
+    assert L.halo_srs_window_bits(0) == c_s
+    got = opening()
+    for a, b in zip(ref, got):
+        assert np.array_equal(a, b)
+
+
 @pytest.mark.parametrize("k", [2, 3, 5])
 def test_ipa_lockstep_sessions_equal_single(hal, corc, k):
     """halo_ipa_round_lr_multi over k sessions in lockstep (their weighted rounds share one L/R MSM,
@@ -303,6 +340,63 @@ def test_sharded_ipa_virtual_ranks(hal, corc, cname, cid, n, world):
     assert len(Ls2) == len(Ls)
     for a, b in zip(Ls + Rs, Ls2 + Rs2):
         assert np.array_equal(a, b)
+    assert np.array_equal(U, U2)
+    assert np.array_equal(cfin, c2)
+
+
+@pytest.mark.parametrize("logn,world", [(20, 8), (14, 4), (12, 2)])
+def test_sharded_ipa_weighted_virtual_ranks(hal, logn, world):
+    """The distributed opening on the weighted-round path: rank r's resident SRS
+    is its shard G[r::P] with window-shifted copies, its session the single-GPU weighted one over
+    c[r::P] with z^P and H'_r = z^r H' (halo_amd.dist.GpuWeightedIpaOps).  The virtual ranks run one
+    after another against a fixed challenge sequence (each needs its own resident shard on the one
+    GPU); every L, R, U and c equals the single-GPU opening over the whole SRS with the same
+    challenges -- 2^20 over 8 ranks is the BASELINE size."""
+    from halo_amd.dist import GpuIpaOps, GpuWeightedIpaOps, sharded_ipa_fixed_challenges
+
+    c = P.PALLAS
+    r = c.scalar
+    n = 1 << logn
+    L = hal.load()
+    hal.check(L.halo_srs_synthesize(0, n, 4242 + logn))
+    G = np.zeros((n, 8), dtype=np.uint64)
+    hal.check(L.halo_srs_read(0, 0, n, hal.ptr(G)))
+    hal.check(L.halo_srs_precompute_windows(0))
+    rng = np.random.default_rng(logn)
+    cs = np.ascontiguousarray(rng.integers(0, 2**62, size=(n, 4), dtype=np.uint64))
+    pr = random.Random(logn)
+    z = fe([pr.randrange(1, r)], r)[0]
+    Hp = G[3].copy()
+    xis = [fe([pr.randrange(1, r)], r)[0] for _ in range(logn)]
+    xinv = [fe([P.inv(P.from_mont(P.limbs_to_int(x), r), r)], r)[0] for x in xis]
+    # the single-GPU opening over the whole resident SRS (weighted rounds too)
+    ses = pcdl.IpaSession(cs, z, Hp, "pallas")
+    Ls, Rs = [], []
+    for k in range(logn):
+        Lk, Rk = ses.round_lr()
+        Ls.append(Lk.copy())
+        Rs.append(Rk.copy())
+        ses.fold(xis[k], xinv[k])
+    U, cfin = ses.end()
+
+    def ops_for_rank(k):
+        group.PublicParams.upload("pallas", np.ascontiguousarray(G[k::world]), precompute_windows=True)
+        return GpuWeightedIpaOps("pallas", k, world)
+
+    def shard_for_rank(k):
+        return (np.ascontiguousarray(cs[k::world]), z)
+
+    # the shard sessions must be weighted ones: their G is never materialised
+    probe = ops_for_rank(1)
+    s1 = probe.begin(shard_for_rank(1), Hp)
+    with pytest.raises(hal.HaloError):
+        s1.state()
+    s1.end()
+    Ls2, Rs2, U2, c2 = sharded_ipa_fixed_challenges(ops_for_rank, shard_for_rank, Hp, xis, xinv, world,
+                                                    lambda pts: group.point_sum(pts, "pallas"), GpuIpaOps("pallas"))
+    assert len(Ls2) == logn
+    for k, (a, b) in enumerate(zip(Ls + Rs, Ls2 + Rs2)):
+        assert np.array_equal(a, b), k
     assert np.array_equal(U, U2)
     assert np.array_equal(cfin, c2)
 
