@@ -34,15 +34,56 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 MSM_BYTES_PER_POINT = 96
 NTT_BYTES_PER_ELEM = 64  # read + write 32 B per transform
-# 255-bit Montgomery multiplications/s of one MI355X at k_acc's occupancy (4 waves/SIMD), round-4
-# field code (tools/micro/fe_mul_bench.hip, profiles/r04_micro.txt: 1.80e11; round 3's code: 1.77e11)
-MODMUL_PEAK = 1.80e11
-# raw VALU issue ceiling: v_mad_u64_u32 back to back, 3.09e13 lane-instructions/s on one MI355X
-# (tools/micro/modmul_bench.hip, profiles/r04_micro.txt); every VOP3 integer op issues at that rate
-RAW_VOP3_PEAK = 3.09e13
-# k_acc's VALU instructions per wave (16 additions per lane, K = 16) from the committed counters
-# (profiles/r04_pmc_kernels.txt) -- a per-build constant, valid for the 2^20 headline configuration
-KACC_VALU_PER_WAVE = 27659
+# VALU issue ceilings per instruction class (lane-instructions/s of one MI355X, the fastest measured
+# instruction of each class at 8 waves/SIMD: tools/micro/issue_bench.hip -> profiles/issue_rates.json).
+# A kernel's compute ceiling is its dispatch's counted VALU instructions (rocprofv3 SQ_INSTS_VALU,
+# _INT64, _INT32; profiles/pmc_summary.json "valu", stamped with the library hash) issued at these
+# rates, class by class (issue costs add on a SIMD: the mixed kernels of issue_bench check it).
+ISSUE_RATES_PATH = os.path.join(ROOT, "profiles", "issue_rates.json")
+
+
+def valu_ceiling(valu: dict, rates: dict):
+    """(issue-time ceiling in s, lane-instructions, dynamic class mix) of one dispatch.  The dynamic
+    INT64 count splits into multiply-adds and other 64-bit ops, the INT32 count into VOP3 and VOP1/2
+    encodings, by the kernel's static class counts; the remaining VALU (moves, selects, lane reads)
+    issue as VOP1/2."""
+    st = valu["static_classes"]
+    tot, i64, i32 = valu["valu_per_dispatch"], valu["int64_per_dispatch"], valu["int32_per_dispatch"]
+    m64 = st["mad64"] / max(1, st["mad64"] + st["vop3_64"])
+    v3 = st["vop3"] / max(1, st["vop3"] + st["vop2"])
+    n = {"mad64": i64 * m64, "vop3_64": i64 * (1 - m64), "vop3": i32 * v3,
+         "vop2": i32 * (1 - v3) + max(0.0, tot - i64 - i32)}
+    t = sum(n[c] * 64 / rates[c] for c in n)
+    return t, tot * 64, {c: n[c] / tot for c in n}
+
+
+def compute_roofline(key: str, launch_ms: float, iso_ms, pmc, lib_ok: bool, note: str):
+    """The compute roofline object of one kernel (None without this build's counters / the rates)."""
+    if not lib_ok or not pmc or key not in pmc or "valu" not in pmc[key] or not os.path.exists(ISSUE_RATES_PATH):
+        return {"bound": "valu-issue", "frac": None, "note": "no VALU counters of this library build "
+                "(tools/pmc_valu.sh) or no profiles/issue_rates.json"}
+    rates = json.load(open(ISSUE_RATES_PATH))
+    t_min, lanes, mix = valu_ceiling(pmc[key]["valu"], rates["rates"])
+    peak = lanes / t_min
+    out = {
+        "bound": "valu-issue",
+        "kernel": pmc[key]["valu"]["kernel"],
+        "unit": "VALU lane-instructions/s",
+        "achieved": lanes / (launch_ms * 1e-3) if launch_ms else None,
+        "peak": peak,
+        "frac": t_min / (launch_ms * 1e-3) if launch_ms else None,
+        "ceiling_ms": t_min * 1e3,
+        "valu_lane_instructions_per_launch": lanes,
+        "dynamic_mix": mix,
+        "class_rates": rates["rates"],
+        "note": note + "; peak = this dispatch's counted VALU issued class by class at the measured per-class "
+                       "rates (profiles/issue_rates.json, tools/micro/issue_bench.hip), so frac = ceiling time / "
+                       "launch time",
+    }
+    if iso_ms:
+        out["isolated"] = {"achieved": lanes / (iso_ms * 1e-3), "frac": t_min / (iso_ms * 1e-3),
+                           "launch_ms": iso_ms}
+    return out
 
 
 def parse():
@@ -737,12 +778,14 @@ def main():
     traffic = None
     traffic_note = "no profiles/pmc_summary.json"
     pmc_path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    pmc, pmc_ok = None, False
     if os.path.exists(pmc_path):
         try:
             import hashlib
             pmc = json.load(open(pmc_path))
             lib_sha = hashlib.sha256(open(H.LIB_PATH, "rb").read()).hexdigest()
-            if pmc.get("library_sha256") == lib_sha:
+            pmc_ok = pmc.get("library_sha256") == lib_sha
+            if pmc_ok:
                 traffic = pmc.get("msm_acc", {}).get("hbm_bytes_per_launch")
                 traffic_note = "rocprofv3 FETCH_SIZE + WRITE_SIZE (separate passes) of this library build, " \
                                "profiles/pmc_summary.json"
@@ -787,15 +830,19 @@ def main():
             prove["cpu"] = cpu_prove_baseline(L, H, curve, args.curve, args.prove_cpu, small)
 
     madds = n * (-(-255 // window_bits)) if window_bits else 0  # one mixed addition per nonzero digit
-    valu_achieved = madds * 10 / (acc_avg_ms * 1e-3) if acc_avg_ms > 0 else 0.0
-    # issue: k_acc's lane-instructions per launch (waves x the counted VALU per wave x 64 lanes) over the
-    # live launch time, against the raw v_mad_u64_u32 issue rate (only at the 2^20 headline shape, where
-    # the committed per-wave count applies: 15 windows, K = 16)
-    kacc_waves = (madds // 16 + 63) // 64 if args.logn == 20 and window_bits == 17 else 0
-    issue_achieved = kacc_waves * KACC_VALU_PER_WAVE * 64 / (acc_avg_ms * 1e-3) if acc_avg_ms > 0 and kacc_waves else None
-    # the same rates over k_acc's isolated launch time (the standalone MSMs after the timed region)
-    valu_iso = madds * 10 / (acc_iso_ms * 1e-3) if acc_iso_ms > 0 else 0.0
-    issue_iso = kacc_waves * KACC_VALU_PER_WAVE * 64 / (acc_iso_ms * 1e-3) if acc_iso_ms > 0 and kacc_waves else None
+    # the counted VALU of k_acc applies to the configuration it was counted on (2^20 points, 17-bit windows)
+    headline_shape = args.logn == 20 and window_bits == 17
+    acc_compute = compute_roofline("msm_acc", acc_avg_ms, acc_iso_ms, pmc, pmc_ok and headline_shape,
+                                   "k_acc over the timed region's mean launch time (live, beside the other stream's "
+                                   "front); isolated: the standalone MSMs after it")
+    acc_compute["modmul_rate"] = {
+        "achieved": madds * 10 / (acc_avg_ms * 1e-3) if acc_avg_ms > 0 else None,
+        "unit": "modmul/s", "note": "XYZZ mixed additions (8M + 2S, counted as 10) per launch over the live launch "
+                                    "time (informational: not a ceiling)"}
+    if ntt_main is not None:
+        ntt_main["compute_roofline"] = compute_roofline(
+            "ntt_pass", ntt_main.get("pass_kernel_avg_ms"), None, pmc, pmc_ok and args.ntt_logn == 22,
+            "k_ntt_pass<Fp, 2048> (the 11-bit Stockham pass, 4 per pair) over its mean launch time in the pair loop")
 
     line = {
         "metric": "MSM points/sec (Pippenger, Pallas, 2^20 points, resident SRS)",
@@ -838,32 +885,7 @@ def main():
                     "front and the previous step's tail, isolated_launch_ms over the standalone MSMs after it",
         },
         "cpu_baseline": cpu,
-        "compute_roofline": {
-            "bound": "valu",
-            "kernel": "k_acc",
-            "unit": "modmul/s",
-            "achieved": valu_achieved,
-            "peak": MODMUL_PEAK,
-            "frac": valu_achieved / MODMUL_PEAK,
-            "note": "XYZZ mixed additions (8M + 2S, counted as 10 modmul) per launch / mean launch time, against the "
-                    "measured Montgomery multiplication rate of one MI355X at 4 waves/SIMD (tools/micro/fe_mul_bench.hip)",
-            "isolated": {
-                "achieved": valu_iso,
-                "frac": valu_iso / MODMUL_PEAK,
-                "issue_achieved": issue_iso,
-                "issue_frac": issue_iso / RAW_VOP3_PEAK if issue_iso else None,
-                "note": "over k_acc's isolated launch time (roofline.isolated_launch_ms)",
-            },
-            "issue": {
-                "unit": "VALU lane-instructions/s",
-                "achieved": issue_achieved,
-                "peak": RAW_VOP3_PEAK,
-                "frac": issue_achieved / RAW_VOP3_PEAK if issue_achieved else None,
-                "note": "k_acc's counted VALU instructions (KACC_VALU_PER_WAVE per wave, profiles/r04_pmc_kernels.txt) "
-                        "over the live launch time, against back-to-back v_mad_u64_u32 issue (tools/micro/modmul_bench.hip); "
-                        "VOP2 ops (v_and, v_add_u32) issue twice as fast, so a mix can slightly exceed it",
-            },
-        },
+        "compute_roofline": acc_compute,
         "extra": {
             "msm_single_latency_ms": min(lat) if lat else None,
             "pipelined_equals_sync": sync_ok,

@@ -19,6 +19,7 @@
 #include <vector>
 
 #include <chrono>
+#include <thread>
 
 #include "dispatch.hpp"
 #include "glv.hpp"
@@ -1026,6 +1027,9 @@ struct halo_ipa_session {
     DevBuf cs2, zs2;  // ping-pong partners of cs / zs (tail rounds with a deferred fold)
     DevBuf own_table, w[2], scal, side, part;
     BatchScratch mat;  // weighted -> tail switch (msm_shared_batch)
+    // handed out by ipa_acquire and not yet returned by ipa_release (guarded by g_pool_mu): every
+    // session entry point refuses a handle that is not open, and a second end cannot pool it twice
+    bool in_use = false;
     // ---- per-opening state (reset by ipa_acquire)
     int curve = 0;
     size_t n = 0, m = 0;
@@ -1119,6 +1123,7 @@ halo_ipa_session* ipa_acquire(DeviceState* st) {
                 halo_ipa_session* ses = g_pool[i];
                 g_pool.erase(g_pool.begin() + i);
                 ses->reset_state();
+                ses->in_use = true;
                 return ses;
             }
     }
@@ -1135,13 +1140,30 @@ halo_ipa_session* ipa_acquire(DeviceState* st) {
         set_error(HALO_EDEVICE, "halo_ipa_begin: stream / pinned buffer allocation failed");
         return nullptr;
     }
+    {
+        std::lock_guard<std::mutex> g(g_pool_mu);
+        ses->in_use = true;
+    }
     return ses;
+}
+
+// the handle is an open session (checked before anything touches its state)
+bool ipa_is_open(const halo_ipa_session* ses) {
+    std::lock_guard<std::mutex> g(g_pool_mu);
+    return ses && ses->in_use;
 }
 
 // Back to the pool once its stream is idle (the pinned staging is then free); beyond IPA_POOL_MAX
 // idle sessions on the device the resources are released.
 void ipa_release(halo_ipa_session* ses) {
     if (!ses) return;
+    {
+        // a handle that is not open (a second end of the same handle) is neither touched nor pooled
+        // twice: two later openings would otherwise share its streams and buffers
+        std::lock_guard<std::mutex> g(g_pool_mu);
+        if (!ses->in_use) return;
+        ses->in_use = false;
+    }
     if (ses->s) (void)hipStreamSynchronize(ses->s);
     ses->table_ref.reset();  // a retired SRS multiples table is freed with its last session
     // an idle session keeps at most "ipa_pool_keep_bytes" of device buffers (tuning, default 1 GB: a
@@ -1150,9 +1172,6 @@ void ipa_release(halo_ipa_session* ses) {
     if ((long long)ses->buffer_bytes() > tuning(TUNE_IPA_POOL_KEEP)) ses->release_large();
     {
         std::lock_guard<std::mutex> g(g_pool_mu);
-        // a session already idle (a second end of the same handle) is not pooled twice: two later
-        // openings would otherwise share its streams and buffers
-        if (std::find(g_pool.begin(), g_pool.end(), ses) != g_pool.end()) return;
         size_t same = 0;
         for (halo_ipa_session* p : g_pool) same += p->device == ses->device;
         if (same < IPA_POOL_MAX) {
@@ -2200,8 +2219,15 @@ static int ipa_poll_lr(halo_ipa_session* ses) {
     const uint32_t seq = ses->poll_seq;
     const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t spin = 0;; spin++) {
-        if (__atomic_load_n(&fl[0], __ATOMIC_ACQUIRE) == seq && __atomic_load_n(&fl[1], __ATOMIC_ACQUIRE) == seq)
+        if (__atomic_load_n(&fl[0], __ATOMIC_ACQUIRE) == seq && __atomic_load_n(&fl[1], __ATOMIC_ACQUIRE) == seq) {
+            // the flags are the round's last stores, stream-ordered after any fold it followed
+            ses->fold_inflight = false;
             return HALO_OK;
+        }
+        // spin politely: a pause per probe, and past ~1 ms (a round is 0.1-2 ms) give the core up between
+        // probes (the spin holds the device mutex)
+        __builtin_ia32_pause();
+        if (spin > (1u << 16)) std::this_thread::yield();
         if ((spin & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) break;
     }
     HALO_HIP(hipStreamSynchronize(ses->s));
@@ -2226,6 +2252,7 @@ extern "C" int halo_ipa_round_lr_multi(halo_ipa_session* const* ses, size_t k, h
     std::lock_guard<std::mutex> g(st->mu);
     for (size_t i = 0; i < k; i++) {
         if (!ses[i]) return set_error(HALO_EINVAL, "halo_ipa_round_lr_multi: null session %zu", i);
+        if (!ipa_is_open(ses[i])) return set_error(HALO_EINVAL, "halo_ipa_round_lr_multi: session %zu is not open", i);
         ses[i]->solo = k == 1;
         HALO_CHECK(ipa_round_launch(st, ses[i]));
     }
@@ -2258,6 +2285,7 @@ extern "C" int halo_ipa_fold_multi(halo_ipa_session* const* ses, size_t k, const
     std::lock_guard<std::mutex> g(st->mu);
     for (size_t i = 0; i < k; i++) {
         if (!ses[i]) return set_error(HALO_EINVAL, "halo_ipa_fold_multi: null session %zu", i);
+        if (!ipa_is_open(ses[i])) return set_error(HALO_EINVAL, "halo_ipa_fold_multi: session %zu is not open", i);
         HALO_CHECK(ipa_fold_launch(st, ses[i], &xi[i], &xi_inv[i]));
     }
     // no host wait: the fold is stream-ordered before the next round (which synchronises), so the host
@@ -2268,6 +2296,7 @@ extern "C" int halo_ipa_fold_multi(halo_ipa_session* const* ses, size_t k, const
 extern "C" int halo_ipa_state(halo_ipa_session* ses, size_t* m, halo_wrapped_point_t* gs, halo_fe_t* cs, halo_fe_t* zs) {
     clear_error();
     if (!ses) return set_error(HALO_EINVAL, "halo_ipa_state: null session");
+    if (!ipa_is_open(ses)) return set_error(HALO_EINVAL, "halo_ipa_state: the session is not open");
     DeviceState* st = current_state();
     if (!st) return HALO_EDEVICE;
     std::lock_guard<std::mutex> g(st->mu);
@@ -2292,6 +2321,7 @@ extern "C" int halo_ipa_state(halo_ipa_session* ses, size_t* m, halo_wrapped_poi
 extern "C" int halo_ipa_end(halo_ipa_session* ses, halo_wrapped_point_t* U, halo_fe_t* c) {
     clear_error();
     if (!ses) return set_error(HALO_EINVAL, "halo_ipa_end: null session");
+    if (!ipa_is_open(ses)) return set_error(HALO_EINVAL, "halo_ipa_end: the session is not open (already ended)");
     int rc = HALO_OK;
     if (U || c) {
         DeviceState* st = current_state();

@@ -63,7 +63,7 @@ struct NttPassArgs {
 // LDS layout: limb-major (SoA), limb l of position p at smem[l * NE + swz(p)].  swz XORs the bank
 // bits with a linear function of p >> 5, chosen so that every ds_read_b32 / ds_write_b32 of the load,
 // group and store phases is conflict-free (each half-wave's 32 positions on 32 banks): for NE = 1024
-// over r = 1..8, for NE = 2048 over r = 9..11 including the unit-twiddle thread order of ntt_unit_tau.
+// over r = 1..8, for NE = 2048 over r = 9..11, including the unit groups' thread order (ntt_unit_tau).
 // tools/ntt_swizzle.py enumerates the access patterns and checks / searches the constants.  (A
 // 4096-element variant for 2 x 12-bit passes at 2^24 was measured 47 % slower than 3 x 8 bits: one
 // 1024-thread block per CU and 32-byte strided column loads; not kept.)
@@ -246,10 +246,14 @@ HALO_DEV Fe<F> ntt_tw(const uint32_t (&w)[NLIMB]) {
 // twiddles of stage s and of stage s + 1's first pair are 1 (the wave-uniform unit group of
 // ntt_unit_tau: three of the four multiplications skipped).  An unmultiplied butterfly operand keeps
 // its own limb interval instead of a product's [0, 1), so the unit group first carries its inputs
-// exactly: v0 + v1 + v2 + v3 then stays below 4 (2^29 - 1) < 2^31.  norm: normalize the outputs (every
-// group except, when the output path multiplies nothing, the pass's last).
+// exactly: v0 + v1 + v2 + v3 then stays below 4 (2^29 - 1) < 2^31.
+// norm: 0 none (the pass's last group when the output path multiplies nothing: fs_settle takes limbs in
+// (-4, 4)), 1 partial, 2 full.  From normalized inputs a group leaves v0 in [0, 3), v1, v2 in (-1, 2)
+// and v3 in (-2, 1) (units of 2^29): normalizing v0 alone leaves every output within (-2, 2), and a
+// group from such inputs stays mult-safe (operands within (-3, 3)) and ends within (-4, 4), where
+// every output is normalized.  So groups alternate partial / full: 5 fs_norm per 8 outputs, not 8.
 template <class F, bool UNIT>
-HALO_DEV void ntt_group4(Fe<F> (&v)[NTT_EPT], uint32_t G, const NttGroupTw& t, bool norm) {
+HALO_DEV void ntt_group4(Fe<F> (&v)[NTT_EPT], uint32_t G, const NttGroupTw& t, uint32_t norm) {
     if (UNIT) {
 #pragma unroll
         for (int m = 0; m < NTT_EPT; m++) v[m] = fs_carry(v[m]);
@@ -268,20 +272,34 @@ HALO_DEV void ntt_group4(Fe<F> (&v)[NTT_EPT], uint32_t G, const NttGroupTw& t, b
         v[3] = fs_sub(v[1], x);
         v[1] = fs_add(v[1], x);
     }
-    if (norm) {
+    if (norm == 2) {
 #pragma unroll
         for (int m = 0; m < NTT_EPT; m++) v[m] = fs_norm(v[m]);
+    } else if (norm == 1) {
+        v[0] = fs_norm(v[0]);
     }
 }
 
-// Thread order of the stage-1 group on one-column 2048-element blocks (the 11-bit passes of 2^21 and
-// 2^22): the group's position bit 0 -- its twiddle index k0 -- comes from thread bit 8, i.e. from the
-// wave (waves 0-3: k0 = 0, unit twiddles; waves 4-7: k0 = 1), so the skip is wave-uniform, and each SIMD
-// holds one unit and one full wave of the block (waves w and w + 4 share a SIMD,
-// MI355X_MICROARCH.md LDS).  Saves 3 of the group's 4 multiplications in half the waves: 0.375
-// multiplications per element per pass.
-HALO_DEV uint32_t ntt_unit_tau(uint32_t tau) {
-    return ((tau << 1) | (tau >> 8)) & 511u;
+// Wave-uniform unit twiddles.  The group at stage US has twiddle index k0 = position mod 2^US; in its
+// thread order ntt_unit_tau the position's low US bits come from the wave's thread bits (the top US
+// bits of the thread index), so k0 is the same on a whole wave and the k0 = 0 waves skip the
+// multiplications by 1 (stage US, and stage US + 1's first pair: three of four).
+//  * one-column 2048-element blocks (the 11-bit passes of 2^21 / 2^22): US = 1, position bit 0 = thread
+//    bit 8, so waves 0-3 are unit and 4-7 not -- each SIMD holds one of each (waves w and w + 4 share a
+//    SIMD, MI355X_MICROARCH.md LDS): 0.375 multiplications per element per pass saved;
+//  * 1024-element blocks (the <= 8-bit passes: 2^23, 2^24, ...): US = 2, wave 0 of the block's four
+//    is unit (with four blocks per CU starting on varying SIMDs the skips spread over the SIMDs):
+//    0.19 per element per pass.
+// Other 2048-element shapes (T = 2, 4: 2^17..2^20) would put the skips on two of a block's four SIMDs
+// only, so they keep the plain order.
+template <int NE>
+HALO_DEV uint32_t ntt_unit_stage(uint32_t T) {
+    return NE == NTT_E_BIG ? (T == 1u ? 1u : 0u) : 2u;
+}
+template <int NE>
+HALO_DEV uint32_t ntt_unit_tau(uint32_t tau, uint32_t us) {
+    constexpr uint32_t LG_TH = NE == NTT_E_BIG ? 9u : 8u;
+    return ((tau << us) | (tau >> (LG_TH - us))) & ((1u << LG_TH) - 1u);
 }
 
 // raw workgroup barrier: LDS writes complete, global loads left in flight (a __syncthreads() would
@@ -375,28 +393,32 @@ __global__ __launch_bounds__(NE / NTT_EPT) void k_ntt_pass(NttPassArgs a) {
     }
     // ---- remaining stages in radix-4 groups through LDS; each group's twiddles are loaded before the
     // barrier that precedes its LDS reads
-    const bool unit_blocks = NE == NTT_E_BIG && T == 1u;
-    // wave-uniform: thread bit 8 (NE = 2048 blocks have 512 threads)
-    const bool unit_wave = unit_blocks && (__builtin_amdgcn_readfirstlane(tau) >> 8) == 0u;
+    const uint32_t US = ntt_unit_stage<NE>(T);
+    constexpr uint32_t LG_TH = NE == NTT_E_BIG ? 9u : 8u;
+    // wave-uniform: the top US thread bits (the wave's) are zero
+    const bool unit_wave = US != 0u && (__builtin_amdgcn_readfirstlane(tau) >> (LG_TH - US)) == 0u;
     // the output path multiplies unless the last pass's pre-twiddle table carries out_const
     const bool out_mul = a.out_ark && !a.out_scaled;
     uint32_t s = a.prune ? a.prune : G0;
+    // the next group's inputs are normalized: loaded values (pruned pass) or ntt_first's G0 = 2 output;
+    // G0 = 1 leaves (-1, 2)
+    bool in_norm = a.prune != 0 || G0 != 1;
     NttGroupTw tw;
     {
-        const uint32_t tt = (unit_blocks && s == 1) ? ntt_unit_tau(tau) : tau;
+        const uint32_t tt = (US != 0u && s == US) ? ntt_unit_tau<NE>(tau, US) : tau;
         if (s < r) ntt_group_tw_load(tw, s, (r - s) < 2u ? (r - s) : 2u, tt & ((1u << s) - 1), a.stage_tw);
     }
     // Wave-local exchanges: a group at stage s <= 6 (2^s <= 64) reads and writes exactly its wave's
     // chunk of EPT * 64 consecutive positions [EPT 64 w, EPT 64 (w + 1)), and so does the load phase
     // of a one-column block (base = EPT tau); between two such phases the wave only waits for its own
-    // LDS writes.  (The stage-1 unit order of ntt_unit_tau spans the block: full barriers around it.)
-    auto wave_local = [&](uint32_t sg) { return sg <= 6u && !(unit_blocks && sg == 1u); };
+    // LDS writes.  (The unit group's order of ntt_unit_tau spans the block: full barriers around it.)
+    auto wave_local = [&](uint32_t sg) { return sg <= 6u && !(US != 0u && sg == US); };
     ntt_lds_barrier((T == 1u || R < (uint32_t)EPT) && s < r && wave_local(s));
     for (; s < r; s += 2) {
         const uint32_t G = (r - s) < 2u ? (r - s) : 2u;
         const uint32_t h = 1u << s;
-        const bool unit_grp = unit_blocks && s == 1;
-        const uint32_t tt = unit_grp ? ntt_unit_tau(tau) : tau;
+        const bool unit_grp = US != 0u && s == US;
+        const uint32_t tt = unit_grp ? ntt_unit_tau<NE>(tau, US) : tau;
         const uint32_t gb = (tt & (h - 1)) | ((tt >> s) << (s + 2));
         const uint32_t shb = ntt_swz_hi<NE>(gb >> 5);
 #pragma unroll
@@ -405,11 +427,15 @@ __global__ __launch_bounds__(NE / NTT_EPT) void k_ntt_pass(NttPassArgs a) {
             const uint32_t ph = (pos ^ shb) ^ ntt_swz_hi<NE>(((uint32_t)m * h) >> 5);
             if (pos < EB) v[m] = lds_get_soa<F>(data, ph, NE);
         }
-        const bool norm = s + 2 < r || out_mul;
+        // partial after normalized inputs (the unit group carries its inputs itself, and a one-stage
+        // group (G = 1, the last of an odd remainder) leaves (-1, 2) / (-2, 1)... within the partial bound)
+        const bool in_norm_g = in_norm || (unit_grp && unit_wave);
+        const uint32_t norm = (s + 2 >= r && !out_mul) ? 0u : (in_norm_g ? 1u : 2u);
         if (unit_grp && unit_wave)
             ntt_group4<F, true>(v, G, tw, norm);
         else
             ntt_group4<F, false>(v, G, tw, norm);
+        in_norm = norm == 2;
         // (no barrier here: a thread writes back exactly the positions it read)
 #pragma unroll
         for (int m = 0; m < EPT; m++) {
@@ -419,7 +445,7 @@ __global__ __launch_bounds__(NE / NTT_EPT) void k_ntt_pass(NttPassArgs a) {
         }
         const uint32_t sn = s + 2;
         if (sn < r) {
-            const uint32_t tn = (unit_blocks && sn == 1) ? ntt_unit_tau(tau) : tau;
+            const uint32_t tn = (US != 0u && sn == US) ? ntt_unit_tau<NE>(tau, US) : tau;
             ntt_group_tw_load(tw, sn, (r - sn) < 2u ? (r - sn) : 2u, tn & ((1u << sn) - 1), a.stage_tw);
         }
         ntt_lds_barrier(wave_local(s) && sn < r && wave_local(sn));
@@ -602,7 +628,7 @@ static std::vector<unsigned> ntt_radices(unsigned logn) {
         r.push_back(logn);
         return r;
     }
-    if (logn >= 17 && logn <= 2 * NTT_MAX_LOG_R_BIG) {
+    if (logn >= 17 && logn <= std::min<long long>(2 * NTT_MAX_LOG_R_BIG, tuning(TUNE_NTT_BIG_MAX_LOG))) {
         r.push_back((logn + 1) / 2);
         r.push_back(logn / 2);
         return r;
@@ -633,8 +659,9 @@ static unsigned ntt_pass0_prune(unsigned lr, unsigned prune) {
 template <class F>
 static int get_twiddles(DeviceState* st, int field, unsigned logn, int inverse, DeviceState::Twiddles** out,
                         hipStream_t s) {
+    const unsigned r0 = ntt_radices(logn)[0];
     for (auto& t : st->tw)
-        if (t->field == field && t->logn == (int)logn && t->inverse == inverse) {
+        if (t->field == field && t->logn == (int)logn && t->inverse == inverse && t->r0 == r0) {
             *out = t.get();
             return HALO_OK;
         }
@@ -642,6 +669,7 @@ static int get_twiddles(DeviceState* st, int field, unsigned logn, int inverse, 
     t->field = field;
     t->logn = (int)logn;
     t->inverse = inverse;
+    t->r0 = r0;
     t->lo_bits = (int)((logn + 1) / 2);
     const size_t nlo = (size_t)1 << t->lo_bits, nhi = (size_t)1 << (logn - t->lo_bits);
     HALO_CHECK(t->lo.reserve(nlo * 32));

@@ -2,7 +2,7 @@
 
 ADVICE r04: the signed reduction narrows the column headroom to 2^63, so correctness rests on operand
 bounds (fields.hpp: at most one loose operand with limbs < 2^30; ntt.hip: the NTT's signed-limb operand
-with limbs in (-2, 3) x 2^29).  This executes the exact instruction list the generator emits -- 64-bit
+with limbs in [-3, 3] x 2^29).  This executes the exact instruction list the generator emits -- 64-bit
 two's complement accumulators, v_mad_u64_u32 / v_mad_i64_i32 / v_ashrrev_i64 / v_alignbit_b32 -- on
 limb-adversarial and random operands, asserts that every column's exact value stays inside the signed
 64-bit range (the register and the integer agree), and checks the result against Python integers:
@@ -132,18 +132,22 @@ def test_fe_mul_and_sqr_column_bounds(field):
 
 @pytest.mark.parametrize("field", ["fp", "fq"])
 def test_ntt_signed_products(field):
-    """ntt.hip fs_mul (fe_muls_asm): a signed-limb operand with low limbs in (-2, 3) x 2^29 -- the
+    """ntt.hip fs_mul (fe_muls_asm): a signed-limb operand with low limbs in [-3, 3] x 2^29 -- the
     widest a butterfly operand gets between two fs_norm -- times a normalized twiddle below 2p; the
     result is a b R'^-1 mod p with low limbs in [0, 2^29) and |value| < p + |a b| / R'."""
     p = PRIMES[field]
     rinv = pow(RP, -1, p)
     rng = random.Random(2)
-    hi = 3 * (1 << 29) - 3   # u + t + t' from normalized limbs: <= 3 (2^29 - 1)
-    lo = -(2 * (1 << 29) - 2)
+    # the widest operands ntt.hip feeds fs_mul: after a partially normalized group (inputs within
+    # [-2^30 - 1, 2^30 + 1]) one butterfly reaches +-3 x 2^29
+    hi = 3 * (1 << 29)
+    lo = -3 * (1 << 29)
     top_hi = 20 * p >> (B * (N - 1))  # the value bound (|x| < ~20 p) bounds the top limb
     cases = [([hi] * (N - 1) + [top_hi], limbs(2 * p - 1)),
              ([lo] * (N - 1) + [-top_hi], limbs(2 * p - 1)),
-             ([hi, lo] * 4 + [top_hi], [MASK] * (N - 1) + [(1 << 24) - 1])]
+             ([hi, lo] * 4 + [top_hi], [MASK] * (N - 1) + [(1 << 24) - 1]),
+             ([hi] * (N - 1) + [top_hi], [MASK] * (N - 1) + [(1 << 24) - 1]),
+             ([lo] * (N - 1) + [-top_hi], [MASK] * (N - 1) + [(1 << 24) - 1])]
     for _ in range(300):
         a = [rng.randint(lo, hi) for _ in range(N - 1)] + [rng.randint(-top_hi, top_hi)]
         cases.append((a, limbs(rng.randrange(2 * p))))

@@ -16,11 +16,19 @@ import random
 import sys
 
 
-def tau_remap(tau, th):
-    """Thread -> position-bits order of the unit-twiddle group (ntt.hip ntt_unit_tau): the top thread
-    bit becomes the lowest (the group at stage 1 then has a wave-uniform twiddle index k0)."""
+def unit_stage(NE, T):
+    """Stage of the wave-uniform unit-twiddle group (ntt.hip ntt_unit_stage): 1 on one-column
+    2048-element blocks, 2 on 1024-element blocks, none (0) otherwise."""
+    if NE == 2048:
+        return 1 if T == 1 else 0
+    return 2
+
+
+def tau_remap(tau, th, us):
+    """Thread -> position-bits order of the unit-twiddle group (ntt.hip ntt_unit_tau): the top `us`
+    thread bits (the wave's) become the lowest, so the group at stage us has a wave-uniform k0."""
     lg = th.bit_length() - 1
-    return ((tau << 1) | (tau >> (lg - 1))) & (th - 1)
+    return ((tau << us) | (tau >> (lg - us))) & (th - 1)
 
 
 def patterns(NE):
@@ -58,7 +66,8 @@ def patterns(NE):
                     for h in range(TH // 32):
                         ps = []
                         for tau in range(32 * h, 32 * h + 32):
-                            tt = tau_remap(tau, TH) if (T == 1 and NE == 2048 and s == 1) else tau
+                            us = unit_stage(NE, T)
+                            tt = tau_remap(tau, TH, us) if (us and s == us) else tau
                             gb = (tt & (hh - 1)) | ((tt >> s) << (s + 2))
                             ps.append(gb + m * hh)
                         yield [p for p in ps if p < EB]

@@ -6,7 +6,10 @@ from halo_amd import _lib as H
 H.ensure_device(0)
 L = H.load()
 s = torch.cuda.Stream()
-for logn in [int(x) for x in (sys.argv[1:] or ['20', '22', '24'])]:
+for kv in [a for a in sys.argv[1:] if '=' in a]:  # tuning A/B: key=value
+    k, v = kv.split('=')
+    H.set_tuning(k, int(v))
+for logn in [int(x) for x in ([a for a in sys.argv[1:] if '=' not in a] or ['20', '22', '24'])]:
     N = 1 << logn
     g = torch.Generator(device='cuda'); g.manual_seed(logn)
     x = torch.randint(0, 2**62, (N, 4), dtype=torch.int64, device='cuda', generator=g)

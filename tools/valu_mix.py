@@ -8,8 +8,9 @@ the substring prints the static VALU counts of the whole function and of its inn
 region between the largest backward branch's target and the branch), split into the issue classes
 measured by tools/micro/issue_bench.hip:
   mad64 -- v_mad_u64_u32 / v_mad_i64_i32;
+  vop3_64 -- the other 64-bit VOP3 integer ops (v_ashrrev_i64, v_lshl_add_u64, v_lshlrev_b64, ...);
   vop3  -- every other VALU in a VOP3 encoding (no _e32 suffix: v_add3_u32, v_alignbit_b32,
-           v_ashrrev_i64, v_lshl_add_u64, v_bfe_*, *_e64 forms, ...);
+           v_bfe_*, *_e64 forms, ...);
   vop2  -- VOP1 / VOP2 encodings (_e32 suffix: v_and_b32_e32, v_add_u32_e32, v_mov_b32_e32, ...).
 The loop body's mix stands for the kernel's dynamic mix when the loop dominates (k_acc: 16 additions
 per lane; k_ntt_pass: the radix-4 group loop); bench.py weights the measured per-class costs by it.
@@ -74,11 +75,13 @@ def klass(op):
         return "mad64"
     if op.endswith("_e32") or "_dpp" in op or "_sdwa" in op:
         return "vop2"
+    if any(t in op for t in ("_i64", "_u64", "_b64")):
+        return "vop3_64"
     return "vop3"
 
 
 def mix(insts):
-    c = {"mad64": 0, "vop3": 0, "vop2": 0}
+    c = {"mad64": 0, "vop3_64": 0, "vop3": 0, "vop2": 0}
     for _, op, _ in insts:
         k = klass(op)
         if k:
