@@ -111,6 +111,8 @@ def parse():
     ap.add_argument("--msm-streams", type=int, default=2,
                     help="streams the pipelined headline MSMs alternate over (independent MSMs; round 4, one box: "
                          "1 / 2 / 3 streams 1.26 / 1.233 / 1.296 ms/step)")
+    ap.add_argument("--shift-c", type=int, default=0,
+                    help="A/B: window width of the headline's shifted SRS copies (0 = the library default)")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
                     help="halo_set_tuning before the run (A/B of path selections; results are identical)")
     return ap.parse_args()
@@ -174,7 +176,10 @@ def main():
         # ---- setup (outside the timed region): resident SRS = this rank's block of the global SRS
         seed = 0x48414C4F + rank  # distinct bases per rank
         H.check(L.halo_srs_synthesize(curve, n, seed))
-        H.check(L.halo_srs_precompute_windows(curve))
+        if args.shift_c:  # A/B of the window width of the shifted copies (every window: a full set)
+            H.check(L.halo_srs_precompute_window_range(curve, args.shift_c, 0, 0))
+        else:
+            H.check(L.halo_srs_precompute_windows(curve))
         nbatch = max(1, min(steps, 8 if logn <= 22 else 2))
         # < 2^252 < r: valid canonical Montgomery representatives
         scalars = torch.randint(-(2**63), 2**63 - 1, (nbatch, n, 4), dtype=torch.int64, device="cuda", generator=gen)

@@ -894,15 +894,19 @@ __global__ void k_scale_ark(uint4* x, int count, const uint4* k) {
 }
 
 // c / z folds (pcdl.rs:430-435) and the weight update w' = interleave(w, xi w)
+// xi | xi^-1 (ark words) as one by-value kernel argument
+struct ArkScalarPair {
+    uint4 v[4];
+};
+
 template <class Cv>
-__global__ __launch_bounds__(256) void k_tail_fold(uint4* cs, uint4* zs, size_t m, const uint4* xi_ark,
-                                                   const uint4* xi_inv_ark, const uint4* w_in, uint4* w_out,
-                                                   size_t wlen) {
+__global__ __launch_bounds__(256) void k_tail_fold(uint4* cs, uint4* zs, size_t m, ArkScalarPair x,
+                                                   const uint4* w_in, uint4* w_out, size_t wlen) {
     using S = typename Cv::Scalar;
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const Fe<S> xi = fe_from_ark<S>(xi_ark);
+    const Fe<S> xi = fe_from_ark<S>(x.v);
     if (i < m) {
-        const Fe<S> xinv = fe_from_ark<S>(xi_inv_ark);
+        const Fe<S> xinv = fe_from_ark<S>(x.v + 2);
         fe_to_ark(cs + 2 * i, fe_add(fe_from_ark<S>(cs + 2 * i), fe_mul(fe_from_ark<S>(cs + 2 * (i + m)), xinv)));
         fe_to_ark(zs + 2 * i, fe_add(fe_from_ark<S>(zs + 2 * i), fe_mul(fe_from_ark<S>(zs + 2 * (i + m)), xi)));
     }
@@ -2177,27 +2181,34 @@ static int ipa_fold_now(DeviceState* st, halo_ipa_session* ses, const halo_fe_t*
     // the previous fold's H2D copy from the pinned staging must have completed (a round in between
     // synchronises the stream; two folds in a row wait here)
     if (ses->fold_inflight) HALO_HIP(hipStreamSynchronize(s));
-    ses->fold_inflight = true;
-    memcpy(ses->pinned + 128, xi, 32);
-    memcpy(ses->pinned + 160, xi_inv, 32);
-    HALO_HIP(hipMemcpyAsync(sm + 384, ses->pinned + 128, 64, hipMemcpyHostToDevice, s));
     const size_t m = ses->m;
-    ses->srs_round0 = false;
-    if (!ses->tail && !ses->weighted) {  // G itself is folded below
-        HALO_CHECK(ipa_ensure_gs(st, ses));
-        ses->gs_srs_prefix = false;
-    }
     if (ses->tail || ses->weighted) {
+        // xi, xi^-1 as kernel arguments: no staging copy, so nothing for a later fold to wait on
+        ArkScalarPair x;
+        memcpy(&x.v[0], xi, 32);
+        memcpy(&x.v[2], xi_inv, 32);
+        ses->srs_round0 = false;
         DISPATCH_CURVE(ses->curve, Cv, {
             hipLaunchKernelGGL(k_tail_fold<Cv>, dim3(gridn(std::max(m, ses->wlen), 256)), dim3(256), 0, s,
-                               ses->cs.as<uint4>(), ses->zs.as<uint4>(), m, (const uint4*)(sm + 384),
-                               (const uint4*)(sm + 416), ses->w[ses->wcur].as<const uint4>(),
+                               ses->cs.as<uint4>(), ses->zs.as<uint4>(), m, x, ses->w[ses->wcur].as<const uint4>(),
                                ses->w[ses->wcur ^ 1].as<uint4>(), ses->wlen);
         });
         HALO_HIP(hipGetLastError());
         ses->wcur ^= 1;
         ses->wlen *= 2;
-    } else {
+        ses->m /= 2;
+        return HALO_OK;
+    }
+    ses->fold_inflight = true;
+    memcpy(ses->pinned + 128, xi, 32);
+    memcpy(ses->pinned + 160, xi_inv, 32);
+    HALO_HIP(hipMemcpyAsync(sm + 384, ses->pinned + 128, 64, hipMemcpyHostToDevice, s));
+    ses->srs_round0 = false;
+    if (!ses->tail && !ses->weighted) {  // G itself is folded below
+        HALO_CHECK(ipa_ensure_gs(st, ses));
+        ses->gs_srs_prefix = false;
+    }
+    {
         DISPATCH_CURVE(ses->curve, Cv, {
             ProfScope prof("ipa_fold", s);
             HALO_LAUNCH(prof, k_ipa_fold<Cv>, dim3(gridn(m, FOLD_THREADS)), dim3(FOLD_THREADS), 0, s, ses->gs.as<uint4>(),

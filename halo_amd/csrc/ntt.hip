@@ -427,10 +427,11 @@ __global__ __launch_bounds__(NE / NTT_EPT) void k_ntt_pass(NttPassArgs a) {
             const uint32_t ph = (pos ^ shb) ^ ntt_swz_hi<NE>(((uint32_t)m * h) >> 5);
             if (pos < EB) v[m] = lds_get_soa<F>(data, ph, NE);
         }
-        // partial after normalized inputs (the unit group carries its inputs itself, and a one-stage
-        // group (G = 1, the last of an odd remainder) leaves (-1, 2) / (-2, 1)... within the partial bound)
-        const bool in_norm_g = in_norm || (unit_grp && unit_wave);
-        const uint32_t norm = (s + 2 >= r && !out_mul) ? 0u : (in_norm_g ? 1u : 2u);
+        // partial after normalized inputs, full otherwise.  The choice is block-uniform: the next group
+        // reads positions other waves wrote (the unit group's thread order crosses waves), so the unit
+        // waves -- whose carried inputs would allow a partial normalization -- follow the same rule as
+        // the others (a one-stage group, G = 1, stays within the partial bound too)
+        const uint32_t norm = (s + 2 >= r && !out_mul) ? 0u : (in_norm ? 1u : 2u);
         if (unit_grp && unit_wave)
             ntt_group4<F, true>(v, G, tw, norm);
         else
