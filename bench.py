@@ -43,16 +43,18 @@ ISSUE_RATES_PATH = os.path.join(ROOT, "profiles", "issue_rates.json")
 
 
 def valu_ceiling(valu: dict, rates: dict):
-    """(issue-time ceiling in s, lane-instructions, dynamic class mix) of one dispatch.  The dynamic
-    INT64 count splits into multiply-adds and other 64-bit ops, the INT32 count into VOP3 and VOP1/2
-    encodings, by the kernel's static class counts; the remaining VALU (moves, selects, lane reads)
-    issue as VOP1/2."""
+    """(issue-time ceiling in s, lane-instructions, dynamic class mix) of one dispatch.  The counted
+    SQ_INSTS_VALU_INT64 splits over the 64-bit classes (mad_u64, mad_i64, ashr64, other64) and
+    SQ_INSTS_VALU_INT32 over vop3 / vop2 in the proportions of the kernel's static code; the remaining
+    VALU (moves, selects, lane reads) issue as VOP1 / VOP2."""
     st = valu["static_classes"]
     tot, i64, i32 = valu["valu_per_dispatch"], valu["int64_per_dispatch"], valu["int32_per_dispatch"]
-    m64 = st["mad64"] / max(1, st["mad64"] + st["vop3_64"])
-    v3 = st["vop3"] / max(1, st["vop3"] + st["vop2"])
-    n = {"mad64": i64 * m64, "vop3_64": i64 * (1 - m64), "vop3": i32 * v3,
-         "vop2": i32 * (1 - v3) + max(0.0, tot - i64 - i32)}
+    c64 = ("mad_u64", "mad_i64", "ashr64", "other64")
+    s64 = max(1, sum(st[c] for c in c64))
+    s32 = max(1, st["vop3"] + st["vop2"])
+    n = {c: i64 * st[c] / s64 for c in c64}
+    n["vop3"] = i32 * st["vop3"] / s32
+    n["vop2"] = i32 * st["vop2"] / s32 + max(0.0, tot - i64 - i32)
     t = sum(n[c] * 64 / rates[c] for c in n)
     return t, tot * 64, {c: n[c] / tot for c in n}
 

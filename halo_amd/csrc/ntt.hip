@@ -272,11 +272,12 @@ HALO_DEV void ntt_group4(Fe<F> (&v)[NTT_EPT], uint32_t G, const NttGroupTw& t, u
         v[3] = fs_sub(v[1], x);
         v[1] = fs_add(v[1], x);
     }
+    // (written as two independent conditions: an if / else-if form made the compiler hold 144 VGPRs,
+    // one wave per SIMD fewer)
+    if (norm != 0) v[0] = fs_norm(v[0]);
     if (norm == 2) {
 #pragma unroll
-        for (int m = 0; m < NTT_EPT; m++) v[m] = fs_norm(v[m]);
-    } else if (norm == 1) {
-        v[0] = fs_norm(v[0]);
+        for (int m = 1; m < NTT_EPT; m++) v[m] = fs_norm(v[m]);
     }
 }
 
@@ -316,7 +317,7 @@ HALO_DEV void ntt_lds_barrier(bool wave_only = false) {
 // G0 stages are done straight from the global loads, the rest in radix-4 groups through LDS, and a
 // final coalesced store phase writes y[(j / Ns) Ns R + (j mod Ns) + k Ns].
 template <class F, int NE>
-__global__ __launch_bounds__(NE / NTT_EPT) void k_ntt_pass(NttPassArgs a) {
+__global__ __launch_bounds__(NE / NTT_EPT, 4) void k_ntt_pass(NttPassArgs a) {
     constexpr int EPT = NTT_EPT;
     constexpr uint32_t TH = NE / EPT;
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -635,6 +636,19 @@ static std::vector<unsigned> ntt_radices(unsigned logn) {
         return r;
     }
     const unsigned passes = (logn + NTT_MAX_LOG_R_MULTI - 1) / NTT_MAX_LOG_R_MULTI;
+    if (tuning(TUNE_NTT_EVEN_SPLIT)) {
+        // even radices where possible (an odd pass ends in a one-stage group: a whole LDS round trip
+        // and normalization for half a group's butterflies): 8s, trimmed by 2 from the back, at most
+        // one odd pass (2^22 = 8 + 8 + 6, 2^23 = 8 + 8 + 7)
+        r.assign(passes, (unsigned)NTT_MAX_LOG_R_MULTI);
+        unsigned excess = passes * NTT_MAX_LOG_R_MULTI - logn;
+        for (unsigned k = passes; excess >= 2; k = (k == 1 ? passes : k - 1)) {
+            r[k - 1] -= 2;
+            excess -= 2;
+        }
+        if (excess) r[passes - 1] -= 1;
+        return r;
+    }
     unsigned left = logn;
     for (unsigned p = 0; p < passes; p++) {
         unsigned take = (left + (passes - p) - 1) / (passes - p);
@@ -642,6 +656,13 @@ static std::vector<unsigned> ntt_radices(unsigned logn) {
         left -= take;
     }
     return r;
+}
+
+// the split as one key (5 bits per pass) for the twiddle-table cache
+static uint64_t ntt_split_key(unsigned logn) {
+    uint64_t k = 0;
+    for (unsigned x : ntt_radices(logn)) k = (k << 5) | x;
+    return k;
 }
 
 // Stages of pass 0 (radix 2^lr) that a zero tail lets the pass skip (NttPassArgs::prune): only when
@@ -660,9 +681,9 @@ static unsigned ntt_pass0_prune(unsigned lr, unsigned prune) {
 template <class F>
 static int get_twiddles(DeviceState* st, int field, unsigned logn, int inverse, DeviceState::Twiddles** out,
                         hipStream_t s) {
-    const unsigned r0 = ntt_radices(logn)[0];
+    const uint64_t split = ntt_split_key(logn);
     for (auto& t : st->tw)
-        if (t->field == field && t->logn == (int)logn && t->inverse == inverse && t->r0 == r0) {
+        if (t->field == field && t->logn == (int)logn && t->inverse == inverse && t->split == split) {
             *out = t.get();
             return HALO_OK;
         }
@@ -670,7 +691,7 @@ static int get_twiddles(DeviceState* st, int field, unsigned logn, int inverse, 
     t->field = field;
     t->logn = (int)logn;
     t->inverse = inverse;
-    t->r0 = r0;
+    t->split = split;
     t->lo_bits = (int)((logn + 1) / 2);
     const size_t nlo = (size_t)1 << t->lo_bits, nhi = (size_t)1 << (logn - t->lo_bits);
     HALO_CHECK(t->lo.reserve(nlo * 32));

@@ -36,7 +36,7 @@ void clear_error();
 
 // ---- tuning (halo_set_tuning): path selections the parity tests pin; read on every use
 enum TuneKey { TUNE_IPA_WEIGHTED, TUNE_IPA_TAIL, TUNE_IPA_SRS_TAIL_N, TUNE_IPA_MAT_N, TUNE_MSM_MULTI_MAX, TUNE_IPA_POOL_KEEP,
-               TUNE_NTT_BIG_MAX_LOG, TUNE_COUNT };
+               TUNE_NTT_BIG_MAX_LOG, TUNE_NTT_EVEN_SPLIT, TUNE_COUNT };
 long long tuning(TuneKey k);
 
 // ---- device buffers ---------------------------------------------------------------------------
@@ -108,7 +108,7 @@ struct DeviceState {
         DevBuf stage;    // stage twiddles: entry 2^s - 1 + k = omega_{2^(s+1)}^k, s < 11 (9 limbs, 48 B each)
         DevBuf pass[4];  // per-pass pre-twiddle tables (logn <= 24), see ntt.hip
         bool has_pass = false;
-        unsigned r0 = 0;  // the first pass's radix the tables were built for (ntt_radices, tuning-dependent)
+        uint64_t split = 0;  // the pass split the tables were built for (ntt_radices, tuning-dependent)
     };
     std::vector<std::unique_ptr<Twiddles>> tw;
     struct RTable {

@@ -4,8 +4,10 @@
 #   kernel_stats.csv     rocprofv3 --kernel-trace --stats of the 2^20 MSM + 2^22 NTT bench
 #   kstats.txt           its per-kernel table (tools/kstats.py)
 #   bench_traced.json    the bench line of that traced run; trace_exit.txt its exit status
-#   pmc_summary.json     FETCH_SIZE / WRITE_SIZE per dispatch (separate --pmc passes), stamped with
-#                        the library's sha256 (bench.py uses it as roofline.traffic only if it matches)
+#   pmc_summary.json     FETCH_SIZE / WRITE_SIZE per dispatch (separate --pmc passes) and the VALU
+#                        counts of k_acc / k_ntt_pass (tools/pmc_valu.sh), stamped with the library's
+#                        sha256 (bench.py uses them -- roofline.traffic, compute_roofline -- only if it
+#                        matches)
 #   pmc_kernels.txt      per-kernel SQ / LDS / HBM counters of the MSM kernels (tools/pmc_kernels.sh)
 #   prove_kstats.txt     kernel statistics of the 2^20 naive_prover pipeline (tools/prof_prove.sh)
 set -o pipefail
@@ -27,6 +29,7 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_f -o 
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_w -o run -- python3 bench.py --no-cpu --sizes "" --ipa 0 --prove 0 $LEGS "" --steps 3 --warmup 1 > /dev/null 2>&1 || exit 1
 python3 tools/make_pmc_summary.py $O/pmc_f $O/pmc_w $O/pmc_summary.json "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes) of 'python3 bench.py --no-cpu --sizes \"\" --ipa 0 --prove 0 $LEGS \"\" --steps 3 --warmup 1', ${tag}" > /dev/null
 rm -rf $O/trace $O/pmc_f/*/ $O/pmc_w/*/ 2>/dev/null
+bash tools/pmc_valu.sh $O/pmc_summary.json > $O/pmc_valu.log 2>&1 || { tail -5 $O/pmc_valu.log; exit 1; }
 python3 tools/kstats.py $O/kernel_stats.csv > $O/kstats.txt
 bash tools/pmc_kernels.sh $tag > /dev/null && cp gpurun_out/pmc_k/$tag/summary.txt $O/pmc_kernels.txt
 rm -rf gpurun_out/pmc_k/$tag/[a-e]

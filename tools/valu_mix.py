@@ -7,8 +7,8 @@ translation unit), disassembles them (llvm-objdump), and for each kernel whose m
 the substring prints the static VALU counts of the whole function and of its innermost loop body (the
 region between the largest backward branch's target and the branch), split into the issue classes
 measured by tools/micro/issue_bench.hip:
-  mad64 -- v_mad_u64_u32 / v_mad_i64_i32;
-  vop3_64 -- the other 64-bit VOP3 integer ops (v_ashrrev_i64, v_lshl_add_u64, v_lshlrev_b64, ...);
+  mad_u64, mad_i64 -- v_mad_u64_u32, v_mad_i64_i32;
+  ashr64  -- v_ashrrev_i64;  other64 -- the other 64-bit VOP3 integer ops (v_lshl_add_u64, ...);
   vop3  -- every other VALU in a VOP3 encoding (no _e32 suffix: v_add3_u32, v_alignbit_b32,
            v_bfe_*, *_e64 forms, ...);
   vop2  -- VOP1 / VOP2 encodings (_e32 suffix: v_and_b32_e32, v_add_u32_e32, v_mov_b32_e32, ...).
@@ -71,17 +71,25 @@ def functions(co):
 def klass(op):
     if not op.startswith("v_") or op.startswith("v_mfma"):
         return None
-    if op in ("v_mad_u64_u32", "v_mad_i64_i32"):
-        return "mad64"
+    if op == "v_mad_u64_u32":
+        return "mad_u64"
+    if op == "v_mad_i64_i32":
+        return "mad_i64"
     if op.endswith("_e32") or "_dpp" in op or "_sdwa" in op:
         return "vop2"
+    if op == "v_ashrrev_i64":
+        return "ashr64"
     if any(t in op for t in ("_i64", "_u64", "_b64")):
-        return "vop3_64"
+        return "other64"
     return "vop3"
 
 
+CLASSES = ("mad_u64", "mad_i64", "ashr64", "other64", "vop3", "vop2")
+INT64 = ("mad_u64", "mad_i64", "ashr64", "other64")
+
+
 def mix(insts):
-    c = {"mad64": 0, "vop3_64": 0, "vop3": 0, "vop2": 0}
+    c = dict.fromkeys(CLASSES, 0)
     for _, op, _ in insts:
         k = klass(op)
         if k:
