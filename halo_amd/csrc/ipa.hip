@@ -1018,7 +1018,7 @@ struct halo_ipa_session {
     // ---- resources (kept across pooled uses)
     int device = -1;
     hipStream_t s = nullptr;
-    hipStream_t s2 = nullptr;           // weighted rounds above IPA_PAIR_MAX: R's MSM (created on first use)
+    hipStream_t s2 = nullptr;           // weighted rounds above ipa_pair_max: R's MSM (created on first use)
     bool solo = true;                   // the round call advances this session alone (s2 is used then)
     bool slots_reset = false;           // this opening restarted the MSM slot assignment (msm_slots_reset)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -1407,7 +1407,6 @@ static size_t ipa_srs_tail_max() {  // tuning "ipa_srs_tail_n" (default 4096; th
 // Measured (opening 2^12 / 2^16 / 2^20, ms): 1024: 6.2 / 10.4 / 29.3; 2048: 5.6 / 9.3 / 27.6;
 // 4096 (tail 4096): 6.5 / 10.7 / 27.4; 8192: 6.4 / 12.8 / 28.4.
 // (tuning "ipa_mat_n", default 2048)
-constexpr size_t IPA_PAIR_MAX = (size_t)1 << 18;  // weighted rounds: L and R as one MSM up to this half
 static size_t ipa_mat_n() {  // 0 keeps the weighted rounds to the end
     return (size_t)tuning(TUNE_IPA_MAT_N);
 }
@@ -2085,7 +2084,7 @@ static int ipa_round_launch(DeviceState* st, halo_ipa_session* ses) {
         // 2^14 / 2^17 / 2^18 / 2^19 / 2^20 ms, two MSMs vs one: 7.5 / 11.3 / 14.4 / 19.3 / 27.2 vs
         // 6.9 / 10.3 / 13.2 / 17.8 / 29.0 (round 4, after the sort and accumulation changes: 2^20
         // 21.7 vs 22.7 ms)
-        if (half <= IPA_PAIR_MAX) {
+        if (half <= (size_t)tuning(TUNE_IPA_PAIR_MAX)) {
             const MsmPairIO io{sl, sr, sm + 128, sm + 160, sm + 512, sm + 640};
             HALO_CHECK(msm_srs_pairs_device(st, ses->curve, 1, &io, half, lgm, ses->htab_ptr, s, hr));
         } else if (ses->solo) {

@@ -17,6 +17,8 @@
 // entries is known only on the device (scan total) -- kernels bound themselves by it, so no host
 // round trip is needed.
 #include <algorithm>
+#include <utility>
+#include <vector>
 #include <type_traits>
 #include <cstdlib>
 
@@ -31,7 +33,12 @@ namespace halo {
 constexpr int RS_THREADS = 512;
 // Tiles of RS_THREADS x 16 rounds: 8192 entries, runs of ~32 entries = 128 B per digit, 64 KB of LDS
 // staging.  (Measured: 4096-entry tiles, 4 workgroups per CU, were no faster.)
-constexpr int RS_BINS = 256;
+constexpr int RS_BINS = 256;      // bins of an 8-bit digit pass
+constexpr int RS_BINS_MAX = 512;  // ... of a 9-bit pass (17- / 18-bit keys in two passes)
+// tile rounds of a digit pass: 16 (8192 entries) for 8-bit digits; 14 for 9-bit digits, whose
+// per-wave histograms (8 x 512 words) would otherwise leave one scatter workgroup per CU
+template <int BITS>
+constexpr int rs_rounds() { return BITS == 8 ? 16 : 14; }
 constexpr size_t RS_STAGE_BYTES = 2 * 4 * RS_THREADS * 16;  // k_rs_scatter's key / value staging
 constexpr uint32_t RS_NONE = 0xffffffffu;
 
@@ -108,27 +115,30 @@ HALO_DEV bool rs_last_arriver(uint32_t* c, uint32_t total, uint32_t* flag) {
     __syncthreads();
     return *flag != 0;
 }
+template <int BINS>
 HALO_DEV void rs_publish_and_scan(const uint32_t* h, uint32_t tile, uint32_t ntiles, uint32_t* hist, uint32_t* chunk,
                                   uint32_t* ctr, uint32_t* count) {
+    static_assert(BINS <= RS_THREADS, "one thread per digit");
+    constexpr int DPL = BINS / 64;  // digits per lane of the wave-0 scan
     __shared__ uint32_t flag;
-    __shared__ uint32_t s[RS_BINS];
+    __shared__ uint32_t s[BINS];
     const uint32_t d = threadIdx.x;
-    if (d < RS_BINS) __hip_atomic_store(hist + (size_t)tile * RS_BINS + d, h[d], RS_RLX_AGENT);
+    if (d < BINS) __hip_atomic_store(hist + (size_t)tile * BINS + d, h[d], RS_RLX_AGENT);
     const uint32_t ch = tile / RS_CH, nchunks = (ntiles + RS_CH - 1) / RS_CH;
     const uint32_t t0 = ch * RS_CH, nt = min((uint32_t)RS_CH, ntiles - t0);
     if (!rs_last_arriver(ctr + ch, nt, &flag)) return;
     rs_acquire();
-    if (d < RS_BINS) {
+    if (d < BINS) {
         uint32_t v[RS_CH];
 #pragma unroll
-        for (int i = 0; i < RS_CH; i++) v[i] = (i < (int)nt) ? hist[(size_t)(t0 + i) * RS_BINS + d] : 0u;
+        for (int i = 0; i < RS_CH; i++) v[i] = (i < (int)nt) ? hist[(size_t)(t0 + i) * BINS + d] : 0u;
         uint32_t run = 0;
 #pragma unroll
         for (int i = 0; i < RS_CH; i++) {
-            if (i < (int)nt) hist[(size_t)(t0 + i) * RS_BINS + d] = run;  // read by the scatter launch
+            if (i < (int)nt) hist[(size_t)(t0 + i) * BINS + d] = run;  // read by the scatter launch
             run += v[i];
         }
-        __hip_atomic_store(chunk + (size_t)ch * RS_BINS + d, run, RS_RLX_AGENT);
+        __hip_atomic_store(chunk + (size_t)ch * BINS + d, run, RS_RLX_AGENT);
     }
     if (d == 0) __hip_atomic_store(ctr + ch, 0u, RS_RLX_AGENT);
     if (!rs_last_arriver(ctr + nchunks, nchunks, &flag)) return;
@@ -136,24 +146,24 @@ HALO_DEV void rs_publish_and_scan(const uint32_t* h, uint32_t tile, uint32_t nti
     // per digit: total over the chunks, then (after the digit scan) the chunks' exclusive prefix plus
     // the digit's base; the loads go in batches of U so their latencies overlap
     constexpr uint32_t U = 16;
-    if (d < RS_BINS) {
+    if (d < BINS) {
         uint32_t run = 0;
         for (uint32_t c0 = 0; c0 < nchunks; c0 += U) {
             uint32_t v[U];
 #pragma unroll
-            for (uint32_t i = 0; i < U; i++) v[i] = (c0 + i < nchunks) ? chunk[(size_t)(c0 + i) * RS_BINS + d] : 0u;
+            for (uint32_t i = 0; i < U; i++) v[i] = (c0 + i < nchunks) ? chunk[(size_t)(c0 + i) * BINS + d] : 0u;
 #pragma unroll
             for (uint32_t i = 0; i < U; i++) run += v[i];
         }
         s[d] = run;
     }
     __syncthreads();
-    // exclusive scan of the digit totals (wave 0: 4 digits per lane)
+    // exclusive scan of the digit totals (wave 0: DPL digits per lane)
     if (d < 64) {
-        uint32_t c[4], sum = 0;
+        uint32_t c[DPL], sum = 0;
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            c[q] = s[d * 4 + q];
+        for (int q = 0; q < DPL; q++) {
+            c[q] = s[d * DPL + q];
             sum += c[q];
         }
         uint32_t incl = sum;
@@ -164,22 +174,22 @@ HALO_DEV void rs_publish_and_scan(const uint32_t* h, uint32_t tile, uint32_t nti
         }
         uint32_t ex = incl - sum;
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            s[d * 4 + q] = ex;
+        for (int q = 0; q < DPL; q++) {
+            s[d * DPL + q] = ex;
             ex += c[q];
         }
         if (d == 63 && count) *count = incl;
     }
     __syncthreads();
-    if (d < RS_BINS) {
+    if (d < BINS) {
         uint32_t run = s[d];
         for (uint32_t c0 = 0; c0 < nchunks; c0 += U) {
             uint32_t v[U];
 #pragma unroll
-            for (uint32_t i = 0; i < U; i++) v[i] = (c0 + i < nchunks) ? chunk[(size_t)(c0 + i) * RS_BINS + d] : 0u;
+            for (uint32_t i = 0; i < U; i++) v[i] = (c0 + i < nchunks) ? chunk[(size_t)(c0 + i) * BINS + d] : 0u;
 #pragma unroll
             for (uint32_t i = 0; i < U; i++) {
-                if (c0 + i < nchunks) chunk[(size_t)(c0 + i) * RS_BINS + d] = run;
+                if (c0 + i < nchunks) chunk[(size_t)(c0 + i) * BINS + d] = run;
                 run += v[i];
             }
         }
@@ -187,12 +197,14 @@ HALO_DEV void rs_publish_and_scan(const uint32_t* h, uint32_t tile, uint32_t nti
     if (d == 0) __hip_atomic_store(ctr + nchunks, 0u, RS_RLX_AGENT);
 }
 
-template <int ROUNDS, bool PASS0>
+template <int BITS, bool PASS0>
 __global__ __launch_bounds__(RS_THREADS) void k_rs_hist(RsIn in, uint32_t ntiles, uint32_t* hist, uint32_t* chunk,
                                                         uint32_t* ctr, uint32_t* count) {
+    constexpr int ROUNDS = rs_rounds<BITS>();
+    constexpr int BINS = 1 << BITS;
     constexpr int RS_TILE = RS_THREADS * ROUNDS;
-    __shared__ uint32_t h[RS_BINS];
-    if (threadIdx.x < RS_BINS) h[threadIdx.x] = 0;
+    __shared__ uint32_t h[BINS];
+    if (threadIdx.x < BINS) h[threadIdx.x] = 0;
     const size_t limit = rs_limit(in);
     const size_t base = (size_t)blockIdx.x * RS_TILE;
     // every round's load in flight before the first use (keys only: the histogram needs no values)
@@ -205,10 +217,10 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_hist(RsIn in, uint32_t ntiles
     for (int r = 0; r < ROUNDS; r++) {
         uint32_t k, v;
         if (rs_decode<PASS0>(in, base + (size_t)r * RS_THREADS + threadIdx.x, limit, A[r], Bv[r], k, v))
-            atomicAdd(&h[(k >> in.shift) & 255u], 1u);
+            atomicAdd(&h[(k >> in.shift) & (BINS - 1u)], 1u);
     }
     __syncthreads();
-    rs_publish_and_scan(h, blockIdx.x, ntiles, hist, chunk, ctr, count);
+    rs_publish_and_scan<BINS>(h, blockIdx.x, ntiles, hist, chunk, ctr, count);
 }
 
 // Fused first pass of the window-shifted MSM's sort (single bucket set): the entries are recoded
@@ -228,28 +240,32 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_hist_sc(const uint4* sc, uint
             if (d != DIGIT_NONE) atomicAdd(&h[d & 255u], 1u);
         });
     __syncthreads();
-    rs_publish_and_scan(h, blockIdx.x, ntiles, hist, chunk, ctr, count);
+    rs_publish_and_scan<RS_BINS>(h, blockIdx.x, ntiles, hist, chunk, ctr, count);
 }
 
 // Each wave owns a contiguous eighth of the tile (1024 entries, 16 rounds of 64), so ranking is
 // wave-local (ballots + a wave-private LDS run counter per digit) and the workgroup needs only
 // three barriers: after the per-wave histograms, after the prefix, after staging.
 // SF: void, or the scalar field of a fused first pass (k_rs_hist_sc's entries, in.sc != null)
-template <int ROUNDS, class SF = void, bool PASS0 = false>
+template <int BITS, class SF = void, bool PASS0 = false>
 __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(RsIn in, const uint32_t* tile_off, const uint32_t* chunk_off,
                                                            uint32_t* keys_out, uint32_t* vals_out) {
+    constexpr int ROUNDS = rs_rounds<BITS>();
+    constexpr int BINS = 1 << BITS;
+    constexpr uint32_t DMASK = BINS - 1;
+    constexpr int DPL = BINS / 64;
     constexpr int RS_TILE = RS_THREADS * ROUNDS;
     constexpr int WAVES = RS_THREADS / 64;
-    constexpr int PER_WAVE = RS_TILE / WAVES;  // 1024
-    __shared__ uint32_t goff[RS_BINS];           // global start of this tile's run per digit
-    __shared__ uint32_t lstart[RS_BINS];         // tile-local start per digit
-    __shared__ uint32_t wpos[WAVES][RS_BINS];    // per-wave histogram, then per-wave next position
+    constexpr int PER_WAVE = RS_TILE / WAVES;  // 1024 (8-bit digits) / 896 (9-bit)
+    __shared__ uint32_t goff[BINS];           // global start of this tile's run per digit
+    __shared__ uint32_t lstart[BINS];         // tile-local start per digit
+    __shared__ uint32_t wpos[WAVES][BINS];    // per-wave histogram, then per-wave next position
     // the staging arrays (64 KB) are dynamic LDS (RS_STAGE_BYTES at launch): with a static size the
     // compiler derives the LDS-limited occupancy (4 waves per SIMD) and pads the VGPR allocation to
     // match it (76 used -> 97 allocated), which would keep the workgroup from being resident beside
     // the previous MSM's tail kernels (k_merge: 2 waves per SIMD of 161 VGPRs).  (Measured: 2^20
     // headline unchanged, 1.337 vs 1.336 ms -- the front and the tail contend for VALU issue, not slots.)
-    static_assert(2 * 4 * RS_TILE == RS_STAGE_BYTES, "staging size");
+    static_assert(2 * 4 * RS_TILE <= RS_STAGE_BYTES, "staging size");
     extern __shared__ uint32_t rs_stage[];
     uint32_t* skey = rs_stage;
     uint32_t* sval = rs_stage + RS_TILE;
@@ -288,18 +304,18 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(RsIn in, const uint32
             if (rs_decode<PASS0>(in, wbase + (size_t)r * 64 + lane, limit, A[r], Bv[r], K[r], V[r])) validmask |= 1u << r;
         }
     }
-    if (tid < RS_BINS) {
-        goff[tid] = tile_off[(size_t)blockIdx.x * RS_BINS + tid] + chunk_off[(size_t)(blockIdx.x / RS_CH) * RS_BINS + tid];
+    if (tid < BINS) {
+        goff[tid] = tile_off[(size_t)blockIdx.x * BINS + tid] + chunk_off[(size_t)(blockIdx.x / RS_CH) * BINS + tid];
 #pragma unroll
         for (int w = 0; w < WAVES; w++) wpos[w][tid] = 0;
     }
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < R; r++)
-        if ((validmask >> r) & 1u) atomicAdd(&wpos[wave][(K[r] >> in.shift) & 255u], 1u);
+        if ((validmask >> r) & 1u) atomicAdd(&wpos[wave][(K[r] >> in.shift) & DMASK], 1u);
     __syncthreads();
     // thread tid = digit: tile-local exclusive prefix over digits (wave-0 shuffle scan of 4 digits/lane)
-    if (tid < RS_BINS) {
+    if (tid < BINS) {
         uint32_t cnt = 0;
 #pragma unroll
         for (int w = 0; w < WAVES; w++) cnt += wpos[w][tid];
@@ -307,11 +323,11 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(RsIn in, const uint32
     }
     __syncthreads();
     if (wave == 0) {
-        uint32_t c[4];
+        uint32_t c[DPL];
         uint32_t sum = 0;
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            c[q] = lstart[lane * 4 + q];
+        for (int q = 0; q < DPL; q++) {
+            c[q] = lstart[lane * DPL + q];
             sum += c[q];
         }
         uint32_t incl = sum;
@@ -322,14 +338,14 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(RsIn in, const uint32
         }
         uint32_t ex = incl - sum;
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            lstart[lane * 4 + q] = ex;
+        for (int q = 0; q < DPL; q++) {
+            lstart[lane * DPL + q] = ex;
             ex += c[q];
         }
         if (lane == 63) total = incl;
     }
     __syncthreads();
-    if (tid < RS_BINS) {
+    if (tid < BINS) {
         uint32_t p = lstart[tid];
 #pragma unroll
         for (int w = 0; w < WAVES; w++) {
@@ -347,7 +363,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(RsIn in, const uint32
 #pragma unroll
         for (int r = 0; r < R; r++) {
             if (!((validmask >> r) & 1u)) continue;
-            const uint32_t pos = atomicAdd(&wpos[wave][(K[r] >> in.shift) & 255u], 1u);
+            const uint32_t pos = atomicAdd(&wpos[wave][(K[r] >> in.shift) & DMASK], 1u);
             skey[pos] = K[r];
             sval[pos] = V[r];
         }
@@ -357,10 +373,10 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(RsIn in, const uint32
     for (int r = 0; r < R; r++) {
         const uint32_t k = K[r], v = V[r];
         const bool valid = (validmask >> r) & 1u;
-        const uint32_t dg = (k >> in.shift) & 255u;
+        const uint32_t dg = (k >> in.shift) & DMASK;
         uint64_t same = __ballot(valid);
 #pragma unroll
-        for (int b = 0; b < 8; b++) {
+        for (int b = 0; b < BITS; b++) {
             const uint64_t m = __ballot((dg >> b) & 1u);
             same &= ((dg >> b) & 1u) ? m : ~m;
         }
@@ -379,7 +395,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(RsIn in, const uint32
     // write runs: staging index i belongs to digit dg, global position goff[dg] + (i - lstart[dg])
     for (uint32_t i = tid; i < total; i += RS_THREADS) {
         const uint32_t k = skey[i];
-        const uint32_t dg = (k >> in.shift) & 255u;
+        const uint32_t dg = (k >> in.shift) & DMASK;
         const uint32_t g = goff[dg] + (i - lstart[dg]);
         if (g >= in.E) continue;  // inconsistent offsets: never write outside the arrays
         keys_out[g] = k;
@@ -486,30 +502,51 @@ int device_exclusive_scan(const uint32_t* in, size_t n, uint32_t* out, DevBuf& t
     return HALO_OK;
 }
 
+// Digit passes (shift, bits) for key_bits-bit keys: 8-bit passes up to 16 bits; 17 / 18 bits in two
+// passes with a 9-bit one (the IPA's paired L / R MSMs: key = (side, 16-bit bucket)) instead of a third
+// pass; wider keys in 8-bit passes.  A fused first pass (recoding from the scalars) is always 8 bits.
+static std::vector<std::pair<uint32_t, uint32_t>> rs_plan(uint32_t key_bits, bool fused) {
+    std::vector<std::pair<uint32_t, uint32_t>> P;
+    if (key_bits == 17 || (key_bits == 18 && !fused)) {
+        const uint32_t b0 = (key_bits == 18) ? 9 : 8;
+        P.push_back({0, b0});
+        P.push_back({b0, key_bits - b0});
+        return P;
+    }
+    const uint32_t passes = std::max<uint32_t>(1, (key_bits + 7) / 8);
+    for (uint32_t p = 0; p < passes; p++) P.push_back({8 * p, 8});
+    return P;
+}
+
 int msm_radix_sort(const uint32_t* digits, size_t E, size_t npw, uint32_t B, uint32_t key_bits, SortScratch& S,
                    uint32_t** keys_out, uint32_t** vals_out, const uint32_t** count_out, uint32_t* bstart, size_t NB,
                    hipStream_t s, const RsFused* fused) {
-    constexpr int RS_TILE = RS_THREADS * 16;
-    const uint32_t ntiles = (uint32_t)std::max<size_t>(1, (E + RS_TILE - 1) / RS_TILE);
+    const auto plan = rs_plan(key_bits, fused != nullptr);
+    auto tiles_of = [&](uint32_t bits) {
+        const size_t tile = (size_t)RS_THREADS * (bits == 8 ? rs_rounds<8>() : rs_rounds<9>());
+        return (uint32_t)std::max<size_t>(1, (E + tile - 1) / tile);
+    };
+    uint32_t ntmax = 1;
+    for (auto& q : plan) ntmax = std::max(ntmax, tiles_of(q.second));
     // fused first pass: tiles of RS_THREADS scalars x W windows
-    const uint32_t ntiles0 = fused ? (uint32_t)std::max<size_t>(1, (fused->n + RS_THREADS - 1) / RS_THREADS) : ntiles;
-    const uint32_t ntmax = std::max(ntiles, ntiles0);
+    const uint32_t ntiles0 = fused ? (uint32_t)std::max<size_t>(1, (fused->n + RS_THREADS - 1) / RS_THREADS) : 0u;
+    ntmax = std::max(ntmax, ntiles0);
     HALO_CHECK(S.keys[0].reserve(std::max<size_t>(E, 1) * 4));
     HALO_CHECK(S.keys[1].reserve(std::max<size_t>(E, 1) * 4));
     HALO_CHECK(S.vals[0].reserve(std::max<size_t>(E, 1) * 4));
     HALO_CHECK(S.vals[1].reserve(std::max<size_t>(E, 1) * 4));
-    HALO_CHECK(S.hist.reserve((size_t)RS_BINS * ntmax * 4));
+    HALO_CHECK(S.hist.reserve((size_t)RS_BINS_MAX * ntmax * 4));
     const size_t nchmax = (ntmax + RS_CH - 1) / RS_CH;
-    HALO_CHECK(S.offs.reserve(nchmax * RS_BINS * 4));
+    HALO_CHECK(S.offs.reserve(nchmax * RS_BINS_MAX * 4));
     HALO_CHECK(S.count.reserve(16));
     // the last-arriver counters start at zero and are reset by their last arrivers
     // (a reallocation may return the freed address: the capacity, not the pointer, tells)
     const size_t ctr_had = S.ctr.bytes;
     HALO_CHECK(S.ctr.reserve((nchmax + 1) * 4));
     if (S.ctr.bytes != ctr_had) HALO_HIP(hipMemsetAsync(S.ctr.ptr, 0, S.ctr.bytes, s));
-    const uint32_t passes = std::max<uint32_t>(1, (key_bits + 7) / 8);
     int cur = 0;
-    for (uint32_t p = 0; p < passes; p++) {
+    for (uint32_t p = 0; p < (uint32_t)plan.size(); p++) {
+        const uint32_t bits = plan[p].second;
         RsIn in;
         in.digits = digits;
         in.keys = S.keys[cur ^ 1].as<const uint32_t>();
@@ -519,9 +556,11 @@ int msm_radix_sort(const uint32_t* digits, size_t E, size_t npw, uint32_t B, uin
         in.npw = npw;
         in.B = B;
         in.pass = p;
-        in.shift = 8 * p;
+        in.shift = plan[p].first;
         const bool fp = fused && p == 0;
-        const uint32_t nt = fp ? ntiles0 : ntiles;
+        const uint32_t nt = fp ? ntiles0 : tiles_of(bits);
+        uint32_t* hist = S.hist.as<uint32_t>();
+        uint32_t* offs = S.offs.as<uint32_t>();
         if (fp) {
             in.sc = (const uint4*)fused->scalars;
             in.n_sc = (uint32_t)fused->n;
@@ -529,25 +568,29 @@ int msm_radix_sort(const uint32_t* digits, size_t E, size_t npw, uint32_t B, uin
             in.W = fused->W;
             DISPATCH_FIELD(fused->field, SF, {
                 hipLaunchKernelGGL(k_rs_hist_sc<SF>, dim3(nt), dim3(RS_THREADS), 0, s, in.sc, in.n_sc, in.c, in.W, nt,
-                                   S.hist.as<uint32_t>(), S.offs.as<uint32_t>(), S.ctr.as<uint32_t>(),
-                                   S.count.as<uint32_t>());
-            });
-        } else {
-            // pass 0 also stores the number of valid (nonzero-digit) entries
-            auto kh = p == 0 ? k_rs_hist<16, true> : k_rs_hist<16, false>;
-            hipLaunchKernelGGL(kh, dim3(nt), dim3(RS_THREADS), 0, s, in, nt, S.hist.as<uint32_t>(), S.offs.as<uint32_t>(),
-                               S.ctr.as<uint32_t>(), p == 0 ? S.count.as<uint32_t>() : nullptr);
-        }
-        if (fp) {
-            DISPATCH_FIELD(fused->field, SF, {
-                hipLaunchKernelGGL((k_rs_scatter<16, SF>), dim3(nt), dim3(RS_THREADS), RS_STAGE_BYTES, s, in,
-                                   S.hist.as<const uint32_t>(), S.offs.as<const uint32_t>(), S.keys[cur].as<uint32_t>(),
+                                   hist, offs, S.ctr.as<uint32_t>(), S.count.as<uint32_t>());
+                hipLaunchKernelGGL((k_rs_scatter<8, SF>), dim3(nt), dim3(RS_THREADS), RS_STAGE_BYTES, s, in,
+                                   (const uint32_t*)hist, (const uint32_t*)offs, S.keys[cur].as<uint32_t>(),
                                    S.vals[cur].as<uint32_t>());
             });
         } else {
-            auto ks = p == 0 ? k_rs_scatter<16, void, true> : k_rs_scatter<16, void, false>;
-            hipLaunchKernelGGL(ks, dim3(nt), dim3(RS_THREADS), RS_STAGE_BYTES, s, in, S.hist.as<const uint32_t>(),
-                               S.offs.as<const uint32_t>(), S.keys[cur].as<uint32_t>(), S.vals[cur].as<uint32_t>());
+            // pass 0 also stores the number of valid (nonzero-digit) entries
+            uint32_t* cnt = p == 0 ? S.count.as<uint32_t>() : nullptr;
+            if (bits == 9) {
+                auto kh = p == 0 ? k_rs_hist<9, true> : k_rs_hist<9, false>;
+                auto ks = p == 0 ? k_rs_scatter<9, void, true> : k_rs_scatter<9, void, false>;
+                hipLaunchKernelGGL(kh, dim3(nt), dim3(RS_THREADS), 0, s, in, nt, hist, offs, S.ctr.as<uint32_t>(), cnt);
+                // (the exact staging: 2 x 4 B x 7168 entries, so two workgroups fit in a CU's LDS)
+                hipLaunchKernelGGL(ks, dim3(nt), dim3(RS_THREADS), 2 * 4 * RS_THREADS * rs_rounds<9>(), s, in,
+                                   (const uint32_t*)hist, (const uint32_t*)offs, S.keys[cur].as<uint32_t>(),
+                                   S.vals[cur].as<uint32_t>());
+            } else {
+                auto kh = p == 0 ? k_rs_hist<8, true> : k_rs_hist<8, false>;
+                auto ks = p == 0 ? k_rs_scatter<8, void, true> : k_rs_scatter<8, void, false>;
+                hipLaunchKernelGGL(kh, dim3(nt), dim3(RS_THREADS), 0, s, in, nt, hist, offs, S.ctr.as<uint32_t>(), cnt);
+                hipLaunchKernelGGL(ks, dim3(nt), dim3(RS_THREADS), RS_STAGE_BYTES, s, in, (const uint32_t*)hist,
+                                   (const uint32_t*)offs, S.keys[cur].as<uint32_t>(), S.vals[cur].as<uint32_t>());
+            }
         }
         HALO_HIP(hipGetLastError());
         cur ^= 1;

@@ -6,6 +6,8 @@ sys.path.insert(0, '/root/repo')
 import numpy as np
 from halo_amd import _lib as H
 H.ensure_device(0)
+for _kv in [x for x in os.environ.get('TUNE', '').split(',') if x]:  # tuning A/B: TUNE=key=value,...
+    H.set_tuning(_kv.split('=')[0], int(_kv.split('=')[1]))
 L = H.load()
 R = 0x40000000000000000000000000000000224698FC0994A8DD8C46EB2100000001
 

@@ -16,6 +16,8 @@ from halo_amd import pcdl  # noqa: E402
 def main():
     lgs = [int(a) for a in sys.argv[1:]] or [2, 6, 10, 12, 16]
     H.ensure_device(0)
+    for _kv in [x for x in os.environ.get('TUNE', '').split(',') if x]:  # tuning A/B: TUNE=key=value,...
+        H.set_tuning(_kv.split('=')[0], int(_kv.split('=')[1]))
     L = H.load()
     N = 1 << max(lgs)
     H.check(L.halo_srs_synthesize(0, N, 0x50434C44))

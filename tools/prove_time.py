@@ -6,6 +6,8 @@ from halo_amd import prover
 if os.environ.get("NO_XI") == "1":  # A/B: H' = xi_0 H on the host side (halo_curve_op + H' sessions)
     del prover.DeviceBackend.ipa_many_xi
 H.ensure_device(0)
+for _kv in [x for x in os.environ.get('TUNE', '').split(',') if x]:  # tuning A/B: TUNE=key=value,...
+    H.set_tuning(_kv.split('=')[0], int(_kv.split('=')[1]))
 L = H.load()
 for arg in (sys.argv[1:] or ['16', '20']):
     logn = int(arg)
