@@ -381,15 +381,20 @@ extern "C" int halo_pcdl_hiding_blind(halo_curve_t curve, const halo_fe_t* q, si
     const size_t n = d + 1;
     HALO_CHECK(st->scratch[0].reserve(d * 32 + 64));
     HALO_CHECK(st->scratch[1].reserve(n * 32));
-    HALO_CHECK(st->scratch[2].reserve(64 + 64));
+    HALO_CHECK(st->scratch[2].reserve(64 + 128));
     char* small = st->scratch[2].as<char>();
     HALO_CHECK(copy_h2d(st->scratch[0].ptr, q, d * 32, s));
     HALO_CHECK(copy_h2d(small, z, 32, s));
     HALO_CHECK(copy_h2d(small + 32, w_bar, 32, s));
     HALO_CHECK(pcdl_pbar_device(curve, st->scratch[0].ptr, d, small, st->scratch[1].ptr, s));
-    HALO_CHECK(msm_srs_device(st, curve, st->scratch[1].ptr, n, small + 32, small + 64, s));
+    // C_bar as packed XYZZ, converted on the host (no inversion on the MSM's last lane)
+    HALO_CHECK(msm_srs_device(st, curve, st->scratch[1].ptr, n, small + 32, small + 64, s, false, true));
     if (p_bar_out) HALO_CHECK(copy_d2h(p_bar_out, st->scratch[1].ptr, n * 32, s));
-    return copy_d2h(C_bar_out, small + 64, 64, s);
+    alignas(16) uint64_t buf[16];
+    HALO_CHECK(copy_d2h(buf, small + 64, 128, s));
+    HALO_HIP(hipStreamSynchronize(s));
+    host_xyzz_to_wrapped(curve, buf, C_bar_out);
+    return HALO_OK;
 }
 
 extern "C" int halo_pcdl_hiding_combine(halo_curve_t curve, const halo_fe_t* p, size_t len, const halo_fe_t* p_bar,

@@ -331,18 +331,19 @@ static int dot_device(int field, const void* x, const void* y, size_t n, void* o
 // session keeps G0 = G at the switch round and the fold weights w (G_j[i] = sum_u w[u] G0[i + u len],
 // fold: w' = interleave(w, xi w)).  L and R are then direct sums over G0 with expanded scalars
 //   k = j + u len:  s[k] = c[m + j] w[u] (j < m, -> L),  c[j - m] w[u] (j >= m, -> R),
-// evaluated from a table d 2^(4 win) G0[k] (win < 32, 1 <= d <= 15, built once per session): each
-// scalar is split by GLV, s = k1 + lambda k2 with |k1|, |k2| < 2^128, so every (k, win, half) term
-// is one table entry (or phi of it, x -> beta x) selected by a 4-bit digit -- no per-term
-// double-and-add chain on the rounds' critical path -- and the terms go through block trees.  The
-// table's doubling chain is 124 doublings instead of 248; the 15 multiples of each 2^(4 win) G0[k]
-// cost 14 curve operations per (win, k) lane, once.
+// evaluated from a table d 2^(4 win) G0[k] (win < 32, 1 <= d <= 8, built once per session): each
+// scalar is split by GLV, s = k1 + lambda k2 with |k1|, |k2| < 0.47 x 2^128, so every (k, win, half)
+// term is one table entry (or phi of it, x -> beta x, or its negative) selected by a signed 4-bit
+// digit in [-8, 7] -- no per-term double-and-add chain on the rounds' critical path -- and the terms
+// go through block trees.  The table's doubling chain is 124 doublings instead of 248; the 8
+// multiples of each 2^(4 win) G0[k] cost 7 curve operations per (win, k), once (round 5: signed
+// digits, was 15 unsigned multiples -- half the table build and half the table's footprint).
 // U = sum_u w[u] G0[u] at the end.  c and z keep their ordinary elementwise folds (pcdl.rs:430-435).
 constexpr size_t IPA_TAIL_N = 2048;
 constexpr int IPA_HTAB = 128;  // entries 2^i H' of the session's hiding table (GLV split of the scalar)
 constexpr int TAIL_DB = 4;                            // digit bits
 constexpr int TAIL_TBL = 128 / TAIL_DB;               // table windows per 128-bit GLV half
-constexpr int TAIL_MUL = (1 << TAIL_DB) - 1;          // multiples d = 1..15 per window
+constexpr int TAIL_MUL = 1 << (TAIL_DB - 1);           // multiples d = 1..8 per window (signed digits)
 constexpr int TAIL_WIN = 2 * TAIL_TBL;  // terms per point: 32 windows x (k1, k2)
 // threads per tail block: 256, one wave per SIMD (512 measured slower, opening 2^10 1.93 -> 2.13 ms: two
 // waves' quad trees then share a SIMD's issue slots)
@@ -367,15 +368,33 @@ __global__ __launch_bounds__(64) void k_tail_table(const uint4* gs, int gs_xyzz,
     }
 }
 
-// entry (w, d, k) of the tail table: d 2^(4 w) G0[k], 1 <= d <= 15 (XYZZ); ld = the number of
+// entry (w, d, k) of the tail table: d 2^(4 w) G0[k], 1 <= d <= 8 (XYZZ); ld = the number of
 // points the table was built for (a session may use a prefix of the SRS's table)
 HALO_DEV size_t tail_entry(size_t w, uint32_t d, size_t ld, size_t k) {
     return 8 * ((w * TAIL_MUL + (d - 1)) * ld + k);
 }
 
-// The multiples 2..15 of each window base P = 2^(4 w) G0[k] written by k_tail_table.  Lane
-// (j, w, k), j < 4, owns d = 4j + 1 .. 4j + 4: it forms (4j + 1) P by double-and-add, then a running
-// sum (two live points) -- at most 7 dependent curve operations per lane instead of 14.
+// Signed windows: a GLV half |k| < 0.47 x 2^128 (the lattice bound, tests/test_field_bounds.py) is kept
+// as k + 0x8888...8 (< 2^128), whose nibble e of window w is the digit e - 8 in [-8, 7] of k.
+HALO_DEV void tail_bias(uint32_t (&k)[5]) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        c += (uint64_t)k[q] + 0x88888888u;
+        k[q] = (uint32_t)c;
+        c >>= 32;
+    }
+}
+// window bw of a biased word: |digit| (0..8) and whether the digit is negative
+HALO_DEV uint32_t tail_digit(uint32_t word, uint32_t bw, bool& neg) {
+    const uint32_t e = (word >> (TAIL_DB * (bw % (32 / TAIL_DB)))) & 15u;
+    neg = e < 8;
+    return neg ? 8 - e : e - 8;
+}
+
+// The multiples 2..8 of each window base P = 2^(4 w) G0[k] written by k_tail_table.  Lane
+// (j, w, k), j < 4, owns d = 2j + 1, 2j + 2: it forms (2j + 1) P by double-and-add, then adds P --
+// at most 5 dependent curve operations per lane.
 constexpr int TAIL_MLANES = 4;
 template <class Cv>
 __global__ __launch_bounds__(64) void k_tail_mults(size_t n0, uint4* table) {
@@ -385,19 +404,15 @@ __global__ __launch_bounds__(64) void k_tail_mults(size_t n0, uint4* table) {
     const uint32_t j = (uint32_t)(t / ((size_t)TAIL_TBL * n0));
     const size_t r = t % ((size_t)TAIL_TBL * n0), w = r / n0, k = r % n0;
     const XYZZ<F> p = xyzz_load<F>(table + tail_entry(w, 1, n0, k));
-    const uint32_t s = 4 * j + 1;
+    const uint32_t s = 2 * j + 1;
     XYZZ<F> cur = p;
 #pragma unroll 1
-    for (int b = 31 - __clz(s) - 1; b >= 0; b--) {  // s P, s = 4 j + 1 (bit 0 set: the last step adds)
+    for (int b = 31 - __clz(s) - 1; b >= 0; b--) {  // s P, s = 2 j + 1 (bit 0 set: the last step adds)
         cur = xyzz_dbl(cur);
         if ((s >> b) & 1u) cur = xyzz_add(cur, p);
     }
     if (j) xyzz_store(table + tail_entry(w, s, n0, k), cur);
-#pragma unroll 1
-    for (uint32_t d = s + 1; d <= min(s + 3, (uint32_t)TAIL_MUL); d++) {
-        cur = (d == 2) ? xyzz_dbl(p) : xyzz_add(cur, p);
-        xyzz_store(table + tail_entry(w, d, n0, k), cur);
-    }
+    xyzz_store(table + tail_entry(w, s + 1, n0, k), j ? xyzz_add(cur, p) : xyzz_dbl(p));
 }
 
 // mode 0: L/R scalars of the current round (len = 2m); mode 1: U's scalars s[k] = w[k]
@@ -411,6 +426,8 @@ HALO_DEV void tail_scalar_val(const Fe<typename Cv::Scalar>& v, uint8_t sd, size
     bool n1, n2;
     fe_pack(fe_canon(fe_mul(v, one_raw)), w8);
     glv::decompose<typename Cv::K>(w8, n1, k1, n2, k2);
+    tail_bias(k1);
+    tail_bias(k2);
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         scal[8 * k + q] = k1[q];
@@ -551,12 +568,13 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail_msm(const uint4* table, s
     if (valid) {
         constexpr uint32_t DPW = 32 / TAIL_DB;  // digits per scalar word
         const uint32_t half = (uint32_t)win / TAIL_TBL, bw = (uint32_t)win % TAIL_TBL;
-        const uint32_t d = (scal[8 * k + 4 * half + bw / DPW] >> (TAIL_DB * (bw % DPW))) & (uint32_t)TAIL_MUL;
+        bool dneg;
+        const uint32_t d = tail_digit(scal[8 * k + 4 * half + bw / DPW], bw, dneg);
         const uint32_t sk = side[k];
         if (d) {
             XYZZ<F> t = xyzz_load<F>(table + tail_entry(bw, d, ld, k));
             if (half) t.X = fe_mul(t.X, fe_from_const<F>(Cv::K::BETA));  // phi
-            if ((sk >> (1 + half)) & 1u) t = xyzz_neg(t);
+            if ((((sk >> (1 + half)) & 1u) != 0) != dneg) t = xyzz_neg(t);
             acc = first ? xyzz_add(acc, t) : t;
         }
     }
@@ -783,14 +801,17 @@ __global__ __launch_bounds__(TAIL_THREADS, 1) void k_tail_round(const TailRoundA
             bool n1, n2;
             fe_pack(fe_canon(fe_mul(fe_mul(c, wu), one_raw)), w8);
             glv::decompose<typename Cv::K>(w8, n1, k1, n2, k2);
+            tail_bias(k1);
+            tail_bias(k2);
             constexpr uint32_t DPW = 32 / TAIL_DB;  // digits per scalar word
             const uint32_t win = tid & 63, half = win / TAIL_TBL, bw = win % TAIL_TBL;
             const uint32_t word = half ? tail_word(k2, bw / DPW) : tail_word(k1, bw / DPW);
-            const uint32_t d = (word >> (TAIL_DB * (bw % DPW))) & (uint32_t)TAIL_MUL;
+            bool dneg;
+            const uint32_t d = tail_digit(word, bw, dneg);
             if (d) {
                 XYZZ<F> t = xyzz_load<F>(a.table + tail_entry(bw, d, a.ld, k));
                 if (half) t.X = fe_mul(t.X, fe_from_const<F>(Cv::K::BETA));  // phi
-                if (half ? n2 : n1) t = xyzz_neg(t);
+                if ((half ? n2 : n1) != dneg) t = xyzz_neg(t);
                 acc = t;
             }
         }
@@ -1674,6 +1695,9 @@ static int ipa_eval_cs(halo_ipa_session* ses, size_t len, halo_fe_t* v_out) {
 //   (transcript: absorb C', z, v; xi_0 = challenge)
 //   halo_pcdl_open_start(H, xi_0)           H' = xi_0 H; then halo_ipa_round_lr / fold / end
 // ---------------------------------------------------------------------------------------------
+// Up to COMBINE_MSM_MAX coefficients halo_pcdl_open_combine forms C' through an MSM of alpha p_bar (see there)
+constexpr size_t COMBINE_MSM_MAX = (size_t)1 << 16;
+
 extern "C" int halo_pcdl_open_begin(halo_curve_t curve, const halo_fe_t* p, size_t len, size_t d, const halo_fe_t* z,
                                     halo_fe_t* v_out, halo_ipa_session** out) {
     clear_error();
@@ -1722,14 +1746,15 @@ extern "C" int halo_pcdl_open_blind(halo_ipa_session* ses, const halo_fe_t* q, c
     HALO_CHECK(copy_h2d(ses->tmp.ptr, q, d * 32, s));
     HALO_CHECK(copy_h2d(sm + SM_WBAR, w_bar, 32, s));
     HALO_CHECK(pcdl_pbar_device(ses->curve, ses->tmp.ptr, d, sm, ses->pbar.ptr, s));  // z at sm[0, 32)
-    if (n <= std::min(srs_small_max(), srs.n)) {  // (the combine's MSM route needs no device copy of C_bar)
-        HALO_CHECK(msm_srs_small(st, ses->curve, ses->pbar.ptr, n, sm + SM_WBAR, sm + SM_T, s, true));
-        HALO_HIP(hipMemcpyAsync(ses->pinned + 128, sm + SM_T, 128, hipMemcpyDeviceToHost, s));
-        HALO_HIP(hipStreamSynchronize(s));
-        host_xyzz_to_wrapped(ses->curve, ses->pinned + 128, C_bar);
-    } else {
-        HALO_CHECK(msm_srs_device(st, ses->curve, ses->pbar.ptr, n, sm + SM_WBAR, sm + SM_CBAR, s));
-        HALO_CHECK(copy_d2h(C_bar, sm + SM_CBAR, 64, s));
+    // C_bar as packed XYZZ, converted on the host: the MSM's last lane no longer runs an inversion (~0.1 ms
+    // of dependent multiplications at the end of the blind)
+    HALO_CHECK(msm_srs_device(st, ses->curve, ses->pbar.ptr, n, sm + SM_WBAR, sm + SM_T, s, false, true));
+    HALO_HIP(hipMemcpyAsync(ses->pinned + 128, sm + SM_T, 128, hipMemcpyDeviceToHost, s));
+    HALO_HIP(hipStreamSynchronize(s));
+    host_xyzz_to_wrapped(ses->curve, ses->pinned + 128, C_bar);
+    if (n > COMBINE_MSM_MAX) {  // pcdl_combine_device reads C_bar on the device
+        memcpy(ses->pinned + 128, C_bar, 64);
+        HALO_HIP(hipMemcpyAsync(sm + SM_CBAR, ses->pinned + 128, 64, hipMemcpyHostToDevice, s));
     }
     ses->blinded = true;
     return HALO_OK;
@@ -1766,18 +1791,12 @@ extern "C" int halo_pcdl_open_combine(halo_ipa_session* ses, const halo_fe_t* al
     // Up to COMBINE_MSM_MAX coefficients C' is formed as C + MSM(G, alpha p_bar) - w S (= C + alpha C_bar - w' S,
     // since C_bar = MSM(G, p_bar) + w_bar S): an MSM (the table path, or the bucket pipeline) instead of
     // the lone-lane scalar multiplications of k_hiding_point (~1.3 ms of dependent curve operations).
-    const SrsState& srs = st->srs[ses->curve];
-    constexpr size_t COMBINE_MSM_MAX = (size_t)1 << 16;
     if (ses->n <= COMBINE_MSM_MAX) {
         HALO_CHECK(pcdl_combine_scalars_device(ses->curve, ses->cs.ptr, ses->pbar.ptr, ses->n, sm + SM_ALPHA, sm + SM_W,
                                                sm + SM_WBAR, sm + SM_WP, sm + SM_NEGW, s));
-        if (ses->n <= std::min(srs_small_max(), srs.n)) {
-            HALO_CHECK(msm_srs_small(st, ses->curve, ses->pbar.ptr, ses->n, sm + SM_NEGW, sm + SM_T, s, true));
-            HALO_CHECK(xyzz_add_wrapped_device(ses->curve, sm + SM_T, sm + SM_C, s, false));
-        } else {
-            HALO_CHECK(msm_srs_device(st, ses->curve, ses->pbar.ptr, ses->n, sm + SM_NEGW, sm + SM_CP, s));
-            HALO_CHECK(xyzz_add_wrapped_device(ses->curve, sm + SM_T, sm + SM_C, s, true, sm + SM_CP));
-        }
+        // the MSM as packed XYZZ (no inversion on the device), + C, converted on the host below
+        HALO_CHECK(msm_srs_device(st, ses->curve, ses->pbar.ptr, ses->n, sm + SM_NEGW, sm + SM_T, s, false, true));
+        HALO_CHECK(xyzz_add_wrapped_device(ses->curve, sm + SM_T, sm + SM_C, s, false));
         HALO_HIP(hipMemcpyAsync(ses->pinned, sm + SM_WP, 32, hipMemcpyDeviceToHost, s));
         HALO_HIP(hipMemcpyAsync(ses->pinned + 128, sm + SM_T, 128, hipMemcpyDeviceToHost, s));
         HALO_HIP(hipStreamSynchronize(s));

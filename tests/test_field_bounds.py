@@ -159,3 +159,46 @@ def test_ntt_signed_products(field):
         assert (rv - av * wv * rinv) % p == 0
         bound = p + abs(av * wv) // RP + 1
         assert -bound < rv < bound + p
+
+
+# ---------------------------------------------------------------------------------------------
+# GLV halves for the IPA tail's signed 4-bit windows (ipa.hip tail_bias / tail_digit): a half k is
+# stored as |k| + 0x8888...8 in 128 bits, so |k| must stay below 2^128 - 0x8888...8 (~0.467 x 2^128).
+# ---------------------------------------------------------------------------------------------
+def _glv_consts():
+    import re
+    src = open(os.path.join(ROOT, "halo_amd", "csrc", "consts.hpp")).read()
+    out = {}
+    for name in ("PallasCurveCfg", "VestaCurveCfg"):
+        body = src[src.index(f"struct {name}"):]
+        body = body[:body.index("\n};")]
+        c = {}
+        for key in ("A1", "A2", "B1", "B2", "G1", "G2"):
+            words = re.search(rf"GLV_{key}\[\d+\] = \{{([^}}]*)\}}", body).group(1)
+            mag = sum(int(w, 16) << (32 * i) for i, w in enumerate(words.split(",")))
+            neg = int(re.search(rf"GLV_{key}_NEG = (\d)", body).group(1))
+            c[key] = -mag if neg else mag
+        out[name] = c
+    return out
+
+
+@pytest.mark.parametrize("curve,r", [("PallasCurveCfg", PRIMES["fq"]), ("VestaCurveCfg", PRIMES["fp"])])
+def test_glv_halves_fit_signed_windows(curve, r):
+    c = _glv_consts()[curve]
+    limit = (1 << 128) - sum(8 << (4 * w) for w in range(32))
+    # the rounding bound: |k1| <= (|a1| + |a2|) / 2 + 1, |k2| <= (|b1| + |b2|) / 2 + 1
+    assert (abs(c["A1"]) + abs(c["A2"])) // 2 + 1 < limit
+    assert (abs(c["B1"]) + abs(c["B2"])) // 2 + 1 < limit
+
+    def decompose(k):  # glv.hpp decompose on Python integers (round_shift384 included)
+        c1 = (k * abs(c["G1"]) + (1 << 383)) >> 384
+        c2 = (k * abs(c["G2"]) + (1 << 383)) >> 384
+        c1 = -c1 if c["G1"] < 0 else c1
+        c2 = -c2 if c["G2"] < 0 else c2
+        return k - c1 * c["A1"] - c2 * c["A2"], -c1 * c["B1"] - c2 * c["B2"]
+
+    rng = random.Random(5)
+    ks = [0, 1, r - 1, r // 2, r // 2 + 1, r // 3, 2 * r // 3] + [rng.randrange(r) for _ in range(20000)]
+    for k in ks:
+        k1, k2 = decompose(k)
+        assert abs(k1) < limit and abs(k2) < limit, (k, k1, k2)
