@@ -1967,6 +1967,63 @@ static int ipa_tail_sums(halo_ipa_session* ses, int mode, hipStream_t s) {
     return HALO_OK;
 }
 
+// MSM of at most TINY_MSM_MAX caller points (acc::prover's C = sum alpha^i U_i, acc.rs:166): the bucket
+// pipeline's latency there is its Horner over 43 windows of 6 bits (~250 quad doublings in k_final).
+// Here every scalar is split by GLV into two 128-bit halves with signed 4-bit windows (tail_bias), so
+// 32 windows suffice: wave w forms window w's term d P_i (or phi(d P_i)) for its 2n (point, half) lanes
+// by double-and-add (|d| <= 8: at most four curve operations), sums them with the wave's quad tree, and
+// k_final's Horner over the 32 window sums (4 quad doublings each) finishes: ~124 doublings in all.
+constexpr size_t TINY_MSM_MAX = 32;
+template <class Cv>
+__global__ __launch_bounds__(256) void k_tiny_window_sums(const uint4* bases, const uint4* scalars_ark, uint32_t n,
+                                                          uint4* window_sums) {
+    using F = typename Cv::Base;
+    using S = typename Cv::Scalar;
+    const uint32_t w = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    XYZZ<F> acc = xyzz_id<F>();
+    if (lane < 2 * n && w < (uint32_t)TAIL_TBL) {
+        const uint32_t i = lane >> 1, half = lane & 1u;
+        uint32_t w8[8], k1[5], k2[5];
+        bool n1, n2;
+        fe_ark_to_canonical_words<S>(scalars_ark + 2 * i, w8);
+        glv::decompose<typename Cv::K>(w8, n1, k1, n2, k2);
+        tail_bias(k1);
+        tail_bias(k2);
+        bool dneg;
+        const uint32_t bw = w, word = half ? tail_word(k2, bw / 8) : tail_word(k1, bw / 8);
+        const uint32_t d = tail_digit(word, bw, dneg);
+        Affine<F> a = aff_load<F>(bases + 4 * i);
+        if (d && !aff_is_id(a)) {
+            if (half) a.x = fe_mul(a.x, fe_from_const<F>(Cv::K::BETA));  // phi
+            if ((half ? n2 : n1) != dneg) a.y = fe_neg(a.y);
+            const XYZZ<F> P = xyzz_from_aff(a);
+            XYZZ<F> t = P;
+#pragma unroll 1
+            for (int b = 31 - __clz(d) - 1; b >= 0; b--) {
+                t = xyzz_dbl(t);
+                if ((d >> b) & 1u) t = xyzz_add(t, P);
+            }
+            acc = t;
+        }
+    }
+    acc = wave_group_sum<F>(acc, 64u);
+    if (lane == 0 && w < (uint32_t)TAIL_TBL) xyzz_store(window_sums + 8 * w, acc);
+}
+
+// sum_i scalars[i] bases[i] (internal affine bases, ark scalars, n <= TINY_MSM_MAX) -> packed XYZZ at
+// out_xyzz (device), stream-ordered on s; scratch: 32 XYZZ window sums (4 KiB).
+int halo::msm_tiny(int curve, const void* bases_int, const void* scalars_ark, size_t n, void* scratch, void* out_xyzz,
+                   hipStream_t s) {
+    if (n < 1 || n > TINY_MSM_MAX) return set_error(HALO_EINVAL, "tiny MSM: n (%zu) outside [1, %zu]", n, TINY_MSM_MAX);
+    DISPATCH_CURVE(curve, Cv, {
+        hipLaunchKernelGGL(k_tiny_window_sums<Cv>, dim3(TAIL_TBL / 4), dim3(256), 0, s, (const uint4*)bases_int,
+                           (const uint4*)scalars_ark, (uint32_t)n, (uint4*)scratch);
+    });
+    HALO_HIP(hipGetLastError());
+    return msm_final_launch(curve, (const uint4*)scratch, TAIL_TBL, TAIL_DB, nullptr, (uint4*)out_xyzz, 1, s);
+}
+size_t halo::msm_tiny_max() { return TINY_MSM_MAX; }
+
 // The SRS prefix's multiples table d 2^(4 w) G_k (k < n0 = min(srs_tab_n(), srs.n)), built on first
 // use per SRS (k_tail_table + k_tail_mults on stream s; small_tab_ev marks its completion for other
 // streams).  SrsState::invalidate_derived() (every writer of the SRS points) forces a rebuild.  The

@@ -1751,8 +1751,14 @@ extern "C" int halo_msm(halo_curve_t curve, const halo_wrapped_point_t* bases, s
     HALO_CHECK(copy_h2d(st->scratch[0].ptr, bases, n * 64, s));
     HALO_CHECK(copy_h2d(st->scratch[2].ptr, scalars, n * 32, s));
     HALO_CHECK(convert_wrapped_to_internal(curve, st->scratch[0].ptr, st->scratch[1].ptr, n, s));
-    HALO_CHECK(msm_device(st, curve, st->scratch[1].ptr, st->scratch[2].ptr, n, nullptr, nullptr, st->scratch[3].ptr, s,
-                          false, false, true));
+    if (n >= 1 && n <= msm_tiny_max()) {  // a few points: GLV windows + one 32-window Horner (ipa.hip)
+        HALO_CHECK(st->scratch[3].reserve(128 + 32 * 128));
+        HALO_CHECK(msm_tiny(curve, st->scratch[1].ptr, st->scratch[2].ptr, n, st->scratch[3].as<char>() + 128,
+                            st->scratch[3].ptr, s));
+    } else {
+        HALO_CHECK(msm_device(st, curve, st->scratch[1].ptr, st->scratch[2].ptr, n, nullptr, nullptr, st->scratch[3].ptr,
+                              s, false, false, true));
+    }
     return d2h_point(curve, st->scratch[3].ptr, out, s);
 }
 

@@ -75,6 +75,11 @@ size_t srs_small_max();  // largest MSM on the table path (HALO_SRS_SMALL_N, def
 // min(srs_tab_n(), srs.n) points); stream s waits for its completion.  Shared by the small MSMs and
 // by IPA sessions whose tail rounds start on the unfolded SRS prefix.
 int srs_small_table(DeviceState* st, int curve, hipStream_t s);
+// MSM of n <= msm_tiny_max() caller points (internal affine) by GLV windows and one Horner (ipa.hip):
+// packed XYZZ to out_xyzz (device); scratch >= 4 KiB of device memory.  Stream-ordered on s.
+int msm_tiny(int curve, const void* bases_int, const void* scalars_ark, size_t n, void* scratch, void* out_xyzz,
+             hipStream_t s);
+size_t msm_tiny_max();
 // out_xyzz: the result as 128 B packed XYZZ (host_xyzz_to_wrapped) instead of a WrappedPoint.
 int msm_srs_small(DeviceState* st, int curve, const void* scalars_ark, size_t n, const void* hide_scalar,
                   void* d_out_wrapped, hipStream_t s, bool out_xyzz = false);
