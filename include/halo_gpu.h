@@ -77,7 +77,9 @@ int halo_stream_sync(void* stream);
  * "ipa_mat_n" (weighted rounds materialise G at this length; 0 = never; default 2048),
  * "msm_multi_max" (commitment batches of polynomials up to this length run as one MSM; default
  * 2^18), "ipa_pool_keep_bytes" (an idle pooled IPA session keeps at most this many bytes of device
- * buffers; default 2^30).  Every setting yields the same results; the parity tests pin each path with it.  The
+ * buffers; default 2^30), "ipa_pair_max" (weighted rounds up to this half-length form L and R as one
+ * MSM; default 2^19), "ntt_big_max_log" (NTTs up to 2^this use 11-bit passes; default 22),
+ * "ntt_even_split" (1: stages split evenly over the passes; default 0).  Every setting yields the same results; the parity tests pin each path with it.  The
  * reference has no counterpart (host-side knob of this backend only).  HALO_EINVAL on an unknown key. */
 int halo_set_tuning(const char* key, long long value);
 int halo_get_tuning(const char* key, long long* value);
