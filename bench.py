@@ -14,8 +14,13 @@ Also measured (reported under "extra"): the 2^22 NTT + iNTT pair (BASELINE.json 
 
 The roofline object prices the dominant kernel (MSM bucket accumulation, `k_acc`): achieved =
 96 B/point (64 B affine base + 32 B scalar) x points per launch / its mean launch time
-from hipEvents recorded on its stream inside libhalo_gpu (halo_profile_*).  cpu_baseline times the
-C restatement of arkworks' msm_bigint_wnaf (oracle/oracle.c, "port") on the host cores, rank 0, N=1.
+from hipEvents recorded on its stream inside libhalo_gpu (halo_profile_*); traffic = the counted HBM
+bytes (FETCH_SIZE / WRITE_SIZE) of this library build from profiles/pmc_summary.json.  The MSM and the
+NTT are VALU-bound, so compute_roofline (k_acc) and extra.ntt.compute_roofline (k_ntt_pass) price each
+kernel's counted VALU instructions class by class at the measured per-class issue rates
+(profiles/issue_rates.json): frac = that issue-time ceiling / the measured launch time.
+cpu_baseline times the C restatement of arkworks' msm_bigint_wnaf (oracle/oracle.c, "port") on the
+host cores, rank 0, N=1.
 """
 from __future__ import annotations
 
