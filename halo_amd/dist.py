@@ -34,6 +34,18 @@ def allgather_words(words: np.ndarray, dist, device=None) -> np.ndarray:
     return torch.stack(parts).cpu().numpy().view(np.uint64).reshape((world,) + a.shape)
 
 
+def allgather_rows(t, dist):
+    """One flat all_gather_into_tensor of a rank's 1-D tensor `t` (k words) -> (world, k) tensor on t's
+    device.  The output is allocated flat (world * k), the form both RCCL and gloo accept."""
+    import torch
+
+    world = dist.get_world_size()
+    flat = t.reshape(-1)
+    out = torch.empty(world * flat.numel(), dtype=flat.dtype, device=flat.device)
+    dist.all_gather_into_tensor(out, flat)
+    return out.view(world, flat.numel())
+
+
 def allgather_points(partial: np.ndarray, dist, device=None) -> np.ndarray:
     """All-gather one WrappedPoint (8 x u64) per rank -> (world, 8) uint64 array."""
     return allgather_words(np.asarray(partial, dtype=np.uint64).reshape(8), dist, device)
@@ -563,8 +575,8 @@ def torch_gather_arrays(dist, device=None):
 def torch_reduce_lr(dist, curve, device):
     """reduce_lr() for sharded_ipa_rounds with one shard per rank on a GPU: the rank's (L_r, R_r)
     (2 x 64 B) go to the device once, one all_gather_into_tensor over RCCL collects every rank's,
-    and halo_point_sum_dev sums the L column and the R column on the device (strided 128-B rows);
-    only the two sums come back to the host, for the transcript."""
+    and halo_point_sum_dev sums the L column and the R column on the device; only the two sums come
+    back to the host, for the transcript."""
     import ctypes
 
     import torch
@@ -583,15 +595,13 @@ def torch_reduce_lr(dist, curve, device):
         (Lr, Rr), = lrs
         t = torch.from_numpy(np.concatenate([np.asarray(Lr, np.uint64).reshape(8),
                                              np.asarray(Rr, np.uint64).reshape(8)]).view(np.int64)).to(gdev)
-        allv = torch.empty((world, 16), dtype=torch.int64, device=gdev)
-        dist.all_gather_into_tensor(allv, t)
-        allv = allv.to(device)
+        allv = allgather_rows(t, dist).to(device)
+        cols = (allv[:, :8].contiguous(), allv[:, 8:].contiguous())  # every rank's L, every rank's R
         out = torch.empty(16, dtype=torch.int64, device=device)
         sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-        H.check(L_.halo_point_sum_dev(cid, ctypes.c_void_p(allv.data_ptr()), world, 128,
-                                      ctypes.c_void_p(out.data_ptr()), sp))
-        H.check(L_.halo_point_sum_dev(cid, ctypes.c_void_p(allv.data_ptr() + 64), world, 128,
-                                      ctypes.c_void_p(out.data_ptr() + 64), sp))
+        for k in range(2):
+            H.check(L_.halo_point_sum_dev(cid, ctypes.c_void_p(cols[k].data_ptr()), world, 64,
+                                          ctypes.c_void_p(out.data_ptr() + 64 * k), sp))
         o = out.cpu().numpy().view(np.uint64)
         return o[:8].copy(), o[8:].copy()
 

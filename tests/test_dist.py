@@ -450,3 +450,41 @@ def test_partition_window_bits_balanced():
         spans = [window_range(W, r, world) for r in range(world)]
         assert spans[0][0] == 0 and spans[-1][1] == W
         assert len({hi - lo for lo, hi in spans}) == 1
+
+
+def _rows_worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+
+    from halo_amd.dist import allgather_rows
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # a rank's (L_r, R_r) as 16 words, as torch_reduce_lr gathers them ahead of halo_point_sum_dev
+    t = torch.arange(16, dtype=torch.int64) + 100 * rank
+    got = allgather_rows(t, dist)
+    q.put((rank, list(got.shape), got.tolist()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_allgather_rows_gloo(world):
+    """The distributed opening's per-round L/R gather (dist.torch_reduce_lr -> allgather_rows): one
+    flat all_gather_into_tensor, (world, 16) rows in rank order.  gloo rejects a (world, k) output
+    for a (k,) input, so the gather runs flat (found by the two-rank bench rehearsal on one GPU)."""
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rows_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    exp = [[w + 100 * r for w in range(16)] for r in range(world)]
+    for _, shape, rows in out:
+        assert shape == [world, 16] and rows == exp

@@ -416,3 +416,36 @@ def test_sharded_poly_eval_virtual_ranks(hal, n, world):
     exp = poly.evaluate_batch([coeffs], z, "fp")[0]
     assert np.array_equal(got, exp)
     assert unfe(exp, m) == [P.horner(unfe(coeffs, m), unfe(z, m)[0], m)]
+
+
+@pytest.mark.parametrize("world", [2, 5])
+def test_torch_reduce_lr_device_sum(hal, corc, world):
+    """dist.torch_reduce_lr (the distributed opening's per-round L/R reduction in bench.py --gpus N):
+    every rank's (L_r, R_r) gathered as 16-word rows, then the L column and the R column summed on
+    the device by halo_point_sum_dev == the oracle's point sums.  The collective is a stub that plays
+    the other ranks' rows (gloo / RCCL gather semantics: one flat tensor of world x 16 words)."""
+    import torch
+
+    from halo_amd.dist import torch_reduce_lr
+    c = P.PALLAS
+    g = corc.srs_generate("pallas", 2 * world)
+    rows = [np.concatenate([g[2 * r], g[2 * r + 1]]).astype(np.uint64) for r in range(world)]
+
+    class StubDist:
+        def get_world_size(self):
+            return world
+
+        def get_backend(self):
+            return "gloo"
+
+        def all_gather_into_tensor(self, out, t):
+            assert out.shape == (world * 16,) and t.shape == (16,)
+            for r in range(world):
+                out[16 * r:16 * (r + 1)] = t if r == 0 else torch.from_numpy(rows[r].view(np.int64))
+
+    L, R = torch_reduce_lr(StubDist(), "pallas", "cuda")([(rows[0][:8], rows[0][8:])])
+    expL = expR = None
+    for r in range(world):
+        expL = P.add(c, expL, P.wrapped_to_point(c, [int(x) for x in rows[r][:8]]))
+        expR = P.add(c, expR, P.wrapped_to_point(c, [int(x) for x in rows[r][8:]]))
+    assert L.tolist() == P.point_to_wrapped(c, expL) and R.tolist() == P.point_to_wrapped(c, expR)
