@@ -1,11 +1,11 @@
-# SQ counters of the NTT pass kernels at 2^22 (tools/ntt_time.py 22: 2 x 11-bit passes per transform),
+# SQ counters of the NTT pass kernels at 2^${1:-22} (tools/ntt_time.py: 11-bit passes up to 2^22, 8-bit above),
 # run through gpurun from the repo root; per kernel: lane-instructions per element per pass, the VALU
 # issue rate, the LDS-instruction share and the share of wave cycles waiting on LDS / anything.
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 O=gpurun_out/pmc_ntt; rm -rf $O; mkdir -p $O
-timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAVES SQ_LDS_IDX_ACTIVE SQ_WAVE_CYCLES SQ_INSTS_SALU SQ_WAIT_INST_LDS --output-format csv -d $O/a -o run -- python3 tools/ntt_time.py 22 > $O/a.log 2>&1 || exit 1
-timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_INSTS_VMEM --output-format csv -d $O/b -o run -- python3 tools/ntt_time.py 22 > $O/b.log 2>&1 || exit 1
-python3 - $O <<'PY'
+timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAVES SQ_LDS_IDX_ACTIVE SQ_WAVE_CYCLES SQ_INSTS_SALU SQ_WAIT_INST_LDS --output-format csv -d $O/a -o run -- python3 tools/ntt_time.py ${1:-22} > $O/a.log 2>&1 || exit 1
+timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_INSTS_VMEM --output-format csv -d $O/b -o run -- python3 tools/ntt_time.py ${1:-22} > $O/b.log 2>&1 || exit 1
+python3 - $O ${1:-22} <<'PY'
 import csv, glob, sys, collections
 O = sys.argv[1]
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
@@ -17,7 +17,7 @@ for sub in ('a', 'b'):
         agg[k][r['Counter_Name']].append(float(r['Counter_Value']))
 for k, d in agg.items():
     c = {n: sum(v) / len(v) for n, v in d.items()}
-    elems = 1 << 22  # per pass (one transform)
+    elems = 1 << int(sys.argv[2])  # per pass (one transform)
     cyc = c['GRBM_GUI_ACTIVE'] / 8
     print(k)
     print(f"  VALU lane-instructions per element per pass: {c['SQ_INSTS_VALU'] * 64 / elems:.0f}")
