@@ -2358,21 +2358,24 @@ extern "C" int halo_ipa_round_lr_multi(halo_ipa_session* const* ses, size_t k, h
 
 extern "C" int halo_ipa_fold(halo_ipa_session* ses, const halo_fe_t* xi, const halo_fe_t* xi_inv) {
     clear_error();
-    if (!ses || !xi || !xi_inv) return set_error(HALO_EINVAL, "halo_ipa_fold: null argument");
+    if (!ses || !xi) return set_error(HALO_EINVAL, "halo_ipa_fold: null argument");
     return halo_ipa_fold_multi(&ses, 1, xi, xi_inv);
 }
 
 extern "C" int halo_ipa_fold_multi(halo_ipa_session* const* ses, size_t k, const halo_fe_t* xi,
                                    const halo_fe_t* xi_inv) {
     clear_error();
-    if (!ses || !xi || !xi_inv) return set_error(HALO_EINVAL, "halo_ipa_fold_multi: null argument");
+    if (!ses || !xi) return set_error(HALO_EINVAL, "halo_ipa_fold_multi: null argument");
     DeviceState* st = current_state();
     if (!st) return HALO_EDEVICE;
     std::lock_guard<std::mutex> g(st->mu);
     for (size_t i = 0; i < k; i++) {
         if (!ses[i]) return set_error(HALO_EINVAL, "halo_ipa_fold_multi: null session %zu", i);
         if (!ipa_is_open(ses[i])) return set_error(HALO_EINVAL, "halo_ipa_fold_multi: session %zu is not open", i);
-        HALO_CHECK(ipa_fold_launch(st, ses[i], &xi[i], &xi_inv[i]));
+        halo_fe_t inv;  // xi_inv == NULL: xi^-1 formed here, as the reference's fold does (pcdl.rs:430)
+        if (!xi_inv && !host_scalar_inverse(ses[i]->curve, &xi[i], &inv))
+            return set_error(HALO_EINVAL, "halo_ipa_fold_multi: xi %zu is zero (no inverse)", i);
+        HALO_CHECK(ipa_fold_launch(st, ses[i], &xi[i], xi_inv ? &xi_inv[i] : &inv));
     }
     // no host wait: the fold is stream-ordered before the next round (which synchronises), so the host
     // goes on to the transcript and the next round's launches while it runs

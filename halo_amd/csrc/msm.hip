@@ -1488,6 +1488,23 @@ void host_xyzz_to_wrapped2(int curve, const void* const* xyzz, void* const* wrap
         host_xyzz_to_wrapped2_t<VestaCurve::Base>(xyzz, wrapped, k);
 }
 
+template <class S>
+static bool host_scalar_inverse_t(const void* x_ark, void* out_ark) {
+    static const HostMont M(S::MODULUS64);
+    uint64_t x[4];
+    for (int i = 0; i < 4; i++) x[i] = ((const uint64_t*)x_ark)[i];
+    if (M.geq_p(x)) M.sub_p(x);
+    if (!(x[0] | x[1] | x[2] | x[3])) return false;
+    uint64_t r[4];
+    M.inv(x, r);  // Montgomery-domain inverse: (x R)^-1 R^2 = x^-1 R, the ark form of x^-1
+    for (int i = 0; i < 4; i++) ((uint64_t*)out_ark)[i] = r[i];
+    return true;
+}
+bool host_scalar_inverse(int curve, const void* x_ark, void* out_ark) {
+    return curve == HALO_PALLAS ? host_scalar_inverse_t<PallasCurve::Scalar>(x_ark, out_ark)
+                                : host_scalar_inverse_t<VestaCurve::Scalar>(x_ark, out_ark);
+}
+
 void host_xyzz_to_wrapped(int curve, const void* xyzz, void* wrapped) {
     if (curve == HALO_PALLAS)
         host_xyzz_to_wrapped_t<PallasCurve::Base>(xyzz, wrapped);

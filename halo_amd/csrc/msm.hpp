@@ -101,6 +101,9 @@ int xyzz_add_wrapped_device(int curve, void* xyzz, const void* wrapped, hipStrea
 // Host conversion of a 128-B packed XYZZ point (internal format, each coordinate < 2p) to an ark
 // WrappedPoint: one inversion in 4 x 64-bit Montgomery arithmetic on the CPU (identity -> (0, 0)).
 void host_xyzz_to_wrapped(int curve, const void* xyzz, void* wrapped);
+// x^-1 of an ark (Montgomery) scalar of the curve's scalar field, on the host (binary extended Euclid);
+// false for x = 0
+bool host_scalar_inverse(int curve, const void* x_ark, void* out_ark);
 // k <= 16 points at once with one inversion (Montgomery's trick)
 void host_xyzz_to_wrapped2(int curve, const void* const* xyzz, void* const* wrapped, int k);
 int convert_wrapped_to_internal(int curve, const void* in, void* out, size_t n, hipStream_t s);

@@ -67,7 +67,7 @@ struct SrsState {
         DevBuf t;
     };
     std::vector<std::unique_ptr<HTable>> h_tables;
-    // d 2^(4 w) G_k (k < small_n0, w < 32, d < 16), XYZZ: small SRS MSMs, IPA tails (ipa.hip); shared
+    // d 2^(4 w) G_k (k < small_n0, w < 32, 1 <= d <= 8), XYZZ: small SRS MSMs, IPA tails (ipa.hip); shared
     // with the open IPA sessions that read it, so a rebuild never overwrites a buffer in use
     std::shared_ptr<DevBuf> small_tab;
     size_t small_n0 = 0;             // 0 = not built for the current SRS

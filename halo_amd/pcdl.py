@@ -84,8 +84,10 @@ class IpaSession:
         H.check(H.load().halo_ipa_round_lr(self._s, H.ptr(L), H.ptr(R)))
         return L, R
 
-    def fold(self, xi, xi_inv):
-        H.check(H.load().halo_ipa_fold(self._s, H.ptr(H.fe_array(xi, 1)), H.ptr(H.fe_array(xi_inv, 1))))
+    def fold(self, xi, xi_inv=None):
+        """xi_inv None: the library forms xi^-1 itself (halo_ipa_fold with a NULL xi_inv)."""
+        H.check(H.load().halo_ipa_fold(self._s, H.ptr(H.fe_array(xi, 1)),
+                                       None if xi_inv is None else H.ptr(H.fe_array(xi_inv, 1))))
 
     def state(self, with_gs: bool = True):
         """(m, gs, cs, zs): the folded vectors (length 2m).  Sessions over the resident SRS do not
@@ -197,7 +199,7 @@ def open_without_eval(p, C, d: int, z, v, w=None, transcript=None, q=None, w_bar
             transcript.absorb_fr([xi])
             transcript.absorb_g([Lp, Rp])
             xi = np.ascontiguousarray(transcript.challenge(), dtype=np.uint64)
-            ses.fold(xi, _ark_inverse(xi, cid))
+            ses.fold(xi)  # xi^-1 formed by the library (pcdl.rs:430)
         U, c = ses.end()
     finally:
         if ses._s is not None:  # an assertion or error above: return the session to the pool

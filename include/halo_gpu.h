@@ -357,11 +357,12 @@ int halo_pcdl_open_start(halo_ipa_session* s, const halo_wrapped_point_t* H, con
 /* L = <c_r, G_l> + H' <c_r, z_l>,  R = <c_l, G_r> + H' <c_l, z_r>  (pcdl.rs:412-418) */
 int halo_ipa_round_lr(halo_ipa_session* s, halo_wrapped_point_t* L, halo_wrapped_point_t* R);
 /* G_l[j] = G_l[j] + xi G_r[j] (affine), c_l[j] += xi^-1 c_r[j], z_l[j] += xi z_r[j]; m /= 2
- * (pcdl.rs:427-437). */
+ * (pcdl.rs:427-437).  xi_inv may be NULL: the library forms xi^-1 on the host (binary extended
+ * Euclid), as the reference's fold does itself; xi = 0 is HALO_EINVAL. */
 int halo_ipa_fold(halo_ipa_session* s, const halo_fe_t* xi, const halo_fe_t* xi_inv);
 /* k independent openings advanced in lockstep (each session has its own stream; all k rounds /
  * folds are enqueued before any is waited for, so the openings overlap on the device): L[i], R[i]
- * of session i; xi[i], xi_inv[i] for session i. */
+ * of session i; xi[i], xi_inv[i] for session i (xi_inv NULL: formed on the host). */
 int halo_ipa_round_lr_multi(halo_ipa_session* const* ses, size_t k, halo_wrapped_point_t* L,
                             halo_wrapped_point_t* R);
 int halo_ipa_fold_multi(halo_ipa_session* const* ses, size_t k, const halo_fe_t* xi, const halo_fe_t* xi_inv);

@@ -449,3 +449,31 @@ def test_torch_reduce_lr_device_sum(hal, corc, world):
         expL = P.add(c, expL, P.wrapped_to_point(c, [int(x) for x in rows[r][:8]]))
         expR = P.add(c, expR, P.wrapped_to_point(c, [int(x) for x in rows[r][8:]]))
     assert L.tolist() == P.point_to_wrapped(c, expL) and R.tolist() == P.point_to_wrapped(c, expR)
+
+
+@pytest.mark.parametrize("cname,cid", CURVES)
+def test_ipa_fold_forms_xi_inverse(hal, corc, cname, cid):
+    """halo_ipa_fold with xi_inv = NULL forms xi^-1 on the host (pcdl.rs:430): the same opening as
+    with the caller's inverse, and xi = 0 is refused (HALO_EINVAL)."""
+    c = P.CURVES[cname]
+    r = c.scalar
+    n = 64
+    g = corc.srs_generate(cname, n)
+    group.PublicParams.upload(cname, g, precompute_windows=False)
+    rng = random.Random(7)
+    cs = fe([rng.randrange(r) for _ in range(n)], r)
+    z = fe([rng.randrange(r)], r)
+    Hp = np.array(P.point_to_wrapped(c, P.mul_fast(c, 5, c.generator)), dtype=np.uint64)
+    challenge, inverse = transcript(cname)
+    exp = pcdl.ipa_rounds(cs, z, Hp, challenge, inverse, cname)
+    challenge, _ = transcript(cname)
+    got = pcdl.ipa_rounds(cs, z, Hp, challenge, lambda x: None, cname)
+    for a, b in zip(exp, got):
+        assert np.array_equal(np.asarray(a, dtype=np.uint64), np.asarray(b, dtype=np.uint64))
+    ses = pcdl.IpaSession.from_vectors(g[:n], cs, fe(P.construct_powers(P.from_mont(P.limbs_to_int(z[0]), r), n, r), r),
+                                       Hp, cname)
+    ses.round_lr()
+    with pytest.raises(hal.HaloError):
+        ses.fold(np.zeros(4, dtype=np.uint64))
+    s, ses._s = ses._s, None  # release without the remaining rounds
+    hal.check(hal.load().halo_ipa_end(s, None, None))
