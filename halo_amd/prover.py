@@ -693,8 +693,8 @@ class DeviceBackend:
             self.H.check(self.L.halo_ipa_round_lr_multi(sess, k, self.H.ptr(Lb), self.H.ptr(Rb)))
             xs = [ch() for ch in chals]
             xa = np.ascontiguousarray(np.stack([self.fe(x) for x in xs]))
-            xia = np.ascontiguousarray(np.stack([self.fe(pow(x, -1, self.m)) for x in xs]))
-            self.H.check(self.L.halo_ipa_fold_multi(sess, k, self.H.ptr(xa), self.H.ptr(xia)))
+            # xi^-1 formed by the library (halo_ipa_fold_multi with a NULL xi_inv, pcdl.rs:430)
+            self.H.check(self.L.halo_ipa_fold_multi(sess, k, self.H.ptr(xa), None))
             for i in range(k):
                 Ls[i].append(Lb[i].copy())
                 Rs[i].append(Rb[i].copy())
