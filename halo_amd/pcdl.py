@@ -78,16 +78,29 @@ class IpaSession:
         self._s = s
         return self
 
+    def _stage(self):
+        """Per-session staging arrays with their addresses taken once: a round's ctypes call then
+        passes plain integers (numpy's per-call ctypes pointer objects cost a few us each, on a
+        ~100 us round of the small openings)."""
+        st = getattr(self, "_st", None)
+        if st is None:
+            lr, xi = np.zeros((2, 8), dtype=np.uint64), np.zeros(4, dtype=np.uint64)
+            st = self._st = (lr, lr.ctypes.data, lr.ctypes.data + 64, xi, xi.ctypes.data, H.load())
+        return st
+
     def round_lr(self):
-        L = np.zeros(8, dtype=np.uint64)
-        R = np.zeros(8, dtype=np.uint64)
-        H.check(H.load().halo_ipa_round_lr(self._s, H.ptr(L), H.ptr(R)))
-        return L, R
+        lr, pl, pr, _, _, lib = self._stage()
+        H.check(lib.halo_ipa_round_lr(self._s, pl, pr))
+        return lr[0].copy(), lr[1].copy()
 
     def fold(self, xi, xi_inv=None):
         """xi_inv None: the library forms xi^-1 itself (halo_ipa_fold with a NULL xi_inv)."""
-        H.check(H.load().halo_ipa_fold(self._s, H.ptr(H.fe_array(xi, 1)),
-                                       None if xi_inv is None else H.ptr(H.fe_array(xi_inv, 1))))
+        _, _, _, xb, px, lib = self._stage()
+        if xi_inv is not None:
+            H.check(lib.halo_ipa_fold(self._s, H.ptr(H.fe_array(xi, 1)), H.ptr(H.fe_array(xi_inv, 1))))
+            return
+        np.copyto(xb, np.asarray(xi, dtype=np.uint64).reshape(4))
+        H.check(lib.halo_ipa_fold(self._s, px, None))
 
     def state(self, with_gs: bool = True):
         """(m, gs, cs, zs): the folded vectors (length 2m).  Sessions over the resident SRS do not
