@@ -481,6 +481,7 @@ struct TailFoldArgs {
     uint4 *cs_out, *zs_out, *w_out;
     size_t wlen_in;  // fold weights before the fold
     int active;
+    uint4* w_one;  // the first tail round: w = [1] (not yet in memory): use 1, and store it here
 };
 
 // The hiding term dot * P' of one side as lane terms: lane t < 256 returns the table entry for bit t
@@ -540,7 +541,9 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail_msm(const uint4* table, s
                                                             const uint8_t* side, size_t n0, size_t m, int mode, uint32_t nbs,
                                                             uint4* part, const uint4* htab, const uint4* dots_ark,
                                                             const uint32_t* hkw, uint4* out_xyzz,
-                                                            uint32_t* host = nullptr, uint32_t seq = 0) {
+                                                            uint32_t* host = nullptr, uint32_t seq = 0,
+                                                            const uint4* plus_wrapped = nullptr,
+                                                            const uint4* copy_src = nullptr, uint4* copy_dst = nullptr) {
     using F = typename Cv::Base;
     __shared__ uint4 red[TAIL_THREADS / 2 * 8];
     __shared__ uint32_t kw[10];
@@ -581,7 +584,12 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail_msm(const uint4* table, s
     acc = block_group_sum<F>(acc, TAIL_THREADS, red);
     if (out_xyzz && nbs == 1) {
         if (tid == 0) {
+            if (plus_wrapped) acc = xyzz_madd(acc, aff_from_wrapped<F>(plus_wrapped));
             xyzz_store(out_xyzz + 8 * bsd, acc);
+            if (copy_src) {  // 32 B beside the result, so that one D2H copy takes both
+                copy_dst[0] = copy_src[0];
+                copy_dst[1] = copy_src[1];
+            }
             if (host) tail_emit_host(host, host + 64, bsd, acc, seq);
         }
     } else if (tid == 0) {
@@ -766,7 +774,8 @@ __global__ __launch_bounds__(256) void k_tail_digits(const uint4* cs, const uint
         if (u & 1) wu = fe_mul(wu, fe_from_ark<S>(f.xi));
     } else {
         c = fe_from_ark<S>(cs + 2 * ci);
-        wu = fe_from_ark<S>(w + 2 * u);
+        wu = f.w_one ? fe_one<S>() : fe_from_ark<S>(w + 2 * u);
+        if (f.w_one && k == 0) fe_to_ark(f.w_one, wu);
     }
     tail_scalar_val<Cv>(fe_mul(c, wu), (j < m) ? 0 : 1, k, scal, side);
 }
@@ -793,7 +802,8 @@ __global__ __launch_bounds__(TAIL_THREADS, 1) void k_tail_round(const TailRoundA
                 if (u & 1) wu = fe_mul(wu, fe_from_ark<S>(f.xi));
             } else {
                 c = fe_from_ark<S>(a.cs + 2 * ci);
-                wu = fe_from_ark<S>(a.w + 2 * u);
+                wu = f.w_one ? fe_one<S>() : fe_from_ark<S>(a.w + 2 * u);
+                if (f.w_one && k == 0 && (tid & 63) == 0) fe_to_ark(f.w_one, wu);
             }
             Fe<S> one_raw = fe_zero<S>();  // internal (x 2^261) -> canonical: Montgomery product with 1
             one_raw.v[0] = 1;
@@ -842,7 +852,8 @@ template <class Cv>
 __global__ __launch_bounds__(TAIL_THREADS) void k_tail_final(const uint4* part, int nblk, const uint4* htab,
                                                               const uint4* dots_ark, uint4* out_wrapped,
                                                               int xyzz_out, uint32_t* host = nullptr,
-                                                              uint32_t seq = 0) {
+                                                              uint32_t seq = 0, const uint4* plus_wrapped = nullptr,
+                                                              const uint4* copy_src = nullptr, uint4* copy_dst = nullptr) {
     using F = typename Cv::Base;
     using S = typename Cv::Scalar;
     __shared__ uint4 red[TAIL_THREADS / 2 * 8];
@@ -877,6 +888,11 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail_final(const uint4* part, 
         acc = xyzz_add(acc, xyzz_load<F>(part + 8 * (2 * (size_t)(b * per_side + j) + b)));
     acc = block_group_sum<F>(acc, TAIL_THREADS, red);
     if (tid == 0) {
+        if (plus_wrapped) acc = xyzz_madd(acc, aff_from_wrapped<F>(plus_wrapped));  // (the combine's + C)
+        if (copy_src) {  // 32 B beside the result, so that one D2H copy takes both
+            copy_dst[0] = copy_src[0];
+            copy_dst[1] = copy_src[1];
+        }
         if (xyzz_out) {  // 128 B per side, converted on the host (host_xyzz_to_wrapped)
             xyzz_store(out_wrapped + 8 * b, acc);
             if (host) tail_emit_host(host, host + 64, b, acc, seq);
@@ -1073,6 +1089,7 @@ struct halo_ipa_session {
     std::shared_ptr<DevBuf> table_ref;  // keeps the SRS's table alive while the session reads it
     bool fold_inflight = false;       // a fold's H2D copy of xi may still read `pinned`
     bool fold_pending = false;        // tail rounds: the last fold is applied by the next launch (k_tail_prep)
+    bool w_one_pending = false;       // entered the tail rounds: w = [1] is written by the next tail launch
     halo_fe_t pend_xi{}, pend_xinv{};
     size_t pend_m = 0;                // the half-length m the pending fold folds (before its m /= 2)
     bool htab_waited = false;         // round 1 waited for it (later rounds follow a host sync of round 1)
@@ -1093,7 +1110,7 @@ struct halo_ipa_session {
         wcur = 0;
         table = nullptr;
         table_ld = 0;
-        fold_inflight = htab_waited = xi_mode = fold_pending = slots_reset = false;
+        fold_inflight = htab_waited = xi_mode = fold_pending = slots_reset = w_one_pending = false;
         htab_ptr = nullptr;
         started = blinded = combined = false;
     }
@@ -1695,6 +1712,99 @@ static int ipa_eval_cs(halo_ipa_session* ses, size_t len, halo_fe_t* v_out) {
 //   (transcript: absorb C', z, v; xi_0 = challenge)
 //   halo_pcdl_open_start(H, xi_0)           H' = xi_0 H; then halo_ipa_round_lr / fold / end
 // ---------------------------------------------------------------------------------------------
+// scratch of a small SRS MSM over n points: GLV words (n x 32 B) | sides (n B, 256-B aligned) | partials;
+// stream s waits for the previous small MSM (done with the scratch) and for the SRS multiples table
+static int small_msm_scratch(DeviceState* st, int curve, size_t n, hipStream_t s, char** scr, size_t* o_side,
+                             size_t* o_part, size_t* nblk) {
+    SrsState& srs = st->srs[curve];
+    const size_t nmax = std::min(srs_small_max(), srs.n);
+    if (n < 1 || n > nmax) return set_error(HALO_EINVAL, "small SRS MSM: n (%zu) outside [1, %zu]", n, nmax);
+    *nblk = (TAIL_WIN * n + TAIL_THREADS - 1) / TAIL_THREADS;
+    *o_side = n * 32;
+    *o_part = *o_side + ((n + 255) & ~(size_t)255);
+    if (srs.small_ev) HALO_HIP(hipStreamWaitEvent(s, srs.small_ev, 0));  // the previous small MSM is done with small_scr
+    else HALO_HIP(hipEventCreateWithFlags(&srs.small_ev, hipEventDisableTiming));
+    HALO_CHECK(srs.small_scr.reserve(*o_part + *nblk * 256));
+    HALO_CHECK(srs_small_table(st, curve, s));
+    *scr = (char*)srs.small_scr.ptr;
+    return HALO_OK;
+}
+
+// The small MSM after its scalars' GLV words are in the scratch (small_msm_scratch): the table sums with
+// the hiding term w S in block 0 (2^i S table), an XYZZ result from the one block or k_tail_final, plus an
+// optional point added at the end and a 32-B side copy (copy_src -> copy_dst) beside it.
+static int small_msm_sums(DeviceState* st, int curve, char* scr, size_t o_side, size_t o_part, size_t nblk, size_t n,
+                          const void* hide_scalar, void* d_out, hipStream_t s, bool out_xyzz, const void* plus_wrapped,
+                          const void* copy_src, void* copy_dst) {
+    SrsState& srs = st->srs[curve];
+    DISPATCH_CURVE(curve, Cv, {
+        const bool direct = out_xyzz && nblk == 1;
+        hipLaunchKernelGGL(k_tail_msm<Cv>, dim3((unsigned)nblk), dim3(TAIL_THREADS), 0, s,
+                           srs.small_tab->as<const uint4>(), srs.small_n0, (const uint32_t*)scr,
+                           (const uint8_t*)(scr + o_side), n, (size_t)0, 1, (uint32_t)nblk, (uint4*)(scr + o_part),
+                           hide_scalar ? srs.s_table.as<const uint4>() : (const uint4*)nullptr, (const uint4*)hide_scalar,
+                           (const uint32_t*)nullptr, direct ? (uint4*)d_out : (uint4*)nullptr, (uint32_t*)nullptr, 0u,
+                           (const uint4*)plus_wrapped, (const uint4*)copy_src, (uint4*)copy_dst);
+        if (!direct)
+            hipLaunchKernelGGL(k_tail_final<Cv>, dim3(1), dim3(TAIL_THREADS), 0, s, (const uint4*)(scr + o_part),
+                               (int)nblk, (const uint4*)nullptr, (const uint4*)nullptr, (uint4*)d_out, (int)out_xyzz,
+                               (uint32_t*)nullptr, 0u, (const uint4*)plus_wrapped, (const uint4*)copy_src,
+                               (uint4*)copy_dst);
+    });
+    HALO_HIP(hipGetLastError());
+    HALO_HIP(hipEventRecord(srs.small_ev, s));
+    return HALO_OK;
+}
+
+// The hiding combine's scalars for a small SRS MSM in one launch (was k_put_args + k_combine_scalars +
+// k_tail_scalars): p' = p + alpha p_bar in place, p_bar <- alpha p_bar, the MSM scalars alpha p_bar as
+// GLV words and sides in the small MSM's scratch, w' = w + alpha w_bar and -w, and C (by value) to its
+// staging slot for the final's + C.  alpha, w, C by value (no host-to-device copy).
+struct CombineSmallArgs {
+    uint4 alpha[2], w[2], C[4];  // ark / WrappedPoint words
+};
+template <class Cv>
+__global__ __launch_bounds__(256) void k_combine_small(const CombineSmallArgs a, uint4* p, uint4* pb, size_t n,
+                                                       const uint4* w_bar, uint4* w_prime, uint4* negw, uint4* C_out,
+                                                       uint32_t* scal, uint8_t* side) {
+    using S = typename Cv::Scalar;
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const Fe<S> al = fe_from_ark<S>(a.alpha);
+    if (i < n) {
+        const Fe<S> t = fe_mul(al, fe_from_ark<S>(pb + 2 * i));
+        fe_to_ark(p + 2 * i, fe_add(fe_from_ark<S>(p + 2 * i), t));
+        fe_to_ark(pb + 2 * i, t);
+        tail_scalar_val<Cv>(t, 0, i, scal, side);
+    }
+    if (i == 0) {
+        const Fe<S> wv = fe_from_ark<S>(a.w);
+        fe_to_ark(w_prime, fe_add(wv, fe_mul(al, fe_from_ark<S>(w_bar))));
+        fe_to_ark(negw, fe_neg(wv));
+#pragma unroll
+        for (int k = 0; k < 4; k++) C_out[k] = a.C[k];
+    }
+}
+
+// The hiding blind's scalars for a small SRS MSM in one launch (was an H2D copy of w_bar + k_pbar +
+// k_tail_scalars): p_bar = (X - z) q (d + 1 coefficients, pcdl.rs:344-347) to p_bar_out and as GLV words
+// and sides in the small MSM's scratch, and w_bar (by value) to its staging slot (the MSM's hiding scalar).
+template <class Cv>
+__global__ __launch_bounds__(256) void k_pbar_small(const uint4* q, size_t d, const uint4* z, const ArkScalarPair wb,
+                                                    uint4* w_bar_out, uint4* p_bar_out, uint32_t* scal, uint8_t* side) {
+    using S = typename Cv::Scalar;
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) {
+        w_bar_out[0] = wb.v[0];
+        w_bar_out[1] = wb.v[1];
+    }
+    if (i > d) return;
+    const Fe<S> a = i >= 1 ? fe_from_ark<S>(q + 2 * (i - 1)) : fe_zero<S>();
+    const Fe<S> b = i < d ? fe_from_ark<S>(q + 2 * i) : fe_zero<S>();
+    const Fe<S> t = fe_sub(a, fe_mul(fe_from_ark<S>(z), b));
+    fe_to_ark(p_bar_out + 2 * i, t);
+    tail_scalar_val<Cv>(t, 0, i, scal, side);
+}
+
 // Up to COMBINE_MSM_MAX coefficients halo_pcdl_open_combine forms C' through an MSM of alpha p_bar (see there)
 constexpr size_t COMBINE_MSM_MAX = (size_t)1 << 16;
 
@@ -1744,11 +1854,27 @@ extern "C" int halo_pcdl_open_blind(halo_ipa_session* ses, const halo_fe_t* q, c
     HALO_CHECK(ses->pbar.reserve(n * 32));
     HALO_CHECK(ses->tmp.reserve(std::max<size_t>(4096 * 32, d * 32)));
     HALO_CHECK(copy_h2d(ses->tmp.ptr, q, d * 32, s));
-    HALO_CHECK(copy_h2d(sm + SM_WBAR, w_bar, 32, s));
-    HALO_CHECK(pcdl_pbar_device(ses->curve, ses->tmp.ptr, d, sm, ses->pbar.ptr, s));  // z at sm[0, 32)
     // C_bar as packed XYZZ, converted on the host: the MSM's last lane no longer runs an inversion (~0.1 ms
     // of dependent multiplications at the end of the blind)
-    HALO_CHECK(msm_srs_device(st, ses->curve, ses->pbar.ptr, n, sm + SM_WBAR, sm + SM_T, s, false, true));
+    if (n <= std::min(srs_small_max(), srs.n)) {  // p_bar, its GLV words and w_bar in one launch (k_pbar_small)
+        char* scr;
+        size_t o_side, o_part, nblk;
+        HALO_CHECK(small_msm_scratch(st, ses->curve, n, s, &scr, &o_side, &o_part, &nblk));
+        ArkScalarPair wb;
+        memcpy(&wb.v[0], w_bar, 32);
+        DISPATCH_CURVE(ses->curve, Cv, {
+            hipLaunchKernelGGL(k_pbar_small<Cv>, dim3(gridn(n, 256)), dim3(256), 0, s, ses->tmp.as<const uint4>(), d,
+                               (const uint4*)sm, wb, (uint4*)(sm + SM_WBAR), ses->pbar.as<uint4>(), (uint32_t*)scr,
+                               (uint8_t*)(scr + o_side));  // z at sm[0, 32)
+        });
+        HALO_HIP(hipGetLastError());
+        HALO_CHECK(small_msm_sums(st, ses->curve, scr, o_side, o_part, nblk, n, sm + SM_WBAR, sm + SM_T, s, true, nullptr,
+                                  nullptr, nullptr));
+    } else {
+        HALO_CHECK(copy_h2d(sm + SM_WBAR, w_bar, 32, s));
+        HALO_CHECK(pcdl_pbar_device(ses->curve, ses->tmp.ptr, d, sm, ses->pbar.ptr, s));  // z at sm[0, 32)
+        HALO_CHECK(msm_srs_device(st, ses->curve, ses->pbar.ptr, n, sm + SM_WBAR, sm + SM_T, s, false, true));
+    }
     HALO_HIP(hipMemcpyAsync(ses->pinned + 128, sm + SM_T, 128, hipMemcpyDeviceToHost, s));
     HALO_HIP(hipStreamSynchronize(s));
     host_xyzz_to_wrapped(ses->curve, ses->pinned + 128, C_bar);
@@ -1772,7 +1898,8 @@ extern "C" int halo_pcdl_open_combine(halo_ipa_session* ses, const halo_fe_t* al
     std::lock_guard<std::mutex> g(st->mu);
     hipStream_t s = ses->s;
     char* sm = ses->small.as<char>();
-    {  // alpha, w, C and S (internal) in one launch
+    const bool small = ses->n <= std::min(srs_small_max(), st->srs[ses->curve].n);  // (k_combine_small takes them by value)
+    if (!small) {  // alpha, w, C and S (internal) in one launch
         PutArgs a{};
         const void* src[4] = {alpha, w, C, st->srs[ses->curve].S};
         const size_t off[4] = {SM_ALPHA, SM_W, SM_C, SM_S};
@@ -1792,11 +1919,37 @@ extern "C" int halo_pcdl_open_combine(halo_ipa_session* ses, const halo_fe_t* al
     // since C_bar = MSM(G, p_bar) + w_bar S): an MSM (the table path, or the bucket pipeline) instead of
     // the lone-lane scalar multiplications of k_hiding_point (~1.3 ms of dependent curve operations).
     if (ses->n <= COMBINE_MSM_MAX) {
-        HALO_CHECK(pcdl_combine_scalars_device(ses->curve, ses->cs.ptr, ses->pbar.ptr, ses->n, sm + SM_ALPHA, sm + SM_W,
-                                               sm + SM_WBAR, sm + SM_WP, sm + SM_NEGW, s));
         // the MSM as packed XYZZ (no inversion on the device), + C, converted on the host below
-        HALO_CHECK(msm_srs_device(st, ses->curve, ses->pbar.ptr, ses->n, sm + SM_NEGW, sm + SM_T, s, false, true));
-        HALO_CHECK(xyzz_add_wrapped_device(ses->curve, sm + SM_T, sm + SM_C, s, false));
+        if (small) {
+            // one launch for every scalar (k_combine_small), then the small MSM whose final block adds C and
+            // puts w' beside the sum: one device-to-host copy of both
+            char* scr;
+            size_t o_side, o_part, nblk;
+            HALO_CHECK(small_msm_scratch(st, ses->curve, ses->n, s, &scr, &o_side, &o_part, &nblk));
+            CombineSmallArgs a;
+            memcpy(a.alpha, alpha, 32);
+            memcpy(a.w, w, 32);
+            memcpy(a.C, C, 64);
+            DISPATCH_CURVE(ses->curve, Cv, {
+                hipLaunchKernelGGL(k_combine_small<Cv>, dim3(gridn(ses->n, 256)), dim3(256), 0, s, a, ses->cs.as<uint4>(),
+                                   ses->pbar.as<uint4>(), ses->n, (const uint4*)(sm + SM_WBAR), (uint4*)(sm + SM_WP),
+                                   (uint4*)(sm + SM_NEGW), (uint4*)(sm + SM_C), (uint32_t*)scr, (uint8_t*)(scr + o_side));
+            });
+            HALO_HIP(hipGetLastError());
+            HALO_CHECK(small_msm_sums(st, ses->curve, scr, o_side, o_part, nblk, ses->n, sm + SM_NEGW, sm + SM_T, s, true,
+                                      sm + SM_C, sm + SM_WP, sm + SM_T + 128));
+            HALO_HIP(hipMemcpyAsync(ses->pinned + 128, sm + SM_T, 160, hipMemcpyDeviceToHost, s));
+            HALO_HIP(hipStreamSynchronize(s));
+            memcpy(w_prime, ses->pinned + 256, 32);
+            host_xyzz_to_wrapped(ses->curve, ses->pinned + 128, C_prime);
+            ses->combined = true;
+            return HALO_OK;
+        } else {
+            HALO_CHECK(pcdl_combine_scalars_device(ses->curve, ses->cs.ptr, ses->pbar.ptr, ses->n, sm + SM_ALPHA,
+                                                   sm + SM_W, sm + SM_WBAR, sm + SM_WP, sm + SM_NEGW, s));
+            HALO_CHECK(msm_srs_device(st, ses->curve, ses->pbar.ptr, ses->n, sm + SM_NEGW, sm + SM_T, s, false, true));
+            HALO_CHECK(xyzz_add_wrapped_device(ses->curve, sm + SM_T, sm + SM_C, s, false));
+        }
         HALO_HIP(hipMemcpyAsync(ses->pinned, sm + SM_WP, 32, hipMemcpyDeviceToHost, s));
         HALO_HIP(hipMemcpyAsync(ses->pinned + 128, sm + SM_T, 128, hipMemcpyDeviceToHost, s));
         HALO_HIP(hipStreamSynchronize(s));
@@ -1867,10 +2020,8 @@ static int ipa_enter_tail(DeviceState* st, halo_ipa_session* ses, hipStream_t s)
         ses->table = ses->own_table.as<const uint4>();
         ses->table_ld = n0;
     }
-    DISPATCH_CURVE(ses->curve, Cv, {
-        hipLaunchKernelGGL(k_set_one_ark<typename Cv::Scalar>, dim3(1), dim3(64), 0, s, ses->w[0].as<uint4>());
-    });
-    HALO_HIP(hipGetLastError());
+    // w = [1]: the next round's first launch uses 1 and stores it (TailFoldArgs::w_one), no launch here
+    ses->w_one_pending = true;
     ses->n0 = n0;
     ses->wlen = 1;
     ses->wcur = 0;
@@ -1882,12 +2033,17 @@ static int ipa_enter_tail(DeviceState* st, halo_ipa_session* ses, hipStream_t s)
 // scalars and dots come from k_tail_prep (one launch), the hiding terms ride in each side's first
 // k_tail_msm block, and k_tail_final runs only when a side spans several blocks.
 // mode 1: U = sum_u w[u] G0[u] -> small[256..384) as XYZZ (converted on the host).
-static int ipa_tail_sums(halo_ipa_session* ses, int mode, hipStream_t s) {
+static int ipa_tail_sums(halo_ipa_session* ses, int mode, hipStream_t s, const void* copy_src = nullptr,
+                         void* copy_dst = nullptr) {
     const size_t n0 = ses->n0, m = ses->m;
     char* sm = (char*)ses->small.ptr;
     if (mode == 0) {  // one fused launch (k_tail_round) up to TAIL_FUSE_N points, three above
         TailFoldArgs f{};
         f.active = ses->fold_pending;
+        if (ses->w_one_pending) {  // (no fold is pending right after the switch to the tail rounds)
+            f.w_one = ses->w[ses->wcur].as<uint4>();
+            ses->w_one_pending = false;
+        }
         if (f.active) {  // the previous round's fold, applied here (halo_ipa_fold deferred it)
             memcpy(&f.xi, &ses->pend_xi, 32);
             memcpy(&f.xinv, &ses->pend_xinv, 32);
@@ -1949,6 +2105,13 @@ static int ipa_tail_sums(halo_ipa_session* ses, int mode, hipStream_t s) {
         return HALO_OK;
     }
     // mode 1: U = sum_u w[u] G0[u]
+    if (ses->w_one_pending) {
+        DISPATCH_CURVE(ses->curve, Cv, {
+            hipLaunchKernelGGL(k_set_one_ark<typename Cv::Scalar>, dim3(1), dim3(64), 0, s, ses->w[ses->wcur].as<uint4>());
+        });
+        HALO_HIP(hipGetLastError());
+        ses->w_one_pending = false;
+    }
     const size_t nblk = (TAIL_WIN * n0 + TAIL_THREADS - 1) / TAIL_THREADS;
     uint4* out = (uint4*)(sm + 256);
     DISPATCH_CURVE(ses->curve, Cv, {
@@ -1958,10 +2121,11 @@ static int ipa_tail_sums(halo_ipa_session* ses, int mode, hipStream_t s) {
         hipLaunchKernelGGL(k_tail_msm<Cv>, dim3((unsigned)nblk), dim3(TAIL_THREADS), 0, s, ses->table, ses->table_ld,
                            ses->scal.as<const uint32_t>(), ses->side.as<const uint8_t>(), n0, m, 1, (uint32_t)nblk,
                            ses->part.as<uint4>(), (const uint4*)nullptr, (const uint4*)nullptr, (const uint32_t*)nullptr,
-                           out);
+                           out, (uint32_t*)nullptr, 0u, (const uint4*)nullptr, (const uint4*)copy_src, (uint4*)copy_dst);
         if (nblk > 1)
             hipLaunchKernelGGL(k_tail_final<Cv>, dim3(1), dim3(TAIL_THREADS), 0, s, ses->part.as<const uint4>(), (int)nblk,
-                               (const uint4*)nullptr, (const uint4*)nullptr, out, 1);
+                               (const uint4*)nullptr, (const uint4*)nullptr, out, 1, (uint32_t*)nullptr, 0u,
+                               (const uint4*)nullptr, (const uint4*)copy_src, (uint4*)copy_dst);
     });
     HALO_HIP(hipGetLastError());
     return HALO_OK;
@@ -2058,36 +2222,18 @@ int halo::srs_small_table(DeviceState* st, int curve, hipStream_t s) {
 // with the SRS's multiples table (leading dimension small_n0 >= n); mode 1 of k_tail_scalars /
 // k_tail_msm gives sum_k s[k] G0[k] (64 n table terms), k_tail_final adds w S from the 2^i S table.
 int halo::msm_srs_small(DeviceState* st, int curve, const void* scalars_ark, size_t n, const void* hide_scalar,
-                  void* d_out_wrapped, hipStream_t s, bool out_xyzz) {
-    SrsState& srs = st->srs[curve];
-    const size_t nmax = std::min(srs_small_max(), srs.n);
-    if (n < 1 || n > nmax) return set_error(HALO_EINVAL, "small SRS MSM: n (%zu) outside [1, %zu]", n, nmax);
-    const size_t nblk = (TAIL_WIN * n + TAIL_THREADS - 1) / TAIL_THREADS;
-    // scratch: GLV words (n x 32 B) | sides (n B, 256-B aligned) | partials
-    const size_t o_side = n * 32, o_part = o_side + ((n + 255) & ~(size_t)255);
-    if (srs.small_ev) HALO_HIP(hipStreamWaitEvent(s, srs.small_ev, 0));  // the previous small MSM is done with small_scr
-    else HALO_HIP(hipEventCreateWithFlags(&srs.small_ev, hipEventDisableTiming));
-    HALO_CHECK(srs.small_scr.reserve(o_part + nblk * 256));
-    HALO_CHECK(srs_small_table(st, curve, s));
-    char* scr = (char*)srs.small_scr.ptr;
+                  void* d_out_wrapped, hipStream_t s, bool out_xyzz, const void* plus_wrapped) {
+    if (plus_wrapped && !out_xyzz) return set_error(HALO_EINVAL, "small SRS MSM: + point needs the XYZZ output");
+    char* scr;
+    size_t o_side, o_part, nblk;
+    HALO_CHECK(small_msm_scratch(st, curve, n, s, &scr, &o_side, &o_part, &nblk));
     DISPATCH_CURVE(curve, Cv, {
         hipLaunchKernelGGL(k_tail_scalars<Cv>, dim3(gridn(n, 256)), dim3(256), 0, s, (const uint4*)nullptr,
                            (const uint4*)scalars_ark, n, (size_t)1, (size_t)0, 1, (uint32_t*)scr, (uint8_t*)(scr + o_side));
-        // the hiding term w S rides in block 0 (2^i S table); one block and an XYZZ result: no k_tail_final
-        const bool direct = out_xyzz && nblk == 1;
-        hipLaunchKernelGGL(k_tail_msm<Cv>, dim3((unsigned)nblk), dim3(TAIL_THREADS), 0, s,
-                           srs.small_tab->as<const uint4>(), srs.small_n0, (const uint32_t*)scr,
-                           (const uint8_t*)(scr + o_side), n, (size_t)0, 1, (uint32_t)nblk, (uint4*)(scr + o_part),
-                           hide_scalar ? srs.s_table.as<const uint4>() : (const uint4*)nullptr, (const uint4*)hide_scalar,
-                           (const uint32_t*)nullptr, direct ? (uint4*)d_out_wrapped : (uint4*)nullptr);
-        if (!direct)
-            hipLaunchKernelGGL(k_tail_final<Cv>, dim3(1), dim3(TAIL_THREADS), 0, s, (const uint4*)(scr + o_part),
-                               (int)nblk, (const uint4*)nullptr, (const uint4*)nullptr, (uint4*)d_out_wrapped,
-                               (int)out_xyzz);
     });
     HALO_HIP(hipGetLastError());
-    HALO_HIP(hipEventRecord(srs.small_ev, s));
-    return HALO_OK;
+    return small_msm_sums(st, curve, scr, o_side, o_part, nblk, n, hide_scalar, d_out_wrapped, s, out_xyzz, plus_wrapped,
+                          nullptr, nullptr);
 }
 
 static int ipa_copy_out(halo_ipa_session* ses) {
@@ -2429,8 +2575,8 @@ extern "C" int halo_ipa_end(halo_ipa_session* ses, halo_wrapped_point_t* U, halo
             if (ses->m != 0)
                 rc = set_error(HALO_EINVAL, "halo_ipa_end: U needs every round in the weighted / tail rounds (m = %zu)",
                                ses->m);
-            else if (ses->tail)
-                rc = ipa_tail_sums(ses, 1, s);  // XYZZ at [256, 384), converted below
+            else if (ses->tail)  // XYZZ at [256, 384), converted below; c = cs[0] copied to [384, 416) by its last block
+                rc = ipa_tail_sums(ses, 1, s, ses->cs.ptr, sm + 384);
             else
                 rc = msm_srs_range_device(st, ses->curve, 0, ses->w[ses->wcur].ptr, ses->n0, nullptr, nullptr, sm + 256,
                                           s, false);
@@ -2446,8 +2592,6 @@ extern "C" int halo_ipa_end(halo_ipa_session* ses, halo_wrapped_point_t* U, halo
         }
         // one copy through the pinned staging: U (wrapped, or XYZZ [256, 384) after tail rounds), c
         const bool u_xyzz = ses->tail;
-        if (!rc && u_xyzz && hipMemcpyAsync(sm + 384, ses->cs.ptr, 32, hipMemcpyDeviceToDevice, s) != hipSuccess)
-            rc = set_error(HALO_EDEVICE, "ipa end copy failed");
         if (!rc && hipMemcpyAsync(ses->pinned + 256, sm + 256, u_xyzz ? 160 : 96, hipMemcpyDeviceToHost, s) != hipSuccess)
             rc = set_error(HALO_EDEVICE, "ipa end copy failed");
         if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = set_error(HALO_EDEVICE, "ipa end synchronisation failed");

@@ -81,8 +81,9 @@ int msm_tiny(int curve, const void* bases_int, const void* scalars_ark, size_t n
              hipStream_t s);
 size_t msm_tiny_max();
 // out_xyzz: the result as 128 B packed XYZZ (host_xyzz_to_wrapped) instead of a WrappedPoint.
+// plus_wrapped (device WrappedPoint, or null): added to the result.
 int msm_srs_small(DeviceState* st, int curve, const void* scalars_ark, size_t n, const void* hide_scalar,
-                  void* d_out_wrapped, hipStream_t s, bool out_xyzz = false);
+                  void* d_out_wrapped, hipStream_t s, bool out_xyzz = false, const void* plus_wrapped = nullptr);
 // The hiding branch of pcdl::open_without_eval on device buffers (field_ops.hip), stream-ordered on s:
 // p_bar = (X - z) q (q: d ark coefficients, z: ark scalar) -> d + 1 ark coefficients;
 // p' = p (len coefficients, zero-padded to n) + alpha p_bar (p' may alias p), w' = w + alpha w_bar,
