@@ -154,44 +154,110 @@ HALO_DEV Jac<F> jac_dbl_quad(const Jac<F>& p) {
     r.Z = fe_dbl(YZ);
     return r;
 }
+// p + q as xyzz_add_quad, valid in the quad's lane 2 only, with the trivial cases done inside the quad:
+// an identity operand (idp / idq, quad-uniform) yields the other operand, reassembled in lane 2 by DPP
+// quad broadcasts from the coordinates the quad fetched anyway (role 0: p.X, q.ZZ; 1: q.X, p.ZZ;
+// 2: p.Y, q.ZZZ; 3: q.Y, p.ZZZ) -- no lane gathers, so a tree level can leave its sums in place.
+template <class F>
+HALO_DEV XYZZ<F> xyzz_add_quad_lane2(const XYZZ<F>& v, uint32_t s1, uint32_t s2, bool idp, bool idq) {
+    const uint32_t role = threadIdx.x & 3u;
+    const uint32_t odd = (role & 1u) ? ~0u : 0u, lo = role < 2 ? ~0u : 0u, r2 = role == 2 ? ~0u : 0u;
+    const uint32_t sa = (role & 1u) ? s2 : s1, sb = (role & 1u) ? s1 : s2;
+    Fe<F> a, b;
+#pragma unroll
+    for (int l = 0; l < NLIMB; l++) {
+        const uint32_t x = __shfl(v.X.v[l], (int)sa), y = __shfl(v.Y.v[l], (int)sa);
+        const uint32_t zz = __shfl(v.ZZ.v[l], (int)sb), zzz = __shfl(v.ZZZ.v[l], (int)sb);
+        a.v[l] = (x & lo) | (y & ~lo);
+        b.v[l] = (zz & lo) | (zzz & ~lo);
+    }
+    XYZZ<F> r = xyzz_id<F>();
+    if (!__all(idp || idq)) {
+        const Fe<F> t1 = fe_mul(a, b);
+        constexpr int SWAP = qp(1, 0, 3, 2);
+        const Fe<F> t1s = qperm<SWAP>(t1), bs = qperm<SWAP>(b);
+        const Fe<F> d = fe_sub_k<2>(pick(odd, t1, t1s), pick(odd, t1s, t1));
+        const Fe<F> t2 = fe_mul(pick(odd, b, d), pick(odd, bs, d));
+        const Fe<F> PPb = qperm<qp(0, 0, 0, 0)>(t2), Ab = qperm<qp(0, 1, 1, 3)>(t2);
+        const Fe<F> t3 = fe_mul(pick(lo, pick(odd, d, t1), Ab), PPb);
+        const Fe<F> Bb = qperm<qp(0, 3, 2, 3)>(t2), Qb = qperm<qp(0, 1, 0, 3)>(t3), PPPb = qperm<qp(1, 1, 1, 1)>(t3);
+        r.X = fe_reduce_8p(fe_sub_k<6>(t2, fe_add_nc(PPPb, fe_add_nc(Qb, Qb))));
+        const Fe<F> t4 = fe_mul(pick(lo, Bb, pick(odd, t1s, d)), pick(r2, fe_sub_k<2>(Qb, r.X), PPPb));
+        r.Y = fe_sub(t4, qperm<qp(0, 1, 3, 3)>(t4));
+        r.ZZ = t3;
+        r.ZZZ = qperm<qp(0, 1, 1, 3)>(t4);
+        const bool exc = role == 2 && !idp && !idq && fe_is_zero(t3);
+        if (__any(exc)) {  // P == +-Q: doubling or the identity (rare)
+            XYZZ<F> p;
+            p.X = qperm<qp(0, 0, 0, 0)>(a);
+            p.Y = qperm<qp(2, 2, 2, 2)>(a);
+            p.ZZ = qperm<qp(1, 1, 1, 1)>(b);
+            p.ZZZ = qperm<qp(3, 3, 3, 3)>(b);
+            if (exc) r = fe_is_zero_4p(d) ? xyzz_dbl(p) : xyzz_id<F>();
+        }
+    }
+    if (__any(idp != idq)) {  // one identity operand: the other one (wave-uniform branch: every lane
+                              // takes part in the broadcasts, the choice is a per-lane pick)
+        const uint32_t mq = idp ? ~0u : 0u;
+        XYZZ<F> o;
+        o.X = pick(mq, qperm<qp(1, 1, 1, 1)>(a), qperm<qp(0, 0, 0, 0)>(a));
+        o.Y = pick(mq, qperm<qp(3, 3, 3, 3)>(a), qperm<qp(2, 2, 2, 2)>(a));
+        o.ZZ = pick(mq, qperm<qp(0, 0, 0, 0)>(b), qperm<qp(1, 1, 1, 1)>(b));
+        o.ZZZ = pick(mq, qperm<qp(2, 2, 2, 2)>(b), qperm<qp(3, 3, 3, 3)>(b));
+        if (idp != idq) r = o;
+    }
+    if (idp && idq) r = xyzz_id<F>();
+    return r;
+}
+
 // sum over aligned groups of G lanes (G a power of two <= 64), valid in the group's first lane.  The
-// points live as a flat list (group g's at lanes [g G, g G + G)); a level turns the list of groups of
-// size gs into one of size gs / 2 by 64 / G * gs / 2 quad additions (16 per batch), each addition's
-// sum moved to its lane in the new list.
+// points form a flat list (group g's elements [g G, g G + G)); a level turns the list of groups of
+// size gs into one of size gs / 2 by 64 / G * gs / 2 quad additions (16 per batch, at most two
+// batches), and each sum stays where its quad formed it: element a of the new list at lane
+// 4 (a mod 16) + 2 (batch 0) or 4 (a mod 16) (batch 1, moved inside the quad by a DPP broadcast).
+// The next level gathers its operands from there, so no level moves its sums across lanes.
 template <class F>
 HALO_DEV XYZZ<F> wave_group_sum(XYZZ<F> v, uint32_t G) {
     const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t r0m = (lane & 3u) == 0u ? ~0u : 0u;
+    bool placed = false;  // false: element e at lane e
+    auto where = [&](uint32_t e) { return placed ? ((4u * (e & 15u) + (e < 16u ? 2u : 0u)) & 63u) : (e & 63u); };
     for (uint32_t gs = G; gs > 1; gs >>= 1) {
         const uint32_t m = gs >> 1, nadd = (64u / G) * m;  // 64 / G groups x m additions
         const uint32_t idv = xyzz_is_id(v) ? 1u : 0u;
-        XYZZ<F> nxt = xyzz_id<F>();
+        XYZZ<F> nxt;
         for (uint32_t b = 0; b * 16 < nadd; b++) {
-            // the quad's addition a = 16 b + lane / 4: lanes s1 = g gs + i and s2 = s1 + m
             const uint32_t a = b * 16 + (lane >> 2);
-            const uint32_t s1 = ((a / m) * gs + a % m) & 63u, s2 = (s1 + m) & 63u;
+            const uint32_t e1 = (a / m) * gs + a % m, e2 = e1 + m;
+            const uint32_t s1 = where(e1), s2 = where(e2);
             const uint32_t fp = __shfl(idv, (int)s1), fq = __shfl(idv, (int)s2);
             const bool idp = a >= nadd || fp != 0u, idq = a >= nadd || fq != 0u;
-            XYZZ<F> r = xyzz_id<F>();
-            if (!__all(idp || idq)) r = xyzz_add_quad(v, s1, s2, idp, idq);
-            // lane c = 16 b + j of the new list takes addition c's sum (quad j, lane 2), or, for an identity
-            // operand, the other operand itself
-            const uint32_t c = lane, j = (c - b * 16) & 15u;
-            const bool mine = c >= b * 16 && c < b * 16 + 16 && c < nadd;
-            const uint32_t c1 = ((c / m) * gs + c % m) & 63u, c2 = (c1 + m) & 63u;
-            const bool cp = __shfl(idv, (int)c1) != 0u, cq = __shfl(idv, (int)c2) != 0u;
-            const bool triv = mine && (cp || cq);
-            XYZZ<F> t = xyzz_shfl(r, (int)(4 * j + 2));
-            if (__any(triv)) {
-                const XYZZ<F> o = xyzz_shfl(v, (int)(cp ? c2 : c1));
-                if (triv) t = o;
+            const XYZZ<F> r = xyzz_add_quad_lane2(v, s1, s2, idp, idq);
+            if (b == 0) {
+                nxt = r;
+            } else {  // batch 1's sums to lane 0 of their quads
+                nxt.X = pick(r0m, qperm<qp(2, 2, 2, 2)>(r.X), nxt.X);
+                nxt.Y = pick(r0m, qperm<qp(2, 2, 2, 2)>(r.Y), nxt.Y);
+                nxt.ZZ = pick(r0m, qperm<qp(2, 2, 2, 2)>(r.ZZ), nxt.ZZ);
+                nxt.ZZZ = pick(r0m, qperm<qp(2, 2, 2, 2)>(r.ZZZ), nxt.ZZZ);
             }
-            if (mine) nxt = t;
         }
         v = nxt;
+        placed = true;
     }
-    // group g's sum is at lane g now; its first lane is g G
-    return G > 1 && G < 64 ? xyzz_shfl(v, (int)(lane / G)) : v;
+    if (!placed) return v;
+    if (G == 64) {  // element 0 (lane 2) to its quad
+        XYZZ<F> r;
+        r.X = qperm<qp(2, 2, 2, 2)>(v.X);
+        r.Y = qperm<qp(2, 2, 2, 2)>(v.Y);
+        r.ZZ = qperm<qp(2, 2, 2, 2)>(v.ZZ);
+        r.ZZZ = qperm<qp(2, 2, 2, 2)>(v.ZZZ);
+        return r;
+    }
+    // group g's sum is element g; every lane of the group gets it
+    return xyzz_shfl(v, (int)where(lane / G));
 }
+
 // sum over aligned groups of G threads (G a power of two <= blockDim): valid in the group's first
 // thread.  Every wave sums its lanes (G <= 64: its groups) cooperatively; for G > 64 the first wave
 // of the block sums the waves' sums of every group and hands each group's sum back to its first

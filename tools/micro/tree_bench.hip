@@ -1,7 +1,10 @@
 // Single-wave / single-block latency of the XYZZ tree sums (tree.hpp) on gfx950: one block runs
 // ITER dependent group sums (the sum re-enters lane 0), so the time per call is the critical path of
-// one tree.  Build twice to A/B the quad-cooperative levels against one addition per lane:
-//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I../../halo_amd/csrc [-DHALO_TREE_COOP=0] -o tb tree_bench.hip
+// one tree:
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I../../halo_amd/csrc -o tb tree_bench.hip
+// (round 5: the levels that leave their sums in place measured 20.9 us per isolated 64-lane tree
+// against 19.6 us for the round-3 levels that moved every sum to its list position, yet the library's
+// tail rounds and small MSMs ran faster with them: pcdl::open 2^10 1.54 -> 1.48 ms, interleaved)
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 
@@ -73,8 +76,8 @@ int main() {
         CHECK(hipMemcpy(h, out, 128, hipMemcpyDeviceToHost));
         uint32_t x = 0;
         for (int i = 0; i < 32; i++) x = x * 31 + h[i];
-        printf("block %3d G %3u live %2u: %.2f us per tree (COOP=%d, check %08x)\n", c.block, c.G, c.live,
-               ms * 1e3 / ITER, HALO_TREE_COOP, x);
+        printf("block %3d G %3u live %2u: %.2f us per tree (check %08x)\n", c.block, c.G, c.live,
+               ms * 1e3 / ITER, x);
     }
     return 0;
 }
