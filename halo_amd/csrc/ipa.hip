@@ -278,14 +278,13 @@ __global__ __launch_bounds__(FOLD_THREADS, 4) void k_ipa_fold(uint4* gs, uint4* 
 template <class Cv>
 __global__ __launch_bounds__(64) void k_pow2_xyzz_from_wrapped(const uint4* P_wrapped, uint4* out_xyzz, int count) {
     using F = typename Cv::Base;
-    // the doubling chain runs in Jacobian coordinates (dbl-2009-l: 1M + 5S, vs 6M + 3S in XYZZ); the
-    // per-entry XYZZ conversion (Z^2, Z^3) is off the chain's dependency path.  Quad-cooperative
-    // doublings (lanes 0-3, jac_dbl_quad) when the tree code is cooperative.
+    // quad-cooperative XYZZ doublings on lanes 0-3 (xyzz_dbl_quad: three product rounds, 4.0 k cycles
+    // against 6.3 k for the Jacobian jac_dbl_quad with its longer add / double tail, tools/micro/tree_parts.hip)
     if (threadIdx.x >= 4) return;
-    Jac<F> j = jac_from_xyzz(xyzz_from_aff(aff_from_wrapped<F>(P_wrapped)));
+    XYZZ<F> q = xyzz_from_aff(aff_from_wrapped<F>(P_wrapped));
     for (int i = 0; i < count; i++) {
-        if (threadIdx.x == 0) xyzz_store(out_xyzz + 8 * i, jac_to_xyzz(j));
-        j = jac_dbl_quad(j);
+        if (threadIdx.x == 0) xyzz_store(out_xyzz + 8 * i, q);
+        q = xyzz_dbl_quad(q);
     }
 }
 
@@ -349,9 +348,10 @@ constexpr int TAIL_WIN = 2 * TAIL_TBL;  // terms per point: 32 windows x (k1, k2
 // waves' quad trees then share a SIMD's issue slots)
 constexpr int TAIL_THREADS = 256;
 
-// the doubling chain in Jacobian coordinates (dbl-2009-l: 7 multiplications against XYZZ's 9), by a
-// quad of lanes per point (jac_dbl_quad: three product rounds per doubling; TAIL_TABLE_LANES = 4) --
-// the chain is latency-bound and the grid is small (n0 <= 8192 points)
+// the doubling chain by a quad of lanes per point (xyzz_dbl_quad: three product rounds per doubling,
+// 4.0 k cycles against 6.3 k for the Jacobian jac_dbl_quad -- fewer products, but a longer tail of
+// additions and doublings on every lane; tools/micro/tree_parts.hip; TAIL_TABLE_LANES = 4) -- the
+// chain is latency-bound and the grid is small (n0 <= 8192 points)
 constexpr int TAIL_TABLE_LANES = 4;
 template <class Cv>
 __global__ __launch_bounds__(64) void k_tail_table(const uint4* gs, int gs_xyzz, size_t n0, uint4* table) {
@@ -361,10 +361,10 @@ __global__ __launch_bounds__(64) void k_tail_table(const uint4* gs, int gs_xyzz,
     const bool lead = threadIdx.x % TAIL_TABLE_LANES == 0;
     const XYZZ<F> p0 = gs_xyzz ? xyzz_load<F>(gs + 8 * k) : xyzz_from_aff(aff_load<F>(gs + 4 * k));
     if (lead) xyzz_store(table + 8 * k, p0);
-    Jac<F> j = jac_from_xyzz(p0);
+    XYZZ<F> q = p0;
     for (int w = 1; w < TAIL_TBL; w++) {
-        for (int b = 0; b < TAIL_DB; b++) j = jac_dbl_quad(j);
-        if (lead) xyzz_store(table + 8 * ((size_t)w * TAIL_MUL * n0 + k), jac_to_xyzz(j));
+        for (int b = 0; b < TAIL_DB; b++) q = xyzz_dbl_quad(q);
+        if (lead) xyzz_store(table + 8 * ((size_t)w * TAIL_MUL * n0 + k), q);
     }
 }
 
@@ -1492,7 +1492,7 @@ static int ipa_h_table(DeviceState* st, int curve, const halo_wrapped_point_t* H
 //   [1280) S (internal), [1344) C' out
 constexpr size_t SM_BYTES = 2048;
 constexpr size_t SM_WBAR = 1024, SM_ALPHA = 1056, SM_W = 1088, SM_WP = 1120, SM_C = 1152, SM_CBAR = 1216, SM_S = 1280,
-                 SM_CP = 1344, SM_NEGW = 1408, SM_T = 1536, SM_EVAL = 1664, SM_V = 1696,  // SM_T: 128 B XYZZ
+                 SM_CP = 1344, SM_NEGW = 1408, SM_T = 1536, SM_V = 1696,  // SM_T: 128 B XYZZ
                  SM_HKW = 1728,  // 2 x 10 words: the dots' GLV splits (k_tail_digits -> k_tail_round)
                  SM_CTR = 1856;  // 2 x u32 arrival counters of k_tail_round, 1 of k_weighted_prep (zero between launches)
 

@@ -269,14 +269,12 @@ __global__ __launch_bounds__(64) void k_final(const uint4* window_sums, int W, i
     using F = typename Cv::Base;
     XYZZ<F> horner = xyzz_id<F>();
     // every quad of the wave runs the same Horner chain (identical data, so every branch is uniform):
-    // quad-cooperative doublings (3 product rounds instead of 7) and additions (4 instead of 14)
+    // quad-cooperative doublings (xyzz_dbl_quad: 4.0 k cycles per doubling against 6.3 k for the
+    // Jacobian jac_dbl_quad, tools/micro/tree_parts.hip) and additions (4 product rounds instead of 14)
     const uint32_t s1 = threadIdx.x & 60u;
     for (int w = W - 1; w >= 0; w--) {
-        if (w != W - 1 && !xyzz_is_id(horner)) {
-            Jac<F> j = jac_from_xyzz(horner);
-            for (int k = 0; k < c; k++) j = jac_dbl_quad(j);
-            horner = jac_to_xyzz(j);
-        }
+        if (w != W - 1 && !xyzz_is_id(horner))
+            for (int k = 0; k < c; k++) horner = xyzz_dbl_quad(horner);
         const XYZZ<F> ws = xyzz_load<F>(window_sums + 8 * w);
         const bool idp = xyzz_is_id(horner), idq = xyzz_is_id(ws);
         if (idp || idq) {

@@ -131,29 +131,6 @@ HALO_DEV XYZZ<F> xyzz_dbl_quad(const XYZZ<F>& p) {
     r.ZZZ = qperm<qp(2, 2, 2, 2)>(t3);
     return r;
 }
-// 2p in Jacobian coordinates by the quad (dbl-2009-l as jac_dbl; every lane of an aligned quad holds p
-// and gets 2p): A = X^2, B = Y^2, Y Z | C = B^2, (X + B)^2, F = E^2 | E (D - X3), one product per lane
-// per round, the first two rounds exchanged by DPP quad broadcasts (the last product every lane forms
-// itself).
-template <class F>
-HALO_DEV Jac<F> jac_dbl_quad(const Jac<F>& p) {
-    const uint32_t role = threadIdx.x & 3u;
-    const uint32_t r1 = role == 1 ? ~0u : 0u, r2 = role == 2 ? ~0u : 0u;
-    // lane 0 (and 3): A = X^2; 1: B = Y^2; 2: Y Z
-    const Fe<F> t1 = fe_mul(pick(r1 | r2, p.Y, p.X), pick(r2, p.Z, pick(r1, p.Y, p.X)));
-    const Fe<F> A = qperm<qp(0, 0, 0, 0)>(t1), B = qperm<qp(1, 1, 1, 1)>(t1), YZ = qperm<qp(2, 2, 2, 2)>(t1);
-    const Fe<F> E = fe_add(A, fe_dbl(A));
-    // lane 0 (and 3): C = B^2; 1: (X + B)^2; 2: F = E^2
-    const Fe<F> t2 = fe_sqr(pick(r1, fe_add(p.X, B), pick(r2, E, B)));
-    const Fe<F> C = qperm<qp(0, 0, 0, 0)>(t2), XB2 = qperm<qp(1, 1, 1, 1)>(t2), Fv = qperm<qp(2, 2, 2, 2)>(t2);
-    const Fe<F> D = fe_dbl(fe_sub(fe_sub(XB2, A), C));
-    Jac<F> r;
-    r.X = fe_sub(Fv, fe_dbl(D));
-    const Fe<F> C8 = fe_dbl(fe_dbl(fe_dbl(C)));
-    r.Y = fe_sub(fe_mul(E, fe_sub(D, r.X)), C8);
-    r.Z = fe_dbl(YZ);
-    return r;
-}
 // p + q as xyzz_add_quad, valid in the quad's lane 2 only, with the trivial cases done inside the quad:
 // an identity operand (idp / idq, quad-uniform) yields the other operand, reassembled in lane 2 by DPP
 // quad broadcasts from the coordinates the quad fetched anyway (role 0: p.X, q.ZZ; 1: q.X, p.ZZ;

@@ -4,6 +4,7 @@
 #   SIZES="22 23 24" bash tools/ab.sh ntt  <lib> ...    NTT pairs (tools/ntt_time.py)
 #   SIZES="2 6 10"   bash tools/ab.sh pcdl <lib> ...    pcdl::open sweep (tools/pcdl_open_time.py)
 #   SIZES="16 20"    bash tools/ab.sh ipa  <lib> ...    IPA openings (tools/ipa_time.py)
+#   SIZES="16"       bash tools/ab.sh prove <lib> ...   naive_prover rounds (tools/prove_time.py, warm repetition)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 what=$1; shift
@@ -27,7 +28,9 @@ print('ms/step %.4f  k_acc %.3f  latency %.3f  ntt pair %.3f' % (d['ms_per_step'
           | sed 's/begin+eval.*rounds=/rounds=/' || exit 1 ;;
       ipa)
         HALO_LIB=$PWD/$lib REPS=2 timeout -k 10 300 python tools/ipa_time.py ${SIZES:-16 20} 2>&1 | grep "^open" || exit 1 ;;
-      *) echo "unknown: $what (msm | ntt | pcdl | ipa)"; exit 2 ;;
+      prove)
+        HALO_LIB=$PWD/$lib timeout -k 10 200 python tools/prove_time.py ${SIZES:-16} 2>&1 | grep '"rep": 1' || exit 1 ;;
+      *) echo "unknown: $what (msm | ntt | pcdl | ipa | prove)"; exit 2 ;;
     esac
   done
 done
