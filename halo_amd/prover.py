@@ -387,6 +387,7 @@ class DeviceBackend:
         self.curve = H.CURVES[curve]
         self.field = H.SCALAR_FIELD[self.curve]
         self.m = SCALAR_MODULUS[curve]
+        self.r_inv = pow(1 << 256, -1, self.m)  # ark Montgomery words -> canonical (once, not per value)
         self.stream = torch.cuda.current_stream().cuda_stream
         self.sp = ctypes.c_void_p(self.stream)
         hp = np.zeros(8, dtype=np.uint64)
@@ -400,7 +401,7 @@ class DeviceBackend:
 
     def to_int(self, a: np.ndarray) -> int:
         v = int(a[0]) | int(a[1]) << 64 | int(a[2]) << 128 | int(a[3]) << 192
-        return v * pow(1 << 256, -1, self.m) % self.m
+        return v * self.r_inv % self.m
 
     def _p(self, t):
         return ctypes.c_void_p(t.data_ptr())
