@@ -122,6 +122,7 @@ SIGNATURES = {
     "halo_ipa_fold": [_vp, _vp, _vp],
     "halo_ipa_state": [_vp, ctypes.POINTER(_sz), _vp, _vp, _vp],
     "halo_ipa_end": [_vp, _vp, _vp],
+    "halo_ipa_end_multi": [_vp, _sz, _vp, _vp],
     "halo_ipa_fold_host": [ctypes.c_int, _vp, _vp, _vp, _sz, _vp, _vp],
     "halo_field_op": [ctypes.c_int, ctypes.c_int, _vp, _vp, _sz, _vp],
     "halo_curve_op": [ctypes.c_int, ctypes.c_int, _vp, _vp, _vp, _sz, _vp],

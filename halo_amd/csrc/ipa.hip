@@ -2553,6 +2553,55 @@ extern "C" int halo_ipa_state(halo_ipa_session* ses, size_t* m, halo_wrapped_poi
     return HALO_OK;
 }
 
+// halo_ipa_end in two halves: the device work enqueued on the session's stream (st->mu held), then the
+// wait, the host conversion and the release -- halo_ipa_end_multi enqueues every session's end before
+// it waits for any, so the lockstep openings' final U sums overlap on the device.
+static int ipa_end_enqueue(DeviceState* st, halo_ipa_session* ses) {
+    hipStream_t s = ses->s;
+    char* sm = (char*)ses->small.ptr;
+    int rc = HALO_OK;
+    if (!ses->started) {
+        rc = set_error(HALO_EINVAL, "halo_ipa_end: session not started");
+    } else if ((rc = ipa_apply_pending_fold(st, ses))) {
+    } else if (ses->tail || ses->weighted) {
+        // U = G_0 = sum_u w[u] G0[u] (len = 1 once every round ran)
+        if (ses->m != 0)
+            rc = set_error(HALO_EINVAL, "halo_ipa_end: U needs every round in the weighted / tail rounds (m = %zu)",
+                           ses->m);
+        else if (ses->tail)  // XYZZ at [256, 384), converted below; c = cs[0] copied to [384, 416) by its last block
+            rc = ipa_tail_sums(ses, 1, s, ses->cs.ptr, sm + 384);
+        else
+            rc = msm_srs_range_device(st, ses->curve, 0, ses->w[ses->wcur].ptr, ses->n0, nullptr, nullptr, sm + 256, s,
+                                      false);
+        if (!rc && !ses->tail && hipMemcpyAsync(sm + 320, ses->cs.ptr, 32, hipMemcpyDeviceToDevice, s) != hipSuccess)
+            rc = set_error(HALO_EDEVICE, "ipa end copy failed");
+    } else if ((rc = ipa_ensure_gs(st, ses))) {
+    } else {
+        DISPATCH_CURVE(ses->curve, Cv, {
+            hipLaunchKernelGGL(k_copy_first_wrapped<Cv>, dim3(1), dim3(64), 0, s, ses->gs.as<const uint4>(),
+                               ses->cs.as<const uint4>(), (uint4*)(sm + 256), (uint4*)(sm + 320));
+        });
+        if (hipGetLastError() != hipSuccess) rc = set_error(HALO_EDEVICE, "ipa end launch failed");
+    }
+    // one copy through the pinned staging: U (wrapped, or XYZZ [256, 384) after tail rounds), c
+    if (!rc && hipMemcpyAsync(ses->pinned + 256, sm + 256, ses->tail ? 160 : 96, hipMemcpyDeviceToHost, s) != hipSuccess)
+        rc = set_error(HALO_EDEVICE, "ipa end copy failed");
+    return rc;
+}
+
+static int ipa_end_finish(halo_ipa_session* ses, halo_wrapped_point_t* U, halo_fe_t* c) {
+    const bool u_xyzz = ses->tail;
+    if (hipStreamSynchronize(ses->s) != hipSuccess) return set_error(HALO_EDEVICE, "ipa end synchronisation failed");
+    if (U) {
+        if (u_xyzz)
+            host_xyzz_to_wrapped(ses->curve, ses->pinned + 256, U);
+        else
+            memcpy(U, ses->pinned + 256, 64);
+    }
+    if (c) memcpy(c, ses->pinned + (u_xyzz ? 384 : 320), 32);
+    return HALO_OK;
+}
+
 extern "C" int halo_ipa_end(halo_ipa_session* ses, halo_wrapped_point_t* U, halo_fe_t* c) {
     clear_error();
     if (!ses) return set_error(HALO_EINVAL, "halo_ipa_end: null session");
@@ -2565,45 +2614,40 @@ extern "C" int halo_ipa_end(halo_ipa_session* ses, halo_wrapped_point_t* U, halo
             return HALO_EDEVICE;
         }
         std::lock_guard<std::mutex> g(st->mu);
-        hipStream_t s = ses->s;
-        char* sm = (char*)ses->small.ptr;
-        if (!ses->started) {
-            rc = set_error(HALO_EINVAL, "halo_ipa_end: session not started");
-        } else if ((rc = ipa_apply_pending_fold(st, ses))) {
-        } else if (ses->tail || ses->weighted) {
-            // U = G_0 = sum_u w[u] G0[u] (len = 1 once every round ran)
-            if (ses->m != 0)
-                rc = set_error(HALO_EINVAL, "halo_ipa_end: U needs every round in the weighted / tail rounds (m = %zu)",
-                               ses->m);
-            else if (ses->tail)  // XYZZ at [256, 384), converted below; c = cs[0] copied to [384, 416) by its last block
-                rc = ipa_tail_sums(ses, 1, s, ses->cs.ptr, sm + 384);
-            else
-                rc = msm_srs_range_device(st, ses->curve, 0, ses->w[ses->wcur].ptr, ses->n0, nullptr, nullptr, sm + 256,
-                                          s, false);
-            if (!rc && !ses->tail && hipMemcpyAsync(sm + 320, ses->cs.ptr, 32, hipMemcpyDeviceToDevice, s) != hipSuccess)
-                rc = set_error(HALO_EDEVICE, "ipa end copy failed");
-        } else if ((rc = ipa_ensure_gs(st, ses))) {
-        } else {
-            DISPATCH_CURVE(ses->curve, Cv, {
-                hipLaunchKernelGGL(k_copy_first_wrapped<Cv>, dim3(1), dim3(64), 0, s, ses->gs.as<const uint4>(),
-                                   ses->cs.as<const uint4>(), (uint4*)(sm + 256), (uint4*)(sm + 320));
-            });
-            if (hipGetLastError() != hipSuccess) rc = set_error(HALO_EDEVICE, "ipa end launch failed");
-        }
-        // one copy through the pinned staging: U (wrapped, or XYZZ [256, 384) after tail rounds), c
-        const bool u_xyzz = ses->tail;
-        if (!rc && hipMemcpyAsync(ses->pinned + 256, sm + 256, u_xyzz ? 160 : 96, hipMemcpyDeviceToHost, s) != hipSuccess)
-            rc = set_error(HALO_EDEVICE, "ipa end copy failed");
-        if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = set_error(HALO_EDEVICE, "ipa end synchronisation failed");
-        if (!rc && U) {
-            if (u_xyzz)
-                host_xyzz_to_wrapped(ses->curve, ses->pinned + 256, U);
-            else
-                memcpy(U, ses->pinned + 256, 64);
-        }
-        if (!rc && c) memcpy(c, ses->pinned + (u_xyzz ? 384 : 320), 32);
+        rc = ipa_end_enqueue(st, ses);
+        if (!rc) rc = ipa_end_finish(ses, U, c);
     }
     ipa_release(ses);
+    return rc;
+}
+
+extern "C" int halo_ipa_end_multi(halo_ipa_session* const* ses, size_t k, halo_wrapped_point_t* U, halo_fe_t* c) {
+    clear_error();
+    if (k && !ses) return set_error(HALO_EINVAL, "halo_ipa_end_multi: null session list");
+    for (size_t i = 0; i < k; i++) {
+        if (!ses[i]) return set_error(HALO_EINVAL, "halo_ipa_end_multi: null session %zu", i);
+        if (!ipa_is_open(ses[i]))
+            return set_error(HALO_EINVAL, "halo_ipa_end_multi: session %zu is not open (already ended)", i);
+        for (size_t j = 0; j < i; j++)
+            if (ses[j] == ses[i]) return set_error(HALO_EINVAL, "halo_ipa_end_multi: session %zu listed twice", i);
+    }
+    int rc = HALO_OK;
+    if (k && (U || c)) {
+        DeviceState* st = current_state();
+        if (!st) {
+            for (size_t i = 0; i < k; i++) ipa_release(ses[i]);
+            return HALO_EDEVICE;
+        }
+        std::lock_guard<std::mutex> g(st->mu);
+        for (size_t i = 0; i < k && !rc; i++) rc = ipa_end_enqueue(st, ses[i]);
+        // every stream is drained before any session goes back to the pool, failed or not
+        for (size_t i = 0; i < k; i++) {
+            const int r = rc ? (hipStreamSynchronize(ses[i]->s) == hipSuccess ? HALO_OK : HALO_EDEVICE)
+                             : ipa_end_finish(ses[i], U ? U + i : nullptr, c ? c + i : nullptr);
+            if (!rc && r) rc = r;
+        }
+    }
+    for (size_t i = 0; i < k; i++) ipa_release(ses[i]);
     return rc;
 }
 

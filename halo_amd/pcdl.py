@@ -124,6 +124,20 @@ class IpaSession:
         H.check(H.load().halo_ipa_end(s, H.ptr(U), H.ptr(c)))
         return U, c
 
+    @staticmethod
+    def end_many(sessions):
+        """end() of lockstep sessions in one halo_ipa_end_multi call (their final U sums overlap on the
+        device); [(U, c)] in order."""
+        k = len(sessions)
+        U = np.zeros((k, 8), dtype=np.uint64)
+        c = np.zeros((k, 4), dtype=np.uint64)
+        handles = [s_._s for s_ in sessions]
+        for s_ in sessions:
+            s_._s = None
+        arr = (ctypes.c_void_p * k)(*[h.value for h in handles])
+        H.check(H.load().halo_ipa_end_multi(arr, k, H.ptr(U), H.ptr(c)))
+        return [(U[i].copy(), c[i].copy()) for i in range(k)]
+
 
 def ipa_rounds(cs, z, H_prime, challenge: Callable, inverse: Callable, curve="pallas"):
     """The round loop of open_without_eval (pcdl.rs:392-450) given p'.coeffs resized to n, z, H' and

@@ -700,13 +700,10 @@ class DeviceBackend:
                 Ls[i].append(Lb[i].copy())
                 Rs[i].append(Rb[i].copy())
                 xis[i].append(xs[i])
-        outs = []
-        for i in range(k):
-            U = np.zeros(8, dtype=np.uint64)
-            c0 = np.zeros(4, dtype=np.uint64)
-            self.H.check(self.L.halo_ipa_end(ctypes.c_void_p(sess[i]), self.H.ptr(U), self.H.ptr(c0)))
-            outs.append((Ls[i], Rs[i], U, self.to_int(c0), xis[i]))
-        return outs
+        Us = np.zeros((k, 8), dtype=np.uint64)
+        c0s = np.zeros((k, 4), dtype=np.uint64)
+        self.H.check(self.L.halo_ipa_end_multi(sess, k, self.H.ptr(Us), self.H.ptr(c0s)))
+        return [(Ls[i], Rs[i], Us[i].copy(), self.to_int(c0s[i]), xis[i]) for i in range(k)]
 
     def ipa_many_xi(self, jobs, chals):
         return self.ipa_many(jobs, chals, xi_mode=True)

@@ -376,6 +376,11 @@ int halo_ipa_state(halo_ipa_session* s, size_t* m, halo_wrapped_point_t* gs, hal
  * session's streams and device buffers go back to a per-device pool (reused by the next opening;
  * released by halo_shutdown), so a warm opening allocates nothing. */
 int halo_ipa_end(halo_ipa_session* s, halo_wrapped_point_t* U, halo_fe_t* c);
+/* halo_ipa_end of k lockstep sessions (U[i], c[i] of session i; U or c may be NULL): every session's
+ * final U sum is enqueued on its own stream before any is waited for.  Argument errors (a null,
+ * closed or repeated session) release nothing; otherwise every listed session is released, also on
+ * an error. */
+int halo_ipa_end_multi(halo_ipa_session* const* ses, size_t k, halo_wrapped_point_t* U, halo_fe_t* c);
 /* One stateless fold over host vectors of length 2m (the loop body of pcdl.rs:427-435), in place
  * on the left halves. */
 int halo_ipa_fold_host(halo_curve_t curve, halo_wrapped_point_t* gs, halo_fe_t* cs, halo_fe_t* zs,

@@ -179,7 +179,8 @@ def test_ipa_wide_shifted_windows(hal, corc, c_s):
 @pytest.mark.parametrize("k", [2, 3, 5])
 def test_ipa_lockstep_sessions_equal_single(hal, corc, k):
     """halo_ipa_round_lr_multi over k sessions in lockstep (their weighted rounds share one L/R MSM,
-    up to 4 sessions per MSM) gives every session's L, R, U, c exactly as that session run alone."""
+    up to 4 sessions per MSM) and halo_ipa_end_multi give every session's L, R, U, c exactly as that
+    session run alone with halo_ipa_end."""
     import ctypes
     c = P.PALLAS
     r = c.scalar
@@ -208,7 +209,7 @@ def test_ipa_lockstep_sessions_equal_single(hal, corc, k):
             for q in range(len(idx)):
                 out[q][0].append(Lb[q].copy())
                 out[q][1].append(Rb[q].copy())
-        ends = [s_.end() for s_ in sess]
+        ends = pcdl.IpaSession.end_many(sess) if len(sess) > 1 else [s_.end() for s_ in sess]
         return [(o[0], o[1], e[0], e[1]) for o, e in zip(out, ends)]
 
     together = run(list(range(k)))
@@ -477,3 +478,31 @@ def test_ipa_fold_forms_xi_inverse(hal, corc, cname, cid):
         ses.fold(np.zeros(4, dtype=np.uint64))
     s, ses._s = ses._s, None  # release without the remaining rounds
     hal.check(hal.load().halo_ipa_end(s, None, None))
+
+
+@pytest.mark.gpu
+def test_ipa_end_multi_arguments(hal, corc):
+    """halo_ipa_end_multi refuses a repeated or closed session without releasing anything (HALO_EINVAL),
+    and releases every listed session otherwise (U, c NULL: no final sum)."""
+    import ctypes
+    c = P.PALLAS
+    r = c.scalar
+    n = 64
+    g = corc.srs_generate("pallas", n)
+    group.PublicParams.upload("pallas", g, precompute_windows=False)
+    rng = random.Random(11)
+    Hp = np.array(P.point_to_wrapped(c, P.mul_fast(c, 3, c.generator)), dtype=np.uint64)
+    L = hal.load()
+    sess = []
+    for _ in range(2):
+        cs = fe([rng.randrange(r) for _ in range(n)], r)
+        z = rng.randrange(r)
+        sess.append(pcdl.IpaSession.from_vectors(g[:n], cs, fe(P.construct_powers(z, n, r), r), Hp, "pallas"))
+    h = [s_._s.value for s_ in sess]
+    dup = (ctypes.c_void_p * 2)(h[0], h[0])
+    assert L.halo_ipa_end_multi(dup, 2, None, None) == 1  # HALO_EINVAL
+    both = (ctypes.c_void_p * 2)(h[0], h[1])
+    for s_ in sess:
+        s_._s = None
+    hal.check(L.halo_ipa_end_multi(both, 2, None, None))
+    assert L.halo_ipa_end_multi(both, 2, None, None) == 1  # HALO_EINVAL  # both closed now
