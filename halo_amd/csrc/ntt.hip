@@ -316,7 +316,10 @@ HALO_DEV void ntt_lds_barrier(bool wave_only = false) {
 // owns T = NE / R consecutive columns.  Each thread holds EPT elements in registers; the first
 // G0 stages are done straight from the global loads, the rest in radix-4 groups through LDS, and a
 // final coalesced store phase writes y[(j / Ns) Ns R + (j mod Ns) + k Ns].
-template <class F, int NE>
+// FULL: the block's T R positions fill all NE (every transform of at least NE elements), so no phase
+// tests a position against EB -- without the tests the compiler also drops the register copies that
+// the conditional LDS reads and writes cost (36 v_mov per group and thread in the 2048-element kernel)
+template <class F, int NE, bool FULL>
 __global__ __launch_bounds__(NE / NTT_EPT, 4) void k_ntt_pass(NttPassArgs a) {
     constexpr int EPT = NTT_EPT;
     constexpr uint32_t TH = NE / EPT;
@@ -351,7 +354,7 @@ __global__ __launch_bounds__(NE / NTT_EPT, 4) void k_ntt_pass(NttPassArgs a) {
 #pragma unroll
     for (int m = 0; m < EPT; m++) {
         const uint32_t pos = base + m;
-        if (pos < EB) {
+        if (FULL || pos < EB) {
             const uint32_t t = pos >> r;
             const uint32_t pl = a.prune ? (pos & ~((1u << a.prune) - 1u)) : pos;  // the group's nonzero input
             const uint32_t rho = r ? (__brev(pl & (R - 1)) >> (32 - r)) : 0;
@@ -390,7 +393,7 @@ __global__ __launch_bounds__(NE / NTT_EPT, 4) void k_ntt_pass(NttPassArgs a) {
         const uint32_t pb = ntt_swz<NE>(base);
 #pragma unroll
         for (int m = 0; m < EPT; m++)
-            if (base + m < EB) lds_put_soa(data, pb ^ (uint32_t)m, NE, v[m]);
+            if (FULL || base + m < EB) lds_put_soa(data, pb ^ (uint32_t)m, NE, v[m]);
     }
     // ---- remaining stages in radix-4 groups through LDS; each group's twiddles are loaded before the
     // barrier that precedes its LDS reads
@@ -426,7 +429,7 @@ __global__ __launch_bounds__(NE / NTT_EPT, 4) void k_ntt_pass(NttPassArgs a) {
         for (int m = 0; m < EPT; m++) {
             const uint32_t pos = gb + (uint32_t)m * h;
             const uint32_t ph = (pos ^ shb) ^ ntt_swz_hi<NE>(((uint32_t)m * h) >> 5);
-            if (pos < EB) v[m] = lds_get_soa<F>(data, ph, NE);
+            if (FULL || pos < EB) v[m] = lds_get_soa<F>(data, ph, NE);
         }
         // partial after normalized inputs, full otherwise.  The choice is block-uniform: the next group
         // reads positions other waves wrote (the unit group's thread order crosses waves), so the unit
@@ -443,7 +446,7 @@ __global__ __launch_bounds__(NE / NTT_EPT, 4) void k_ntt_pass(NttPassArgs a) {
         for (int m = 0; m < EPT; m++) {
             const uint32_t pos = gb + (uint32_t)m * h;
             const uint32_t ph = (pos ^ shb) ^ ntt_swz_hi<NE>(((uint32_t)m * h) >> 5);
-            if (pos < EB) lds_put_soa(data, ph, NE, v[m]);
+            if (FULL || pos < EB) lds_put_soa(data, ph, NE, v[m]);
         }
         const uint32_t sn = s + 2;
         if (sn < r) {
@@ -457,7 +460,7 @@ __global__ __launch_bounds__(NE / NTT_EPT, 4) void k_ntt_pass(NttPassArgs a) {
 #pragma unroll
     for (int i = 0; i < EPT; i++) {
         const uint32_t idx = tau + TH * (uint32_t)i;
-        if (idx >= EB) continue;
+        if (!FULL && idx >= EB) continue;
         uint32_t k, t;
         if (a.log_ns == 0) {
             t = idx >> r;
@@ -785,10 +788,15 @@ static int ntt_device(DeviceState* st, int field, const void* d_in, void* d_out,
         const size_t lds = NE * NLIMB * 4;
         dim3 grid((unsigned)(NJ / T), (unsigned)batch);
         ProfScope prof("ntt_pass", s);
-        if (NE == NTT_E_BIG)
-            HALO_LAUNCH(prof, (k_ntt_pass<F, NTT_E_BIG>), grid, dim3(NTT_E_BIG / NTT_EPT), lds, s, a);
+        const bool full = (T << lr) == NE;
+        if (NE == NTT_E_BIG && full)
+            HALO_LAUNCH(prof, (k_ntt_pass<F, NTT_E_BIG, true>), grid, dim3(NTT_E_BIG / NTT_EPT), lds, s, a);
+        else if (NE == NTT_E_BIG)
+            HALO_LAUNCH(prof, (k_ntt_pass<F, NTT_E_BIG, false>), grid, dim3(NTT_E_BIG / NTT_EPT), lds, s, a);
+        else if (full)
+            HALO_LAUNCH(prof, (k_ntt_pass<F, NTT_E, true>), grid, dim3(NTT_E / NTT_EPT), lds, s, a);
         else
-            HALO_LAUNCH(prof, (k_ntt_pass<F, NTT_E>), grid, dim3(NTT_E / NTT_EPT), lds, s, a);
+            HALO_LAUNCH(prof, (k_ntt_pass<F, NTT_E, false>), grid, dim3(NTT_E / NTT_EPT), lds, s, a);
         HALO_HIP(hipGetLastError());
         log_ns += lr;
     }
