@@ -131,12 +131,19 @@ HALO_DEV XYZZ<F> xyzz_dbl_quad(const XYZZ<F>& p) {
     r.ZZZ = qperm<qp(2, 2, 2, 2)>(t3);
     return r;
 }
-// p + q as xyzz_add_quad, valid in the quad's lane 2 only, with the trivial cases done inside the quad:
-// an identity operand (idp / idq, quad-uniform) yields the other operand, reassembled in lane 2 by DPP
-// quad broadcasts from the coordinates the quad fetched anyway (role 0: p.X, q.ZZ; 1: q.X, p.ZZ;
-// 2: p.Y, q.ZZZ; 3: q.Y, p.ZZZ) -- no lane gathers, so a tree level can leave its sums in place.
+// p + q as xyzz_add_quad, valid in the quad's lane 2 only, for the tree levels below:
+//  * an identity operand (idp / idq, quad-uniform) yields the other operand, reassembled in lane 2 by
+//    DPP quad broadcasts from the coordinates the quad fetched anyway (role 0: p.X, q.ZZ; 1: q.X, p.ZZ;
+//    2: p.Y, q.ZZZ; 3: q.Y, p.ZZZ) -- no lane gathers, so a level can leave its sums in place; two
+//    identities give q, the identity;
+//  * lazy coordinates: X3 = RR - PPP - 2Q + 6p stays in (0, 8p) and Y3 in (0, 4p) (normalized limbs,
+//    valid multiplication operands: the products here stay below 40 p^2 < p 2^261), so the two
+//    conditional-subtraction chains per addition go; wave_group_sum reduces its result once.
+// Operands may be lazy the same way (the previous level's sums).
+// live: the quad's addition exists (a tree level's last batch may have idle quads; their r is left
+// undefined, and they neither force the multiplications nor the identity path).
 template <class F>
-HALO_DEV XYZZ<F> xyzz_add_quad_lane2(const XYZZ<F>& v, uint32_t s1, uint32_t s2, bool idp, bool idq) {
+HALO_DEV XYZZ<F> xyzz_add_quad_lane2(const XYZZ<F>& v, uint32_t s1, uint32_t s2, bool idp, bool idq, bool live) {
     const uint32_t role = threadIdx.x & 3u;
     const uint32_t odd = (role & 1u) ? ~0u : 0u, lo = role < 2 ? ~0u : 0u, r2 = role == 2 ? ~0u : 0u;
     const uint32_t sa = (role & 1u) ? s2 : s1, sb = (role & 1u) ? s1 : s2;
@@ -148,8 +155,8 @@ HALO_DEV XYZZ<F> xyzz_add_quad_lane2(const XYZZ<F>& v, uint32_t s1, uint32_t s2,
         a.v[l] = (x & lo) | (y & ~lo);
         b.v[l] = (zz & lo) | (zzz & ~lo);
     }
-    XYZZ<F> r = xyzz_id<F>();
-    if (!__all(idp || idq)) {
+    XYZZ<F> r;
+    if (!__all(!live || idp || idq)) {
         const Fe<F> t1 = fe_mul(a, b);
         constexpr int SWAP = qp(1, 0, 3, 2);
         const Fe<F> t1s = qperm<SWAP>(t1), bs = qperm<SWAP>(b);
@@ -158,12 +165,12 @@ HALO_DEV XYZZ<F> xyzz_add_quad_lane2(const XYZZ<F>& v, uint32_t s1, uint32_t s2,
         const Fe<F> PPb = qperm<qp(0, 0, 0, 0)>(t2), Ab = qperm<qp(0, 1, 1, 3)>(t2);
         const Fe<F> t3 = fe_mul(pick(lo, pick(odd, d, t1), Ab), PPb);
         const Fe<F> Bb = qperm<qp(0, 3, 2, 3)>(t2), Qb = qperm<qp(0, 1, 0, 3)>(t3), PPPb = qperm<qp(1, 1, 1, 1)>(t3);
-        r.X = fe_reduce_8p(fe_sub_k<6>(t2, fe_add_nc(PPPb, fe_add_nc(Qb, Qb))));
-        const Fe<F> t4 = fe_mul(pick(lo, Bb, pick(odd, t1s, d)), pick(r2, fe_sub_k<2>(Qb, r.X), PPPb));
-        r.Y = fe_sub(t4, qperm<qp(0, 1, 3, 3)>(t4));
+        r.X = fe_sub_k<6>(t2, fe_add_nc(PPPb, fe_add_nc(Qb, Qb)));  // (lane 2: t2 = RR) in (0, 8p)
+        const Fe<F> t4 = fe_mul(pick(lo, Bb, pick(odd, t1s, d)), pick(r2, fe_sub_k<8>(Qb, r.X), PPPb));
+        r.Y = fe_sub_k<2>(t4, qperm<qp(0, 1, 3, 3)>(t4));  // in (0, 4p)
         r.ZZ = t3;
         r.ZZZ = qperm<qp(0, 1, 1, 3)>(t4);
-        const bool exc = role == 2 && !idp && !idq && fe_is_zero(t3);
+        const bool exc = live && role == 2 && !idp && !idq && fe_is_zero(t3);
         if (__any(exc)) {  // P == +-Q: doubling or the identity (rare)
             XYZZ<F> p;
             p.X = qperm<qp(0, 0, 0, 0)>(a);
@@ -173,7 +180,7 @@ HALO_DEV XYZZ<F> xyzz_add_quad_lane2(const XYZZ<F>& v, uint32_t s1, uint32_t s2,
             if (exc) r = fe_is_zero_4p(d) ? xyzz_dbl(p) : xyzz_id<F>();
         }
     }
-    if (__any(idp != idq)) {  // one identity operand: the other one (wave-uniform branch: every lane
+    if (__any(live && (idp || idq))) {  // an identity operand: the other one (wave-uniform branch: every lane
                               // takes part in the broadcasts, the choice is a per-lane pick)
         const uint32_t mq = idp ? ~0u : 0u;
         XYZZ<F> o;
@@ -181,9 +188,8 @@ HALO_DEV XYZZ<F> xyzz_add_quad_lane2(const XYZZ<F>& v, uint32_t s1, uint32_t s2,
         o.Y = pick(mq, qperm<qp(3, 3, 3, 3)>(a), qperm<qp(2, 2, 2, 2)>(a));
         o.ZZ = pick(mq, qperm<qp(0, 0, 0, 0)>(b), qperm<qp(1, 1, 1, 1)>(b));
         o.ZZZ = pick(mq, qperm<qp(2, 2, 2, 2)>(b), qperm<qp(3, 3, 3, 3)>(b));
-        if (idp != idq) r = o;
+        if (idp || idq) r = o;
     }
-    if (idp && idq) r = xyzz_id<F>();
     return r;
 }
 
@@ -208,8 +214,7 @@ HALO_DEV XYZZ<F> wave_group_sum(XYZZ<F> v, uint32_t G) {
             const uint32_t e1 = (a / m) * gs + a % m, e2 = e1 + m;
             const uint32_t s1 = where(e1), s2 = where(e2);
             const uint32_t fp = __shfl(idv, (int)s1), fq = __shfl(idv, (int)s2);
-            const bool idp = a >= nadd || fp != 0u, idq = a >= nadd || fq != 0u;
-            const XYZZ<F> r = xyzz_add_quad_lane2(v, s1, s2, idp, idq);
+            const XYZZ<F> r = xyzz_add_quad_lane2(v, s1, s2, fp != 0u, fq != 0u, a < nadd);
             if (b == 0) {
                 nxt = r;
             } else {  // batch 1's sums to lane 0 of their quads
@@ -223,6 +228,8 @@ HALO_DEV XYZZ<F> wave_group_sum(XYZZ<F> v, uint32_t G) {
         placed = true;
     }
     if (!placed) return v;
+    v.X = fe_reduce_8p(v.X);  // the lazy coordinates of xyzz_add_quad_lane2, reduced once
+    v.Y = fe_reduce_2p(v.Y);
     if (G == 64) {  // element 0 (lane 2) to its quad
         XYZZ<F> r;
         r.X = qperm<qp(2, 2, 2, 2)>(v.X);
