@@ -854,7 +854,7 @@ def main():
     if ntt_main is not None:
         ntt_main["compute_roofline"] = compute_roofline(
             "ntt_pass", ntt_main.get("pass_kernel_avg_ms"), None, pmc, pmc_ok and args.ntt_logn == 22,
-            "k_ntt_pass<Fp, 2048> (the 11-bit Stockham pass, 4 per pair) over its mean launch time in the pair loop")
+            "k_ntt_pass<Fp, 2048, full blocks> (the 11-bit Stockham pass, 4 per pair) over its mean launch time in the pair loop")
 
     line = {
         "metric": "MSM points/sec (Pippenger, Pallas, 2^20 points, resident SRS)",

@@ -2,7 +2,7 @@
 
 usage: python3 tools/pmc_valu_merge.py <acc_dir> <ntt_dir> <pmc_summary.json>
 
-Per kernel key (msm_acc: k_acc<PallasCurve> of the headline; ntt_pass: k_ntt_pass<FpCfg, 2048> of the
+Per kernel key (msm_acc: k_acc<PallasCurve> of the headline; ntt_pass: k_ntt_pass<FpCfg, 2048, true> (full blocks) of the
 2^22 pair) it stores, per dispatch: SQ_INSTS_VALU, SQ_INSTS_VALU_INT64, SQ_INSTS_VALU_INT32, SQ_WAVES
 (wave-instructions), and the kernel's static class counts from tools/valu_mix.py, which split the
 dynamic INT64 count into multiply-adds and other 64-bit ops and the INT32 count into VOP3 and
@@ -19,7 +19,7 @@ from pmc_summary import load, summarise  # noqa: E402
 import valu_mix  # noqa: E402
 
 KERNELS = {"msm_acc": ("acc", "k_acc<halo::PallasCurve>", "5k_accINS_11PallasCurve"),
-           "ntt_pass": ("ntt", "k_ntt_pass<halo::FpCfg, 2048>", "k_ntt_passINS_5FpCfgELi2048")}
+           "ntt_pass": ("ntt", "k_ntt_pass<halo::FpCfg, 2048, true>", "k_ntt_passINS_5FpCfgELi2048ELb1E")}
 
 
 def main():
