@@ -118,7 +118,9 @@ __global__ __launch_bounds__(256) void k_merge(const uint32_t* bstart, const uin
 //    sums, depth ~12); k_bitcombine: lane k doubles its term (<= log B times), then a tree sum.
 //    ~2.1 B adds in total at depth ~40 (a running-sum reduction needs 2 B adds at depth 2 B / #threads).
 // ---------------------------------------------------------------------------------------------
-// grid (ceil(H / (256 / L)) + L, SW), 256 threads
+// grid (ceil(H / (256 / L)) + (H <= 64 ? ceil(L / 4) : L), SW), 256 threads.  Columns of at most 64
+// buckets (c <= 15: the 2^16 SRS's MSMs) take one wave each, four to a block: a block per column left
+// three idle waves per block and 2.5 waves per SIMD over the pair MSM's 640 blocks (80 us per launch).
 template <class Cv>
 __global__ __launch_bounds__(256) void k_rowcol(const uint4* bucket_sums, uint32_t L, uint32_t H, uint4* rows,
                                                 uint4* cols) {
@@ -136,6 +138,12 @@ __global__ __launch_bounds__(256) void k_rowcol(const uint4* bucket_sums, uint32
         // tree over the L lanes of each row (rows are contiguous groups of L threads)
         v = block_group_sum<F>(v, L, red);
         if (l == 0 && h < H) xyzz_store(rows + 8 * ((size_t)w * H + h), v);
+    } else if (H <= 64) {  // short columns: one per wave, four per block (block-uniform branch)
+        const uint32_t l = (blockIdx.x - nrb) * 4 + (tid >> 6), h = tid & 63u;
+        XYZZ<F> v = xyzz_id<F>();
+        if (l < L && h < H) v = xyzz_load<F>(bs + 8 * ((size_t)h * L + l));
+        v = wave_group_sum<F>(v, 64);
+        if (h == 0 && l < L) xyzz_store(cols + 8 * ((size_t)w * L + l), v);
     } else {
         const uint32_t l = blockIdx.x - nrb;
         XYZZ<F> acc = xyzz_id<F>();
@@ -323,7 +331,8 @@ static int tail_launch_t(const MsmTailArgs& a, hipStream_t ts) {
             return HALO_OK;
         }
         const uint32_t nrb = (a.H + (256 / a.L) - 1) / (256 / a.L);
-        hipLaunchKernelGGL(k_rowcol<Cv>, dim3(nrb + a.L, a.SW), dim3(256), 0, ts, (const uint4*)a.bucket_sums, a.L,
+        const uint32_t ncb = a.H <= 64 ? (a.L + 3) / 4 : a.L;
+        hipLaunchKernelGGL(k_rowcol<Cv>, dim3(nrb + ncb, a.SW), dim3(256), 0, ts, (const uint4*)a.bucket_sums, a.L,
                            a.H, a.rows, a.cols);
         hipLaunchKernelGGL(k_bitterms<Cv>, dim3(a.NT, a.SW), dim3(256), 0, ts, (const uint4*)a.rows,
                            (const uint4*)a.cols, a.H, a.L, a.logH, a.terms);

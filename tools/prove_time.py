@@ -15,7 +15,10 @@ for arg in (sys.argv[1:] or ['16', '20']):
     for curve in ('pallas',):
         cid = H.CURVES[curve]
         H.check(L.halo_srs_synthesize(cid, n, 99))
-        H.check(L.halo_srs_precompute_windows(cid))
+        if os.environ.get("SHIFT_C"):  # A/B: window width of the shifted SRS copies (0 = the library default)
+            H.check(L.halo_srs_precompute_window_range(cid, int(os.environ["SHIFT_C"]), 0, 0))
+        else:
+            H.check(L.halo_srs_precompute_windows(cid))
         B = prover.DeviceBackend(curve)
         wit = prover.synthetic_witness(B, n, seed=1)
         B.sync()
