@@ -1043,6 +1043,26 @@ __global__ __launch_bounds__(256) void k_weighted_prep(const uint4* cs, const ui
     }
 }
 
+// The dot blocks of k_weighted_prep alone (no scalars), as a MsmPreHide hook of the pair MSM
+struct WeightedDots {
+    const uint4 *cs, *zs;
+    size_t m;
+    uint4* part;
+    uint32_t* ctr;
+    const uint4* xi0;
+    uint4* dots;
+    uint32_t ndot;
+    int curve;
+};
+static void weighted_dots_launch(hipStream_t ts, void* ctx) {
+    const WeightedDots& d = *(const WeightedDots*)ctx;
+    DISPATCH_CURVE(d.curve, Cv, {
+        hipLaunchKernelGGL(k_weighted_prep<typename Cv::Scalar>, dim3(d.ndot), dim3(256), 0, ts, d.cs, d.zs,
+                           (const uint4*)nullptr, d.m, 0, (size_t)0, (uint4*)nullptr, (uint4*)nullptr, d.part, d.ctr,
+                           d.xi0, d.dots, d.ndot);
+    });
+}
+
 }  // namespace halo
 
 using namespace halo;
@@ -2281,7 +2301,9 @@ static int ipa_round_launch(DeviceState* st, halo_ipa_session* ses) {
         return HALO_OK;
     }
     if (ses->weighted) {
-        // the round's weighted scalars and its two dots (scaled by xi_0) in one launch
+        // the round's weighted scalars (k_weighted_prep without its dot blocks) on s, and in the pair path
+        // its two dots (scaled by xi_0) on the MSM's tail stream just before the hiding terms that read
+        // them (MsmPreHide), beside the digit / sort / accumulation phase
         const size_t half = ses->n0 / 2;  // = wlen * m terms per side
         const uint32_t lgm = ilog2(m);
         const char* sl = cs + m * 32;     // round 0 (w = [1]): the scalars are c_r, c_l themselves
@@ -2289,14 +2311,18 @@ static int ipa_round_launch(DeviceState* st, halo_ipa_session* ses) {
         char* sb = (char*)ses->scal.ptr;
         const unsigned nbk = gridn(half, 256), ndot = std::min(nbk, 256u);
         HALO_CHECK(ses->tmp.reserve((size_t)ndot * 64));
-        DISPATCH_CURVE(ses->curve, Cv, {
-            hipLaunchKernelGGL(k_weighted_prep<typename Cv::Scalar>, dim3(nbk), dim3(256), 0, s, (const uint4*)cs,
-                               (const uint4*)zs, ses->w[ses->wcur].as<const uint4>(), m, (int)lgm, half,
-                               ses->wlen > 1 ? (uint4*)sb : nullptr, (uint4*)(sb + half * 32), ses->tmp.as<uint4>(),
-                               (uint32_t*)(sm + SM_CTR + 8), ses->xi_mode ? (const uint4*)(sm + 192) : nullptr,
-                               (uint4*)(sm + 128), ndot);
-        });
-        HALO_HIP(hipGetLastError());
+        const bool pair = half <= (size_t)tuning(TUNE_IPA_PAIR_MAX);
+        WeightedDots wd{(const uint4*)cs, (const uint4*)zs, m, ses->tmp.as<uint4>(), (uint32_t*)(sm + SM_CTR + 8),
+                        ses->xi_mode ? (const uint4*)(sm + 192) : nullptr, (uint4*)(sm + 128), ndot, ses->curve};
+        if (ses->wlen > 1 || !pair) {
+            DISPATCH_CURVE(ses->curve, Cv, {
+                hipLaunchKernelGGL(k_weighted_prep<typename Cv::Scalar>, dim3(ses->wlen > 1 ? nbk : ndot), dim3(256), 0,
+                                   s, (const uint4*)cs, (const uint4*)zs, ses->w[ses->wcur].as<const uint4>(), m,
+                                   (int)lgm, half, ses->wlen > 1 ? (uint4*)sb : nullptr, (uint4*)(sb + half * 32),
+                                   wd.part, wd.ctr, wd.xi0, wd.dots, pair ? 0u : ndot);
+            });
+            HALO_HIP(hipGetLastError());
+        }
         if (ses->wlen > 1) {
             sl = sb;
             sr = sb + half * 32;
@@ -2306,9 +2332,10 @@ static int ipa_round_launch(DeviceState* st, halo_ipa_session* ses) {
         // 2^14 / 2^17 / 2^18 / 2^19 / 2^20 ms, two MSMs vs one: 7.5 / 11.3 / 14.4 / 19.3 / 27.2 vs
         // 6.9 / 10.3 / 13.2 / 17.8 / 29.0 (round 4, after the sort and accumulation changes: 2^20
         // 21.7 vs 22.7 ms)
-        if (half <= (size_t)tuning(TUNE_IPA_PAIR_MAX)) {
+        if (pair) {
             const MsmPairIO io{sl, sr, sm + 128, sm + 160, sm + 512, sm + 640};
-            HALO_CHECK(msm_srs_pairs_device(st, ses->curve, 1, &io, half, lgm, ses->htab_ptr, s, hr));
+            const MsmPreHide pre{weighted_dots_launch, &wd};
+            HALO_CHECK(msm_srs_pairs_device(st, ses->curve, 1, &io, half, lgm, ses->htab_ptr, s, hr, &pre));
         } else if (ses->solo) {
             // L on the session stream and R on its second stream: the two MSMs' fronts, accumulations and
             // reduction tails overlap, instead of R's front waiting for L's accumulation (measured, 2^20

@@ -774,7 +774,7 @@ static int msm_multi_device_t(DeviceState* st, const void* const* scalars, const
 // ---------------------------------------------------------------------------------------------
 template <class Cv>
 static int msm_srs_pairs_t(DeviceState* st, size_t np, const MsmPairIO* io, size_t half, uint32_t lgm,
-                           const uint4* hide_table, hipStream_t s, hipEvent_t hide_ready) {
+                           const uint4* hide_table, hipStream_t s, hipEvent_t hide_ready, const MsmPreHide* pre_hide) {
     SrsState& srs = st->srs[curve_id<Cv>()];
     const size_t m = (size_t)1 << lgm;
     if (!srs.shifted_c) return set_error(HALO_EINVAL, "msm_srs_pairs: no window-shifted SRS");
@@ -816,6 +816,10 @@ static int msm_srs_pairs_t(DeviceState* st, size_t np, const MsmPairIO* io, size
     HALO_HIP(hipEventRecord(M.start, s));
     HALO_HIP(hipStreamWaitEvent(ts, M.start, 0));
     if (hide_ready) HALO_HIP(hipStreamWaitEvent(ts, hide_ready, 0));
+    if (pre_hide) {
+        pre_hide->fn(ts, pre_hide->ctx);
+        HALO_HIP(hipGetLastError());
+    }
     HideScalars hs{};
     PairOuts outs{};
     for (size_t q = 0; q < np; q++) {
@@ -885,10 +889,10 @@ static int msm_srs_pairs_t(DeviceState* st, size_t np, const MsmPairIO* io, size
 }
 
 int msm_srs_pairs_device(DeviceState* st, int curve, size_t np, const MsmPairIO* io, size_t half, uint32_t lgm,
-                         const void* hide_table, hipStream_t s, hipEvent_t hide_ready) {
+                         const void* hide_table, hipStream_t s, hipEvent_t hide_ready, const MsmPreHide* pre_hide) {
     int rc;
     DISPATCH_CURVE(curve, Cv, {
-        rc = msm_srs_pairs_t<Cv>(st, np, io, half, lgm, (const uint4*)hide_table, s, hide_ready);
+        rc = msm_srs_pairs_t<Cv>(st, np, io, half, lgm, (const uint4*)hide_table, s, hide_ready, pre_hide);
     });
     return rc;
 }

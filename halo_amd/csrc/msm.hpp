@@ -57,8 +57,15 @@ struct MsmPairIO {
     const void *sl, *sr, *hide_l, *hide_r;
     void *out_l, *out_r;
 };
+// pre_hide (optional): enqueued on the MSM's tail stream right before the hiding terms, after the MSM
+// start (the caller's prior work on s) -- the IPA's weighted rounds form the hiding terms' dots there,
+// beside the digit / sort / accumulation phase instead of ahead of it.
+struct MsmPreHide {
+    void (*fn)(hipStream_t ts, void* ctx);
+    void* ctx;
+};
 int msm_srs_pairs_device(DeviceState* st, int curve, size_t np, const MsmPairIO* io, size_t half, uint32_t lgm,
-                         const void* hide_table, hipStream_t s, hipEvent_t hide_ready);
+                         const void* hide_table, hipStream_t s, hipEvent_t hide_ready, const MsmPreHide* pre_hide = nullptr);
 // shift_stride > 0: bases are the resident window-shifted SRS (copy w = 2^(c_s w) G at w shift_stride):
 // every c_s-bit digit of w[u] is split into three unsigned sub-digits, so the final Horner runs
 // over three windows (~2 c_s / 3 doublings) instead of ~255 / c windows (~255 doublings).
