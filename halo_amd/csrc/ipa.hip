@@ -543,7 +543,8 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail_msm(const uint4* table, s
                                                             const uint32_t* hkw, uint4* out_xyzz,
                                                             uint32_t* host = nullptr, uint32_t seq = 0,
                                                             const uint4* plus_wrapped = nullptr,
-                                                            const uint4* copy_src = nullptr, uint4* copy_dst = nullptr) {
+                                                            const uint4* copy_src = nullptr, uint4* copy_dst = nullptr,
+                                                            uint32_t tpl = 1) {
     using F = typename Cv::Base;
     __shared__ uint4 red[TAIL_THREADS / 2 * 8];
     __shared__ uint32_t kw[10];
@@ -552,35 +553,39 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail_msm(const uint4* table, s
     const uint32_t bsd = mode == 0 ? (uint32_t)(blockIdx.x >= nbs) : 0u;
     const bool first = htab && blockIdx.x == bsd * nbs;
     if (first) acc = hiding_lane_term<Cv>(htab, dots_ark + 2 * bsd, hkw ? hkw + 10 * bsd : nullptr, kw);
-    uint32_t sd = 0;
-    size_t win = 0, k = 0;
-    bool valid;
-    if (mode == 0) {
-        sd = blockIdx.x >= nbs;
-        const size_t q = (size_t)(blockIdx.x - sd * nbs) * TAIL_THREADS + tid, hn = n0 / 2;
-        valid = q < (size_t)TAIL_WIN * hn;
-        win = q / hn;
-        const size_t r = q % hn, u = r / m, j = r % m;
-        k = j + u * 2 * m + sd * m;
-    } else {
-        const size_t t = (size_t)blockIdx.x * TAIL_THREADS + tid;
-        valid = t < (size_t)TAIL_WIN * n0;
-        win = t / n0;
-        k = t % n0;
-    }
-    if (valid) {
+    const uint32_t sd = bsd;
+    const size_t hn = n0 / 2, total = mode == 0 ? (size_t)TAIL_WIN * hn : (size_t)TAIL_WIN * n0;
+    const size_t q0 = (size_t)(blockIdx.x - sd * nbs) * TAIL_THREADS + tid, qstride = (size_t)nbs * TAIL_THREADS;
+    // term q of the side: mode 0 (win, u, j) at point k = j + u 2m + sd m; mode 1 t = win n0 + k
+    auto term = [&](size_t q) {
+        XYZZ<F> t = xyzz_id<F>();
+        if (q >= total) return t;
+        size_t win, k;
+        if (mode == 0) {
+            win = q / hn;
+            const size_t r = q % hn, u = r / m, j = r % m;
+            k = j + u * 2 * m + sd * m;
+        } else {
+            win = q / n0;
+            k = q % n0;
+        }
         constexpr uint32_t DPW = 32 / TAIL_DB;  // digits per scalar word
         const uint32_t half = (uint32_t)win / TAIL_TBL, bw = (uint32_t)win % TAIL_TBL;
         bool dneg;
         const uint32_t d = tail_digit(scal[8 * k + 4 * half + bw / DPW], bw, dneg);
         const uint32_t sk = side[k];
         if (d) {
-            XYZZ<F> t = xyzz_load<F>(table + tail_entry(bw, d, ld, k));
+            t = xyzz_load<F>(table + tail_entry(bw, d, ld, k));
             if (half) t.X = fe_mul(t.X, fe_from_const<F>(Cv::K::BETA));  // phi
             if ((((sk >> (1 + half)) & 1u) != 0) != dneg) t = xyzz_neg(t);
-            acc = first ? xyzz_add(acc, t) : t;
         }
-    }
+        return t;
+    };
+    // tpl = 2 (grids beyond one block per CU): each lane first adds its two terms, so the trees run at
+    // one wave per SIMD instead of two sharing a SIMD's issue slots
+    XYZZ<F> t = term(q0);
+    if (tpl == 2) t = xyzz_add(t, term(q0 + qstride));
+    acc = first ? xyzz_add(acc, t) : t;
     acc = block_group_sum<F>(acc, TAIL_THREADS, red);
     if (out_xyzz && nbs == 1) {
         if (tid == 0) {
@@ -2049,11 +2054,18 @@ static int ipa_enter_tail(DeviceState* st, halo_ipa_session* ses, hipStream_t s)
     return HALO_OK;
 }
 
+// k_tail_msm's terms per lane: 2 once a one-term grid would put more than one block on a CU (two waves
+// sharing a SIMD's issue slots through the whole tree): a lane's own addition of its two terms costs
+// less than the slower tree (opening 2^16, n0 = 2048: 512 blocks of one term or 256 of two)
+static uint32_t tail_terms_per_lane(const DeviceState* st, size_t blocks_one_term) {
+    return blocks_one_term > (size_t)st->num_cu ? 2u : 1u;
+}
+
 // mode 0: L, R of the current round (with their dot * H' terms) -> small[512..768) as XYZZ; the round's
 // scalars and dots come from k_tail_prep (one launch), the hiding terms ride in each side's first
 // k_tail_msm block, and k_tail_final runs only when a side spans several blocks.
 // mode 1: U = sum_u w[u] G0[u] -> small[256..384) as XYZZ (converted on the host).
-static int ipa_tail_sums(halo_ipa_session* ses, int mode, hipStream_t s, const void* copy_src = nullptr,
+static int ipa_tail_sums(const DeviceState* st, halo_ipa_session* ses, int mode, hipStream_t s, const void* copy_src = nullptr,
                          void* copy_dst = nullptr) {
     const size_t n0 = ses->n0, m = ses->m;
     char* sm = (char*)ses->small.ptr;
@@ -2096,7 +2108,9 @@ static int ipa_tail_sums(halo_ipa_session* ses, int mode, hipStream_t s, const v
                 hipLaunchKernelGGL(k_tail_round<Cv>, dim3(2 * ra.nbs + 2), dim3(TAIL_THREADS), 0, s, ra, f);
             });
         } else {  // k_tail_digits (the point scalars and the dots) + k_tail_msm + k_tail_final
-            const size_t nbs = (TAIL_WIN * (n0 / 2) + TAIL_THREADS - 1) / TAIL_THREADS, nblk = 2 * nbs;
+            const size_t nbs1 = (TAIL_WIN * (n0 / 2) + TAIL_THREADS - 1) / TAIL_THREADS;
+            const uint32_t tpl = tail_terms_per_lane(st, 2 * nbs1);
+            const size_t nbs = (TAIL_WIN * (n0 / 2) + TAIL_THREADS * tpl - 1) / (TAIL_THREADS * tpl), nblk = 2 * nbs;
             DISPATCH_CURVE(ses->curve, Cv, {
                 hipLaunchKernelGGL(k_tail_digits<Cv>, dim3(gridn(n0, 256) + 2), dim3(256), 0, s, ses->cs.as<const uint4>(),
                                    ses->zs.as<const uint4>(), ses->w[ses->wcur].as<const uint4>(), n0, m, f,
@@ -2105,7 +2119,8 @@ static int ipa_tail_sums(halo_ipa_session* ses, int mode, hipStream_t s, const v
                 hipLaunchKernelGGL(k_tail_msm<Cv>, dim3((unsigned)nblk), dim3(TAIL_THREADS), 0, s, ses->table, ses->table_ld,
                                    ses->scal.as<const uint32_t>(), ses->side.as<const uint8_t>(), n0, m, 0, (uint32_t)nbs,
                                    ses->part.as<uint4>(), (const uint4*)ses->htab_ptr, (const uint4*)(sm + 128),
-                                   (const uint32_t*)(sm + SM_HKW), (uint4*)(sm + 512), ra.host, ra.seq);
+                                   (const uint32_t*)(sm + SM_HKW), (uint4*)(sm + 512), ra.host, ra.seq, (const uint4*)nullptr,
+                                   (const uint4*)nullptr, (uint4*)nullptr, tpl);
                 if (nbs > 1)
                     hipLaunchKernelGGL(k_tail_final<Cv>, dim3(2), dim3(TAIL_THREADS), 0, s, ses->part.as<const uint4>(),
                                        (int)nblk, (const uint4*)nullptr, (const uint4*)nullptr, (uint4*)(sm + 512), 1,
@@ -2132,7 +2147,8 @@ static int ipa_tail_sums(halo_ipa_session* ses, int mode, hipStream_t s, const v
         HALO_HIP(hipGetLastError());
         ses->w_one_pending = false;
     }
-    const size_t nblk = (TAIL_WIN * n0 + TAIL_THREADS - 1) / TAIL_THREADS;
+    const uint32_t tpl = tail_terms_per_lane(st, (TAIL_WIN * n0 + TAIL_THREADS - 1) / TAIL_THREADS);
+    const size_t nblk = (TAIL_WIN * n0 + TAIL_THREADS * tpl - 1) / (TAIL_THREADS * tpl);
     uint4* out = (uint4*)(sm + 256);
     DISPATCH_CURVE(ses->curve, Cv, {
         hipLaunchKernelGGL(k_tail_scalars<Cv>, dim3(gridn(n0, 256)), dim3(256), 0, s, ses->cs.as<const uint4>(),
@@ -2141,7 +2157,7 @@ static int ipa_tail_sums(halo_ipa_session* ses, int mode, hipStream_t s, const v
         hipLaunchKernelGGL(k_tail_msm<Cv>, dim3((unsigned)nblk), dim3(TAIL_THREADS), 0, s, ses->table, ses->table_ld,
                            ses->scal.as<const uint32_t>(), ses->side.as<const uint8_t>(), n0, m, 1, (uint32_t)nblk,
                            ses->part.as<uint4>(), (const uint4*)nullptr, (const uint4*)nullptr, (const uint32_t*)nullptr,
-                           out, (uint32_t*)nullptr, 0u, (const uint4*)nullptr, (const uint4*)copy_src, (uint4*)copy_dst);
+                           out, (uint32_t*)nullptr, 0u, (const uint4*)nullptr, (const uint4*)copy_src, (uint4*)copy_dst, tpl);
         if (nblk > 1)
             hipLaunchKernelGGL(k_tail_final<Cv>, dim3(1), dim3(TAIL_THREADS), 0, s, ses->part.as<const uint4>(), (int)nblk,
                                (const uint4*)nullptr, (const uint4*)nullptr, out, 1, (uint32_t*)nullptr, 0u,
@@ -2297,7 +2313,7 @@ static int ipa_round_launch(DeviceState* st, halo_ipa_session* ses) {
     ses->htab_waited = true;
     if (ses->tail) {  // k_tail_prep forms the dots (scaled by xi_0) with the round's scalars
         if (hr) HALO_HIP(hipStreamWaitEvent(s, hr, 0));
-        HALO_CHECK(ipa_tail_sums(ses, 0, s));  // (L and R reach `pinned` from the kernels: no copy)
+        HALO_CHECK(ipa_tail_sums(st, ses, 0, s));  // (L and R reach `pinned` from the kernels: no copy)
         return HALO_OK;
     }
     if (ses->weighted) {
@@ -2596,7 +2612,7 @@ static int ipa_end_enqueue(DeviceState* st, halo_ipa_session* ses) {
             rc = set_error(HALO_EINVAL, "halo_ipa_end: U needs every round in the weighted / tail rounds (m = %zu)",
                            ses->m);
         else if (ses->tail)  // XYZZ at [256, 384), converted below; c = cs[0] copied to [384, 416) by its last block
-            rc = ipa_tail_sums(ses, 1, s, ses->cs.ptr, sm + 384);
+            rc = ipa_tail_sums(st, ses, 1, s, ses->cs.ptr, sm + 384);
         else
             rc = msm_srs_range_device(st, ses->curve, 0, ses->w[ses->wcur].ptr, ses->n0, nullptr, nullptr, sm + 256, s,
                                       false);
