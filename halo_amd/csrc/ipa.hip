@@ -1726,6 +1726,13 @@ static int ipa_eval_cs(halo_ipa_session* ses, size_t len, halo_fe_t* v_out) {
     return HALO_OK;
 }
 
+// k_tail_msm's terms per lane: 2 once a one-term grid would put more than one block on a CU (two waves
+// sharing a SIMD's issue slots through the whole tree): a lane's own addition of its two terms costs
+// less than the slower tree (opening 2^16, n0 = 2048: 512 blocks of one term or 256 of two)
+static uint32_t tail_terms_per_lane(const DeviceState* st, size_t blocks_one_term) {
+    return blocks_one_term > (size_t)st->num_cu ? 2u : 1u;
+}
+
 // ---------------------------------------------------------------------------------------------
 // pcdl::open_without_eval (pcdl.rs:326-392) with p, p_bar and p' kept in the session's buffers
 // (the hiding open used to download p_bar / p' and upload p, p_bar, p' between three
@@ -1744,7 +1751,8 @@ static int small_msm_scratch(DeviceState* st, int curve, size_t n, hipStream_t s
     SrsState& srs = st->srs[curve];
     const size_t nmax = std::min(srs_small_max(), srs.n);
     if (n < 1 || n > nmax) return set_error(HALO_EINVAL, "small SRS MSM: n (%zu) outside [1, %zu]", n, nmax);
-    *nblk = (TAIL_WIN * n + TAIL_THREADS - 1) / TAIL_THREADS;
+    const uint32_t tpl = tail_terms_per_lane(st, (TAIL_WIN * n + TAIL_THREADS - 1) / TAIL_THREADS);
+    *nblk = (TAIL_WIN * n + TAIL_THREADS * tpl - 1) / (TAIL_THREADS * tpl);
     *o_side = n * 32;
     *o_part = *o_side + ((n + 255) & ~(size_t)255);
     if (srs.small_ev) HALO_HIP(hipStreamWaitEvent(s, srs.small_ev, 0));  // the previous small MSM is done with small_scr
@@ -1764,12 +1772,13 @@ static int small_msm_sums(DeviceState* st, int curve, char* scr, size_t o_side, 
     SrsState& srs = st->srs[curve];
     DISPATCH_CURVE(curve, Cv, {
         const bool direct = out_xyzz && nblk == 1;
+        const uint32_t tpl = tail_terms_per_lane(st, (TAIL_WIN * n + TAIL_THREADS - 1) / TAIL_THREADS);
         hipLaunchKernelGGL(k_tail_msm<Cv>, dim3((unsigned)nblk), dim3(TAIL_THREADS), 0, s,
                            srs.small_tab->as<const uint4>(), srs.small_n0, (const uint32_t*)scr,
                            (const uint8_t*)(scr + o_side), n, (size_t)0, 1, (uint32_t)nblk, (uint4*)(scr + o_part),
                            hide_scalar ? srs.s_table.as<const uint4>() : (const uint4*)nullptr, (const uint4*)hide_scalar,
                            (const uint32_t*)nullptr, direct ? (uint4*)d_out : (uint4*)nullptr, (uint32_t*)nullptr, 0u,
-                           (const uint4*)plus_wrapped, (const uint4*)copy_src, (uint4*)copy_dst);
+                           (const uint4*)plus_wrapped, (const uint4*)copy_src, (uint4*)copy_dst, tpl);
         if (!direct)
             hipLaunchKernelGGL(k_tail_final<Cv>, dim3(1), dim3(TAIL_THREADS), 0, s, (const uint4*)(scr + o_part),
                                (int)nblk, (const uint4*)nullptr, (const uint4*)nullptr, (uint4*)d_out, (int)out_xyzz,
@@ -2052,13 +2061,6 @@ static int ipa_enter_tail(DeviceState* st, halo_ipa_session* ses, hipStream_t s)
     ses->wcur = 0;
     ses->tail = true;
     return HALO_OK;
-}
-
-// k_tail_msm's terms per lane: 2 once a one-term grid would put more than one block on a CU (two waves
-// sharing a SIMD's issue slots through the whole tree): a lane's own addition of its two terms costs
-// less than the slower tree (opening 2^16, n0 = 2048: 512 blocks of one term or 256 of two)
-static uint32_t tail_terms_per_lane(const DeviceState* st, size_t blocks_one_term) {
-    return blocks_one_term > (size_t)st->num_cu ? 2u : 1u;
 }
 
 // mode 0: L, R of the current round (with their dot * H' terms) -> small[512..768) as XYZZ; the round's
