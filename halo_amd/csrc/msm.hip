@@ -605,6 +605,7 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
     HALO_HIP(hipEventRecord(M.acc_done, s));
     HALO_HIP(hipStreamWaitEvent(ts, M.acc_done, 0));
     MsmTailArgs ta;
+    ta.num_cu = (uint32_t)st->num_cu;
     ta.n = n;
     ta.skeys = M.skeys;
     ta.scount = M.scount;
@@ -726,6 +727,7 @@ static int msm_multi_device_t(DeviceState* st, const void* const* scalars, const
         HALO_HIP(hipGetLastError());
     }
     MsmTailArgs ta;
+    ta.num_cu = (uint32_t)st->num_cu;
     ta.n = E;
     ta.skeys = skeys;
     ta.scount = scount;
@@ -849,6 +851,7 @@ static int msm_srs_pairs_t(DeviceState* st, size_t np, const MsmPairIO* io, size
         HALO_HIP(hipGetLastError());
     }
     MsmTailArgs ta;
+    ta.num_cu = (uint32_t)st->num_cu;
     ta.n = E;
     ta.skeys = skeys;
     ta.scount = scount;
@@ -1173,6 +1176,7 @@ static int msm_shared_batch_t(DeviceState* st, const uint4* bases, const uint4* 
                        P_first, P_last, S.bucket_sums.as<uint4>(), S.bstart.as<uint32_t>(), (uint32_t)NB, 31u, 0u, 1u);
     HALO_HIP(hipGetLastError());
     MsmTailArgs ta;
+    ta.num_cu = (uint32_t)st->num_cu;
     ta.n = T;
     ta.skeys = S.keys.as<const uint32_t>();
     ta.scount = tot + 1;

@@ -142,6 +142,7 @@ struct MsmTailArgs {
     int final_mode = 0;
     const uint4* final_hide = nullptr;
     uint4* final_out = nullptr;
+    uint32_t num_cu = 256;  // the device's CUs: sizes k_rowcol's entries per lane
 };
 int msm_tail_launch(int curve, const MsmTailArgs& a, hipStream_t ts);
 // Horner over W window sums (+ the hiding term) -> ark WrappedPoint, or packed XYZZ (xyzz_out)

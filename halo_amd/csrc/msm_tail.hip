@@ -118,38 +118,46 @@ __global__ __launch_bounds__(256) void k_merge(const uint32_t* bstart, const uin
 //    sums, depth ~12); k_bitcombine: lane k doubles its term (<= log B times), then a tree sum.
 //    ~2.1 B adds in total at depth ~40 (a running-sum reduction needs 2 B adds at depth 2 B / #threads).
 // ---------------------------------------------------------------------------------------------
-// grid (ceil(H / (256 / L)) + (H <= 64 ? ceil(L / 4) : L), SW), 256 threads.  Columns of at most 64
-// buckets (c <= 15: the 2^16 SRS's MSMs) take one wave each, four to a block: a block per column left
-// three idle waves per block and 2.5 waves per SIMD over the pair MSM's 640 blocks (80 us per launch).
+// grid (rowcol_blocks(L, H, epl).x, SW), 256 threads.  epl: entries per lane (1, 2 or 4; rowcol_epl) --
+// a lane first adds its epl entries of a row or column, then groups of L / epl (rows) or
+// min(256, H / epl) (columns) lanes sum them as one tree each, several rows / columns to a block.  The
+// launch is latency-bound: enough entries per lane keep it at one wave per SIMD (the 2^20 pair MSM's
+// 2 x 2^16 buckets as 1024 one-entry blocks put four waves on each SIMD; a block per short column left
+// three of its waves idle).
+struct RowcolShape {
+    uint32_t gr, rpb, nrb, gc, cpb, ncb;
+};
+__host__ __device__ __forceinline__ RowcolShape rowcol_shape(uint32_t L, uint32_t H, uint32_t epl) {
+    RowcolShape r;
+    r.gr = L / epl;
+    r.rpb = 256 / r.gr;
+    r.nrb = (H + r.rpb - 1) / r.rpb;
+    r.gc = H / epl < 256 ? H / epl : 256;
+    r.cpb = 256 / r.gc;
+    r.ncb = (L + r.cpb - 1) / r.cpb;
+    return r;
+}
 template <class Cv>
-__global__ __launch_bounds__(256) void k_rowcol(const uint4* bucket_sums, uint32_t L, uint32_t H, uint4* rows,
+__global__ __launch_bounds__(256) void k_rowcol(const uint4* bucket_sums, uint32_t L, uint32_t H, uint32_t epl, uint4* rows,
                                                 uint4* cols) {
     using F = typename Cv::Base;
     __shared__ uint4 red[128 * 8];
     const uint32_t w = blockIdx.y, tid = threadIdx.x;
-    const uint32_t B = L * H;
-    const uint4* bs = bucket_sums + 8 * (size_t)w * B;
-    const uint32_t rpb = 256 / L;  // rows per block
-    const uint32_t nrb = (H + rpb - 1) / rpb;
-    if (blockIdx.x < nrb) {  // (uniform per block)
-        const uint32_t h = blockIdx.x * rpb + tid / L, l = tid % L;
-        XYZZ<F> v = xyzz_id<F>();
-        if (h < H) v = xyzz_load<F>(bs + 8 * ((size_t)h * L + l));
-        // tree over the L lanes of each row (rows are contiguous groups of L threads)
-        v = block_group_sum<F>(v, L, red);
-        if (l == 0 && h < H) xyzz_store(rows + 8 * ((size_t)w * H + h), v);
-    } else if (H <= 64) {  // short columns: one per wave, four per block (block-uniform branch)
-        const uint32_t l = (blockIdx.x - nrb) * 4 + (tid >> 6), h = tid & 63u;
-        XYZZ<F> v = xyzz_id<F>();
-        if (l < L && h < H) v = xyzz_load<F>(bs + 8 * ((size_t)h * L + l));
-        v = wave_group_sum<F>(v, 64);
-        if (h == 0 && l < L) xyzz_store(cols + 8 * ((size_t)w * L + l), v);
-    } else {
-        const uint32_t l = blockIdx.x - nrb;
-        XYZZ<F> acc = xyzz_id<F>();
-        for (uint32_t h = tid; h < H; h += 256) acc = xyzz_add(acc, xyzz_load<F>(bs + 8 * ((size_t)h * L + l)));
-        acc = block_group_sum<F>(acc, 256, red);
-        if (tid == 0) xyzz_store(cols + 8 * ((size_t)w * L + l), acc);
+    const uint4* bs = bucket_sums + 8 * (size_t)w * L * H;
+    const RowcolShape sh = rowcol_shape(L, H, epl);
+    XYZZ<F> v = xyzz_id<F>();
+    if (blockIdx.x < sh.nrb) {  // (uniform per block) rows: groups of gr lanes
+        const uint32_t h = blockIdx.x * sh.rpb + tid / sh.gr, l0 = tid % sh.gr;
+        if (h < H)
+            for (uint32_t l = l0; l < L; l += sh.gr) v = xyzz_add(v, xyzz_load<F>(bs + 8 * ((size_t)h * L + l)));
+        v = block_group_sum<F>(v, sh.gr, red);
+        if (l0 == 0 && h < H) xyzz_store(rows + 8 * ((size_t)w * H + h), v);
+    } else {  // columns: groups of gc lanes
+        const uint32_t l = (blockIdx.x - sh.nrb) * sh.cpb + tid / sh.gc, h0 = tid % sh.gc;
+        if (l < L)
+            for (uint32_t h = h0; h < H; h += sh.gc) v = xyzz_add(v, xyzz_load<F>(bs + 8 * ((size_t)h * L + l)));
+        v = block_group_sum<F>(v, sh.gc, red);
+        if (h0 == 0 && l < L) xyzz_store(cols + 8 * ((size_t)w * L + l), v);
     }
 }
 
@@ -330,10 +338,16 @@ static int tail_launch_t(const MsmTailArgs& a, hipStream_t ts) {
             HALO_HIP(hipGetLastError());
             return HALO_OK;
         }
-        const uint32_t nrb = (a.H + (256 / a.L) - 1) / (256 / a.L);
-        const uint32_t ncb = a.H <= 64 ? (a.L + 3) / 4 : a.L;
-        hipLaunchKernelGGL(k_rowcol<Cv>, dim3(nrb + ncb, a.SW), dim3(256), 0, ts, (const uint4*)a.bucket_sums, a.L,
-                           a.H, a.rows, a.cols);
+        // entries per lane: the fewest (1, 2, 4) that keep the grid within one block per CU
+        uint32_t epl = 1;
+        while (epl < 4 && 2 * epl <= std::min(a.L, a.H)) {
+            const RowcolShape sh = rowcol_shape(a.L, a.H, epl);
+            if ((size_t)(sh.nrb + sh.ncb) * a.SW <= (size_t)a.num_cu) break;
+            epl *= 2;
+        }
+        const RowcolShape sh = rowcol_shape(a.L, a.H, epl);
+        hipLaunchKernelGGL(k_rowcol<Cv>, dim3(sh.nrb + sh.ncb, a.SW), dim3(256), 0, ts, (const uint4*)a.bucket_sums,
+                           a.L, a.H, epl, a.rows, a.cols);
         hipLaunchKernelGGL(k_bitterms<Cv>, dim3(a.NT, a.SW), dim3(256), 0, ts, (const uint4*)a.rows,
                            (const uint4*)a.cols, a.H, a.L, a.logH, a.terms);
         const int fin = a.SW == 1 ? a.final_mode : 0;
