@@ -102,6 +102,19 @@ __global__ void k_digits(const uint4* scalars, size_t n, int c, int W, uint32_t*
     });
 }
 
+// k_digits over up to 8 scalar vectors of one length n in one launch (blockIdx.y = vector p, digits at
+// digits + p SN): the pair MSMs' L and R sides, which took one launch each, one after the other
+struct DigitSrcs {
+    const uint4* s[8];
+};
+template <class S>
+__global__ void k_digits_multi(DigitSrcs src, size_t n, int c, int W, uint32_t* digits, size_t SN) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t* d = digits + (size_t)blockIdx.y * SN;
+    scalar_signed_digits<S>(src.s[blockIdx.y] + 2 * i, c, W, [&](int w, uint32_t out) { d[(size_t)w * n + i] = out; });
+}
+
 // GLV recoding (bases not window-shifted): s = k1 + lambda k2 with |k1|, |k2| < 2^128, so each
 // scalar gives W = ceil(129 / c) signed digits for point i (k1) and W for phi(G_i) (k2, entry
 // n + i): the same number of bucket additions as W = ceil(255 / c) digits of s, but the Horner
@@ -834,9 +847,10 @@ static int msm_srs_pairs_t(DeviceState* st, size_t np, const MsmPairIO* io, size
     HALO_HIP(hipGetLastError());
     HALO_HIP(hipEventRecord(M.front_done, ts));
     uint32_t* digits = M.digits.as<uint32_t>();
-    for (int p = 0; p < P; p++)
-        hipLaunchKernelGGL(k_digits<typename Cv::Scalar>, dim3(grid_for(half, 256)), dim3(256), 0, s,
-                           (const uint4*)(p & 1 ? io[p / 2].sr : io[p / 2].sl), half, c, W, digits + p * SN, half, 0, W);
+    DigitSrcs ds{};
+    for (int p = 0; p < P; p++) ds.s[p] = (const uint4*)(p & 1 ? io[p / 2].sr : io[p / 2].sl);
+    hipLaunchKernelGGL(k_digits_multi<typename Cv::Scalar>, dim3(grid_for(half, 256), P), dim3(256), 0, s, ds, half, c, W,
+                       digits, SN);
     HALO_HIP(hipGetLastError());
     uint32_t *skeys = nullptr, *svals = nullptr;
     const uint32_t* scount = nullptr;
