@@ -308,17 +308,6 @@ __global__ __launch_bounds__(256) void k_hide_terms(const uint4* hide_table, Hid
     hide_term_block<Cv>(hide_table, hs.sc[blockIdx.x], glv, hide_out + 8 * blockIdx.x);
 }
 
-// msm_srs_pairs' outputs: out[p] = window_sums[p] + hide[p], packed XYZZ
-struct PairOuts {
-    uint4* o[8];
-};
-template <class Cv>
-__global__ __launch_bounds__(64) void k_pairs_out(const uint4* window_sums, const uint4* hide, PairOuts outs, int P) {
-    using F = typename Cv::Base;
-    const int p = threadIdx.x;
-    if (p >= P) return;
-    xyzz_store(outs.o[p], xyzz_add(xyzz_load<F>(window_sums + 8 * p), xyzz_load<F>(hide + 8 * p)));
-}
 
 // ---------------------------------------------------------------------------------------------
 // SRS precomputation: window-shifted bases 2^(c w) G_i (w < W) and the hiding table 2^i S
@@ -836,7 +825,7 @@ static int msm_srs_pairs_t(DeviceState* st, size_t np, const MsmPairIO* io, size
         HALO_HIP(hipGetLastError());
     }
     HideScalars hs{};
-    PairOuts outs{};
+    MsmOuts8 outs{};
     for (size_t q = 0; q < np; q++) {
         hs.sc[2 * q] = (const uint4*)io[q].hide_l;
         hs.sc[2 * q + 1] = (const uint4*)io[q].hide_r;
@@ -894,10 +883,10 @@ static int msm_srs_pairs_t(DeviceState* st, size_t np, const MsmPairIO* io, size
     ta.hide_table = nullptr;
     ta.hide_scalar = nullptr;
     ta.out_wrapped = nullptr;
+    ta.pair_hide = hide_slot;  // k_bitcombine adds the hiding terms and writes the outputs
+    ta.pair_outs = outs;
+    HALO_HIP(hipStreamWaitEvent(s, M.front_done, 0));  // the hiding terms (done beside the front)
     HALO_CHECK(msm_tail_launch(curve_id<Cv>(), ta, s));
-    HALO_HIP(hipStreamWaitEvent(s, M.front_done, 0));  // the hiding terms
-    hipLaunchKernelGGL(k_pairs_out<Cv>, dim3(1), dim3(64), 0, s, M.window_sums.as<const uint4>(),
-                       (const uint4*)hide_slot, outs, P);
     HALO_HIP(hipGetLastError());
     HALO_HIP(hipEventRecord(M.tail_done, s));
     M.tail_pending = true;

@@ -123,6 +123,9 @@ int ntt_device_dispatch(DeviceState* st, int field, const void* d_in, void* d_ou
 constexpr uint32_t MSM_GROUP = 64;
 
 // Inputs of the MSM's reduction tail (msm_tail.hip), launched on the tail stream.
+struct MsmOuts8 {
+    uint4* o[8];
+};
 struct MsmTailArgs {
     size_t n, NB, E, ng1, ng2;
     const uint32_t* skeys;
@@ -143,6 +146,10 @@ struct MsmTailArgs {
     const uint4* final_hide = nullptr;
     uint4* final_out = nullptr;
     uint32_t num_cu = 256;  // the device's CUs: sizes k_rowcol's entries per lane
+    // pair MSMs (msm_srs_pairs): k_bitcombine's block w writes pair_outs.o[w] = its window sum +
+    // pair_hide[w] (packed XYZZ) instead of window_sums -- no separate output launch
+    const uint4* pair_hide = nullptr;
+    MsmOuts8 pair_outs{};
 };
 int msm_tail_launch(int curve, const MsmTailArgs& a, hipStream_t ts);
 // Horner over W window sums (+ the hiding term) -> ark WrappedPoint, or packed XYZZ (xyzz_out)

@@ -190,7 +190,8 @@ __global__ __launch_bounds__(256) void k_bitterms(const uint4* rows, const uint4
 // lone-wave launch fewer on the tail's critical path.
 template <class Cv>
 __global__ __launch_bounds__(64) void k_bitcombine(const uint4* terms, uint32_t NT, uint32_t logH, uint32_t logL,
-                                                   uint4* window_sums, int fin, const uint4* hide, uint4* out) {
+                                                   uint4* window_sums, int fin, const uint4* hide, uint4* out,
+                                                   const uint4* pair_hide, MsmOuts8 pair_outs) {
     using F = typename Cv::Base;
     const uint32_t w = blockIdx.x, k = threadIdx.x;
     XYZZ<F> v = xyzz_id<F>();
@@ -227,6 +228,10 @@ __global__ __launch_bounds__(64) void k_bitcombine(const uint4* terms, uint32_t 
         v = wave_group_sum<F>(v, G);
     }
     if (k != 0) return;
+    if (pair_hide) {  // a pair MSM's output w: + its hiding term (MsmTailArgs::pair_outs)
+        xyzz_store(pair_outs.o[w], xyzz_add(v, xyzz_load<F>(pair_hide + 8 * w)));
+        return;
+    }
     if (fin == 0) {
         xyzz_store(window_sums + 8 * w, v);
         return;
@@ -352,7 +357,7 @@ static int tail_launch_t(const MsmTailArgs& a, hipStream_t ts) {
                            (const uint4*)a.cols, a.H, a.L, a.logH, a.terms);
         const int fin = a.SW == 1 ? a.final_mode : 0;
         hipLaunchKernelGGL(k_bitcombine<Cv>, dim3(a.SW), dim3(64), 0, ts, (const uint4*)a.terms, a.NT, a.logH, a.logL,
-                           a.window_sums, fin, a.final_hide, a.final_out);
+                           a.window_sums, fin, a.final_hide, a.final_out, a.pair_hide, a.pair_outs);
     }
     HALO_HIP(hipGetLastError());
     return HALO_OK;
