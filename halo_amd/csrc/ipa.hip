@@ -2351,9 +2351,16 @@ static int ipa_round_launch(DeviceState* st, halo_ipa_session* ses) {
         // 6.9 / 10.3 / 13.2 / 17.8 / 29.0 (round 4, after the sort and accumulation changes: 2^20
         // 21.7 vs 22.7 ms)
         if (pair) {
+            // L and R reach `pinned` from k_bitcombine itself (polled, as the tail rounds): no copy
             const MsmPairIO io{sl, sr, sm + 128, sm + 160, sm + 512, sm + 640};
             const MsmPreHide pre{weighted_dots_launch, &wd};
-            HALO_CHECK(msm_srs_pairs_device(st, ses->curve, 1, &io, half, lgm, ses->htab_ptr, s, hr, &pre));
+            uint32_t seq = ++ses->poll_seq;
+            if (seq == 0) seq = ++ses->poll_seq;  // (0 is the flags' initial value)
+            HALO_CHECK(msm_srs_pairs_device(st, ses->curve, 1, &io, half, lgm, ses->htab_ptr, s, hr, &pre,
+                                            (uint32_t*)(ses->pinned + 256), seq));
+            HALO_CHECK(msm_join(st, s));
+            ses->poll_pending = true;
+            return HALO_OK;
         } else if (ses->solo) {
             // L on the session stream and R on its second stream: the two MSMs' fronts, accumulations and
             // reduction tails overlap, instead of R's front waiting for L's accumulation (measured, 2^20

@@ -778,7 +778,8 @@ static int msm_multi_device_t(DeviceState* st, const void* const* scalars, const
 // ---------------------------------------------------------------------------------------------
 template <class Cv>
 static int msm_srs_pairs_t(DeviceState* st, size_t np, const MsmPairIO* io, size_t half, uint32_t lgm,
-                           const uint4* hide_table, hipStream_t s, hipEvent_t hide_ready, const MsmPreHide* pre_hide) {
+                           const uint4* hide_table, hipStream_t s, hipEvent_t hide_ready, const MsmPreHide* pre_hide,
+                           uint32_t* host_emit, uint32_t seq) {
     SrsState& srs = st->srs[curve_id<Cv>()];
     const size_t m = (size_t)1 << lgm;
     if (!srs.shifted_c) return set_error(HALO_EINVAL, "msm_srs_pairs: no window-shifted SRS");
@@ -885,6 +886,10 @@ static int msm_srs_pairs_t(DeviceState* st, size_t np, const MsmPairIO* io, size
     ta.out_wrapped = nullptr;
     ta.pair_hide = hide_slot;  // k_bitcombine adds the hiding terms and writes the outputs
     ta.pair_outs = outs;
+    if (np == 1) {
+        ta.pair_host = host_emit;
+        ta.pair_seq = seq;
+    }
     HALO_HIP(hipStreamWaitEvent(s, M.front_done, 0));  // the hiding terms (done beside the front)
     HALO_CHECK(msm_tail_launch(curve_id<Cv>(), ta, s));
     HALO_HIP(hipGetLastError());
@@ -895,10 +900,12 @@ static int msm_srs_pairs_t(DeviceState* st, size_t np, const MsmPairIO* io, size
 }
 
 int msm_srs_pairs_device(DeviceState* st, int curve, size_t np, const MsmPairIO* io, size_t half, uint32_t lgm,
-                         const void* hide_table, hipStream_t s, hipEvent_t hide_ready, const MsmPreHide* pre_hide) {
+                         const void* hide_table, hipStream_t s, hipEvent_t hide_ready, const MsmPreHide* pre_hide,
+                         uint32_t* host_emit, uint32_t seq) {
     int rc;
     DISPATCH_CURVE(curve, Cv, {
-        rc = msm_srs_pairs_t<Cv>(st, np, io, half, lgm, (const uint4*)hide_table, s, hide_ready, pre_hide);
+        rc = msm_srs_pairs_t<Cv>(st, np, io, half, lgm, (const uint4*)hide_table, s, hide_ready, pre_hide, host_emit,
+                                 seq);
     });
     return rc;
 }

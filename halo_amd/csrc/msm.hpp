@@ -64,8 +64,10 @@ struct MsmPreHide {
     void (*fn)(hipStream_t ts, void* ctx);
     void* ctx;
 };
+// host_emit (np == 1 only): L and R also go to pinned host memory with flags = seq (MsmTailArgs::pair_host)
 int msm_srs_pairs_device(DeviceState* st, int curve, size_t np, const MsmPairIO* io, size_t half, uint32_t lgm,
-                         const void* hide_table, hipStream_t s, hipEvent_t hide_ready, const MsmPreHide* pre_hide = nullptr);
+                         const void* hide_table, hipStream_t s, hipEvent_t hide_ready, const MsmPreHide* pre_hide = nullptr,
+                         uint32_t* host_emit = nullptr, uint32_t seq = 0);
 // shift_stride > 0: bases are the resident window-shifted SRS (copy w = 2^(c_s w) G at w shift_stride):
 // every c_s-bit digit of w[u] is split into three unsigned sub-digits, so the final Horner runs
 // over three windows (~2 c_s / 3 doublings) instead of ~255 / c windows (~255 doublings).
@@ -150,6 +152,10 @@ struct MsmTailArgs {
     // pair_hide[w] (packed XYZZ) instead of window_sums -- no separate output launch
     const uint4* pair_hide = nullptr;
     MsmOuts8 pair_outs{};
+    // optional: outputs 0 and 1 also stored straight into pinned host memory (32 words each) with
+    // release flags = pair_seq at pair_host + 64 words (the IPA's polled L / R, as its tail rounds)
+    uint32_t* pair_host = nullptr;
+    uint32_t pair_seq = 0;
 };
 int msm_tail_launch(int curve, const MsmTailArgs& a, hipStream_t ts);
 // Horner over W window sums (+ the hiding term) -> ark WrappedPoint, or packed XYZZ (xyzz_out)

@@ -188,10 +188,25 @@ __global__ __launch_bounds__(256) void k_bitterms(const uint4* rows, const uint4
 // grid SW, 64 threads: S_w = T_0 + sum_j 2^(j + logL) U_j + sum_j 2^j V_j.  fin (SW == 1): lane 0 then
 // finishes the MSM as k_final would (+ hide, -> ark WrappedPoint (1) or packed XYZZ (2)), one
 // lone-wave launch fewer on the tail's critical path.
+// XYZZ point -> 32 words of pinned host memory (system-scope stores), then its flag = seq (release)
+template <class F>
+__device__ __forceinline__ void pair_emit_host(uint32_t* host, uint32_t* flag, const XYZZ<F>& v, uint32_t seq) {
+    const Fe<F>* c[4] = {&v.X, &v.Y, &v.ZZ, &v.ZZZ};
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        uint32_t w[8];
+        fe_pack(*c[k], w);
+#pragma unroll
+        for (int i = 0; i < 8; i++) __hip_atomic_store(host + 8 * k + i, w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 template <class Cv>
 __global__ __launch_bounds__(64) void k_bitcombine(const uint4* terms, uint32_t NT, uint32_t logH, uint32_t logL,
                                                    uint4* window_sums, int fin, const uint4* hide, uint4* out,
-                                                   const uint4* pair_hide, MsmOuts8 pair_outs) {
+                                                   const uint4* pair_hide, MsmOuts8 pair_outs, uint32_t* pair_host,
+                                                   uint32_t pair_seq) {
     using F = typename Cv::Base;
     const uint32_t w = blockIdx.x, k = threadIdx.x;
     XYZZ<F> v = xyzz_id<F>();
@@ -229,7 +244,9 @@ __global__ __launch_bounds__(64) void k_bitcombine(const uint4* terms, uint32_t 
     }
     if (k != 0) return;
     if (pair_hide) {  // a pair MSM's output w: + its hiding term (MsmTailArgs::pair_outs)
-        xyzz_store(pair_outs.o[w], xyzz_add(v, xyzz_load<F>(pair_hide + 8 * w)));
+        const XYZZ<F> r = xyzz_add(v, xyzz_load<F>(pair_hide + 8 * w));
+        xyzz_store(pair_outs.o[w], r);
+        if (pair_host && w < 2) pair_emit_host(pair_host + 32 * w, pair_host + 64 + w, r, pair_seq);
         return;
     }
     if (fin == 0) {
@@ -357,7 +374,7 @@ static int tail_launch_t(const MsmTailArgs& a, hipStream_t ts) {
                            (const uint4*)a.cols, a.H, a.L, a.logH, a.terms);
         const int fin = a.SW == 1 ? a.final_mode : 0;
         hipLaunchKernelGGL(k_bitcombine<Cv>, dim3(a.SW), dim3(64), 0, ts, (const uint4*)a.terms, a.NT, a.logH, a.logL,
-                           a.window_sums, fin, a.final_hide, a.final_out, a.pair_hide, a.pair_outs);
+                           a.window_sums, fin, a.final_hide, a.final_out, a.pair_hide, a.pair_outs, a.pair_host, a.pair_seq);
     }
     HALO_HIP(hipGetLastError());
     return HALO_OK;
