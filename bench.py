@@ -106,6 +106,8 @@ def parse():
     ap.add_argument("--sizes", default="24", help="extra MSM / NTT sizes (log2, comma separated) under extra.sizes")
     ap.add_argument("--dist-ntt-logn", type=int, default=24, help="distributed single NTT size (N > 1 only; 0 = off)")
     ap.add_argument("--ipa", type=int, default=1, help="measure the 2^logn IPA opening (extra.ipa_open)")
+    ap.add_argument("--batch-ntt", type=int, default=1,
+                    help="the prover's 42 NTT(8n) at n = 2^20 split by transform over the ranks (extra.batch_ntt)")
     ap.add_argument("--dist-ipa", type=int, default=1, help="N > 1: the sharded 2^logn opening (extra.dist_ipa)")
     ap.add_argument("--prove", type=int, default=20, help="log2 n of the naive_prover pipeline (extra.prove; 0 = off)")
     ap.add_argument("--prove-cpu", type=int, default=16, help="log2 n of the prover's CPU-baseline comparison")
@@ -643,6 +645,7 @@ def main():
     ntt_main = measure_ntt(args.ntt_logn)
     ntt_main["workload"] += " (BASELINE.json configs[2])"
     sizes = {}
+    ntt24_keys = []
     size_checks = {}  # 2^lg MSM: (scalars[0] on the host, SRS seed, result), verified in the CPU leg
     for lg in [int(v) for v in args.sizes.split(",") if v.strip()]:
         e, a_ms, _, ok, lt, sc0, chk = measure_msm(lg, 4, 2, check_sync=False)
@@ -657,6 +660,8 @@ def main():
             "roofline_frac": MSM_BYTES_PER_POINT * (1 << lg) * world * 4 / e / 1e9 / HBM_PEAK_GBS,
         }
         sizes[f"ntt_2^{lg}"] = measure_ntt(lg, nrep=4)
+        if lg == 24:  # the 8-bit passes' kernel, priced like the 2^22 pair's (after the PMC load below)
+            ntt24_keys.append(f"ntt_2^{lg}")
         torch.cuda.empty_cache()
         if world > 1 and (world & (world - 1)) == 0:
             # BASELINE configs[4]: one 2^lg-point MSM partitioned across the ranks (strong scaling)
@@ -707,6 +712,83 @@ def main():
         }
         del xl, y, z
 
+    # ---- the prover's NTTs sharded by transform: round 0 of the 2^20
+    # naive_prover evaluates 42 polynomials of degree < 2^20 over the 8n = 2^23 domain (protocol.rs:88-106),
+    # independent transforms, so rank r takes transforms r, r + P, ... with no exchange at all
+    # (halo_ntt_dev_zero_tail, one batched call per rank).  Strong scaling over the fixed 42 transforms;
+    # measured at every N (N = 1: all 42 on one GPU), beside the four-step dist_ntt
+    def measure_batch_ntt(lg=23, lg_nz=20, T=42, reps=3):
+        N_ = 1 << lg
+        mine = [t for t in range(T) if t % world == rank]
+        x0 = torch.zeros((len(mine), N_, 4), dtype=torch.int64, device="cuda")
+        for i, t in enumerate(mine):  # transform t's coefficients depend on t only (any rank can recompute it)
+            gt = torch.Generator(device="cuda")
+            gt.manual_seed(7000 + t)
+            x0[i, :1 << lg_nz] = torch.randint(-(2**63), 2**63 - 1, (1 << lg_nz, 4), dtype=torch.int64, device="cuda",
+                                               generator=gt)
+        x0[:, :, 3] &= 0x0FFFFFFFFFFFFFFF
+        x = torch.empty_like(x0)
+        xp = ctypes.c_void_p(x.data_ptr())
+        best = None
+        for rep in range(reps + 1):  # (the first call builds the twiddle tables: untimed)
+            x.copy_(x0)
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            a0 = time.perf_counter()
+            if mine:
+                H.check(L.halo_ntt_dev_zero_tail(H.FP, xp, lg, len(mine), 1 << lg_nz, sp))
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            dt = time.perf_counter() - a0
+            if world > 1:
+                tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+                dt = float(tt.item())
+            if rep and (best is None or dt < best):
+                best = dt
+        wts = (torch.arange(N_ * 4, device="cuda", dtype=torch.int64) % 1009 + 1).view(N_, 4)
+
+        def digest(y):  # per transform: an integer weighted sum (exact, order-free mod 2^64)
+            return torch.stack([(y[i] * wts).sum() for i in range(y.shape[0])])
+
+        dig = torch.zeros(T, dtype=torch.int64, device="cuda")
+        if mine:
+            dig[mine] = digest(x)
+        # round trip: the inverse transforms give back the coefficients (and the zero tail)
+        if mine:
+            H.check(L.halo_ntt_dev(H.FP, xp, lg, len(mine), 1, sp))
+        torch.cuda.synchronize()
+        ok = torch.tensor([int(torch.equal(x, x0))], device="cuda")
+        matches = None
+        if world > 1:
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            dist.all_reduce(dig, op=dist.ReduceOp.SUM)  # each transform's digest from its owner (others add 0)
+            if rank == 0:  # rank 0 recomputes every transform alone (the one-GPU result)
+                y = torch.zeros((1, N_, 4), dtype=torch.int64, device="cuda")
+                one = []
+                for t in range(T):
+                    gt = torch.Generator(device="cuda")
+                    gt.manual_seed(7000 + t)
+                    y.zero_()
+                    y[0, :1 << lg_nz] = torch.randint(-(2**63), 2**63 - 1, (1 << lg_nz, 4), dtype=torch.int64,
+                                                      device="cuda", generator=gt)
+                    y[0, :, 3] &= 0x0FFFFFFFFFFFFFFF
+                    H.check(L.halo_ntt_dev_zero_tail(H.FP, ctypes.c_void_p(y.data_ptr()), lg, 1, 1 << lg_nz, sp))
+                    one.append(digest(y)[0])
+                matches = bool(torch.equal(torch.stack(one), dig))
+                del y
+        del x, x0, wts
+        torch.cuda.empty_cache()
+        return {"workload": f"naive_prover round 0's {T} NTT(8n) at n = 2^{lg_nz} (zero-tail 2^{lg} transforms of "
+                            f"degree < 2^{lg_nz} polynomials, halo_ntt_dev_zero_tail) split by transform over {world} "
+                            f"rank(s), no exchange", "ms": best * 1e3, "transforms_per_s": T / best,
+                "transforms_on_rank0": len([t for t in range(T) if t % world == 0]), "scaling": "strong",
+                "roundtrip_bit_exact": bool(ok.item()), "matches_single_gpu": matches}
+
+    batch_ntt = measure_batch_ntt() if args.batch_ntt else None
+
     # ---- distributed IPA opening (strided shards, halo_amd.dist.sharded_ipa_rounds), N > 1 only:
     # every rank synthesizes the same 2^logn SRS and then keeps only its shard G[i P + r] resident (with
     # its window-shifted copies), so each shard runs the weighted rounds (GpuWeightedIpaOps); the
@@ -714,7 +796,8 @@ def main():
     dist_ipa = None
     if world > 1 and args.ipa and args.dist_ipa:
         from halo_amd import pcdl as PC
-        from halo_amd.dist import GpuWeightedIpaOps, sharded_ipa_rounds, torch_gather_arrays, torch_reduce_lr
+        from halo_amd.dist import (GpuWeightedIpaOps, sharded_ipa_rounds, torch_gather_arrays, torch_reduce_lr,
+                                   torch_reduce_lr_dev)
         from halo_amd.group import PublicParams
         n_ = 1 << args.logn
         H.check(L.halo_srs_synthesize(curve, n_, 777))
@@ -748,28 +831,40 @@ def main():
         shard = (np.ascontiguousarray(cs[rank::world]), z_ark)
         ops = GpuWeightedIpaOps(args.curve, rank, world)
         gather = torch_gather_arrays(dist, "cuda")
-        reduce_lr = torch_reduce_lr(dist, args.curve, "cuda")
-        best = None
-        for _ in range(3):
-            ks["k"] = 0
-            dist.barrier()
-            torch.cuda.synchronize()
-            a0 = time.perf_counter()
-            Ls, Rs, U, c0 = sharded_ipa_rounds([shard], hp, challenge, inverse, ops, world, gather, reduce_lr)
-            torch.cuda.synchronize()
-            tt = torch.tensor([time.perf_counter() - a0], dtype=torch.float64, device="cuda")
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            best = float(tt.item()) if best is None else min(best, float(tt.item()))
-        same = None
-        if rank == 0:
-            Ls1, Rs1, U1, c1 = ref
-            same = all(np.array_equal(a_, b_) for a_, b_ in zip(Ls + Rs + [U, c0], Ls1 + Rs1 + [U1, c1]))
+
+        def run_sharded(device_lr):
+            reduce_lr = (torch_reduce_lr_dev if device_lr else torch_reduce_lr)(dist, args.curve, "cuda")
+            best, res = None, None
+            for _ in range(3):
+                ks["k"] = 0
+                dist.barrier()
+                torch.cuda.synchronize()
+                a0 = time.perf_counter()
+                res = sharded_ipa_rounds([shard], hp, challenge, inverse, ops, world, gather, reduce_lr,
+                                         device_lr=device_lr)
+                torch.cuda.synchronize()
+                tt = torch.tensor([time.perf_counter() - a0], dtype=torch.float64, device="cuda")
+                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+                best = float(tt.item()) if best is None else min(best, float(tt.item()))
+            same = None
+            if rank == 0:
+                Ls, Rs, U, c0 = res
+                Ls1, Rs1, U1, c1 = ref
+                same = all(np.array_equal(a_, b_) for a_, b_ in zip(Ls + Rs + [U, c0], Ls1 + Rs1 + [U1, c1]))
+            return best, same
+
+        best_dev, same_dev = run_sharded(True)
+        best_host, same_host = run_sharded(False)
         dist_ipa = {
             "workload": f"pcdl open 2^{args.logn} sharded over {world} ranks (rank r: resident SRS shard G[r::P] "
-                        f"with window-shifted copies, weighted rounds; per-round RCCL all-gather of L_r, R_r "
-                        f"summed on the device; last lg P rounds collapsed)",
-            "open_ms": best * 1e3,
-            "matches_single_gpu": same,
+                        f"with window-shifted copies, weighted rounds; per round the ranks' L_r, R_r stay on the "
+                        f"device (halo_ipa_round_lr_dev), one RCCL all-gather, an XYZZ sum on the device and one "
+                        f"D2H for the transcript; last lg P rounds collapsed)",
+            "open_ms": best_dev * 1e3,
+            "matches_single_gpu": same_dev,
+            "host_pair_reduce": {"open_ms": best_host * 1e3, "matches_single_gpu": same_host,
+                                 "note": "round 5's reduce: each rank's pair through the host (D2H, affine, H2D) "
+                                         "before the gather, affine device sums"},
         }
         del G, cs
 
@@ -834,6 +929,19 @@ def main():
             "n": 1 << args.prove,
             "ms": {k: v * 1e3 for k, v in main_out["times"].items()},
         }
+        # the prover's kernels against their VALU-issue ceilings (tools/pmc_prove.sh: kernel statistics and
+        # VALU counters of the same 2^20 prove, stamped with the library hash; attached only for this build)
+        pv_path = os.path.join(ROOT, "profiles", "prove_valu.json")
+        if args.prove == 20 and os.path.exists(pv_path):
+            import hashlib
+            pv = json.load(open(pv_path))
+            if pv.get("library_sha256") == hashlib.sha256(open(H.LIB_PATH, "rb").read()).hexdigest():
+                prove["kernel_rooflines"] = {
+                    "source": "profiles/prove_valu.json (" + pv["source"] + ")",
+                    "kernels": {k: {f: e.get(f) for f in ("calls", "mean_us", "share", "ceiling_us", "compute_frac")}
+                                for k, e in pv["kernels"].items()}}
+            else:
+                prove["kernel_rooflines"] = {"note": "profiles/prove_valu.json was measured on another library build"}
         if not args.no_cpu:
             prove["verified"] = cpu_prove_check(L, H, curve, args.curve, 1 << args.prove, main_out)
         if not args.no_cpu and args.prove_cpu:
@@ -851,6 +959,10 @@ def main():
         "achieved": madds * 10 / (acc_avg_ms * 1e-3) if acc_avg_ms > 0 else None,
         "unit": "modmul/s", "note": "XYZZ mixed additions (8M + 2S, counted as 10) per launch over the live launch "
                                     "time (informational: not a ceiling)"}
+    for key in ntt24_keys:
+        sizes[key]["compute_roofline"] = compute_roofline(
+            "ntt_pass_1024", sizes[key].get("pass_kernel_avg_ms"), None, pmc, pmc_ok,
+            "k_ntt_pass<Fp, 1024, full blocks> (the 8-bit Stockham pass, 6 per 2^24 pair) over its mean launch time")
     if ntt_main is not None:
         ntt_main["compute_roofline"] = compute_roofline(
             "ntt_pass", ntt_main.get("pass_kernel_avg_ms"), None, pmc, pmc_ok and args.ntt_logn == 22,
@@ -905,6 +1017,7 @@ def main():
             "sizes": sizes,
             "dist_ntt": dist_ntt,
             "dist_ipa": dist_ipa,
+            "batch_ntt": batch_ntt,
             "ipa_open": ipa,
             "evals_op": evals,
             "hbm_copy": hbm_copy,

@@ -79,6 +79,8 @@ SIGNATURES = {
     "halo_srs_read": [ctypes.c_int, _sz, _sz, _vp],
     "halo_point_sum": [ctypes.c_int, _vp, _sz, _vp],
     "halo_point_sum_dev": [ctypes.c_int, _vp, _sz, _sz, _vp, _vp],
+    "halo_point_sum_xyzz_dev": [ctypes.c_int, _vp, _sz, _sz, _vp, _vp],
+    "halo_xyzz_to_wrapped": [ctypes.c_int, _vp, _sz, _vp],
     "halo_profile_enable": [ctypes.c_int],
     "halo_profile_read": [ctypes.c_char_p, ctypes.POINTER(_sz), ctypes.POINTER(ctypes.c_double)],
     "halo_profile_reset": [],
@@ -113,6 +115,7 @@ SIGNATURES = {
     "halo_ipa_begin_dev_xi": [ctypes.c_int, _vp, _sz, _vp, _vp, _vp, ctypes.POINTER(_vp)],
     "halo_ipa_round_lr_multi": [_vp, _sz, _vp, _vp],
     "halo_ipa_fold_multi": [_vp, _sz, _vp, _vp],
+    "halo_ipa_round_lr_dev": [_vp, _vp, _vp],
     "halo_ipa_begin_vectors": [ctypes.c_int, _vp, _vp, _vp, _sz, _vp, ctypes.POINTER(_vp)],
     "halo_pcdl_open_begin": [ctypes.c_int, _vp, _sz, _sz, _vp, _vp, ctypes.POINTER(_vp)],
     "halo_pcdl_open_blind": [_vp, _vp, _vp, _vp],

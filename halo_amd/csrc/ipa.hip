@@ -16,6 +16,7 @@
 //  * &Poly * &Poly (protocol.rs:132-139, pcdl.rs:215): NTT, pointwise product, iNTT, trim.
 #include <algorithm>
 #include <cstring>
+#include <unordered_set>
 #include <vector>
 
 #include <chrono>
@@ -1085,6 +1086,7 @@ struct halo_ipa_session {
     bool slots_reset = false;           // this opening restarted the MSM slot assignment (msm_slots_reset)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     hipEvent_t htab_ready = nullptr;  // recorded after the session's own 2^i H' table
+    hipEvent_t lr_ready = nullptr;    // halo_ipa_round_lr_dev: L, R copied out (created on first use)
     uint8_t* pinned = nullptr;  // [128, 192) xi|xi_inv (H2D), [256, 512) L|R XYZZ (D2H or tail_emit_host),
                                 // [512, 520) the L / R flags of tail_emit_host: coherent, several sessions in flight
     uint32_t poll_seq = 0;      // the last tail round's flag value (monotonic over the session object's life)
@@ -1157,6 +1159,8 @@ struct halo_ipa_session {
         if (s) (void)hipStreamSynchronize(s);
         if (s2) (void)hipStreamSynchronize(s2);
         if (htab_ready) (void)hipEventDestroy(htab_ready);
+        if (lr_ready) (void)hipEventDestroy(lr_ready);
+        lr_ready = nullptr;
         if (ev_fork) (void)hipEventDestroy(ev_fork);
         if (ev_join) (void)hipEventDestroy(ev_join);
         if (s) (void)hipStreamDestroy(s);
@@ -1180,6 +1184,19 @@ namespace {
 constexpr size_t IPA_POOL_MAX = 8;  // idle sessions kept per device
 std::mutex g_pool_mu;
 std::vector<halo_ipa_session*> g_pool;
+// every session object that exists (open or pooled), guarded by g_pool_mu: a handle is looked up here
+// before anything dereferences it, so a handle whose session was destroyed (the pool was full at its
+// end, or halo_shutdown ran) is refused instead of read after free
+std::unordered_set<const halo_ipa_session*> g_live;
+
+void ipa_destroy(halo_ipa_session* ses) {
+    {
+        std::lock_guard<std::mutex> g(g_pool_mu);
+        g_live.erase(ses);
+    }
+    ses->destroy();
+    delete ses;
+}
 
 // A session for the current device: from the pool, or new with its streams and pinned staging.
 halo_ipa_session* ipa_acquire(DeviceState* st) {
@@ -1196,14 +1213,17 @@ halo_ipa_session* ipa_acquire(DeviceState* st) {
     }
     auto* ses = new halo_ipa_session();
     ses->device = st->device;
+    {
+        std::lock_guard<std::mutex> g(g_pool_mu);
+        g_live.insert(ses);
+    }
     // one stream per session (a side stream for the H' table of explicit-H' sessions was measured: with
     // HIP's default 4 hardware queues it shares a queue with the MSM tail streams, ~0.3 ms per 2^16
     // round; the prover's and pcdl::open's sessions use the resident 2^i H tables and build none)
     if (hipStreamCreateWithFlags(&ses->s, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&ses->htab_ready, hipEventDisableTiming) != hipSuccess ||
         hipHostMalloc((void**)&ses->pinned, 1024, hipHostMallocCoherent) != hipSuccess) {
-        ses->destroy();
-        delete ses;
+        ipa_destroy(ses);
         set_error(HALO_EDEVICE, "halo_ipa_begin: stream / pinned buffer allocation failed");
         return nullptr;
     }
@@ -1214,10 +1234,12 @@ halo_ipa_session* ipa_acquire(DeviceState* st) {
     return ses;
 }
 
-// the handle is an open session (checked before anything touches its state)
+// the handle is an open session (checked before anything touches its state).  A
+// handle of a destroyed session, or of one idle in the pool, is refused; a pooled session handed to a
+// later opening is that opening's again, so a handle must not be used after its end (halo_gpu.h)
 bool ipa_is_open(const halo_ipa_session* ses) {
     std::lock_guard<std::mutex> g(g_pool_mu);
-    return ses && ses->in_use;
+    return ses && g_live.count(ses) && ses->in_use;
 }
 
 // Back to the pool once its stream is idle (the pinned staging is then free); beyond IPA_POOL_MAX
@@ -1228,7 +1250,7 @@ void ipa_release(halo_ipa_session* ses) {
         // a handle that is not open (a second end of the same handle) is neither touched nor pooled
         // twice: two later openings would otherwise share its streams and buffers
         std::lock_guard<std::mutex> g(g_pool_mu);
-        if (!ses->in_use) return;
+        if (!g_live.count(ses) || !ses->in_use) return;
         ses->in_use = false;
     }
     if (ses->s) (void)hipStreamSynchronize(ses->s);
@@ -1246,8 +1268,7 @@ void ipa_release(halo_ipa_session* ses) {
             return;
         }
     }
-    ses->destroy();
-    delete ses;
+    ipa_destroy(ses);
 }
 }  // namespace
 
@@ -1258,6 +1279,7 @@ void halo::ipa_shutdown() {
     (void)hipGetDevice(&cur);
     for (halo_ipa_session* ses : g_pool) {
         (void)hipSetDevice(ses->device);
+        g_live.erase(ses);
         ses->destroy();
         delete ses;
     }
@@ -2554,6 +2576,27 @@ extern "C" int halo_ipa_round_lr_multi(halo_ipa_session* const* ses, size_t k, h
     return HALO_OK;
 }
 
+// One round whose L and R stay on the device (the distributed opening's per-round reduce):
+// the round is enqueued as halo_ipa_round_lr enqueues it, L and R (packed XYZZ, 2 x 128 B) are copied to
+// d_lr on the session's stream, and `stream` is ordered after that copy.  No host wait: the caller
+// gathers and sums the ranks' pairs on the device (halo_point_sum_xyzz_dev) and brings one sum home.
+extern "C" int halo_ipa_round_lr_dev(halo_ipa_session* ses, void* d_lr, void* stream) {
+    clear_error();
+    if (!ses || !d_lr) return set_error(HALO_EINVAL, "halo_ipa_round_lr_dev: null argument");
+    DeviceState* st = current_state();
+    if (!st) return HALO_EDEVICE;
+    std::lock_guard<std::mutex> g(st->mu);
+    if (!ipa_is_open(ses)) return set_error(HALO_EINVAL, "halo_ipa_round_lr_dev: the session is not open");
+    ses->solo = true;
+    HALO_CHECK(ipa_round_launch(st, ses));
+    ses->poll_pending = false;  // (the copy a tail / pair round emits to the pinned staging is not waited for)
+    HALO_HIP(hipMemcpyAsync(d_lr, (char*)ses->small.ptr + 512, 256, hipMemcpyDeviceToDevice, ses->s));
+    if (!ses->lr_ready) HALO_HIP(hipEventCreateWithFlags(&ses->lr_ready, hipEventDisableTiming));
+    HALO_HIP(hipEventRecord(ses->lr_ready, ses->s));
+    HALO_HIP(hipStreamWaitEvent((hipStream_t)stream, ses->lr_ready, 0));
+    return HALO_OK;
+}
+
 extern "C" int halo_ipa_fold(halo_ipa_session* ses, const halo_fe_t* xi, const halo_fe_t* xi_inv) {
     clear_error();
     if (!ses || !xi) return set_error(HALO_EINVAL, "halo_ipa_fold: null argument");
@@ -2567,14 +2610,19 @@ extern "C" int halo_ipa_fold_multi(halo_ipa_session* const* ses, size_t k, const
     DeviceState* st = current_state();
     if (!st) return HALO_EDEVICE;
     std::lock_guard<std::mutex> g(st->mu);
+    // every session checked and every inverse formed before the first fold is enqueued: an argument
+    // error leaves all k sessions where they were (lockstep openings stay in step)
+    std::vector<halo_fe_t> inv(xi_inv ? 0 : k);
     for (size_t i = 0; i < k; i++) {
         if (!ses[i]) return set_error(HALO_EINVAL, "halo_ipa_fold_multi: null session %zu", i);
         if (!ipa_is_open(ses[i])) return set_error(HALO_EINVAL, "halo_ipa_fold_multi: session %zu is not open", i);
-        halo_fe_t inv;  // xi_inv == NULL: xi^-1 formed here, as the reference's fold does (pcdl.rs:430)
-        if (!xi_inv && !host_scalar_inverse(ses[i]->curve, &xi[i], &inv))
+        for (size_t j = 0; j < i; j++)
+            if (ses[j] == ses[i]) return set_error(HALO_EINVAL, "halo_ipa_fold_multi: session %zu listed twice", i);
+        // xi_inv == NULL: xi^-1 formed here, as the reference's fold does (pcdl.rs:430)
+        if (!xi_inv && !host_scalar_inverse(ses[i]->curve, &xi[i], &inv[i]))
             return set_error(HALO_EINVAL, "halo_ipa_fold_multi: xi %zu is zero (no inverse)", i);
-        HALO_CHECK(ipa_fold_launch(st, ses[i], &xi[i], xi_inv ? &xi_inv[i] : &inv));
     }
+    for (size_t i = 0; i < k; i++) HALO_CHECK(ipa_fold_launch(st, ses[i], &xi[i], xi_inv ? &xi_inv[i] : &inv[i]));
     // no host wait: the fold is stream-ordered before the next round (which synchronises), so the host
     // goes on to the transcript and the next round's launches while it runs
     return HALO_OK;

@@ -1639,6 +1639,24 @@ __global__ __launch_bounds__(256) void k_point_sum(const uint4* pts_wrapped, siz
     if (threadIdx.x == 0) aff_to_wrapped(out_wrapped, xyzz_to_aff(xyzz_load<F>(red)));
 }
 
+// Sum of k packed XYZZ points (stride_bytes apart) -> packed XYZZ (no affine conversion on the device)
+template <class Cv>
+__global__ __launch_bounds__(256) void k_point_sum_xyzz(const uint4* pts, size_t k, size_t stride_u4, uint4* out) {
+    using F = typename Cv::Base;
+    __shared__ uint4 red[256 * 8];
+    XYZZ<F> acc = xyzz_id<F>();
+    for (size_t i = threadIdx.x; i < k; i += 256) acc = xyzz_add(acc, xyzz_load<F>(pts + stride_u4 * i));
+    xyzz_store(red + 8 * threadIdx.x, acc);
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+        if ((int)threadIdx.x < off)
+            xyzz_store(red + 8 * threadIdx.x,
+                       xyzz_add(xyzz_load<F>(red + 8 * threadIdx.x), xyzz_load<F>(red + 8 * (threadIdx.x + off))));
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) xyzz_store(out, xyzz_load<F>(red));
+}
+
 }  // namespace halo
 
 static int check_curve(halo_curve_t c) {
@@ -1688,6 +1706,30 @@ extern "C" int halo_point_sum_dev(halo_curve_t curve, const void* d_pts, size_t 
         hipLaunchKernelGGL(k_point_sum<Cv>, dim3(1), dim3(256), 0, s, (const uint4*)d_pts, k, (uint4*)d_out);
     });
     HALO_HIP(hipGetLastError());
+    return HALO_OK;
+}
+
+extern "C" int halo_point_sum_xyzz_dev(halo_curve_t curve, const void* d_pts, size_t k, size_t stride_bytes, void* d_out,
+                                       void* stream) {
+    clear_error();
+    HALO_CHECK(check_curve(curve));
+    if (!d_out || (k && !d_pts)) return set_error(HALO_EINVAL, "halo_point_sum_xyzz_dev: null buffer");
+    if (stride_bytes < 128 || stride_bytes % 16)
+        return set_error(HALO_EINVAL, "halo_point_sum_xyzz_dev: stride %zu (a multiple of 16, at least 128)", stride_bytes);
+    hipStream_t s = (hipStream_t)stream;
+    DISPATCH_CURVE(curve, Cv, {
+        hipLaunchKernelGGL(k_point_sum_xyzz<Cv>, dim3(1), dim3(256), 0, s, (const uint4*)d_pts, k, stride_bytes / 16,
+                           (uint4*)d_out);
+    });
+    HALO_HIP(hipGetLastError());
+    return HALO_OK;
+}
+
+extern "C" int halo_xyzz_to_wrapped(halo_curve_t curve, const void* xyzz, size_t k, halo_wrapped_point_t* out) {
+    clear_error();
+    HALO_CHECK(check_curve(curve));
+    if (k && (!xyzz || !out)) return set_error(HALO_EINVAL, "halo_xyzz_to_wrapped: null buffer");
+    for (size_t i = 0; i < k; i++) host_xyzz_to_wrapped(curve, (const char*)xyzz + 128 * i, out + i);
     return HALO_OK;
 }
 

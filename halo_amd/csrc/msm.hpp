@@ -1,5 +1,6 @@
 // Internal interfaces shared between msm.hip, ipa.hip and the multi-GPU glue.
 #pragma once
+#include <vector>
 #include "runtime.hpp"
 
 namespace halo {
@@ -118,8 +119,11 @@ bool host_scalar_inverse(int curve, const void* x_ark, void* out_ark);
 void host_xyzz_to_wrapped2(int curve, const void* const* xyzz, void* const* wrapped, int k);
 int convert_wrapped_to_internal(int curve, const void* in, void* out, size_t n, hipStream_t s);
 int convert_internal_to_wrapped(int curve, const void* in, void* out, size_t n, hipStream_t s);
+// rad: the pass split to launch (null: ntt_radices(logn)); a caller that sized anything by the split
+// (the zero-tail prune) passes the vector it used
 int ntt_device_dispatch(DeviceState* st, int field, const void* d_in, void* d_out, void* d_tmp, unsigned logn,
-                        size_t batch, int inverse, hipStream_t s, void* d_tmp2 = nullptr, unsigned prune = 0);
+                        size_t batch, int inverse, hipStream_t s, void* d_tmp2 = nullptr, unsigned prune = 0,
+                        const std::vector<unsigned>* rad = nullptr);
 
 // chunk-partial group size of the skew guard (msm_tail.hip k_group_sums)
 constexpr uint32_t MSM_GROUP = 64;

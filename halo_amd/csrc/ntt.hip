@@ -472,17 +472,17 @@ __global__ __launch_bounds__(NE / NTT_EPT, 4) void k_ntt_pass(NttPassArgs a) {
         const size_t j = j0 + t;
         const size_t dst = ((j >> a.log_ns) << (a.log_ns + r)) + (j & (Ns - 1)) + (size_t)k * Ns;
         Fe<F> x = lds_get_soa<F>(data, ntt_swz<NE>(t * R + k), NE);
-        if (a.out_ark) {
-            if (out_mul) {
-                Fe<F> oc;
+        if (out_mul) {
+            Fe<F> oc;
 #pragma unroll
-                for (int l = 0; l < NLIMB; l++) oc.v[l] = a.out_const[l];
-                x = fs_mul(x, oc);
-            }
-            fe_store(out + 2 * dst, fe_canon(fe_reduce_2p(fs_settle(x))));
-        } else {
-            fe_store(out + 2 * dst, fs_settle(x));
+            for (int l = 0; l < NLIMB; l++) oc.v[l] = a.out_const[l];
+            x = fs_mul(x, oc);
         }
+        x = fs_settle(x);
+        if (a.out_ark) x = fe_canon(fe_reduce_2p(x));
+        // one store statement: with a store on each branch the compiler merged their common words into
+        // four stores per element (dword, dword, misaligned dwordx4, dwordx3) instead of two dwordx4
+        fe_store(out + 2 * dst, x);
     }
 }
 
@@ -662,9 +662,9 @@ static std::vector<unsigned> ntt_radices(unsigned logn) {
 }
 
 // the split as one key (5 bits per pass) for the twiddle-table cache
-static uint64_t ntt_split_key(unsigned logn) {
+static uint64_t ntt_split_key(const std::vector<unsigned>& rad) {
     uint64_t k = 0;
-    for (unsigned x : ntt_radices(logn)) k = (k << 5) | x;
+    for (unsigned x : rad) k = (k << 5) | x;
     return k;
 }
 
@@ -681,10 +681,12 @@ static unsigned ntt_pass0_prune(unsigned lr, unsigned prune) {
     return (pr >= g0 && pr < lr) ? pr : 0u;
 }
 
+// `rad`: the pass split the caller launches with (ntt_radices read once per transform, so a concurrent
+// halo_set_tuning of the split keys cannot pair tables built for one split with passes of another)
 template <class F>
-static int get_twiddles(DeviceState* st, int field, unsigned logn, int inverse, DeviceState::Twiddles** out,
-                        hipStream_t s) {
-    const uint64_t split = ntt_split_key(logn);
+static int get_twiddles(DeviceState* st, int field, unsigned logn, int inverse, const std::vector<unsigned>& rad,
+                        DeviceState::Twiddles** out, hipStream_t s) {
+    const uint64_t split = ntt_split_key(rad);
     for (auto& t : st->tw)
         if (t->field == field && t->logn == (int)logn && t->inverse == inverse && t->split == split) {
             *out = t.get();
@@ -713,7 +715,6 @@ static int get_twiddles(DeviceState* st, int field, unsigned logn, int inverse, 
     }
     // per-pass pre-twiddle tables (one multiplication per element instead of two)
     if (logn <= NTT_FULL_TABLE_MAX_LOG) {
-        const std::vector<unsigned> rad = ntt_radices(logn);
         unsigned log_ns = 0;
         for (size_t p = 0; p < rad.size(); p++) {
             if (p > 0) {
@@ -742,16 +743,17 @@ static int get_twiddles(DeviceState* st, int field, unsigned logn, int inverse, 
 // d_in, d_tmp2 (same size) takes that pass's output instead.  Buffers hold batch * N elements.
 template <class F>
 static int ntt_device(DeviceState* st, int field, const void* d_in, void* d_out, void* d_tmp, void* d_tmp2,
-                      unsigned logn, size_t batch, int inverse, hipStream_t s, unsigned prune = 0) {
+                      unsigned logn, size_t batch, int inverse, hipStream_t s, unsigned prune,
+                      const std::vector<unsigned>* rad_in) {
     if (logn > 30) return set_error(HALO_EINVAL, "NTT domain 2^%u too large", logn);
     const size_t N = (size_t)1 << logn;
     if (logn == 0) {
         if (d_in != d_out) HALO_HIP(hipMemcpyAsync(d_out, d_in, batch * 32, hipMemcpyDeviceToDevice, s));
         return HALO_OK;
     }
+    const std::vector<unsigned> rad = rad_in ? *rad_in : ntt_radices(logn);
     DeviceState::Twiddles* tw = nullptr;
-    HALO_CHECK(get_twiddles<F>(st, field, logn, inverse, &tw, s));
-    const std::vector<unsigned> rad = ntt_radices(logn);
+    HALO_CHECK(get_twiddles<F>(st, field, logn, inverse, rad, &tw, s));
     const int P = (int)rad.size();
     std::vector<const void*> srcs(P);
     std::vector<void*> dsts(P);
@@ -804,10 +806,11 @@ static int ntt_device(DeviceState* st, int field, const void* d_in, void* d_out,
 }
 
 int ntt_device_dispatch(DeviceState* st, int field, const void* d_in, void* d_out, void* d_tmp, unsigned logn,
-                        size_t batch, int inverse, hipStream_t s, void* d_tmp2, unsigned prune) {
+                        size_t batch, int inverse, hipStream_t s, void* d_tmp2, unsigned prune,
+                        const std::vector<unsigned>* rad) {
     int rc;
     DISPATCH_FIELD(field, F, {
-        rc = ntt_device<F>(st, field, d_in, d_out, d_tmp, d_tmp2, logn, batch, inverse, s, prune);
+        rc = ntt_device<F>(st, field, d_in, d_out, d_tmp, d_tmp2, logn, batch, inverse, s, prune, rad);
     });
     return rc;
 }
@@ -930,13 +933,14 @@ extern "C" int halo_ntt_dev_zero_tail(halo_field_t field, void* d_data, unsigned
     HALO_CHECK(st->scratch[5].reserve(batch * N * 32));
     // the tail's contents are ignored: zero exactly what pass 0 will read beyond nonzero_len (up to
     // 2^ceil(lg nonzero_len) when it prunes, the whole tail otherwise)
-    const unsigned pr = log_n ? ntt_pass0_prune(ntt_radices(log_n)[0], log_n - lg_nz) : 0u;
+    const std::vector<unsigned> rad = ntt_radices(log_n);  // one read: the zeroed span and the passes agree
+    const unsigned pr = log_n ? ntt_pass0_prune(rad[0], log_n - lg_nz) : 0u;
     const size_t read_end = pr ? (N >> pr) : N;
     if (read_end > nonzero_len)
         for (size_t b = 0; b < batch; b++)
             HALO_HIP(hipMemsetAsync((char*)d_data + (b * N + nonzero_len) * 32, 0, (read_end - nonzero_len) * 32, s));
     return ntt_device_dispatch(st, field, d_data, d_data, st->scratch[4].ptr, log_n, batch, 0, s, st->scratch[5].ptr,
-                               log_n - lg_nz);
+                               log_n - lg_nz, &rad);
 }
 
 extern "C" int halo_ntt_twiddle_dev(halo_field_t field, void* d_data, unsigned log_n, size_t rows, size_t cols,
@@ -954,7 +958,7 @@ extern "C" int halo_ntt_twiddle_dev(halo_field_t field, void* d_data, unsigned l
     const unsigned thr = 256, blocks = (unsigned)((cnt + thr - 1) / thr);
     DISPATCH_FIELD(field, F, {
         DeviceState::Twiddles* tw = nullptr;
-        HALO_CHECK(get_twiddles<F>(st, field, log_n, inverse ? 1 : 0, &tw, s));
+        HALO_CHECK(get_twiddles<F>(st, field, log_n, inverse ? 1 : 0, ntt_radices(log_n), &tw, s));
         hipLaunchKernelGGL(k_twiddle_mat<F>, dim3(blocks), dim3(thr), 0, s, (uint4*)d_data, rows, cols, row0, col0,
                            log_n, tw->lo.as<const uint4>(), tw->hi.as<const uint4>(), (uint32_t)tw->lo_bits);
     });

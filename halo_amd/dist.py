@@ -342,6 +342,9 @@ class IpaOps:
     def round_lr(self, ses):  # -> (L, R) WrappedPoints of this shard (H' terms included)
         raise NotImplementedError
 
+    def round_lr_dev(self, ses):  # -> the same pair left on the device (sharded_ipa_rounds device_lr=True)
+        raise NotImplementedError
+
     def fold(self, ses, xi, xi_inv):
         raise NotImplementedError
 
@@ -360,6 +363,11 @@ class IpaOps:
     def shard_len(self, shard) -> int:
         return len(shard[1])
 
+    def trivial_final(self, shard):  # n / P == 1: the shard's only element, (g (1, 8), c (1, 4), z (1, 4))
+        g, c, z = shard
+        return (np.asarray(g, dtype=np.uint64).reshape(-1, 8)[:1], np.asarray(c, dtype=np.uint64).reshape(-1, 4)[:1],
+                np.asarray(z, dtype=np.uint64).reshape(-1, 4)[:1])
+
 
 class GpuIpaOps(IpaOps):
     """Shard sessions over explicit vectors: shard = (gs, cs, zs)."""
@@ -375,6 +383,15 @@ class GpuIpaOps(IpaOps):
 
     def round_lr(self, ses):
         return ses.round_lr()
+
+    def round_lr_dev(self, ses):
+        """L_r, R_r as one device tensor (32 int64 = two packed XYZZ points, halo_ipa_round_lr_dev) on the
+        current torch stream: no host round trip; torch_reduce_lr_dev gathers and sums them."""
+        import torch
+
+        t = torch.empty(32, dtype=torch.int64, device="cuda")
+        ses.round_lr_dev(t.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        return t
 
     def fold(self, ses, xi, xi_inv):
         ses.fold(xi, xi_inv)
@@ -439,13 +456,24 @@ class GpuWeightedIpaOps(GpuIpaOps):
     def shard_len(self, shard) -> int:
         return len(shard[0])
 
+    def trivial_final(self, shard):
+        """n / P == 1: the shard is the global element j = rank -- G_rank is element 0 of the rank's
+        resident SRS shard, c_rank the shard's one scalar, and z_rank = z^rank."""
+        from . import _lib as H
+        from .group import _curve
 
-def ipa_shard_steps(ops: IpaOps, shard, H_prime, rounds: int):
-    """One rank's shard session as a generator: yields (L_r, R_r) each round, receives (xi, xi_inv),
-    returns the fully folded (g, c, z) element."""
+        cs, z = shard
+        g = np.zeros((1, 8), dtype=np.uint64)
+        H.check(H.load().halo_srs_read(_curve(self.curve), 0, 1, H.ptr(g)))
+        return g, np.asarray(cs, dtype=np.uint64).reshape(-1, 4)[:1].copy(), self._pow(z, self.rank).reshape(1, 4)
+
+
+def ipa_shard_steps(ops: IpaOps, shard, H_prime, rounds: int, device_lr: bool = False):
+    """One rank's shard session as a generator: yields (L_r, R_r) each round (device_lr: the pair as a
+    device tensor, ops.round_lr_dev), receives (xi, xi_inv), returns the fully folded (g, c, z) element."""
     ses = ops.begin(shard, H_prime)
     for _ in range(rounds):
-        xi, xi_inv = yield ops.round_lr(ses)
+        xi, xi_inv = yield (ops.round_lr_dev(ses) if device_lr else ops.round_lr(ses))
         ops.fold(ses, xi, xi_inv)
     return ops.final(ses)
 
@@ -469,14 +497,15 @@ def _drive(gens, reduce_lr, challenge, inverse, xi, Ls, Rs, rounds: int):
 
 
 def sharded_ipa_rounds(local_shards, H_prime, challenge: Callable, inverse: Callable, ops: IpaOps, world: int,
-                       gather: Callable, reduce_lr: Callable | None = None):
+                       gather: Callable, reduce_lr: Callable | None = None, device_lr: bool = False):
     """Distributed pcdl round loop.  ``local_shards``: the shards this process holds (ops.begin's
     description; (gs, cs, zs) strided vectors for GpuIpaOps, (cs, z) for GpuWeightedIpaOps) -- one
     with a real communicator, all P with virtual ranks; ``gather(objs)`` returns the list of every
     rank's objs in rank order (torch_gather_arrays(dist), or identity for virtual ranks);
     ``reduce_lr(local (L_r, R_r) list) -> (L, R)`` the round's sums over every rank (default: gather,
-    then ops.point_sum; torch_reduce_lr sums on the device).  Returns (Ls, Rs, U, c) exactly as the
-    single-session ipa_rounds does."""
+    then ops.point_sum; torch_reduce_lr sums on the device).  device_lr: the shard rounds leave L_r, R_r
+    on the device (ops.round_lr_dev) and reduce_lr is torch_reduce_lr_dev (gather, XYZZ sum and one D2H).
+    Returns (Ls, Rs, U, c) exactly as the single-session ipa_rounds does."""
     if world < 1 or world & (world - 1):
         raise ValueError("world size must be a power of two")
     n_loc = ops.shard_len(local_shards[0])
@@ -489,12 +518,11 @@ def sharded_ipa_rounds(local_shards, H_prime, challenge: Callable, inverse: Call
     Ls, Rs = [], []
     xi = None
     if n_loc >= 2:
-        gens = [ipa_shard_steps(ops, sh, H_prime, n_loc.bit_length() - 1) for sh in local_shards]
+        gens = [ipa_shard_steps(ops, sh, H_prime, n_loc.bit_length() - 1, device_lr) for sh in local_shards]
         xi, finals = _drive(gens, reduce_lr, challenge, inverse, xi, Ls, Rs, n_loc.bit_length() - 1)
         finals = gather(finals)
-    else:
-        finals = gather([(np.asarray(g).reshape(-1, 8)[:1], np.asarray(c).reshape(-1, 4)[:1],
-                          np.asarray(z).reshape(-1, 4)[:1]) for g, c, z in local_shards])
+    else:  # one element per rank: no shard rounds
+        finals = gather([ops.trivial_final(sh) for sh in local_shards])
     G = np.concatenate([f[0] for f in finals])
     C = np.concatenate([f[1] for f in finals])
     Z = np.concatenate([f[2] for f in finals])
@@ -511,19 +539,21 @@ def sharded_ipa_rounds(local_shards, H_prime, challenge: Callable, inverse: Call
 
 
 def sharded_ipa_fixed_challenges(ops_for_rank: Callable, shard_for_rank: Callable, H_prime, xis, xi_invs, world: int,
-                                 point_sum: Callable, ops_final: IpaOps):
+                                 point_sum: Callable, ops_final: IpaOps, reduce_pairs: Callable | None = None):
     """Virtual ranks run ONE AT A TIME (each may need its own resident SRS shard) against a challenge
     sequence fixed in advance (xis[k] for round k, independent of L and R): rank r's generator is
     driven to the end before rank r + 1 starts, then the per-round L_r, R_r are summed and the last
     lg P rounds run on the gathered finals.  Used by the GPU test of the weighted shards on one
-    device; the live transcript needs real ranks (sharded_ipa_rounds).  Returns (Ls, Rs, U, c)."""
+    device; the live transcript needs real ranks (sharded_ipa_rounds).  reduce_pairs: the shards leave
+    L_r, R_r on the device (ops.round_lr_dev) and reduce_pairs((P, 32) device rows) sums them
+    (xyzz_pair_reducer), as torch_reduce_lr_dev does after its all-gather.  Returns (Ls, Rs, U, c)."""
     per_rank, finals = [], []
     rounds = None
     for r in range(world):
         ops = ops_for_rank(r)
         shard = shard_for_rank(r)
         rounds = ops.shard_len(shard).bit_length() - 1
-        g = ipa_shard_steps(ops, shard, H_prime, rounds)
+        g = ipa_shard_steps(ops, shard, H_prime, rounds, reduce_pairs is not None)
         lr = [next(g)]
         for k in range(rounds):
             try:
@@ -531,8 +561,14 @@ def sharded_ipa_fixed_challenges(ops_for_rank: Callable, shard_for_rank: Callabl
             except StopIteration as e:
                 finals.append(e.value)
         per_rank.append(lr[:rounds])
-    Ls = [point_sum(np.stack([per_rank[r][k][0] for r in range(world)])) for k in range(rounds)]
-    Rs = [point_sum(np.stack([per_rank[r][k][1] for r in range(world)])) for k in range(rounds)]
+    if reduce_pairs is not None:
+        import torch
+
+        pairs = [reduce_pairs(torch.stack([per_rank[r][k] for r in range(world)])) for k in range(rounds)]
+        Ls, Rs = [p[0] for p in pairs], [p[1] for p in pairs]
+    else:
+        Ls = [point_sum(np.stack([per_rank[r][k][0] for r in range(world)])) for k in range(rounds)]
+        Rs = [point_sum(np.stack([per_rank[r][k][1] for r in range(world)])) for k in range(rounds)]
     G = np.concatenate([f[0] for f in finals])
     C = np.concatenate([f[1] for f in finals])
     Z = np.concatenate([f[2] for f in finals])
@@ -604,5 +640,50 @@ def torch_reduce_lr(dist, curve, device):
                                           ctypes.c_void_p(out.data_ptr() + 64 * k), sp))
         o = out.cpu().numpy().view(np.uint64)
         return o[:8].copy(), o[8:].copy()
+
+    return f
+
+
+def xyzz_pair_reducer(curve, device):
+    """The device half of torch_reduce_lr_dev: rows (k, 32) int64 on the device, row r = rank r's L_r | R_r
+    as packed XYZZ -> (L, R) WrappedPoints: halo_point_sum_xyzz_dev over each column (no inversion on the
+    device), one D2H of the two sums, host conversion (halo_xyzz_to_wrapped)."""
+    import ctypes
+
+    import torch
+
+    from . import _lib as H
+    from .group import _curve
+
+    L_ = H.load()
+    cid = _curve(curve)
+    out = torch.empty(32, dtype=torch.int64, device=device)
+    wrapped = np.zeros((2, 8), dtype=np.uint64)
+
+    def f(rows):
+        rows = rows.contiguous()
+        sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        for k in range(2):
+            H.check(L_.halo_point_sum_xyzz_dev(cid, ctypes.c_void_p(rows.data_ptr() + 128 * k), rows.shape[0], 256,
+                                               ctypes.c_void_p(out.data_ptr() + 128 * k), sp))
+        host = np.ascontiguousarray(out.cpu().numpy())
+        H.check(L_.halo_xyzz_to_wrapped(cid, H.ptr(host), 2, H.ptr(wrapped)))
+        return wrapped[0].copy(), wrapped[1].copy()
+
+    return f
+
+
+def torch_reduce_lr_dev(dist, curve, device):
+    """reduce_lr() for sharded_ipa_rounds(device_lr=True), one shard per rank: the rank's (L_r, R_r) is
+    already on the device as packed XYZZ (GpuIpaOps.round_lr_dev), one all_gather_into_tensor over RCCL
+    collects every rank's 256 B, and xyzz_pair_reducer sums the L and R columns on the device and brings
+    the two sums home in one D2H.  Against torch_reduce_lr: no D2H + host conversion + H2D of the rank's
+    own pair, and no lone-lane affine conversion in the device sums."""
+    gloo = dist.get_backend() != "nccl"  # (the one-GPU rehearsal gathers host tensors)
+    pair_sum = xyzz_pair_reducer(curve, device)
+
+    def f(lrs):
+        (t,) = lrs
+        return pair_sum(allgather_rows(t.cpu() if gloo else t, dist).to(device))
 
     return f

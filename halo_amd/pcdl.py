@@ -93,6 +93,12 @@ class IpaSession:
         H.check(lib.halo_ipa_round_lr(self._s, pl, pr))
         return lr[0].copy(), lr[1].copy()
 
+    def round_lr_dev(self, d_lr: int, stream: int) -> None:
+        """halo_ipa_round_lr_dev: the round's L and R land in the 256 device bytes at d_lr as packed XYZZ,
+        ordered before later work on `stream`; no host wait."""
+        _, _, _, _, _, lib = self._stage()
+        H.check(lib.halo_ipa_round_lr_dev(self._s, ctypes.c_void_p(d_lr), ctypes.c_void_p(stream)))
+
     def fold(self, xi, xi_inv=None):
         """xi_inv None: the library forms xi^-1 itself (halo_ipa_fold with a NULL xi_inv)."""
         _, _, _, xb, px, lib = self._stage()
@@ -132,10 +138,20 @@ class IpaSession:
         U = np.zeros((k, 8), dtype=np.uint64)
         c = np.zeros((k, 4), dtype=np.uint64)
         handles = [s_._s for s_ in sessions]
-        for s_ in sessions:
-            s_._s = None
+        # the library's argument checks first, here: they release nothing, so the handles must stay
+        if any(h is None for h in handles):
+            raise ValueError("end_many: a session was already ended")
+        if len({h.value for h in handles}) != k:
+            raise ValueError("end_many: a session is listed twice")
         arr = (ctypes.c_void_p * k)(*[h.value for h in handles])
-        H.check(H.load().halo_ipa_end_multi(arr, k, H.ptr(U), H.ptr(c)))
+        rc = H.load().halo_ipa_end_multi(arr, k, H.ptr(U), H.ptr(c))
+        # past its argument checks the call releases every session, also on an error (halo_gpu.h); an
+        # argument error (its own "halo_ipa_end_multi:" messages) releases none, and the handles stay
+        # with their wrappers so that end() can still release them
+        if rc == H.HALO_OK or not H.last_error().startswith("halo_ipa_end_multi:"):
+            for s_ in sessions:
+                s_._s = None
+        H.check(rc)
         return [(U[i].copy(), c[i].copy()) for i in range(k)]
 
 

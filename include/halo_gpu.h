@@ -193,6 +193,14 @@ int halo_point_sum(halo_curve_t curve, const halo_wrapped_point_t* pts, size_t k
 /* Device variant: k WrappedPoints at d_pts (stride_bytes = 64) summed into d_out, on `stream`. */
 int halo_point_sum_dev(halo_curve_t curve, const void* d_pts, size_t k, size_t stride_bytes, void* d_out,
                        void* stream);
+/* The same sum over packed XYZZ points (128 B each: X, Y, ZZ, ZZZ in the library's internal Montgomery
+ * form, as halo_ipa_round_lr_dev writes them), stride_bytes apart, into one packed XYZZ point: no
+ * affine conversion (and no inversion) on the device.  A distributed opening sums its ranks' L_r, R_r
+ * with it and converts the one sum on the host (halo_xyzz_to_wrapped). */
+int halo_point_sum_xyzz_dev(halo_curve_t curve, const void* d_pts, size_t k, size_t stride_bytes, void* d_out,
+                            void* stream);
+/* k packed XYZZ points (host memory) -> affine WrappedPoints (host binary extended Euclid). */
+int halo_xyzz_to_wrapped(halo_curve_t curve, const void* xyzz, size_t k, halo_wrapped_point_t* out);
 /* Window size the device MSM uses for n points. */
 int halo_msm_window_bits(size_t n);
 /* Window size of the resident SRS's window-shifted copies (halo_srs_precompute_windows), or 0 when
@@ -362,10 +370,17 @@ int halo_ipa_round_lr(halo_ipa_session* s, halo_wrapped_point_t* L, halo_wrapped
 int halo_ipa_fold(halo_ipa_session* s, const halo_fe_t* xi, const halo_fe_t* xi_inv);
 /* k independent openings advanced in lockstep (each session has its own stream; all k rounds /
  * folds are enqueued before any is waited for, so the openings overlap on the device): L[i], R[i]
- * of session i; xi[i], xi_inv[i] for session i (xi_inv NULL: formed on the host). */
+ * of session i; xi[i], xi_inv[i] for session i (xi_inv NULL: formed on the host).  The fold checks
+ * every session and xi before it enqueues any fold: an argument error (a null, closed or repeated
+ * session, xi = 0) leaves all k sessions unfolded. */
 int halo_ipa_round_lr_multi(halo_ipa_session* const* ses, size_t k, halo_wrapped_point_t* L,
                             halo_wrapped_point_t* R);
 int halo_ipa_fold_multi(halo_ipa_session* const* ses, size_t k, const halo_fe_t* xi, const halo_fe_t* xi_inv);
+/* One round whose L, R stay on the device: d_lr (256 B of device memory) receives L then R as packed XYZZ
+ * (halo_point_sum_xyzz_dev's format), ordered before later work on `stream`; no host wait.  The
+ * distributed opening's per-round reduce (pcdl.rs:412-418 summed over the ranks' shards):
+ * round_lr_dev -> all-gather -> halo_point_sum_xyzz_dev -> one D2H -> halo_xyzz_to_wrapped. */
+int halo_ipa_round_lr_dev(halo_ipa_session* s, void* d_lr, void* stream);
 /* Current half-length m, and the folded vectors (length 2m) copied back to the host (any of the
  * output pointers may be NULL).  Sessions over the resident SRS do not materialise G in their
  * weighted / tail rounds (the default; HALO_IPA_WEIGHTED=0 and HALO_IPA_TAIL=0 keep G folded every
@@ -374,7 +389,10 @@ int halo_ipa_state(halo_ipa_session* s, size_t* m, halo_wrapped_point_t* gs, hal
                    halo_fe_t* zs);
 /* U = G_0 and c_0 after the last round (in weighted / tail rounds U is only defined then).  The
  * session's streams and device buffers go back to a per-device pool (reused by the next opening;
- * released by halo_shutdown), so a warm opening allocates nothing. */
+ * released by halo_shutdown), so a warm opening allocates nothing.  After its end a handle must not
+ * be used again: every entry point refuses (HALO_EINVAL) a handle whose session was destroyed or is
+ * idle in the pool, but once the pool hands that session to a later opening the old handle names the
+ * new opening. */
 int halo_ipa_end(halo_ipa_session* s, halo_wrapped_point_t* U, halo_fe_t* c);
 /* halo_ipa_end of k lockstep sessions (U[i], c[i] of session i; U or c may be NULL): every session's
  * final U sum is enqueued on its own stream before any is waited for.  Argument errors (a null,

@@ -209,6 +209,9 @@ class OracleIpaOps(IpaOps):
         return (np.array([P.point_to_wrapped(c, s["G"][0])], dtype=np.uint64), self._fe(s["C"][:1]),
                 self._fe(s["Z"][:1]))
 
+    def round_lr_dev(self, s):  # (the CPU stand-in of a device-resident pair: the plumbing of device_lr)
+        return self.round_lr(s)
+
     def point_sum(self, pts):
         P, c = self.P, self.c
         acc = None
@@ -254,7 +257,7 @@ def ipa_instance(cname, n, seed=5):
     return g, fe(cs), fe(zs), np.array(P.point_to_wrapped(c, Hp), dtype=np.uint64)
 
 
-def _ipa_worker(rank, world, port, cname, n, q):
+def _ipa_worker(rank, world, port, cname, n, q, device_lr=False):
     sys.path.insert(0, ROOT)
     import torch.distributed as dist
 
@@ -266,7 +269,8 @@ def _ipa_worker(rank, world, port, cname, n, q):
     g, cs, zs, Hp = ipa_instance(cname, n)
     shard = (ipa_shard(g, rank, world), ipa_shard(cs, rank, world), ipa_shard(zs, rank, world))
     ch, inv = ipa_transcript(cname)
-    Ls, Rs, U, c = sharded_ipa_rounds([shard], Hp, ch, inv, OracleIpaOps(cname), world, torch_gather_arrays(dist))
+    Ls, Rs, U, c = sharded_ipa_rounds([shard], Hp, ch, inv, OracleIpaOps(cname), world, torch_gather_arrays(dist),
+                                      device_lr=device_lr)
     q.put((rank, [x.tolist() for x in Ls], [x.tolist() for x in Rs], U.tolist(), c.tolist()))
     dist.barrier()
     dist.destroy_process_group()
@@ -280,12 +284,15 @@ def single_session_ipa(cname, g, cs, zs, Hp):
     return sharded_ipa_rounds([(g, cs, zs)], Hp, ch, inv, OracleIpaOps(cname), 1, lambda objs: objs)
 
 
-@pytest.mark.parametrize("world,n,cname", [(2, 16, "pallas"), (4, 16, "vesta"), (4, 4, "pallas")])
-def test_sharded_ipa_gloo(corc, world, n, cname):
+@pytest.mark.parametrize("world,n,cname,device_lr", [(2, 16, "pallas", False), (4, 16, "vesta", False),
+                                                     (4, 4, "pallas", False), (2, 16, "vesta", True)])
+def test_sharded_ipa_gloo(corc, world, n, cname, device_lr):
+    """device_lr: the shard rounds go through ops.round_lr_dev (the device-resident per-round reduce's
+    plumbing; its device half is tests/test_gpu_ipa_eval.py::test_sharded_ipa_weighted_virtual_ranks)."""
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_ipa_worker, args=(r, world, port, cname, n, q)) for r in range(world)]
+    procs = [ctx.Process(target=_ipa_worker, args=(r, world, port, cname, n, q, device_lr)) for r in range(world)]
     for p in procs:
         p.start()
     out = sorted([q.get(timeout=300) for _ in range(world)])

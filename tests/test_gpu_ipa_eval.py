@@ -353,7 +353,7 @@ def test_sharded_ipa_weighted_virtual_ranks(hal, logn, world):
     after another against a fixed challenge sequence (each needs its own resident shard on the one
     GPU); every L, R, U and c equals the single-GPU opening over the whole SRS with the same
     challenges -- 2^20 over 8 ranks is the BASELINE size."""
-    from halo_amd.dist import GpuIpaOps, GpuWeightedIpaOps, sharded_ipa_fixed_challenges
+    from halo_amd.dist import GpuIpaOps, GpuWeightedIpaOps, sharded_ipa_fixed_challenges, xyzz_pair_reducer
 
     c = P.PALLAS
     r = c.scalar
@@ -399,6 +399,55 @@ def test_sharded_ipa_weighted_virtual_ranks(hal, logn, world):
     assert len(Ls2) == logn
     for k, (a, b) in enumerate(zip(Ls + Rs, Ls2 + Rs2)):
         assert np.array_equal(a, b), k
+    assert np.array_equal(U, U2)
+    assert np.array_equal(cfin, c2)
+    # the device-resident per-round reduce: L_r, R_r left on the device as packed
+    # XYZZ (halo_ipa_round_lr_dev), summed there (halo_point_sum_xyzz_dev), one D2H per round
+    Ls3, Rs3, U3, c3 = sharded_ipa_fixed_challenges(ops_for_rank, shard_for_rank, Hp, xis, xinv, world, None,
+                                                    GpuIpaOps("pallas"),
+                                                    reduce_pairs=xyzz_pair_reducer("pallas", "cuda"))
+    for k, (a, b) in enumerate(zip(Ls + Rs, Ls3 + Rs3)):
+        assert np.array_equal(a, b), k
+    assert np.array_equal(U, U3)
+    assert np.array_equal(cfin, c3)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_ipa_weighted_one_element_per_rank(hal, world):
+    """n == P on the weighted path: no shard rounds run, each rank contributes its one
+    element (G_r = element 0 of its resident shard, c_r, z^r) through GpuWeightedIpaOps.trivial_final,
+    and the lg P collapsed rounds reproduce the single-GPU opening of the same instance.  Virtual
+    ranks: rank r's shard is uploaded before its element is read; gather hands the collected elements
+    to sharded_ipa_rounds."""
+    from halo_amd.dist import GpuWeightedIpaOps, sharded_ipa_rounds
+
+    c = P.PALLAS
+    r = c.scalar
+    n = world
+    L = hal.load()
+    hal.check(L.halo_srs_synthesize(0, 64, 5150 + world))
+    G = np.zeros((n, 8), dtype=np.uint64)
+    hal.check(L.halo_srs_read(0, 0, n, hal.ptr(G)))
+    pr = random.Random(world)
+    cs = fe([pr.randrange(r) for _ in range(n)], r)
+    z = fe([pr.randrange(1, r)], r)[0]
+    Hp = np.array(P.point_to_wrapped(c, P.mul_fast(c, pr.randrange(1, r), c.generator)), dtype=np.uint64)
+    challenge, inverse = transcript("pallas")
+    group.PublicParams.upload("pallas", np.ascontiguousarray(G), precompute_windows=False)
+    Ls, Rs, U, cfin = pcdl.ipa_rounds(cs, z, Hp, challenge, inverse, "pallas")
+    finals = []
+    for k in range(world):
+        group.PublicParams.upload("pallas", np.ascontiguousarray(G[k::world]), precompute_windows=False)
+        fin = GpuWeightedIpaOps("pallas", k, world).trivial_final((np.ascontiguousarray(cs[k::world]), z))
+        assert np.array_equal(fin[0][0], G[k]) and np.array_equal(fin[1][0], cs[k])
+        assert unfe(fin[2], r) == [pow(unfe([z], r)[0], k, r)]
+        finals.append(fin)
+    ops0 = GpuWeightedIpaOps("pallas", 0, world)
+    Ls2, Rs2, U2, c2 = sharded_ipa_rounds([(np.ascontiguousarray(cs[0::world]), z)], Hp, challenge, inverse, ops0,
+                                          world, lambda objs: finals)
+    assert len(Ls2) == len(Ls)
+    for a, b in zip(Ls + Rs, Ls2 + Rs2):
+        assert np.array_equal(a, b)
     assert np.array_equal(U, U2)
     assert np.array_equal(cfin, c2)
 
