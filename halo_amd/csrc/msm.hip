@@ -839,12 +839,21 @@ static int msm_srs_pairs_t(DeviceState* st, size_t np, const MsmPairIO* io, size
     uint32_t* digits = M.digits.as<uint32_t>();
     DigitSrcs ds{};
     for (int p = 0; p < P; p++) ds.s[p] = (const uint4*)(p & 1 ? io[p / 2].sr : io[p / 2].sl);
-    hipLaunchKernelGGL(k_digits_multi<typename Cv::Scalar>, dim3(grid_for(half, 256), P), dim3(256), 0, s, ds, half, c, W,
-                       digits, SN);
-    HALO_HIP(hipGetLastError());
+    // the digit recoding fused into the sort's first pass (thread = scalar, round = window), as the
+    // headline MSM's: no digit array written and read back (W <= 16 windows and keys of <= 17 bits, so
+    // the first pass is an 8-bit one)
+    const bool fuse = W <= 16 && key_bits <= 17;
+    RsFused fz{nullptr, half, c, W, curve_id<Cv>() == HALO_PALLAS ? HALO_FP : HALO_FQ, P, {}};
+    for (int p = 0; p < P; p++) fz.srcs[p] = ds.s[p];
+    if (!fuse) {
+        hipLaunchKernelGGL(k_digits_multi<typename Cv::Scalar>, dim3(grid_for(half, 256), P), dim3(256), 0, s, ds, half,
+                           c, W, digits, SN);
+        HALO_HIP(hipGetLastError());
+    }
     uint32_t *skeys = nullptr, *svals = nullptr;
     const uint32_t* scount = nullptr;
-    HALO_CHECK(msm_radix_sort(digits, E, SN, B, key_bits, M.sort, &skeys, &svals, &scount, nullptr, NB, s));
+    HALO_CHECK(msm_radix_sort(digits, E, SN, B, key_bits, M.sort, &skeys, &svals, &scount, nullptr, NB, s,
+                              fuse ? &fz : nullptr));
     {
         ProfScope prof("msm_acc", s);
         const uint32_t nblocks = (uint32_t)grid_for(nchunks, 256);

@@ -42,9 +42,25 @@ constexpr int rs_rounds() { return BITS == 8 ? 16 : 14; }
 constexpr size_t RS_STAGE_BYTES = 2 * 4 * RS_THREADS * 16;  // k_rs_scatter's key / value staging
 constexpr uint32_t RS_NONE = 0xffffffffu;
 
+// The scalars of a fused first pass: P outputs of n scalars each (output p at s[p], keys offset by p B)
+struct RsScalars {
+    const uint4* s[8] = {};
+    uint32_t n = 0, P = 1, B = 0;
+};
+// (output p of the global scalar g and its scalar's address: a select chain, not a dynamic index into
+// the kernel-argument array, which would go through scratch memory)
+HALO_DEV const uint4* rs_scalar(const RsScalars& sc, uint32_t g, uint32_t& p, uint32_t& i) {
+    p = sc.P == 1 ? 0u : g / sc.n;
+    i = g - p * sc.n;
+    const uint4* src = sc.s[0];
+#pragma unroll
+    for (uint32_t q = 1; q < 8; q++)
+        if (p == q) src = sc.s[q];
+    return src + 2 * (size_t)i;
+}
+
 struct RsIn {
-    const uint4* sc = nullptr;  // fused pass 0: the ark scalars (k_rs_hist_sc / k_rs_scatter<.., S>)
-    uint32_t n_sc = 0;
+    RsScalars sc;  // fused pass 0: the ark scalars (k_rs_hist_sc / k_rs_scatter<.., S>)
     int c = 0, W = 0;
     const uint32_t* digits;  // pass 0 only
     const uint32_t* keys;    // later passes
@@ -227,18 +243,21 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_hist(RsIn in, uint32_t ntiles
 // from the scalars here instead of being written by k_digits and read back (32 B of scalar per
 // W = 15 entries instead of 2 x 4 B per entry).  Thread = one scalar, round = window: a tile is
 // RS_THREADS scalars x W windows.  Entry key = |d| - 1, value = (w n + i) | sign, as k_digits + pass 0.
+// (P > 1 outputs: key p B + |d| - 1 has the same low byte as |d| - 1, B being a multiple of 256)
 template <class S>
-__global__ __launch_bounds__(RS_THREADS) void k_rs_hist_sc(const uint4* sc, uint32_t n, int c, int W, uint32_t ntiles,
+__global__ __launch_bounds__(RS_THREADS) void k_rs_hist_sc(const RsScalars sc, int c, int W, uint32_t ntiles,
                                                          uint32_t* hist, uint32_t* chunk, uint32_t* ctr,
                                                          uint32_t* count) {
     __shared__ uint32_t h[RS_BINS];
     if (threadIdx.x < RS_BINS) h[threadIdx.x] = 0;
     __syncthreads();
-    const uint32_t i = blockIdx.x * RS_THREADS + threadIdx.x;
-    if (i < n)
-        scalar_signed_digits<S>(sc + 2 * (size_t)i, c, W, [&](int, uint32_t d) {
+    const uint32_t g = blockIdx.x * RS_THREADS + threadIdx.x;
+    if (g < sc.P * sc.n) {
+        uint32_t p, i;
+        scalar_signed_digits<S>(rs_scalar(sc, g, p, i), c, W, [&](int, uint32_t d) {
             if (d != DIGIT_NONE) atomicAdd(&h[d & 255u], 1u);
         });
+    }
     __syncthreads();
     rs_publish_and_scan<RS_BINS>(h, blockIdx.x, ntiles, hist, chunk, ctr, count);
 }
@@ -283,15 +302,19 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(RsIn in, const uint32
             K[r] = 0;
             V[r] = 0;
         }
-        const uint32_t i = blockIdx.x * RS_THREADS + tid;
-        if (i < in.n_sc)
-            scalar_signed_digits<SF, R>(in.sc + 2 * (size_t)i, in.c, in.W, [&](int w, uint32_t d) {
+        const uint32_t g = blockIdx.x * RS_THREADS + tid;
+        if (g < in.sc.P * in.sc.n) {
+            uint32_t p, i;
+            const uint4* src = rs_scalar(in.sc, g, p, i);
+            const uint32_t koff = p * in.sc.B;
+            scalar_signed_digits<SF, R>(src, in.c, in.W, [&](int w, uint32_t d) {
                 if (d != DIGIT_NONE) {
-                    K[w] = d & 0x7fffffffu;
-                    V[w] = ((uint32_t)w * in.n_sc + i) | (d & 0x80000000u);
+                    K[w] = koff + (d & 0x7fffffffu);
+                    V[w] = ((uint32_t)w * in.sc.n + i) | (d & 0x80000000u);
                     validmask |= 1u << w;
                 }
             });
+        }
     } else {
         // all loads of the tile issued back to back (memory-level parallelism), kept in registers
         uint32_t A[R], Bv[R];
@@ -529,7 +552,10 @@ int msm_radix_sort(const uint32_t* digits, size_t E, size_t npw, uint32_t B, uin
     uint32_t ntmax = 1;
     for (auto& q : plan) ntmax = std::max(ntmax, tiles_of(q.second));
     // fused first pass: tiles of RS_THREADS scalars x W windows
-    const uint32_t ntiles0 = fused ? (uint32_t)std::max<size_t>(1, (fused->n + RS_THREADS - 1) / RS_THREADS) : 0u;
+    const size_t nsc = fused ? fused->n * (size_t)fused->P : 0;
+    if (fused && (fused->P < 1 || fused->P > 8 || fused->W > rs_rounds<8>() || nsc >= (1ull << 31) / 16))
+        return set_error(HALO_EINVAL, "fused sort pass: %d outputs, %d windows, %zu scalars", fused->P, fused->W, nsc);
+    const uint32_t ntiles0 = fused ? (uint32_t)std::max<size_t>(1, (nsc + RS_THREADS - 1) / RS_THREADS) : 0u;
     ntmax = std::max(ntmax, ntiles0);
     HALO_CHECK(S.keys[0].reserve(std::max<size_t>(E, 1) * 4));
     HALO_CHECK(S.keys[1].reserve(std::max<size_t>(E, 1) * 4));
@@ -562,12 +588,15 @@ int msm_radix_sort(const uint32_t* digits, size_t E, size_t npw, uint32_t B, uin
         uint32_t* hist = S.hist.as<uint32_t>();
         uint32_t* offs = S.offs.as<uint32_t>();
         if (fp) {
-            in.sc = (const uint4*)fused->scalars;
-            in.n_sc = (uint32_t)fused->n;
+            for (int q = 0; q < 8; q++)
+                in.sc.s[q] = (const uint4*)(fused->P == 1 ? (q == 0 ? fused->scalars : nullptr) : fused->srcs[q]);
+            in.sc.n = (uint32_t)fused->n;
+            in.sc.P = (uint32_t)fused->P;
+            in.sc.B = B;
             in.c = fused->c;
             in.W = fused->W;
             DISPATCH_FIELD(fused->field, SF, {
-                hipLaunchKernelGGL(k_rs_hist_sc<SF>, dim3(nt), dim3(RS_THREADS), 0, s, in.sc, in.n_sc, in.c, in.W, nt,
+                hipLaunchKernelGGL(k_rs_hist_sc<SF>, dim3(nt), dim3(RS_THREADS), 0, s, in.sc, in.c, in.W, nt,
                                    hist, offs, S.ctr.as<uint32_t>(), S.count.as<uint32_t>());
                 hipLaunchKernelGGL((k_rs_scatter<8, SF>), dim3(nt), dim3(RS_THREADS), RS_STAGE_BYTES, s, in,
                                    (const uint32_t*)hist, (const uint32_t*)offs, S.keys[cur].as<uint32_t>(),
