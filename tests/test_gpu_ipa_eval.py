@@ -412,6 +412,68 @@ def test_sharded_ipa_weighted_virtual_ranks(hal, logn, world):
     assert np.array_equal(cfin, c3)
 
 
+def oracle_ipa_loop(corc, cname, G, cs, zs, Hp, xis, xinvs):
+    """pcdl.rs:404-438 on the C oracle: per round L = <c_r, G_l> + <c_r, z_l> H' and R likewise (one
+    oracle MSM each, H' as an extra base), then the oracle fold (pcdl.rs:427-435)."""
+    field = "fp" if cname == "pallas" else "fq"
+    G, C, Z = (np.ascontiguousarray(a) for a in (G, cs, zs))
+    Ls, Rs = [], []
+    for k in range(len(G).bit_length() - 1):
+        m = len(G) // 2
+        dl = corc.scalar_dot(field, C[m:], Z[:m])
+        dr = corc.scalar_dot(field, C[:m], Z[m:])
+        Ls.append(corc.msm(cname, np.ascontiguousarray(np.vstack([G[:m], Hp[None]])),
+                           np.ascontiguousarray(np.vstack([C[m:], dl[None]]))))
+        Rs.append(corc.msm(cname, np.ascontiguousarray(np.vstack([G[m:], Hp[None]])),
+                           np.ascontiguousarray(np.vstack([C[:m], dr[None]]))))
+        G, C, Z = corc.ipa_fold(cname, G, C, Z, xis[k], xinvs[k])
+    return Ls, Rs, G[0], C[0]
+
+
+@pytest.mark.parametrize("logn,world", [(15, 2), (15, 4)])
+def test_sharded_ipa_weighted_vs_oracle(hal, corc, logn, world):
+    """The distributed opening on the weighted-round path checked against the C oracle's round loop
+    directly (the 2^20 virtual-rank test compares with the one-GPU opening only).  At
+    2^15 over 2 / 4 ranks each shard runs weighted rounds (2^14 / 2^13 per rank), the switch and tail
+    rounds; both per-round reduces (host pairs and the device-resident XYZZ sums) must give the
+    oracle's L, R, U, c."""
+    from halo_amd.dist import GpuIpaOps, GpuWeightedIpaOps, sharded_ipa_fixed_challenges, xyzz_pair_reducer
+
+    c = P.PALLAS
+    r = c.scalar
+    n = 1 << logn
+    L = hal.load()
+    hal.check(L.halo_srs_synthesize(0, n, 777 + logn))
+    G = np.zeros((n, 8), dtype=np.uint64)
+    hal.check(L.halo_srs_read(0, 0, n, hal.ptr(G)))
+    pr = random.Random(logn * world)
+    cs = fe([pr.randrange(r) for _ in range(n)], r)
+    zv = pr.randrange(1, r)
+    z = fe([zv], r)[0]
+    zs = fe(P.construct_powers(zv, n, r), r)
+    Hp = G[5].copy()
+    xis = [fe([pr.randrange(1, r)], r)[0] for _ in range(logn)]
+    xinv = [fe([P.inv(P.from_mont(P.limbs_to_int(x), r), r)], r)[0] for x in xis]
+    Ls, Rs, U, cfin = oracle_ipa_loop(corc, "pallas", G, cs, zs, Hp, xis, xinv)
+
+    def ops_for_rank(k):
+        group.PublicParams.upload("pallas", np.ascontiguousarray(G[k::world]), precompute_windows=True)
+        return GpuWeightedIpaOps("pallas", k, world)
+
+    def shard_for_rank(k):
+        return (np.ascontiguousarray(cs[k::world]), z)
+
+    for reduce_pairs in (None, xyzz_pair_reducer("pallas", "cuda")):
+        Ls2, Rs2, U2, c2 = sharded_ipa_fixed_challenges(ops_for_rank, shard_for_rank, Hp, xis, xinv, world,
+                                                        lambda pts: group.point_sum(pts, "pallas"),
+                                                        GpuIpaOps("pallas"), reduce_pairs=reduce_pairs)
+        assert len(Ls2) == logn
+        for k, (a, b) in enumerate(zip(Ls + Rs, Ls2 + Rs2)):
+            assert np.array_equal(a, b), k
+        assert np.array_equal(U, U2)
+        assert np.array_equal(cfin, c2)
+
+
 @pytest.mark.parametrize("world", [2, 4])
 def test_sharded_ipa_weighted_one_element_per_rank(hal, world):
     """n == P on the weighted path: no shard rounds run, each rank contributes its one

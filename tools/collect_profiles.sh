@@ -10,6 +10,10 @@
 #                        matches)
 #   pmc_kernels.txt      per-kernel SQ / LDS / HBM counters of the MSM kernels (tools/pmc_kernels.sh)
 #   prove_kstats.txt     kernel statistics of the 2^20 naive_prover pipeline (tools/prof_prove.sh)
+#   prove_valu.json      the prover kernels' VALU counts and compute fractions (tools/pmc_prove.sh)
+#   pmc_ntt22.txt / pmc_ntt24.txt   SQ stall counters of the NTT pass kernels (tools/pmc_ntt.sh)
+#   bench_stamped.json   the default bench line again, with pmc_summary.json / prove_valu.json of this
+#                        build in place (roofline.traffic and every compute roofline filled)
 set -o pipefail
 tag=${1:-r02}
 cd $GRAFT_REPO_ROOT
@@ -34,4 +38,9 @@ python3 tools/kstats.py $O/kernel_stats.csv > $O/kstats.txt
 bash tools/pmc_kernels.sh $tag > /dev/null && cp gpurun_out/pmc_k/$tag/summary.txt $O/pmc_kernels.txt
 rm -rf gpurun_out/pmc_k/$tag/[a-e]
 bash tools/prof_prove.sh 20 > /dev/null && cp gpurun_out/prof_prove/kstats.txt $O/prove_kstats.txt
+bash tools/pmc_prove.sh 20 > $O/pmc_prove.log 2>&1 && cp gpurun_out/pmc_prove/prove_valu.json $O/ || { tail -5 $O/pmc_prove.log; exit 1; }
+bash tools/pmc_ntt.sh 22 > $O/pmc_ntt22.txt 2>&1 && bash tools/pmc_ntt.sh 24 > $O/pmc_ntt24.txt 2>&1 || exit 1
+cp $O/pmc_summary.json profiles/pmc_summary.json && cp $O/prove_valu.json profiles/prove_valu.json
+timeout -k 10 500 python bench.py > $O/bench_stamped_full.json 2> $O/bench_stamped.err || { tail -20 $O/bench_stamped.err; exit 1; }
+tail -n 1 $O/bench_stamped_full.json > $O/bench_stamped.json
 head -n 30 $O/kstats.txt
