@@ -80,6 +80,7 @@ SIGNATURES = {
     "halo_point_sum": [ctypes.c_int, _vp, _sz, _vp],
     "halo_point_sum_dev": [ctypes.c_int, _vp, _sz, _sz, _vp, _vp],
     "halo_point_sum_xyzz_dev": [ctypes.c_int, _vp, _sz, _sz, _vp, _vp],
+    "halo_point_sum_rows_dev": [ctypes.c_int, _vp, _sz, _sz, _vp, _vp],
     "halo_xyzz_to_wrapped": [ctypes.c_int, _vp, _sz, _vp],
     "halo_profile_enable": [ctypes.c_int],
     "halo_profile_read": [ctypes.c_char_p, ctypes.POINTER(_sz), ctypes.POINTER(ctypes.c_double)],

@@ -193,6 +193,9 @@ int halo_point_sum(halo_curve_t curve, const halo_wrapped_point_t* pts, size_t k
 /* Device variant: k WrappedPoints at d_pts (stride_bytes = 64) summed into d_out, on `stream`. */
 int halo_point_sum_dev(halo_curve_t curve, const void* d_pts, size_t k, size_t stride_bytes, void* d_out,
                        void* stream);
+/* rows independent sums at once (one launch): row b sums the k WrappedPoints d_pts[b k .. b k + k) into
+ * d_out[b] -- the combine of `rows` point-partitioned MSMs after one all-gather (bench.py --gpus N). */
+int halo_point_sum_rows_dev(halo_curve_t curve, const void* d_pts, size_t rows, size_t k, void* d_out, void* stream);
 /* The same sum over packed XYZZ points (128 B each: X, Y, ZZ, ZZZ in the library's internal Montgomery
  * form, as halo_ipa_round_lr_dev writes them), stride_bytes apart, into one packed XYZZ point: no
  * affine conversion (and no inversion) on the device.  A distributed opening sums its ranks' L_r, R_r

@@ -323,6 +323,30 @@ def test_point_sum(hal, corc):
     assert list(group.point_sum(g[:0], "pallas")) == [0] * 8
 
 
+@pytest.mark.parametrize("rows,k", [(20, 8), (3, 1), (5, 300)])
+def test_point_sum_rows_dev(hal, corc, rows, k):
+    """halo_point_sum_rows_dev (the N-rank combine of several steps in one launch): row b of the result
+    is the oracle sum of its k points; a row of identities sums to the identity."""
+    import ctypes
+
+    import torch
+
+    c = P.PALLAS
+    g = corc.srs_generate("pallas", rows * k)
+    g[:k] = 0  # row 0: identities only
+    d_pts = torch.from_numpy(g.view(np.int64).copy()).cuda()
+    d_out = torch.zeros((rows, 8), dtype=torch.int64, device="cuda")
+    hal.check(hal.load().halo_point_sum_rows_dev(0, ctypes.c_void_p(d_pts.data_ptr()), rows, k,
+                                                 ctypes.c_void_p(d_out.data_ptr()), None))
+    got = d_out.cpu().numpy().view(np.uint64)
+    for b in range(rows):
+        exp = None
+        for x in g[b * k:(b + 1) * k]:
+            if int(x.any()):
+                exp = P.add(c, exp, P.wrapped_to_point(c, list(x)))
+        assert list(got[b]) == (P.point_to_wrapped(c, exp) if exp is not None else [0] * 8), b
+
+
 def test_srs_read_roundtrip(hal, corc):
     g = corc.srs_generate("vesta", 1000)
     group.PublicParams.upload("vesta", g, precompute_windows=False)
