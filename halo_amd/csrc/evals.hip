@@ -242,6 +242,11 @@ __global__ __launch_bounds__(256) void k_gate_affine(const GateArgs a, size_t N,
         aa = fe_add(aa, fe_mul(l_ad, yr));
     }
 
+    // (the three constraint groups one after another: their loads are not hoisted above the previous
+    // group's products, so the kernel's live set is one group's, not all three -- 256 VGPRs and one
+    // wave per SIMD otherwise)
+    Fe<F> acc = fe_mul(Q(6), aa);
+    asm volatile("" ::: "memory");
     // affine_mul_constraints_generic (protocol.rs:851-937), two_pow_i = r[0]
     Fe<F> am;
     {
@@ -283,6 +288,8 @@ __global__ __launch_bounds__(256) void k_gate_affine(const GateArgs a, size_t N,
         am = fe_sub(fe_add(am, NW(2)), fe_add(av, fe_mul(bv, R(0))));
     }
 
+    acc = fe_add(acc, fe_mul(Q(7), am));
+    asm volatile("" ::: "memory");
     // eq_generic (protocol.rs:1001-1011)
     Fe<F> eq;
     {
@@ -290,8 +297,6 @@ __global__ __launch_bounds__(256) void k_gate_affine(const GateArgs a, size_t N,
         eq = fe_add(fe_mul(ab, e), fe_sub(fe_add(fe_mul(ab, W(4)), e), W(2)));
     }
 
-    Fe<F> acc = fe_mul(Q(6), aa);
-    acc = fe_add(acc, fe_mul(Q(7), am));
     acc = fe_add(acc, fe_mul(Q(8), eq));
     fe_store(t + 2 * i, acc);
 }

@@ -421,8 +421,6 @@ struct MsmPipe {
     int slot_next[2] = {0, 0};
     uint64_t slot_used[2] = {0, 0}, clock = 0;
     hipStream_t tail[MSM_SETS] = {};  // one per scratch set: consecutive tails run concurrently
-    hipStream_t lo[MSM_SETS] = {}, hi[MSM_SETS] = {};  // least / greatest priority (tuning msm_front_prio)
-    hipEvent_t ev_a[MSM_SETS] = {}, ev_b[MSM_SETS] = {};
 };
 static MsmPipe g_msm_pipe[64];  // per device
 
@@ -461,14 +459,6 @@ static int msm_pick_set(MsmPipe& P, hipStream_t s, bool advance) {
 static int pipe_init(MsmPipe& P) {
     if (P.tail[0]) return HALO_OK;
     for (auto& t : P.tail) HALO_HIP(hipStreamCreateWithFlags(&t, hipStreamNonBlocking));
-    int least = 0, greatest = 0;
-    HALO_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    for (int k = 0; k < MSM_SETS; k++) {
-        HALO_HIP(hipStreamCreateWithPriority(&P.lo[k], hipStreamNonBlocking, least));
-        HALO_HIP(hipStreamCreateWithPriority(&P.hi[k], hipStreamNonBlocking, greatest));
-        HALO_HIP(hipEventCreateWithFlags(&P.ev_a[k], hipEventDisableTiming));
-        HALO_HIP(hipEventCreateWithFlags(&P.ev_b[k], hipEventDisableTiming));
-    }
     for (auto& m : P.set) {
         HALO_HIP(hipEventCreateWithFlags(&m.acc_done, hipEventDisableTiming));
         HALO_HIP(hipEventCreateWithFlags(&m.tail_done, hipEventDisableTiming));
@@ -488,16 +478,7 @@ void msm_shutdown() {
             (void)hipStreamDestroy(t);
             t = nullptr;
         }
-        for (int k = 0; k < MSM_SETS; k++) {
-            for (hipStream_t* t : {&P.lo[k], &P.hi[k]}) {
-                if (*t) (void)hipStreamSynchronize(*t), (void)hipStreamDestroy(*t);
-                *t = nullptr;
-            }
-            for (hipEvent_t* e : {&P.ev_a[k], &P.ev_b[k]}) {
-                if (*e) (void)hipEventDestroy(*e);
-                *e = nullptr;
-            }
-        }
+
         for (auto& m : P.set) {
             for (hipEvent_t* e : {&m.acc_done, &m.tail_done, &m.start, &m.front_done}) {
                 if (*e) (void)hipEventDestroy(*e);
@@ -600,23 +581,8 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
         uint32_t *skeys = nullptr, *svals = nullptr;
         const uint32_t* scount = nullptr;
         RsFused fz{scalars_ark, n, c, W_all, curve_id<Cv>() == HALO_PALLAS ? HALO_FP : HALO_FQ};
-        const long long prio = fuse ? tuning(TUNE_MSM_FRONT_PRIO) : 0;
-        const hipStream_t fs = prio == 1 ? PP.lo[set] : s;  // the sort's stream
-        if (fs != s) {
-            HALO_HIP(hipEventRecord(PP.ev_a[set], s));
-            HALO_HIP(hipStreamWaitEvent(fs, PP.ev_a[set], 0));
-        }
         HALO_CHECK(msm_radix_sort(M.digits.as<const uint32_t>(), E, SN, B, key_bits, M.sort, &skeys, &svals, &scount,
-                                  nullptr, NB, fs, fuse ? &fz : nullptr));
-        if (fs != s) {
-            HALO_HIP(hipEventRecord(PP.ev_b[set], fs));
-            HALO_HIP(hipStreamWaitEvent(s, PP.ev_b[set], 0));
-        }
-        const hipStream_t as = prio == 2 ? PP.hi[set] : s;  // k_acc's stream
-        if (as != s) {
-            HALO_HIP(hipEventRecord(PP.ev_a[set], s));
-            HALO_HIP(hipStreamWaitEvent(as, PP.ev_a[set], 0));
-        }
+                                  nullptr, NB, s, fuse ? &fz : nullptr));
         const uint32_t nblocks = (uint32_t)grid_for(nchunks, 256);
         // the resident window-shifted SRS without identity points: k_acc skips the bases' identity test
         const SrsState& srs_c = st->srs[curve_id<Cv>()];
@@ -625,17 +591,13 @@ static int msm_device_t(DeviceState* st, const uint4* bases_int, bool shifted, s
                                (const char*)bases_int < srs_c.shifted.as<const char>() + srs_c.shifted.bytes;
         const uint32_t check_q = (srs_bases && !srs_c.shifted_has_id) ? 0u : 1u;
         {
-            ProfScope prof("msm_acc", as);
-            HALO_LAUNCH(prof, k_acc<Cv>, dim3(nblocks), dim3(256), 0, as, (const uint32_t*)skeys,
+            ProfScope prof("msm_acc", s);
+            HALO_LAUNCH(prof, k_acc<Cv>, dim3(nblocks), dim3(256), 0, s, (const uint32_t*)skeys,
                         (const uint32_t*)svals, scount, K, bases_int, (uint32_t)nn, is_pow2(nn) ? ilog2(nn) : 0xffu,
                         (shifted && (shift_stride != nn || blk_lg < 32)) ? shift_stride : (size_t)0, blk_lg,
                         glv ? (uint32_t)nn : 0u, P_first,
                         P_last, M.bucket_sums.as<uint4>(), M.bstart.as<uint32_t>(), (uint32_t)NB, 31u, 0u,
                         check_q);
-        }
-        if (as != s) {
-            HALO_HIP(hipEventRecord(PP.ev_b[set], as));
-            HALO_HIP(hipStreamWaitEvent(s, PP.ev_b[set], 0));
         }
         M.skeys = skeys;
         M.scount = scount;

@@ -284,18 +284,18 @@ HALO_DEV void ntt_group4(Fe<F> (&v)[NTT_EPT], uint32_t G, const NttGroupTw& t, u
 // Wave-uniform unit twiddles.  The group at stage US has twiddle index k0 = position mod 2^US; in its
 // thread order ntt_unit_tau the position's low US bits come from the wave's thread bits (the top US
 // bits of the thread index), so k0 is the same on a whole wave and the k0 = 0 waves skip the
-// multiplications by 1 (stage US, and stage US + 1's first pair: three of four).
-//  * one-column 2048-element blocks (the 11-bit passes of 2^21 / 2^22): US = 1, position bit 0 = thread
-//    bit 8, so waves 0-3 are unit and 4-7 not -- each SIMD holds one of each (waves w and w + 4 share a
-//    SIMD, MI355X_MICROARCH.md LDS): 0.375 multiplications per element per pass saved;
-//  * 1024-element blocks (the <= 8-bit passes: 2^23, 2^24, ...): US = 2, wave 0 of the block's four
-//    is unit (with four blocks per CU starting on varying SIMDs the skips spread over the SIMDs):
-//    0.19 per element per pass.
-// Other 2048-element shapes (T = 2, 4: 2^17..2^20) would put the skips on two of a block's four SIMDs
-// only, so they keep the plain order.
+// multiplications by 1 (stage US, and stage US + 1's first pair: three of four).  1024-element blocks
+// (the <= 8-bit passes: 2^23, 2^24, ...): US = 2, wave 0 of the block's four is unit (with four blocks
+// per CU starting on varying SIMDs the skips spread over the SIMDs): 0.19 per element per pass.
+// 2048-element blocks: none (below).
+// (round 6: the 2048-element blocks no longer use it -- their unit group at stage 1 spans the block, so
+// it cost two full barriers per pass; without it the groups up to stage 6 stay wave-local: 2^22 pair
+// 0.968-0.976 -> 0.949-0.957 ms interleaved, against 3 % more multiplications.  On 1024-element blocks
+// the same change lost 1 % at 2^23 / 2^24, so they keep it.)
 template <int NE>
 HALO_DEV uint32_t ntt_unit_stage(uint32_t T) {
-    return NE == NTT_E_BIG ? (T == 1u ? 1u : 0u) : 2u;
+    (void)T;
+    return NE == NTT_E_BIG ? 0u : 2u;
 }
 template <int NE>
 HALO_DEV uint32_t ntt_unit_tau(uint32_t tau, uint32_t us) {

@@ -151,17 +151,15 @@ static void prof_drain() {
 // ---- tuning ----------------------------------------------------------------------------------
 static const char* const kTuneNames[TUNE_COUNT] = {"ipa_weighted", "ipa_tail",           "ipa_srs_tail_n", "ipa_mat_n",
                                                    "msm_multi_max", "ipa_pool_keep_bytes", "ntt_big_max_log",
-                                                   "ntt_even_split", "ipa_pair_max", "msm_front_prio"};
+                                                   "ntt_even_split", "ipa_pair_max"};
 // ntt_big_max_log: the largest transform split into two passes on 2048-element blocks (2^17..2^this);
 // larger ones, and any below 2^17, take passes of <= 8 bits on 1024-element blocks (ntt.hip ntt_radices)
 // ntt_even_split: passes of <= 8 bits split into even radices where possible (ntt_radices)
 // ipa_pair_max: weighted IPA rounds up to this many terms per side run L and R as one MSM (2^19: every
 // weighted round of a 2^20 opening; the pair's 17-bit keys sort in a 9-bit and an 8-bit pass)
-// msm_front_prio (A/B): 1 = the window-shifted MSM's sort on a least-priority stream, 2 = its k_acc on a
-// greatest-priority stream, 0 = both on the issuing stream
-static const long long kTuneDefault[TUNE_COUNT] = {1, 1, 4096, 2048, 1ll << 18, 1ll << 30, 22, 0, 1ll << 19, 0};
+static const long long kTuneDefault[TUNE_COUNT] = {1, 1, 4096, 2048, 1ll << 18, 1ll << 30, 22, 0, 1ll << 19};
 static std::atomic<long long> g_tune[TUNE_COUNT] = {{1},  {1},  {4096}, {2048}, {1ll << 18},
-                                                    {1ll << 30}, {22}, {0},  {1ll << 19}, {0}};
+                                                    {1ll << 30}, {22}, {0},  {1ll << 19}};
 long long tuning(TuneKey k) { return g_tune[k].load(std::memory_order_relaxed); }
 static int tune_index(const char* key) {
     if (!key) return -1;

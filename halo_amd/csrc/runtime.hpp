@@ -36,7 +36,7 @@ void clear_error();
 
 // ---- tuning (halo_set_tuning): path selections the parity tests pin; read on every use
 enum TuneKey { TUNE_IPA_WEIGHTED, TUNE_IPA_TAIL, TUNE_IPA_SRS_TAIL_N, TUNE_IPA_MAT_N, TUNE_MSM_MULTI_MAX, TUNE_IPA_POOL_KEEP,
-               TUNE_NTT_BIG_MAX_LOG, TUNE_NTT_EVEN_SPLIT, TUNE_IPA_PAIR_MAX, TUNE_MSM_FRONT_PRIO, TUNE_COUNT };
+               TUNE_NTT_BIG_MAX_LOG, TUNE_NTT_EVEN_SPLIT, TUNE_IPA_PAIR_MAX, TUNE_COUNT };
 long long tuning(TuneKey k);
 
 // ---- device buffers ---------------------------------------------------------------------------

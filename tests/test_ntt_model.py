@@ -17,7 +17,7 @@ import ntt_model  # noqa: E402
 
 
 @pytest.mark.parametrize("NE,r,T,kw", [
-    (2048, 11, 1, {}),                      # 2^21 / 2^22 passes: G0 = 1, unit group at stage 1
+    (2048, 11, 1, {}),                      # 2^21 / 2^22 passes: G0 = 1 (no unit group since round 6)
     (2048, 11, 1, {"out_mul": True}),       # ... last pass whose output path multiplies
     (2048, 11, 1, {"prune": 3}),            # ... zero-tail first pass
     (2048, 10, 2, {"pretwiddle": True}),    # 2^20 passes

@@ -144,7 +144,7 @@ def run_block(NE, r, T, loads, stage_tw, pretw, prune=0, out_mul_const=None, rng
         for m in range(EPT):
             if base + m < EB:
                 lds[base + m] = v[m]
-    US = (1 if T == 1 else 0) if NE == 2048 else 2
+    US = 0 if NE == 2048 else 2  # (ntt.hip ntt_unit_stage: the 2048-element blocks have no unit group since round 6)
     out_mul = out_mul_const is not None
     in_norm = {tau: (prune != 0 or G0 != 1) for tau in range(TH)}
     s = prune if prune else G0
