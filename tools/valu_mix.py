@@ -31,7 +31,9 @@ TARGET = "hipv4-amdgcn-amd-amdhsa--gfx950"
 
 def code_objects(lib, tmp):
     fat = os.path.join(tmp, "fatbin.bin")
-    subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={fat}", lib], check=True)
+    # an explicit output file: with only an input objcopy rewrites the library in place (new sha256)
+    subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={fat}", lib, os.path.join(tmp, "discard.so")],
+                   check=True)
     data = open(fat, "rb").read()
     offs = [m.start() for m in re.finditer(re.escape(MAGIC), data)] + [len(data)]
     out = []
