@@ -19,7 +19,7 @@ tag=${1:-r02}
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/evid_${tag}
 rm -rf $O && mkdir -p $O
-LEGS='--varbase 0 --commit-batch 0 --pcdl'
+LEGS='--varbase 0 --commit-batch 0 --batch-ntt 0 --pcdl'
 timeout -k 10 500 python bench.py > $O/bench_full.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
 tail -n 1 $O/bench_full.json > $O/bench.json
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT

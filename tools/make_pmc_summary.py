@@ -16,7 +16,7 @@ from pmc_summary import load, summarise  # noqa: E402
 
 KERNELS = {  # key -> (kernel-name substring, fetch correction)
     "msm_acc": ("k_acc<", 1.0),
-    "ntt_pass": ("k_ntt_pass<", 2.0),
+    "ntt_pass": ("k_ntt_pass<halo::FpCfg, 2048, true>", 2.0),  # the 2^22 pair's full-block pass only
     "rs_scatter": ("k_rs_scatter", 2.0),
     "rs_hist": ("k_rs_hist", 2.0),
     "msm_digits": ("k_digits<", 2.0),

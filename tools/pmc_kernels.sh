@@ -7,7 +7,7 @@ tag=$1; shift
 D=gpurun_out/pmc_k/$tag; rm -rf $D; mkdir -p $D
 run() {  # run <pass> <rocprofv3 args...>
   local p=$1; shift
-  timeout -s KILL 120 rocprofv3 "$@" --output-format csv -d $D/$p -o run -- python3 bench.py --no-cpu --sizes "" --ipa 0 --prove 0 --varbase 0 --commit-batch 0 --pcdl "" --steps 3 --warmup 1 "${BARGS[@]}" > $D/$p.log 2>&1 || { tail -5 $D/$p.log; return 1; }
+  timeout -s KILL 120 rocprofv3 "$@" --output-format csv -d $D/$p -o run -- python3 bench.py --no-cpu --sizes "" --ipa 0 --prove 0 --varbase 0 --commit-batch 0 --batch-ntt 0 --pcdl "" --steps 3 --warmup 1 "${BARGS[@]}" > $D/$p.log 2>&1 || { tail -5 $D/$p.log; return 1; }
 }
 BARGS=("$@")
 run a --kernel-trace --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU &&

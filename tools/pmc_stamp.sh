@@ -4,7 +4,7 @@ cd $GRAFT_REPO_ROOT
 tag=${1:-r03d}
 O=gpurun_out/stamp_$tag; rm -rf $O; mkdir -p $O
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-LEGS='--varbase 0 --commit-batch 0 --pcdl'
+LEGS='--varbase 0 --commit-batch 0 --batch-ntt 0 --pcdl'
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_f -o run -- python3 bench.py --no-cpu --sizes "" --ipa 0 --prove 0 $LEGS "" --steps 3 --warmup 1 > /dev/null 2>&1 || exit 1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_w -o run -- python3 bench.py --no-cpu --sizes "" --ipa 0 --prove 0 $LEGS "" --steps 3 --warmup 1 > /dev/null 2>&1 || exit 1
 python3 tools/make_pmc_summary.py $O/pmc_f $O/pmc_w $O/pmc_summary.json "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes) of 'python3 bench.py --no-cpu --sizes \"\" --ipa 0 --prove 0 $LEGS \"\" --steps 3 --warmup 1', ${tag}" > /dev/null || exit 1

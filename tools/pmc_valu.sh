@@ -7,7 +7,7 @@
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 O=gpurun_out/pmc_valu; rm -rf $O; mkdir -p $O
 C="SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_WAVES"
-timeout -s KILL 240 rocprofv3 --pmc $C --output-format csv -d $O/acc -o run -- python3 bench.py --no-cpu --sizes "" --ipa 0 --prove 0 --varbase 0 --commit-batch 0 --pcdl "" --steps 3 --warmup 1 > $O/acc.log 2>&1 || { tail -5 $O/acc.log; exit 1; }
+timeout -s KILL 240 rocprofv3 --pmc $C --output-format csv -d $O/acc -o run -- python3 bench.py --no-cpu --sizes "" --ipa 0 --prove 0 --varbase 0 --commit-batch 0 --batch-ntt 0 --pcdl "" --steps 3 --warmup 1 > $O/acc.log 2>&1 || { tail -5 $O/acc.log; exit 1; }
 timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d $O/ntt -o run -- python3 tools/ntt_time.py 22 > $O/ntt.log 2>&1 || { tail -5 $O/ntt.log; exit 1; }
 timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d $O/ntt24 -o run -- python3 tools/ntt_time.py 24 > $O/ntt24.log 2>&1 || { tail -5 $O/ntt24.log; exit 1; }
 S=${1:-profiles/pmc_summary.json}
