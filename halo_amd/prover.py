@@ -421,13 +421,17 @@ class DeviceBackend:
         return self.torch.from_numpy(np.stack([self.fe(x) for x in xs]).view(np.int64)).cuda()
 
     def sparse_vec(self, n, entries):
-        out = np.zeros((n, 4), dtype=np.uint64)
-        for i, x in entries.items():
-            out[i] = self.fe(x)
-        return self.torch.from_numpy(out.view(np.int64)).cuda()
+        # zeroed on the device; only the nonzero entries cross PCIe (a host-built 2^20 x 32 B vector cost
+        # 2-4 ms of host time and a pageable copy per call)
+        out = self.torch.zeros((n, 4), dtype=self.torch.int64, device="cuda")
+        if entries:
+            idx = self.torch.tensor(list(entries.keys()), dtype=self.torch.int64, device="cuda")
+            vals = np.stack([self.fe(x) for x in entries.values()]).view(np.int64)
+            out[idx] = self.torch.from_numpy(vals).cuda()
+        return out
 
     def ones(self, n):
-        return DevEvals(self, self.torch.from_numpy(np.tile(self.fe(1), (n, 1)).view(np.int64)).cuda())
+        return DevEvals(self, self.torch.from_numpy(self.fe(1).view(np.int64)).cuda().repeat(n, 1))
 
     def length(self, p):
         return p.shape[0]
