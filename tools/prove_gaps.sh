@@ -6,27 +6,25 @@ O=gpurun_out/prove_gaps
 rm -rf $O && mkdir -p $O
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/t -o run -- python3 tools/prove_time.py ${1:-20} > $O/log 2>&1 || { tail -20 $O/log; exit 1; }
 f=$(find $O/t -name "*kernel_trace.csv" | head -1)
-python3 - "$f" > $O/gaps.txt <<'PY'
-import csv, sys
+python3 - "$f" $O/log > $O/gaps.txt <<'PY'
+import csv, json, sys
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r['Start_Timestamp']))
+reps = [json.loads(l) for l in open(sys.argv[2]) if l.startswith('{')]
 short = lambda r: r['Kernel_Name'].split('(')[0].replace('void ', '').replace('halo::', '')[:48]
-# the repetitions start with the same first kernel after the one-time setup (k_synth_bases, k_shift_windows):
-# split at the largest host gap in the second half of the trace
 ks = [(int(r['Start_Timestamp']), int(r['End_Timestamp']), short(r)) for r in rows]
 ks = [k for k in ks if not k[2].startswith(('k_synth_bases', 'k_shift_windows'))]
-half = len(ks) // 2
-cut = max(range(half // 2, len(ks) - 1), key=lambda i: ks[i + 1][0] - max(k[1] for k in ks[: i + 1]))
-rep = ks[cut + 1:]
-t0 = rep[0][0]
-busy, gaps, end = 0, [], rep[0][0]
+# the second repetition: kernels starting after its host start stamp (CLOCK_MONOTONIC, the trace's clock)
+r1 = reps[-1]["start_ns"]
+rep = [k for k in ks if k[0] >= r1]
+t0 = r1
+print("rep 1 host times (ms):", reps[-1]["times_ms"])
+busy, gaps, end, prev_name = 0, [], t0, '(host start)'
 for i, (s, e, n) in enumerate(rep):
     if s > end:
         gaps.append((s - end, end - t0, prev_name, n))
     busy += max(0, e - max(s, end))
     if e > end:
         end, prev_name = e, n
-    if i == 0:
-        prev_name = n
 span = end - t0
 print(f"kernels {len(rep)}  span {span / 1e6:.2f} ms  busy (union) {busy / 1e6:.2f} ms  idle {(span - busy) / 1e6:.2f} ms")
 tot = {}

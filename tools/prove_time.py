@@ -23,6 +23,8 @@ for arg in (sys.argv[1:] or ['16', '20']):
         wit = prover.synthetic_witness(B, n, seed=1)
         B.sync()
         for rep in range(2):
+            B.sync()
+            t_ns = time.clock_gettime_ns(time.CLOCK_MONOTONIC)  # rocprofv3's trace clock (tools/prove_gaps.sh)
             out = prover.naive_prover(B, wit, n, prover.Challenges(B.m))
-            print(json.dumps({"logn": logn, "curve": curve, "rep": rep,
+            print(json.dumps({"logn": logn, "curve": curve, "rep": rep, "start_ns": t_ns,
                               "times_ms": {k: round(v * 1e3, 2) for k, v in out["times"].items()}}), flush=True)
