@@ -218,6 +218,16 @@ def test_ipa_lockstep_sessions_equal_single(hal, corc, k):
         for a, b in zip(together[i][0] + together[i][1], alone[0] + alone[1]):
             assert np.array_equal(a, b), i
         assert np.array_equal(together[i][2], alone[2]) and np.array_equal(together[i][3], alone[3]), i
+    # and the lockstep session 0 against the C oracle's round loop itself (not only the lone session)
+    to_int = lambda x: P.from_mont(P.limbs_to_int(x), r)
+    zv = to_int(jobs[0][1][0])
+    Hp = np.array(P.point_to_wrapped(c, P.mul_fast(c, to_int(jobs[0][2][0]), P.wrapped_to_point(c, Hw))),
+                  dtype=np.uint64)
+    Ls, Rs, U, c0 = oracle_ipa_loop(corc, "pallas", g, jobs[0][0], fe(P.construct_powers(zv, n, r), r), Hp, chal[0],
+                                    inv[0])
+    for a, b in zip(together[0][0] + together[0][1], Ls + Rs):
+        assert np.array_equal(a, b)
+    assert np.array_equal(together[0][2], U) and np.array_equal(together[0][3], c0)
 
 
 def test_ipa_fold_large_vs_c_oracle(hal, corc):

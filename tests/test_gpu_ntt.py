@@ -315,10 +315,11 @@ def test_divide_by_vanishing_poly(hal, tag):
 
 @pytest.mark.parametrize("logn,nz", [(8, 32), (8, 33), (12, 100), (18, 1 << 15), (20, 1 << 17), (20, 5),
                                      (23, 1 << 20), (23, (1 << 20) - 3), (22, 1 << 20)])
-def test_ntt_zero_tail_matches_full(hal, logn, nz):
+def test_ntt_zero_tail_matches_full(hal, corc, logn, nz):
     """halo_ntt_dev_zero_tail (first pass skips the stages that only replicate the nonzero prefix; the
     tail's contents are ignored, here garbage) equals halo_ntt_dev on the zero-padded input: 1-, 2- and
-    3-pass sizes, power-of-two and ragged prefixes."""
+    3-pass sizes, power-of-two and ragged prefixes -- and both equal the C oracle's NTT of the
+    zero-padded input (corc, ark-poly's radix-2 FFT restated)."""
     import torch
 
     N = 1 << logn
@@ -330,10 +331,12 @@ def test_ntt_zero_tail_matches_full(hal, logn, nz):
     y = x.clone()
     y[nz:] = torch.randint(0, 2**62, (N - nz, 4), dtype=torch.int64, device="cuda", generator=g)  # ignored tail
     s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    x0 = x.cpu().numpy().view(np.uint64).copy()  # the zero-padded input, before the in-place transform
     hal.check(L.halo_ntt_dev(0, ctypes.c_void_p(x.data_ptr()), logn, 1, 0, s))
     hal.check(L.halo_ntt_dev_zero_tail(0, ctypes.c_void_p(y.data_ptr()), logn, 1, nz, s))
     torch.cuda.synchronize()
     assert torch.equal(x, y)
+    assert np.array_equal(y.cpu().numpy().view(np.uint64), corc.ntt("fp", x0))
 
 
 def test_ntt_dev_concurrent_streams(hal, corc):
